@@ -1,0 +1,59 @@
+# Build for the MI355X (gfx950) framework.
+#   make -j8            -> slate_d35_amd/libslate_amd.so + slate_d35_amd/_slate*.so
+# Device code: hipcc --offload-arch=gfx950 (only target).  Host code: g++ + OpenMP.
+ROCM      ?= /opt/rocm
+ARCH      ?= gfx950
+PYTHON    ?= python3
+BUILD     := build/obj
+PKG       := slate_d35_amd
+
+HIPCC     := $(ROCM)/bin/hipcc
+CXX       := g++
+PY_INC    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_paths()['include'])")
+PYBIND_INC:= $(shell $(PYTHON) -c "import pybind11;print(pybind11.get_include())")
+PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_var('EXT_SUFFIX'))")
+
+INC       := -Icsrc/include -Icsrc/kernels -I$(ROCM)/include
+DEFS      := -D__HIP_PLATFORM_AMD__ -DSLATE_AMD_VERSION=\"2026.10.0\"
+CXXFLAGS  := -std=c++17 -O3 -fPIC -fopenmp -march=x86-64-v3 -Wall -Wno-unused-function -Wno-sign-compare $(INC) $(DEFS)
+HIPFLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -Wno-unused-result $(INC) $(DEFS)
+LDLIBS    := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -fopenmp
+
+HIP_SRC   := $(wildcard csrc/kernels/*.hip)
+CC_SRC    := $(wildcard csrc/src/*.cc)
+HIP_OBJ   := $(patsubst csrc/kernels/%.hip,$(BUILD)/k_%.o,$(HIP_SRC))
+CC_OBJ    := $(patsubst csrc/src/%.cc,$(BUILD)/s_%.o,$(CC_SRC))
+HDRS      := $(wildcard csrc/include/slate_amd/*.hh) $(wildcard csrc/kernels/*.hh) $(wildcard csrc/src/*.hh)
+
+LIB       := $(PKG)/libslate_amd.so
+PYMOD     := $(PKG)/_slate$(PY_EXT)
+TESTER    := build/slate_tester
+
+all: $(LIB) $(PYMOD)
+
+$(BUILD):
+	mkdir -p $(BUILD)
+
+$(BUILD)/k_%.o: csrc/kernels/%.hip csrc/kernels/*.hh | $(BUILD)
+	$(HIPCC) $(HIPFLAGS) -c $< -o $@
+
+$(BUILD)/s_%.o: csrc/src/%.cc $(HDRS) | $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LIB): $(HIP_OBJ) $(CC_OBJ)
+	$(CXX) -shared -o $@ $^ $(LDLIBS)
+
+$(BUILD)/bind.o: csrc/python/bind.cc $(HDRS) | $(BUILD)
+	$(CXX) $(CXXFLAGS) -I$(PY_INC) -I$(PYBIND_INC) -fvisibility=hidden -c $< -o $@
+
+$(PYMOD): $(BUILD)/bind.o $(LIB)
+	$(CXX) -shared -o $@ $(BUILD)/bind.o -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
+
+tester: $(TESTER)
+$(TESTER): csrc/tools/tester.cc $(LIB)
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDLIBS)
+
+clean:
+	rm -rf build $(LIB) $(PYMOD)
+
+.PHONY: all clean tester

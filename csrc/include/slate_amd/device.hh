@@ -1,0 +1,95 @@
+// Device runtime: one GPU per process, HIP streams/events, caching memory pool.
+//
+// Reference counterparts: BLAS++ Queue per device (MatrixStorage.hh:574-591:
+// one comm queue + compute queues), Memory block pool (src/core/Memory.cc).
+// Here: one process owns one MI355X; streams are created once per process and
+// reused; device memory comes from a size-bucketed caching pool so drivers
+// never call hipMalloc (which synchronises) in their hot loop.
+#pragma once
+
+#include "exception.hh"
+
+#include <hip/hip_runtime.h>
+#include <cstddef>
+#include <cstdint>
+#include <map>
+#include <mutex>
+#include <vector>
+
+#define slate_hip_call(call) do {                                              \
+    hipError_t _e = (call);                                                    \
+    if (_e != hipSuccess)                                                      \
+        throw ::slate::DeviceException(std::string(#call) + ": " +             \
+              hipGetErrorString(_e), __func__, __FILE__, __LINE__);            \
+    } while (0)
+
+namespace slate {
+namespace device {
+
+/// Number of streams ("queues") per process.  Index semantics follow the
+/// reference's queue indices (potrf.cc:66, getrf.cc:122: queue 0 = trailing
+/// update, 1 = panel, 2.. = lookahead columns) plus a dedicated comm stream.
+constexpr int kNumQueues = 8;
+constexpr int kCommQueue = kNumQueues - 1;
+
+/// True iff a HIP device is visible to this process.
+bool available();
+int  count();
+
+/// Select the device used by this process (default: $LOCAL_RANK % count).
+void set_device(int dev);
+int  get_device();
+
+/// Per-process stream set.  Queue 1 (panel) is created with high priority.
+hipStream_t queue(int index);
+void sync_all();
+
+/// Pooled event (disable-timing events for dependency edges).
+hipEvent_t event_get();
+void event_put(hipEvent_t e);
+
+/// Caching device allocator.  Blocks are bucketed by rounded size and reused;
+/// callers must ensure stream work using a block is complete before freeing
+/// it (drivers free their workspace only after syncing their streams).
+void* malloc(size_t bytes);
+void  free(void* ptr);
+void* malloc_host(size_t bytes);   // pinned host memory
+void  free_host(void* ptr);
+/// Release all cached (unused) blocks back to HIP.
+void  release_cache();
+/// Bytes held in use / cached.
+size_t bytes_in_use();
+size_t bytes_cached();
+
+void memcpy_async(void* dst, const void* src, size_t bytes, hipStream_t s);
+void memcpy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch,
+                    size_t width, size_t height, hipStream_t s);
+void memset_async(void* dst, int v, size_t bytes, hipStream_t s);
+
+/// RAII typed device buffer from the pool.
+template <typename T>
+class Buffer {
+public:
+    Buffer() = default;
+    explicit Buffer(size_t n) { resize(n); }
+    ~Buffer() { reset(); }
+    Buffer(Buffer const&) = delete;
+    Buffer& operator=(Buffer const&) = delete;
+    Buffer(Buffer&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }
+    Buffer& operator=(Buffer&& o) noexcept { reset(); p_ = o.p_; n_ = o.n_; o.p_ = nullptr; o.n_ = 0; return *this; }
+    void resize(size_t n) {
+        if (n <= n_) return;
+        reset();
+        p_ = static_cast<T*>(device::malloc(std::max<size_t>(n, 1) * sizeof(T)));
+        n_ = n;
+    }
+    void reset() { if (p_) device::free(p_); p_ = nullptr; n_ = 0; }
+    T* data() const { return p_; }
+    size_t size() const { return n_; }
+private:
+    T* p_ = nullptr;
+    size_t n_ = 0;
+};
+
+}  // namespace device
+}  // namespace slate

@@ -1,0 +1,64 @@
+// Process grid: p x q processes, one GPU each, with row and column
+// communicators.  Reference: the p x q MPI grid of func::process_2d_grid
+// (func.hh:179) plus the implicit row/column rank sets used by listBcast.
+#pragma once
+
+#include "comm.hh"
+
+#include <memory>
+
+namespace slate {
+
+class Grid {
+public:
+    /// world: all p*q ranks; row: my process row (size q, rank = my column);
+    /// col: my process column (size p, rank = my row).
+    Grid(int p, int q, GridOrder order, CommPtr world, CommPtr row, CommPtr col);
+
+    /// 1 x 1 grid on a SelfComm.
+    static std::shared_ptr<Grid> self();
+
+    int p() const { return p_; }
+    int q() const { return q_; }
+    GridOrder order() const { return order_; }
+    int rank() const { return world_->rank(); }
+    int size() const { return p_ * q_; }
+    int myrow() const { return myrow_; }
+    int mycol() const { return mycol_; }
+
+    /// world rank of process (r, c)
+    int rank_of(int r, int c) const {
+        return order_ == GridOrder::Col ? r + c * p_ : r * q_ + c;
+    }
+    int row_of(int rank) const { return order_ == GridOrder::Col ? rank % p_ : rank / q_; }
+    int col_of(int rank) const { return order_ == GridOrder::Col ? rank / p_ : rank % q_; }
+
+    Comm& world() const { return *world_; }
+    Comm& row()   const { return *row_; }
+    Comm& col()   const { return *col_; }
+    CommPtr world_ptr() const { return world_; }
+    CommPtr row_ptr() const { return row_; }
+    CommPtr col_ptr() const { return col_; }
+
+    /// The same processes viewed as a q x p grid (tile (i,j) of a matrix on
+    /// the transposed grid lives where tile (j,i) lives on this grid);
+    /// reference func::transpose_grid (func.hh:230).
+    std::shared_ptr<Grid> transposed() const;
+
+    bool same_processes(Grid const& o) const { return world_.get() == o.world_.get(); }
+
+private:
+    int p_, q_;
+    GridOrder order_;
+    int myrow_, mycol_;
+    CommPtr world_, row_, col_;
+};
+
+using GridPtr = std::shared_ptr<Grid>;
+
+/// Default grid for new matrices when none is given (1 x 1 self unless the
+/// embedding runtime installed one).
+GridPtr default_grid();
+void set_default_grid(GridPtr g);
+
+}  // namespace slate

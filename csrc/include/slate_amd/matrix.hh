@@ -1,0 +1,410 @@
+// Distributed tiled matrices.
+//
+// Reference: BaseMatrix.hh (view fields :766-800, MOSI tileGet :2640-2723),
+// MatrixStorage.hh (TileNode map :35-160, 2D block-cyclic default :478-516),
+// Matrix.hh (fromLAPACK :293, fromScaLAPACK :347, fromDevices :397,
+// emptyLike :432, insertLocalTiles :832), and the Trapezoid/Triangular/
+// Symmetric/Hermitian/Band subclasses.
+//
+// MI355X-first storage: instead of a std::map of separately allocated nb x nb
+// tiles, every process holds ONE contiguous column-major local array (the
+// ScaLAPACK local layout of the 2D block-cyclic distribution) on its GPU
+// and/or host.  A tile is a view into it.  Because local indices are monotone
+// in global indices, the local part of ANY sub-matrix view is a contiguous
+// strided block, so a trailing update is one large local GEMM per process.
+// Coherency between the host and device instance is MOSI at matrix
+// granularity (MatrixStorage::get).
+#pragma once
+
+#include "types.hh"
+#include "util.hh"
+#include "grid.hh"
+#include "device.hh"
+
+#include <functional>
+#include <memory>
+
+namespace slate {
+
+//------------------------------------------------------------------------------
+/// Non-owning view of one tile (reference Tile.hh:395-419).
+template <typename T>
+struct Tile {
+    T* data = nullptr;
+    int64_t mb = 0, nb = 0, stride = 0;
+    Op op = Op::NoTrans;
+    Uplo uplo = Uplo::General;
+    int device = HostNum;
+    int64_t mb_() const { return op == Op::NoTrans ? mb : nb; }
+    int64_t nb_() const { return op == Op::NoTrans ? nb : mb; }
+    /// element (i, j) of the (op-applied) tile, host tiles only
+    T at(int64_t i, int64_t j) const {
+        if (op == Op::NoTrans) return data[i + j * stride];
+        T v = data[j + i * stride];
+        return op == Op::ConjTrans ? slate::conj(v) : v;
+    }
+};
+
+/// Local strided block (storage orientation).
+template <typename T>
+struct LocalBlock {
+    T* ptr = nullptr;
+    int64_t m = 0, n = 0, ld = 1;
+    bool empty() const { return m <= 0 || n <= 0; }
+    T* at(int64_t i, int64_t j) const { return ptr + i + j * ld; }
+};
+
+//------------------------------------------------------------------------------
+/// Per-process storage of a distributed matrix.
+template <typename T>
+class MatrixStorage {
+public:
+    /// rsrc/csrc: process row/column owning the first tile row/column
+    /// (ScaLAPACK descriptor RSRC/CSRC).
+    MatrixStorage(int64_t m, int64_t n, int64_t mb, int64_t nb, GridPtr grid, int rsrc = 0, int csrc = 0);
+    ~MatrixStorage();
+    MatrixStorage(MatrixStorage const&) = delete;
+    MatrixStorage& operator=(MatrixStorage const&) = delete;
+
+    int64_t m, n, mb, nb;
+    GridPtr grid;
+    int rsrc, csrc;
+    int64_t mloc, nloc, lld;
+    /// my process row/column relative to the source (for numroc)
+    int rrel() const { return (grid->myrow() - rsrc + grid->p()) % grid->p(); }
+    int crel() const { return (grid->mycol() - csrc + grid->q()) % grid->q(); }
+    int row_owner(int64_t tile_row) const { return int((tile_row + rsrc) % grid->p()); }
+    int col_owner(int64_t tile_col) const { return int((tile_col + csrc) % grid->q()); }
+
+    /// Attach user memory as the origin instance (reference TileKind::UserOwned).
+    void attach(T* ptr, int64_t ld, Loc loc);
+    /// Allocate the instance at `loc` if missing (SlateOwned), no data movement.
+    void allocate(Loc loc);
+    bool has(Loc loc) const { return (loc == Loc::Host ? host_ : dev_) != nullptr; }
+
+    /// Coherent access (MOSI at matrix granularity): makes the instance at
+    /// `loc` valid (copying from the other one if needed) and, when
+    /// `for_write`, invalidates the other instance.  Returns the base pointer.
+    T* get(Loc loc, bool for_write);
+    /// Pointer without coherency action.
+    T* raw(Loc loc) const { return loc == Loc::Host ? host_ : dev_; }
+    int64_t ld(Loc loc) const { return loc == Loc::Host ? host_ld_ : dev_ld_; }
+    MOSI_State state(Loc loc) const { return loc == Loc::Host ? host_state_ : dev_state_; }
+    /// Mark the instance at loc modified (others invalid).
+    void modified(Loc loc);
+    /// Copy the modified instance back to the origin (tileUpdateAllOrigin).
+    void update_origin();
+    Loc origin() const { return origin_; }
+    /// Free the non-origin instance (releaseLocalWorkspace analog).
+    void release_workspace();
+    TileKind kind() const { return kind_; }
+
+private:
+    void copy_instance(Loc to);
+    T* host_ = nullptr;
+    T* dev_ = nullptr;
+    int64_t host_ld_ = 0, dev_ld_ = 0;
+    bool host_owned_ = false, dev_owned_ = false;
+    MOSI_State host_state_ = Invalid, dev_state_ = Invalid;
+    Loc origin_ = Loc::Host;
+    TileKind kind_ = TileKind::SlateOwned;
+};
+
+/// Matrix kind tag (for the derived view classes).
+enum class MatrixKind : char {
+    General = 'G', Trapezoid = 'Z', Triangular = 'T', Symmetric = 'S', Hermitian = 'H',
+    Band = 'B', TriangularBand = 't', HermitianBand = 'h',
+};
+
+//------------------------------------------------------------------------------
+/// A view of a distributed matrix (reference BaseMatrix.hh).  Offsets r0/c0
+/// and dims m_/n_ are in storage orientation; op() maps logical (i, j) to
+/// storage (j, i) when transposed.
+template <typename T>
+class BaseMatrix {
+public:
+    using value_type = T;
+    BaseMatrix() = default;
+    BaseMatrix(std::shared_ptr<MatrixStorage<T>> s)
+        : storage_(s), r0_(0), c0_(0), m_(s->m), n_(s->n) {}
+
+    // ---- dimensions (op applied)
+    int64_t m() const { return op_ == Op::NoTrans ? m_ : n_; }
+    int64_t n() const { return op_ == Op::NoTrans ? n_ : m_; }
+    int64_t mt() const { return op_ == Op::NoTrans ? smt() : snt(); }
+    int64_t nt() const { return op_ == Op::NoTrans ? snt() : smt(); }
+    int64_t tileMb(int64_t i) const { return op_ == Op::NoTrans ? srow_size(i) : scol_size(i); }
+    int64_t tileNb(int64_t j) const { return op_ == Op::NoTrans ? scol_size(j) : srow_size(j); }
+    Op op() const { return op_; }
+    Uplo uplo() const { return uplo_; }
+    /// uplo as seen in storage orientation
+    Uplo uplo_physical() const { return op_ == Op::NoTrans ? uplo_ : flip(uplo_); }
+    Diag diag() const { return diag_; }
+    MatrixKind matrix_kind() const { return kind_; }
+
+    // ---- distribution
+    GridPtr grid() const { return storage_->grid; }
+    int mpiRank() const { return storage_->grid->rank(); }
+    int64_t mb() const { return storage_->mb; }
+    int64_t nb() const { return storage_->nb; }
+    /// rank owning logical tile (i, j)
+    int tileRank(int64_t i, int64_t j) const {
+        int64_t si, sj; to_storage(i, j, si, sj);
+        auto& g = *storage_->grid;
+        return g.rank_of(storage_->row_owner(stile_r(si)), storage_->col_owner(stile_c(sj)));
+    }
+    bool tileIsLocal(int64_t i, int64_t j) const { return tileRank(i, j) == mpiRank(); }
+    int tileDevice(int64_t i, int64_t j) const { return tileIsLocal(i, j) ? 0 : HostNum; }
+    /// process row / column owning storage tile-row/col (storage orientation)
+    int srow_owner(int64_t si) const { return storage_->row_owner(stile_r(si)); }
+    int scol_owner(int64_t sj) const { return storage_->col_owner(stile_c(sj)); }
+    void gridinfo(GridOrder& order, int& p, int& q, int& myrow, int& mycol) const {
+        auto& g = *storage_->grid;
+        order = g.order(); p = g.p(); q = g.q(); myrow = g.myrow(); mycol = g.mycol();
+    }
+    int num_devices() const { return device::available() ? 1 : 0; }
+
+    // ---- views (tile index ranges are inclusive, as in the reference)
+    /// sub-matrix of logical tiles [i1..i2] x [j1..j2]
+    BaseMatrix sub(int64_t i1, int64_t i2, int64_t j1, int64_t j2) const;
+    /// element slice rows [r1..r2], cols [c1..c2] (inclusive)
+    BaseMatrix slice(int64_t r1, int64_t r2, int64_t c1, int64_t c2) const;
+
+    /// storage-orientation element offsets/dims
+    int64_t row0() const { return r0_; }
+    int64_t col0() const { return c0_; }
+    int64_t srows() const { return m_; }
+    int64_t scols() const { return n_; }
+
+    // ---- local data access
+    /// Local strided block of this view at `loc` (storage orientation).
+    /// Applies coherency: for_write invalidates the other instance.
+    LocalBlock<T> local(Loc loc, bool for_write = false) const;
+    /// Local block without coherency action (storage must be valid at loc).
+    LocalBlock<T> local_raw(Loc loc) const;
+    /// Local rows/cols ranges in the local array (storage orientation)
+    int64_t lrow_begin() const;
+    int64_t lrow_end() const;
+    int64_t lcol_begin() const;
+    int64_t lcol_end() const;
+    /// View of logical tile (i, j); must be local.
+    Tile<T> tile(int64_t i, int64_t j, Loc loc) const;
+    Tile<T> operator()(int64_t i, int64_t j) const { return tile(i, j, Loc::Host); }
+
+    /// Element access (global logical indices), host instance, local only.
+    T& elem(int64_t i, int64_t j);
+
+    std::shared_ptr<MatrixStorage<T>> storage() const { return storage_; }
+    bool aligned() const { return r0_ % storage_->mb == 0 && c0_ % storage_->nb == 0; }
+
+    /// Make the host or device instance valid; mark modified.
+    void tileGetAllForReading(Loc loc) const { storage_->get(loc, false); }
+    void tileGetAllForWriting(Loc loc) const { storage_->get(loc, true); }
+    void tileUpdateAllOrigin() const { storage_->update_origin(); }
+    void releaseWorkspace() const { storage_->release_workspace(); }
+
+    // ---- op flips (friends transpose/conj_transpose)
+    BaseMatrix transpose_view(bool conj) const {
+        BaseMatrix r = *this;
+        r.uplo_ = flip(uplo_);
+        std::swap(r.kl_, r.ku_);
+        if (op_ == Op::NoTrans) r.op_ = conj ? Op::ConjTrans : Op::Trans;
+        else {
+            slate_error_if_msg((op_ == Op::ConjTrans) != conj && is_complex_v<T>,
+                               "cannot mix transpose and conj_transpose");
+            r.op_ = Op::NoTrans;
+        }
+        return r;
+    }
+
+    // mutable meta (used by derived-class constructors)
+    void set_uplo(Uplo u) { uplo_ = u; }
+    void set_diag(Diag d) { diag_ = d; }
+    void set_kind(MatrixKind k) { kind_ = k; }
+    int64_t kl() const { return kl_; }
+    int64_t ku() const { return ku_; }
+    void set_band(int64_t kl, int64_t ku) { kl_ = kl; ku_ = ku; }
+
+protected:
+    void to_storage(int64_t i, int64_t j, int64_t& si, int64_t& sj) const {
+        if (op_ == Op::NoTrans) { si = i; sj = j; } else { si = j; sj = i; }
+    }
+    // storage-orientation tile counts and sizes of this view
+    int64_t stile_r0() const { return r0_ / storage_->mb; }
+    int64_t stile_c0() const { return c0_ / storage_->nb; }
+    int64_t stile_r(int64_t si) const { return stile_r0() + si; }
+    int64_t stile_c(int64_t sj) const { return stile_c0() + sj; }
+    int64_t smt() const { return m_ == 0 ? 0 : (r0_ + m_ - 1) / storage_->mb - stile_r0() + 1; }
+    int64_t snt() const { return n_ == 0 ? 0 : (c0_ + n_ - 1) / storage_->nb - stile_c0() + 1; }
+    int64_t srow_start(int64_t si) const { return std::max(r0_, stile_r(si) * storage_->mb); }
+    int64_t scol_start(int64_t sj) const { return std::max(c0_, stile_c(sj) * storage_->nb); }
+    int64_t srow_size(int64_t si) const {
+        return std::min(r0_ + m_, (stile_r(si) + 1) * storage_->mb) - srow_start(si);
+    }
+    int64_t scol_size(int64_t sj) const {
+        return std::min(c0_ + n_, (stile_c(sj) + 1) * storage_->nb) - scol_start(sj);
+    }
+
+    std::shared_ptr<MatrixStorage<T>> storage_;
+    int64_t r0_ = 0, c0_ = 0, m_ = 0, n_ = 0;
+    Op op_ = Op::NoTrans;
+    Uplo uplo_ = Uplo::General;
+    Diag diag_ = Diag::NonUnit;
+    MatrixKind kind_ = MatrixKind::General;
+    int64_t kl_ = 0, ku_ = 0;
+};
+
+//------------------------------------------------------------------------------
+// Concrete matrix classes.  They share BaseMatrix's storage/views and differ
+// in the meta-data (kind, uplo, diag, bandwidths) that drivers dispatch on.
+
+template <typename T> class Matrix;
+
+template <typename T>
+class Matrix : public BaseMatrix<T> {
+public:
+    using BaseMatrix<T>::BaseMatrix;
+    Matrix() = default;
+    /// Distributed m x n matrix with nb x nb tiles on a p x q grid (storage
+    /// allocated lazily by insertLocalTiles), reference Matrix.hh:41-55.
+    Matrix(int64_t m, int64_t n, int64_t nb, GridPtr grid = nullptr)
+        : Matrix(m, n, nb, nb, grid) {}
+    Matrix(int64_t m, int64_t n, int64_t mb, int64_t nb, GridPtr grid, int rsrc = 0, int csrc = 0)
+        : BaseMatrix<T>(std::make_shared<MatrixStorage<T>>(m, n, mb, nb, grid ? grid : default_grid(), rsrc, csrc)) {}
+    explicit Matrix(BaseMatrix<T> const& b) : BaseMatrix<T>(b) { this->set_kind(MatrixKind::General); }
+
+    /// Wrap a column-major LAPACK array (1 x 1 grid or replicated-rank use).
+    static Matrix fromLAPACK(int64_t m, int64_t n, T* A, int64_t lda, int64_t nb, Loc loc = Loc::Host);
+    /// Wrap a ScaLAPACK local array (2D block-cyclic on `grid`).
+    static Matrix fromScaLAPACK(int64_t m, int64_t n, T* A, int64_t lld, int64_t mb, int64_t nb,
+                                GridPtr grid, Loc loc = Loc::Host);
+    /// Wrap a device-resident local array (reference fromDevices).
+    static Matrix fromDevices(int64_t m, int64_t n, T* dA, int64_t lld, int64_t mb, int64_t nb, GridPtr grid) {
+        return fromScaLAPACK(m, n, dA, lld, mb, nb, grid, Loc::Device);
+    }
+
+    /// Allocate local storage at the target's location (Matrix.hh:832).
+    void insertLocalTiles(Target target = Target::Host) const {
+        this->storage_->allocate(target == Target::Devices ? Loc::Device : Loc::Host);
+        auto loc = target == Target::Devices ? Loc::Device : Loc::Host;
+        if (this->storage_->state(loc) == Invalid) this->storage_->modified(loc);
+    }
+
+    /// New matrix with the same shape & distribution, no data (Matrix.hh:432).
+    Matrix emptyLike(int64_t mb = 0, int64_t nb = 0, Op deepOp = Op::NoTrans) const;
+
+    Matrix sub(int64_t i1, int64_t i2, int64_t j1, int64_t j2) const { return Matrix(BaseMatrix<T>::sub(i1, i2, j1, j2)); }
+    Matrix slice(int64_t r1, int64_t r2, int64_t c1, int64_t c2) const { return Matrix(BaseMatrix<T>::slice(r1, r2, c1, c2)); }
+};
+
+template <typename T>
+class BaseTrapezoidMatrix : public BaseMatrix<T> {
+public:
+    BaseTrapezoidMatrix() = default;
+    BaseTrapezoidMatrix(Uplo uplo, BaseMatrix<T> const& b, MatrixKind k, Diag d = Diag::NonUnit)
+        : BaseMatrix<T>(b) {
+        slate_error_if_msg(uplo == Uplo::General, "trapezoid matrix requires Upper or Lower");
+        this->set_uplo(uplo); this->set_kind(k); this->set_diag(d);
+    }
+    Matrix<T> general() const { Matrix<T> r{BaseMatrix<T>(*this)}; r.set_uplo(Uplo::General); return r; }
+};
+
+template <typename T>
+class TrapezoidMatrix : public BaseTrapezoidMatrix<T> {
+public:
+    TrapezoidMatrix() = default;
+    TrapezoidMatrix(Uplo uplo, Diag diag, BaseMatrix<T> const& b)
+        : BaseTrapezoidMatrix<T>(uplo, b, MatrixKind::Trapezoid, diag) {}
+    TrapezoidMatrix(Uplo uplo, Diag diag, int64_t m, int64_t n, int64_t nb, GridPtr g = nullptr)
+        : TrapezoidMatrix(uplo, diag, Matrix<T>(m, n, nb, g)) {}
+};
+
+template <typename T>
+class TriangularMatrix : public BaseTrapezoidMatrix<T> {
+public:
+    TriangularMatrix() = default;
+    TriangularMatrix(Uplo uplo, Diag diag, BaseMatrix<T> const& b)
+        : BaseTrapezoidMatrix<T>(uplo, b, MatrixKind::Triangular, diag) {
+        slate_error_if_msg(b.m() != b.n(), "triangular matrix must be square");
+    }
+    TriangularMatrix(Uplo uplo, Diag diag, int64_t n, int64_t nb, GridPtr g = nullptr)
+        : TriangularMatrix(uplo, diag, Matrix<T>(n, n, nb, g)) {}
+};
+
+template <typename T>
+class SymmetricMatrix : public BaseTrapezoidMatrix<T> {
+public:
+    SymmetricMatrix() = default;
+    SymmetricMatrix(Uplo uplo, BaseMatrix<T> const& b)
+        : BaseTrapezoidMatrix<T>(uplo, b, MatrixKind::Symmetric) {
+        slate_error_if_msg(b.m() != b.n(), "symmetric matrix must be square");
+    }
+    SymmetricMatrix(Uplo uplo, int64_t n, int64_t nb, GridPtr g = nullptr)
+        : SymmetricMatrix(uplo, Matrix<T>(n, n, nb, g)) {}
+};
+
+template <typename T>
+class HermitianMatrix : public BaseTrapezoidMatrix<T> {
+public:
+    HermitianMatrix() = default;
+    HermitianMatrix(Uplo uplo, BaseMatrix<T> const& b)
+        : BaseTrapezoidMatrix<T>(uplo, b, MatrixKind::Hermitian) {
+        slate_error_if_msg(b.m() != b.n(), "Hermitian matrix must be square");
+    }
+    HermitianMatrix(Uplo uplo, int64_t n, int64_t nb, GridPtr g = nullptr)
+        : HermitianMatrix(uplo, Matrix<T>(n, n, nb, g)) {}
+};
+
+/// General band matrix with lower/upper bandwidths kl/ku.  Storage is the
+/// full local array; only tiles intersecting the band are touched by drivers.
+template <typename T>
+class BandMatrix : public BaseMatrix<T> {
+public:
+    BandMatrix() = default;
+    BandMatrix(int64_t kl, int64_t ku, BaseMatrix<T> const& b) : BaseMatrix<T>(b) {
+        this->set_kind(MatrixKind::Band); this->set_band(kl, ku);
+    }
+    BandMatrix(int64_t m, int64_t n, int64_t kl, int64_t ku, int64_t nb, GridPtr g = nullptr)
+        : BandMatrix(kl, ku, Matrix<T>(m, n, nb, g)) {}
+    int64_t lowerBandwidth() const { return this->kl(); }
+    int64_t upperBandwidth() const { return this->ku(); }
+};
+
+template <typename T>
+class TriangularBandMatrix : public BaseMatrix<T> {
+public:
+    TriangularBandMatrix() = default;
+    TriangularBandMatrix(Uplo uplo, Diag diag, int64_t kd, BaseMatrix<T> const& b) : BaseMatrix<T>(b) {
+        this->set_kind(MatrixKind::TriangularBand); this->set_uplo(uplo); this->set_diag(diag);
+        this->set_band(uplo == Uplo::Lower ? kd : 0, uplo == Uplo::Upper ? kd : 0);
+    }
+    int64_t bandwidth() const { return std::max(this->kl(), this->ku()); }
+};
+
+template <typename T>
+class HermitianBandMatrix : public BaseMatrix<T> {
+public:
+    HermitianBandMatrix() = default;
+    HermitianBandMatrix(Uplo uplo, int64_t kd, BaseMatrix<T> const& b) : BaseMatrix<T>(b) {
+        this->set_kind(MatrixKind::HermitianBand); this->set_uplo(uplo);
+        this->set_band(uplo == Uplo::Lower ? kd : 0, uplo == Uplo::Upper ? kd : 0);
+    }
+    HermitianBandMatrix(Uplo uplo, int64_t n, int64_t kd, int64_t nb, GridPtr g = nullptr)
+        : HermitianBandMatrix(uplo, kd, Matrix<T>(n, n, nb, g)) {}
+    int64_t bandwidth() const { return std::max(this->kl(), this->ku()); }
+};
+
+//------------------------------------------------------------------------------
+/// Shallow transposes (reference Tile.hh:40-112 / BaseMatrix transpose).
+template <typename M> M transpose(M const& A) {
+    M r = A;
+    static_cast<BaseMatrix<typename M::value_type>&>(r) = A.transpose_view(false);
+    return r;
+}
+template <typename M> M conj_transpose(M const& A) {
+    M r = A;
+    static_cast<BaseMatrix<typename M::value_type>&>(r) = A.transpose_view(true);
+    return r;
+}
+
+}  // namespace slate

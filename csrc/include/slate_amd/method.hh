@@ -1,0 +1,74 @@
+// Algorithm selection (reference include/slate/method.hh:25-315).
+#pragma once
+
+#include "types.hh"
+
+#include <algorithm>
+#include <string>
+
+namespace slate {
+
+typedef int Method;
+const Method baseMethodError = -1;
+const Method baseMethodAuto = 0;
+
+namespace MethodTrsm {
+const Method Error = baseMethodError, Auto = baseMethodAuto, TrsmA = 1, TrsmB = 2;
+inline Method str2method(std::string s) {
+    std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+    if (s == "auto") return Auto;
+    if (s == "a" || s == "trsma") return TrsmA;
+    if (s == "b" || s == "trsmb") return TrsmB;
+    throw Exception("unknown trsm method");
+}
+}  // namespace MethodTrsm
+
+namespace MethodGemm {
+const Method Error = baseMethodError, Auto = baseMethodAuto, GemmA = 1, GemmC = 2;
+/// GemmA (stationary A, reduce C) when B is a single block column, else
+/// GemmC (SUMMA, stationary C); reference method.hh:87-98.
+template <typename M>
+inline Method select_algo(M const& A, M const& B, Options const&) {
+    (void)A;
+    return B.nt() < 2 ? GemmA : GemmC;
+}
+inline Method str2method(std::string s) {
+    std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+    if (s == "auto") return Auto;
+    if (s == "a" || s == "gemma") return GemmA;
+    if (s == "c" || s == "gemmc") return GemmC;
+    throw Exception("unknown gemm method");
+}
+}  // namespace MethodGemm
+
+namespace MethodHemm {
+const Method Error = baseMethodError, Auto = baseMethodAuto, HemmA = 1, HemmC = 2;
+}
+
+namespace MethodCholQR {
+const Method Error = baseMethodError, Auto = baseMethodAuto, GemmA = 1, GemmC = 2, HerkA = 3, HerkC = 4;
+}
+
+namespace MethodGels {
+const Method Error = baseMethodError, Auto = baseMethodAuto, Geqrf = 1, Cholqr = 2;
+inline Method str2method(std::string s) {
+    std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+    if (s == "auto") return Auto;
+    if (s == "qr" || s == "geqrf") return Geqrf;
+    if (s == "cholqr") return Cholqr;
+    throw Exception("unknown gels method");
+}
+}  // namespace MethodGels
+
+namespace MethodLU {
+const Method Error = baseMethodError, Auto = baseMethodAuto, PartialPiv = 1, CALU = 2, NoPiv = 3;
+inline Method str2method(std::string s) {
+    std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+    if (s == "auto" || s == "ppiv" || s == "partialpiv") return PartialPiv;
+    if (s == "calu" || s == "tntpiv") return CALU;
+    if (s == "nopiv") return NoPiv;
+    throw Exception("unknown LU method");
+}
+}  // namespace MethodLU
+
+}  // namespace slate

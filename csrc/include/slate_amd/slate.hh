@@ -1,0 +1,167 @@
+// Public C++ API (reference include/slate/slate.hh:43-1410).
+//
+// Traditional BLAS/LAPACK-named drivers taking distributed matrices and an
+// Options map.  Option::Target selects Host (C++/OpenMP tile kernels) or
+// Devices (gfx950 HIP kernels on this process's GPU).  Every driver is
+// collective over the matrices' process grid.
+#pragma once
+
+#include "enums.hh"
+#include "types.hh"
+#include "exception.hh"
+#include "util.hh"
+#include "device.hh"
+#include "comm.hh"
+#include "grid.hh"
+#include "matrix.hh"
+#include "func.hh"
+#include "method.hh"
+
+#include <vector>
+
+namespace slate {
+
+/// T factors of a QR/LQ factorization: T[0] holds one nb x nb block per
+/// panel (block column k -> columns [k*nb, (k+1)*nb) of an nb x n matrix
+/// replicated on the panel's process column).
+template <typename T>
+using TriangularFactors = std::vector<Matrix<T>>;
+
+//------------------------------------------------------------------------------
+// Level-3 BLAS
+template <typename T>
+void gemm(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts = {});
+template <typename T>
+void gemmA(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts = {});
+template <typename T>
+void gemmC(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts = {});
+
+template <typename T>
+void hemm(Side side, T alpha, HermitianMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
+          Options const& opts = {});
+template <typename T>
+void symm(Side side, T alpha, SymmetricMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
+          Options const& opts = {});
+template <typename T>
+void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMatrix<T>& C, Options const& opts = {});
+template <typename T>
+void syrk(T alpha, Matrix<T> const& A, T beta, SymmetricMatrix<T>& C, Options const& opts = {});
+template <typename T>
+void her2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, real_type<T> beta, HermitianMatrix<T>& C,
+           Options const& opts = {});
+template <typename T>
+void syr2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, SymmetricMatrix<T>& C, Options const& opts = {});
+template <typename T>
+void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Auxiliary
+template <typename T>
+void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T>& B, Options const& opts = {});
+template <typename Ts, typename Td>
+void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts = {});
+template <typename T>
+void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options const& opts = {});
+template <typename T>
+void scale_row_col(Equed equed, std::vector<real_type<T>> const& R, std::vector<real_type<T>> const& C,
+                   Matrix<T>& A, Options const& opts = {});
+template <typename T>
+void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts = {});
+/// Set each element via a lambda of global indices (reference set_lambdas.cc).
+template <typename T>
+void set(std::function<T(int64_t, int64_t)> const& value, BaseMatrix<T>& A, Options const& opts = {});
+/// Gather the whole matrix to every rank's host array (ld = m).
+template <typename T>
+void gather(BaseMatrix<T> const& A, std::vector<T>& full, Options const& opts = {});
+/// B = A with any source/target distributions (reference redistribute.cc).
+template <typename T>
+void redistribute(Matrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Norms (reference norm.cc, colNorms.cc)
+template <typename T>
+real_type<T> norm(Norm norm, BaseMatrix<T> const& A, Options const& opts = {});
+template <typename T>
+void colNorms(Norm norm, Matrix<T> const& A, real_type<T>* values, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Cholesky
+template <typename T>
+int64_t potrf(HermitianMatrix<T>& A, Options const& opts = {});
+template <typename T>
+void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t potri(HermitianMatrix<T>& A, Options const& opts = {});
+template <typename T>
+int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
+template <typename T>
+int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
+template <typename T>
+real_type<T> pocondest(Norm in_norm, HermitianMatrix<T>& A, real_type<T> Anorm, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// LU
+template <typename T>
+int64_t getrf(Matrix<T>& A, Pivots& pivots, Options const& opts = {});
+template <typename T>
+int64_t getrf_nopiv(Matrix<T>& A, Options const& opts = {});
+template <typename T>
+int64_t getrf_tntpiv(Matrix<T>& A, Pivots& pivots, Options const& opts = {});
+template <typename T>
+void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t gesv(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
+template <typename T>
+int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter,
+                         Options const& opts = {});
+template <typename T>
+int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts = {});
+template <typename T>
+real_type<T> gecondest(Norm in_norm, Matrix<T>& A, real_type<T> Anorm, Options const& opts = {});
+template <typename T>
+int64_t trtri(TriangularMatrix<T>& A, Options const& opts = {});
+template <typename T>
+void trtrm(TriangularMatrix<T>& A, Options const& opts = {});
+template <typename T>
+real_type<T> trcondest(Norm in_norm, TriangularMatrix<T>& A, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// QR / LQ / least squares
+template <typename T>
+void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts = {});
+template <typename T>
+void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C,
+           Options const& opts = {});
+template <typename T>
+void gelqf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts = {});
+template <typename T>
+void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C,
+           Options const& opts = {});
+template <typename T>
+void gels(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options const& opts = {});
+template <typename T>
+int64_t cholqr(Matrix<T>& A, Matrix<T>& R, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Eigenvalues / SVD (host-centric, reference heev.cc / svd.cc)
+template <typename T>
+void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts = {});
+template <typename T>
+void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts = {});
+
+/// Wait for all device work of this process (drivers already synchronize).
+void sync();
+
+}  // namespace slate

@@ -1,0 +1,383 @@
+// Auxiliary gfx950 kernels: set / copy+convert / add / scale / transpose /
+// diagonal-block triangular inverse / small Cholesky / row permutation.
+//
+// Reference counterparts: src/cuda/device_{geset,tzset,gecopy,tzcopy,geadd,
+// tzadd,gescale,tzscale,gescale_row_col,transpose}.cu.  The reference launches
+// one thread block per tile with one thread per row; here the local array is
+// one strided block, so kernels use a 2-D grid of 64x4 thread tiles where
+// consecutive lanes walk consecutive rows (coalesced column-major access) and
+// each thread handles several columns.
+#include "device_common.hh"
+#include "kernels.hh"
+
+namespace slate_amd {
+namespace dev {
+
+namespace {
+
+constexpr int TX = 64, TY = 4, COLS_PER_THREAD = 8;
+
+inline dim3 grid2d(int64_t m, int64_t n) {
+    int64_t gx = (m + TX - 1) / TX;
+    int64_t gy = (n + TY * COLS_PER_THREAD - 1) / (TY * COLS_PER_THREAD);
+    return dim3((unsigned)gx, (unsigned)std::min<int64_t>(gy, 65535));
+}
+
+// in-triangle test: uplo 'L' keeps i >= j (+ offset), 'U' keeps i <= j, 'G' all
+__device__ inline bool in_tri(char uplo, int64_t i, int64_t j) {
+    return uplo == 'G' || (uplo == 'L' ? i >= j : i <= j);
+}
+
+template <typename T>
+__global__ void set_kernel(char uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda) {
+    int64_t i = blockIdx.x * (int64_t)TX + threadIdx.x;
+    if (i >= m) return;
+    for (int64_t j = blockIdx.y * (int64_t)TY * COLS_PER_THREAD + threadIdx.y; j < n;
+         j += (int64_t)gridDim.y * TY * COLS_PER_THREAD) {
+        #pragma unroll
+        for (int c = 0; c < COLS_PER_THREAD; ++c) {
+            int64_t jj = j + c * TY;
+            if (jj < n && in_tri(uplo, i, jj))
+                A[i + jj * lda] = (i == jj) ? diag : offdiag;
+        }
+    }
+}
+
+template <typename Ts, typename Td>
+__device__ inline Td convert(Ts v) {
+    if constexpr (is_cplx<Ts>::value && is_cplx<Td>::value)
+        return Td((real_t<Td>)v.re, (real_t<Td>)v.im);
+    else if constexpr (is_cplx<Td>::value)
+        return Td((real_t<Td>)v, 0);
+    else if constexpr (is_cplx<Ts>::value)
+        return Td(v.re);
+    else
+        return Td(v);
+}
+
+// B = op(A) with precision conversion; trans: 'N', 'T', 'C'.
+// For op != N, reads A[j + i*lda] (uncoalesced on one side; transposes of
+// large matrices go through transpose_kernel instead).
+template <typename Ts, typename Td>
+__global__ void copy_kernel(char uplo, char trans, int64_t m, int64_t n,
+                            const Ts* A, int64_t lda, Td* B, int64_t ldb) {
+    int64_t i = blockIdx.x * (int64_t)TX + threadIdx.x;
+    if (i >= m) return;
+    for (int64_t j = blockIdx.y * (int64_t)TY * COLS_PER_THREAD + threadIdx.y; j < n;
+         j += (int64_t)gridDim.y * TY * COLS_PER_THREAD) {
+        #pragma unroll
+        for (int c = 0; c < COLS_PER_THREAD; ++c) {
+            int64_t jj = j + c * TY;
+            if (jj < n && in_tri(uplo, i, jj)) {
+                Ts v = trans == 'N' ? A[i + jj * lda] : A[jj + i * lda];
+                if (trans == 'C') v = conj(v);
+                B[i + jj * ldb] = convert<Ts, Td>(v);
+            }
+        }
+    }
+}
+
+// B = alpha A + beta B
+template <typename T>
+__global__ void add_kernel(char uplo, int64_t m, int64_t n, T alpha, const T* A, int64_t lda,
+                           T beta, T* B, int64_t ldb) {
+    int64_t i = blockIdx.x * (int64_t)TX + threadIdx.x;
+    if (i >= m) return;
+    bool bz = is_zero(beta);
+    for (int64_t j = blockIdx.y * (int64_t)TY * COLS_PER_THREAD + threadIdx.y; j < n;
+         j += (int64_t)gridDim.y * TY * COLS_PER_THREAD) {
+        #pragma unroll
+        for (int c = 0; c < COLS_PER_THREAD; ++c) {
+            int64_t jj = j + c * TY;
+            if (jj < n && in_tri(uplo, i, jj)) {
+                T v = alpha * A[i + jj * lda];
+                if (!bz) v += beta * B[i + jj * ldb];
+                B[i + jj * ldb] = v;
+            }
+        }
+    }
+}
+
+// A *= numer/denom  (computed as one multiplier, overflow-safe split as in
+// LAPACK lascl is done on the host side by choosing mul)
+template <typename T>
+__global__ void scale_kernel(char uplo, int64_t m, int64_t n, real_t<T> mul, T* A, int64_t lda) {
+    int64_t i = blockIdx.x * (int64_t)TX + threadIdx.x;
+    if (i >= m) return;
+    for (int64_t j = blockIdx.y * (int64_t)TY * COLS_PER_THREAD + threadIdx.y; j < n;
+         j += (int64_t)gridDim.y * TY * COLS_PER_THREAD) {
+        #pragma unroll
+        for (int c = 0; c < COLS_PER_THREAD; ++c) {
+            int64_t jj = j + c * TY;
+            if (jj < n && in_tri(uplo, i, jj)) A[i + jj * lda] = A[i + jj * lda] * mul;
+        }
+    }
+}
+
+// A = diag(R) A diag(C)  (equilibration); R or C may be null
+template <typename T>
+__global__ void scale_row_col_kernel(int64_t m, int64_t n, const real_t<T>* R, const real_t<T>* C,
+                                     T* A, int64_t lda) {
+    int64_t i = blockIdx.x * (int64_t)TX + threadIdx.x;
+    if (i >= m) return;
+    real_t<T> r = R ? R[i] : real_t<T>(1);
+    for (int64_t j = blockIdx.y * (int64_t)TY * COLS_PER_THREAD + threadIdx.y; j < n;
+         j += (int64_t)gridDim.y * TY * COLS_PER_THREAD) {
+        #pragma unroll
+        for (int c = 0; c < COLS_PER_THREAD; ++c) {
+            int64_t jj = j + c * TY;
+            if (jj < n) A[i + jj * lda] = A[i + jj * lda] * (r * (C ? C[jj] : real_t<T>(1)));
+        }
+    }
+}
+
+// Out-of-place transpose through an LDS tile (reference device_transpose.cu
+// :242-506 uses NB=32 tiles with an [NB][NX+1] pad; same idea, 64-wide rows).
+template <typename T>
+__global__ void transpose_kernel(bool conjugate, int64_t m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb) {
+    constexpr int NBT = 64;
+    __shared__ T tile[NBT][NBT + 1];
+    int64_t i0 = blockIdx.x * (int64_t)NBT, j0 = blockIdx.y * (int64_t)NBT;
+    int tx = threadIdx.x, ty = threadIdx.y;  // 64 x 4
+    for (int jj = ty; jj < NBT; jj += 4) {
+        int64_t i = i0 + tx, j = j0 + jj;
+        if (i < m && j < n) tile[jj][tx] = A[i + j * lda];
+    }
+    __syncthreads();
+    for (int ii = ty; ii < NBT; ii += 4) {
+        int64_t j = j0 + tx, i = i0 + ii;   // B is n x m: B[j, i] = A[i, j]
+        if (i < m && j < n) {
+            T v = tile[tx][ii];
+            B[j + i * ldb] = conjugate ? conj(v) : v;
+        }
+    }
+}
+
+//------------------------------------------------------------------------------
+// Inverse of the diagonal nbs x nbs blocks of a triangular matrix (nbs <= 64).
+// Block b of A (at A + b*nbs*(1+lda)) is inverted into W (same position in W,
+// ld ldw); the full square block is written (zeros outside the triangle).
+// One 64-lane wave per block; lane j computes column j of the inverse by
+// substitution against the LDS copy of the block.
+template <typename T>
+__global__ void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
+                                  const T* A, int64_t lda, T* W, int64_t ldw) {
+    __shared__ T L[64][65];
+    __shared__ T X[64][65];
+    const int b = blockIdx.x;
+    const int64_t off = (int64_t)b * nbs;
+    const int nb = (int)min<int64_t>(nbs, n - off);
+    const int lane = threadIdx.x;
+    const T* Ab = A + off + off * lda;
+    T* Wb = W + off + off * ldw;
+    for (int j = 0; j < nb; ++j)
+        L[lane][j] = lane < nb ? Ab[lane + j * lda] : zero<T>();
+    __syncthreads();
+    const bool unit = (diag == 'U');
+    const int j = lane;
+    if (j < nb) {
+        if (uplo == 'L') {
+            for (int i = 0; i < j; ++i) X[i][j] = zero<T>();
+            X[j][j] = unit ? one<T>() : one<T>() / L[j][j];
+            for (int i = j + 1; i < nb; ++i) {
+                T s = zero<T>();
+                for (int l = j; l < i; ++l) s += L[i][l] * X[l][j];
+                X[i][j] = unit ? -s : -(s / L[i][i]);
+            }
+        } else {
+            for (int i = j + 1; i < nb; ++i) X[i][j] = zero<T>();
+            X[j][j] = unit ? one<T>() : one<T>() / L[j][j];
+            for (int i = j - 1; i >= 0; --i) {
+                T s = zero<T>();
+                for (int l = i + 1; l <= j; ++l) s += L[i][l] * X[l][j];
+                X[i][j] = unit ? -s : -(s / L[i][i]);
+            }
+        }
+    }
+    __syncthreads();
+    if (lane < nb)
+        for (int jj = 0; jj < nb; ++jj) Wb[lane + jj * ldw] = X[lane][jj];
+}
+
+//------------------------------------------------------------------------------
+// Cholesky of a small (n <= 64) diagonal block in LDS, lower or upper.
+// info (if non-null) receives info_offset + first failing column (1-based)
+// when *info is still 0.  The block's other triangle is not touched.
+template <typename T>
+__global__ void potrf_small_kernel(char uplo, int n, T* A, int64_t lda, int* info, int info_offset) {
+    __shared__ T S[64][65];
+    __shared__ int fail;
+    const int tid = threadIdx.x, nthr = blockDim.x;
+    // load as lower (for upper, load the conjugate transpose)
+    for (int e = tid; e < n * n; e += nthr) {
+        int i = e % n, j = e / n;
+        if (i >= j) S[i][j] = uplo == 'L' ? A[i + (int64_t)j * lda] : conj(A[j + (int64_t)i * lda]);
+    }
+    if (tid == 0) fail = 0;
+    __syncthreads();
+    for (int j = 0; j < n; ++j) {
+        if (tid == 0) {
+            real_t<T> d = real(S[j][j]);
+            if (!(d > 0)) { fail = j + 1; }
+            else S[j][j] = make_val<T>(sqrt((double)d));
+        }
+        __syncthreads();
+        if (fail) break;
+        T djj = S[j][j];
+        for (int i = j + 1 + tid; i < n; i += nthr) S[i][j] = S[i][j] / djj;
+        __syncthreads();
+        int len = n - j - 1;
+        for (int e = tid; e < len * len; e += nthr) {
+            int i = j + 1 + e % len, c = j + 1 + e / len;
+            if (i >= c) S[i][c] -= S[i][j] * conj(S[c][j]);
+        }
+        __syncthreads();
+    }
+    if (fail && info && tid == 0 && *info == 0) *info = info_offset + fail;
+    for (int e = tid; e < n * n; e += nthr) {
+        int i = e % n, j = e / n;
+        if (i >= j) {
+            if (uplo == 'L') A[i + (int64_t)j * lda] = S[i][j];
+            else A[j + (int64_t)i * lda] = conj(S[i][j]);
+        }
+    }
+}
+
+//------------------------------------------------------------------------------
+// Row permutation: for each pair p, row dst[p] of every column receives the
+// value of row src[p] (all reads happen before any write within a column).
+// One 256-thread workgroup per column strip of COLS columns.
+template <typename T>
+__global__ void permute_rows_kernel(int64_t n, T* A, int64_t lda, const int64_t* dst,
+                                    const int64_t* src, const int* npairs_ptr, int max_pairs) {
+    constexpr int PER = 8;
+    const int npairs = npairs_ptr ? min(*npairs_ptr, max_pairs) : max_pairs;
+    const int64_t j = blockIdx.x;
+    if (j >= n) return;
+    T* col = A + j * lda;
+    for (int base = 0; base < npairs; base += 256 * PER) {
+        T v[PER];
+        #pragma unroll
+        for (int r = 0; r < PER; ++r) {
+            int p = base + threadIdx.x + r * 256;
+            if (p < npairs) v[r] = col[src[p]];
+        }
+        __syncthreads();
+        #pragma unroll
+        for (int r = 0; r < PER; ++r) {
+            int p = base + threadIdx.x + r * 256;
+            if (p < npairs) col[dst[p]] = v[r];
+        }
+        __syncthreads();
+    }
+}
+
+// Sequential interchanges applied to a column strip (LAPACK laswp semantics,
+// ipiv 0-based absolute rows), used when the pivot count is tiny.
+template <typename T>
+__global__ void laswp_kernel(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2,
+                             const int64_t* ipiv, int64_t ipiv_offset) {
+    int64_t j = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (j >= n) return;
+    T* col = A + j * lda;
+    for (int64_t k = k1; k < k2; ++k) {
+        int64_t p = ipiv[k - ipiv_offset];
+        if (p != k) { T t = col[k]; col[k] = col[p]; col[p] = t; }
+    }
+}
+
+}  // namespace
+
+//------------------------------------------------------------------------------
+// launchers
+template <typename T>
+void geset(char uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(set_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, uplo, m, n, offdiag, diag, A, lda);
+}
+
+template <typename Ts, typename Td>
+void gecopy(char uplo, char trans, int64_t m, int64_t n, const Ts* A, int64_t lda, Td* B, int64_t ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    if (trans != 'N' && uplo == 'G' && std::is_same<Ts, Td>::value) {
+        // B (m x n) = op(A), A is n x m: tile transpose over A's (n x m) index space
+        dim3 g((unsigned)((n + 63) / 64), (unsigned)((m + 63) / 64));
+        hipLaunchKernelGGL(transpose_kernel<Ts>, g, dim3(64, 4), 0, s, trans == 'C',
+                           n, m, A, lda, reinterpret_cast<Ts*>(B), ldb);
+        return;
+    }
+    hipLaunchKernelGGL((copy_kernel<Ts, Td>), grid2d(m, n), dim3(TX, TY), 0, s, uplo, trans, m, n, A, lda, B, ldb);
+}
+
+template <typename T>
+void geadd(char uplo, int64_t m, int64_t n, T alpha, const T* A, int64_t lda, T beta, T* B, int64_t ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(add_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, uplo, m, n, alpha, A, lda, beta, B, ldb);
+}
+
+template <typename T>
+void gescale(char uplo, int64_t m, int64_t n, real_t<T> mul, T* A, int64_t lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(scale_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, uplo, m, n, mul, A, lda);
+}
+
+template <typename T>
+void gescale_row_col(int64_t m, int64_t n, const real_t<T>* R, const real_t<T>* C, T* A, int64_t lda, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(scale_row_col_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, m, n, R, C, A, lda);
+}
+
+template <typename T>
+void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t ldw, hipStream_t s) {
+    if (n <= 0) return;
+    int nblk = (int)((n + nbs - 1) / nbs);
+    hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, ldw);
+}
+
+template <typename T>
+void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(potrf_small_kernel<T>, dim3(1), dim3(256), 0, s, uplo, n, A, lda, info, info_offset);
+}
+
+template <typename T>
+void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
+                  const int* npairs, int max_pairs, hipStream_t s) {
+    if (n <= 0 || max_pairs <= 0) return;
+    hipLaunchKernelGGL(permute_rows_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src, npairs, max_pairs);
+}
+
+template <typename T>
+void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* ipiv, int64_t ipiv_offset, hipStream_t s) {
+    if (n <= 0 || k2 <= k1) return;
+    hipLaunchKernelGGL(laswp_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, A, lda, k1, k2, ipiv, ipiv_offset);
+}
+
+#define SLATE_INST_AUX(T)                                                                                  \
+    template void geset<T>(char, int64_t, int64_t, T, T, T*, int64_t, hipStream_t);                       \
+    template void geadd<T>(char, int64_t, int64_t, T, const T*, int64_t, T, T*, int64_t, hipStream_t);   \
+    template void gescale<T>(char, int64_t, int64_t, real_t<T>, T*, int64_t, hipStream_t);                \
+    template void gescale_row_col<T>(int64_t, int64_t, const real_t<T>*, const real_t<T>*, T*, int64_t, hipStream_t); \
+    template void trtri_diag<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t);   \
+    template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \
+    template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
+    template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);
+
+SLATE_INST_AUX(float)
+SLATE_INST_AUX(double)
+SLATE_INST_AUX(cplx<float>)
+SLATE_INST_AUX(cplx<double>)
+
+#define SLATE_INST_COPY(Ts, Td) \
+    template void gecopy<Ts, Td>(char, char, int64_t, int64_t, const Ts*, int64_t, Td*, int64_t, hipStream_t);
+SLATE_INST_COPY(float, float)
+SLATE_INST_COPY(double, double)
+SLATE_INST_COPY(float, double)
+SLATE_INST_COPY(double, float)
+SLATE_INST_COPY(cplx<float>, cplx<float>)
+SLATE_INST_COPY(cplx<double>, cplx<double>)
+SLATE_INST_COPY(cplx<float>, cplx<double>)
+SLATE_INST_COPY(cplx<double>, cplx<float>)
+
+}  // namespace dev
+}  // namespace slate_amd

@@ -1,0 +1,75 @@
+// Shared device-side definitions for the gfx950 (CDNA4) kernels.
+//
+// Everything here is written for 64-wide wavefronts and the CDNA4 MFMA
+// register layouts; there is no other target.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include "dev_types.hh"
+
+namespace slate_amd {
+namespace dev {
+
+__device__ inline float  absval(float x)  { return fabsf(x); }
+__device__ inline double absval(double x) { return fabs(x); }
+__device__ inline float  absval(cplx<float> x)  { return hypotf(x.re, x.im); }
+__device__ inline double absval(cplx<double> x) { return hypot(x.re, x.im); }
+// |re| + |im| (LAPACK cabs1), used for pivot search
+__device__ inline float  abs1(float x)  { return fabsf(x); }
+__device__ inline double abs1(double x) { return fabs(x); }
+__device__ inline float  abs1(cplx<float> x)  { return fabsf(x.re) + fabsf(x.im); }
+__device__ inline double abs1(cplx<double> x) { return fabs(x.re) + fabs(x.im); }
+
+
+
+template <typename T> __host__ __device__ inline T make_val(double r) { return T(r); }
+template <> __host__ __device__ inline cplx<float>  make_val<cplx<float>>(double r)  { return {float(r), 0.f}; }
+template <> __host__ __device__ inline cplx<double> make_val<cplx<double>>(double r) { return {r, 0.0}; }
+
+template <typename T> __host__ __device__ inline T zero() { return make_val<T>(0.0); }
+template <typename T> __host__ __device__ inline T one()  { return make_val<T>(1.0); }
+
+__device__ inline bool is_zero(float x) { return x == 0.f; }
+__device__ inline bool is_zero(double x) { return x == 0.0; }
+template <typename R> __device__ inline bool is_zero(cplx<R> x) { return x.re == R(0) && x.im == R(0); }
+
+// NaN-propagating max, as in the reference's max_nan (device_util.cuh)
+template <typename R>
+__device__ inline R max_nan(R x, R y) { return (isnan(y) || y >= x) ? y : x; }
+
+//------------------------------------------------------------------------------
+// Wavefront helpers (64 lanes).
+constexpr int kWave = 64;
+
+template <typename R>
+__device__ inline R wave_sum(R v) {
+    #pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+template <typename R>
+__device__ inline R wave_max_nan(R v) {
+    #pragma unroll
+    for (int off = 32; off > 0; off >>= 1)
+        v = max_nan(v, __shfl_xor(v, off, 64));
+    return v;
+}
+
+//------------------------------------------------------------------------------
+// XCD-aware bijective remap of a 1-D grid: blocks b and b+8 share an XCD (L2)
+// under round-robin dispatch, so hand each XCD a contiguous chunk of the
+// logical tile order.  Speed only; any placement is correct.
+__device__ inline int xcd_remap(int bid, int nblocks) {
+    constexpr int NX = 8;
+    if (nblocks < NX) return bid;
+    int xcd = bid % NX;
+    int q = nblocks / NX, r = nblocks % NX;
+    int base = (xcd < r) ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    return base + bid / NX;
+}
+
+}  // namespace dev
+}  // namespace slate_amd

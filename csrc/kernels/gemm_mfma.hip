@@ -1,0 +1,327 @@
+// MFMA GEMM for gfx950: C = alpha * op(A) * op(B) + beta * C  (real types).
+//
+// Replaces the reference's batched vendor gemm (src/internal/internal_gemm.cc:498,
+// blas::batch::gemm over nb x nb tiles) with ONE large local GEMM per call:
+// trailing updates in the drivers hand us the whole local sub-matrix.
+//
+// CDNA4 design:
+//  * fp64: v_mfma_f64_16x16x4_f64 (64 cyc/SIMD, 2048 flop), fp32:
+//    v_mfma_f32_16x16x4_f32 (32 cyc/SIMD).  One wave owns a 64x64 sub-tile =
+//    4x4 MFMA tiles = 16 independent accumulator chains, so one wave per SIMD
+//    already issues back-to-back.
+//  * 256-thread workgroup (4 waves, 2x2) per 128x128 C tile, BK=16, LDS
+//    double buffer with register prefetch (one barrier per K-tile).
+//  * LDS image is [k][m] with row stride BM+16 elements: the MFMA operand
+//    read (lanes 0-15 consecutive m, lanes 16-31 next k) then lands the two
+//    16-lane halves on disjoint bank halves (ds_read_b64: bank=(a/4)%64).
+//  * Operands are swapped in the MFMA (D = B^T A^T) so that the accumulator's
+//    lane index runs along M: the column-major epilogue stores 16 consecutive
+//    rows (128 B for fp64) per column instead of 4.
+//  * XCD-aware grouped tile order (blocks b, b+8 share an L2).
+#include "device_common.hh"
+#include "kernels.hh"
+
+namespace slate_amd {
+namespace dev {
+
+template <typename T> struct Mfma;
+
+template <> struct Mfma<double> {
+    using acc_t = double __attribute__((ext_vector_type(4)));
+    __device__ static inline acc_t run(double a, double b, acc_t c) {
+        return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+    }
+    // C/D layout of v_mfma_f64_16x16x4_f64: col = lane&15, row = (lane>>4) + 4*reg
+    __device__ static inline int row(int lane, int r) { return (lane >> 4) + 4 * r; }
+};
+
+template <> struct Mfma<float> {
+    using acc_t = float __attribute__((ext_vector_type(4)));
+    __device__ static inline acc_t run(float a, float b, acc_t c) {
+        return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0);
+    }
+    // C/D layout of v_mfma_f32_16x16x4_f32: col = lane&15, row = 4*(lane>>4) + reg
+    __device__ static inline int row(int lane, int r) { return 4 * (lane >> 4) + r; }
+};
+
+// Load a BX x BK operand tile into registers. Element (x, kk) of the operand
+// lives at X[x*sx + kk*sk]; KCONTIG means sk == 1 (else sx == 1).
+template <typename T, int BX, int BK, bool KCONTIG>
+struct TileLoader {
+    static constexpr int VEC = 16 / sizeof(T);
+    static constexpr int NV  = BX * BK / VEC;   // vectors per tile
+    static constexpr int NVT = NV / 256;        // vectors per thread
+    static_assert(NV % 256 == 0, "tile must split evenly over 256 threads");
+    T r[NVT][VEC];
+
+    __device__ inline void coords(int v, int& x, int& kk) const {
+        if constexpr (KCONTIG) {
+            constexpr int KV = BK / VEC;
+            kk = (v % KV) * VEC;
+            x  = v / KV;
+        } else {
+            constexpr int XV = BX / VEC;
+            x  = (v % XV) * VEC;
+            kk = v / XV;
+        }
+    }
+
+    __device__ inline void load(const T* __restrict__ X, int64_t ld, int64_t x0, int64_t k0,
+                                int64_t xdim, int64_t kdim, bool fast) {
+        const int tid = threadIdx.x;
+        if (fast) {
+            #pragma unroll
+            for (int i = 0; i < NVT; ++i) {
+                int x, kk;
+                coords(tid + 256 * i, x, kk);
+                const T* p = KCONTIG ? X + (k0 + kk) + (x0 + x) * ld
+                                     : X + (x0 + x) + (k0 + kk) * ld;
+                if constexpr (sizeof(T) == 8) {
+                    using v2 = double __attribute__((ext_vector_type(2)));
+                    v2 t = *reinterpret_cast<const v2*>(p);
+                    r[i][0] = t[0]; r[i][1] = t[1];
+                } else {
+                    using v4 = float __attribute__((ext_vector_type(4)));
+                    v4 t = *reinterpret_cast<const v4*>(p);
+                    r[i][0] = t[0]; r[i][1] = t[1]; r[i][2] = t[2]; r[i][3] = t[3];
+                }
+            }
+        } else {
+            #pragma unroll
+            for (int i = 0; i < NVT; ++i) {
+                int x, kk;
+                coords(tid + 256 * i, x, kk);
+                #pragma unroll
+                for (int e = 0; e < VEC; ++e) {
+                    int64_t gx = x0 + x + (KCONTIG ? 0 : e);
+                    int64_t gk = k0 + kk + (KCONTIG ? e : 0);
+                    r[i][e] = (gx < xdim && gk < kdim)
+                            ? (KCONTIG ? X[gk + gx * ld] : X[gx + gk * ld]) : T(0);
+                }
+            }
+        }
+    }
+
+    // store into LDS image L[kk][x], row stride LD elements
+    template <int LD>
+    __device__ inline void store(T* L) const {
+        const int tid = threadIdx.x;
+        #pragma unroll
+        for (int i = 0; i < NVT; ++i) {
+            int x, kk;
+            coords(tid + 256 * i, x, kk);
+            if constexpr (KCONTIG) {
+                #pragma unroll
+                for (int e = 0; e < VEC; ++e)
+                    L[(kk + e) * LD + x] = r[i][e];
+            } else {
+                #pragma unroll
+                for (int e = 0; e < VEC; ++e)
+                    L[kk * LD + x + e] = r[i][e];
+            }
+        }
+    }
+};
+
+// TRI: 0 = full C; 'L' / 'U' = only the lower / upper triangle of a square C
+// is computed (tiles outside it are never launched; diagonal tiles are masked).
+template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI>
+__global__ __launch_bounds__(256, 2)
+void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
+                      const T* __restrict__ A, int64_t lda, int64_t sA,
+                      const T* __restrict__ B, int64_t ldb, int64_t sB,
+                      T beta, T* __restrict__ C, int64_t ldc, int64_t sC,
+                      bool aligned)
+{
+    using M = Mfma<T>;
+    using acc_t = typename M::acc_t;
+    constexpr int PAD = 16;
+    constexpr int LDA_S = BM + PAD, LDB_S = BN + PAD;
+    constexpr int WTM = BM / 2, WTN = BN / 2;       // per-wave tile (2x2 waves)
+    constexpr int TM = WTM / 16, TN = WTN / 16;     // MFMA tiles per wave
+    constexpr int A_ELEMS = BK * LDA_S, B_ELEMS = BK * LDB_S;
+
+    __shared__ T smem[2 * (A_ELEMS + B_ELEMS)];
+
+    // batch offset
+    const int64_t bz = blockIdx.y;
+    A += bz * sA; B += bz * sB; C += bz * sC;
+
+    // tile coordinates: XCD remap, then grouped order (GROUP tile-rows)
+    const int mt = (int)((m + BM - 1) / BM), nt = (int)((n + BN - 1) / BN);
+    int tm, tn;
+    if constexpr (TRI == 0) {
+        const int nblk = mt * nt;
+        int bid = xcd_remap(blockIdx.x, nblk);
+        constexpr int GROUP = 8;
+        int group = bid / (GROUP * nt);
+        int first_m = group * GROUP;
+        int gsize = min(mt - first_m, GROUP);
+        int within = bid % (GROUP * nt);
+        tm = first_m + within % gsize;
+        tn = within / gsize;
+    } else {
+        // triangular enumeration: row r holds r+1 tiles (BM == BN, mt == nt)
+        const int nblk = mt * (mt + 1) / 2;
+        int t = xcd_remap(blockIdx.x, nblk);
+        int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+        while ((r + 1) * (r + 2) / 2 <= t) ++r;
+        while (r * (r + 1) / 2 > t) --r;
+        int c = t - r * (r + 1) / 2;
+        if constexpr (TRI == 'L') { tm = r; tn = c; } else { tm = c; tn = r; }
+    }
+    const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+
+    const int lane = threadIdx.x & 63;
+    const int wid  = threadIdx.x >> 6;
+    const int wm = wid >> 1, wn = wid & 1;
+
+    acc_t acc[TM][TN];
+    #pragma unroll
+    for (int i = 0; i < TM; ++i)
+        #pragma unroll
+        for (int j = 0; j < TN; ++j)
+            acc[i][j] = acc_t{0, 0, 0, 0};
+
+    TileLoader<T, BM, BK, A_KC> la;
+    TileLoader<T, BN, BK, B_KC> lb;
+    const bool mfull = (m0 + BM <= m), nfull = (n0 + BN <= n);
+
+    const int KT = (int)((k + BK - 1) / BK);
+    if (KT > 0) {
+        bool kfull = (BK <= k);
+        la.load(A, lda, m0, 0, m, k, aligned && mfull && kfull);
+        lb.load(B, ldb, n0, 0, n, k, aligned && nfull && kfull);
+        la.template store<LDA_S>(smem);
+        lb.template store<LDB_S>(smem + A_ELEMS);
+        __syncthreads();
+    }
+
+    for (int kt = 0; kt < KT; ++kt) {
+        const int cur = kt & 1;
+        const bool more = (kt + 1 < KT);
+        if (more) {
+            int64_t k0 = (int64_t)(kt + 1) * BK;
+            bool kfull = (k0 + BK <= k);
+            la.load(A, lda, m0, k0, m, k, aligned && mfull && kfull);
+            lb.load(B, ldb, n0, k0, n, k, aligned && nfull && kfull);
+        }
+        const T* As = smem + cur * (A_ELEMS + B_ELEMS);
+        const T* Bs = As + A_ELEMS;
+        #pragma unroll
+        for (int s = 0; s < BK / 4; ++s) {
+            const int kr = s * 4 + (lane >> 4);
+            T a[TM], b[TN];
+            #pragma unroll
+            for (int i = 0; i < TM; ++i)
+                a[i] = As[kr * LDA_S + wm * WTM + i * 16 + (lane & 15)];
+            #pragma unroll
+            for (int j = 0; j < TN; ++j)
+                b[j] = Bs[kr * LDB_S + wn * WTN + j * 16 + (lane & 15)];
+            #pragma unroll
+            for (int i = 0; i < TM; ++i)
+                #pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = M::run(b[j], a[i], acc[i][j]);
+        }
+        if (more) {
+            T* Asn = smem + (cur ^ 1) * (A_ELEMS + B_ELEMS);
+            la.template store<LDA_S>(Asn);
+            lb.template store<LDB_S>(Asn + A_ELEMS);
+        }
+        __syncthreads();
+    }
+
+    // epilogue: lane&15 runs along M (contiguous in column-major C)
+    const bool beta_zero = (beta == T(0));
+    #pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int64_t gm = m0 + wm * WTM + i * 16 + (lane & 15);
+        #pragma unroll
+        for (int j = 0; j < TN; ++j) {
+            #pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gn = n0 + wn * WTN + j * 16 + M::row(lane, r);
+                bool in = gm < m && gn < n;
+                if constexpr (TRI == 'L') in = in && gm >= gn;
+                if constexpr (TRI == 'U') in = in && gm <= gn;
+                if (in) {
+                    T* c = C + gm + gn * ldc;
+                    T v = alpha * acc[i][j][r];
+                    if (!beta_zero) v += beta * (*c);
+                    *c = v;
+                }
+            }
+        }
+    }
+}
+
+template <typename T, bool A_KC, bool B_KC, char TRI = 0>
+static void launch_gemm(int64_t m, int64_t n, int64_t k, T alpha,
+                        const T* A, int64_t lda, int64_t sA,
+                        const T* B, int64_t ldb, int64_t sB,
+                        T beta, T* C, int64_t ldc, int64_t sC,
+                        int64_t batch, hipStream_t stream)
+{
+    constexpr int BM = 128, BN = 128, BK = 16;
+    constexpr int VEC = 16 / sizeof(T);
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };
+    bool aligned = al(A) && al(B) && (lda % VEC == 0) && (ldb % VEC == 0)
+                && (batch == 1 || (sA % VEC == 0 && sB % VEC == 0));
+    int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
+    int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
+    dim3 grid((unsigned)nblk, (unsigned)batch);
+    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI>), grid, dim3(256), 0, stream,
+                       m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+}
+
+template <typename T>
+void gemm_real(char transA, char transB, int64_t m, int64_t n, int64_t k,
+               T alpha, const T* A, int64_t lda, int64_t sA,
+               const T* B, int64_t ldb, int64_t sB,
+               T beta, T* C, int64_t ldc, int64_t sC, int64_t batch, hipStream_t stream)
+{
+    if (m <= 0 || n <= 0 || batch <= 0) return;
+    // op(A) = A: contiguous along M; op(A) = A^T: contiguous along K.
+    // op(B) = B: contiguous along K; op(B) = B^T: contiguous along N.
+    bool a_kc = (transA != 'N'), b_kc = (transB == 'N');
+    if (a_kc && b_kc)
+        launch_gemm<T, true, true>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, stream);
+    else if (a_kc)
+        launch_gemm<T, true, false>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, stream);
+    else if (b_kc)
+        launch_gemm<T, false, true>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, stream);
+    else
+        launch_gemm<T, false, false>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, batch, stream);
+}
+
+// C(uplo triangle of n x n) = alpha op(A) op(B) + beta C   (herk/syrk/her2k core)
+template <typename T>
+void gemm_tri_real(char uplo, char transA, char transB, int64_t n, int64_t k,
+                   T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
+                   T beta, T* C, int64_t ldc, hipStream_t stream)
+{
+    if (n <= 0) return;
+    bool a_kc = (transA != 'N'), b_kc = (transB == 'N');
+#define SLATE_TRI_LAUNCH(U)                                                                   \
+    if (a_kc && b_kc) launch_gemm<T, true, true, U>(n, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, stream); \
+    else if (a_kc)    launch_gemm<T, true, false, U>(n, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, stream); \
+    else if (b_kc)    launch_gemm<T, false, true, U>(n, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, stream); \
+    else              launch_gemm<T, false, false, U>(n, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, stream);
+    if (uplo == 'L') { SLATE_TRI_LAUNCH('L') }
+    else { SLATE_TRI_LAUNCH('U') }
+#undef SLATE_TRI_LAUNCH
+}
+
+template void gemm_tri_real<double>(char, char, char, int64_t, int64_t, double, const double*, int64_t,
+                                    const double*, int64_t, double, double*, int64_t, hipStream_t);
+template void gemm_tri_real<float>(char, char, char, int64_t, int64_t, float, const float*, int64_t,
+                                   const float*, int64_t, float, float*, int64_t, hipStream_t);
+
+template void gemm_real<double>(char, char, int64_t, int64_t, int64_t, double, const double*, int64_t, int64_t,
+                                const double*, int64_t, int64_t, double, double*, int64_t, int64_t, int64_t, hipStream_t);
+template void gemm_real<float>(char, char, int64_t, int64_t, int64_t, float, const float*, int64_t, int64_t,
+                               const float*, int64_t, int64_t, float, float*, int64_t, int64_t, int64_t, hipStream_t);
+
+}  // namespace dev
+}  // namespace slate_amd

@@ -1,0 +1,92 @@
+// Device kernel API (host-callable launchers) for the gfx950 kernels.
+// Counterpart of the reference's include/slate/internal/device.hh plus the
+// vendor BLAS/LAPACK calls it makes (internal_gemm.cc:498, internal_potrf.cc:72,
+// internal_getrf_tntpiv.cc:325, internal_geqrf.cc:255), all hand-written here.
+//
+// All launchers are asynchronous on `stream`.  Matrices are column-major with
+// leading dimension ld.  Op chars: 'N', 'T', 'C'.  Uplo chars: 'L', 'U', 'G'.
+// Scalar types are the device types of dev_types.hh (cplx<R> for complex).
+#pragma once
+
+#include <hip/hip_runtime_api.h>
+#include <cstdint>
+#include "dev_types.hh"
+
+namespace slate_amd {
+namespace dev {
+
+template <typename T> using rt = typename real_type_t<T>::type;
+
+// ---- GEMM (gemm_mfma.hip: real MFMA; gemm_cplx.hip: complex)
+template <typename T>
+void gemm_real(char transA, char transB, int64_t m, int64_t n, int64_t k,
+               T alpha, const T* A, int64_t lda, int64_t sA,
+               const T* B, int64_t ldb, int64_t sB,
+               T beta, T* C, int64_t ldc, int64_t sC, int64_t batch, hipStream_t stream);
+template <typename T>
+void gemm_tri_real(char uplo, char transA, char transB, int64_t n, int64_t k,
+                   T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
+                   T beta, T* C, int64_t ldc, hipStream_t stream);
+template <typename T>
+void gemm_cplx(char uplo, char transA, char transB, int64_t m, int64_t n, int64_t k,
+               T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
+               T beta, T* C, int64_t ldc, hipStream_t stream);
+
+// ---- aux (aux.hip)
+template <typename T>
+void geset(char uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda, hipStream_t s);
+template <typename Ts, typename Td>
+void gecopy(char uplo, char trans, int64_t m, int64_t n, const Ts* A, int64_t lda, Td* B, int64_t ldb, hipStream_t s);
+template <typename T>
+void geadd(char uplo, int64_t m, int64_t n, T alpha, const T* A, int64_t lda, T beta, T* B, int64_t ldb, hipStream_t s);
+template <typename T>
+void gescale(char uplo, int64_t m, int64_t n, rt<T> mul, T* A, int64_t lda, hipStream_t s);
+template <typename T>
+void gescale_row_col(int64_t m, int64_t n, const rt<T>* R, const rt<T>* C, T* A, int64_t lda, hipStream_t s);
+template <typename T>
+void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t ldw, hipStream_t s);
+template <typename T>
+void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s);
+template <typename T>
+void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
+                  const int* npairs, int max_pairs, hipStream_t s);
+template <typename T>
+void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* ipiv, int64_t ipiv_offset, hipStream_t s);
+
+// ---- norms (norm.hip): per-column / per-row / per-block partial results
+// kind: 'M' max, '1' column sums, 'I' row sums, 'F' column (scale, sumsq)
+template <typename T>
+void genorm_partial(char kind, char uplo, char diag, int64_t m, int64_t n, const T* A, int64_t lda,
+                    int64_t goff_row, int64_t goff_col, rt<T>* out, hipStream_t s);
+
+// ---- panels (panel.hip)
+template <typename T>
+void lu_colmax(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c, rt<T>* pval, int64_t* pidx,
+               int nparts, hipStream_t s);
+template <typename T>
+void lu_pivot(int nparts, const rt<T>* pval, const int64_t* pidx, int64_t r, int64_t c, T* A, int64_t lda,
+              int64_t ncols, int64_t* ipiv, int64_t ipiv_base, int64_t* perm, int* info, int64_t info_offset,
+              int64_t* piv_out, hipStream_t s);
+template <typename T>
+void lu_update(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, rt<T>* pval, int64_t* pidx,
+               hipStream_t s);
+void iota(int64_t n, int64_t* p, hipStream_t s);
+void perm_pairs(int64_t k, const int64_t* perm, const int64_t* ipiv_local, int64_t* dst, int64_t* src, hipStream_t s);
+
+template <typename T>
+void qr_colnorm(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c, rt<T>* psum, T* alpha_out,
+                int nparts, hipStream_t s);
+template <typename T>
+void qr_reflect_dots(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, int nparts_norm,
+                     const rt<T>* psum, const T* alpha_in, T* tau_out, T* pdots, int nblocks, hipStream_t s);
+template <typename T>
+void qr_update(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, int nparts, const T* pdots,
+               const T* tau_in, rt<T>* psum_next, T* alpha_next, int nblocks, hipStream_t s);
+template <typename T>
+void tsip(int64_t K, int m, int n, T alpha, const T* A, int64_t lda, const T* B, int64_t ldb, T beta,
+          T* C, int64_t ldc, T* work, int64_t work_elems, hipStream_t s);
+template <typename T>
+void larft_small(int k, const T* tau, T* Tm, int64_t ldt, hipStream_t s);
+
+}  // namespace dev
+}  // namespace slate_amd

@@ -1,0 +1,379 @@
+// pybind11 bindings for the native library (module slate_d35_amd._slate).
+//
+// Exposes the process grid / communicators, the distributed matrix classes,
+// DLPack export of device-resident local arrays (zero-copy into torch), and
+// every driver.  The GIL is released while drivers run; host communicators
+// implemented in Python (torch.distributed / gloo) re-acquire it through the
+// trampoline below.
+#include <pybind11/pybind11.h>
+#include <pybind11/numpy.h>
+#include <pybind11/stl.h>
+#include <pybind11/functional.h>
+
+#include "slate_amd/slate.hh"
+#include "slate_amd/trace.hh"
+#include "slate_amd/runtime.hh"
+#include "bind_drivers.hh"
+
+#include <complex>
+#include <cstring>
+
+namespace py = pybind11;
+using namespace slate;
+
+//------------------------------------------------------------------------------
+// Host communicator implemented in Python.
+class PyHostComm : public HostComm {
+public:
+    using HostComm::HostComm;
+    int rank() const override { PYBIND11_OVERRIDE_PURE(int, HostComm, rank, ); }
+    int size() const override { PYBIND11_OVERRIDE_PURE(int, HostComm, size, ); }
+    std::string name() const override { return "python-host"; }
+    void bcast_raw(void* buf, size_t count, ScalarType t, int root, hipStream_t) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "bcast_raw");
+        f(reinterpret_cast<uintptr_t>(buf), count * scalar_size(t), std::string(1, char(t)), root);
+    }
+    void allreduce_raw(const void* send, void* recv, size_t count, ScalarType t, ReduceOp op, hipStream_t) override {
+        py::gil_scoped_acquire g;
+        if (send != recv) std::memcpy(recv, send, count * scalar_size(t));
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "allreduce_raw");
+        f(reinterpret_cast<uintptr_t>(recv), count, std::string(1, char(t)), std::string(1, char(op)));
+    }
+    void allgather_raw(const void* send, void* recv, size_t count, ScalarType t, hipStream_t) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "allgather_raw");
+        f(reinterpret_cast<uintptr_t>(send), reinterpret_cast<uintptr_t>(recv), count * scalar_size(t));
+    }
+    void send_raw(const void* buf, size_t count, ScalarType t, int peer, hipStream_t) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "send_raw");
+        f(reinterpret_cast<uintptr_t>(buf), count * scalar_size(t), peer);
+    }
+    void recv_raw(void* buf, size_t count, ScalarType t, int peer, hipStream_t) override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "recv_raw");
+        f(reinterpret_cast<uintptr_t>(buf), count * scalar_size(t), peer);
+    }
+    void group_start() override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "group_start");
+        if (f) f();
+    }
+    void group_end() override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "group_end");
+        if (f) f();
+    }
+    void barrier() override {
+        py::gil_scoped_acquire g;
+        py::function f = py::get_override(static_cast<const HostComm*>(this), "barrier");
+        f();
+    }
+};
+
+//------------------------------------------------------------------------------
+// DLPack (minimal ABI-compatible definitions)
+namespace dl {
+struct DLDevice { int32_t device_type; int32_t device_id; };
+struct DLDataType { uint8_t code; uint8_t bits; uint16_t lanes; };
+struct DLTensor { void* data; DLDevice device; int32_t ndim; DLDataType dtype; int64_t* shape; int64_t* strides; uint64_t byte_offset; };
+struct DLManagedTensor { DLTensor dl_tensor; void* manager_ctx; void (*deleter)(DLManagedTensor*); };
+constexpr int32_t kDLCPU = 1, kDLROCM = 10;
+constexpr uint8_t kDLFloat = 2, kDLComplex = 5;
+
+struct Ctx {
+    std::shared_ptr<void> keep;
+    int64_t shape[2];
+    int64_t strides[2];
+};
+
+template <typename T>
+DLDataType dtype_of() {
+    if constexpr (std::is_same_v<T, float>) return {kDLFloat, 32, 1};
+    else if constexpr (std::is_same_v<T, double>) return {kDLFloat, 64, 1};
+    else if constexpr (std::is_same_v<T, std::complex<float>>) return {kDLComplex, 64, 1};
+    else return {kDLComplex, 128, 1};
+}
+
+template <typename T>
+py::capsule export_local(BaseMatrix<T> const& A, Loc loc) {
+    LocalBlock<T> b = A.local(loc, false);
+    auto* mt = new DLManagedTensor();
+    auto* ctx = new Ctx();
+    ctx->keep = A.storage();
+    // column-major (m x n, ld) as a 2-D tensor with strides (1, ld)
+    ctx->shape[0] = b.m; ctx->shape[1] = b.n;
+    ctx->strides[0] = 1; ctx->strides[1] = b.ld;
+    mt->dl_tensor.data = b.ptr ? static_cast<void*>(b.ptr) : reinterpret_cast<void*>(uintptr_t(256));
+    mt->dl_tensor.device = {loc == Loc::Device ? kDLROCM : kDLCPU, loc == Loc::Device ? device::get_device() : 0};
+    mt->dl_tensor.ndim = 2;
+    mt->dl_tensor.dtype = dtype_of<T>();
+    mt->dl_tensor.shape = ctx->shape;
+    mt->dl_tensor.strides = ctx->strides;
+    mt->dl_tensor.byte_offset = 0;
+    mt->manager_ctx = ctx;
+    mt->deleter = [](DLManagedTensor* self) {
+        delete static_cast<Ctx*>(self->manager_ctx);
+        delete self;
+    };
+    return py::capsule(mt, "dltensor", [](PyObject* cap) {
+        if (PyCapsule_IsValid(cap, "dltensor")) {
+            auto* m = static_cast<DLManagedTensor*>(PyCapsule_GetPointer(cap, "dltensor"));
+            if (m && m->deleter) m->deleter(m);
+        }
+    });
+}
+}  // namespace dl
+
+//------------------------------------------------------------------------------
+Options to_options(py::dict d) {
+    Options o;
+    for (auto kv : d) {
+        std::string k = py::str(kv.first);
+        py::handle v = kv.second;
+        if (k == "target") {
+            if (py::isinstance<py::str>(v)) o[Option::Target] = str2target(v.cast<std::string>());
+            else o[Option::Target] = v.cast<Target>();
+        }
+        else if (k == "lookahead") o[Option::Lookahead] = v.cast<int64_t>();
+        else if (k == "block_size" || k == "nb") o[Option::BlockSize] = v.cast<int64_t>();
+        else if (k == "inner_blocking" || k == "ib") o[Option::InnerBlocking] = v.cast<int64_t>();
+        else if (k == "max_panel_threads") o[Option::MaxPanelThreads] = v.cast<int64_t>();
+        else if (k == "tolerance") o[Option::Tolerance] = v.cast<double>();
+        else if (k == "max_iterations") o[Option::MaxIterations] = v.cast<int64_t>();
+        else if (k == "use_fallback_solver") o[Option::UseFallbackSolver] = v.cast<bool>();
+        else if (k == "pivot_threshold") o[Option::PivotThreshold] = v.cast<double>();
+        else if (k == "hold_local_workspace") o[Option::HoldLocalWorkspace] = v.cast<bool>();
+        else if (k == "depth") o[Option::Depth] = v.cast<int64_t>();
+        else if (k == "method_gemm") o[Option::MethodGemm] = v.cast<int64_t>();
+        else if (k == "method_lu") o[Option::MethodLU] = v.cast<int64_t>();
+        else if (k == "method_trsm") o[Option::MethodTrsm] = v.cast<int64_t>();
+        else if (k == "method_gels") o[Option::MethodGels] = v.cast<int64_t>();
+        else if (k == "method_cholqr") o[Option::MethodCholQR] = v.cast<int64_t>();
+        else if (k == "method_hemm") o[Option::MethodHemm] = v.cast<int64_t>();
+        else if (k == "method_eig") o[Option::MethodEig] = OptionValue(int64_t(v.cast<std::string>()[0]));
+        else if (k == "print_verbose") o[Option::PrintVerbose] = v.cast<int64_t>();
+        else if (k == "print_edge_items") o[Option::PrintEdgeItems] = v.cast<int64_t>();
+        else if (k == "print_width") o[Option::PrintWidth] = v.cast<int64_t>();
+        else if (k == "print_precision") o[Option::PrintPrecision] = v.cast<int64_t>();
+        else throw Exception("unknown option: " + k);
+    }
+    return o;
+}
+
+//------------------------------------------------------------------------------
+template <typename T>
+void bind_type(py::module_& m, const char* sfx) {
+    using R = real_type<T>;
+    std::string s(sfx);
+    auto BM = py::class_<BaseMatrix<T>>(m, ("BaseMatrix_" + s).c_str())
+        .def_property_readonly("m", &BaseMatrix<T>::m)
+        .def_property_readonly("n", &BaseMatrix<T>::n)
+        .def_property_readonly("mt", &BaseMatrix<T>::mt)
+        .def_property_readonly("nt", &BaseMatrix<T>::nt)
+        .def_property_readonly("mb", &BaseMatrix<T>::mb)
+        .def_property_readonly("nb", &BaseMatrix<T>::nb)
+        .def_property_readonly("op", &BaseMatrix<T>::op)
+        .def_property_readonly("uplo", &BaseMatrix<T>::uplo)
+        .def_property_readonly("diag", &BaseMatrix<T>::diag)
+        .def_property_readonly("kl", &BaseMatrix<T>::kl)
+        .def_property_readonly("ku", &BaseMatrix<T>::ku)
+        .def_property_readonly("grid", &BaseMatrix<T>::grid)
+        .def("tileMb", &BaseMatrix<T>::tileMb)
+        .def("tileNb", &BaseMatrix<T>::tileNb)
+        .def("tileRank", &BaseMatrix<T>::tileRank)
+        .def("tileIsLocal", &BaseMatrix<T>::tileIsLocal)
+        .def("mpiRank", &BaseMatrix<T>::mpiRank)
+        .def("local_shape", [](BaseMatrix<T> const& A) {
+            return py::make_tuple(A.lrow_end() - A.lrow_begin(), A.lcol_end() - A.lcol_begin());
+        })
+        .def("local_row_indices", [](BaseMatrix<T> const& A) {
+            // global (view-relative, storage orientation) row index of each local row
+            auto& st = *A.storage();
+            std::vector<int64_t> r;
+            for (int64_t l = A.lrow_begin(); l < A.lrow_end(); ++l)
+                r.push_back(l2g(l, st.mb, st.rrel(), st.grid->p()) - A.row0());
+            return r;
+        })
+        .def("local_col_indices", [](BaseMatrix<T> const& A) {
+            auto& st = *A.storage();
+            std::vector<int64_t> r;
+            for (int64_t l = A.lcol_begin(); l < A.lcol_end(); ++l)
+                r.push_back(l2g(l, st.nb, st.crel(), st.grid->q()) - A.col0());
+            return r;
+        })
+        .def("get_local", [](BaseMatrix<T> const& A) {
+            // copy of the local block (storage orientation) as Fortran-order numpy
+            LocalBlock<T> b = A.local(Loc::Host, false);
+            py::array_t<T, py::array::f_style> out({b.m, b.n});
+            T* o = out.mutable_data();
+            for (int64_t j = 0; j < b.n; ++j)
+                if (b.m) std::memcpy(o + j * b.m, b.ptr + j * b.ld, b.m * sizeof(T));
+            return out;
+        })
+        .def("set_local", [](BaseMatrix<T>& A, py::array_t<T, py::array::f_style | py::array::forcecast> a) {
+            LocalBlock<T> b = A.local(Loc::Host, true);
+            if (a.ndim() != 2 || a.shape(0) != b.m || a.shape(1) != b.n)
+                throw Exception("set_local: shape mismatch");
+            const T* src = a.data();
+            for (int64_t j = 0; j < b.n; ++j)
+                if (b.m) std::memcpy(b.ptr + j * b.ld, src + j * b.m, b.m * sizeof(T));
+        })
+        .def("local_dlpack", [](BaseMatrix<T> const& A, bool device) {
+            return dl::export_local<T>(A, device ? Loc::Device : Loc::Host);
+        }, py::arg("device") = true)
+        .def("mark_modified", [](BaseMatrix<T>& A, bool device) {
+            A.storage()->modified(device ? Loc::Device : Loc::Host);
+        }, py::arg("device") = true)
+        .def("gather", [](BaseMatrix<T> const& A) {
+            std::vector<T> full;
+            {
+                py::gil_scoped_release r;
+                gather(A, full);
+            }
+            py::array_t<T, py::array::f_style> out({A.m(), A.n()});
+            if (!full.empty()) std::memcpy(out.mutable_data(), full.data(), full.size() * sizeof(T));
+            return out;
+        })
+        .def("insertLocalTiles", [](BaseMatrix<T>& A, Target t) {
+            Matrix<T>(A).insertLocalTiles(t);
+        }, py::arg("target") = Target::Host)
+        .def("tileUpdateAllOrigin", &BaseMatrix<T>::tileUpdateAllOrigin)
+        .def("releaseWorkspace", &BaseMatrix<T>::releaseWorkspace)
+        .def("origin_is_device", [](BaseMatrix<T> const& A) { return A.storage()->origin() == Loc::Device; });
+
+    py::class_<Matrix<T>, BaseMatrix<T>>(m, ("Matrix_" + s).c_str())
+        .def(py::init([](int64_t mm, int64_t n, int64_t mb, int64_t nb, GridPtr g) {
+            return Matrix<T>(mm, n, mb, nb, g ? g : default_grid());
+        }), py::arg("m"), py::arg("n"), py::arg("mb"), py::arg("nb"), py::arg("grid") = nullptr)
+        .def(py::init([](BaseMatrix<T> const& b) { return Matrix<T>(b); }))
+        .def_static("fromDevicePointer", [](int64_t mm, int64_t n, uintptr_t ptr, int64_t lld, int64_t mb,
+                                              int64_t nb, GridPtr g) {
+            return Matrix<T>::fromScaLAPACK(mm, n, reinterpret_cast<T*>(ptr), lld, mb, nb, g, Loc::Device);
+        })
+        .def_static("fromHostPointer", [](int64_t mm, int64_t n, uintptr_t ptr, int64_t lld, int64_t mb,
+                                            int64_t nb, GridPtr g) {
+            return Matrix<T>::fromScaLAPACK(mm, n, reinterpret_cast<T*>(ptr), lld, mb, nb, g, Loc::Host);
+        })
+        .def("sub", &Matrix<T>::sub)
+        .def("slice", &Matrix<T>::slice)
+        .def("emptyLike", &Matrix<T>::emptyLike, py::arg("mb") = 0, py::arg("nb") = 0, py::arg("deepOp") = Op::NoTrans)
+        .def("transpose", [](Matrix<T> const& A) { return transpose(A); })
+        .def("conj_transpose", [](Matrix<T> const& A) { return conj_transpose(A); });
+
+    py::class_<BaseTrapezoidMatrix<T>, BaseMatrix<T>>(m, ("BaseTrapezoidMatrix_" + s).c_str());
+    py::class_<TrapezoidMatrix<T>, BaseTrapezoidMatrix<T>>(m, ("TrapezoidMatrix_" + s).c_str())
+        .def(py::init<Uplo, Diag, BaseMatrix<T> const&>())
+        .def("transpose", [](TrapezoidMatrix<T> const& A) { return transpose(A); })
+        .def("conj_transpose", [](TrapezoidMatrix<T> const& A) { return conj_transpose(A); });
+    py::class_<TriangularMatrix<T>, BaseTrapezoidMatrix<T>>(m, ("TriangularMatrix_" + s).c_str())
+        .def(py::init<Uplo, Diag, BaseMatrix<T> const&>())
+        .def("transpose", [](TriangularMatrix<T> const& A) { return transpose(A); })
+        .def("conj_transpose", [](TriangularMatrix<T> const& A) { return conj_transpose(A); });
+    py::class_<SymmetricMatrix<T>, BaseTrapezoidMatrix<T>>(m, ("SymmetricMatrix_" + s).c_str())
+        .def(py::init<Uplo, BaseMatrix<T> const&>())
+        .def("transpose", [](SymmetricMatrix<T> const& A) { return transpose(A); });
+    py::class_<HermitianMatrix<T>, BaseTrapezoidMatrix<T>>(m, ("HermitianMatrix_" + s).c_str())
+        .def(py::init<Uplo, BaseMatrix<T> const&>())
+        .def("conj_transpose", [](HermitianMatrix<T> const& A) { return conj_transpose(A); });
+    py::class_<BandMatrix<T>, BaseMatrix<T>>(m, ("BandMatrix_" + s).c_str())
+        .def(py::init<int64_t, int64_t, BaseMatrix<T> const&>());
+    py::class_<TriangularBandMatrix<T>, BaseMatrix<T>>(m, ("TriangularBandMatrix_" + s).c_str())
+        .def(py::init<Uplo, Diag, int64_t, BaseMatrix<T> const&>());
+    py::class_<HermitianBandMatrix<T>, BaseMatrix<T>>(m, ("HermitianBandMatrix_" + s).c_str())
+        .def(py::init<Uplo, int64_t, BaseMatrix<T> const&>());
+
+    bind_drivers<T>(m, s);
+}
+
+PYBIND11_MODULE(_slate, m) {
+    m.doc() = "slate_d35_amd native library (MI355X / gfx950)";
+
+    py::enum_<Target>(m, "Target")
+        .value("Host", Target::Host).value("HostTask", Target::HostTask).value("HostNest", Target::HostNest)
+        .value("HostBatch", Target::HostBatch).value("Devices", Target::Devices);
+    py::enum_<Op>(m, "Op").value("NoTrans", Op::NoTrans).value("Trans", Op::Trans).value("ConjTrans", Op::ConjTrans);
+    py::enum_<Uplo>(m, "Uplo").value("Upper", Uplo::Upper).value("Lower", Uplo::Lower).value("General", Uplo::General);
+    py::enum_<Diag>(m, "Diag").value("NonUnit", Diag::NonUnit).value("Unit", Diag::Unit);
+    py::enum_<Side>(m, "Side").value("Left", Side::Left).value("Right", Side::Right);
+    py::enum_<Norm>(m, "Norm").value("One", Norm::One).value("Two", Norm::Two).value("Inf", Norm::Inf)
+        .value("Fro", Norm::Fro).value("Max", Norm::Max);
+    py::enum_<GridOrder>(m, "GridOrder").value("Col", GridOrder::Col).value("Row", GridOrder::Row);
+    py::enum_<Equed>(m, "Equed").value("None_", Equed::None).value("Row", Equed::Row).value("Col", Equed::Col)
+        .value("Both", Equed::Both);
+    py::enum_<Job>(m, "Job").value("NoVec", Job::NoVec).value("Vec", Job::Vec);
+
+    py::class_<Comm, std::shared_ptr<Comm>>(m, "Comm")
+        .def("rank", &Comm::rank)
+        .def("size", &Comm::size)
+        .def("name", &Comm::name)
+        .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>());
+    py::class_<SelfComm, Comm, std::shared_ptr<SelfComm>>(m, "SelfComm").def(py::init<>());
+    py::class_<HostComm, PyHostComm, Comm, std::shared_ptr<HostComm>>(m, "HostComm").def(py::init<>());
+    m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
+    m.def("make_rccl_comm", [](py::bytes uid, int nranks, int rank) {
+        std::string s = uid;
+        py::gil_scoped_release r;
+        return make_rccl_comm(s, nranks, rank);
+    });
+    m.def("rccl_split", [](CommPtr parent, int color, int key) {
+        py::gil_scoped_release r;
+        return rccl_split(parent, color, key);
+    });
+
+    py::class_<Grid, std::shared_ptr<Grid>>(m, "Grid")
+        .def(py::init<int, int, GridOrder, CommPtr, CommPtr, CommPtr>())
+        .def_static("self", &Grid::self)
+        .def_property_readonly("p", &Grid::p)
+        .def_property_readonly("q", &Grid::q)
+        .def_property_readonly("order", &Grid::order)
+        .def_property_readonly("rank", &Grid::rank)
+        .def_property_readonly("myrow", &Grid::myrow)
+        .def_property_readonly("mycol", &Grid::mycol)
+        .def("rank_of", &Grid::rank_of)
+        .def("transposed", &Grid::transposed)
+        .def_property_readonly("world", &Grid::world_ptr)
+        .def_property_readonly("row_comm", &Grid::row_ptr)
+        .def_property_readonly("col_comm", &Grid::col_ptr);
+    m.def("default_grid", &default_grid);
+    m.def("set_default_grid", &set_default_grid);
+
+    // device runtime
+    m.def("device_available", &device::available);
+    m.def("device_count", &device::count);
+    m.def("set_device", &device::set_device);
+    m.def("get_device", &device::get_device);
+    m.def("sync", &slate::sync, py::call_guard<py::gil_scoped_release>());
+    m.def("release_cache", &device::release_cache);
+    m.def("bytes_in_use", &device::bytes_in_use);
+    m.def("version", &slate::version);
+    m.def("timers", []() { return timers(); });
+    m.def("clear_timers", []() { timers().clear(); });
+
+    // tracing
+    auto tr = m.def_submodule("trace");
+    tr.def("on", &trace::Trace::on);
+    tr.def("off", &trace::Trace::off);
+    tr.def("is_on", &trace::Trace::is_on);
+    tr.def("comment", &trace::Trace::comment);
+    tr.def("clear", &trace::Trace::clear);
+    tr.def("finish", [](CommPtr c, std::string base) {
+        py::gil_scoped_release r;
+        return trace::Trace::finish(c.get(), base);
+    }, py::arg("comm") = nullptr, py::arg("basename") = "");
+    tr.def("events", []() {
+        py::list out;
+        for (auto& e : trace::Trace::events())
+            out.append(py::make_tuple(std::string(e.name), e.start, e.stop, e.lane));
+        return out;
+    });
+
+    m.def("options", &to_options);
+
+    bind_type<float>(m, "s");
+    bind_type<double>(m, "d");
+    bind_type<std::complex<float>>(m, "c");
+    bind_type<std::complex<double>>(m, "z");
+    bind_mixed(m);
+}

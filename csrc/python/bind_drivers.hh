@@ -1,0 +1,88 @@
+// Driver bindings, templated over the scalar type.
+#pragma once
+
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+#include "slate_amd/slate.hh"
+
+namespace py = pybind11;
+
+slate::Options to_options(py::dict d);
+
+template <typename T>
+void bind_drivers(py::module_& m, std::string const& s) {
+    using namespace slate;
+    using R = real_type<T>;
+    using G = py::call_guard<py::gil_scoped_release>;
+    auto O = [](py::dict d) { return to_options(d); };
+    (void)O;
+#define DEF(name, ...) m.def((std::string(name) + "_" + s).c_str(), __VA_ARGS__)
+
+    // ---- level 3 BLAS
+    DEF("gemm", [](T a, Matrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; gemm(a, A, B, b, C, op); });
+    DEF("gemmA", [](T a, Matrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; gemmA(a, A, B, b, C, op); });
+    DEF("gemmC", [](T a, Matrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; gemmC(a, A, B, b, C, op); });
+    DEF("hemm", [](Side sd, T a, HermitianMatrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; hemm(sd, a, A, B, b, C, op); });
+    DEF("symm", [](Side sd, T a, SymmetricMatrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; symm(sd, a, A, B, b, C, op); });
+    DEF("herk", [](R a, Matrix<T> const& A, R b, HermitianMatrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; herk(a, A, b, C, op); });
+    DEF("syrk", [](T a, Matrix<T> const& A, T b, SymmetricMatrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; syrk(a, A, b, C, op); });
+    DEF("her2k", [](T a, Matrix<T> const& A, Matrix<T> const& B, R b, HermitianMatrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; her2k(a, A, B, b, C, op); });
+    DEF("syr2k", [](T a, Matrix<T> const& A, Matrix<T> const& B, T b, SymmetricMatrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; syr2k(a, A, B, b, C, op); });
+    DEF("trmm", [](Side sd, T a, TriangularMatrix<T> const& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; trmm(sd, a, A, B, op); });
+    DEF("trsm", [](Side sd, T a, TriangularMatrix<T> const& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; trsm(sd, a, A, B, op); });
+
+    // ---- aux
+    DEF("add", [](T a, Matrix<T> const& A, T b, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; add(a, A, b, B, op); });
+    DEF("tzadd", [](T a, BaseTrapezoidMatrix<T> const& A, T b, BaseTrapezoidMatrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; add(a, A, b, B, op); });
+    DEF("copy", [](BaseMatrix<T> const& A, BaseMatrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; slate::copy<T, T>(A, B, op); });
+    DEF("scale", [](R num, R den, BaseMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; scale(num, den, A, op); });
+    DEF("scale_row_col", [](Equed e, std::vector<R> const& Rv, std::vector<R> const& Cv, Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; scale_row_col(e, Rv, Cv, A, op); });
+    DEF("set", [](T off, T d, BaseMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; set(off, d, A, op); });
+    DEF("set_lambda", [](std::function<T(int64_t, int64_t)> f, BaseMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); set(f, A, op); });
+    DEF("redistribute", [](Matrix<T> const& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; redistribute(A, B, op); });
+    DEF("norm", [](Norm n, BaseMatrix<T> const& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return norm(n, A, op); });
+    DEF("colNorms", [](Norm n, Matrix<T> const& A, py::dict o) {
+        Options op = to_options(o);
+        std::vector<R> v(A.n());
+        { py::gil_scoped_release r; colNorms(n, A, v.data(), op); }
+        return v;
+    });
+
+    // ---- Cholesky
+    DEF("potrf", [](HermitianMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return potrf(A, op); });
+
+#undef DEF
+}
+
+inline void bind_mixed(py::module_& m) {
+    using namespace slate;
+    m.def("copy_d2s", [](BaseMatrix<double> const& A, BaseMatrix<float>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; slate::copy<double, float>(A, B, op); });
+    m.def("copy_s2d", [](BaseMatrix<float> const& A, BaseMatrix<double>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; slate::copy<float, double>(A, B, op); });
+    m.def("copy_z2c", [](BaseMatrix<std::complex<double>> const& A, BaseMatrix<std::complex<float>>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; slate::copy<std::complex<double>, std::complex<float>>(A, B, op); });
+    m.def("copy_c2z", [](BaseMatrix<std::complex<float>> const& A, BaseMatrix<std::complex<double>>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; slate::copy<std::complex<float>, std::complex<double>>(A, B, op); });
+}

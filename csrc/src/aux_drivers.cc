@@ -1,0 +1,598 @@
+// Auxiliary distributed drivers: copy (with precision conversion and
+// transposition), add, scale, set, gather, redistribute, norms, and the
+// info reduction helpers.  Reference: src/copy.cc, add.cc, scale.cc,
+// scale_row_col.cc, set.cc, set_lambdas.cc, redistribute.cc, norm.cc,
+// colNorms.cc, internal_reduce_info.cc.
+#include "internal.hh"
+
+#include <cstring>
+#include <functional>
+#include <numeric>
+
+namespace slate {
+namespace internal {
+
+int64_t reduce_info(int64_t info, Comm& comm) {
+    if (comm.size() == 1) return info;
+    int64_t v = info == 0 ? INT64_MAX : info;
+    v = comm.allreduce_scalar<int64_t>(v, ReduceOp::Min);
+    return v == INT64_MAX ? 0 : v;
+}
+
+int64_t fetch_info(Target t, int* info) {
+    if (t != Target::Devices) return info[0];
+    int h = 0;
+    slate_hip_call(hipMemcpy(&h, info, sizeof(int), hipMemcpyDeviceToHost));
+    return h;
+}
+
+namespace {
+
+/// true if every tile of A and B has the same size and owner
+template <typename Ta, typename Tb>
+bool same_layout(BaseMatrix<Ta> const& A, BaseMatrix<Tb> const& B) {
+    if (A.m() != B.m() || A.n() != B.n() || A.mt() != B.mt() || A.nt() != B.nt()) return false;
+    if (!A.grid()->same_processes(*B.grid())) return false;
+    for (int64_t i = 0; i < A.mt(); ++i) if (A.tileMb(i) != B.tileMb(i)) return false;
+    for (int64_t j = 0; j < A.nt(); ++j) if (A.tileNb(j) != B.tileNb(j)) return false;
+    for (int64_t j = 0; j < A.nt(); ++j)
+        for (int64_t i = 0; i < A.mt(); ++i)
+            if (A.tileRank(i, j) != B.tileRank(i, j)) return false;
+    return true;
+}
+
+inline bool is_trapezoid_kind(MatrixKind k) {
+    return k == MatrixKind::Trapezoid || k == MatrixKind::Triangular ||
+           k == MatrixKind::Symmetric || k == MatrixKind::Hermitian;
+}
+
+/// iterate over the local tiles of a view (logical indices), giving storage pointers
+template <typename T, typename F>
+void for_local_tiles(BaseMatrix<T> const& A, Loc loc, F f) {
+    for (int64_t j = 0; j < A.nt(); ++j)
+        for (int64_t i = 0; i < A.mt(); ++i)
+            if (A.tileIsLocal(i, j)) f(i, j, A.tile(i, j, loc));
+}
+
+}  // namespace
+
+/// B = op(A) tile by tile over p2p (generic redistribution).
+template <typename Ts, typename Td>
+void redistribute_any(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Target target, Uplo mask) {
+    slate_error_if_msg(A.m() != B.m() || A.n() != B.n(), "redistribute: dimension mismatch");
+    slate_error_if_msg(A.mt() != B.mt() || A.nt() != B.nt(), "redistribute: tile grids differ");
+    for (int64_t i = 0; i < A.mt(); ++i) slate_error_if_msg(A.tileMb(i) != B.tileMb(i), "redistribute: tile sizes differ");
+    for (int64_t j = 0; j < A.nt(); ++j) slate_error_if_msg(A.tileNb(j) != B.tileNb(j), "redistribute: tile sizes differ");
+    Comm& world = A.grid()->world();
+    const int me = world.rank();
+    const Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    A.storage()->get(loc, false);
+    B.storage()->get(loc, true);
+    // tile list in a deterministic order; buffers: one dense tile per transfer
+    struct Xfer { int64_t i, j; int src, dst; size_t off; int64_t mb, nb; };
+    std::vector<Xfer> sends, recvs;
+    size_t soff = 0, roff = 0;
+    for (int64_t j = 0; j < B.nt(); ++j)
+        for (int64_t i = 0; i < B.mt(); ++i) {
+            if (mask == Uplo::Lower && i < j) continue;
+            if (mask == Uplo::Upper && i > j) continue;
+            int src = A.tileRank(i, j), dst = B.tileRank(i, j);
+            int64_t mb = B.tileMb(i), nb = B.tileNb(j);
+            if (src == me && dst == me) {
+                Tile<Ts> ta = A.tile(i, j, loc);
+                Tile<Td> tb = B.tile(i, j, loc);
+                // tile of op(A): stored (ta.op != N ? transposed) tile
+                lb::copy(c, mask == Uplo::General || i != j ? Uplo::General : mask, ta.op,
+                         mb, nb, ta.data, ta.stride, tb.data, tb.stride);
+            } else if (src == me) {
+                sends.push_back({i, j, src, dst, soff, mb, nb}); soff += size_t(mb) * nb;
+            } else if (dst == me) {
+                recvs.push_back({i, j, src, dst, roff, mb, nb}); roff += size_t(mb) * nb;
+            }
+        }
+    if (world.size() == 1) {
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+        return;
+    }
+    Work<Ts> sbuf(target, std::max<size_t>(soff, 1));
+    Work<Ts> rbuf(target, std::max<size_t>(roff, 1));
+    for (auto& x : sends) {
+        Tile<Ts> ta = A.tile(x.i, x.j, loc);
+        // pack op(A) tile as dense mb x nb (storage-op applied)
+        lb::copy(c, Uplo::General, ta.op, x.mb, x.nb, ta.data, ta.stride, sbuf.data() + x.off, x.mb);
+    }
+    std::vector<Comm::P2P> ops;
+    for (auto& x : sends) ops.push_back({sbuf.data() + x.off, size_t(x.mb * x.nb), x.dst, true});
+    for (auto& x : recvs) ops.push_back({rbuf.data() + x.off, size_t(x.mb * x.nb), x.src, false});
+    world.exchange(ops, scalar_type<Ts>(), loc, c.stream);
+    for (auto& x : recvs) {
+        Tile<Td> tb = B.tile(x.i, x.j, loc);
+        lb::copy(c, mask == Uplo::General || x.i != x.j ? Uplo::General : mask, Op::NoTrans, x.mb, x.nb,
+                 rbuf.data() + x.off, x.mb, tb.data, tb.stride);
+    }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+}
+
+template <typename T>
+void redistribute_op(BaseMatrix<T> const& A, BaseMatrix<T>& B, Target target) {
+    redistribute_any<T, T>(A, B, target, Uplo::General);
+}
+
+template void redistribute_op<float>(BaseMatrix<float> const&, BaseMatrix<float>&, Target);
+template void redistribute_op<double>(BaseMatrix<double> const&, BaseMatrix<double>&, Target);
+template void redistribute_op<std::complex<float>>(BaseMatrix<std::complex<float>> const&, BaseMatrix<std::complex<float>>&, Target);
+template void redistribute_op<std::complex<double>>(BaseMatrix<std::complex<double>> const&, BaseMatrix<std::complex<double>>&, Target);
+
+}  // namespace internal
+
+using namespace internal;
+
+//------------------------------------------------------------------------------
+template <typename Ts, typename Td>
+void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
+    trace::Block tb("copy");
+    Target target = resolve_target(opts);
+    Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    Uplo mask = Uplo::General;
+    if (is_trapezoid_kind(B.matrix_kind())) mask = B.uplo();
+    if (A.op() == Op::NoTrans && B.op() == Op::NoTrans && same_layout(A, B) && A.aligned() && B.aligned()) {
+        LocalBlock<Ts> la = A.local(loc, false);
+        LocalBlock<Td> lbk = B.local(loc, true);
+        if (mask == Uplo::General || A.grid()->size() == 1) {
+            lb::copy(c, mask, Op::NoTrans, la.m, la.n, la.ptr, la.ld, lbk.ptr, lbk.ld);
+        } else {
+            // trapezoid on a distributed grid: copy tiles in the triangle
+            for (int64_t j = 0; j < A.nt(); ++j)
+                for (int64_t i = 0; i < A.mt(); ++i) {
+                    if (!A.tileIsLocal(i, j)) continue;
+                    if (mask == Uplo::Lower ? i < j : i > j) continue;
+                    Tile<Ts> ta = A.tile(i, j, loc);
+                    Tile<Td> tbt = B.tile(i, j, loc);
+                    lb::copy(c, i == j ? mask : Uplo::General, Op::NoTrans, ta.mb, ta.nb, ta.data, ta.stride,
+                             tbt.data, tbt.stride);
+                }
+        }
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    } else {
+        redistribute_any<Ts, Td>(A, B, target, mask);
+    }
+    B.storage()->update_origin();
+}
+
+template <typename T>
+void redistribute(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    copy<T, T>(A, B, opts);
+}
+
+template <typename T>
+void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("add");
+    Target target = resolve_target(opts);
+    Loc loc = loc_of(target);
+    slate_error_if_msg(!same_layout(A, B) || A.op() != B.op(), "add: matrices must share a layout");
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    LocalBlock<T> la = A.local(loc, false);
+    LocalBlock<T> lbk = B.local(loc, true);
+    lb::add(c, Uplo::General, la.m, la.n, alpha, la.ptr, la.ld, beta, lbk.ptr, lbk.ld);
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    B.storage()->update_origin();
+}
+
+template <typename T>
+void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T>& B, Options const& opts) {
+    trace::Block tb("tzadd");
+    Target target = resolve_target(opts);
+    Loc loc = loc_of(target);
+    slate_error_if_msg(!same_layout(A, B), "add: matrices must share a layout");
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    A.storage()->get(loc, false);
+    B.storage()->get(loc, true);
+    Uplo u = B.uplo_physical();
+    for (int64_t j = 0; j < A.nt(); ++j)
+        for (int64_t i = 0; i < A.mt(); ++i) {
+            if (!A.tileIsLocal(i, j)) continue;
+            if (u == Uplo::Lower ? i < j : i > j) continue;
+            Tile<T> ta = A.tile(i, j, loc), tbt = B.tile(i, j, loc);
+            lb::add(c, i == j ? u : Uplo::General, ta.mb, ta.nb, alpha, ta.data, ta.stride, beta, tbt.data, tbt.stride);
+        }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    B.storage()->update_origin();
+}
+
+template <typename T>
+void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options const& opts) {
+    trace::Block tb("scale");
+    Target target = resolve_target(opts);
+    Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    bool trap = is_trapezoid_kind(A.matrix_kind());
+    A.storage()->get(loc, true);
+    if (!trap || A.grid()->size() == 1) {
+        LocalBlock<T> la = A.local_raw(loc);
+        lb::scale(c, trap ? A.uplo_physical() : Uplo::General, la.m, la.n, numer, denom, la.ptr, la.ld);
+    } else {
+        Uplo u = A.uplo_physical();
+        for (int64_t j = 0; j < A.nt(); ++j)
+            for (int64_t i = 0; i < A.mt(); ++i) {
+                if (!A.tileIsLocal(i, j)) continue;
+                int64_t si = A.op() == Op::NoTrans ? i : j, sj = A.op() == Op::NoTrans ? j : i;
+                if (u == Uplo::Lower ? si < sj : si > sj) continue;
+                Tile<T> t = A.tile(i, j, loc);
+                lb::scale(c, si == sj ? u : Uplo::General, t.mb, t.nb, numer, denom, t.data, t.stride);
+            }
+    }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    A.storage()->update_origin();
+}
+
+template <typename T>
+void scale_row_col(Equed equed, std::vector<real_type<T>> const& R, std::vector<real_type<T>> const& C,
+                   Matrix<T>& A, Options const& opts) {
+    trace::Block tb("scale_row_col");
+    Target target = resolve_target(opts);
+    Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    slate_error_if_msg(A.op() != Op::NoTrans, "scale_row_col: NoTrans view required");
+    LocalBlock<T> la = A.local(loc, true);
+    using Rt = real_type<T>;
+    // local slices of R and C
+    std::vector<Rt> r(la.m), cs(la.n);
+    auto& s = *A.storage();
+    for (int64_t il = 0; il < la.m; ++il) {
+        int64_t g = l2g(A.lrow_begin() + il, s.mb, s.rrel(), s.grid->p()) - A.row0();
+        r[il] = (equed == Equed::Row || equed == Equed::Both) ? R[g] : Rt(1);
+    }
+    for (int64_t jl = 0; jl < la.n; ++jl) {
+        int64_t g = l2g(A.lcol_begin() + jl, s.nb, s.crel(), s.grid->q()) - A.col0();
+        cs[jl] = (equed == Equed::Col || equed == Equed::Both) ? C[g] : Rt(1);
+    }
+    if (c.dev()) {
+        Work<Rt> dr(target, r.size() + 1), dc(target, cs.size() + 1);
+        device::memcpy_async(dr.data(), r.data(), r.size() * sizeof(Rt), c.stream);
+        device::memcpy_async(dc.data(), cs.data(), cs.size() * sizeof(Rt), c.stream);
+        lb::scale_row_col(c, la.m, la.n, dr.data(), dc.data(), la.ptr, la.ld);
+        slate_hip_call(hipStreamSynchronize(c.stream));
+    } else {
+        lb::scale_row_col(c, la.m, la.n, r.data(), cs.data(), la.ptr, la.ld);
+    }
+    A.storage()->update_origin();
+}
+
+template <typename T>
+void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
+    trace::Block tb("set");
+    Target target = resolve_target(opts);
+    Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    bool trap = is_trapezoid_kind(A.matrix_kind());
+    Uplo u = trap ? A.uplo_physical() : Uplo::General;
+    A.storage()->get(loc, true);
+    for (int64_t j = 0; j < A.nt(); ++j)
+        for (int64_t i = 0; i < A.mt(); ++i) {
+            if (!A.tileIsLocal(i, j)) continue;
+            int64_t si = A.op() == Op::NoTrans ? i : j, sj = A.op() == Op::NoTrans ? j : i;
+            if (u == Uplo::Lower && si < sj) continue;
+            if (u == Uplo::Upper && si > sj) continue;
+            Tile<T> t = A.tile(i, j, loc);
+            if (si == sj) lb::set(c, u, t.mb, t.nb, offdiag, diag, t.data, t.stride);
+            else lb::set(c, Uplo::General, t.mb, t.nb, offdiag, offdiag, t.data, t.stride);
+        }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    A.storage()->update_origin();
+}
+
+template <typename T>
+void set(std::function<T(int64_t, int64_t)> const& value, BaseMatrix<T>& A, Options const&) {
+    trace::Block tb("set_lambda");
+    // evaluated on the host instance, then marked modified
+    auto& s = *A.storage();
+    T* base = s.get(Loc::Host, true);
+    int64_t ld = s.ld(Loc::Host);
+    LocalBlock<T> la = A.local_raw(Loc::Host);
+    (void)base;
+    for (int64_t jl = 0; jl < la.n; ++jl) {
+        int64_t gc = l2g(A.lcol_begin() + jl, s.nb, s.crel(), s.grid->q()) - A.col0();
+        for (int64_t il = 0; il < la.m; ++il) {
+            int64_t gr = l2g(A.lrow_begin() + il, s.mb, s.rrel(), s.grid->p()) - A.row0();
+            int64_t i = A.op() == Op::NoTrans ? gr : gc, j = A.op() == Op::NoTrans ? gc : gr;
+            T v = value(i, j);
+            if (A.op() == Op::ConjTrans) v = slate::conj(v);
+            la.ptr[il + jl * ld] = v;
+        }
+    }
+}
+
+template <typename T>
+void gather(BaseMatrix<T> const& A, std::vector<T>& full, Options const& opts) {
+    trace::Block tb("gather");
+    (void)opts;
+    int64_t m = A.m(), n = A.n();
+    full.assign(size_t(m) * n, T(0));
+    auto& s = *A.storage();
+    // host instance of the local data
+    T* base = s.get(Loc::Host, false);
+    (void)base;
+    LocalBlock<T> la = A.local_raw(Loc::Host);
+    Comm& world = A.grid()->world();
+    // pack my local block (storage orientation) with its global indices
+    std::vector<T> mine(size_t(la.m) * la.n);
+    for (int64_t j = 0; j < la.n; ++j)
+        for (int64_t i = 0; i < la.m; ++i) mine[i + j * la.m] = la.ptr[i + j * la.ld];
+    int size = world.size();
+    std::vector<int64_t> dims(2 * size);
+    int64_t md[2] = {la.m, la.n};
+    world.allgather(md, dims.data(), 2, ScalarType::Int64, Loc::Host, nullptr);
+    int64_t mx = 1;
+    for (int r = 0; r < size; ++r) mx = std::max(mx, dims[2 * r] * dims[2 * r + 1]);
+    std::vector<T> sendb(mx), recvb(size_t(mx) * size);
+    std::copy(mine.begin(), mine.end(), sendb.begin());
+    world.allgather(sendb.data(), recvb.data(), size_t(mx), scalar_type<T>(), Loc::Host, nullptr);
+    auto& g = *s.grid;
+    for (int r = 0; r < size; ++r) {
+        int pr = g.row_of(r), pc = g.col_of(r);
+        int rrel = (pr - s.rsrc + g.p()) % g.p(), crel = (pc - s.csrc + g.q()) % g.q();
+        int64_t rb = g2l_ceil(A.row0(), s.mb, rrel, g.p()), cb = g2l_ceil(A.col0(), s.nb, crel, g.q());
+        int64_t lm = dims[2 * r], ln = dims[2 * r + 1];
+        T const* src = recvb.data() + size_t(mx) * r;
+        for (int64_t j = 0; j < ln; ++j) {
+            int64_t gc = l2g(cb + j, s.nb, crel, g.q()) - A.col0();
+            for (int64_t i = 0; i < lm; ++i) {
+                int64_t gr = l2g(rb + i, s.mb, rrel, g.p()) - A.row0();
+                T v = src[i + j * lm];
+                if (A.op() == Op::NoTrans) full[gr + gc * m] = v;
+                else full[gc + gr * m] = A.op() == Op::ConjTrans ? slate::conj(v) : v;
+            }
+        }
+    }
+}
+
+//------------------------------------------------------------------------------
+// norms
+namespace {
+
+template <typename T>
+struct NormParts {
+    using R = real_type<T>;
+    std::vector<R> colsum, rowsum;  // global-length vectors (storage orientation)
+    R maxv = 0, scale = 0, sumsq = 1;
+};
+
+/// local partial norms of the view in storage orientation with mask
+template <typename T>
+void local_parts(BaseMatrix<T> const& A, Target target, char kind, Uplo mask, Diag diag,
+                 int64_t kl, int64_t ku, NormParts<T>& P) {
+    using R = real_type<T>;
+    Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    auto& s = *A.storage();
+    A.storage()->get(loc, false);
+    int64_t M = A.srows(), N = A.scols();
+    if (kind == '1') P.colsum.assign(N, 0);
+    if (kind == 'I') P.rowsum.assign(M, 0);
+    bool band = kl >= 0 || ku >= 0;
+    // per local tile (for trapezoid / band masks the global offsets matter)
+    int64_t smt = A.op() == Op::NoTrans ? A.mt() : A.nt();
+    int64_t snt = A.op() == Op::NoTrans ? A.nt() : A.mt();
+    BaseMatrix<T> As = A.op() == Op::NoTrans ? A : A.transpose_view(A.op() == Op::ConjTrans);
+    for (int64_t j = 0; j < snt; ++j)
+        for (int64_t i = 0; i < smt; ++i) {
+            if (!As.tileIsLocal(i, j)) continue;
+            if (mask == Uplo::Lower && i < j) continue;
+            if (mask == Uplo::Upper && i > j) continue;
+            int64_t gr = grow_of(As, i), gc = gcol_of(As, j);
+            Tile<T> t = As.tile(i, j, loc);
+            if (band) {
+                // skip tiles entirely outside the band
+                if (gr - (gc + t.nb - 1) > kl) continue;
+                if (gc - (gr + t.mb - 1) > ku) continue;
+            }
+            std::vector<R> out(kind == 'I' ? t.mb : (kind == 'F' ? 2 * t.nb : t.nb));
+            if (band) {
+                // host-side masked evaluation on a copy (band tiles are few)
+                std::vector<T> h(size_t(t.mb) * t.nb);
+                if (c.dev()) {
+                    device::memcpy2d_async(h.data(), t.mb * sizeof(T), t.data, t.stride * sizeof(T), t.mb * sizeof(T), t.nb, c.stream);
+                    slate_hip_call(hipStreamSynchronize(c.stream));
+                } else {
+                    for (int64_t jj = 0; jj < t.nb; ++jj) for (int64_t ii = 0; ii < t.mb; ++ii) h[ii + jj * t.mb] = t.data[ii + jj * t.stride];
+                }
+                for (int64_t jj = 0; jj < t.nb; ++jj) for (int64_t ii = 0; ii < t.mb; ++ii) {
+                    int64_t gi = gr + ii, gj = gc + jj;
+                    if (gi - gj > kl || gj - gi > ku) h[ii + jj * t.mb] = T(0);
+                }
+                lb::norm_partial(lb::Ctx::host(), kind, mask, diag, t.mb, t.nb, h.data(), t.mb, gr, gc, out.data());
+            } else {
+                lb::norm_partial(c, kind, mask, diag, t.mb, t.nb, t.data, t.stride, gr, gc, out.data());
+            }
+            if (kind == 'M') for (R v : out) P.maxv = max_nan(P.maxv, v);
+            else if (kind == '1') for (int64_t jj = 0; jj < t.nb; ++jj) P.colsum[gc + jj] += out[jj];
+            else if (kind == 'I') for (int64_t ii = 0; ii < t.mb; ++ii) P.rowsum[gr + ii] += out[ii];
+            else for (int64_t jj = 0; jj < t.nb; ++jj) combine_sumsq(P.scale, P.sumsq, out[2 * jj], out[2 * jj + 1]);
+        }
+    (void)s;
+}
+
+template <typename T>
+real_type<T> finish_norm(BaseMatrix<T> const& A, char kind, NormParts<T>& P) {
+    using R = real_type<T>;
+    Comm& w = A.grid()->world();
+    if (kind == 'M') {
+        R v = P.maxv;
+        if (w.size() > 1) {
+            // NaN-propagating max: allreduce max on values with NaN mapped to +inf marker
+            R nanflag = std::isnan(v) ? R(1) : R(0);
+            nanflag = w.allreduce_scalar<R>(nanflag, ReduceOp::Max);
+            v = w.allreduce_scalar<R>(std::isnan(v) ? R(0) : v, ReduceOp::Max);
+            if (nanflag > 0) v = std::numeric_limits<R>::quiet_NaN();
+        }
+        return v;
+    }
+    if (kind == '1' || kind == 'I') {
+        auto& vec = kind == '1' ? P.colsum : P.rowsum;
+        allreduce_host(w, vec.data(), vec.size(), ReduceOp::Sum);
+        R v = 0;
+        for (R x : vec) v = max_nan(v, x);
+        return v;
+    }
+    // Frobenius: gather (scale, sumsq) pairs
+    if (w.size() > 1) {
+        std::vector<R> pairs(2 * w.size());
+        R mine[2] = {P.scale, P.sumsq};
+        w.allgather(mine, pairs.data(), 2, scalar_type<R>(), Loc::Host, nullptr);
+        R sc = 0, sq = 1;
+        for (int r = 0; r < w.size(); ++r) combine_sumsq(sc, sq, pairs[2 * r], pairs[2 * r + 1]);
+        P.scale = sc; P.sumsq = sq;
+    }
+    return P.scale * std::sqrt(P.sumsq);
+}
+
+}  // namespace
+
+template <typename T>
+real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
+    trace::Block tb("norm");
+    using R = real_type<T>;
+    Target target = resolve_target(opts);
+    // normalize: work in storage orientation; One<->Inf swap for transposed views
+    Norm nrm = in_norm;
+    if (A.op() != Op::NoTrans) {
+        if (nrm == Norm::One) nrm = Norm::Inf;
+        else if (nrm == Norm::Inf) nrm = Norm::One;
+    }
+    BaseMatrix<T> As = A.op() == Op::NoTrans ? A : A.transpose_view(A.op() == Op::ConjTrans);
+    MatrixKind k = A.matrix_kind();
+    char kind = nrm == Norm::Max ? 'M' : nrm == Norm::One ? '1' : nrm == Norm::Inf ? 'I' : 'F';
+    if (nrm == Norm::Two) slate_not_implemented("two-norm of a matrix");
+    int64_t kl = -1, ku = -1;
+    if (k == MatrixKind::Band || k == MatrixKind::TriangularBand || k == MatrixKind::HermitianBand) {
+        kl = As.kl(); ku = As.ku();
+    }
+    bool sym = (k == MatrixKind::Symmetric || k == MatrixKind::Hermitian || k == MatrixKind::HermitianBand);
+    Uplo mask = (k == MatrixKind::General || k == MatrixKind::Band) ? Uplo::General : As.uplo_physical();
+    Diag diag = (k == MatrixKind::Triangular || k == MatrixKind::Trapezoid || k == MatrixKind::TriangularBand)
+              ? As.diag() : Diag::NonUnit;
+    if (k == MatrixKind::HermitianBand) { kl = ku = std::max(As.kl(), As.ku()); }
+    if (!sym) {
+        NormParts<T> P;
+        local_parts(As, target, kind, mask, diag, kl, ku, P);
+        return finish_norm(As, kind, P);
+    }
+    // symmetric/Hermitian from one triangle
+    if (kind == 'M') {
+        NormParts<T> P;
+        local_parts(As, target, 'M', mask, diag, kl, ku, P);
+        return finish_norm(As, 'M', P);
+    }
+    if (kind == '1' || kind == 'I') {
+        NormParts<T> Pc, Pr, Pd;
+        local_parts(As, target, '1', mask, diag, kl, ku, Pc);
+        local_parts(As, target, 'I', mask, diag, kl, ku, Pr);
+        Comm& w = As.grid()->world();
+        allreduce_host(w, Pc.colsum.data(), Pc.colsum.size(), ReduceOp::Sum);
+        allreduce_host(w, Pr.rowsum.data(), Pr.rowsum.size(), ReduceOp::Sum);
+        // diagonal magnitudes (counted in both)
+        std::vector<T> full;
+        std::vector<R> d(As.srows(), 0);
+        {
+            // diagonal: gather via per-tile host reads
+            Loc loc = loc_of(target);
+            lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+            for (int64_t i = 0; i < std::min(As.mt(), As.nt()); ++i) {
+                if (!As.tileIsLocal(i, i)) continue;
+                Tile<T> t = As.tile(i, i, loc);
+                int64_t nd = std::min(t.mb, t.nb);
+                std::vector<T> h(nd);
+                if (c.dev()) {
+                    device::memcpy2d_async(h.data(), sizeof(T), t.data, (t.stride + 1) * sizeof(T), sizeof(T), nd, c.stream);
+                    slate_hip_call(hipStreamSynchronize(c.stream));
+                } else for (int64_t ii = 0; ii < nd; ++ii) h[ii] = t.data[ii * (t.stride + 1)];
+                for (int64_t ii = 0; ii < nd; ++ii) d[grow_of(As, i) + ii] = std::abs(h[ii]);
+            }
+            allreduce_host(w, d.data(), d.size(), ReduceOp::Sum);
+        }
+        R v = 0;
+        for (size_t j = 0; j < d.size(); ++j) v = max_nan(v, Pc.colsum[j] + Pr.rowsum[j] - d[j]);
+        return v;
+    }
+    // Frobenius: 2 * |triangle|^2 - |diag|^2
+    NormParts<T> Pt;
+    local_parts(As, target, 'F', mask, diag, kl, ku, Pt);
+    R tri = finish_norm(As, 'F', Pt);
+    // diagonal Frobenius
+    NormParts<T> Pd;
+    {
+        Loc loc = loc_of(target);
+        lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+        for (int64_t i = 0; i < std::min(As.mt(), As.nt()); ++i) {
+            if (!As.tileIsLocal(i, i)) continue;
+            Tile<T> t = As.tile(i, i, loc);
+            int64_t nd = std::min(t.mb, t.nb);
+            std::vector<T> h(nd);
+            if (c.dev()) {
+                device::memcpy2d_async(h.data(), sizeof(T), t.data, (t.stride + 1) * sizeof(T), sizeof(T), nd, c.stream);
+                slate_hip_call(hipStreamSynchronize(c.stream));
+            } else for (int64_t ii = 0; ii < nd; ++ii) h[ii] = t.data[ii * (t.stride + 1)];
+            for (int64_t ii = 0; ii < nd; ++ii) add_sumsq(Pd.scale, Pd.sumsq, R(std::abs(h[ii])));
+        }
+    }
+    R dg = finish_norm(As, 'F', Pd);
+    R v2 = 2 * tri * tri - dg * dg;
+    return std::sqrt(std::max<R>(v2, 0));
+}
+
+template <typename T>
+void colNorms(Norm in_norm, Matrix<T> const& A, real_type<T>* values, Options const& opts) {
+    trace::Block tb("colNorms");
+    using R = real_type<T>;
+    Target target = resolve_target(opts);
+    slate_error_if_msg(in_norm != Norm::Max, "colNorms: only Norm::Max is supported (as the reference)");
+    slate_error_if_msg(A.op() != Op::NoTrans, "colNorms: NoTrans view required");
+    Loc loc = loc_of(target);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    int64_t n = A.n();
+    std::vector<R> v(n, 0);
+    LocalBlock<T> la = A.local(loc, false);
+    auto& s = *A.storage();
+    if (!la.empty()) {
+        std::vector<R> out(la.n);
+        lb::norm_partial(c, 'M', Uplo::General, Diag::NonUnit, la.m, la.n, la.ptr, la.ld, 0, 0, out.data());
+        for (int64_t jl = 0; jl < la.n; ++jl)
+            v[l2g(A.lcol_begin() + jl, s.nb, s.crel(), s.grid->q()) - A.col0()] = out[jl];
+    }
+    allreduce_host(A.grid()->world(), v.data(), v.size(), ReduceOp::Max);
+    std::copy(v.begin(), v.end(), values);
+}
+
+void sync() { if (device::available()) device::sync_all(); }
+
+//------------------------------------------------------------------------------
+#define SLATE_AUX_INST(T)                                                                               \
+    template void redistribute<T>(Matrix<T> const&, Matrix<T>&, Options const&);                       \
+    template void add<T>(T, Matrix<T> const&, T, Matrix<T>&, Options const&);                          \
+    template void add<T>(T, BaseTrapezoidMatrix<T> const&, T, BaseTrapezoidMatrix<T>&, Options const&); \
+    template void scale<T>(real_type<T>, real_type<T>, BaseMatrix<T>&, Options const&);                 \
+    template void scale_row_col<T>(Equed, std::vector<real_type<T>> const&, std::vector<real_type<T>> const&, Matrix<T>&, Options const&); \
+    template void set<T>(T, T, BaseMatrix<T>&, Options const&);                                          \
+    template void set<T>(std::function<T(int64_t, int64_t)> const&, BaseMatrix<T>&, Options const&);     \
+    template void gather<T>(BaseMatrix<T> const&, std::vector<T>&, Options const&);                     \
+    template real_type<T> norm<T>(Norm, BaseMatrix<T> const&, Options const&);                           \
+    template void colNorms<T>(Norm, Matrix<T> const&, real_type<T>*, Options const&);
+
+SLATE_AUX_INST(float)
+SLATE_AUX_INST(double)
+SLATE_AUX_INST(std::complex<float>)
+SLATE_AUX_INST(std::complex<double>)
+
+#define SLATE_COPY_INST(Ts, Td) template void copy<Ts, Td>(BaseMatrix<Ts> const&, BaseMatrix<Td>&, Options const&);
+SLATE_COPY_INST(float, float)
+SLATE_COPY_INST(double, double)
+SLATE_COPY_INST(float, double)
+SLATE_COPY_INST(double, float)
+SLATE_COPY_INST(std::complex<float>, std::complex<float>)
+SLATE_COPY_INST(std::complex<double>, std::complex<double>)
+SLATE_COPY_INST(std::complex<float>, std::complex<double>)
+SLATE_COPY_INST(std::complex<double>, std::complex<float>)
+
+}  // namespace slate

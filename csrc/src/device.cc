@@ -1,0 +1,206 @@
+// Device runtime implementation (see device.hh).
+#include "slate_amd/device.hh"
+
+#include <cstdlib>
+#include <algorithm>
+#include <string>
+
+namespace slate {
+namespace device {
+
+namespace {
+
+struct State {
+    std::mutex mtx;
+    int device = -1;
+    bool streams_ready = false;
+    hipStream_t streams[kNumQueues] = {};
+    std::vector<hipEvent_t> events;
+    // caching allocator: bucket size -> free list; ptr -> bucket size
+    std::multimap<size_t, void*> free_blocks;
+    std::map<void*, size_t> live;
+    size_t in_use = 0, cached = 0;
+};
+
+State& st() {
+    static State* s = new State();  // intentionally leaked: outlives static dtors
+    return *s;
+}
+
+size_t bucket(size_t bytes) {
+    // round to 2 MiB for large blocks, power-of-two-ish for small ones
+    const size_t big = size_t(2) << 20;
+    if (bytes >= big) return (bytes + big - 1) / big * big;
+    size_t b = 256;
+    while (b < bytes) b <<= 1;
+    return b;
+}
+
+void ensure_device_locked(State& s) {
+    if (s.device >= 0) return;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        throw DeviceException("no HIP device available", __func__, __FILE__, __LINE__);
+    int dev = 0;
+    if (const char* lr = std::getenv("LOCAL_RANK")) dev = std::atoi(lr) % n;
+    slate_hip_call(hipSetDevice(dev));
+    s.device = dev;
+}
+
+void ensure_streams_locked(State& s) {
+    ensure_device_locked(s);
+    if (s.streams_ready) return;
+    int lo = 0, hi = 0;
+    slate_hip_call(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    for (int i = 0; i < kNumQueues; ++i) {
+        // panel queue (1) gets the highest priority so panels preempt the
+        // trailing update; comm queue also high so broadcasts are not starved.
+        int prio = (i == 1 || i == kCommQueue) ? hi : lo;
+        slate_hip_call(hipStreamCreateWithPriority(&s.streams[i], hipStreamNonBlocking, prio));
+    }
+    s.streams_ready = true;
+}
+
+}  // namespace
+
+bool available() {
+    int n = 0;
+    return hipGetDeviceCount(&n) == hipSuccess && n > 0;
+}
+
+int count() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+void set_device(int dev) {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    if (s.device == dev) return;
+    slate_error_if_msg(s.streams_ready, "set_device after streams were created");
+    slate_hip_call(hipSetDevice(dev));
+    s.device = dev;
+}
+
+int get_device() {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_device_locked(s);
+    return s.device;
+}
+
+hipStream_t queue(int index) {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_streams_locked(s);
+    slate_assert(index >= 0 && index < kNumQueues);
+    return s.streams[index];
+}
+
+void sync_all() {
+    auto& s = st();
+    if (!s.streams_ready) return;
+    for (int i = 0; i < kNumQueues; ++i)
+        slate_hip_call(hipStreamSynchronize(s.streams[i]));
+}
+
+hipEvent_t event_get() {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_device_locked(s);
+    if (!s.events.empty()) {
+        hipEvent_t e = s.events.back();
+        s.events.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    slate_hip_call(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+
+void event_put(hipEvent_t e) {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    s.events.push_back(e);
+}
+
+void* malloc(size_t bytes) {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_device_locked(s);
+    size_t b = bucket(bytes);
+    auto it = s.free_blocks.find(b);
+    void* p = nullptr;
+    if (it != s.free_blocks.end()) {
+        p = it->second;
+        s.free_blocks.erase(it);
+        s.cached -= b;
+    } else {
+        hipError_t e = hipMalloc(&p, b);
+        if (e != hipSuccess) {
+            // release the cache and retry once
+            (void)hipGetLastError();
+            for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
+            s.free_blocks.clear();
+            s.cached = 0;
+            slate_hip_call(hipMalloc(&p, b));
+        }
+    }
+    s.live[p] = b;
+    s.in_use += b;
+    return p;
+}
+
+void free(void* ptr) {
+    if (!ptr) return;
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    auto it = s.live.find(ptr);
+    slate_assert(it != s.live.end());
+    size_t b = it->second;
+    s.live.erase(it);
+    s.in_use -= b;
+    s.free_blocks.emplace(b, ptr);
+    s.cached += b;
+}
+
+void release_cache() {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
+    s.free_blocks.clear();
+    s.cached = 0;
+}
+
+size_t bytes_in_use() { return st().in_use; }
+size_t bytes_cached() { return st().cached; }
+
+void* malloc_host(size_t bytes) {
+    void* p = nullptr;
+    slate_hip_call(hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    return p;
+}
+
+void free_host(void* ptr) {
+    if (ptr) (void)hipHostFree(ptr);
+}
+
+void memcpy_async(void* dst, const void* src, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    slate_hip_call(hipMemcpyAsync(dst, src, bytes, hipMemcpyDefault, s));
+}
+
+void memcpy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch,
+                    size_t width, size_t height, hipStream_t s) {
+    if (width == 0 || height == 0) return;
+    slate_hip_call(hipMemcpy2DAsync(dst, dpitch, src, spitch, width, height, hipMemcpyDefault, s));
+}
+
+void memset_async(void* dst, int v, size_t bytes, hipStream_t s) {
+    if (bytes == 0) return;
+    slate_hip_call(hipMemsetAsync(dst, v, bytes, s));
+}
+
+}  // namespace device
+}  // namespace slate

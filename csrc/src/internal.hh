@@ -1,0 +1,126 @@
+// Driver-internal helpers: distribution math over a view, panel broadcasts
+// and tile exchanges.  These replace the reference's listBcast / listReduce /
+// tileSend / tileRecv (BaseMatrix.hh:1762-2456) with whole-panel collectives:
+// one contiguous buffer per panel per communicator instead of one message
+// per tile.
+#pragma once
+
+#include "slate_amd/slate.hh"
+#include "slate_amd/runtime.hh"
+#include "slate_amd/trace.hh"
+
+#include <vector>
+
+namespace slate {
+namespace internal {
+
+/// Local row offset within `A`'s local block for view row-tile index i (first
+/// local row whose global index is >= start of tile i).
+template <typename T>
+inline int64_t lrow_of(BaseMatrix<T> const& A, int64_t i) {
+    auto& s = *A.storage();
+    int64_t g = (i < A.mt() ? std::max<int64_t>(0, (A.row0() / s.mb + i) * s.mb - A.row0()) : A.srows());
+    return g2l_ceil(A.row0() + std::min(g, A.srows()), s.mb, s.rrel(), s.grid->p()) - A.lrow_begin();
+}
+template <typename T>
+inline int64_t lcol_of(BaseMatrix<T> const& A, int64_t j) {
+    auto& s = *A.storage();
+    int64_t g = (j < A.nt() ? std::max<int64_t>(0, (A.col0() / s.nb + j) * s.nb - A.col0()) : A.scols());
+    return g2l_ceil(A.col0() + std::min(g, A.scols()), s.nb, s.crel(), s.grid->q()) - A.lcol_begin();
+}
+
+/// Global row/col (within view) where tile i/j starts.
+template <typename T>
+inline int64_t grow_of(BaseMatrix<T> const& A, int64_t i) {
+    auto& s = *A.storage();
+    if (i >= A.mt()) return A.srows();
+    return std::max<int64_t>(0, (A.row0() / s.mb + i) * s.mb - A.row0());
+}
+template <typename T>
+inline int64_t gcol_of(BaseMatrix<T> const& A, int64_t j) {
+    auto& s = *A.storage();
+    if (j >= A.nt()) return A.scols();
+    return std::max<int64_t>(0, (A.col0() / s.nb + j) * s.nb - A.col0());
+}
+
+/// Dense device/host buffer sized for panels.
+template <typename T>
+class Work {
+public:
+    Work() = default;
+    Work(Target t, size_t n) { resize(t, n); }
+    void resize(Target t, size_t n) {
+        dev_ = (t == Target::Devices);
+        if (n <= n_) return;
+        release();
+        n_ = std::max<size_t>(n, 1);
+        if (dev_) p_ = static_cast<T*>(device::malloc(n_ * sizeof(T)));
+        else { h_.assign(n_, T(0)); p_ = h_.data(); }
+    }
+    ~Work() { release(); }
+    Work(Work&& o) noexcept { *this = std::move(o); }
+    Work& operator=(Work&& o) noexcept {
+        release();
+        p_ = o.p_; n_ = o.n_; dev_ = o.dev_; h_ = std::move(o.h_);
+        if (!dev_) p_ = h_.data();
+        o.p_ = nullptr; o.n_ = 0;
+        return *this;
+    }
+    T* data() const { return p_; }
+    size_t size() const { return n_; }
+private:
+    void release() {
+        if (dev_ && p_) device::free(p_);
+        p_ = nullptr; n_ = 0; h_.clear();
+    }
+    T* p_ = nullptr;
+    size_t n_ = 0;
+    bool dev_ = false;
+    std::vector<T> h_;
+};
+
+/// Location of a target.
+inline Loc loc_of(Target t) { return t == Target::Devices ? Loc::Device : Loc::Host; }
+
+/// Normalize a HostTask/HostNest/HostBatch/Host target; Devices requires a GPU.
+inline Target resolve_target(Options const& opts) {
+    Target t = get_target(opts, Target::HostTask);
+    if (t == Target::Devices && !device::available())
+        slate_error("Target::Devices requested but no HIP device is available");
+    return t;
+}
+
+/// Broadcast a contiguous buffer over `comm` from `root` (stream-ordered).
+template <typename T>
+inline void bcast(Comm& comm, T* buf, size_t count, int root, lb::Ctx const& c) {
+    if (comm.size() == 1 || count == 0) return;
+    comm.bcast(buf, count, root, c.loc(), c.stream);
+}
+
+/// Pack a strided block into a dense buffer (ld = m).
+template <typename T>
+inline void pack(lb::Ctx const& c, int64_t m, int64_t n, T const* A, int64_t lda, T* W) {
+    lb::copy2d(c, m, n, A, lda, W, m);
+}
+
+/// Reduce info across ranks (reference internal_reduce_info.cc): min over
+/// nonzero values.
+int64_t reduce_info(int64_t info, Comm& comm);
+
+/// Read a device (or host) int info.
+int64_t fetch_info(Target t, int* info);
+
+/// All-gather of per-column norms etc. helper: allreduce on host vector.
+template <typename R>
+inline void allreduce_host(Comm& comm, R* v, size_t n, ReduceOp op) {
+    if (comm.size() == 1 || n == 0) return;
+    comm.allreduce(v, v, n, scalar_type<R>(), op, Loc::Host, nullptr);
+}
+
+/// General redistribution B = op(A) between two matrices over the same world
+/// (any grids / tile sizes with equal element counts), tile by tile over p2p.
+template <typename T>
+void redistribute_op(BaseMatrix<T> const& A, BaseMatrix<T>& B, Target target);
+
+}  // namespace internal
+}  // namespace slate

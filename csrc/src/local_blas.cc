@@ -1,0 +1,811 @@
+// Local BLAS/LAPACK dispatch: host C++ kernels or gfx950 device kernels.
+#include "slate_amd/local_blas.hh"
+#include "slate_amd/host_blas.hh"
+#include "../kernels/kernels.hh"
+
+#include <map>
+#include <mutex>
+#include <cstring>
+
+namespace slate {
+namespace lb {
+
+using slate_amd::dev::dptr;
+using slate_amd::dev::dval;
+namespace kd = slate_amd::dev;
+
+//==============================================================================
+// Scratch arenas
+namespace {
+
+struct Arena {
+    struct Chunk { char* p; size_t size; };
+    std::vector<Chunk> chunks;
+    size_t cur = 0;      // current chunk index
+    size_t off = 0;      // offset in current chunk
+};
+
+std::mutex g_arena_mtx;
+std::map<hipStream_t, Arena>& arenas() {
+    static auto* m = new std::map<hipStream_t, Arena>();
+    return *m;
+}
+
+inline size_t align256(size_t b) { return (b + 255) / 256 * 256; }
+
+}  // namespace
+
+Scratch::Scratch(Ctx const& ctx) : ctx_(ctx), arena_(nullptr), mark_(0) {
+    if (ctx_.dev()) {
+        std::lock_guard<std::mutex> g(g_arena_mtx);
+        Arena& a = arenas()[ctx_.stream];
+        arena_ = &a;
+        mark_ = (a.cur << 40) | a.off;
+    }
+}
+
+Scratch::~Scratch() {
+    if (ctx_.dev()) {
+        std::lock_guard<std::mutex> g(g_arena_mtx);
+        Arena& a = *static_cast<Arena*>(arena_);
+        a.cur = mark_ >> 40;
+        a.off = mark_ & ((size_t(1) << 40) - 1);
+    }
+    for (void* p : host_) std::free(p);
+}
+
+void* Scratch::alloc_bytes(size_t bytes) {
+    bytes = align256(std::max<size_t>(bytes, 1));
+    if (!ctx_.dev()) {
+        void* p = nullptr;
+        if (posix_memalign(&p, 256, bytes) != 0) throw std::bad_alloc();
+        std::memset(p, 0, bytes);
+        host_.push_back(p);
+        return p;
+    }
+    std::lock_guard<std::mutex> g(g_arena_mtx);
+    Arena& a = *static_cast<Arena*>(arena_);
+    while (true) {
+        if (a.cur < a.chunks.size()) {
+            auto& c = a.chunks[a.cur];
+            if (a.off + bytes <= c.size) {
+                void* p = c.p + a.off;
+                a.off += bytes;
+                return p;
+            }
+            // try next chunk
+            if (a.cur + 1 < a.chunks.size()) { a.cur++; a.off = 0; continue; }
+        }
+        // allocate a new chunk (at least 64 MiB, or twice the request)
+        size_t sz = std::max<size_t>(size_t(64) << 20, 2 * bytes);
+        char* p = static_cast<char*>(device::malloc(sz));
+        a.chunks.push_back({p, sz});
+        a.cur = a.chunks.size() - 1;
+        a.off = 0;
+    }
+}
+
+//==============================================================================
+namespace {
+
+inline char opc(Op op) { return char(op); }
+inline char upc(Uplo u) { return char(u); }
+
+template <typename T> constexpr bool is_real_v = !is_complex_v<T>;
+
+// device gemm dispatch (real -> MFMA, complex -> complex kernel)
+template <typename T>
+void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
+           T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    if (m <= 0 || n <= 0) return;
+    if constexpr (is_real_v<T>) {
+        char ta = opA == Op::NoTrans ? 'N' : 'T', tb = opB == Op::NoTrans ? 'N' : 'T';
+        if (uplo == 'G') kd::gemm_real<T>(ta, tb, m, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, s);
+        else {
+            slate_assert(m == n);
+            kd::gemm_tri_real<T>(uplo, ta, tb, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
+        }
+    } else {
+        kd::gemm_cplx(uplo, opc(opA), opc(opB), m, n, k, dval(alpha), dptr(A), lda, dptr(B), ldb,
+                      dval(beta), dptr(C), ldc, s);
+    }
+}
+
+template <typename T>
+void dset(hipStream_t s, char uplo, int64_t m, int64_t n, T off, T diag, T* A, int64_t lda) {
+    kd::geset(uplo, m, n, dval(off), dval(diag), dptr(A), lda, s);
+}
+
+template <typename T>
+void dcopy(hipStream_t s, int64_t m, int64_t n, T const* A, int64_t lda, T* B, int64_t ldb) {
+    if (m <= 0 || n <= 0) return;
+    device::memcpy2d_async(B, ldb * sizeof(T), A, lda * sizeof(T), m * sizeof(T), n, s);
+}
+
+}  // namespace
+
+//==============================================================================
+// BLAS-3
+
+template <typename T>
+void gemm(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
+          T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) { host::gemm(opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc); return; }
+    if constexpr (is_real_v<T>) {
+        // real: ConjTrans == Trans
+        if (opA == Op::ConjTrans) opA = Op::Trans;
+        if (opB == Op::ConjTrans) opB = Op::Trans;
+    }
+    dgemm(c.stream, 'G', opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}
+
+template <typename T>
+void gemm_tri(Ctx const& c, Uplo uplo, Op opA, Op opB, int64_t n, int64_t k, T alpha,
+              T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    if (n <= 0) return;
+    if (!c.dev()) {
+        // compute full into temp and copy the triangle
+        std::vector<T> W(size_t(n) * n);
+        for (int64_t j = 0; j < n; ++j) for (int64_t i = 0; i < n; ++i) W[i + j * n] = C[i + j * ldc];
+        host::gemm(opA, opB, n, n, k, alpha, A, lda, B, ldb, beta, W.data(), n);
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < n; ++i)
+                if (uplo == Uplo::Lower ? i >= j : i <= j) C[i + j * ldc] = W[i + j * n];
+        return;
+    }
+    if constexpr (is_real_v<T>) {
+        if (opA == Op::ConjTrans) opA = Op::Trans;
+        if (opB == Op::ConjTrans) opB = Op::Trans;
+    }
+    dgemm(c.stream, upc(uplo), opA, opB, n, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}
+
+template <typename T>
+void herk(Ctx const& c, Uplo uplo, Op op, int64_t n, int64_t k, real_type<T> alpha,
+          T const* A, int64_t lda, real_type<T> beta, T* C, int64_t ldc) {
+    if (n <= 0) return;
+    if (!c.dev()) { host::rankk(true, uplo, op, n, k, T(alpha), A, lda, T(beta), C, ldc); return; }
+    // C = alpha op(A) op(A)^H: op = N -> A A^H ; op = C -> A^H A
+    Op o1 = op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans;
+    Op o2 = op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans;
+    gemm_tri(c, uplo, o1, o2, n, k, T(alpha), A, lda, A, lda, T(beta), C, ldc);
+}
+
+template <typename T>
+void syrk(Ctx const& c, Uplo uplo, Op op, int64_t n, int64_t k, T alpha,
+          T const* A, int64_t lda, T beta, T* C, int64_t ldc) {
+    if (n <= 0) return;
+    if (!c.dev()) { host::rankk(false, uplo, op, n, k, alpha, A, lda, beta, C, ldc); return; }
+    Op o1 = op == Op::NoTrans ? Op::NoTrans : Op::Trans;
+    Op o2 = op == Op::NoTrans ? Op::Trans : Op::NoTrans;
+    gemm_tri(c, uplo, o1, o2, n, k, alpha, A, lda, A, lda, beta, C, ldc);
+}
+
+template <typename T>
+void her2k(Ctx const& c, Uplo uplo, Op op, int64_t n, int64_t k, T alpha, T const* A, int64_t lda,
+           T const* B, int64_t ldb, real_type<T> beta, T* C, int64_t ldc) {
+    if (n <= 0) return;
+    if (!c.dev()) { host::rank2k(true, uplo, op, n, k, alpha, A, lda, B, ldb, T(beta), C, ldc); return; }
+    Op o1 = op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans;
+    Op o2 = op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans;
+    gemm_tri(c, uplo, o1, o2, n, k, alpha, A, lda, B, ldb, T(beta), C, ldc);
+    gemm_tri(c, uplo, o1, o2, n, k, slate::conj(alpha), B, ldb, A, lda, T(1), C, ldc);
+}
+
+template <typename T>
+void syr2k(Ctx const& c, Uplo uplo, Op op, int64_t n, int64_t k, T alpha, T const* A, int64_t lda,
+           T const* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    if (n <= 0) return;
+    if (!c.dev()) { host::rank2k(false, uplo, op, n, k, alpha, A, lda, B, ldb, beta, C, ldc); return; }
+    Op o1 = op == Op::NoTrans ? Op::NoTrans : Op::Trans;
+    Op o2 = op == Op::NoTrans ? Op::Trans : Op::NoTrans;
+    gemm_tri(c, uplo, o1, o2, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+    gemm_tri(c, uplo, o1, o2, n, k, alpha, B, ldb, A, lda, T(1), C, ldc);
+}
+
+template <typename T>
+void hemm(Ctx const& c, Side side, Uplo uplo, int64_t m, int64_t n, T alpha, T const* A, int64_t lda,
+          T const* B, int64_t ldb, T beta, T* C, int64_t ldc, bool hermitian) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) { host::symm(hermitian, side, uplo, m, n, alpha, A, lda, B, ldb, beta, C, ldc); return; }
+    // expand the symmetric/Hermitian block into a dense scratch copy, then gemm
+    int64_t na = side == Side::Left ? m : n;
+    Scratch sc(c);
+    T* F = sc.alloc<T>(size_t(na) * na);
+    dcopy(c.stream, na, na, A, lda, F, na);
+    // G = full matrix: mirror (conj-)transpose of F, then the stored triangle
+    T* G = sc.alloc<T>(size_t(na) * na);
+    kd::gecopy('G', hermitian ? 'C' : 'T', na, na, dptr(F), na, dptr(G), na, c.stream);
+    kd::gecopy(upc(uplo), 'N', na, na, dptr(F), na, dptr(G), na, c.stream);
+    if (side == Side::Left) dgemm(c.stream, 'G', Op::NoTrans, Op::NoTrans, m, n, m, alpha, G, na, B, ldb, beta, C, ldc);
+    else dgemm(c.stream, 'G', Op::NoTrans, Op::NoTrans, m, n, n, alpha, B, ldb, G, na, beta, C, ldc);
+}
+
+//------------------------------------------------------------------------------
+template <typename T>
+void trtri_to(Ctx const& c, Uplo uplo, Diag diag, int64_t n, T const* A, int64_t lda, T* W, int64_t ldw) {
+    if (n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j) for (int64_t i = 0; i < n; ++i) {
+            bool in = uplo == Uplo::Lower ? i >= j : i <= j;
+            W[i + j * ldw] = in ? A[i + j * lda] : T(0);
+        }
+        host::trtri(uplo, diag, n, W, ldw);
+        return;
+    }
+    hipStream_t s = c.stream;
+    constexpr int NBS = 64;
+    dset(s, 'G', n, n, T(0), T(0), W, ldw);
+    kd::trtri_diag(upc(uplo), char(diag), n, NBS, dptr(A), lda, dptr(W), ldw, s);
+    Scratch sc(c);
+    T* tmp = sc.alloc<T>(size_t(n) * n / 2 + NBS * NBS);
+    for (int64_t sz = NBS; sz < n; sz *= 2) {
+        for (int64_t p = 0; p + sz < n; p += 2 * sz) {
+            int64_t s2 = std::min(sz, n - p - sz);
+            if (uplo == Uplo::Lower) {
+                // X21 = -X22 * A21 * X11 ; A21 = A[p+sz : +s2, p : +sz]
+                dgemm(s, 'G', Op::NoTrans, Op::NoTrans, s2, sz, sz, T(1), A + (p + sz) + p * lda, lda,
+                      W + p + p * ldw, ldw, T(0), tmp, s2);
+                dgemm(s, 'G', Op::NoTrans, Op::NoTrans, s2, sz, s2, T(-1), W + (p + sz) + (p + sz) * ldw, ldw,
+                      tmp, s2, T(0), W + (p + sz) + p * ldw, ldw);
+            } else {
+                // X12 = -X11 * A12 * X22 ; A12 = A[p : +sz, p+sz : +s2]
+                dgemm(s, 'G', Op::NoTrans, Op::NoTrans, sz, s2, s2, T(1), A + p + (p + sz) * lda, lda,
+                      W + (p + sz) + (p + sz) * ldw, ldw, T(0), tmp, sz);
+                dgemm(s, 'G', Op::NoTrans, Op::NoTrans, sz, s2, sz, T(-1), W + p + p * ldw, ldw,
+                      tmp, sz, T(0), W + p + (p + sz) * ldw, ldw);
+            }
+        }
+    }
+}
+
+template <typename T>
+void trtri(Ctx const& c, Uplo uplo, Diag diag, int64_t n, T* A, int64_t lda) {
+    if (n <= 0) return;
+    if (!c.dev()) { host::trtri(uplo, diag, n, A, lda); return; }
+    Scratch sc(c);
+    T* W = sc.alloc<T>(size_t(n) * n);
+    trtri_to(c, uplo, diag, n, A, lda, W, n);
+    // copy back the triangle (keep the other triangle of A untouched)
+    kd::gecopy(upc(uplo), 'N', n, n, dptr(W), n, dptr(A), lda, c.stream);
+}
+
+template <typename T>
+void trsm(Ctx const& c, Side side, Uplo uplo, Op op, Diag diag, int64_t m, int64_t n, T alpha,
+          T const* A, int64_t lda, T* B, int64_t ldb) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) { host::trsm(side, uplo, op, diag, m, n, alpha, A, lda, B, ldb); return; }
+    if constexpr (is_real_v<T>) { if (op == Op::ConjTrans) op = Op::Trans; }
+    hipStream_t s = c.stream;
+    if (alpha != T(1)) kd::geadd('G', m, n, dval(alpha), dptr(B), ldb, dval(T(0)), dptr(B), ldb, s);
+    const int64_t na = side == Side::Left ? m : n;
+    const int64_t BS = 512;
+    const bool lower_eff = (uplo == Uplo::Lower) == (op == Op::NoTrans);
+    Scratch sc(c);
+    const int64_t bs0 = std::min(BS, na);
+    T* Ainv = sc.alloc<T>(size_t(bs0) * bs0);
+    T* W = sc.alloc<T>(size_t(side == Side::Left ? bs0 * n : m * bs0));
+    int64_t nblk = ceildiv(na, BS);
+    for (int64_t t = 0; t < nblk; ++t) {
+        // Left: forward if lower_eff; Right: forward if !lower_eff
+        bool forward = (side == Side::Left) ? lower_eff : !lower_eff;
+        int64_t bi = forward ? t : nblk - 1 - t;
+        int64_t i0 = bi * BS, b = std::min(BS, na - i0);
+        trtri_to(c, uplo, diag, b, A + i0 + i0 * lda, lda, Ainv, b);
+        if (side == Side::Left) {
+            dcopy(s, b, n, B + i0, ldb, W, b);
+            dgemm(s, 'G', op, Op::NoTrans, b, n, b, T(1), Ainv, b, W, b, T(0), B + i0, ldb);
+            // remaining rows
+            int64_t r0 = forward ? i0 + b : 0, r1 = forward ? na : i0;
+            if (r1 > r0) {
+                if (op == Op::NoTrans)
+                    dgemm(s, 'G', Op::NoTrans, Op::NoTrans, r1 - r0, n, b, T(-1), A + r0 + i0 * lda, lda,
+                          B + i0, ldb, T(1), B + r0, ldb);
+                else
+                    dgemm(s, 'G', op, Op::NoTrans, r1 - r0, n, b, T(-1), A + i0 + r0 * lda, lda,
+                          B + i0, ldb, T(1), B + r0, ldb);
+            }
+        } else {
+            dcopy(s, m, b, B + i0 * ldb, ldb, W, m);
+            dgemm(s, 'G', Op::NoTrans, op, m, b, b, T(1), W, m, Ainv, b, T(0), B + i0 * ldb, ldb);
+            int64_t r0 = forward ? i0 + b : 0, r1 = forward ? na : i0;
+            if (r1 > r0) {
+                if (op == Op::NoTrans)
+                    dgemm(s, 'G', Op::NoTrans, Op::NoTrans, m, r1 - r0, b, T(-1), B + i0 * ldb, ldb,
+                          A + i0 + r0 * lda, lda, T(1), B + r0 * ldb, ldb);
+                else
+                    dgemm(s, 'G', Op::NoTrans, op, m, r1 - r0, b, T(-1), B + i0 * ldb, ldb,
+                          A + r0 + i0 * lda, lda, T(1), B + r0 * ldb, ldb);
+            }
+        }
+    }
+}
+
+template <typename T>
+void trmm(Ctx const& c, Side side, Uplo uplo, Op op, Diag diag, int64_t m, int64_t n, T alpha,
+          T const* A, int64_t lda, T* B, int64_t ldb) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) { host::trmm(side, uplo, op, diag, m, n, alpha, A, lda, B, ldb); return; }
+    if constexpr (is_real_v<T>) { if (op == Op::ConjTrans) op = Op::Trans; }
+    hipStream_t s = c.stream;
+    int64_t na = side == Side::Left ? m : n;
+    Scratch sc(c);
+    T* F = sc.alloc<T>(size_t(na) * na);
+    T* W = sc.alloc<T>(size_t(m) * n);
+    // dense triangle with explicit zeros; unit diagonal set by walking the
+    // diagonal as a 1 x na view with ld = na + 1
+    dset(s, 'G', na, na, T(0), T(0), F, na);
+    kd::gecopy(upc(uplo), 'N', na, na, dptr(A), lda, dptr(F), na, s);
+    if (diag == Diag::Unit) dset(s, 'G', 1, na, T(1), T(1), F, na + 1);
+    dcopy(s, m, n, B, ldb, W, m);
+    if (side == Side::Left) dgemm(s, 'G', op, Op::NoTrans, m, n, m, alpha, F, na, W, m, T(0), B, ldb);
+    else dgemm(s, 'G', Op::NoTrans, op, m, n, n, alpha, W, m, F, na, T(0), B, ldb);
+}
+
+//------------------------------------------------------------------------------
+template <typename T>
+void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int64_t info_offset) {
+    if (n <= 0) return;
+    if (!c.dev()) {
+        int64_t r = host::potrf(uplo, n, A, lda);
+        if (r != 0 && info && *info == 0) *info = int(info_offset + r);
+        return;
+    }
+    constexpr int64_t NB0 = 64;
+    if (n <= NB0) { kd::potrf_small(upc(uplo), int(n), dptr(A), lda, info, int(info_offset), c.stream); return; }
+    int64_t n1 = roundup(ceildiv(n, 2), NB0), n2 = n - n1;
+    potrf(c, uplo, n1, A, lda, info, info_offset);
+    if (uplo == Uplo::Lower) {
+        trsm(c, Side::Right, Uplo::Lower, Op::ConjTrans, Diag::NonUnit, n2, n1, T(1), A, lda, A + n1, lda);
+        herk(c, Uplo::Lower, Op::NoTrans, n2, n1, real_type<T>(-1), A + n1, lda, real_type<T>(1), A + n1 + n1 * lda, lda);
+    } else {
+        trsm(c, Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, n1, n2, T(1), A, lda, A + n1 * lda, lda);
+        herk(c, Uplo::Upper, Op::ConjTrans, n2, n1, real_type<T>(-1), A + n1 * lda, lda, real_type<T>(1), A + n1 + n1 * lda, lda);
+    }
+    potrf(c, uplo, n2, A + n1 + n1 * lda, lda, info, info_offset + n1);
+}
+
+template <typename T>
+void lauum(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda) {
+    if (n <= 0) return;
+    if (!c.dev()) { host::lauum(uplo, n, A, lda); return; }
+    Scratch sc(c);
+    T* F = sc.alloc<T>(size_t(n) * n);
+    dset(c.stream, 'G', n, n, T(0), T(0), F, n);
+    kd::gecopy(upc(uplo), 'N', n, n, dptr(A), lda, dptr(F), n, c.stream);
+    if (uplo == Uplo::Lower)
+        gemm_tri(c, Uplo::Lower, Op::ConjTrans, Op::NoTrans, n, n, T(1), F, n, F, n, T(0), A, lda);
+    else
+        gemm_tri(c, Uplo::Upper, Op::NoTrans, Op::ConjTrans, n, n, T(1), F, n, F, n, T(0), A, lda);
+}
+
+//------------------------------------------------------------------------------
+// LU panel
+namespace {
+
+template <typename T>
+struct LuPanelDev {
+    hipStream_t s;
+    int64_t m, ncols;          // panel rows, panel width (swaps span all ncols)
+    T* A0; int64_t lda;
+    int64_t* ipiv; int64_t* perm;
+    int* info; int64_t info_offset;
+    real_type<T>* pval; int64_t* pidx;
+    bool pivot;
+    Ctx ctx;
+
+    void narrow(int64_t c0, int64_t nn) {
+        using DT = kd::dev_t<T>;
+        DT* A = dptr(A0);
+        int64_t kmax = std::min(nn, m - c0);
+        if (kmax <= 0) return;
+        int nparts = int(ceildiv(m - c0, 256));
+        if (pivot) kd::lu_colmax<DT>(m, c0, A, lda, c0, pval, pidx, nparts, s);
+        for (int64_t j = 0; j < kmax; ++j) {
+            int64_t col = c0 + j;
+            if (pivot)
+                kd::lu_pivot<DT>(nparts, pval, pidx, col, col, A, lda, ncols, ipiv, 0, perm, info, info_offset, nullptr, s);
+            else
+                kd::lu_pivot<DT>(0, pval, pidx, col, col, A, lda, ncols, ipiv, 0, perm, info, info_offset, nullptr, s);
+            kd::lu_update<DT>(m, col, col, c0 + nn, A, lda, pval, pidx, s);
+            nparts = int(ceildiv(m - col - 1, 256));
+        }
+    }
+
+    void rec(int64_t c0, int64_t nn) {
+        constexpr int64_t W = 32;
+        if (c0 >= m) return;
+        if (nn <= W) { narrow(c0, nn); return; }
+        int64_t n1 = roundup(ceildiv(nn, 2), W), n2 = nn - n1;
+        rec(c0, n1);
+        if (c0 + n1 > m) return;
+        // U12 = L11^{-1} A12 ; A22 -= L21 U12
+        trsm(ctx, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, n1, n2, T(1),
+             A0 + c0 + c0 * lda, lda, A0 + c0 + (c0 + n1) * lda, lda);
+        dgemm(s, 'G', Op::NoTrans, Op::NoTrans, m - c0 - n1, n2, n1, T(-1),
+              A0 + (c0 + n1) + c0 * lda, lda, A0 + c0 + (c0 + n1) * lda, lda, T(1),
+              A0 + (c0 + n1) + (c0 + n1) * lda, lda);
+        rec(c0 + n1, n2);
+    }
+};
+
+}  // namespace
+
+template <typename T>
+void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, int64_t* perm,
+                 int* info, int64_t info_offset, bool pivot) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        std::vector<int64_t> piv(std::min(m, n));
+        int64_t r = host::getrf(m, n, A, lda, piv.data(), pivot);
+        if (r != 0 && info && *info == 0) *info = int(info_offset + r);
+        for (size_t j = 0; j < piv.size(); ++j) ipiv[j] = piv[j];
+        if (perm) {
+            for (int64_t i = 0; i < m; ++i) perm[i] = i;
+            for (size_t j = 0; j < piv.size(); ++j) std::swap(perm[j], perm[piv[j]]);
+        }
+        return;
+    }
+    Scratch sc(c);
+    LuPanelDev<T> P;
+    P.s = c.stream; P.m = m; P.ncols = n; P.A0 = A; P.lda = lda; P.ipiv = ipiv; P.perm = perm;
+    P.info = info; P.info_offset = info_offset; P.pivot = pivot; P.ctx = c;
+    int64_t np = ceildiv(m, 256) + 1;
+    P.pval = sc.alloc<real_type<T>>(np);
+    P.pidx = sc.alloc<int64_t>(np);
+    if (perm) kd::iota(m, perm, c.stream);
+    P.rec(0, std::min(m, n));
+    // columns beyond min(m,n) (wide panel): U12 = L11^{-1} A12
+    if (n > m)
+        trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, m, n - m, T(1), A, lda, A + m * lda, lda);
+}
+
+template <typename T>
+void apply_perm(Ctx const& c, int64_t k, int64_t const* perm, int64_t const* ipiv, int64_t n, T* B, int64_t ldb) {
+    if (k <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        // rows [0, k) and pivot rows: new[t] = old[perm[t]]
+        std::vector<int64_t> rows;
+        for (int64_t t = 0; t < k; ++t) rows.push_back(t);
+        for (int64_t t = 0; t < k; ++t) if (ipiv[t] >= k) rows.push_back(ipiv[t]);
+        std::vector<T> tmp(rows.size());
+        for (int64_t j = 0; j < n; ++j) {
+            T* col = B + j * ldb;
+            for (size_t r = 0; r < rows.size(); ++r) tmp[r] = col[perm[rows[r]]];
+            for (size_t r = 0; r < rows.size(); ++r) col[rows[r]] = tmp[r];
+        }
+        return;
+    }
+    Scratch sc(c);
+    int64_t* dst = sc.alloc<int64_t>(2 * k);
+    int64_t* src = sc.alloc<int64_t>(2 * k);
+    kd::perm_pairs(k, perm, ipiv, dst, src, c.stream);
+    kd::permute_rows(n, dptr(B), ldb, dst, src, nullptr, int(2 * k), c.stream);
+}
+
+//------------------------------------------------------------------------------
+// QR panel
+template <typename T>
+void form_v(Ctx const& c, int64_t m, int64_t k, T const* A, int64_t lda, T* W, int64_t ldw) {
+    if (m <= 0 || k <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < k; ++j)
+            for (int64_t i = 0; i < m; ++i)
+                W[i + j * ldw] = i < j ? T(0) : (i == j ? T(1) : A[i + j * lda]);
+        return;
+    }
+    dcopy(c.stream, m, k, A, lda, W, ldw);
+    dset(c.stream, 'U', std::min(m, k), k, T(0), T(1), W, ldw);
+}
+
+template <typename T>
+void larfb(Ctx const& c, Side side, Op op, int64_t m, int64_t n, int64_t k, T const* V, int64_t ldv,
+           T const* Tm, int64_t ldt, T* C, int64_t ldc) {
+    if (m <= 0 || n <= 0 || k <= 0) return;
+    if (!c.dev()) { host::larfb(side, op, m, n, k, V, ldv, Tm, ldt, C, ldc); return; }
+    hipStream_t s = c.stream;
+    Scratch sc(c);
+    int64_t mv = side == Side::Left ? m : n;
+    T* Vx = sc.alloc<T>(size_t(mv) * k);
+    form_v(c, mv, k, V, ldv, Vx, mv);
+    Op tOp = op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans;
+    if constexpr (is_real_v<T>) { if (tOp == Op::ConjTrans) tOp = Op::Trans; }
+    Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+    if (side == Side::Left) {
+        T* W = sc.alloc<T>(size_t(k) * n);
+        T* W2 = sc.alloc<T>(size_t(k) * n);
+        // W = V^H C (k x n, K = m): tall-skinny when n small
+        if (n <= 64 && k <= 32) {
+            T* work = sc.alloc<T>(size_t(1) << 20);
+            kd::tsip(m, int(k), int(n), dval(T(1)), dptr(Vx), mv, dptr(C), ldc, dval(T(0)), dptr(W), k,
+                     dptr(work), int64_t(1) << 20, s);
+        } else {
+            dgemm(s, 'G', cT, Op::NoTrans, k, n, m, T(1), Vx, mv, C, ldc, T(0), W, k);
+        }
+        dgemm(s, 'G', tOp, Op::NoTrans, k, n, k, T(1), Tm, ldt, W, k, T(0), W2, k);
+        dgemm(s, 'G', Op::NoTrans, Op::NoTrans, m, n, k, T(-1), Vx, mv, W2, k, T(1), C, ldc);
+    } else {
+        T* W = sc.alloc<T>(size_t(m) * k);
+        T* W2 = sc.alloc<T>(size_t(m) * k);
+        dgemm(s, 'G', Op::NoTrans, Op::NoTrans, m, k, n, T(1), C, ldc, Vx, mv, T(0), W, m);
+        dgemm(s, 'G', Op::NoTrans, tOp, m, k, k, T(1), W, m, Tm, ldt, T(0), W2, m);
+        dgemm(s, 'G', Op::NoTrans, cT, m, n, k, T(-1), W2, m, Vx, mv, T(1), C, ldc);
+    }
+}
+
+namespace {
+
+template <typename T>
+struct QrPanelDev {
+    hipStream_t s;
+    int64_t m;
+    T* A0; int64_t lda;
+    T* tau;
+    T* Tm; int64_t ldt;
+    Ctx ctx;
+    real_type<T>* psum; T* alpha; T* pdots; T* work; int64_t work_elems;
+
+    // narrow block [c0, c0+nn): Householder columns + T block (nn x nn at Tm[c0, c0])
+    void narrow(int64_t c0, int64_t nn) {
+        using DT = kd::dev_t<T>;
+        DT* A = dptr(A0);
+        int64_t kmax = std::min(nn, m - c0);
+        if (kmax <= 0) return;
+        int nparts = int(std::max<int64_t>(1, ceildiv(m - c0 - 1, 256)));
+        kd::qr_colnorm<DT>(m, c0, A, lda, c0, psum, dptr(alpha), nparts, s);
+        for (int64_t j = 0; j < kmax; ++j) {
+            int64_t col = c0 + j;
+            int nblk = int(ceildiv(m - col, 256));
+            kd::qr_reflect_dots<DT>(m, col, col, c0 + nn, A, lda, nparts, psum, dptr(alpha), dptr(tau + col),
+                                    dptr(pdots), nblk, s);
+            kd::qr_update<DT>(m, col, col, c0 + nn, A, lda, nblk, dptr(pdots), dptr(tau + col), psum,
+                              dptr(alpha), nblk, s);
+            nparts = nblk;
+        }
+        // T block: S = V^H V then larft recurrence
+        Scratch sc(ctx);
+        int64_t mv = m - c0;
+        T* Vx = sc.alloc<T>(size_t(mv) * kmax);
+        form_v(ctx, mv, kmax, A0 + c0 + c0 * lda, lda, Vx, mv);
+        T* Tb = Tm + c0 + c0 * ldt;
+        kd::tsip(mv, int(kmax), int(kmax), dval(T(1)), dptr(Vx), mv, dptr(Vx), mv, dval(T(0)), dptr(Tb), ldt,
+                 dptr(work), work_elems, s);
+        kd::larft_small(int(kmax), dptr(tau + c0), dptr(Tb), ldt, s);
+    }
+
+    void rec(int64_t c0, int64_t nn) {
+        constexpr int64_t W = 32;
+        if (c0 >= m) return;
+        if (nn <= W) { narrow(c0, nn); return; }
+        int64_t n1 = roundup(ceildiv(nn, 2), W), n2 = nn - n1;
+        rec(c0, n1);
+        // apply H1^H to the right columns
+        larfb(ctx, Side::Left, Op::ConjTrans, m - c0, n2, std::min(n1, m - c0), A0 + c0 + c0 * lda, lda,
+              Tm + c0 + c0 * ldt, ldt, A0 + c0 + (c0 + n1) * lda, lda);
+        rec(c0 + n1, n2);
+        if (c0 + n1 >= m) return;
+        // merge: T12 = -T11 (V1^H V2) T22, V1 rows from c0+n1, V2 rows from c0+n1
+        int64_t k2 = std::min(n2, m - c0 - n1);
+        Scratch sc(ctx);
+        int64_t mv = m - c0 - n1;
+        T* V2 = sc.alloc<T>(size_t(mv) * k2);
+        form_v(ctx, mv, k2, A0 + (c0 + n1) + (c0 + n1) * lda, lda, V2, mv);
+        T* S = sc.alloc<T>(size_t(n1) * k2);
+        Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+        // V1 rows [c0+n1, m) are plain stored (below V1's diagonal block)
+        dgemm(s, 'G', cT, Op::NoTrans, n1, k2, mv, T(1), A0 + (c0 + n1) + c0 * lda, lda, V2, mv, T(0), S, n1);
+        T* S2 = sc.alloc<T>(size_t(n1) * k2);
+        dgemm(s, 'G', Op::NoTrans, Op::NoTrans, n1, k2, k2, T(1), S, n1, Tm + (c0 + n1) + (c0 + n1) * ldt, ldt,
+              T(0), S2, n1);
+        // T11 is upper triangular: zero its strict lower part in the product via trmm
+        trmm(ctx, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, n1, k2, T(-1),
+             Tm + c0 + c0 * ldt, ldt, S2, n1);
+        dcopy(s, n1, k2, S2, n1, Tm + c0 + (c0 + n1) * ldt, ldt);
+    }
+};
+
+}  // namespace
+
+template <typename T>
+void geqrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, T* tau, T* Tm, int64_t ldt) {
+    if (m <= 0 || n <= 0) return;
+    int64_t k = std::min(m, n);
+    if (!c.dev()) {
+        host::geqr2(m, n, A, lda, tau);
+        host::larft(m, k, A, lda, tau, Tm, ldt);
+        return;
+    }
+    Scratch sc(c);
+    QrPanelDev<T> P;
+    P.s = c.stream; P.m = m; P.A0 = A; P.lda = lda; P.tau = tau; P.Tm = Tm; P.ldt = ldt; P.ctx = c;
+    int64_t np = ceildiv(m, 256) + 1;
+    P.psum = sc.alloc<real_type<T>>(np);
+    P.alpha = sc.alloc<T>(2);
+    P.pdots = sc.alloc<T>(size_t(np) * 64);
+    P.work_elems = int64_t(1) << 20;
+    P.work = sc.alloc<T>(P.work_elems);
+    dset(c.stream, 'G', k, k, T(0), T(0), Tm, ldt);
+    P.rec(0, k);
+    if (n > k) {
+        // wide panel: apply Q^H to the remaining columns
+        larfb(c, Side::Left, Op::ConjTrans, m, n - k, k, A, lda, Tm, ldt, A + k * lda, lda);
+    }
+}
+
+//==============================================================================
+// aux
+template <typename T>
+void set(Ctx const& c, Uplo uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < m; ++i) {
+                if (uplo == Uplo::Lower && i < j) continue;
+                if (uplo == Uplo::Upper && i > j) continue;
+                A[i + j * lda] = i == j ? diag : offdiag;
+            }
+        return;
+    }
+    dset(c.stream, upc(uplo), m, n, offdiag, diag, A, lda);
+}
+
+template <typename Ts, typename Td>
+void copy(Ctx const& c, Uplo uplo, Op op, int64_t m, int64_t n, Ts const* A, int64_t lda, Td* B, int64_t ldb) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < m; ++i) {
+                if (uplo == Uplo::Lower && i < j) continue;
+                if (uplo == Uplo::Upper && i > j) continue;
+                Ts v = host::opval(op, A, lda, i, j);
+                if constexpr (is_complex_v<Td>) B[i + j * ldb] = Td(std::real(v), std::imag(v));
+                else B[i + j * ldb] = Td(std::real(v));
+            }
+        return;
+    }
+    if (std::is_same<Ts, Td>::value && op == Op::NoTrans && uplo == Uplo::General) {
+        device::memcpy2d_async(B, ldb * sizeof(Td), A, lda * sizeof(Ts), m * sizeof(Ts), n, c.stream);
+        return;
+    }
+    kd::gecopy(upc(uplo), opc(op), m, n, dptr(A), lda, dptr(B), ldb, c.stream);
+}
+
+template <typename T>
+void add(Ctx const& c, Uplo uplo, int64_t m, int64_t n, T alpha, T const* A, int64_t lda, T beta, T* B, int64_t ldb) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < m; ++i) {
+                if (uplo == Uplo::Lower && i < j) continue;
+                if (uplo == Uplo::Upper && i > j) continue;
+                B[i + j * ldb] = alpha * A[i + j * lda] + (beta == T(0) ? T(0) : beta * B[i + j * ldb]);
+            }
+        return;
+    }
+    kd::geadd(upc(uplo), m, n, dval(alpha), dptr(A), lda, dval(beta), dptr(B), ldb, c.stream);
+}
+
+template <typename T>
+void scale(Ctx const& c, Uplo uplo, int64_t m, int64_t n, real_type<T> numer, real_type<T> denom, T* A, int64_t lda) {
+    if (m <= 0 || n <= 0) return;
+    real_type<T> mul = numer / denom;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < m; ++i) {
+                if (uplo == Uplo::Lower && i < j) continue;
+                if (uplo == Uplo::Upper && i > j) continue;
+                A[i + j * lda] *= mul;
+            }
+        return;
+    }
+    kd::gescale(upc(uplo), m, n, mul, dptr(A), lda, c.stream);
+}
+
+template <typename T>
+void scale_row_col(Ctx const& c, int64_t m, int64_t n, real_type<T> const* R, real_type<T> const* Cs, T* A, int64_t lda) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < m; ++i)
+                A[i + j * lda] *= (R ? R[i] : real_type<T>(1)) * (Cs ? Cs[j] : real_type<T>(1));
+        return;
+    }
+    kd::gescale_row_col(m, n, R, Cs, dptr(A), lda, c.stream);
+}
+
+template <typename T>
+void norm_partial(Ctx const& c, char kind, Uplo uplo, Diag diag, int64_t m, int64_t n, T const* A, int64_t lda,
+                  int64_t goff_row, int64_t goff_col, real_type<T>* out) {
+    using R = real_type<T>;
+    if (m <= 0 || n <= 0) return;
+    auto inc = [&](int64_t i, int64_t j) {
+        int64_t gi = goff_row + i, gj = goff_col + j;
+        return uplo == Uplo::General || (uplo == Uplo::Lower ? gi >= gj : gi <= gj);
+    };
+    if (!c.dev()) {
+        if (kind == 'I') {
+            for (int64_t i = 0; i < m; ++i) out[i] = 0;
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < m; ++i)
+                    if (inc(i, j)) out[i] += (diag == Diag::Unit && goff_row + i == goff_col + j) ? R(1) : std::abs(A[i + j * lda]);
+            return;
+        }
+        for (int64_t j = 0; j < n; ++j) {
+            R v = 0, scl = 0, ssq = 1;
+            for (int64_t i = 0; i < m; ++i) {
+                if (!inc(i, j)) continue;
+                R a = (diag == Diag::Unit && goff_row + i == goff_col + j) ? R(1) : std::abs(A[i + j * lda]);
+                if (kind == 'M') v = max_nan(v, a);
+                else if (kind == '1') v += a;
+                else add_sumsq(scl, ssq, a);
+            }
+            if (kind == 'F') { out[2 * j] = scl; out[2 * j + 1] = scl == 0 ? 0 : ssq; }
+            else out[j] = v;
+        }
+        return;
+    }
+    Scratch sc(c);
+    int64_t cnt = kind == 'I' ? m : (kind == 'F' ? 2 * n : n);
+    R* d = sc.alloc<R>(cnt);
+    kd::genorm_partial(kind, upc(uplo), char(diag), m, n, dptr(A), lda, goff_row, goff_col, d, c.stream);
+    device::memcpy_async(out, d, cnt * sizeof(R), c.stream);
+    slate_hip_call(hipStreamSynchronize(c.stream));
+}
+
+template <typename T>
+void copy2d(Ctx const& c, int64_t m, int64_t n, T const* src, int64_t lds, T* dst, int64_t ldd) {
+    if (m <= 0 || n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t j = 0; j < n; ++j) std::memcpy(dst + j * ldd, src + j * lds, m * sizeof(T));
+        return;
+    }
+    device::memcpy2d_async(dst, ldd * sizeof(T), src, lds * sizeof(T), m * sizeof(T), n, c.stream);
+}
+
+//==============================================================================
+// instantiations
+#define SLATE_LB_INST(T)                                                                                   \
+    template void gemm<T>(Ctx const&, Op, Op, int64_t, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
+    template void gemm_tri<T>(Ctx const&, Uplo, Op, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
+    template void herk<T>(Ctx const&, Uplo, Op, int64_t, int64_t, real_type<T>, T const*, int64_t, real_type<T>, T*, int64_t); \
+    template void syrk<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T, T*, int64_t);  \
+    template void her2k<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, real_type<T>, T*, int64_t); \
+    template void syr2k<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
+    template void hemm<T>(Ctx const&, Side, Uplo, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t, bool); \
+    template void trsm<T>(Ctx const&, Side, Uplo, Op, Diag, int64_t, int64_t, T, T const*, int64_t, T*, int64_t); \
+    template void trmm<T>(Ctx const&, Side, Uplo, Op, Diag, int64_t, int64_t, T, T const*, int64_t, T*, int64_t); \
+    template void potrf<T>(Ctx const&, Uplo, int64_t, T*, int64_t, int*, int64_t);                        \
+    template void trtri<T>(Ctx const&, Uplo, Diag, int64_t, T*, int64_t);                                 \
+    template void trtri_to<T>(Ctx const&, Uplo, Diag, int64_t, T const*, int64_t, T*, int64_t);           \
+    template void lauum<T>(Ctx const&, Uplo, int64_t, T*, int64_t);                                        \
+    template void getrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, int64_t*, int64_t*, int*, int64_t, bool); \
+    template void apply_perm<T>(Ctx const&, int64_t, int64_t const*, int64_t const*, int64_t, T*, int64_t); \
+    template void geqrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, T*, T*, int64_t);             \
+    template void larfb<T>(Ctx const&, Side, Op, int64_t, int64_t, int64_t, T const*, int64_t, T const*, int64_t, T*, int64_t); \
+    template void form_v<T>(Ctx const&, int64_t, int64_t, T const*, int64_t, T*, int64_t);                \
+    template void set<T>(Ctx const&, Uplo, int64_t, int64_t, T, T, T*, int64_t);                           \
+    template void add<T>(Ctx const&, Uplo, int64_t, int64_t, T, T const*, int64_t, T, T*, int64_t);      \
+    template void scale<T>(Ctx const&, Uplo, int64_t, int64_t, real_type<T>, real_type<T>, T*, int64_t);   \
+    template void scale_row_col<T>(Ctx const&, int64_t, int64_t, real_type<T> const*, real_type<T> const*, T*, int64_t); \
+    template void norm_partial<T>(Ctx const&, char, Uplo, Diag, int64_t, int64_t, T const*, int64_t, int64_t, int64_t, real_type<T>*); \
+    template void copy2d<T>(Ctx const&, int64_t, int64_t, T const*, int64_t, T*, int64_t);
+
+SLATE_LB_INST(float)
+SLATE_LB_INST(double)
+SLATE_LB_INST(std::complex<float>)
+SLATE_LB_INST(std::complex<double>)
+
+#define SLATE_LB_COPY(Ts, Td) \
+    template void copy<Ts, Td>(Ctx const&, Uplo, Op, int64_t, int64_t, Ts const*, int64_t, Td*, int64_t);
+SLATE_LB_COPY(float, float)
+SLATE_LB_COPY(double, double)
+SLATE_LB_COPY(float, double)
+SLATE_LB_COPY(double, float)
+SLATE_LB_COPY(std::complex<float>, std::complex<float>)
+SLATE_LB_COPY(std::complex<double>, std::complex<double>)
+SLATE_LB_COPY(std::complex<float>, std::complex<double>)
+SLATE_LB_COPY(std::complex<double>, std::complex<float>)
+
+}  // namespace lb
+}  // namespace slate

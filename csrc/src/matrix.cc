@@ -1,0 +1,282 @@
+// MatrixStorage / BaseMatrix implementation and explicit instantiations.
+#include "slate_amd/matrix.hh"
+
+#include <complex>
+#include <cstring>
+#include <cstdlib>
+
+namespace slate {
+
+namespace {
+int64_t pad_ld(int64_t mloc, size_t elem) {
+    // 256-byte aligned columns, and avoid exact large powers of two (which
+    // alias columns onto the same channels/sets).
+    int64_t align = std::max<int64_t>(1, 256 / int64_t(elem));
+    int64_t ld = roundup(std::max<int64_t>(mloc, 1), align);
+    if (ld * int64_t(elem) % 4096 == 0 && ld > 1024) ld += align;
+    return ld;
+}
+}  // namespace
+
+template <typename T>
+MatrixStorage<T>::MatrixStorage(int64_t m_, int64_t n_, int64_t mb_, int64_t nb_, GridPtr g,
+                                int rsrc_, int csrc_)
+    : m(m_), n(n_), mb(mb_), nb(nb_), grid(g), rsrc(rsrc_), csrc(csrc_)
+{
+    slate_error_if_msg(m < 0 || n < 0, "negative matrix dimension");
+    slate_error_if_msg(mb <= 0 || nb <= 0, "tile size must be positive");
+    slate_error_if_msg(rsrc < 0 || rsrc >= grid->p() || csrc < 0 || csrc >= grid->q(), "bad rsrc/csrc");
+    mloc = numroc(m, mb, rrel(), grid->p());
+    nloc = numroc(n, nb, crel(), grid->q());
+    lld = pad_ld(mloc, sizeof(T));
+}
+
+template <typename T>
+MatrixStorage<T>::~MatrixStorage() {
+    if (host_owned_ && host_) std::free(host_);
+    if (dev_owned_ && dev_) {
+        try { device::free(dev_); } catch (...) {}
+    }
+}
+
+template <typename T>
+void MatrixStorage<T>::attach(T* ptr, int64_t ld_, Loc loc) {
+    slate_error_if_msg(ld_ < std::max<int64_t>(1, mloc), "leading dimension too small");
+    if (loc == Loc::Host) {
+        slate_assert(!host_);
+        host_ = ptr; host_ld_ = ld_; host_owned_ = false; host_state_ = Modified;
+        if (dev_) dev_state_ = Invalid;
+    } else {
+        slate_assert(!dev_);
+        dev_ = ptr; dev_ld_ = ld_; dev_owned_ = false; dev_state_ = Modified;
+        if (host_) host_state_ = Invalid;
+    }
+    origin_ = loc;
+    kind_ = TileKind::UserOwned;
+}
+
+template <typename T>
+void MatrixStorage<T>::allocate(Loc loc) {
+    size_t bytes = size_t(lld) * size_t(std::max<int64_t>(nloc, 1)) * sizeof(T);
+    if (loc == Loc::Host) {
+        if (host_) return;
+        void* p = nullptr;
+        if (posix_memalign(&p, 256, std::max<size_t>(bytes, 256)) != 0) throw std::bad_alloc();
+        host_ = static_cast<T*>(p);
+        host_ld_ = lld; host_owned_ = true;
+        if (!dev_) origin_ = Loc::Host;
+    } else {
+        if (dev_) return;
+        dev_ = static_cast<T*>(device::malloc(std::max<size_t>(bytes, 256)));
+        dev_ld_ = lld; dev_owned_ = true;
+        if (!host_) origin_ = Loc::Device;
+    }
+}
+
+template <typename T>
+void MatrixStorage<T>::copy_instance(Loc to) {
+    T* src = to == Loc::Host ? dev_ : host_;
+    T* dst = to == Loc::Host ? host_ : dev_;
+    int64_t sld = to == Loc::Host ? dev_ld_ : host_ld_;
+    int64_t dld = to == Loc::Host ? host_ld_ : dev_ld_;
+    if (mloc == 0 || nloc == 0) return;
+    hipStream_t s = device::queue(0);
+    device::memcpy2d_async(dst, dld * sizeof(T), src, sld * sizeof(T), mloc * sizeof(T), nloc, s);
+    slate_hip_call(hipStreamSynchronize(s));
+}
+
+template <typename T>
+T* MatrixStorage<T>::get(Loc loc, bool for_write) {
+    allocate(loc);
+    MOSI_State& mine  = loc == Loc::Host ? host_state_ : dev_state_;
+    MOSI_State& other = loc == Loc::Host ? dev_state_ : host_state_;
+    if (mine == Invalid) {
+        if (other != Invalid && has(loc == Loc::Host ? Loc::Device : Loc::Host)) {
+            copy_instance(loc);
+            if (other == Modified) other = Shared;
+        }
+        mine = Shared;
+    }
+    if (for_write) {
+        mine = Modified;
+        if (has(loc == Loc::Host ? Loc::Device : Loc::Host)) other = Invalid;
+    }
+    return raw(loc);
+}
+
+template <typename T>
+void MatrixStorage<T>::modified(Loc loc) {
+    allocate(loc);
+    (loc == Loc::Host ? host_state_ : dev_state_) = Modified;
+    Loc o = loc == Loc::Host ? Loc::Device : Loc::Host;
+    if (has(o)) (o == Loc::Host ? host_state_ : dev_state_) = Invalid;
+}
+
+template <typename T>
+void MatrixStorage<T>::update_origin() {
+    if (state(origin_) == Invalid) get(origin_, false);
+}
+
+template <typename T>
+void MatrixStorage<T>::release_workspace() {
+    Loc o = origin_ == Loc::Host ? Loc::Device : Loc::Host;
+    if (!has(o)) return;
+    update_origin();
+    if (o == Loc::Device && dev_owned_) { device::free(dev_); dev_ = nullptr; dev_state_ = Invalid; dev_owned_ = false; }
+    if (o == Loc::Host && host_owned_)  { std::free(host_); host_ = nullptr; host_state_ = Invalid; host_owned_ = false; }
+}
+
+//------------------------------------------------------------------------------
+template <typename T>
+BaseMatrix<T> BaseMatrix<T>::sub(int64_t i1, int64_t i2, int64_t j1, int64_t j2) const {
+    // logical -> storage tile ranges
+    int64_t si1, si2, sj1, sj2;
+    if (op_ == Op::NoTrans) { si1 = i1; si2 = i2; sj1 = j1; sj2 = j2; }
+    else { si1 = j1; si2 = j2; sj1 = i1; sj2 = i2; }
+    BaseMatrix r = *this;
+    // empty ranges allowed (i2 = i1 - 1)
+    slate_error_if_msg(si1 < 0 || sj1 < 0 || si2 >= std::max<int64_t>(smt(), si1) ||
+                       sj2 >= std::max<int64_t>(snt(), sj1), "sub: tile index out of range");
+    if (si2 < si1) { r.r0_ = si1 < smt() ? srow_start(si1) : r0_ + m_; r.m_ = 0; }
+    else { r.r0_ = srow_start(si1); r.m_ = srow_start(si2) + srow_size(si2) - r.r0_; }
+    if (sj2 < sj1) { r.c0_ = sj1 < snt() ? scol_start(sj1) : c0_ + n_; r.n_ = 0; }
+    else { r.c0_ = scol_start(sj1); r.n_ = scol_start(sj2) + scol_size(sj2) - r.c0_; }
+    // a sub-matrix that is off the diagonal is general
+    if (!(si1 == sj1 && si2 == sj2)) {
+        if (kind_ == MatrixKind::Symmetric || kind_ == MatrixKind::Hermitian ||
+            kind_ == MatrixKind::Triangular || kind_ == MatrixKind::Trapezoid) {
+            // keep uplo for diagonal-touching views; callers re-wrap as needed
+        }
+    }
+    return r;
+}
+
+template <typename T>
+BaseMatrix<T> BaseMatrix<T>::slice(int64_t r1, int64_t r2, int64_t c1, int64_t c2) const {
+    int64_t sr1, sr2, sc1, sc2;
+    if (op_ == Op::NoTrans) { sr1 = r1; sr2 = r2; sc1 = c1; sc2 = c2; }
+    else { sr1 = c1; sr2 = c2; sc1 = r1; sc2 = r2; }
+    slate_error_if_msg(sr1 < 0 || sc1 < 0 || sr2 >= m_ || sc2 >= n_ || sr2 < sr1 - 1 || sc2 < sc1 - 1,
+                       "slice: index out of range");
+    BaseMatrix r = *this;
+    r.r0_ = r0_ + sr1; r.m_ = sr2 - sr1 + 1;
+    r.c0_ = c0_ + sc1; r.n_ = sc2 - sc1 + 1;
+    return r;
+}
+
+template <typename T>
+int64_t BaseMatrix<T>::lrow_begin() const {
+    return g2l_ceil(r0_, storage_->mb, storage_->rrel(), storage_->grid->p());
+}
+template <typename T>
+int64_t BaseMatrix<T>::lrow_end() const {
+    return g2l_ceil(r0_ + m_, storage_->mb, storage_->rrel(), storage_->grid->p());
+}
+template <typename T>
+int64_t BaseMatrix<T>::lcol_begin() const {
+    return g2l_ceil(c0_, storage_->nb, storage_->crel(), storage_->grid->q());
+}
+template <typename T>
+int64_t BaseMatrix<T>::lcol_end() const {
+    return g2l_ceil(c0_ + n_, storage_->nb, storage_->crel(), storage_->grid->q());
+}
+
+template <typename T>
+LocalBlock<T> BaseMatrix<T>::local_raw(Loc loc) const {
+    LocalBlock<T> b;
+    int64_t rb = lrow_begin(), re = lrow_end(), cb = lcol_begin(), ce = lcol_end();
+    b.m = re - rb; b.n = ce - cb;
+    b.ld = std::max<int64_t>(1, storage_->ld(loc));
+    T* base = storage_->raw(loc);
+    b.ptr = base ? base + rb + cb * b.ld : nullptr;
+    return b;
+}
+
+template <typename T>
+LocalBlock<T> BaseMatrix<T>::local(Loc loc, bool for_write) const {
+    storage_->get(loc, for_write);
+    return local_raw(loc);
+}
+
+template <typename T>
+Tile<T> BaseMatrix<T>::tile(int64_t i, int64_t j, Loc loc) const {
+    slate_error_if_msg(!tileIsLocal(i, j), "tile: not local");
+    int64_t si, sj; to_storage(i, j, si, sj);
+    auto& g = *storage_->grid;
+    int64_t gr = srow_start(si), gc = scol_start(sj);
+    int64_t lr = g2l(gr, storage_->mb, g.p()), lc = g2l(gc, storage_->nb, g.q());
+    Tile<T> t;
+    int64_t ld = storage_->ld(loc);
+    T* base = storage_->raw(loc);
+    slate_error_if_msg(!base, "tile: storage not allocated at location");
+    t.data = base + lr + lc * ld;
+    t.mb = srow_size(si); t.nb = scol_size(sj); t.stride = ld;
+    t.op = op_; t.uplo = uplo_physical();
+    t.device = loc == Loc::Host ? HostNum : 0;
+    return t;
+}
+
+template <typename T>
+T& BaseMatrix<T>::elem(int64_t i, int64_t j) {
+    int64_t si = op_ == Op::NoTrans ? i : j, sj = op_ == Op::NoTrans ? j : i;
+    int64_t gr = r0_ + si, gc = c0_ + sj;
+    auto& g = *storage_->grid;
+    slate_error_if_msg(storage_->row_owner(gr / storage_->mb) != g.myrow() ||
+                       storage_->col_owner(gc / storage_->nb) != g.mycol(), "elem: not local");
+    T* base = storage_->get(Loc::Host, false);
+    return base[g2l(gr, storage_->mb, g.p()) + g2l(gc, storage_->nb, g.q()) * storage_->ld(Loc::Host)];
+}
+
+//------------------------------------------------------------------------------
+template <typename T>
+Matrix<T> Matrix<T>::fromLAPACK(int64_t m, int64_t n, T* A, int64_t lda, int64_t nb, Loc loc) {
+    Matrix<T> M(m, n, nb, nb, Grid::self());
+    M.storage_->attach(A, lda, loc);
+    return M;
+}
+
+template <typename T>
+Matrix<T> Matrix<T>::fromScaLAPACK(int64_t m, int64_t n, T* A, int64_t lld, int64_t mb, int64_t nb,
+                                   GridPtr grid, Loc loc) {
+    Matrix<T> M(m, n, mb, nb, grid ? grid : default_grid());
+    M.storage_->attach(A, lld, loc);
+    return M;
+}
+
+template <typename T>
+Matrix<T> Matrix<T>::emptyLike(int64_t mb, int64_t nb, Op deepOp) const {
+    // New storage over the same logical tile grid as this view, with the
+    // first tile on the same rank (so tiles (i, j) of both are co-located).
+    slate_error_if_msg(!this->aligned(), "emptyLike: view must start on a tile boundary");
+    int64_t mt = this->mt(), nt = this->nt();
+    GridPtr g = this->storage_->grid;
+    int64_t tmb = this->op_ == Op::NoTrans ? this->storage_->mb : this->storage_->nb;
+    int64_t tnb = this->op_ == Op::NoTrans ? this->storage_->nb : this->storage_->mb;
+    int64_t m_l = this->m(), n_l = this->n();
+    if (this->op_ != Op::NoTrans) g = g->transposed();
+    int r00 = mt > 0 && nt > 0 ? this->tileRank(0, 0) : this->mpiRank();
+    int rsrc = g->row_of(r00), csrc = g->col_of(r00);
+    if (mb > 0) { tmb = mb; m_l = mt * mb; }
+    if (nb > 0) { tnb = nb; n_l = nt * nb; }
+    if (deepOp != Op::NoTrans) {
+        std::swap(m_l, n_l); std::swap(tmb, tnb); std::swap(rsrc, csrc);
+        g = g->transposed();
+    }
+    return Matrix<T>(m_l, n_l, tmb, tnb, g, rsrc, csrc);
+}
+
+//------------------------------------------------------------------------------
+template class MatrixStorage<float>;
+template class MatrixStorage<double>;
+template class MatrixStorage<std::complex<float>>;
+template class MatrixStorage<std::complex<double>>;
+template class BaseMatrix<float>;
+template class BaseMatrix<double>;
+template class BaseMatrix<std::complex<float>>;
+template class BaseMatrix<std::complex<double>>;
+template class Matrix<float>;
+template class Matrix<double>;
+template class Matrix<std::complex<float>>;
+template class Matrix<std::complex<double>>;
+
+}  // namespace slate

@@ -1,0 +1,227 @@
+// Distributed Cholesky factorization A = L L^H (reference src/potrf.cc:22-303).
+//
+// Per block column k (right-looking, lookahead `la`):
+//   panel (queue 1):   potrf of A(k,k) on its owner; diag tile broadcast down
+//                      the process column (comm queue); trsm of the local
+//                      rows of A(k+1:,k) against L(k,k)^H.
+//   bcast (comm queue): the local rows of L(k+1:,k) along the process row
+//                      (one RCCL broadcast of a contiguous buffer), then the
+//                      tiles each process column needs as the "transposed"
+//                      operand, exchanged by one all-gather in the column
+//                      communicator.
+//   update:            lookahead columns k+1..k+la on their own queues,
+//                      everything else as ONE trailing update on queue 0.
+//                      On a 1x1 grid the trailing update is a single
+//                      triangular-output MFMA GEMM (herk) over the whole
+//                      trailing matrix.
+// The reference instead issues one batched herk/gemm per tile group per
+// step and syncs its queues after each op (internal_herk.cc:491-530).
+#include "internal.hh"
+
+#include <algorithm>
+#include <numeric>
+
+namespace slate {
+
+namespace {
+
+template <typename T>
+int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
+    using namespace internal;
+    auto& g = *A.grid();
+    const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    const int64_t nt = A.nt();
+    if (nt == 0) return 0;
+    slate_error_if_msg(A.mb() != A.nb(), "potrf requires square tiles");
+    slate_error_if_msg(!A.aligned(), "potrf requires a tile-aligned matrix");
+    const int64_t nb = A.nb();
+
+    LocalBlock<T> L = A.local(loc, true);
+    T* a = L.ptr;
+    const int64_t lda = L.ld, mloc = L.m;
+
+    Sched S(target);
+    const int R = int(std::max<int64_t>(2, la + 2));   // workspace ring depth
+    // panel row-broadcast buffers and transposed-operand buffers
+    std::vector<Work<T>> W(R), Wt(R), Dk(R), Ws(R);
+    const int64_t lcm = std::lcm(int64_t(p), int64_t(q));
+    const int64_t maxcnt = ceildiv(nt, lcm) + 1;
+    for (int r = 0; r < R; ++r) {
+        if (q > 1) W[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+        if (p > 1) {
+            Wt[r].resize(target, size_t(p) * maxcnt * nb * nb);
+            Ws[r].resize(target, size_t(maxcnt) * nb * nb);
+            Dk[r].resize(target, size_t(nb) * nb);
+        }
+    }
+    Work<int> dinfo(target, 1);
+    {
+        lb::Ctx c0 = S.ctx(1);
+        if (c0.dev()) device::memset_async(dinfo.data(), 0, sizeof(int), c0.stream);
+        else dinfo.data()[0] = 0;
+    }
+    const int64_t lookahead_queues = device::kNumQueues - 3;  // queues 2..6
+
+    for (int64_t k = 0; k < nt; ++k) {
+        const int64_t kb = A.tileNb(k);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int64_t lr_k = lrow_of(A, k), lr_k1 = lrow_of(A, k + 1);
+        const int64_t mrows = mloc - lr_k1;
+        const int slot = int(k % R);
+        const int64_t kk = grow_of(A, k);
+        const bool in_col = (mycol == qk);
+        const int64_t lc_k = in_col ? lcol_of(A, k) : 0;
+        T* akk = a + lr_k + lc_k * lda;          // diag tile (if mine)
+        T* apan = a + lr_k1 + lc_k * lda;        // my rows below the diagonal
+
+        const int64_t tDiag = Sched::tok(5, slot), tBc = Sched::bcast(slot);
+
+        // ---- panel: potrf(A(k,k))
+        if (in_col && myrow == pk) {
+            S.task(1, {}, {Sched::col(k)}, [&, akk, kb, kk](lb::Ctx const& c) {
+                trace::Block tb("potrf_diag");
+                lb::potrf(c, Uplo::Lower, kb, akk, lda, dinfo.data(), kk);
+            });
+        }
+        // ---- diag tile down the process column
+        T* Lkk = akk;
+        int64_t ldL = lda;
+        if (in_col && p > 1) {
+            T* D = Dk[slot].data();
+            S.task(device::kCommQueue, {Sched::col(k)}, {tDiag}, [&, D, akk, kb, pk](lb::Ctx const& c) {
+                trace::Block tb("bcast_diag");
+                if (myrow == pk) pack(c, kb, kb, akk, lda, D);
+                bcast(g.col(), D, size_t(kb * kb), pk, c);
+            });
+            Lkk = D; ldL = kb;
+        }
+        // ---- panel trsm: A(k+1:, k) = A(k+1:, k) L(k,k)^{-H}
+        if (in_col && mrows > 0) {
+            S.task(1, {tDiag}, {Sched::col(k)}, [&, Lkk, ldL, apan, mrows, kb](lb::Ctx const& c) {
+                trace::Block tb("potrf_trsm");
+                lb::trsm(c, Side::Right, Uplo::Lower, Op::ConjTrans, Diag::NonUnit, mrows, kb, T(1),
+                         Lkk, ldL, apan, lda);
+            });
+        }
+        if (k == nt - 1) break;
+
+        // ---- broadcast the panel along process rows, transposed tiles along columns
+        T* Wk = (q > 1) ? W[slot].data() : apan;
+        const int64_t ldW = (q > 1) ? std::max<int64_t>(mrows, 1) : lda;
+        // tiles J > k that my process column needs, grouped by owning process row
+        std::vector<std::vector<int64_t>> lists(p);
+        for (int64_t J = k + 1; J < nt; ++J)
+            if (A.scol_owner(J) == mycol) lists[A.srow_owner(J)].push_back(J);
+        S.task(device::kCommQueue, {Sched::col(k)}, {tBc}, [&, Wk, apan, mrows, kb, qk, slot, lists, lr_k1, ldW](lb::Ctx const& c) {
+            trace::Block tb("bcast_panel");
+            if (q > 1) {
+                if (mycol == qk) pack(c, mrows, kb, apan, lda, Wk);
+                bcast(g.row(), Wk, size_t(mrows * kb), qk, c);
+            }
+            if (p > 1) {
+                // pack my tiles (rows of Wk) for the column all-gather
+                T* Sb = Ws[slot].data();
+                int64_t cnt = 0;
+                for (int64_t J : lists[myrow]) {
+                    int64_t off = lrow_of(A, J) - lr_k1;
+                    int64_t jb = A.tileMb(J);
+                    lb::copy2d(c, jb, kb, Wk + off, ldW, Sb + cnt * nb * nb, nb);
+                    ++cnt;
+                }
+                g.col().allgather(Sb, Wt[slot].data(), size_t(maxcnt * nb * nb), scalar_type<T>(), c.loc(), c.stream);
+            }
+        });
+
+        // ---- trailing updates
+        auto update = [&, Wk, ldW, kb, slot, lists, lr_k1](lb::Ctx const& c, int64_t j0, int64_t j1) {
+            trace::Block tb("potrf_update");
+            // fast path: 1x1 grid, contiguous range -> one herk over [j0, j1) x [j0, ...)
+            if (p == 1 && q == 1) {
+                int64_t r0 = lrow_of(A, j0), c0 = lcol_of(A, j0), c1 = lcol_of(A, j1);
+                int64_t ncols = c1 - c0, nrows = mloc - r0;
+                T const* Wr = Wk + (r0 - lr_k1);
+                // diagonal square block: herk; rows below: gemm
+                lb::herk(c, Uplo::Lower, Op::NoTrans, ncols, kb, real_type<T>(-1), Wr, ldW, real_type<T>(1),
+                         a + r0 + c0 * lda, lda);
+                if (nrows > ncols)
+                    lb::gemm(c, Op::NoTrans, Op::ConjTrans, nrows - ncols, ncols, kb, T(-1), Wr + ncols, ldW,
+                             Wr, ldW, T(1), a + r0 + ncols + c0 * lda, lda);
+                return;
+            }
+            for (int64_t J = j0; J < j1; ++J) {
+                if (A.scol_owner(J) != mycol) continue;
+                int64_t jb = A.tileNb(J);
+                int64_t rJ = lrow_of(A, J), cJ = lcol_of(A, J);
+                int64_t nrows = mloc - rJ;
+                if (nrows <= 0) continue;
+                // transposed operand L(J, k): jb x kb
+                T const* Bt; int64_t ldB;
+                if (p == 1) { Bt = Wk + (lrow_of(A, J) - lr_k1); ldB = ldW; }
+                else {
+                    int r = A.srow_owner(J);
+                    auto const& lst = lists[r];
+                    int64_t idx = std::find(lst.begin(), lst.end(), J) - lst.begin();
+                    Bt = Wt[slot].data() + (int64_t(r) * maxcnt + idx) * nb * nb; ldB = nb;
+                }
+                T const* Ar = Wk + (rJ - lr_k1);
+                T* Cc = a + rJ + cJ * lda;
+                if (A.srow_owner(J) == myrow) {
+                    // diagonal tile is local: herk on it, gemm below
+                    lb::gemm_tri(c, Uplo::Lower, Op::NoTrans, Op::ConjTrans, jb, kb, T(-1), Ar, ldW, Bt, ldB, T(1), Cc, lda);
+                    if (nrows > jb)
+                        lb::gemm(c, Op::NoTrans, Op::ConjTrans, nrows - jb, jb, kb, T(-1), Ar + jb, ldW, Bt, ldB,
+                                 T(1), Cc + jb, lda);
+                } else {
+                    lb::gemm(c, Op::NoTrans, Op::ConjTrans, nrows, jb, kb, T(-1), Ar, ldW, Bt, ldB, T(1), Cc, lda);
+                }
+            }
+        };
+        int64_t jla_end = std::min(nt, k + 1 + la);
+        for (int64_t j = k + 1; j < jla_end; ++j) {
+            int qi = 2 + int((j - k - 1) % lookahead_queues);
+            S.task(qi, {tBc}, {Sched::col(j)}, [&, update, j](lb::Ctx const& c) { update(c, j, j + 1); });
+        }
+        if (jla_end < nt) {
+            std::vector<int64_t> outs;
+            for (int64_t j = jla_end; j < nt; ++j) outs.push_back(Sched::col(j));
+            S.task(0, {tBc}, outs, [&, update, jla_end](lb::Ctx const& c) { update(c, jla_end, nt); });
+        }
+    }
+    S.wait_all();
+    int64_t info = fetch_info(target, dinfo.data());
+    return reduce_info(info, g.world());
+}
+
+}  // namespace
+
+template <typename T>
+int64_t potrf(HermitianMatrix<T>& A_in, Options const& opts) {
+    trace::Block tb("potrf");
+    Target target = internal::resolve_target(opts);
+    int64_t la = get_option<int64_t>(opts, Option::Lookahead, 1);
+    BaseMatrix<T> A = A_in;
+    if (A.op() != Op::NoTrans) A = A.transpose_view(A.op() == Op::ConjTrans);  // physical view
+    int64_t info;
+    if (A_in.uplo_physical() == Uplo::Lower) {
+        info = potrf_lower(A, target, la);
+    } else {
+        // Upper: factor the conjugate transpose on the transposed grid
+        // (local transposes only), then transpose back.
+        Matrix<T> Ah = Matrix<T>(A).emptyLike(0, 0, Op::ConjTrans);
+        Ah.insertLocalTiles(target);
+        slate::copy<T, T>(conj_transpose(Matrix<T>(A)), Ah, opts);
+        info = potrf_lower(BaseMatrix<T>(Ah), target, la);
+        Matrix<T> Ad(A);
+        slate::copy<T, T>(conj_transpose(Ah), Ad, opts);
+    }
+    A.storage()->update_origin();
+    return info;
+}
+
+template int64_t potrf<float>(HermitianMatrix<float>&, Options const&);
+template int64_t potrf<double>(HermitianMatrix<double>&, Options const&);
+template int64_t potrf<std::complex<float>>(HermitianMatrix<std::complex<float>>&, Options const&);
+template int64_t potrf<std::complex<double>>(HermitianMatrix<std::complex<double>>&, Options const&);
+
+}  // namespace slate

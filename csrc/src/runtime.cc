@@ -1,0 +1,56 @@
+#include "slate_amd/runtime.hh"
+#include "slate_amd/trace.hh"
+
+namespace slate {
+
+Sched::Sched(Target target) : target_(target) {}
+
+Sched::~Sched() {
+    try { wait_all(); } catch (...) {}
+    for (auto e : events_) device::event_put(e);
+}
+
+lb::Ctx Sched::ctx(int queue) const {
+    if (target_ != Target::Devices) return lb::Ctx{target_, nullptr};
+    return lb::Ctx{Target::Devices, device::queue(queue)};
+}
+
+void Sched::task(int queue, std::initializer_list<int64_t> in, std::initializer_list<int64_t> out, Fn fn) {
+    task(queue, std::vector<int64_t>(in), std::vector<int64_t>(out), std::move(fn));
+}
+
+void Sched::task(int queue, std::vector<int64_t> const& in, std::vector<int64_t> const& out, Fn fn) {
+    if (target_ != Target::Devices) {
+        fn(ctx(queue));
+        return;
+    }
+    hipStream_t s = device::queue(queue);
+    used_[queue] = true;
+    // RAW: wait for the last writer of every input and output token;
+    // WAR: outputs also wait for all readers since that write.
+    auto wait = [&](hipEvent_t e) { if (e) slate_hip_call(hipStreamWaitEvent(s, e, 0)); };
+    for (int64_t t : in) wait(tokens_[t].writer);
+    for (int64_t t : out) {
+        auto& st = tokens_[t];
+        wait(st.writer);
+        for (auto e : st.readers) wait(e);
+    }
+    fn(ctx(queue));
+    hipEvent_t e = device::event_get();
+    events_.push_back(e);
+    slate_hip_call(hipEventRecord(e, s));
+    for (int64_t t : in) tokens_[t].readers.push_back(e);
+    for (int64_t t : out) {
+        auto& st = tokens_[t];
+        st.writer = e;
+        st.readers.clear();
+    }
+}
+
+void Sched::wait_all() {
+    if (target_ != Target::Devices) return;
+    for (int q = 0; q < device::kNumQueues; ++q)
+        if (used_[q]) slate_hip_call(hipStreamSynchronize(device::queue(q)));
+}
+
+}  // namespace slate

@@ -1,0 +1,128 @@
+// Standalone GEMM check + timing harness (development tool, not the product).
+// Usage: gemm_bench [m n k] ; checks every transpose combination on odd
+// shapes against a naive device reference, then times large square fp64/fp32.
+#include "../kernels/device_common.hh"
+#include "../kernels/kernels.hh"
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+#include <cmath>
+#include <chrono>
+
+using namespace slate_amd::dev;
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { \
+    printf("HIP error %s at %s:%d\n", hipGetErrorString(e), __FILE__, __LINE__); exit(1);} } while (0)
+
+template <typename T>
+__global__ void ref_gemm(char ta, char tb, int64_t m, int64_t n, int64_t k, T alpha,
+                         const T* A, int64_t lda, const T* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t j = blockIdx.y;
+    if (i >= m || j >= n) return;
+    double s = 0;
+    for (int64_t l = 0; l < k; ++l) {
+        double a = (ta == 'N') ? A[i + l * lda] : A[l + i * lda];
+        double b = (tb == 'N') ? B[l + j * ldb] : B[j + l * ldb];
+        s += a * b;
+    }
+    C[i + j * ldc] = T(alpha * s + (double)beta * (double)C[i + j * ldc]);
+}
+
+__global__ void fill(double* p, int64_t n, uint64_t seed) {
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) {
+        uint64_t x = (i + 1) * 0x9E3779B97F4A7C15ull ^ seed;
+        x ^= x >> 33; x *= 0xff51afd7ed558ccdull; x ^= x >> 33; x *= 0xc4ceb9fe1a85ec53ull; x ^= x >> 33;
+        p[i] = (double)(x >> 11) / (double)(1ull << 53) * 2.0 - 1.0;
+    }
+}
+__global__ void tofloat(const double* s, float* d, int64_t n) {
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    if (i < n) d[i] = (float)s[i];
+}
+
+template <typename T>
+double check(char ta, char tb, int64_t m, int64_t n, int64_t k, int64_t pad) {
+    int64_t am = ta == 'N' ? m : k, an = ta == 'N' ? k : m;
+    int64_t bm = tb == 'N' ? k : n, bn = tb == 'N' ? n : k;
+    int64_t lda = am + pad, ldb = bm + pad, ldc = m + pad;
+    double *dA, *dB, *dC;
+    CHECK(hipMalloc(&dA, lda * an * 8)); CHECK(hipMalloc(&dB, ldb * bn * 8)); CHECK(hipMalloc(&dC, ldc * n * 8));
+    fill<<<(lda * an + 255) / 256, 256>>>(dA, lda * an, 1);
+    fill<<<(ldb * bn + 255) / 256, 256>>>(dB, ldb * bn, 2);
+    fill<<<(ldc * n + 255) / 256, 256>>>(dC, ldc * n, 3);
+    T *A, *B, *C, *C2;
+    CHECK(hipMalloc(&A, lda * an * sizeof(T))); CHECK(hipMalloc(&B, ldb * bn * sizeof(T)));
+    CHECK(hipMalloc(&C, ldc * n * sizeof(T))); CHECK(hipMalloc(&C2, ldc * n * sizeof(T)));
+    if constexpr (sizeof(T) == 8) {
+        CHECK(hipMemcpy(A, dA, lda * an * 8, hipMemcpyDeviceToDevice));
+        CHECK(hipMemcpy(B, dB, ldb * bn * 8, hipMemcpyDeviceToDevice));
+        CHECK(hipMemcpy(C, dC, ldc * n * 8, hipMemcpyDeviceToDevice));
+    } else {
+        tofloat<<<(lda * an + 255) / 256, 256>>>(dA, (float*)A, lda * an);
+        tofloat<<<(ldb * bn + 255) / 256, 256>>>(dB, (float*)B, ldb * bn);
+        tofloat<<<(ldc * n + 255) / 256, 256>>>(dC, (float*)C, ldc * n);
+    }
+    CHECK(hipMemcpy(C2, C, ldc * n * sizeof(T), hipMemcpyDeviceToDevice));
+    T alpha = T(0.7), beta = T(-0.3);
+    gemm_real<T>(ta, tb, m, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, 0);
+    ref_gemm<T><<<dim3((m + 127) / 128, n), 128>>>(ta, tb, m, n, k, alpha, A, lda, B, ldb, beta, C2, ldc);
+    CHECK(hipDeviceSynchronize());
+    std::vector<T> h1(ldc * n), h2(ldc * n);
+    CHECK(hipMemcpy(h1.data(), C, ldc * n * sizeof(T), hipMemcpyDeviceToHost));
+    CHECK(hipMemcpy(h2.data(), C2, ldc * n * sizeof(T), hipMemcpyDeviceToHost));
+    double err = 0;
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < m; ++i)
+            err = fmax(err, fabs((double)h1[i + j * ldc] - (double)h2[i + j * ldc]));
+    hipFree(dA); hipFree(dB); hipFree(dC); hipFree(A); hipFree(B); hipFree(C); hipFree(C2);
+    return err / (double)k;
+}
+
+template <typename T>
+void timeit(char ta, char tb, int64_t n, int64_t k, int reps) {
+    T *A, *B, *C;
+    CHECK(hipMalloc(&A, n * k * sizeof(T))); CHECK(hipMalloc(&B, n * k * sizeof(T))); CHECK(hipMalloc(&C, n * n * sizeof(T)));
+    double* tmp; CHECK(hipMalloc(&tmp, n * k * 8));
+    fill<<<(n * k + 255) / 256, 256>>>(tmp, n * k, 5);
+    if constexpr (sizeof(T) == 8) { CHECK(hipMemcpy(A, tmp, n * k * 8, hipMemcpyDeviceToDevice)); CHECK(hipMemcpy(B, tmp, n * k * 8, hipMemcpyDeviceToDevice)); }
+    else { tofloat<<<(n * k + 255) / 256, 256>>>(tmp, (float*)A, n * k); tofloat<<<(n * k + 255) / 256, 256>>>(tmp, (float*)B, n * k); }
+    CHECK(hipMemset(C, 0, n * n * sizeof(T)));
+    int64_t lda = ta == 'N' ? n : k, ldb = tb == 'N' ? k : n;
+    gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, n, 0, 1, 0);
+    CHECK(hipDeviceSynchronize());
+    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    hipEventRecord(e0);
+    for (int r = 0; r < reps; ++r)
+        gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, n, 0, 1, 0);
+    hipEventRecord(e1); hipEventSynchronize(e1);
+    float ms; hipEventElapsedTime(&ms, e0, e1);
+    double tf = 2.0 * n * n * k * reps / (ms * 1e-3) / 1e12;
+    printf("%s %c%c n=%ld k=%ld : %.3f ms/call  %.2f TFLOP/s\n", sizeof(T) == 8 ? "dgemm" : "sgemm", ta, tb, n, k, ms / reps, tf);
+    hipFree(A); hipFree(B); hipFree(C); hipFree(tmp);
+}
+
+int main(int argc, char** argv) {
+    const char ops[2] = {'N', 'T'};
+    int64_t shapes[][3] = {{1, 1, 1}, {17, 33, 5}, {128, 128, 16}, {129, 131, 67}, {300, 257, 513}, {1000, 999, 77}};
+    bool ok = true;
+    for (auto& s : shapes)
+        for (char ta : ops) for (char tb : ops) for (int pad = 0; pad < 2; ++pad) {
+            double e = check<double>(ta, tb, s[0], s[1], s[2], pad ? 3 : 0);
+            double ef = check<float>(ta, tb, s[0], s[1], s[2], pad ? 3 : 0);
+            bool good = e < 1e-14 && ef < 1e-5;
+            ok &= good;
+            if (!good || s[0] == 300)
+                printf("check %c%c m=%ld n=%ld k=%ld pad=%d: d err/k=%.3e  s err/k=%.3e %s\n", ta, tb, s[0], s[1], s[2], pad, e, ef, good ? "ok" : "FAIL");
+        }
+    printf("correctness: %s\n", ok ? "PASS" : "FAIL");
+    int64_t N = argc > 1 ? atoll(argv[1]) : 8192;
+    timeit<double>('N', 'T', N, 512, 5);
+    timeit<double>('N', 'N', N, 512, 5);
+    timeit<double>('N', 'N', N, N, 2);
+    timeit<double>('T', 'N', N, N, 2);
+    timeit<float>('N', 'N', N, N, 2);
+    timeit<float>('N', 'T', N, 512, 5);
+    return ok ? 0 : 1;
+}

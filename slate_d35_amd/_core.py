@@ -1,0 +1,160 @@
+"""Core Python layer: dtype dispatch and matrix helpers over the native
+library (``_slate``).  Mirrors the reference's C++ API surface
+(include/slate/slate.hh) with Pythonic wrappers; all heavy lifting is in
+C++/HIP.
+"""
+from __future__ import annotations
+
+import os
+import numpy as np
+
+from . import _slate
+
+Target = _slate.Target
+Op = _slate.Op
+Uplo = _slate.Uplo
+Diag = _slate.Diag
+Side = _slate.Side
+Norm = _slate.Norm
+GridOrder = _slate.GridOrder
+Equed = _slate.Equed
+Grid = _slate.Grid
+
+_SUFFIX = {
+    np.dtype(np.float32): "s",
+    np.dtype(np.float64): "d",
+    np.dtype(np.complex64): "c",
+    np.dtype(np.complex128): "z",
+}
+_DTYPE = {v: k for k, v in _SUFFIX.items()}
+
+
+def suffix_of(obj) -> str:
+    """Precision suffix ('s','d','c','z') of a native matrix object or dtype."""
+    if isinstance(obj, str):
+        return obj
+    try:
+        return _SUFFIX[np.dtype(obj)]
+    except TypeError:
+        pass
+    name = type(obj).__name__
+    return name.rsplit("_", 1)[-1]
+
+
+def dtype_of(obj) -> np.dtype:
+    return _DTYPE[suffix_of(obj)]
+
+
+def native(name: str, obj):
+    """The native function `name_<suffix>` for a matrix object."""
+    return getattr(_slate, f"{name}_{suffix_of(obj)}")
+
+
+def _cls(kind: str, dtype):
+    return getattr(_slate, f"{kind}_{suffix_of(dtype)}")
+
+
+def target_of(t) -> Target:
+    if t is None:
+        return Target.Devices if (os.environ.get("SLATE_TARGET", "").lower() in ("d", "devices")) else Target.HostTask
+    if isinstance(t, Target):
+        return t
+    return {"h": Target.Host, "host": Target.Host, "t": Target.HostTask, "task": Target.HostTask,
+            "n": Target.HostNest, "b": Target.HostBatch, "d": Target.Devices,
+            "dev": Target.Devices, "devices": Target.Devices}[str(t).lower()]
+
+
+def opts(target=None, **kw) -> dict:
+    o = dict(kw)
+    if target is not None:
+        o["target"] = target_of(target)
+    return o
+
+
+# ---------------------------------------------------------------- matrices
+def Matrix(m, n, nb=256, dtype=np.float64, grid=None, mb=None):
+    """Distributed m x n matrix with mb x nb tiles on `grid` (no storage yet)."""
+    return _cls("Matrix", dtype)(int(m), int(n), int(mb or nb), int(nb), grid)
+
+
+def HermitianMatrix(uplo, A):
+    return _cls("HermitianMatrix", A)(uplo, A)
+
+
+def SymmetricMatrix(uplo, A):
+    return _cls("SymmetricMatrix", A)(uplo, A)
+
+
+def TriangularMatrix(uplo, diag, A):
+    return _cls("TriangularMatrix", A)(uplo, diag, A)
+
+
+def TrapezoidMatrix(uplo, diag, A):
+    return _cls("TrapezoidMatrix", A)(uplo, diag, A)
+
+
+def BandMatrix(kl, ku, A):
+    return _cls("BandMatrix", A)(kl, ku, A)
+
+
+def TriangularBandMatrix(uplo, diag, kd, A):
+    return _cls("TriangularBandMatrix", A)(uplo, diag, kd, A)
+
+
+def HermitianBandMatrix(uplo, kd, A):
+    return _cls("HermitianBandMatrix", A)(uplo, kd, A)
+
+
+def general(A):
+    """General Matrix view of any matrix object (drops uplo/diag meta)."""
+    return _cls("Matrix", A)(A)
+
+
+def from_numpy(full: np.ndarray, nb=256, grid=None, target=None, dtype=None, mb=None):
+    """Distribute a full (replicated) numpy array: each rank keeps its local
+    tiles.  Storage is allocated at the target's location."""
+    full = np.asarray(full)
+    if dtype is None:
+        dtype = full.dtype if full.dtype in _SUFFIX else np.float64
+    full = full.astype(dtype, copy=False)
+    if full.ndim == 1:
+        full = full.reshape(-1, 1)
+    m, n = full.shape
+    A = Matrix(m, n, nb, dtype, grid, mb=mb)
+    A.insertLocalTiles(Target.Host)
+    rows = A.local_row_indices()
+    cols = A.local_col_indices()
+    if len(rows) and len(cols):
+        A.set_local(np.asfortranarray(full[np.ix_(rows, cols)]))
+    if target_of(target) == Target.Devices:
+        A.insertLocalTiles(Target.Devices)
+    return A
+
+
+def to_numpy(A) -> np.ndarray:
+    """Gather a distributed matrix (logical view) to a full numpy array on every rank."""
+    return A.gather()
+
+
+def empty_like(A, target=None):
+    B = _cls("Matrix", A)(A).emptyLike()
+    B.insertLocalTiles(target_of(target) if target is not None else Target.Host)
+    return B
+
+
+def local_tensor(A, device=True):
+    """Zero-copy torch view of this rank's local block (column-major)."""
+    import torch
+    return torch.utils.dlpack.from_dlpack(A.local_dlpack(device))
+
+
+def transpose(A):
+    return A.transpose()
+
+
+def conj_transpose(A):
+    return A.conj_transpose()
+
+
+def version() -> str:
+    return _slate.version()

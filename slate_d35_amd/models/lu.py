@@ -1,0 +1,125 @@
+"""LU family (reference src/getrf*.cc, getrs*.cc, gesv*.cc, getri*.cc,
+gecondest.cc, trtri.cc, trtrm.cc, trcondest.cc)."""
+from ._wrap import call
+
+__all__ = ["getrf", "getrf_nopiv", "getrf_tntpiv", "getrs", "getrs_nopiv", "gesv", "gesv_nopiv",
+           "gesv_mixed", "gesv_mixed_gmres", "gesv_rbt", "getri", "gecondest", "trtri", "trtrm",
+           "trcondest", "lu_factor", "lu_solve", "lu_solve_using_factor", "lu_inverse_using_factor",
+           "lu_factor_nopiv", "lu_solve_nopiv", "lu_solve_using_factor_nopiv", "lu_rcondest_using_factor",
+           "triangular_rcondest", "gbtrf", "gbtrs", "gbsv", "pbtrf", "pbtrs", "pbsv", "hetrf", "hetrs", "hesv",
+           "indefinite_factor", "indefinite_solve", "indefinite_solve_using_factor"]
+
+
+def getrf(A, target=None, **kw):
+    """LU with partial pivoting; returns (info, pivots) where pivots is a list
+    of lists of (tile_index, offset) as the reference's Pivots."""
+    return call("getrf", A, A, target=target, **kw)
+
+
+def getrf_nopiv(A, target=None, **kw):
+    return call("getrf_nopiv", A, A, target=target, **kw)
+
+
+def getrf_tntpiv(A, target=None, **kw):
+    """Communication-avoiding LU (tournament pivoting); returns (info, pivots)."""
+    return call("getrf_tntpiv", A, A, target=target, **kw)
+
+
+def getrs(A, pivots, B, target=None, **kw):
+    call("getrs", A, A, pivots, B, target=target, **kw)
+
+
+def getrs_nopiv(A, B, target=None, **kw):
+    call("getrs_nopiv", A, A, B, target=target, **kw)
+
+
+def gesv(A, B, target=None, **kw):
+    """Returns (info, pivots)."""
+    return call("gesv", A, A, B, target=target, **kw)
+
+
+def gesv_nopiv(A, B, target=None, **kw):
+    return call("gesv_nopiv", A, A, B, target=target, **kw)
+
+
+def gesv_mixed(A, B, X, target=None, **kw):
+    """fp32 LU + fp64 iterative refinement; returns (info, pivots, iterations)."""
+    return call("gesv_mixed", A, A, B, X, target=target, **kw)
+
+
+def gesv_mixed_gmres(A, B, X, target=None, **kw):
+    return call("gesv_mixed_gmres", A, A, B, X, target=target, **kw)
+
+
+def gesv_rbt(A, B, X, target=None, **kw):
+    return call("gesv_rbt", A, A, B, X, target=target, **kw)
+
+
+def getri(A, pivots, target=None, **kw):
+    return call("getri", A, A, pivots, target=target, **kw)
+
+
+def gecondest(norm, A, anorm, target=None, **kw):
+    return call("gecondest", A, norm, A, anorm, target=target, **kw)
+
+
+def trtri(A, target=None, **kw):
+    return call("trtri", A, A, target=target, **kw)
+
+
+def trtrm(A, target=None, **kw):
+    return call("trtrm", A, A, target=target, **kw)
+
+
+def trcondest(norm, A, target=None, **kw):
+    return call("trcondest", A, norm, A, target=target, **kw)
+
+
+def gbtrf(A, target=None, **kw):
+    return call("gbtrf", A, A, target=target, **kw)
+
+
+def gbtrs(A, pivots, B, target=None, **kw):
+    return call("gbtrs", A, A, pivots, B, target=target, **kw)
+
+
+def gbsv(A, B, target=None, **kw):
+    return call("gbsv", A, A, B, target=target, **kw)
+
+
+def pbtrf(A, target=None, **kw):
+    return call("pbtrf", A, A, target=target, **kw)
+
+
+def pbtrs(A, B, target=None, **kw):
+    return call("pbtrs", A, A, B, target=target, **kw)
+
+
+def pbsv(A, B, target=None, **kw):
+    return call("pbsv", A, A, B, target=target, **kw)
+
+
+def hetrf(A, target=None, **kw):
+    return call("hetrf", A, A, target=target, **kw)
+
+
+def hetrs(A, factors, B, target=None, **kw):
+    return call("hetrs", A, A, factors, B, target=target, **kw)
+
+
+def hesv(A, B, target=None, **kw):
+    return call("hesv", A, A, B, target=target, **kw)
+
+
+lu_factor = getrf
+lu_solve = gesv
+lu_solve_using_factor = getrs
+lu_inverse_using_factor = getri
+lu_factor_nopiv = getrf_nopiv
+lu_solve_nopiv = gesv_nopiv
+lu_solve_using_factor_nopiv = getrs_nopiv
+lu_rcondest_using_factor = gecondest
+triangular_rcondest = trcondest
+indefinite_factor = hetrf
+indefinite_solve = hesv
+indefinite_solve_using_factor = hetrs
