@@ -1,0 +1,168 @@
+#!/usr/bin/env python3
+"""Headline benchmark: fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf /
+dgeqrf at n = 65536 on N MI355X GPUs (BASELINE.json metric).
+
+    python bench.py --gpus N --steps K --warmup W
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+        --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+One process per GPU; a p x q process grid (1x1, 1x2, 2x2, 2x4 by default)
+with RCCL communicators.  Each step runs every routine once on a freshly
+generated synthetic random matrix (counter-hash generator on the device,
+outside the timed region); each routine call is bracketed by a barrier and a
+device synchronize, the per-routine time is the MAX over ranks of the mean
+over the K timed steps.  `value` = total flops / total time over the routine
+suite (whole-job aggregate); per-routine TFLOP/s are in `routines`.
+Flops are LAWN-41 counts (reference docs/latex/flops.py), as the reference
+tester reports them.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+import slate_d35_amd as s  # noqa: E402
+from slate_d35_amd.utils import flops as F  # noqa: E402
+
+METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
+ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=2)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("--routines", default=",".join(ALL))
+    ap.add_argument("--p", type=int, default=0)
+    ap.add_argument("--q", type=int, default=0)
+    ap.add_argument("--lookahead", type=int, default=1)
+    ap.add_argument("--method-lu", default="tntpiv", choices=["ppiv", "tntpiv"])
+    ap.add_argument("--trace", default="")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if s.device_available():
+        s._slate.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, s._slate.device_count()))
+    target = "d" if s.device_available() else "h"
+    p, q = (a.p, a.q) if a.p and a.q else s.choose_grid(world)
+    grid = s.init_grid(p, q)
+    n, nb = a.n, a.nb
+    opts = dict(target=target, lookahead=a.lookahead)
+
+    def barrier_sync():
+        s.sync()
+        if world > 1:
+            grid.world.barrier()
+
+    def max_over_ranks(x):
+        if world == 1:
+            return x
+        import torch
+        import torch.distributed as dist
+        t = torch.tensor([x], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    results = {}
+    routines = [r.strip() for r in a.routines.split(",") if r.strip()]
+    for rname in routines:
+        mats = {}
+        if rname == "dgemm":
+            for key, seed in (("A", 1), ("B", 2), ("C", 3)):
+                M = s.Matrix(n, n, nb, np.float64, grid)
+                M.insertLocalTiles(s.target_of(target))
+                s._slate.generate_matrix_d("rands", M, seed, -1.0, s.opts(target))
+                mats[key] = M
+            flops = F.gemm_flops(n, n, n)
+        else:
+            M = s.Matrix(n, n, nb, np.float64, grid)
+            M.insertLocalTiles(s.target_of(target))
+            mats["A"] = M
+            flops = {"dpotrf": F.potrf_flops, "dgetrf": F.getrf_flops, "dgeqrf": F.geqrf_flops}[rname](n)
+        times = []
+        for step in range(a.warmup + a.steps):
+            if rname != "dgemm":
+                kind = "spd" if rname == "dpotrf" else "rands"
+                s._slate.generate_matrix_d(kind, mats["A"], 100 + step, -1.0, s.opts(target))
+            barrier_sync()
+            if a.trace and step == a.warmup:
+                s.trace.on()
+            t0 = time.perf_counter()
+            if rname == "dgemm":
+                s.gemm(1.0, mats["A"], mats["B"], 0.0, mats["C"], **opts)
+            elif rname == "dpotrf":
+                info = s.potrf(s.HermitianMatrix(s.Uplo.Lower, mats["A"]), **opts)
+                assert info == 0, f"dpotrf info={info}"
+            elif rname == "dgetrf":
+                if a.method_lu == "tntpiv":
+                    info, _ = s.getrf_tntpiv(mats["A"], **opts)
+                else:
+                    info, _ = s.getrf(mats["A"], **opts)
+                assert info == 0, f"dgetrf info={info}"
+            elif rname == "dgeqrf":
+                s.geqrf(mats["A"], **opts)
+            barrier_sync()
+            dt = time.perf_counter() - t0
+            if a.trace and step == a.warmup:
+                s.trace.finish(grid.world, f"{a.trace}_{rname}")
+                s.trace.off()
+            if step >= a.warmup:
+                times.append(dt)
+            if rank == 0:
+                print(f"# {rname} step {step} {'warm' if step < a.warmup else 'timed'}: {dt*1e3:.1f} ms "
+                      f"{flops/dt/1e12:.2f} TFLOP/s", file=sys.stderr, flush=True)
+        t = max_over_ranks(float(np.mean(times)))
+        results[rname] = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops}
+        del mats
+        s.sync()
+        s._slate.release_cache()
+
+    tot_flops = sum(r["flops"] for r in results.values())
+    tot_t = sum(r["ms"] for r in results.values()) / 1e3
+    value = tot_flops / tot_t / 1e12
+    line = {
+        "metric": METRIC,
+        "value": round(value, 3),
+        "unit": "TFLOP/s",
+        "n_gpus": world,
+        "steps": a.steps,
+        "warmup": a.warmup,
+        "ms_per_step": round(tot_t * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "fp64",
+        "data": "synthetic (counter-hash uniform[-1,1); SPD = symmetric + n*I for dpotrf)",
+        "config": {
+            "model": "+".join(results.keys()) + f" n={n} nb={nb}",
+            "global_batch": 1,
+            "seq_len": n,
+            "parallelism": f"2d-block-cyclic {p}x{q} (one process per GPU, RCCL)" if world > 1 else "1x1",
+            "lookahead": a.lookahead,
+            "lu_method": a.method_lu,
+        },
+        "routines": {k: {"tflops": round(v["tflops"], 3), "ms": round(v["ms"], 2)} for k, v in results.items()},
+    }
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+
+
+if __name__ == "__main__":
+    main()

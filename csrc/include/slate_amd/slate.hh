@@ -16,6 +16,7 @@
 #include "matrix.hh"
 #include "func.hh"
 #include "method.hh"
+#include "matgen.hh"
 
 #include <vector>
 

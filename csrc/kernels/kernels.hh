@@ -59,6 +59,11 @@ template <typename T>
 void genorm_partial(char kind, char uplo, char diag, int64_t m, int64_t n, const T* A, int64_t lda,
                     int64_t goff_row, int64_t goff_col, rt<T>* out, hipStream_t s);
 
+// ---- matgen (matgen.hip): fill a block-cyclic local array from a counter hash
+template <typename T>
+void generate(char kind, int64_t mloc, int64_t nloc, T* A, int64_t lda, int64_t mb, int p, int rrel, int64_t row0,
+              int64_t nb, int q, int crel, int64_t col0, uint64_t seed, double shift, hipStream_t s);
+
 // ---- panels (panel.hip)
 template <typename T>
 void lu_colmax(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c, rt<T>* pval, int64_t* pidx,

@@ -4,6 +4,7 @@
 #include <pybind11/pybind11.h>
 #include <pybind11/stl.h>
 #include "slate_amd/slate.hh"
+#include "slate_amd/local_blas.hh"
 
 namespace py = pybind11;
 
@@ -68,9 +69,81 @@ void bind_drivers(py::module_& m, std::string const& s) {
         return v;
     });
 
+    DEF("generate_matrix", [](std::string kind, BaseMatrix<T>& A, uint64_t seed, double shift, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; generate_matrix(kind, A, seed, shift, op); });
+
     // ---- Cholesky
     DEF("potrf", [](HermitianMatrix<T>& A, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; return potrf(A, op); });
+
+    // ---- direct local-kernel access on raw device pointers (single process)
+    auto dctx = []() { return lb::Ctx::device(0); };
+    auto dsync = [](lb::Ctx const& c) { slate_hip_call(hipStreamSynchronize(c.stream)); };
+    auto cop = [](std::string const& x) { return x == "N" ? Op::NoTrans : x == "T" ? Op::Trans : Op::ConjTrans; };
+    auto cup = [](std::string const& x) { return x == "L" ? Uplo::Lower : x == "U" ? Uplo::Upper : Uplo::General; };
+    DEF("lb_gemm", [=](std::string ta, std::string tb, int64_t mm, int64_t n, int64_t k, T a, uintptr_t A, int64_t lda,
+                       uintptr_t B, int64_t ldb, T b, uintptr_t C, int64_t ldc) {
+        py::gil_scoped_release r;
+        auto c = dctx();
+        lb::gemm<T>(c, cop(ta), cop(tb), mm, n, k, a, (T*)A, lda, (T*)B, ldb, b, (T*)C, ldc);
+        dsync(c);
+    });
+    DEF("lb_herk", [=](std::string up, std::string op, int64_t n, int64_t k, R a, uintptr_t A, int64_t lda, R b,
+                       uintptr_t C, int64_t ldc) {
+        py::gil_scoped_release r;
+        auto c = dctx();
+        lb::herk<T>(c, cup(up), cop(op), n, k, a, (T*)A, lda, b, (T*)C, ldc);
+        dsync(c);
+    });
+    DEF("lb_trsm", [=](std::string sd, std::string up, std::string op, std::string dg, int64_t mm, int64_t n, T a,
+                       uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb) {
+        py::gil_scoped_release r;
+        auto c = dctx();
+        lb::trsm<T>(c, sd == "L" ? Side::Left : Side::Right, cup(up), cop(op), dg == "U" ? Diag::Unit : Diag::NonUnit,
+                    mm, n, a, (T*)A, lda, (T*)B, ldb);
+        dsync(c);
+    });
+    DEF("lb_potrf", [=](std::string up, int64_t n, uintptr_t A, int64_t lda) {
+        py::gil_scoped_release r;
+        auto c = dctx();
+        device::Buffer<int> info(1);
+        device::memset_async(info.data(), 0, sizeof(int), c.stream);
+        lb::potrf<T>(c, cup(up), n, (T*)A, lda, info.data(), 0);
+        int h = 0;
+        device::memcpy_async(&h, info.data(), sizeof(int), c.stream);
+        dsync(c);
+        return h;
+    });
+    DEF("lb_getrf_panel", [=](int64_t mm, int64_t n, uintptr_t A, int64_t lda) {
+        std::vector<int64_t> ipiv(std::min(mm, n));
+        int h = 0;
+        {
+            py::gil_scoped_release r;
+            auto c = dctx();
+            device::Buffer<int> info(1);
+            device::Buffer<int64_t> dpiv(ipiv.size() + 1), perm(mm + 1);
+            device::memset_async(info.data(), 0, sizeof(int), c.stream);
+            lb::getrf_panel<T>(c, mm, n, (T*)A, lda, dpiv.data(), perm.data(), info.data(), 0, true);
+            device::memcpy_async(ipiv.data(), dpiv.data(), ipiv.size() * sizeof(int64_t), c.stream);
+            device::memcpy_async(&h, info.data(), sizeof(int), c.stream);
+            dsync(c);
+        }
+        return py::make_tuple(h, ipiv);
+    });
+    DEF("lb_geqrf_panel", [=](int64_t mm, int64_t n, uintptr_t A, int64_t lda) {
+        int64_t k = std::min(mm, n);
+        std::vector<T> tau(k), Tm(k * k);
+        {
+            py::gil_scoped_release r;
+            auto c = dctx();
+            device::Buffer<T> dt(k + 1), dT(k * k + 1);
+            lb::geqrf_panel<T>(c, mm, n, (T*)A, lda, dt.data(), dT.data(), k);
+            device::memcpy_async(tau.data(), dt.data(), k * sizeof(T), c.stream);
+            device::memcpy_async(Tm.data(), dT.data(), k * k * sizeof(T), c.stream);
+            dsync(c);
+        }
+        return py::make_tuple(tau, Tm);
+    });
 
 #undef DEF
 }

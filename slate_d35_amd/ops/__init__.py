@@ -24,8 +24,13 @@ def _suffix(t):
 
 def _cm(t):
     """(ptr, m, n, ld) of a torch tensor viewed as a column-major matrix:
-    a row-major (n x m) contiguous tensor is an m x n column-major matrix."""
+    a row-major (n x m) contiguous tensor is an m x n column-major matrix.
+    Synchronizes torch's stream first: the native kernels run on the
+    framework's own HIP queues."""
+    import torch
     assert t.dim() == 2 and t.stride(1) == 1, "row-major contiguous rows expected"
+    if t.is_cuda:
+        torch.cuda.synchronize(t.device)
     return t.data_ptr(), t.shape[1], t.shape[0], t.stride(0)
 
 
