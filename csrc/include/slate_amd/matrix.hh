@@ -285,9 +285,13 @@ public:
 
     /// Allocate local storage at the target's location (Matrix.hh:832).
     void insertLocalTiles(Target target = Target::Host) const {
-        this->storage_->allocate(target == Target::Devices ? Loc::Device : Loc::Host);
         auto loc = target == Target::Devices ? Loc::Device : Loc::Host;
-        if (this->storage_->state(loc) == Invalid) this->storage_->modified(loc);
+        auto other = loc == Loc::Device ? Loc::Host : Loc::Device;
+        bool fresh = !(this->storage_->has(other) && this->storage_->state(other) != Invalid);
+        this->storage_->allocate(loc);
+        // a brand-new matrix: this instance becomes the valid one; otherwise
+        // the existing valid instance is copied on first coherent access
+        if (fresh && this->storage_->state(loc) == Invalid) this->storage_->modified(loc);
     }
 
     /// New matrix with the same shape & distribution, no data (Matrix.hh:432).

@@ -76,6 +76,72 @@ void bind_drivers(py::module_& m, std::string const& s) {
     DEF("potrf", [](HermitianMatrix<T>& A, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; return potrf(A, op); });
 
+    DEF("potrs", [](HermitianMatrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; potrs(A, B, op); });
+    DEF("posv", [](HermitianMatrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return posv(A, B, op); });
+    DEF("potri", [](HermitianMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return potri(A, op); });
+    DEF("trtri", [](TriangularMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return trtri(A, op); });
+    DEF("trtrm", [](TriangularMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; trtrm(A, op); });
+
+    // ---- LU (pivots as list of lists of (tile_index, offset))
+    auto piv_out = [](Pivots const& P) {
+        py::list out;
+        for (auto const& v : P) {
+            py::list l;
+            for (auto const& x : v) l.append(py::make_tuple(x.tileIndex(), x.elementOffset()));
+            out.append(l);
+        }
+        return out;
+    };
+    auto piv_in = [](py::list L) {
+        Pivots P;
+        for (auto v : L) {
+            std::vector<Pivot> pv;
+            for (auto x : v.cast<py::list>()) {
+                auto t = x.cast<py::tuple>();
+                pv.emplace_back(t[0].cast<int64_t>(), t[1].cast<int64_t>());
+            }
+            P.push_back(pv);
+        }
+        return P;
+    };
+    DEF("getrf", [=](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); Pivots P; int64_t info;
+        { py::gil_scoped_release r; info = getrf(A, P, op); }
+        return py::make_tuple(info, piv_out(P)); });
+    DEF("getrf_tntpiv", [=](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); Pivots P; int64_t info;
+        { py::gil_scoped_release r; info = getrf_tntpiv(A, P, op); }
+        return py::make_tuple(info, piv_out(P)); });
+    DEF("getrf_nopiv", [](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return getrf_nopiv(A, op); });
+    DEF("getrs", [=](Matrix<T> const& A, py::list piv, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; getrs(A, P, B, op); });
+    DEF("getrs_nopiv", [](Matrix<T> const& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; getrs_nopiv(A, B, op); });
+    DEF("gesv", [=](Matrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P; int64_t info;
+        { py::gil_scoped_release r; info = gesv(A, P, B, op); }
+        return py::make_tuple(info, piv_out(P)); });
+    DEF("gesv_nopiv", [](Matrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return gesv_nopiv(A, B, op); });
+    DEF("getri", [=](Matrix<T>& A, py::list piv, py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; return getri(A, P, op); });
+    if constexpr (std::is_same_v<T, double> || std::is_same_v<T, std::complex<double>>) {
+        DEF("gesv_mixed", [=](Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, py::dict o) {
+            Options op = to_options(o); Pivots P; int iter = 0; int64_t info;
+            { py::gil_scoped_release r; info = gesv_mixed(A, P, B, X, iter, op); }
+            return py::make_tuple(info, piv_out(P), iter); });
+        DEF("posv_mixed", [](HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, py::dict o) {
+            Options op = to_options(o); int iter = 0; int64_t info;
+            { py::gil_scoped_release r; info = posv_mixed(A, B, X, iter, op); }
+            return py::make_tuple(info, iter); });
+    }
+
     // ---- direct local-kernel access on raw device pointers (single process)
     auto dctx = []() { return lb::Ctx::device(0); };
     auto dsync = [](lb::Ctx const& c) { slate_hip_call(hipStreamSynchronize(c.stream)); };

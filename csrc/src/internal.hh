@@ -122,5 +122,9 @@ inline void allreduce_host(Comm& comm, R* v, size_t n, ReduceOp op) {
 template <typename T>
 void redistribute_op(BaseMatrix<T> const& A, BaseMatrix<T>& B, Target target);
 
+/// Apply LU pivots to the rows of B (forward: P B; backward: P^T B).
+template <typename T>
+void apply_pivots(Pivots const& pivots, BaseMatrix<T> const& A, Matrix<T>& B, Target target, bool forward);
+
 }  // namespace internal
 }  // namespace slate

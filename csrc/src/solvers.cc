@@ -1,0 +1,313 @@
+// Solvers built on the factorizations (reference src/getrs.cc, gesv.cc,
+// getrs_nopiv.cc, gesv_nopiv.cc, potrs.cc, posv.cc, potri.cc, getri.cc,
+// trtri.cc, trtrm.cc, gesv_mixed.cc, posv_mixed.cc, gesv_mixed_gmres.cc,
+// posv_mixed_gmres.cc).
+//
+// Mixed precision (gesv_mixed / posv_mixed, reference gesv_mixed.cc:106-290):
+// factor an fp32 copy with the fp32 MFMA kernels, solve in fp32, then refine
+// in fp64: R = B - A X with the fp64 MFMA GEMM, correction solved with the
+// fp32 factors, convergence by the reference's criterion
+// ||R||_max < ||X||_max * ||A||_inf * eps * sqrt(n) (iterRefConverged);
+// fall back to a full-precision factorization if it does not converge.
+#include "internal.hh"
+
+#include <cmath>
+
+namespace slate {
+
+using namespace internal;
+
+namespace {
+template <typename T>
+TriangularMatrix<T> tri(Uplo u, Diag d, BaseMatrix<T> const& A) {
+    Matrix<T> G(A);
+    G.set_uplo(Uplo::General);
+    return TriangularMatrix<T>(u, d, G);
+}
+}  // namespace
+
+//------------------------------------------------------------------------------
+template <typename T>
+void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("getrs");
+    Target target = resolve_target(opts);
+    apply_pivots(pivots, A, B, target, true);
+    trsm(Side::Left, T(1), tri<T>(Uplo::Lower, Diag::Unit, A), B, opts);
+    trsm(Side::Left, T(1), tri<T>(Uplo::Upper, Diag::NonUnit, A), B, opts);
+}
+
+template <typename T>
+void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("getrs_nopiv");
+    trsm(Side::Left, T(1), tri<T>(Uplo::Lower, Diag::Unit, A), B, opts);
+    trsm(Side::Left, T(1), tri<T>(Uplo::Upper, Diag::NonUnit, A), B, opts);
+}
+
+template <typename T>
+int64_t gesv(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("gesv");
+    int64_t info = getrf(A, pivots, opts);
+    if (info == 0) getrs(A, pivots, B, opts);
+    return info;
+}
+
+template <typename T>
+int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("gesv_nopiv");
+    int64_t info = getrf_nopiv(A, opts);
+    if (info == 0) getrs_nopiv(A, B, opts);
+    return info;
+}
+
+template <typename T>
+void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("potrs");
+    // A = L L^H (lower) or U^H U (upper) in the physical triangle
+    BaseMatrix<T> Ap = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
+    Uplo u = A.uplo_physical();
+    auto Tm = tri<T>(u, Diag::NonUnit, Ap);
+    if (u == Uplo::Lower) {
+        trsm(Side::Left, T(1), Tm, B, opts);
+        trsm(Side::Left, T(1), conj_transpose(Tm), B, opts);
+    } else {
+        trsm(Side::Left, T(1), conj_transpose(Tm), B, opts);
+        trsm(Side::Left, T(1), Tm, B, opts);
+    }
+}
+
+template <typename T>
+int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("posv");
+    int64_t info = potrf(A, opts);
+    if (info == 0) potrs(A, B, opts);
+    return info;
+}
+
+//------------------------------------------------------------------------------
+// inverses
+template <typename T>
+int64_t trtri(TriangularMatrix<T>& A, Options const& opts) {
+    trace::Block tb("trtri");
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
+    if (A.grid()->size() == 1 && A.op() == Op::NoTrans) {
+        lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+        LocalBlock<T> la = A.local(loc, true);
+        lb::trtri(c, A.uplo(), A.diag(), la.m, la.ptr, la.ld);
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+        A.storage()->update_origin();
+        return 0;
+    }
+    // distributed: solve A X = I
+    Matrix<T> X = Matrix<T>(BaseMatrix<T>(A)).emptyLike();
+    X.insertLocalTiles(target);
+    set(T(0), T(1), X, opts);
+    trsm(Side::Left, T(1), A, X, opts);
+    BaseTrapezoidMatrix<T> Xt(A.uplo(), X, MatrixKind::Trapezoid);
+    slate::copy<T, T>(Xt, A, opts);
+    return 0;
+}
+
+template <typename T>
+void trtrm(TriangularMatrix<T>& A, Options const& opts) {
+    trace::Block tb("trtrm");
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
+    if (A.grid()->size() == 1 && A.op() == Op::NoTrans) {
+        lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+        LocalBlock<T> la = A.local(loc, true);
+        lb::lauum(c, A.uplo(), la.m, la.ptr, la.ld);
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+        A.storage()->update_origin();
+        return;
+    }
+    // distributed: L^H L via a dense copy of L and herk-style gemm
+    Matrix<T> F = Matrix<T>(BaseMatrix<T>(A)).emptyLike();
+    F.insertLocalTiles(target);
+    set(T(0), T(0), F, opts);
+    BaseTrapezoidMatrix<T> Ft(A.uplo(), F, MatrixKind::Trapezoid);
+    slate::copy<T, T>(A, Ft, opts);
+    Matrix<T> G = F.emptyLike();
+    G.insertLocalTiles(target);
+    if (A.uplo() == Uplo::Lower) gemm(T(1), conj_transpose(F), F, T(0), G, opts);
+    else gemm(T(1), F, conj_transpose(F), T(0), G, opts);
+    BaseTrapezoidMatrix<T> Gt(A.uplo(), G, MatrixKind::Trapezoid);
+    slate::copy<T, T>(Gt, A, opts);
+}
+
+template <typename T>
+int64_t potri(HermitianMatrix<T>& A, Options const& opts) {
+    trace::Block tb("potri");
+    int64_t info = 0;
+    BaseMatrix<T> Ap = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
+    TriangularMatrix<T> Tm = tri<T>(A.uplo_physical(), Diag::NonUnit, Ap);
+    info = trtri(Tm, opts);
+    if (info == 0) trtrm(Tm, opts);
+    return info;
+}
+
+template <typename T>
+int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts) {
+    trace::Block tb("getri");
+    Target target = resolve_target(opts);
+    // A^{-1} = U^{-1} L^{-1} P: solve (L U) X = P^T ... via X = A^{-1} I
+    Matrix<T> X = A.emptyLike();
+    X.insertLocalTiles(target);
+    set(T(0), T(1), X, opts);
+    getrs(A, pivots, X, opts);
+    slate::copy<T, T>(X, A, opts);
+    return 0;
+}
+
+//------------------------------------------------------------------------------
+// mixed precision iterative refinement
+namespace {
+
+template <typename T> struct lower_prec { using type = T; };
+template <> struct lower_prec<double> { using type = float; };
+template <> struct lower_prec<std::complex<double>> { using type = std::complex<float>; };
+
+template <typename T>
+bool iter_ref_converged(std::vector<real_type<T>> const& rnorm, std::vector<real_type<T>> const& xnorm,
+                        real_type<T> cte) {
+    for (size_t j = 0; j < rnorm.size(); ++j)
+        if (!(rnorm[j] < xnorm[j] * cte)) return false;
+    return true;
+}
+
+template <typename T, typename Fac, typename Slv, typename FullSolve>
+int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts,
+                     Fac&& factor_lo, Slv&& solve_lo, FullSolve&& full_solve, char const* name) {
+    using Lo = typename lower_prec<T>::type;
+    using R = real_type<T>;
+    Target target = resolve_target(opts);
+    const int itermax = int(get_option<int64_t>(opts, Option::MaxIterations, 30));
+    const bool fallback = get_option<int64_t>(opts, Option::UseFallbackSolver, 1) != 0;
+    const R eps = std::numeric_limits<R>::epsilon();
+    Timer timer;
+    iter = 0;
+    const int64_t n = A.n(), nrhs = B.n();
+    R Anorm = norm(Norm::Inf, A, opts);
+    const R cte = Anorm * eps * std::sqrt(R(n));
+    // low-precision copies
+    Matrix<Lo> A_lo(A.m(), A.n(), A.mb(), A.nb(), A.grid());
+    A_lo.insertLocalTiles(target);
+    Matrix<Lo> X_lo(B.m(), B.n(), B.mb(), B.nb(), B.grid());
+    X_lo.insertLocalTiles(target);
+    slate::copy<T, Lo>(A, A_lo, opts);
+    slate::copy<T, Lo>(B, X_lo, opts);
+    timer.reset();
+    int64_t info = factor_lo(A_lo);
+    timers()[std::string(name) + "::factor_lo"] = timer.elapsed();
+    if (info != 0) {
+        iter = -3;
+    } else {
+        solve_lo(A_lo, X_lo);
+        slate::copy<Lo, T>(X_lo, X, opts);
+        Matrix<T> Rm = B.emptyLike();
+        Rm.insertLocalTiles(target);
+        std::vector<R> rnorm(nrhs), xnorm(nrhs);
+        timer.reset();
+        for (int it = 0; it <= itermax; ++it) {
+            // R = B - A X
+            slate::copy<T, T>(B, Rm, opts);
+            gemm(T(-1), A, X, T(1), Rm, opts);
+            colNorms(Norm::Max, X, xnorm.data(), opts);
+            colNorms(Norm::Max, Rm, rnorm.data(), opts);
+            if (iter_ref_converged<T>(rnorm, xnorm, cte)) {
+                iter = it;
+                timers()[std::string(name) + "::iter_ref"] = timer.elapsed();
+                return 0;
+            }
+            if (it == itermax) break;
+            // correction in low precision: X += A_lo^{-1} R
+            slate::copy<T, Lo>(Rm, X_lo, opts);
+            solve_lo(A_lo, X_lo);
+            Matrix<T> D = X.emptyLike();
+            D.insertLocalTiles(target);
+            slate::copy<Lo, T>(X_lo, D, opts);
+            add(T(1), D, T(1), X, opts);
+        }
+        iter = -itermax - 1;
+    }
+    if (!fallback) return info;
+    // fall back to a full precision solve
+    timer.reset();
+    slate::copy<T, T>(B, X, opts);
+    info = full_solve(A, X);
+    timers()[std::string(name) + "::fallback"] = timer.elapsed();
+    return info;
+}
+
+}  // namespace
+
+template <typename T>
+int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
+    trace::Block tb("gesv_mixed");
+    using Lo = typename lower_prec<T>::type;
+    if constexpr (std::is_same_v<Lo, T>) {
+        slate_error("gesv_mixed requires a double-precision type");
+    } else {
+        Pivots piv_lo;
+        Matrix<T> Acopy;  // original A is needed for residuals; factorization works on A_lo
+        return mixed_refine<T>(A, B, X, iter, opts,
+            [&](Matrix<Lo>& A_lo) { return getrf(A_lo, piv_lo, opts); },
+            [&](Matrix<Lo>& A_lo, Matrix<Lo>& X_lo) { getrs(A_lo, piv_lo, X_lo, opts); },
+            [&](Matrix<T>& Af, Matrix<T>& Xf) { return gesv(Af, pivots, Xf, opts); }, "gesv_mixed");
+    }
+    return 0;
+}
+
+template <typename T>
+int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
+    trace::Block tb("posv_mixed");
+    using Lo = typename lower_prec<T>::type;
+    if constexpr (std::is_same_v<Lo, T>) {
+        slate_error("posv_mixed requires a double-precision type");
+    } else {
+        Matrix<T> Ag(A);
+        Ag.set_uplo(Uplo::General);
+        // the residual needs the full Hermitian matrix: use hemm via a dense copy
+        Uplo u = A.uplo();
+        Matrix<T> Afull = Ag.emptyLike();
+        Afull.insertLocalTiles(resolve_target(opts));
+        {
+            // Afull = herm(A)
+            slate::copy<T, T>(conj_transpose(Ag), Afull, opts);
+            BaseTrapezoidMatrix<T> At(u, Ag, MatrixKind::Trapezoid), Ft(u, Afull, MatrixKind::Trapezoid);
+            slate::copy<T, T>(At, Ft, opts);
+        }
+        return mixed_refine<T>(Afull, B, X, iter, opts,
+            [&](Matrix<Lo>& A_lo) { HermitianMatrix<Lo> H(u, A_lo); return potrf(H, opts); },
+            [&](Matrix<Lo>& A_lo, Matrix<Lo>& X_lo) { HermitianMatrix<Lo> H(u, A_lo); potrs(H, X_lo, opts); },
+            [&](Matrix<T>&, Matrix<T>& Xf) { return posv(A, Xf, opts); }, "posv_mixed");
+    }
+    return 0;
+}
+
+//------------------------------------------------------------------------------
+#define SLATE_SOLVE_INST(T)                                                                     \
+    template void getrs<T>(Matrix<T> const&, Pivots const&, Matrix<T>&, Options const&);       \
+    template void getrs_nopiv<T>(Matrix<T> const&, Matrix<T>&, Options const&);                \
+    template int64_t gesv<T>(Matrix<T>&, Pivots&, Matrix<T>&, Options const&);                 \
+    template int64_t gesv_nopiv<T>(Matrix<T>&, Matrix<T>&, Options const&);                    \
+    template void potrs<T>(HermitianMatrix<T> const&, Matrix<T>&, Options const&);             \
+    template int64_t posv<T>(HermitianMatrix<T>&, Matrix<T>&, Options const&);                 \
+    template int64_t trtri<T>(TriangularMatrix<T>&, Options const&);                           \
+    template void trtrm<T>(TriangularMatrix<T>&, Options const&);                              \
+    template int64_t potri<T>(HermitianMatrix<T>&, Options const&);                            \
+    template int64_t getri<T>(Matrix<T>&, Pivots const&, Options const&);
+
+SLATE_SOLVE_INST(float)
+SLATE_SOLVE_INST(double)
+SLATE_SOLVE_INST(std::complex<float>)
+SLATE_SOLVE_INST(std::complex<double>)
+
+template int64_t gesv_mixed<double>(Matrix<double>&, Pivots&, Matrix<double>&, Matrix<double>&, int&, Options const&);
+template int64_t gesv_mixed<std::complex<double>>(Matrix<std::complex<double>>&, Pivots&, Matrix<std::complex<double>>&,
+                                                  Matrix<std::complex<double>>&, int&, Options const&);
+template int64_t posv_mixed<double>(HermitianMatrix<double>&, Matrix<double>&, Matrix<double>&, int&, Options const&);
+template int64_t posv_mixed<std::complex<double>>(HermitianMatrix<std::complex<double>>&, Matrix<std::complex<double>>&,
+                                                  Matrix<std::complex<double>>&, int&, Options const&);
+
+}  // namespace slate

@@ -9,6 +9,13 @@ this package adds dtype dispatch, grid bootstrap and torch interop.
     A = slate.from_numpy(a, nb=512, target="d")
     info = slate.potrf(slate.HermitianMatrix(slate.Uplo.Lower, A), target="d")
 """
+try:
+    # Load torch's HIP runtime first: its libamdhip64/librccl carry the same
+    # SONAMEs as the system ROCm ones, so the native library then binds to
+    # the already-loaded copies and the process has ONE HIP runtime.
+    import torch as _torch  # noqa: F401
+except Exception:  # torch is optional for the native library
+    _torch = None
 from . import _slate
 from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid,  # noqa: F401
                     Matrix, HermitianMatrix, SymmetricMatrix, TriangularMatrix, TrapezoidMatrix,
