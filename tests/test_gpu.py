@@ -71,7 +71,8 @@ def test_trsm_kernel(dtype, side, uplo, op, diag):
     torch = _torch()
     m, n = 700, 300
     na = m if side == "L" else n
-    t = rnd(na, na, dtype, 6) + 4 * np.eye(na, dtype=dtype)
+    # well-conditioned triangle (random unit triangles are exponentially ill-conditioned)
+    t = rnd(na, na, dtype, 6) / na + 2 * np.eye(na, dtype=dtype)
     t = np.tril(t) if uplo == "L" else np.triu(t)
     te = t.copy()
     if diag == "U":
@@ -201,3 +202,43 @@ def test_generate_matrix_device_matches_host():
         s._slate.generate_matrix_d(kind, A, 5, -1.0, s.opts("d"))
         s._slate.generate_matrix_d(kind, B, 5, -1.0, s.opts("h"))
         np.testing.assert_array_equal(s.to_numpy(A), s.to_numpy(B))
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+@pytest.mark.parametrize("mn", [(700, 700), (900, 500), (500, 900)])
+def test_getrf_driver_device(dtype, mn):
+    m, n = mn
+    nb = 128
+    a = rnd(m, n, dtype, 21)
+    A = s.from_numpy(a, nb=nb, target="d")
+    info, piv = s.getrf(A, target="d", lookahead=1)
+    f = s.to_numpy(A)
+    k = min(m, n)
+    L = np.tril(f[:, :k], -1) + np.eye(m, k)
+    U = np.triu(f[:k, :])
+    ip = [kk * nb + ti * nb + off for kk, pv in enumerate(piv) for (ti, off) in pv]
+    pa = a.copy()
+    for j, p_ in enumerate(ip):
+        pa[[j, p_]] = pa[[p_, j]]
+    assert info == 0 and relerr(L @ U, pa) < 10 * tol(dtype)
+
+
+def test_gesv_mixed_device():
+    n, nb = 1000, 128
+    a = rnd(n, n, np.float64, 31)
+    b = rnd(n, 4, np.float64, 32)
+    A, B = s.from_numpy(a, nb=nb, target="d"), s.from_numpy(b, nb=nb, target="d")
+    X = s.from_numpy(np.zeros_like(b), nb=nb, target="d")
+    info, piv, it = s.gesv_mixed(A, B, X, target="d")
+    x = s.to_numpy(X)
+    assert info == 0 and it >= 0
+    assert np.linalg.norm(a @ x - b, 1) / (np.linalg.norm(a, 1) * np.linalg.norm(x, 1)) < 1e-15 * n
+
+
+def test_posv_device():
+    n, nb = 900, 128
+    a = s.utils.spd_matrix(n)
+    b = rnd(n, 3, np.float64, 33)
+    A, B = s.from_numpy(a, nb=nb, target="d"), s.from_numpy(b, nb=nb, target="d")
+    assert s.posv(s.HermitianMatrix(s.Uplo.Lower, A), B, target="d") == 0
+    assert relerr(a @ s.to_numpy(B), b) < 1e-12
