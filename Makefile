@@ -23,7 +23,7 @@ HIP_SRC   := $(wildcard csrc/kernels/*.hip)
 CC_SRC    := $(wildcard csrc/src/*.cc)
 HIP_OBJ   := $(patsubst csrc/kernels/%.hip,$(BUILD)/k_%.o,$(HIP_SRC))
 CC_OBJ    := $(patsubst csrc/src/%.cc,$(BUILD)/s_%.o,$(CC_SRC))
-HDRS      := $(wildcard csrc/include/slate_amd/*.hh) $(wildcard csrc/kernels/*.hh) $(wildcard csrc/src/*.hh)
+HDRS      := $(wildcard csrc/include/slate_amd/*.hh) $(wildcard csrc/kernels/*.hh) $(wildcard csrc/src/*.hh) $(wildcard csrc/python/*.hh)
 
 LIB       := $(PKG)/libslate_amd.so
 PYMOD     := $(PKG)/_slate$(PY_EXT)

@@ -142,6 +142,26 @@ void bind_drivers(py::module_& m, std::string const& s) {
             return py::make_tuple(info, iter); });
     }
 
+    // ---- QR / LQ
+    DEF("geqrf", [](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); TriangularFactors<T> Tf;
+        { py::gil_scoped_release r; geqrf(A, Tf, op); }
+        return Tf; });
+    DEF("gelqf", [](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); TriangularFactors<T> Tf;
+        { py::gil_scoped_release r; gelqf(A, Tf, op); }
+        return Tf; });
+    DEF("unmqr", [](Side sd, Op opq, Matrix<T> const& A, TriangularFactors<T> const& Tf, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; unmqr(sd, opq, A, Tf, C, op); });
+    DEF("unmlq", [](Side sd, Op opq, Matrix<T> const& A, TriangularFactors<T> const& Tf, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; unmlq(sd, opq, A, Tf, C, op); });
+    DEF("gels", [](Matrix<T>& A, Matrix<T>& BX, py::dict o) {
+        Options op = to_options(o); TriangularFactors<T> Tf;
+        { py::gil_scoped_release r; gels(A, Tf, BX, op); }
+        return Tf; });
+    DEF("cholqr", [](Matrix<T>& A, Matrix<T>& R, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return cholqr(A, R, op); });
+
     // ---- direct local-kernel access on raw device pointers (single process)
     auto dctx = []() { return lb::Ctx::device(0); };
     auto dsync = [](lb::Ctx const& c) { slate_hip_call(hipStreamSynchronize(c.stream)); };

@@ -3,7 +3,7 @@
 # crash/timeout (exit > 1); plain test failures (exit 1) continue.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-BENCH_ARGS=${BENCH_ARGS:-"--routines dgemm,dpotrf,dgetrf --n 32768 --steps 2 --warmup 1"}
+BENCH_ARGS=${BENCH_ARGS:-"--n 32768 --steps 2 --warmup 1"}
 timeout -k 10 ${PYTEST_TIMEOUT:-900} python -m pytest tests -m gpu -q -x ${PYTEST_ARGS:-} > gpurun_out/pytest_gpu.log 2>&1
 rc=$?; tail -30 gpurun_out/pytest_gpu.log
 if [ $rc -gt 1 ]; then echo "pytest rc=$rc -> stop"; exit $rc; fi

@@ -242,3 +242,29 @@ def test_posv_device():
     A, B = s.from_numpy(a, nb=nb, target="d"), s.from_numpy(b, nb=nb, target="d")
     assert s.posv(s.HermitianMatrix(s.Uplo.Lower, A), B, target="d") == 0
     assert relerr(a @ s.to_numpy(B), b) < 1e-12
+
+
+@pytest.mark.parametrize("mn", [(700, 700), (1000, 400)])
+def test_geqrf_driver_device(mn):
+    m, n = mn
+    nb = 128
+    a = rnd(m, n, np.float64, 41)
+    A = s.from_numpy(a, nb=nb, target="d")
+    T = s.geqrf(A, target="d")
+    k = min(m, n)
+    R = np.triu(s.to_numpy(A)[:k, :])
+    C = s.from_numpy(a, nb=nb, target="d")
+    s.unmqr(s.Side.Left, s.Op.ConjTrans, A, T, C, target="d")
+    qa = s.to_numpy(C)
+    assert relerr(qa[:k], R) < 1e-13
+    if m > k:
+        assert np.abs(qa[k:]).max() < 1e-12
+
+
+def test_gels_device():
+    m, n = 900, 300
+    a, b = rnd(m, n, np.float64, 42), rnd(m, 2, np.float64, 43)
+    A, B = s.from_numpy(a, nb=128, target="d"), s.from_numpy(b, nb=128, target="d")
+    s.gels(A, B, target="d")
+    x = s.to_numpy(B)[:n]
+    assert relerr(x, np.linalg.lstsq(a, b, rcond=None)[0]) < 1e-12
