@@ -29,8 +29,11 @@ namespace device {
 /// Number of streams ("queues") per process.  Index semantics follow the
 /// reference's queue indices (potrf.cc:66, getrf.cc:122: queue 0 = trailing
 /// update, 1 = panel, 2.. = lookahead columns) plus a dedicated comm stream.
-constexpr int kNumQueues = 8;
-constexpr int kCommQueue = kNumQueues - 1;
+constexpr int kNumQueues = 9;
+constexpr int kCommQueue = 7;
+/// Trailing-update queue of the factorizations: runs on the CUs not reserved
+/// for the panel/comm queues (queue 0 keeps the whole device).
+constexpr int kTrailQueue = 8;
 
 /// True iff a HIP device is visible to this process.
 bool available();
@@ -43,6 +46,8 @@ int  get_device();
 /// Per-process stream set.  Queue 1 (panel) is created with high priority.
 hipStream_t queue(int index);
 void sync_all();
+/// CUs reserved for the panel/comm queues (0 = no partitioning).
+int reserved_cus();
 
 /// Pooled event (disable-timing events for dependency edges).
 hipEvent_t event_get();

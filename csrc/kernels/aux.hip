@@ -154,91 +154,108 @@ __global__ void transpose_kernel(bool conjugate, int64_t m, int64_t n, const T* 
 }
 
 //------------------------------------------------------------------------------
+// Broadcast lane `src` of v to the whole wave (v_readlane; src is uniform).
+__device__ inline float  bcast_lane(float v, int src)  { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src)); }
+__device__ inline double bcast_lane(double v, int src) {
+    int2 t = __builtin_bit_cast(int2, v);
+    t.x = __builtin_amdgcn_readlane(t.x, src);
+    t.y = __builtin_amdgcn_readlane(t.y, src);
+    return __builtin_bit_cast(double, t);
+}
+template <typename R>
+__device__ inline cplx<R> bcast_lane(cplx<R> v, int src) { return cplx<R>(bcast_lane(v.re, src), bcast_lane(v.im, src)); }
+
 // Inverse of the diagonal nbs x nbs blocks of a triangular matrix (nbs <= 64).
 // Block b of A (at A + b*nbs*(1+lda)) is inverted into W (same position in W,
 // ld ldw); the full square block is written (zeros outside the triangle).
 // One 64-lane wave per block; lane j computes column j of the inverse by
-// substitution against the LDS copy of the block.
+// substitution with the column held in REGISTERS (fully unrolled, static
+// indices); the triangle is read from LDS as wave-uniform broadcasts.
 template <typename T>
-__global__ void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
-                                  const T* A, int64_t lda, T* W, int64_t ldw) {
-    __shared__ T L[64][65];
-    __shared__ T X[64][65];
+__global__ __launch_bounds__(64)
+void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
+                       const T* A, int64_t lda, T* W, int64_t ldw) {
+    __shared__ T L[64][64];
+    __shared__ T rd[64];
     const int b = blockIdx.x;
     const int64_t off = (int64_t)b * nbs;
     const int nb = (int)min<int64_t>(nbs, n - off);
     const int lane = threadIdx.x;
     const T* Ab = A + off + off * lda;
     T* Wb = W + off + off * ldw;
-    for (int j = 0; j < nb; ++j)
-        L[lane][j] = lane < nb ? Ab[lane + j * lda] : zero<T>();
-    __syncthreads();
     const bool unit = (diag == 'U');
+    const bool lower = (uplo == 'L');
+    for (int j = 0; j < 64; ++j)
+        L[lane][j] = (lane < nb && j < nb) ? Ab[lane + j * lda] : (lane == j ? one<T>() : zero<T>());
+    __syncthreads();
+    rd[lane] = unit ? one<T>() : one<T>() / L[lane][lane];
+    __syncthreads();
     const int j = lane;
-    if (j < nb) {
-        if (uplo == 'L') {
-            for (int i = 0; i < j; ++i) X[i][j] = zero<T>();
-            X[j][j] = unit ? one<T>() : one<T>() / L[j][j];
-            for (int i = j + 1; i < nb; ++i) {
-                T s = zero<T>();
-                for (int l = j; l < i; ++l) s += L[i][l] * X[l][j];
-                X[i][j] = unit ? -s : -(s / L[i][i]);
-            }
-        } else {
-            for (int i = j + 1; i < nb; ++i) X[i][j] = zero<T>();
-            X[j][j] = unit ? one<T>() : one<T>() / L[j][j];
-            for (int i = j - 1; i >= 0; --i) {
-                T s = zero<T>();
-                for (int l = i + 1; l <= j; ++l) s += L[i][l] * X[l][j];
-                X[i][j] = unit ? -s : -(s / L[i][i]);
-            }
+    T x[64];
+    if (lower) {
+        #pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            T s = zero<T>();
+            #pragma unroll
+            for (int l = 0; l < i; ++l) s += L[i][l] * x[l];
+            x[i] = (i < j) ? zero<T>() : ((i == j) ? rd[i] : -(s * rd[i]));
+        }
+    } else {
+        #pragma unroll
+        for (int i = 63; i >= 0; --i) {
+            T s = zero<T>();
+            #pragma unroll
+            for (int l = i + 1; l < 64; ++l) s += L[i][l] * x[l];
+            x[i] = (i > j) ? zero<T>() : ((i == j) ? rd[i] : -(s * rd[i]));
         }
     }
-    __syncthreads();
-    if (lane < nb)
-        for (int jj = 0; jj < nb; ++jj) Wb[lane + jj * ldw] = X[lane][jj];
+    if (lane < nb) {
+        #pragma unroll
+        for (int i = 0; i < 64; ++i)
+            if (i < nb) Wb[i + (int64_t)j * ldw] = x[i];
+    }
 }
 
 //------------------------------------------------------------------------------
-// Cholesky of a small (n <= 64) diagonal block in LDS, lower or upper.
-// info (if non-null) receives info_offset + first failing column (1-based)
-// when *info is still 0.  The block's other triangle is not touched.
+// Cholesky of a small (n <= 64) diagonal block: one wave, lane i owns row i
+// of the lower factor in registers (left-looking, fully unrolled); row j's
+// finished entries are broadcast with v_readlane.  Upper is handled as the
+// conjugate transpose.  info (if non-null) receives info_offset + first
+// failing column (1-based) when *info is still 0.
 template <typename T>
-__global__ void potrf_small_kernel(char uplo, int n, T* A, int64_t lda, int* info, int info_offset) {
-    __shared__ T S[64][65];
-    __shared__ int fail;
-    const int tid = threadIdx.x, nthr = blockDim.x;
-    // load as lower (for upper, load the conjugate transpose)
-    for (int e = tid; e < n * n; e += nthr) {
-        int i = e % n, j = e / n;
-        if (i >= j) S[i][j] = uplo == 'L' ? A[i + (int64_t)j * lda] : conj(A[j + (int64_t)i * lda]);
+__global__ __launch_bounds__(64)
+void potrf_small_kernel(char uplo, int n, T* A, int64_t lda, int* info, int info_offset) {
+    const int i = threadIdx.x;
+    T a[64];
+    #pragma unroll
+    for (int l = 0; l < 64; ++l) {
+        T v = zero<T>();
+        if (i < n && l < n && i >= l)
+            v = (uplo == 'L') ? A[i + (int64_t)l * lda] : conj(A[l + (int64_t)i * lda]);
+        a[l] = v;
     }
-    if (tid == 0) fail = 0;
-    __syncthreads();
-    for (int j = 0; j < n; ++j) {
-        if (tid == 0) {
-            real_t<T> d = real(S[j][j]);
-            if (!(d > 0)) { fail = j + 1; }
-            else S[j][j] = make_val<T>(sqrt((double)d));
+    int fail = 0;
+    #pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        if (j < n) {
+            T s = a[j];
+            #pragma unroll
+            for (int l = 0; l < j; ++l) s -= a[l] * conj(bcast_lane(a[l], j));
+            real_t<T> d = real(bcast_lane(s, j));
+            if (!(d > real_t<T>(0)) && fail == 0) fail = j + 1;
+            real_t<T> sd = sqrt(d);
+            if (i == j) a[j] = make_val<T>((double)sd);
+            else if (i > j) a[j] = s * (real_t<T>(1) / sd);
         }
-        __syncthreads();
-        if (fail) break;
-        T djj = S[j][j];
-        for (int i = j + 1 + tid; i < n; i += nthr) S[i][j] = S[i][j] / djj;
-        __syncthreads();
-        int len = n - j - 1;
-        for (int e = tid; e < len * len; e += nthr) {
-            int i = j + 1 + e % len, c = j + 1 + e / len;
-            if (i >= c) S[i][c] -= S[i][j] * conj(S[c][j]);
-        }
-        __syncthreads();
     }
-    if (fail && info && tid == 0 && *info == 0) *info = info_offset + fail;
-    for (int e = tid; e < n * n; e += nthr) {
-        int i = e % n, j = e / n;
-        if (i >= j) {
-            if (uplo == 'L') A[i + (int64_t)j * lda] = S[i][j];
-            else A[j + (int64_t)i * lda] = conj(S[i][j]);
+    if (fail && info && i == 0 && *info == 0) *info = info_offset + fail;
+    if (i < n) {
+        #pragma unroll
+        for (int l = 0; l < 64; ++l) {
+            if (l <= i && l < n) {
+                if (uplo == 'L') A[i + (int64_t)l * lda] = a[l];
+                else A[l + (int64_t)i * lda] = conj(a[l]);
+            }
         }
     }
 }
@@ -337,7 +354,7 @@ void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t ld
 template <typename T>
 void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s) {
     if (n <= 0) return;
-    hipLaunchKernelGGL(potrf_small_kernel<T>, dim3(1), dim3(256), 0, s, uplo, n, A, lda, info, info_offset);
+    hipLaunchKernelGGL(potrf_small_kernel<T>, dim3(1), dim3(64), 0, s, uplo, n, A, lda, info, info_offset);
 }
 
 template <typename T>

@@ -313,6 +313,29 @@ void gemm_tri_real(char uplo, char transA, char transB, int64_t n, int64_t k,
 #undef SLATE_TRI_LAUNCH
 }
 
+// split-K reduction: C = alpha * sum_s P[s] + beta * C (P: splits x m x n, ld m)
+template <typename T>
+__global__ void splitk_reduce_kernel(int64_t m, int64_t n, int splits, const T* __restrict__ P, T alpha, T beta,
+                                     T* __restrict__ C, int64_t ldc) {
+    int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    int64_t j = blockIdx.y;
+    if (i >= m) return;
+    T s = 0;
+    const int64_t mn = m * n;
+    for (int b = 0; b < splits; ++b) s += P[b * mn + i + j * m];
+    T* c = C + i + j * ldc;
+    *c = (beta == T(0)) ? alpha * s : alpha * s + beta * (*c);
+}
+
+template <typename T>
+void splitk_reduce(int64_t m, int64_t n, int splits, const T* P, T alpha, T beta, T* C, int64_t ldc, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    dim3 grid((unsigned)((m + 255) / 256), (unsigned)n);
+    hipLaunchKernelGGL(splitk_reduce_kernel<T>, grid, dim3(256), 0, s, m, n, splits, P, alpha, beta, C, ldc);
+}
+template void splitk_reduce<double>(int64_t, int64_t, int, const double*, double, double, double*, int64_t, hipStream_t);
+template void splitk_reduce<float>(int64_t, int64_t, int, const float*, float, float, float*, int64_t, hipStream_t);
+
 template void gemm_tri_real<double>(char, char, char, int64_t, int64_t, double, const double*, int64_t,
                                     const double*, int64_t, double, double*, int64_t, hipStream_t);
 template void gemm_tri_real<float>(char, char, char, int64_t, int64_t, float, const float*, int64_t,

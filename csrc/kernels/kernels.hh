@@ -28,6 +28,8 @@ void gemm_tri_real(char uplo, char transA, char transB, int64_t n, int64_t k,
                    T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
                    T beta, T* C, int64_t ldc, hipStream_t stream);
 template <typename T>
+void splitk_reduce(int64_t m, int64_t n, int splits, const T* P, T alpha, T beta, T* C, int64_t ldc, hipStream_t s);
+template <typename T>
 void gemm_cplx(char uplo, char transA, char transB, int64_t m, int64_t n, int64_t k,
                T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
                T beta, T* C, int64_t ldc, hipStream_t stream);

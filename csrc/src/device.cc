@@ -14,6 +14,7 @@ struct State {
     std::mutex mtx;
     int device = -1;
     bool streams_ready = false;
+    int reserved_cus = 0;
     hipStream_t streams[kNumQueues] = {};
     std::vector<hipEvent_t> events;
     // caching allocator: bucket size -> free list; ptr -> bucket size
@@ -52,16 +53,48 @@ void ensure_streams_locked(State& s) {
     if (s.streams_ready) return;
     int lo = 0, hi = 0;
     slate_hip_call(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    // CU partitioning: the panel (1) and comm queues run on a reserved set of
+    // CUs so their many short kernels never queue behind the trailing update's
+    // long-running GEMM workgroups; the trailing update (kTrailQueue) runs on
+    // the rest; queue 0 and the lookahead queues (2..6) may use every CU.  SLATE_PANEL_CUS=0 disables it.
+    int ncu = 0;
+    {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, s.device) == hipSuccess) ncu = prop.multiProcessorCount;
+    }
+    int reserve = 32;
+    if (const char* e = std::getenv("SLATE_PANEL_CUS")) reserve = std::atoi(e);
+    if (ncu < 64) reserve = 0;
+    reserve = std::max(0, std::min(reserve, ncu / 2));
+    std::vector<uint32_t> mask_panel, mask_update;
+    if (reserve > 0) {
+        int words = (ncu + 31) / 32;
+        mask_panel.assign(words, 0);
+        mask_update.assign(words, 0);
+        // spread the reserved CUs evenly over the CU index space
+        int stride = ncu / reserve;
+        for (int c = 0; c < ncu; ++c) {
+            bool res = (c % stride == 0) && (c / stride < reserve);
+            (res ? mask_panel : mask_update)[c / 32] |= (1u << (c % 32));
+        }
+    }
+    s.reserved_cus = reserve;
     for (int i = 0; i < kNumQueues; ++i) {
-        // panel queue (1) gets the highest priority so panels preempt the
-        // trailing update; comm queue also high so broadcasts are not starved.
-        int prio = (i == 1 || i == kCommQueue) ? hi : lo;
-        slate_hip_call(hipStreamCreateWithPriority(&s.streams[i], hipStreamNonBlocking, prio));
+        bool panel = (i == 1 || i == kCommQueue);
+        if (reserve > 0 && (panel || i == kTrailQueue)) {
+            auto& m = panel ? mask_panel : mask_update;
+            slate_hip_call(hipExtStreamCreateWithCUMask(&s.streams[i], uint32_t(m.size() * 32), m.data()));
+        } else {
+            int prio = panel ? hi : lo;
+            slate_hip_call(hipStreamCreateWithPriority(&s.streams[i], hipStreamNonBlocking, prio));
+        }
     }
     s.streams_ready = true;
 }
 
 }  // namespace
+
+int reserved_cus() { return st().reserved_cus; }
 
 bool available() {
     int n = 0;

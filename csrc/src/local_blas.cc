@@ -100,6 +100,28 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
     if (m <= 0 || n <= 0) return;
     if constexpr (is_real_v<T>) {
         char ta = opA == Op::NoTrans ? 'N' : 'T', tb = opB == Op::NoTrans ? 'N' : 'T';
+        // split-K for small outputs with a long K (e.g. V^H C in QR panels):
+        // otherwise only a handful of 128x128 tiles would carry all the work
+        const int64_t tiles = ceildiv(m, 128) * ceildiv(n, 128);
+        if (uplo == 'G' && tiles < 128 && k >= 4096) {
+            int64_t splits = std::min<int64_t>(ceildiv(k, 1024), std::max<int64_t>(2, 512 / tiles));
+            int64_t kc = roundup(ceildiv(k, splits), 16);
+            splits = ceildiv(k, kc);
+            int64_t full = k / kc;                 // chunks of exactly kc
+            Scratch sc(Ctx{Target::Devices, s});
+            T* P = sc.alloc<T>(size_t(splits) * m * n);
+            int64_t sA = (ta == 'N') ? kc * lda : kc;
+            int64_t sB = (tb == 'N') ? kc : kc * ldb;
+            if (full > 0)
+                kd::gemm_real<T>(ta, tb, m, n, kc, T(1), A, lda, sA, B, ldb, sB, T(0), P, m, m * n, full, s);
+            if (full < splits) {
+                int64_t krem = k - full * kc;
+                kd::gemm_real<T>(ta, tb, m, n, krem, T(1), A + full * sA, lda, 0, B + full * sB, ldb, 0,
+                                 T(0), P + full * m * n, m, 0, 1, s);
+            }
+            kd::splitk_reduce<T>(m, n, int(splits), P, alpha, beta, C, ldc, s);
+            return;
+        }
         if (uplo == 'G') kd::gemm_real<T>(ta, tb, m, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, s);
         else {
             slate_assert(m == n);

@@ -61,7 +61,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         if (c0.dev()) device::memset_async(dinfo.data(), 0, sizeof(int), c0.stream);
         else dinfo.data()[0] = 0;
     }
-    const int64_t lookahead_queues = device::kNumQueues - 3;  // queues 2..6
+    const int64_t lookahead_queues = 5;  // queues 2..6
 
     for (int64_t k = 0; k < nt; ++k) {
         const int64_t kb = A.tileNb(k);
@@ -185,7 +185,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         if (jla_end < nt) {
             std::vector<int64_t> outs;
             for (int64_t j = jla_end; j < nt; ++j) outs.push_back(Sched::col(j));
-            S.task(0, {tBc}, outs, [&, update, jla_end](lb::Ctx const& c) { update(c, jla_end, nt); });
+            S.task(device::kTrailQueue, {tBc}, outs, [&, update, jla_end](lb::Ctx const& c) { update(c, jla_end, nt); });
         }
     }
     S.wait_all();

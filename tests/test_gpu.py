@@ -268,3 +268,19 @@ def test_gels_device():
     s.gels(A, B, target="d")
     x = s.to_numpy(B)[:n]
     assert relerr(x, np.linalg.lstsq(a, b, rcond=None)[0]) < 1e-12
+
+
+@pytest.mark.parametrize("ta", ["N", "T"])
+def test_gemm_splitk_kernel(ta):
+    """small output, long K -> split-K path"""
+    torch = _torch()
+    m, n, k = 200, 96, 20000
+    a = rnd(m, k, np.float64, 51) if ta == "N" else rnd(k, m, np.float64, 51)
+    b = rnd(k, n, np.float64, 52)
+    c = rnd(m, n, np.float64, 53)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
+    s.ops.gemm(ta, "N", 2.0, tA, tB, 0.5, tC)
+    opa = a if ta == "N" else a.T
+    assert relerr(tC.cpu().numpy().T, 2.0 * opa @ b + 0.5 * c) < 1e-12
