@@ -26,14 +26,17 @@
 namespace slate {
 namespace device {
 
-/// Number of streams ("queues") per process.  Index semantics follow the
-/// reference's queue indices (potrf.cc:66, getrf.cc:122: queue 0 = trailing
-/// update, 1 = panel, 2.. = lookahead columns) plus a dedicated comm stream.
-constexpr int kNumQueues = 9;
-constexpr int kCommQueue = 7;
-/// Trailing-update queue of the factorizations: runs on the CUs not reserved
-/// for the panel/comm queues (queue 0 keeps the whole device).
-constexpr int kTrailQueue = 8;
+/// Number of streams ("queues") per process: 0 = trailing update / default,
+/// 1 = panel (high priority), 2 = lookahead columns, 3 = communication.
+/// Exactly four, because HIP multiplexes streams onto GPU_MAX_HW_QUEUES
+/// (4 by default) in-order hardware queues: more streams would alias onto
+/// the same hardware queue and put panel kernels behind trailing GEMMs.
+/// (The reference uses 2..3+lookahead BLAS++ queues, potrf.cc:66.)
+constexpr int kNumQueues = 4;
+constexpr int kCommQueue = 3;
+constexpr int kLookaheadQueue = 2;
+/// Trailing-update queue of the factorizations.
+constexpr int kTrailQueue = 0;
 
 /// True iff a HIP device is visible to this process.
 bool available();

@@ -62,7 +62,7 @@ void ensure_streams_locked(State& s) {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, s.device) == hipSuccess) ncu = prop.multiProcessorCount;
     }
-    int reserve = 32;
+    int reserve = 0;
     if (const char* e = std::getenv("SLATE_PANEL_CUS")) reserve = std::atoi(e);
     if (ncu < 64) reserve = 0;
     reserve = std::max(0, std::min(reserve, ncu / 2));
@@ -79,10 +79,12 @@ void ensure_streams_locked(State& s) {
         }
     }
     s.reserved_cus = reserve;
+    int prio_unused = 0;
     for (int i = 0; i < kNumQueues; ++i) {
         bool panel = (i == 1 || i == kCommQueue);
-        if (reserve > 0 && (panel || i == kTrailQueue)) {
+        if (reserve > 0 && (panel || i == kTrailQueue || i == kLookaheadQueue)) {
             auto& m = panel ? mask_panel : mask_update;
+            (void)prio_unused;
             slate_hip_call(hipExtStreamCreateWithCUMask(&s.streams[i], uint32_t(m.size() * 32), m.data()));
         } else {
             int prio = panel ? hi : lo;

@@ -159,7 +159,6 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         else dinfo.data()[0] = 0;
     }
     int host_info = 0;
-    const int64_t lookahead_queues = 4;  // queues 2..5 (6: left pivoting)
     std::vector<RowPairs> host_pairs(kt);
 
     for (int64_t k = 0; k < kt; ++k) {
@@ -375,12 +374,12 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         };
         int64_t jla_end = std::min(nt, k + 1 + la);
         for (int64_t j = k + 1; j < jla_end; ++j)
-            range_tasks(2 + int((j - k - 1) % lookahead_queues), j, j + 1);
+            range_tasks(device::kLookaheadQueue, j, j + 1);
         if (jla_end < nt) range_tasks(device::kTrailQueue, jla_end, nt);
 
         // left columns [0, k): apply the step's interchanges (deferred queue)
         if (k > 0 && pivot) {
-            int lq = (p == 1) ? 6 : device::kCommQueue;
+            int lq = (p == 1) ? device::kTrailQueue : device::kCommQueue;
             S.task(lq, {tBc}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
                 auto [c0, c1] = lcols(0, k);
                 permute(c, c0, c1);

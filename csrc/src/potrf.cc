@@ -61,7 +61,6 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         if (c0.dev()) device::memset_async(dinfo.data(), 0, sizeof(int), c0.stream);
         else dinfo.data()[0] = 0;
     }
-    const int64_t lookahead_queues = 5;  // queues 2..6
 
     for (int64_t k = 0; k < nt; ++k) {
         const int64_t kb = A.tileNb(k);
@@ -179,7 +178,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         };
         int64_t jla_end = std::min(nt, k + 1 + la);
         for (int64_t j = k + 1; j < jla_end; ++j) {
-            int qi = 2 + int((j - k - 1) % lookahead_queues);
+            int qi = device::kLookaheadQueue;
             S.task(qi, {tBc}, {Sched::col(j)}, [&, update, j](lb::Ctx const& c) { update(c, j, j + 1); });
         }
         if (jla_end < nt) {

@@ -48,7 +48,6 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         WW2[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         Wtau[r].resize(target, size_t(nb));
     }
-    const int64_t lookahead_queues = 5;  // queues 2..6
     Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
 
     for (int64_t k = 0; k < kt; ++k) {
@@ -161,7 +160,7 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
             S.task(qq, {tB}, cols, [&, update, j0, j1](lb::Ctx const& c) { update(c, j0, j1); });
         };
         int64_t jla_end = std::min(nt, k + 1 + la);
-        for (int64_t j = k + 1; j < jla_end; ++j) range(2 + int((j - k - 1) % lookahead_queues), j, j + 1);
+        for (int64_t j = k + 1; j < jla_end; ++j) range(device::kLookaheadQueue, j, j + 1);
         if (jla_end < nt) range(device::kTrailQueue, jla_end, nt);
         (void)kd;
     }
