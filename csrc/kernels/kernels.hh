@@ -77,6 +77,19 @@ void lu_pivot(int nparts, const rt<T>* pval, const int64_t* pidx, int64_t r, int
 template <typename T>
 void lu_update(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, rt<T>* pval, int64_t* pidx,
                hipStream_t s);
+template <typename T>
+void lu_update2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, rt<T>* pval, int64_t* pidx,
+                 int scale_prev, hipStream_t s);
+template <typename T>
+void lu_scale_col(int64_t m, int64_t c, T* A, int64_t lda, hipStream_t s);
+template <typename T>
+void qr_dots2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, int nparts_norm, const rt<T>* psum,
+               const T* alpha_in, T* tau_out, T* scal_buf, T* pdots, int scale_prev, hipStream_t s);
+template <typename T>
+void qr_update2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, int nparts, const T* pdots,
+                 const T* tau_buf, const T* scal_buf, rt<T>* psum_next, T* alpha_next, hipStream_t s);
+template <typename T>
+void qr_scale_col(int64_t m, int64_t c, T* A, int64_t lda, const T* scal_buf, hipStream_t s);
 void iota(int64_t n, int64_t* p, hipStream_t s);
 void perm_pairs(int64_t k, const int64_t* perm, const int64_t* ipiv_local, int64_t* dst, int64_t* src, hipStream_t s);
 

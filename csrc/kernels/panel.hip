@@ -119,6 +119,53 @@ __global__ void lu_update_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, 
     }
 }
 
+// LU, 2-D parallel column step: grid.x = row blocks over [r, m),
+// grid.y = 1 + nc.  y = 0 applies the DEFERRED scaling of column c-1 (its
+// multipliers are only finalized here so that no block of step c-1 raced
+// with readers of the unscaled column); y = j >= 1 updates column c + j with
+// multipliers recomputed on the fly from the unscaled column c, and y = 1 also
+// produces the partial pivot search of column c + 1.
+template <typename T>
+__global__ void lu_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
+                                   real_t<T>* pval, int64_t* pidx, int scale_prev) {
+    using R = real_t<T>;
+    const int j = blockIdx.y;
+    const int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
+    if (j == 0) {
+        if (scale_prev && i < m) {
+            T d = A[(c - 1) + (c - 1) * lda];
+            T rd = is_zero(d) ? zero<T>() : one<T>() / d;
+            A[i + (c - 1) * lda] = A[i + (c - 1) * lda] * rd;
+        }
+        return;
+    }
+    const int64_t cc = c + j;
+    T d = A[r + c * lda];
+    T rd = is_zero(d) ? zero<T>() : one<T>() / d;
+    T u = A[r + cc * lda];
+    R v = -1; int64_t idx = INT64_MAX;
+    if (i > r && i < m) {
+        T l = A[i + c * lda] * rd;
+        T a = A[i + cc * lda] - l * u;
+        A[i + cc * lda] = a;
+        if (j == 1) { v = abs1(a); idx = i; }
+    }
+    if (j == 1) {
+        block_argmax(v, idx);
+        if (threadIdx.x == 0) { pval[blockIdx.x] = v; pidx[blockIdx.x] = idx; }
+    }
+}
+
+// scale rows (c, m) of column c by 1 / A[c, c]
+template <typename T>
+__global__ void lu_scale_col_kernel(int64_t m, int64_t c, T* A, int64_t lda) {
+    int64_t i = c + 1 + blockIdx.x * (int64_t)PT + threadIdx.x;
+    if (i >= m) return;
+    T d = A[c + c * lda];
+    T rd = is_zero(d) ? zero<T>() : one<T>() / d;
+    A[i + c * lda] = A[i + c * lda] * rd;
+}
+
 template <typename T>
 __global__ void iota_kernel(int64_t n, int64_t* p) {
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
@@ -270,6 +317,115 @@ __global__ void qr_update_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, 
 }
 
 //------------------------------------------------------------------------------
+// QR, 2-D parallel column step (grid.x = row blocks over [r, m), grid.y = 1+nc).
+// Every block reduces the norm partials and forms the reflector redundantly;
+// v is recomputed on the fly as x * scal (v_r = 1) so the stored column c is
+// scaled only in the NEXT step (y = 0 block), avoiding a race with readers.
+template <typename T>
+__device__ inline void qr_block_reflector(int nparts, const real_t<T>* psum, const T* alpha_in,
+                                          T& beta, T& tau, T& scal) {
+    using R = real_t<T>;
+    __shared__ R red[PT];
+    __shared__ T sh[3];
+    R s = 0;
+    for (int k = threadIdx.x; k < nparts; k += PT) s += psum[k];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        R t = 0;
+        for (int k = 0; k < PT; ++k) t += red[k];
+        T b, ta, sc;
+        make_reflector(*alpha_in, t, b, ta, sc);
+        sh[0] = b; sh[1] = ta; sh[2] = sc;
+    }
+    __syncthreads();
+    beta = sh[0]; tau = sh[1]; scal = sh[2];
+}
+
+template <typename T>
+__global__ void qr_dots2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
+                                 int nparts_norm, const real_t<T>* psum, const T* alpha_in,
+                                 T* tau_out, T* scal_buf, T* pdots, int scale_prev) {
+    using R = real_t<T>;
+    T beta, tau, scal;
+    qr_block_reflector(nparts_norm, psum, alpha_in, beta, tau, scal);
+    const int j = blockIdx.y;
+    const int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
+    if (j == 0) {
+        if (blockIdx.x == 0 && threadIdx.x == 0) { tau_out[c] = tau; scal_buf[c] = scal; A[r + c * lda] = beta; }
+        if (scale_prev && i < m) {
+            T sp = scal_buf[c - 1];
+            A[i + (c - 1) * lda] = A[i + (c - 1) * lda] * sp;   // rows >= r are below row c-1
+        }
+        return;
+    }
+    const int64_t cc = c + j;
+    T prod = zero<T>();
+    if (i < m) {
+        T v = (i == r) ? one<T>() : A[i + c * lda] * scal;
+        prod = conj(v) * A[i + cc * lda];
+    }
+    R pr = wave_sum(real(prod)), pim = wave_sum(imag(prod));
+    __shared__ R wr[PT / 64], wi[PT / 64];
+    if ((threadIdx.x & 63) == 0) { wr[threadIdx.x >> 6] = pr; wi[threadIdx.x >> 6] = pim; }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        R a = 0, b = 0;
+        for (int w = 0; w < PT / 64; ++w) { a += wr[w]; b += wi[w]; }
+        T t;
+        if constexpr (is_cplx<T>::value) t = T(a, b); else t = a;
+        pdots[(int64_t)blockIdx.x * 64 + (j - 1)] = t;
+    }
+}
+
+template <typename T>
+__global__ void qr_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
+                                   int nparts, const T* pdots, const T* tau_buf, const T* scal_buf,
+                                   real_t<T>* psum_next, T* alpha_next) {
+    using R = real_t<T>;
+    const int j = blockIdx.y + 1;
+    const int64_t cc = c + j;
+    __shared__ T zsh;
+    if (threadIdx.x == 0) {
+        T t = zero<T>();
+        for (int b = 0; b < nparts; ++b) t += pdots[(int64_t)b * 64 + (j - 1)];
+        zsh = conj(tau_buf[c]) * t;
+    }
+    __syncthreads();
+    const T z = zsh, scal = scal_buf[c];
+    const int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
+    R s = 0;
+    if (i < m) {
+        T v = (i == r) ? one<T>() : A[i + c * lda] * scal;
+        T a = A[i + cc * lda] - v * z;
+        A[i + cc * lda] = a;
+        if (j == 1) {
+            if (i > r + 1) s = real(a) * real(a) + imag(a) * imag(a);
+            if (i == r + 1) *alpha_next = a;
+        }
+    }
+    if (j == 1) {
+        s = wave_sum(s);
+        __shared__ R sh[PT / 64];
+        if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            R t = 0;
+            for (int k = 0; k < PT / 64; ++k) t += sh[k];
+            psum_next[blockIdx.x] = t;
+        }
+    }
+}
+
+// scale rows (c, m) of column c by scal_buf[c]
+template <typename T>
+__global__ void qr_scale_col_kernel(int64_t m, int64_t c, T* A, int64_t lda, const T* scal_buf) {
+    int64_t i = c + 1 + blockIdx.x * (int64_t)PT + threadIdx.x;
+    if (i >= m) return;
+    A[i + c * lda] = A[i + c * lda] * scal_buf[c];
+}
+
+//------------------------------------------------------------------------------
 // Tall-skinny inner product with split-K: P[b] = op(A)(k-chunk b)^op * B(k-chunk b)
 // C (m x n, small) = alpha * A^H B + beta C, A is K x m, B is K x n (both
 // column-major, K long).  Used for V^H V (larft) and V^H C on narrow panels.
@@ -375,6 +531,50 @@ void lu_update(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
     int g = (int)((rows + PT - 1) / PT);
     hipLaunchKernelGGL(lu_update_kernel<T>, dim3(g), dim3(PT), 0, s, m, r, c, cend, A, lda, pval, pidx);
 }
+template <typename T>
+void lu_update2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, rt<T>* pval, int64_t* pidx,
+                 int scale_prev, hipStream_t s) {
+    int64_t rows = m - r;
+    int64_t nc = cend - c - 1;
+    if (rows <= 0) return;
+    int g = (int)((rows + PT - 1) / PT);
+    hipLaunchKernelGGL(lu_update2d_kernel<T>, dim3(g, (unsigned)(1 + nc)), dim3(PT), 0, s, m, r, c, cend, A, lda,
+                       pval, pidx, scale_prev);
+}
+template <typename T>
+void lu_scale_col(int64_t m, int64_t c, T* A, int64_t lda, hipStream_t s) {
+    int64_t rows = m - c - 1;
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(lu_scale_col_kernel<T>, dim3((unsigned)((rows + PT - 1) / PT)), dim3(PT), 0, s, m, c, A, lda);
+}
+template <typename T>
+void qr_dots2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, int nparts_norm, const rt<T>* psum,
+               const T* alpha_in, T* tau_out, T* scal_buf, T* pdots, int scale_prev, hipStream_t s) {
+    int64_t rows = m - r;
+    if (rows <= 0) return;
+    int g = (int)((rows + PT - 1) / PT);
+    int64_t nc = cend - c - 1;
+    hipLaunchKernelGGL(qr_dots2d_kernel<T>, dim3(g, (unsigned)(1 + nc)), dim3(PT), 0, s, m, r, c, cend, A, lda,
+                       nparts_norm, psum, alpha_in, tau_out, scal_buf, pdots, scale_prev);
+}
+template <typename T>
+void qr_update2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, int nparts, const T* pdots,
+                 const T* tau_buf, const T* scal_buf, rt<T>* psum_next, T* alpha_next, hipStream_t s) {
+    int64_t rows = m - r;
+    int64_t nc = cend - c - 1;
+    if (rows <= 0 || nc <= 0) return;
+    int g = (int)((rows + PT - 1) / PT);
+    hipLaunchKernelGGL(qr_update2d_kernel<T>, dim3(g, (unsigned)nc), dim3(PT), 0, s, m, r, c, cend, A, lda,
+                       nparts, pdots, tau_buf, scal_buf, psum_next, alpha_next);
+}
+template <typename T>
+void qr_scale_col(int64_t m, int64_t c, T* A, int64_t lda, const T* scal_buf, hipStream_t s) {
+    int64_t rows = m - c - 1;
+    if (rows <= 0) return;
+    hipLaunchKernelGGL(qr_scale_col_kernel<T>, dim3((unsigned)((rows + PT - 1) / PT)), dim3(PT), 0, s, m, c, A, lda,
+                       scal_buf);
+}
+
 void iota(int64_t n, int64_t* p, hipStream_t s) {
     if (n <= 0) return;
     hipLaunchKernelGGL(iota_kernel<int>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, p);
@@ -433,7 +633,12 @@ void larft_small(int k, const T* tau, T* Tm, int64_t ldt, hipStream_t s) {
                                real_t<T>*, T*, int, hipStream_t);                                             \
     template void tsip<T>(int64_t, int, int, T, const T*, int64_t, const T*, int64_t, T, T*, int64_t, T*,    \
                           int64_t, hipStream_t);                                                               \
-    template void larft_small<T>(int, const T*, T*, int64_t, hipStream_t);
+    template void larft_small<T>(int, const T*, T*, int64_t, hipStream_t);                             \
+    template void lu_update2d<T>(int64_t, int64_t, int64_t, int64_t, T*, int64_t, rt<T>*, int64_t*, int, hipStream_t); \
+    template void lu_scale_col<T>(int64_t, int64_t, T*, int64_t, hipStream_t);                          \
+    template void qr_dots2d<T>(int64_t, int64_t, int64_t, int64_t, T*, int64_t, int, const rt<T>*, const T*, T*, T*, T*, int, hipStream_t); \
+    template void qr_update2d<T>(int64_t, int64_t, int64_t, int64_t, T*, int64_t, int, const T*, const T*, const T*, rt<T>*, T*, hipStream_t); \
+    template void qr_scale_col<T>(int64_t, int64_t, T*, int64_t, const T*, hipStream_t);
 
 SLATE_INST_PANEL(float)
 SLATE_INST_PANEL(double)

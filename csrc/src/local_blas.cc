@@ -426,13 +426,13 @@ struct LuPanelDev {
         if (pivot) kd::lu_colmax<DT>(m, c0, A, lda, c0, pval, pidx, nparts, s);
         for (int64_t j = 0; j < kmax; ++j) {
             int64_t col = c0 + j;
-            if (pivot)
-                kd::lu_pivot<DT>(nparts, pval, pidx, col, col, A, lda, ncols, ipiv, 0, perm, info, info_offset, nullptr, s);
-            else
-                kd::lu_pivot<DT>(0, pval, pidx, col, col, A, lda, ncols, ipiv, 0, perm, info, info_offset, nullptr, s);
-            kd::lu_update<DT>(m, col, col, c0 + nn, A, lda, pval, pidx, s);
-            nparts = int(ceildiv(m - col - 1, 256));
+            kd::lu_pivot<DT>(pivot ? nparts : 0, pval, pidx, col, col, A, lda, ncols, ipiv, 0, perm, info,
+                             info_offset, nullptr, s);
+            // update columns (col, c0+nn); deferred scaling of column col-1
+            kd::lu_update2d<DT>(m, col, col, c0 + nn, A, lda, pval, pidx, j > 0 ? 1 : 0, s);
+            nparts = int(ceildiv(m - col, 256));
         }
+        kd::lu_scale_col<DT>(m, c0 + kmax - 1, A, lda, s);
     }
 
     void rec(int64_t c0, int64_t nn) {
@@ -566,7 +566,7 @@ struct QrPanelDev {
     T* tau;
     T* Tm; int64_t ldt;
     Ctx ctx;
-    real_type<T>* psum; T* alpha; T* pdots; T* work; int64_t work_elems;
+    real_type<T>* psum; T* alpha; T* pdots; T* work; int64_t work_elems; T* scal;
 
     // narrow block [c0, c0+nn): Householder columns + T block (nn x nn at Tm[c0, c0])
     void narrow(int64_t c0, int64_t nn) {
@@ -579,12 +579,13 @@ struct QrPanelDev {
         for (int64_t j = 0; j < kmax; ++j) {
             int64_t col = c0 + j;
             int nblk = int(ceildiv(m - col, 256));
-            kd::qr_reflect_dots<DT>(m, col, col, c0 + nn, A, lda, nparts, psum, dptr(alpha), dptr(tau + col),
-                                    dptr(pdots), nblk, s);
-            kd::qr_update<DT>(m, col, col, c0 + nn, A, lda, nblk, dptr(pdots), dptr(tau + col), psum,
-                              dptr(alpha), nblk, s);
+            kd::qr_dots2d<DT>(m, col, col, c0 + nn, A, lda, nparts, psum, dptr(alpha), dptr(tau), dptr(scal),
+                              dptr(pdots), j > 0 ? 1 : 0, s);
+            kd::qr_update2d<DT>(m, col, col, c0 + nn, A, lda, nblk, dptr(pdots), dptr(tau), dptr(scal), psum,
+                                dptr(alpha), s);
             nparts = nblk;
         }
+        kd::qr_scale_col<DT>(m, c0 + kmax - 1, A, lda, dptr(scal), s);
         // T block: S = V^H V then larft recurrence
         Scratch sc(ctx);
         int64_t mv = m - c0;
@@ -645,6 +646,7 @@ void geqrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, T* tau, 
     P.psum = sc.alloc<real_type<T>>(np);
     P.alpha = sc.alloc<T>(2);
     P.pdots = sc.alloc<T>(size_t(np) * 64);
+    P.scal = sc.alloc<T>(size_t(k) + 1);
     P.work_elems = int64_t(1) << 20;
     P.work = sc.alloc<T>(P.work_elems);
     dset(c.stream, 'G', k, k, T(0), T(0), Tm, ldt);
