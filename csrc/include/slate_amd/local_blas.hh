@@ -98,10 +98,11 @@ void lauum(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda);
 /// (device or host int64 array, length min(m,n)) receives the panel-relative
 /// pivot row.  perm (length m) receives the resulting row permutation
 /// (row t of the result is row perm[t] of the input) when non-null.
-/// pivot=false gives LU without pivoting.
+/// pivot=false gives LU without pivoting; tournament=true selects the pivots
+/// of every 32-column narrow block by tournament (CALU) instead of per column.
 template <typename T>
 void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, int64_t* perm,
-                 int* info, int64_t info_offset, bool pivot = true);
+                 int* info, int64_t info_offset, bool pivot = true, bool tournament = false);
 
 /// Apply a row permutation produced by getrf_panel (perm over the first m
 /// rows, pivots ipiv[0..k)) to n columns of B.

@@ -154,17 +154,6 @@ __global__ void transpose_kernel(bool conjugate, int64_t m, int64_t n, const T* 
 }
 
 //------------------------------------------------------------------------------
-// Broadcast lane `src` of v to the whole wave (v_readlane; src is uniform).
-__device__ inline float  bcast_lane(float v, int src)  { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src)); }
-__device__ inline double bcast_lane(double v, int src) {
-    int2 t = __builtin_bit_cast(int2, v);
-    t.x = __builtin_amdgcn_readlane(t.x, src);
-    t.y = __builtin_amdgcn_readlane(t.y, src);
-    return __builtin_bit_cast(double, t);
-}
-template <typename R>
-__device__ inline cplx<R> bcast_lane(cplx<R> v, int src) { return cplx<R>(bcast_lane(v.re, src), bcast_lane(v.im, src)); }
-
 // Inverse of the diagonal nbs x nbs blocks of a triangular matrix (nbs <= 64).
 // Block b of A (at A + b*nbs*(1+lda)) is inverted into W (same position in W,
 // ld ldw); the full square block is written (zeros outside the triangle).

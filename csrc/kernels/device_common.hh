@@ -34,6 +34,18 @@ __device__ inline bool is_zero(float x) { return x == 0.f; }
 __device__ inline bool is_zero(double x) { return x == 0.0; }
 template <typename R> __device__ inline bool is_zero(cplx<R> x) { return x.re == R(0) && x.im == R(0); }
 
+// Broadcast lane `src` of v to the whole wave (v_readlane; src is uniform).
+__device__ inline float  bcast_lane(float v, int src)  { return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), src)); }
+__device__ inline double bcast_lane(double v, int src) {
+    int2 t = __builtin_bit_cast(int2, v);
+    t.x = __builtin_amdgcn_readlane(t.x, src);
+    t.y = __builtin_amdgcn_readlane(t.y, src);
+    return __builtin_bit_cast(double, t);
+}
+template <typename R>
+__device__ inline cplx<R> bcast_lane(cplx<R> v, int src) { return cplx<R>(bcast_lane(v.re, src), bcast_lane(v.im, src)); }
+
+
 // NaN-propagating max, as in the reference's max_nan (device_util.cuh)
 template <typename R>
 __device__ inline R max_nan(R x, R y) { return (isnan(y) || y >= x) ? y : x; }

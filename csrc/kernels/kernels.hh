@@ -91,6 +91,13 @@ void qr_update2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t ld
 template <typename T>
 void qr_scale_col(int64_t m, int64_t c, T* A, int64_t lda, const T* scal_buf, hipStream_t s);
 void iota(int64_t n, int64_t* p, hipStream_t s);
+/// Tournament-pivoted LU of the narrow block (columns at Ablk, nn <= 32) of a
+/// device panel: rows [r, m), row interchanges applied over ncols columns of
+/// Apanel; work holds tslu_workspace(m - r) int64 entries.
+int64_t tslu_workspace(int64_t rows);
+template <typename T>
+void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
+                 int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s);
 void perm_pairs(int64_t k, const int64_t* perm, const int64_t* ipiv_local, int64_t* dst, int64_t* src, hipStream_t s);
 
 template <typename T>

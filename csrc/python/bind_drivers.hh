@@ -200,7 +200,7 @@ void bind_drivers(py::module_& m, std::string const& s) {
         dsync(c);
         return h;
     });
-    DEF("lb_getrf_panel", [=](int64_t mm, int64_t n, uintptr_t A, int64_t lda) {
+    DEF("lb_getrf_panel", [=](int64_t mm, int64_t n, uintptr_t A, int64_t lda, bool tournament) {
         std::vector<int64_t> ipiv(std::min(mm, n));
         int h = 0;
         {
@@ -209,7 +209,7 @@ void bind_drivers(py::module_& m, std::string const& s) {
             device::Buffer<int> info(1);
             device::Buffer<int64_t> dpiv(ipiv.size() + 1), perm(mm + 1);
             device::memset_async(info.data(), 0, sizeof(int), c.stream);
-            lb::getrf_panel<T>(c, mm, n, (T*)A, lda, dpiv.data(), perm.data(), info.data(), 0, true);
+            lb::getrf_panel<T>(c, mm, n, (T*)A, lda, dpiv.data(), perm.data(), info.data(), 0, true, tournament);
             device::memcpy_async(ipiv.data(), dpiv.data(), ipiv.size() * sizeof(int64_t), c.stream);
             device::memcpy_async(&h, info.data(), sizeof(int), c.stream);
             dsync(c);

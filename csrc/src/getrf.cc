@@ -16,11 +16,10 @@
 //   U row: trsm on process row pk, broadcast down columns; trailing update
 //   A22 -= L21 U12 as one MFMA GEMM per process; lookahead columns on their
 //   own queues.
-// getrf_tntpiv (CALU) shares this driver: with p = 1 the tournament has a
-// single participant and is exactly this local panel; with p > 1 a one-level
-// tournament over the column's processes selects the pivot rows (local LU of
-// each process's rows picks nb candidates; the candidates are reduced by an
-// LU of the stacked blocks on the diagonal process), see panel_tournament().
+// getrf_tntpiv (CALU) shares this driver: its panel (gathered to the diagonal
+// process when p > 1) selects the pivots of every 32-column narrow block by a
+// tournament over 256-row leaves on the device (kernels/tslu.hip), then
+// factors that block without further pivoting.
 #include "internal.hh"
 #include "../kernels/kernels.hh"
 
@@ -139,6 +138,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     T* a = L.ptr;
     const int64_t lda = L.ld, mloc = L.m, nloc = L.n;
     const bool pivot = (mode != PanelMode::NoPiv);
+    const bool tnt = (mode == PanelMode::Tournament);
 
     Sched S(target);
     const int R = int(std::max<int64_t>(2, la + 2));
@@ -183,7 +183,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
                 S.task(1, {}, {Sched::col(k), tPanel}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pv_dst, pv_src](lb::Ctx const& c) {
                     trace::Block t2("getrf_panel");
                     T* ap = a + lr_k + lc_k * lda;
-                    lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot);
+                    lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot, tnt);
                     if (c.dev()) {
                         slate_amd::dev::perm_pairs(kd, perm.data(), pv_ipiv, pv_dst, pv_src, c.stream);
                     } else {
@@ -245,7 +245,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
                             off[r] += ib;
                         }
                         lb::getrf_panel(c, M, kb, full.data(), std::max<int64_t>(M, 1), pv_ipiv, nullptr,
-                                        dinfo.data(), kk, pivot);
+                                        dinfo.data(), kk, pivot, tnt);
                         // scatter back (same layout)
                         std::fill(off.begin(), off.end(), 0);
                         for (int64_t i = k; i < mt; ++i) {
@@ -331,21 +331,23 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         // columns of tiles [j0, j1) local to me
         auto lcols = [&](int64_t j0, int64_t j1) { return std::make_pair(lcol_of(A, j0), lcol_of(A, j1)); };
         T* WUk = WU[slot].data();
-        auto urow = [&, k, kb, lr_k, pk, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        // U row height is kd = tileMb(k) (< kb only for the last block row of a
+        // wide matrix; rows beyond it are not part of the matrix)
+        auto urow = [&, k, kd, lr_k, pk, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
             auto [c0, c1] = lcols(j0, j1);
             if (c1 <= c0) return;
             if (myrow == pk) {
-                // U(k, j0:j1) = L(k,k)^{-1} A(k, j0:j1); L(k,k) = top kb rows of W_k
-                lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kb, c1 - c0, T(1),
+                // U(k, j0:j1) = L(k,k)^{-1} A(k, j0:j1); L(k,k) = top kd rows of W_k
+                lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, c1 - c0, T(1),
                          Wk, std::max<int64_t>(mrows_k, 1), a + lr_k + c0 * lda, lda);
             }
         };
-        auto ubcast = [&, k, kb, lr_k, pk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        auto ubcast = [&, k, kb, kd, lr_k, pk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
             auto [c0, c1] = lcols(j0, j1);
             int64_t nc = c1 - c0;
             if (nc <= 0) return;
             T* dst = WUk + c0 * kb;
-            if (myrow == pk) lb::copy2d(c, kb, nc, a + lr_k + c0 * lda, lda, dst, kb);
+            if (myrow == pk) lb::copy2d(c, kd, nc, a + lr_k + c0 * lda, lda, dst, kb);
             if (p > 1) bcast(g.col(), dst, size_t(kb * nc), pk, c);
         };
         auto update = [&, k, kb, lr_k1, lr_k, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {

@@ -414,7 +414,8 @@ struct LuPanelDev {
     int64_t* ipiv; int64_t* perm;
     int* info; int64_t info_offset;
     real_type<T>* pval; int64_t* pidx;
-    bool pivot;
+    bool pivot, tournament;
+    int64_t* tws;
     Ctx ctx;
 
     void narrow(int64_t c0, int64_t nn) {
@@ -422,6 +423,10 @@ struct LuPanelDev {
         DT* A = dptr(A0);
         int64_t kmax = std::min(nn, m - c0);
         if (kmax <= 0) return;
+        if (tournament && pivot && m - c0 >= 2 * nn) {
+            kd::tslu_narrow<DT>(m, c0, int(kmax), A + c0 * lda, A, lda, ncols, ipiv, perm, info, info_offset, tws, s);
+            return;
+        }
         int nparts = int(ceildiv(m - c0, 256));
         if (pivot) kd::lu_colmax<DT>(m, c0, A, lda, c0, pval, pidx, nparts, s);
         for (int64_t j = 0; j < kmax; ++j) {
@@ -456,7 +461,7 @@ struct LuPanelDev {
 
 template <typename T>
 void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, int64_t* perm,
-                 int* info, int64_t info_offset, bool pivot) {
+                 int* info, int64_t info_offset, bool pivot, bool tournament) {
     if (m <= 0 || n <= 0) return;
     if (!c.dev()) {
         std::vector<int64_t> piv(std::min(m, n));
@@ -472,7 +477,8 @@ void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t*
     Scratch sc(c);
     LuPanelDev<T> P;
     P.s = c.stream; P.m = m; P.ncols = n; P.A0 = A; P.lda = lda; P.ipiv = ipiv; P.perm = perm;
-    P.info = info; P.info_offset = info_offset; P.pivot = pivot; P.ctx = c;
+    P.info = info; P.info_offset = info_offset; P.pivot = pivot; P.tournament = tournament; P.ctx = c;
+    P.tws = tournament ? sc.alloc<int64_t>(size_t(kd::tslu_workspace(m))) : nullptr;
     int64_t np = ceildiv(m, 256) + 1;
     P.pval = sc.alloc<real_type<T>>(np);
     P.pidx = sc.alloc<int64_t>(np);
@@ -649,7 +655,10 @@ void geqrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, T* tau, 
     P.scal = sc.alloc<T>(size_t(k) + 1);
     P.work_elems = int64_t(1) << 20;
     P.work = sc.alloc<T>(P.work_elems);
-    dset(c.stream, 'G', k, k, T(0), T(0), Tm, ldt);
+    // zero all of T (n x n when the panel is wider than tall: the driver's
+    // block update multiplies by the full nb x nb T)
+    int64_t nt_ = std::min(n, ldt);
+    dset(c.stream, 'G', nt_, nt_, T(0), T(0), Tm, ldt);
     P.rec(0, k);
     if (n > k) {
         // wide panel: apply Q^H to the remaining columns
@@ -803,7 +812,7 @@ void copy2d(Ctx const& c, int64_t m, int64_t n, T const* src, int64_t lds, T* ds
     template void trtri<T>(Ctx const&, Uplo, Diag, int64_t, T*, int64_t);                                 \
     template void trtri_to<T>(Ctx const&, Uplo, Diag, int64_t, T const*, int64_t, T*, int64_t);           \
     template void lauum<T>(Ctx const&, Uplo, int64_t, T*, int64_t);                                        \
-    template void getrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, int64_t*, int64_t*, int*, int64_t, bool); \
+    template void getrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, int64_t*, int64_t*, int*, int64_t, bool, bool); \
     template void apply_perm<T>(Ctx const&, int64_t, int64_t const*, int64_t const*, int64_t, T*, int64_t); \
     template void geqrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, T*, T*, int64_t);             \
     template void larfb<T>(Ctx const&, Side, Op, int64_t, int64_t, int64_t, T const*, int64_t, T const*, int64_t, T*, int64_t); \

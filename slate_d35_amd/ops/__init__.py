@@ -66,11 +66,12 @@ def potrf(uplo: str, A):
     return fn(uplo, n, pa, lda)
 
 
-def getrf_panel(A):
-    """LU with partial pivoting of a column-major m x n panel; returns (info, ipiv)."""
+def getrf_panel(A, tournament: bool = False):
+    """LU of a column-major m x n panel; returns (info, ipiv).  Partial pivoting
+    per column, or tournament (CALU) pivoting per 32-column block."""
     fn = getattr(_slate, f"lb_getrf_panel_{_suffix(A)}")
     pa, m, n, lda = _cm(A)
-    return fn(m, n, pa, lda)
+    return fn(m, n, pa, lda, tournament)
 
 
 def geqrf_panel(A):

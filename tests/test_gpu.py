@@ -133,6 +133,40 @@ def test_getrf_panel_kernel(m, n):
     assert ipiv[0] == int(np.argmax(np.abs(a[:, 0])))
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.complex128, np.float32])
+@pytest.mark.parametrize("m,n", [(1000, 64), (8192, 256), (3000, 100), (70000, 32), (300, 300)])
+def test_getrf_panel_tournament(m, n, dt):
+    """CALU panel: P A = L U with the pivots chosen by the device tournament;
+    |L| stays modest (tournament growth) and the factorization is exact."""
+    torch = _torch()
+    a = rnd(m, n, dt, 18)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    info, ipiv = s.ops.getrf_panel(tA, tournament=True)
+    f = tA.cpu().numpy().T
+    k = min(m, n)
+    L = np.tril(f[:, :k], -1) + np.eye(m, k)
+    U = np.triu(f[:k, :])
+    pa = a.copy()
+    for j, p in enumerate(ipiv):
+        pa[[j, p]] = pa[[p, j]]
+    assert info == 0
+    tol = 1e-4 if dt == np.float32 else 1e-12
+    assert relerr(L @ U, pa) < tol
+    assert np.abs(L).max() < 8.0
+    # first pivot is still the column's absolute maximum (the tournament's
+    # first round at every node is a plain max search)
+    assert ipiv[0] == int(np.argmax(np.abs(a[:, 0].real) + np.abs(a[:, 0].imag)))
+
+
+def test_getrf_panel_tournament_singular():
+    torch = _torch()
+    a = rnd(2000, 64, np.float64, 19)
+    a[:, 5] = 0.0
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    info, _ = s.ops.getrf_panel(tA, tournament=True)
+    assert info == 6
+
+
 @pytest.mark.parametrize("m,n", [(1000, 64), (2048, 256), (500, 100)])
 def test_geqrf_panel_kernel(m, n):
     torch = _torch()
