@@ -54,20 +54,40 @@ __device__ inline R max_nan(R x, R y) { return (isnan(y) || y >= x) ? y : x; }
 // Wavefront helpers (64 lanes).
 constexpr int kWave = 64;
 
+// DPP lane moves (32-bit granules; 64-bit values move as two halves).
+template <int CTRL>
+__device__ inline int dpp_i(int x) { return __builtin_amdgcn_update_dpp(x, x, CTRL, 0xF, 0xF, false); }
+template <int CTRL>
+__device__ inline float dpp_r(float x) { return __builtin_bit_cast(float, dpp_i<CTRL>(__builtin_bit_cast(int, x))); }
+template <int CTRL>
+__device__ inline double dpp_r(double x) {
+    int2 t = __builtin_bit_cast(int2, x);
+    t.x = dpp_i<CTRL>(t.x);
+    t.y = dpp_i<CTRL>(t.y);
+    return __builtin_bit_cast(double, t);
+}
+
+// Wave reductions: DPP butterflies inside each 16-lane row (quad_perm
+// [1,0,3,2], [2,3,0,1], row_ror:4, row_ror:8), then v_readlane of the four
+// row results.  No LDS traffic; the result is wave-uniform.
+template <typename R, typename Op>
+__device__ inline R wave_reduce(R v, Op op) {
+    v = op(v, dpp_r<0xB1>(v));
+    v = op(v, dpp_r<0x4E>(v));
+    v = op(v, dpp_r<0x124>(v));
+    v = op(v, dpp_r<0x128>(v));
+    R r0 = bcast_lane(v, 0), r1 = bcast_lane(v, 16), r2 = bcast_lane(v, 32), r3 = bcast_lane(v, 48);
+    return op(op(r0, r1), op(r2, r3));
+}
+
 template <typename R>
 __device__ inline R wave_sum(R v) {
-    #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-        v += __shfl_xor(v, off, 64);
-    return v;
+    return wave_reduce(v, [](R a, R b) { return a + b; });
 }
 
 template <typename R>
 __device__ inline R wave_max_nan(R v) {
-    #pragma unroll
-    for (int off = 32; off > 0; off >>= 1)
-        v = max_nan(v, __shfl_xor(v, off, 64));
-    return v;
+    return wave_reduce(v, [](R a, R b) { return max_nan(a, b); });
 }
 
 //------------------------------------------------------------------------------

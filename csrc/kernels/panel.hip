@@ -325,15 +325,17 @@ template <typename T>
 __device__ inline void qr_block_reflector(int nparts, const real_t<T>* psum, const T* alpha_in,
                                           T& beta, T& tau, T& scal) {
     using R = real_t<T>;
-    __shared__ R red[PT];
+    __shared__ R red[PT / 64];
     __shared__ T sh[3];
     R s = 0;
     for (int k = threadIdx.x; k < nparts; k += PT) s += psum[k];
-    red[threadIdx.x] = s;
+    s = wave_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
     if (threadIdx.x == 0) {
         R t = 0;
-        for (int k = 0; k < PT; ++k) t += red[k];
+        #pragma unroll
+        for (int k = 0; k < PT / 64; ++k) t += red[k];
         T b, ta, sc;
         make_reflector(*alpha_in, t, b, ta, sc);
         sh[0] = b; sh[1] = ta; sh[2] = sc;
@@ -386,10 +388,20 @@ __global__ void qr_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend
     const int j = blockIdx.y + 1;
     const int64_t cc = c + j;
     __shared__ T zsh;
-    if (threadIdx.x == 0) {
-        T t = zero<T>();
-        for (int b = 0; b < nparts; ++b) t += pdots[(int64_t)b * 64 + (j - 1)];
-        zsh = conj(tau_buf[c]) * t;
+    if (threadIdx.x < 64) {
+        // wave 0 reduces this column's dot partials (lane-strided, DPP sum)
+        R tr = 0, ti = 0;
+        for (int b = threadIdx.x; b < nparts; b += 64) {
+            T t = pdots[(int64_t)b * 64 + (j - 1)];
+            tr += real(t); ti += imag(t);
+        }
+        tr = wave_sum(tr);
+        if constexpr (is_cplx<T>::value) ti = wave_sum(ti);
+        if (threadIdx.x == 0) {
+            T t;
+            if constexpr (is_cplx<T>::value) t = T(tr, ti); else t = tr;
+            zsh = conj(tau_buf[c]) * t;
+        }
     }
     __syncthreads();
     const T z = zsh, scal = scal_buf[c];

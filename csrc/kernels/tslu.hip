@@ -8,54 +8,84 @@
 //
 // MI355X design: the tournament is played on a 32-column narrow block inside
 // the recursive device panel (local_blas.cc LuPanelDev), so a 32768-row panel
-// costs a handful of launches instead of two launches per column:
-//   select (leaves: 256 rows per workgroup, one row per lane, rows held in
-//          VGPRs; GEPP with wave argmax + LDS broadcast of the pivot row)
-//   select (tree nodes: fan-in 8 -> 8*32 = 256 candidate rows per workgroup)
-//   pivots (one wave: turn the winners into LAPACK ipiv + a (dst,src) row
-//           permutation, wave-parallel with ballot/readlane)
-//   permute_rows (aux.hip) over the whole panel width
-//   top    (top 32x32 block LU without pivoting in one wave via readlane)
-//   rows   (L21 = A21 U11^{-1}, one row per lane with U11 in LDS)
+// costs four or five launches instead of two launches per column:
+//   select  leaves: 256 rows per workgroup, one row per lane held in VGPRs;
+//           GEPP with a DPP (quad_perm/row_ror) + v_readlane wave argmax and
+//           an LDS broadcast of the pivot row.
+//   select  tree nodes: 512-lane workgroups, fan-in 16 (16 x 32 candidates).
+//   permute each workgroup owns panel columns; it re-derives the interchanges
+//           from the winners in one wave (ballot/readlane, all scalar), applies
+//           the net row permutation to its columns and copies the permuted
+//           top block of the narrow block to a scratch buffer.
+//   rows    wave 0 factors the top 32x32 block (lane = row, v_readlane
+//           broadcasts) and inverts U11; then L21 = A21 * U11^{-1} runs on
+//           v_mfma_f64_16x16x4 for fp64, 16-row slabs per wave.
 #include "device_common.hh"
 #include "kernels.hh"
+
+#include <climits>
+#include <type_traits>
 
 namespace slate_amd {
 namespace dev {
 
 namespace {
 
-constexpr int TW = 32;    // tournament / narrow-block width
-constexpr int TR = 256;   // rows per workgroup
-constexpr int FANIN = TR / TW;
+constexpr int TW = 32;        // tournament / narrow-block width
+constexpr int TR = 256;       // leaf rows per workgroup
+constexpr int NODE_NT = 512;  // node workgroup size
+constexpr int FANIN = NODE_NT / TW;
 
 template <typename R>
-__device__ inline void argmax_pick(R& v, int64_t& idx, R ov, int64_t oi) {
+__device__ inline void argmax_pick(R& v, int& idx, R ov, int oi) {
     // max |v|; ties -> smaller row index (deterministic, LAPACK-like)
     if (ov > v || (ov == v && oi < idx) || (isnan(ov) && !isnan(v))) { v = ov; idx = oi; }
 }
 
-// One tournament round: each workgroup factors up to 256 rows x nn columns with
+template <int CTRL, typename R>
+__device__ inline void argmax_dpp(R& v, int& id) {
+    R ov = dpp_r<CTRL>(v);
+    int oi = dpp_i<CTRL>(id);
+    argmax_pick(v, id, ov, oi);
+}
+
+// Wave-uniform argmax: DPP within rows of 16 lanes, then v_readlane of the
+// four row results (no LDS, no ds_bpermute).
+template <typename R>
+__device__ inline void wave_argmax(R& v, int& id) {
+    argmax_dpp<0xB1>(v, id);    // quad_perm [1,0,3,2]
+    argmax_dpp<0x4E>(v, id);    // quad_perm [2,3,0,1]
+    argmax_dpp<0x124>(v, id);   // row_ror:4
+    argmax_dpp<0x128>(v, id);   // row_ror:8
+    R bv = bcast_lane(v, 0);
+    int bi = __builtin_amdgcn_readlane(id, 0);
+    #pragma unroll
+    for (int q = 1; q < 4; ++q) argmax_pick(bv, bi, bcast_lane(v, 16 * q), __builtin_amdgcn_readlane(id, 16 * q));
+    v = bv; id = bi;
+}
+
+// One tournament round: each workgroup factors up to NT rows x nn columns with
 // partial pivoting and emits its (up to nn) pivot rows, in pivot order.
-// Leaves (cand_in == nullptr) take rows [r + 256*b, ...); nodes take the
-// candidate lists of FANIN children.  Rows are read from the unmodified panel
+// Leaves (cand_in == nullptr) take rows [r + NT*b, ...); nodes take the
+// candidate lists of NT/TW children.  Rows are read from the unmodified panel
 // (CALU plays every round on original rows).
-template <typename T>
-__global__ __launch_bounds__(TR) void tslu_select_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
-                                                         const int64_t* cand_in, const int* cnt_in, int nin,
-                                                         int64_t* cand_out, int* cnt_out) {
+template <typename T, int NT>
+__global__ __launch_bounds__(NT) void tslu_select_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
+                                                         const int* cand_in, const int* cnt_in, int nin,
+                                                         int* cand_out, int* cnt_out) {
     using R = real_t<T>;
-    __shared__ R sv[2][TR / 64];
-    __shared__ int64_t si[2][TR / 64];
+    constexpr int NW = NT / 64;
+    __shared__ R sv[2][NW];
+    __shared__ int si[2][NW];
     __shared__ T prow[2][TW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    int64_t idx = -1;
+    int idx = INT_MAX;
     bool act = false;
     if (cand_in == nullptr) {
-        int64_t i = r + blockIdx.x * (int64_t)TR + tid;
-        if (i < m) { idx = i; act = true; }
+        int64_t i = r + blockIdx.x * (int64_t)NT + tid;
+        if (i < m) { idx = (int)i; act = true; }
     } else {
-        int child = blockIdx.x * FANIN + tid / TW, k = tid % TW;
+        int child = blockIdx.x * (NT / TW) + tid / TW, k = tid % TW;
         if (child < nin && k < cnt_in[child]) { idx = cand_in[child * TW + k]; act = true; }
     }
     T a[TW];
@@ -69,19 +99,14 @@ __global__ __launch_bounds__(TR) void tslu_select_kernel(int64_t m, int64_t r, i
     for (int k = 0; k < TW; ++k) {
         if (k < nn && !done) {
             R v = act ? abs1(a[k]) : R(-1);
-            int64_t id = act ? idx : INT64_MAX;
-            #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) {
-                R ov = __shfl_xor(v, off, 64);
-                int64_t oi = __shfl_xor(id, off, 64);
-                argmax_pick(v, id, ov, oi);
-            }
+            int id = act ? idx : INT_MAX;
+            wave_argmax(v, id);
             if (lane == 0) { sv[k & 1][w] = v; si[k & 1][w] = id; }
             __syncthreads();
             v = sv[k & 1][0]; id = si[k & 1][0];
             #pragma unroll
-            for (int q = 1; q < TR / 64; ++q) argmax_pick(v, id, sv[k & 1][q], si[k & 1][q]);
-            if (id == INT64_MAX) {
+            for (int q = 1; q < NW; ++q) argmax_pick(v, id, sv[k & 1][q], si[k & 1][q]);
+            if (id == INT_MAX) {
                 done = true;                       // uniform: no candidates left
             } else {
                 if (act && idx == id) {
@@ -105,52 +130,87 @@ __global__ __launch_bounds__(TR) void tslu_select_kernel(int64_t m, int64_t r, i
 }
 
 // Winners -> LAPACK ipiv (sequential interchanges with row r+k) and the net
-// row permutation as (dst, src) pairs.  One wave: lanes 0..31 track positions
-// r..r+31, lanes 32..63 the winners that lie below; interchanges are swaps of
-// the `orig` register between two lanes.
-template <typename T>
-__global__ __launch_bounds__(64) void tslu_pivots_kernel(int64_t r, const int64_t* win, const int* wcnt,
-                                                         int64_t* ipiv, int64_t* perm,
-                                                         int64_t* pdst, int64_t* psrc, int* npairs) {
-    const int l = threadIdx.x;
-    const int cnt = *wcnt;
-    int64_t wl = (l & 31) < cnt ? win[l & 31] : -1;
-    int64_t pos = -1;
+// row permutation as (pos <- orig).  One wave: lanes 0..31 track positions
+// r..r+31, lanes 32..63 the winners that lie below; an interchange swaps the
+// `orig` register of two lanes.  Every index is wave-uniform (v_readlane).
+// Returns true in lanes whose position receives a different row.
+__device__ inline bool tslu_interchanges(int r, const int* win, int cnt, int64_t* ipiv, int& pos, int& orig) {
+    const int l = threadIdx.x & 63;
+    int wl = (l & 31) < cnt ? win[l & 31] : -1;
+    pos = -1;
     if (l < 32) { if (l < cnt) pos = r + l; }
     else if (l - 32 < cnt && wl >= r + cnt) pos = wl;
-    int64_t orig = pos;
+    orig = pos;
     for (int k = 0; k < cnt; ++k) {
-        int64_t wk = __shfl(wl, k, 64);
+        int wk = __builtin_amdgcn_readlane(wl, k);
         unsigned long long bal = __ballot(pos >= 0 && orig == wk);
         int ql = __ffsll(bal) - 1;
-        int64_t q = __shfl(pos, ql, 64);
-        if (l == 0) ipiv[r + k] = q;
-        int64_t ok = __shfl(orig, k, 64), oq = __shfl(orig, ql, 64);
+        int q = __builtin_amdgcn_readlane(pos, ql);
+        if (ipiv && l == 0) ipiv[r + k] = q;
+        int ok = __builtin_amdgcn_readlane(orig, k), oq = __builtin_amdgcn_readlane(orig, ql);
         if (l == ql) orig = ok;
         if (l == k) orig = oq;
     }
-    bool mv = pos >= 0 && pos != orig;
-    unsigned long long bal = __ballot(mv);
-    int slot = __popcll(bal & ((1ull << l) - 1));
-    int64_t pv = (mv && perm) ? perm[orig] : 0;
-    if (mv) {
-        pdst[slot] = pos; psrc[slot] = orig;
-        if (perm) perm[pos] = pv;
-    }
-    if (l == 0) *npairs = __popcll(bal);
+    return pos >= 0 && pos != orig;
 }
 
-// After the winners were permuted to rows r..r+nn-1: factor the top nn x nn
-// block in place without pivoting (one wave, lane i = row r+i, pivot-row
-// entries broadcast with v_readlane) and publish U11 + 1/diag to Uws.
+// Apply the tournament's row permutation to panel columns [0, ncols) (a
+// column per wave), record ipiv/perm (workgroup 0), and copy the permuted top
+// block of the narrow block (columns [c0, c0+nn)) to Utop (column-major, ld TW).
 template <typename T>
-__global__ __launch_bounds__(64) void tslu_top_kernel(int64_t r, int nn, T* A, int64_t lda, T* Uws,
-                                                      int* info, int64_t info_offset) {
+__global__ __launch_bounds__(256) void tslu_permute_kernel(int r, int nn, int64_t c0, T* A, int64_t lda,
+                                                           int64_t ncols, const int* win, const int* wcnt,
+                                                           int64_t* ipiv, int64_t* perm, T* Utop) {
+    __shared__ int s_dst[64], s_src[64], s_top[TW];
+    __shared__ int s_np;
     const int tid = threadIdx.x;
-    T a[TW];
-    bool live = tid < nn;
+    const int cnt = *wcnt;
+    if (tid < 64) {
+        int pos, orig;
+        bool mv = tslu_interchanges(r, win, cnt, blockIdx.x == 0 ? ipiv : nullptr, pos, orig);
+        unsigned long long bal = __ballot(mv);
+        int slot = __popcll(bal & ((1ull << tid) - 1));
+        if (mv) { s_dst[slot] = pos; s_src[slot] = orig; }
+        if (tid == 0) s_np = __popcll(bal);
+        // source row of each top position r + p
+        if (tid < 32 && tid < cnt) s_top[tid] = orig;
+        if (blockIdx.x == 0 && perm) {
+            int64_t pv = mv ? perm[orig] : 0;
+            if (mv) perm[pos] = pv;
+        }
+    }
+    __syncthreads();
+    const int np = s_np;
+    const int p = tid & 63;
+    for (int64_t j = blockIdx.x * 4 + (tid >> 6); j < ncols; j += (int64_t)gridDim.x * 4) {
+        T* col = A + j * lda;
+        T v = zero<T>(), u = zero<T>();
+        const bool top = (j >= c0 && j < c0 + nn && p < nn);
+        if (p < np) v = col[s_src[p]];
+        if (top) u = col[s_top[p]];
+        __builtin_amdgcn_wave_barrier();
+        if (p < np) col[s_dst[p]] = v;
+        if (top) Utop[(j - c0) * TW + p] = u;
+    }
+}
+
+__device__ inline void mfma16(double a, double b, double (&c)[4]) {
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    v4d acc = {c[0], c[1], c[2], c[3]};
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    c[0] = acc[0]; c[1] = acc[1]; c[2] = acc[2]; c[3] = acc[3];
+}
+
+// Top block LU without pivoting (one wave; lane i = row i, readlane
+// broadcasts) and column-oriented inverse of U11 (lane j = column j of
+// U11^{-1}, back substitution).  Writes Uinv[i*TW + j] (zero outside the nn x
+// nn triangle); returns the first zero pivot (or -1).
+template <typename T>
+__device__ inline int tslu_top_factor(int nn, const T* Utop, T (&a)[TW], T* Uinv) {
+    const int tid = threadIdx.x & 63;
+    const bool live = tid < nn;
     #pragma unroll
-    for (int j = 0; j < TW; ++j) a[j] = (live && j < nn) ? A[r + tid + j * lda] : zero<T>();
+    for (int j = 0; j < TW; ++j) a[j] = (live && j < nn) ? Utop[j * TW + tid] : zero<T>();
     int bad = -1;
     #pragma unroll
     for (int k = 0; k < TW; ++k) {
@@ -158,7 +218,6 @@ __global__ __launch_bounds__(64) void tslu_top_kernel(int64_t r, int nn, T* A, i
             T d = bcast_lane(a[k], k);
             if (is_zero(d) && bad < 0) bad = k;
             T rd = is_zero(d) ? zero<T>() : one<T>() / d;
-            if (tid == 0) Uws[TW * TW + k] = rd;
             T lk = a[k] * rd;
             #pragma unroll
             for (int j = k + 1; j < TW; ++j) {
@@ -168,61 +227,107 @@ __global__ __launch_bounds__(64) void tslu_top_kernel(int64_t r, int nn, T* A, i
             if (tid > k) a[k] = lk;
         }
     }
-    if (live) {
-        #pragma unroll
-        for (int j = 0; j < TW; ++j) {
-            Uws[tid * TW + j] = a[j];
-            if (j < nn) A[r + tid + j * lda] = a[j];
+    T x[TW];
+    #pragma unroll
+    for (int i = TW - 1; i >= 0; --i) {
+        x[i] = zero<T>();
+        if (i < nn) {
+            T s = (i == tid) ? one<T>() : zero<T>();
+            #pragma unroll
+            for (int k = i + 1; k < TW; ++k)
+                if (k < nn) s -= bcast_lane(a[k], i) * x[k];
+            T d = bcast_lane(a[i], i);
+            x[i] = is_zero(d) ? zero<T>() : s / d;
         }
     }
-    if (tid == 0 && bad >= 0 && info && *info == 0) *info = (int)(info_offset + r + bad + 1);
+    if (tid < TW) {
+        #pragma unroll
+        for (int i = 0; i < TW; ++i) Uinv[i * TW + tid] = x[i];
+    }
+    return bad;
 }
 
-// L21 = A21 U11^{-1}: one row per lane, forward substitution against U11 in LDS.
+// L21 = A21 U11^{-1} for rows [r+nn, m); workgroup 0 also stores the factored
+// top block and the info flag.  256 threads = 4 waves x 4 slabs of 16 rows.
 template <typename T>
-__global__ __launch_bounds__(TR) void tslu_rows_kernel(int64_t m, int64_t r, int nn, T* A, int64_t lda,
-                                                       const T* Uws) {
-    __shared__ T U[TW][TW];
-    __shared__ T rdiag[TW];
-    const int tid = threadIdx.x;
-    for (int e = tid; e < TW * TW; e += TR) {
-        int k = e / TW, j = e % TW;
-        U[k][j] = (k < nn && j > k && j < nn) ? Uws[k * TW + j] : zero<T>();
-    }
-    if (tid < TW) rdiag[tid] = tid < nn ? Uws[TW * TW + tid] : zero<T>();
-    __syncthreads();
-    int64_t i = r + nn + blockIdx.x * (int64_t)TR + tid;
-    if (i >= m) return;
-    T a[TW];
-    #pragma unroll
-    for (int j = 0; j < TW; ++j) a[j] = j < nn ? A[i + j * lda] : zero<T>();
-    // k is a runtime loop (a fully unrolled 32x32 triangle makes the compiler
-    // hoist ~500 LDS loads and spill); a[k] is picked with a select chain.
-    #pragma unroll 1
-    for (int k = 0; k < nn; ++k) {
-        T ak = a[0];
-        #pragma unroll
-        for (int j = 1; j < TW; ++j) ak = (j == k) ? a[j] : ak;
-        T lk = ak * rdiag[k];
-        #pragma unroll
-        for (int j = 0; j < TW; ++j) {
-            T u = U[k][j];                           // zero for j <= k
-            a[j] = (j == k) ? lk : a[j] - lk * u;
+__global__ __launch_bounds__(256) void tslu_rows_kernel(int64_t m, int64_t r, int nn, T* A, int64_t lda,
+                                                        const T* Utop, int* info, int64_t info_offset) {
+    __shared__ T Uinv[TW * TW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    if (w == 0) {
+        T a[TW];
+        int bad = tslu_top_factor<T>(nn, Utop, a, Uinv);
+        if (blockIdx.x == 0) {
+            if (lane < nn) {
+                #pragma unroll
+                for (int j = 0; j < TW; ++j) if (j < nn) A[r + lane + j * lda] = a[j];
+            }
+            if (lane == 0 && bad >= 0 && info && *info == 0) *info = (int)(info_offset + r + bad + 1);
         }
     }
-    #pragma unroll
-    for (int j = 0; j < TW; ++j) if (j < nn) A[i + j * lda] = a[j];
+    __syncthreads();
+    const int64_t base = r + nn + blockIdx.x * (int64_t)256;
+    if constexpr (std::is_same<T, double>::value) {
+        // swapped operands: MFMA A-op = Uinv[k0 + (lane>>4)][n0 + (lane&15)],
+        // B-op = A21[row0 + (lane&15)][k0 + (lane>>4)]; D[n][m] comes back with
+        // lane&15 = row, (lane>>4) + 4*reg = column.
+        double ub[TW / 4][2];
+        #pragma unroll
+        for (int ks = 0; ks < TW / 4; ++ks)
+            #pragma unroll
+            for (int nt = 0; nt < 2; ++nt) ub[ks][nt] = Uinv[(ks * 4 + (lane >> 4)) * TW + nt * 16 + (lane & 15)];
+        #pragma unroll
+        for (int sl = 0; sl < 4; ++sl) {
+            const int64_t row = base + (w * 4 + sl) * 16 + (lane & 15);
+            const bool ok = row < m;
+            double av[TW / 4];
+            #pragma unroll
+            for (int ks = 0; ks < TW / 4; ++ks) {
+                int col = ks * 4 + (lane >> 4);
+                av[ks] = (ok && col < nn) ? A[row + col * lda] : 0.0;
+            }
+            double c0[4] = {0, 0, 0, 0}, c1[4] = {0, 0, 0, 0};
+            #pragma unroll
+            for (int ks = 0; ks < TW / 4; ++ks) {
+                mfma16(ub[ks][0], av[ks], c0);
+                mfma16(ub[ks][1], av[ks], c1);
+            }
+            if (ok) {
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    int col0 = (lane >> 4) + 4 * q, col1 = 16 + col0;
+                    if (col0 < nn) A[row + col0 * lda] = c0[q];
+                    if (col1 < nn) A[row + col1 * lda] = c1[q];
+                }
+            }
+        }
+    } else {
+        // float / complex: one row per thread, FMAs against Uinv in LDS
+        const int64_t row = base + tid;
+        if (row < m) {
+            T av[TW];
+            #pragma unroll
+            for (int k = 0; k < TW; ++k) av[k] = k < nn ? A[row + k * lda] : zero<T>();
+            #pragma unroll 1
+            for (int j = 0; j < nn; ++j) {
+                T s = zero<T>();
+                #pragma unroll
+                for (int k = 0; k < TW; ++k) s += av[k] * Uinv[k * TW + j];
+                A[row + j * lda] = s;
+            }
+        }
+    }
 }
 
 }  // namespace
 
-// U11 + 1/diag (up to 16-byte scalars) first, then candidate ping-pong
-// buffers, counts and the (dst, src) pairs; in int64 units.
-constexpr int64_t kUwsI64 = 2 * TW * (TW + 1);
+// Utop scratch (TW x TW, up to 16-byte scalars) first, then the candidate
+// ping-pong buffers and counts (int); sizes in int64 units.
+constexpr int64_t kUtopI64 = 2 * TW * TW;
 
 int64_t tslu_workspace(int64_t rows) {
     int64_t nleaf = (rows + TR - 1) / TR;
-    return kUwsI64 + 2 * nleaf * TW + nleaf + 2 + 2 * 2 * TW + 1;
+    return kUtopI64 + nleaf * TW + nleaf + 64;
 }
 
 template <typename T>
@@ -231,32 +336,29 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
     int nleaf = (int)((rows + TR - 1) / TR);
-    T* Uws = reinterpret_cast<T*>(work);
-    int64_t* candA = work + kUwsI64;
-    int64_t* candB = candA + (int64_t)nleaf * TW;
-    int* cntA = reinterpret_cast<int*>(candB + (int64_t)nleaf * TW);
-    int* cntB = cntA + nleaf;
-    int64_t* pdst = candB + (int64_t)nleaf * TW + nleaf + 2;
-    int64_t* psrc = pdst + 2 * TW;
-    int* npairs = reinterpret_cast<int*>(psrc + 2 * TW);
-    hipLaunchKernelGGL(tslu_select_kernel<T>, dim3(nleaf), dim3(TR), 0, s, m, r, nn, Ablk, lda,
-                       (const int64_t*)nullptr, (const int*)nullptr, 0, candA, cntA);
+    T* Utop = reinterpret_cast<T*>(work);
+    int* candA = reinterpret_cast<int*>(work + kUtopI64);
+    int* candB = candA + (int64_t)nleaf * TW;
+    int* cntA = candB + (int64_t)nleaf * TW;
+    int* cntB = cntA + nleaf + 1;
+    hipLaunchKernelGGL((tslu_select_kernel<T, TR>), dim3(nleaf), dim3(TR), 0, s, m, r, nn, Ablk, lda,
+                       (const int*)nullptr, (const int*)nullptr, 0, candA, cntA);
     int n = nleaf;
     while (n > 1) {
-        int nn2 = (n + FANIN - 1) / FANIN;
-        hipLaunchKernelGGL(tslu_select_kernel<T>, dim3(nn2), dim3(TR), 0, s, m, r, nn, Ablk, lda,
-                           (const int64_t*)candA, (const int*)cntA, n, candB, cntB);
+        int n2 = (n + FANIN - 1) / FANIN;
+        hipLaunchKernelGGL((tslu_select_kernel<T, NODE_NT>), dim3(n2), dim3(NODE_NT), 0, s, m, r, nn, Ablk, lda,
+                           (const int*)candA, (const int*)cntA, n, candB, cntB);
         std::swap(candA, candB);
         std::swap(cntA, cntB);
-        n = nn2;
+        n = n2;
     }
-    hipLaunchKernelGGL(tslu_pivots_kernel<T>, dim3(1), dim3(64), 0, s, r, (const int64_t*)candA, (const int*)cntA,
-                       ipiv, perm, pdst, psrc, npairs);
-    permute_rows<T>(ncols, Apanel, lda, pdst, psrc, npairs, 2 * TW, s);
-    hipLaunchKernelGGL(tslu_top_kernel<T>, dim3(1), dim3(64), 0, s, r, nn, Ablk, lda, Uws, info, info_offset);
-    if (rows > nn)
-        hipLaunchKernelGGL(tslu_rows_kernel<T>, dim3((unsigned)((rows - nn + TR - 1) / TR)), dim3(TR), 0, s, m, r, nn,
-                           Ablk, lda, (const T*)Uws);
+    const int64_t c0 = (Ablk - Apanel) / lda;
+    const int pgrid = (int)std::min<int64_t>((ncols + 3) / 4, 1024);
+    hipLaunchKernelGGL(tslu_permute_kernel<T>, dim3(pgrid), dim3(256), 0, s, (int)r, nn, c0, Apanel, lda, ncols,
+                       (const int*)candA, (const int*)cntA, ipiv, perm, Utop);
+    const int rgrid = (int)std::max<int64_t>(1, (rows - nn + 255) / 256);
+    hipLaunchKernelGGL(tslu_rows_kernel<T>, dim3(rgrid), dim3(256), 0, s, m, r, nn, Ablk, lda, (const T*)Utop, info,
+                       info_offset);
 }
 
 #define SLATE_INST_TSLU(T) \
