@@ -1,0 +1,134 @@
+"""Multi-process driver checks, run under torch.distributed.run by test_dist.py
+(reference test strategy: the tester with --grid p x q under mpirun, SURVEY.md
+§4.1; here ranks talk over gloo host comms, or RCCL on a multi-GPU node).
+
+usage: dist_worker.py P Q TARGET CASE[,CASE...]
+Every rank computes the same global result from replicated inputs and checks
+it against numpy; a failure raises (non-zero exit of that rank).
+"""
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, ".."))
+sys.path.insert(0, HERE)
+
+import torch  # noqa: F401,E402  (HIP runtime first)
+import slate_d35_amd as s  # noqa: E402
+from slate_d35_amd import parallel  # noqa: E402
+from helpers import rnd, relerr  # noqa: E402
+
+
+def tol(dt):
+    return 5e-4 if dt in (np.float32, np.complex64) else 1e-11
+
+
+def case_gemm(tg, dt, nb):
+    a, b, c = rnd(150, 90, dt, 1), rnd(90, 120, dt, 2), rnd(150, 120, dt, 3)
+    A, B, C = (s.from_numpy(x, nb=nb, target=tg) for x in (a, b, c))
+    s.gemm(1.5, A, B, -0.5, C, target=tg)
+    assert relerr(s.to_numpy(C), 1.5 * a @ b - 0.5 * c) < tol(dt)
+
+
+def case_herk(tg, dt, nb):
+    a = rnd(130, 70, dt, 4)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    C = s.from_numpy(np.zeros((130, 130), dt), nb=nb, target=tg)
+    H = s.HermitianMatrix(s.Uplo.Lower, C)
+    s.herk(1.0, A, 0.0, H, target=tg)
+    ref = a @ a.conj().T
+    assert relerr(np.tril(s.to_numpy(C)), np.tril(ref)) < tol(dt)
+
+
+def case_trsm(tg, dt, nb):
+    n = 140
+    t = (np.tril(rnd(n, n, dt, 5)) / n + 2 * np.eye(n)).astype(dt)
+    b = rnd(n, 60, dt, 6)
+    T = s.TriangularMatrix(s.Uplo.Lower, s.Diag.NonUnit, s.from_numpy(t, nb=nb, target=tg))
+    B = s.from_numpy(b, nb=nb, target=tg)
+    s.trsm(s.Side.Left, 1.0, T, B, target=tg)
+    assert relerr(t @ s.to_numpy(B), b) < tol(dt)
+
+
+def case_potrf(tg, dt, nb):
+    n = 200
+    a = rnd(n, n, dt, 7)
+    a = (a @ a.conj().T + n * np.eye(n)).astype(dt)
+    b = rnd(n, 3, dt, 8)
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb, target=tg))
+    B = s.from_numpy(b, nb=nb, target=tg)
+    info = s.posv(A, B, target=tg)
+    assert info == 0
+    assert relerr(a @ s.to_numpy(B), b) < 10 * tol(dt)
+
+
+def case_getrf(tg, dt, nb):
+    n = 190
+    a = rnd(n, n, dt, 9)
+    b = rnd(n, 4, dt, 10)
+    for method in ("ppiv", "tntpiv"):
+        A = s.from_numpy(a, nb=nb, target=tg)
+        B = s.from_numpy(b, nb=nb, target=tg)
+        kw = {"method_lu": 2} if method == "tntpiv" else {}
+        info, _ = s.gesv(A, B, target=tg, **kw)
+        assert info == 0
+        assert relerr(a @ s.to_numpy(B), b) < 100 * tol(dt), method
+
+
+def case_geqrf(tg, dt, nb):
+    m, n = 230, 120
+    a = rnd(m, n, dt, 11)
+    b = rnd(m, 2, dt, 12)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    B = s.from_numpy(b, nb=nb, target=tg)
+    s.gels(A, B, target=tg)
+    x = s.to_numpy(B)[:n]
+    ref = np.linalg.lstsq(a, b, rcond=None)[0]
+    assert relerr(x, ref) < 100 * tol(dt)
+
+
+def case_norm(tg, dt, nb):
+    a = rnd(170, 110, dt, 13)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    for kind, ref in [(s.Norm.One, np.linalg.norm(a, 1)), (s.Norm.Inf, np.linalg.norm(a, np.inf)),
+                      (s.Norm.Fro, np.linalg.norm(a)), (s.Norm.Max, np.abs(a).max())]:
+        v = s.norm(kind, A, target=tg)
+        assert abs(v - ref) <= 1e-4 * ref, (kind, v, ref)
+
+
+def case_mixed(tg, dt, nb):
+    n = 160
+    a = rnd(n, n, np.float64, 14) + n * np.eye(n)
+    b = rnd(n, 2, np.float64, 15)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    B = s.from_numpy(b, nb=nb, target=tg)
+    X = s.from_numpy(np.zeros_like(b), nb=nb, target=tg)
+    info, _, it = s.gesv_mixed(A, B, X, target=tg)
+    assert info == 0
+    assert relerr(a @ s.to_numpy(X), b) < 1e-12
+
+
+CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
+EXTRA = {}
+
+
+def main():
+    p, q, tg = int(sys.argv[1]), int(sys.argv[2]), sys.argv[3]
+    names = sys.argv[4].split(",")
+    dtypes = [np.float64, np.complex64] if len(sys.argv) < 6 else [getattr(np, d) for d in sys.argv[5].split(",")]
+    parallel.init_grid(p, q, transport=os.environ.get("SLATE_TRANSPORT", "auto"))
+    for name in names:
+        fn = CASES.get(name) or EXTRA[name]
+        for dt in dtypes:
+            if name == "mixed" and dt != np.float64:
+                continue
+            for nb in (32, 48):
+                fn(tg, dt, nb)
+    if parallel.world_rank() == 0:
+        print("DIST_OK", p, q, tg, names, flush=True)
+
+
+if __name__ == "__main__":
+    main()
