@@ -140,7 +140,21 @@ void bind_drivers(py::module_& m, std::string const& s) {
             Options op = to_options(o); int iter = 0; int64_t info;
             { py::gil_scoped_release r; info = posv_mixed(A, B, X, iter, op); }
             return py::make_tuple(info, iter); });
+        DEF("gesv_mixed_gmres", [=](Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, py::dict o) {
+            Options op = to_options(o); Pivots P; int iter = 0; int64_t info;
+            { py::gil_scoped_release r; info = gesv_mixed_gmres(A, P, B, X, iter, op); }
+            return py::make_tuple(info, piv_out(P), iter); });
+        DEF("posv_mixed_gmres", [](HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, py::dict o) {
+            Options op = to_options(o); int iter = 0; int64_t info;
+            { py::gil_scoped_release r; info = posv_mixed_gmres(A, B, X, iter, op); }
+            return py::make_tuple(info, iter); });
     }
+    DEF("gecondest", [](Norm nm, Matrix<T>& A, real_type<T> anorm, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return gecondest(nm, A, anorm, op); });
+    DEF("pocondest", [](Norm nm, HermitianMatrix<T>& A, real_type<T> anorm, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return pocondest(nm, A, anorm, op); });
+    DEF("trcondest", [](Norm nm, TriangularMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return trcondest(nm, A, op); });
 
     // ---- QR / LQ
     DEF("geqrf", [](Matrix<T>& A, py::dict o) {

@@ -13,6 +13,13 @@
 
 namespace slate {
 namespace internal {
+/// Working precision of the mixed-precision solvers' factorization.
+template <typename T> struct lower_prec { using type = T; };
+template <> struct lower_prec<double> { using type = float; };
+template <> struct lower_prec<std::complex<double>> { using type = std::complex<float>; };
+}  // namespace internal
+
+namespace internal {
 
 /// Local row offset within `A`'s local block for view row-tile index i (first
 /// local row whose global index is >= start of tile i).

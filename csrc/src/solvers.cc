@@ -163,9 +163,6 @@ int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts) {
 // mixed precision iterative refinement
 namespace {
 
-template <typename T> struct lower_prec { using type = T; };
-template <> struct lower_prec<double> { using type = float; };
-template <> struct lower_prec<std::complex<double>> { using type = std::complex<float>; };
 
 template <typename T>
 bool iter_ref_converged(std::vector<real_type<T>> const& rnorm, std::vector<real_type<T>> const& xnorm,
