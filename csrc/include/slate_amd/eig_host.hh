@@ -1,0 +1,76 @@
+// Host (CPU, OpenMP) stages of the two-stage eigenvalue / SVD reductions.
+//
+// Reference: hb2st.cc (bulge chasing on one node with OpenMP tasks),
+// tb2bd.cc, sterf.cc / steqr2.cc / stedc*.cc (tridiagonal eigensolvers),
+// bdsqr.cc (bidiagonal SVD through LAPACK++).  There is no vendor LAPACK in
+// this stack, so the small dense kernels are written here:
+//   * hb2st  Householder bulge chasing, band Hermitian -> real tridiagonal
+//   * tb2bd  Householder bulge chasing, upper band -> real upper bidiagonal
+//   * steqr  implicit QL with Wilkinson shifts (EISPACK tql2 formulation);
+//            rotations of one sweep are applied to Z rows in parallel
+//   * stedc  Cuppen divide and conquer with deflation and Gu-Eisenstat
+//            eigenvectors; the merge products use the blocked host gemm
+//   * bdsqr  Golub-Reinsch implicit-shift QR on the bidiagonal
+// The reflectors of hb2st / tb2bd are kept (Reflectors) and applied to the
+// eigen/singular vectors afterwards, in reverse order (reference
+// unmtr_hb2st.cc / unmbr_tb2bd).
+#pragma once
+
+#include "types.hh"
+
+#include <cstdint>
+#include <vector>
+
+namespace slate {
+namespace host {
+
+/// A sequence of Householder reflectors H_k = I - tau_k v_k v_k^H acting on
+/// rows [off_k, off_k + len_k).  Q = H_0 H_1 ... H_{K-1}.
+template <typename T>
+struct Reflectors {
+    std::vector<int64_t> off, len, voff;
+    std::vector<T> tau, v;
+    void push(int64_t o, int64_t l, T t, T const* vec) {
+        off.push_back(o); len.push_back(l); voff.push_back(int64_t(v.size())); tau.push_back(t);
+        v.insert(v.end(), vec, vec + l);
+    }
+    size_t size() const { return tau.size(); }
+    /// C = Q C (trans = false) or Q^H C (trans = true); C is n_rows x ncols.
+    void apply_left(bool trans, int64_t ncols, T* C, int64_t ldc) const;
+};
+
+/// Hermitian band (lower, bandwidth kd, full dense storage n x n in A) to real
+/// symmetric tridiagonal (d, e).  Reflectors and the diagonal phase (so that
+/// A = Q diag(phase) T diag(phase)^H Q^H) are returned for the back-transform.
+template <typename T>
+void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& d, std::vector<real_type<T>>& e,
+           Reflectors<T>& Q, std::vector<T>& phase);
+
+/// Upper band (bandwidth kd, dense m x n storage, m >= n) to real upper
+/// bidiagonal: A = U B V^H with U = QU diag(pu), V = QV diag(pv).
+template <typename T>
+void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& d,
+           std::vector<real_type<T>>& e, Reflectors<T>& QU, Reflectors<T>& QV, std::vector<T>& pu,
+           std::vector<T>& pv);
+
+/// Symmetric tridiagonal eigenproblem (d diagonal, e subdiagonal, n-1).
+/// Eigenvalues ascending in d; when Z != nullptr its columns (zrows rows) are
+/// multiplied by the eigenvector matrix (Z := Z * V).  Returns 0 or the
+/// number of unconverged eigenvalues.
+template <typename R, typename T>
+int64_t steqr(int64_t n, R* d, R* e, T* Z, int64_t ldz, int64_t zrows);
+
+template <typename R>
+int64_t sterf(int64_t n, R* d, R* e);
+
+/// Divide and conquer: eigenvalues ascending in d, eigenvectors in Q (n x n).
+template <typename R>
+int64_t stedc(int64_t n, R* d, R* e, R* Q, int64_t ldq);
+
+/// Bidiagonal SVD: B = diag(d) + superdiag(e) (n x n, upper).  Singular
+/// values descending in d; U (urows x n) := U * Ub, VT (n x vcols) := Vb^T VT.
+template <typename R, typename T>
+int64_t bdsqr(int64_t n, R* d, R* e, T* U, int64_t ldu, int64_t urows, T* VT, int64_t ldvt, int64_t vcols);
+
+}  // namespace host
+}  // namespace slate

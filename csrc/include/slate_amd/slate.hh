@@ -161,6 +161,18 @@ template <typename T>
 void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts = {});
 template <typename T>
 void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts = {});
+/// Stage 1 of heev: Hermitian (dense general storage) -> band of width nb.
+template <typename T>
+void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& opts = {});
+/// Stage 1 of svd: general (m >= n) -> upper band of width nb.
+template <typename T>
+void ge2tb(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<TriangularFactors<T>>& TV,
+           Options const& opts = {});
+template <typename T>
+void hegst(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T> const& B, Options const& opts = {});
+template <typename T>
+void hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_type<T>>& Lambda,
+          Matrix<T>& Z, Options const& opts = {});
 
 /// Wait for all device work of this process (drivers already synchronize).
 void sync();

@@ -14,6 +14,7 @@
 #include "slate_amd/trace.hh"
 #include "slate_amd/runtime.hh"
 #include "bind_drivers.hh"
+#include <pybind11/numpy.h>
 
 #include <complex>
 #include <cstring>
@@ -348,6 +349,31 @@ PYBIND11_MODULE(_slate, m) {
     m.def("release_cache", &device::release_cache);
     m.def("bytes_in_use", &device::bytes_in_use);
     m.def("version", &slate::version);
+    // tridiagonal / bidiagonal host solvers (fp64): return numpy arrays
+    using VD = std::vector<double>;
+    auto mat = [](std::vector<double> const& v, int64_t r, int64_t c) {
+        py::array_t<double, py::array::f_style> a({r, c});
+        std::copy(v.begin(), v.end(), a.mutable_data());
+        return a;
+    };
+    m.def("sterf", [](VD d, VD e) { slate::host::sterf<double>(int64_t(d.size()), d.data(), e.data()); return d; });
+    m.def("steqr", [=](VD d, VD e, bool vectors) {
+        int64_t n = d.size();
+        VD Z(vectors ? n * n : 0);
+        for (int64_t i = 0; vectors && i < n; ++i) Z[i + i * n] = 1;
+        slate::host::steqr<double, double>(n, d.data(), e.data(), vectors ? Z.data() : nullptr, n, vectors ? n : 0);
+        return py::make_tuple(d, mat(Z, vectors ? n : 0, vectors ? n : 0)); });
+    m.def("stedc", [=](VD d, VD e) {
+        int64_t n = d.size();
+        VD Z(n * n);
+        slate::host::stedc<double>(n, d.data(), e.data(), Z.data(), n);
+        return py::make_tuple(d, mat(Z, n, n)); });
+    m.def("bdsqr", [=](VD d, VD e) {
+        int64_t n = d.size();
+        VD U(n * n), VT(n * n);
+        for (int64_t i = 0; i < n; ++i) { U[i + i * n] = 1; VT[i + i * n] = 1; }
+        slate::host::bdsqr<double, double>(n, d.data(), e.data(), U.data(), n, n, VT.data(), n, n);
+        return py::make_tuple(d, mat(U, n, n), mat(VT, n, n)); });
     m.def("timers", []() { return timers(); });
     m.def("clear_timers", []() { timers().clear(); });
 

@@ -5,6 +5,8 @@
 #include <pybind11/stl.h>
 #include "slate_amd/slate.hh"
 #include "slate_amd/local_blas.hh"
+#include "slate_amd/eig_host.hh"
+#include <pybind11/numpy.h>
 
 namespace py = pybind11;
 
@@ -175,6 +177,46 @@ void bind_drivers(py::module_& m, std::string const& s) {
         return Tf; });
     DEF("cholqr", [](Matrix<T>& A, Matrix<T>& R, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; return cholqr(A, R, op); });
+
+    // ---- eigenvalues / SVD (None for an unwanted vector matrix)
+    auto opt_mat = [](py::object z) { return z.is_none() ? Matrix<T>() : z.cast<Matrix<T>>(); };
+    DEF("heev", [=](HermitianMatrix<T>& A, py::object z, py::dict o) {
+        Options op = to_options(o); Matrix<T> Z = opt_mat(z); std::vector<R> L;
+        { py::gil_scoped_release r; heev(A, L, Z, op); }
+        return L; });
+    DEF("hegv", [=](int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, py::object z, py::dict o) {
+        Options op = to_options(o); Matrix<T> Z = opt_mat(z); std::vector<R> L;
+        { py::gil_scoped_release r; hegv(itype, A, B, L, Z, op); }
+        return L; });
+    DEF("hegst", [](int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T> const& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; hegst(itype, A, B, op); });
+    DEF("svd", [=](Matrix<T>& A, py::object u, py::object vt, py::dict o) {
+        Options op = to_options(o); Matrix<T> U = opt_mat(u), VT = opt_mat(vt); std::vector<R> S;
+        { py::gil_scoped_release r; svd(A, S, U, VT, op); }
+        return S; });
+    DEF("he2hb", [](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); std::vector<TriangularFactors<T>> Ts;
+        { py::gil_scoped_release r; he2hb(A, Ts, op); }
+        return Ts; });
+    DEF("ge2tb", [](Matrix<T>& A, py::dict o) {
+        Options op = to_options(o); std::vector<TriangularFactors<T>> TU, TV;
+        { py::gil_scoped_release r; ge2tb(A, TU, TV, op); }
+        return py::make_tuple(TU, TV); });
+    // host stage-2 kernels on dense numpy arrays (column-major copies)
+    DEF("hb2st", [](py::array_t<T, py::array::f_style | py::array::forcecast> a, int64_t kd) {
+        auto b = a.request();
+        int64_t n = b.shape[0];
+        std::vector<T> A((T*)b.ptr, (T*)b.ptr + n * n);
+        std::vector<R> d, e; host::Reflectors<T> Q; std::vector<T> ph;
+        { py::gil_scoped_release r; host::hb2st<T>(n, kd, A.data(), n, d, e, Q, ph); }
+        return py::make_tuple(d, e); });
+    DEF("tb2bd", [](py::array_t<T, py::array::f_style | py::array::forcecast> a, int64_t kd) {
+        auto b = a.request();
+        int64_t m = b.shape[0], n = b.shape[1];
+        std::vector<T> A((T*)b.ptr, (T*)b.ptr + m * n);
+        std::vector<R> d, e; host::Reflectors<T> QU, QV; std::vector<T> pu, pv;
+        { py::gil_scoped_release r; host::tb2bd<T>(m, n, kd, A.data(), m, d, e, QU, QV, pu, pv); }
+        return py::make_tuple(d, e); });
 
     // ---- direct local-kernel access on raw device pointers (single process)
     auto dctx = []() { return lb::Ctx::device(0); };

@@ -1,0 +1,614 @@
+// Host stages of the two-stage eigen/SVD reductions (see eig_host.hh).
+#include "slate_amd/eig_host.hh"
+#include "slate_amd/host_blas.hh"
+#include "slate_amd/exception.hh"
+
+#include <algorithm>
+#include <cmath>
+#include <complex>
+#include <limits>
+#include <numeric>
+
+namespace slate {
+namespace host {
+
+namespace {
+
+template <typename T> inline T cj(T x) { return x; }
+template <typename R> inline std::complex<R> cj(std::complex<R> x) { return std::conj(x); }
+
+/// One Givens rotation (c, s) on columns (i, i+1) of a row-major-agnostic
+/// column-major matrix: [x y] <- [c*x - s*y, s*x + c*y].
+template <typename R>
+struct Rot { int64_t i; R c, s; };
+
+/// Apply a recorded sequence of rotations to the rows of Z in parallel
+/// (every row is independent; the sequence order is preserved per row).
+template <typename R, typename T>
+void apply_rots(std::vector<Rot<R>> const& rots, T* Z, int64_t ldz, int64_t zrows) {
+    if (rots.empty() || Z == nullptr || zrows <= 0) return;
+    const int64_t RB = 64;
+    #pragma omp parallel for schedule(static) if (zrows * int64_t(rots.size()) > 32768)
+    for (int64_t r0 = 0; r0 < zrows; r0 += RB) {
+        int64_t r1 = std::min(zrows, r0 + RB);
+        for (auto const& g : rots) {
+            T* x = Z + g.i * ldz;
+            T* y = Z + (g.i + 1) * ldz;
+            for (int64_t k = r0; k < r1; ++k) {
+                T a = x[k], b = y[k];
+                x[k] = g.c * a - g.s * b;
+                y[k] = g.s * a + g.c * b;
+            }
+        }
+    }
+}
+
+}  // namespace
+
+//------------------------------------------------------------------------------
+template <typename T>
+void Reflectors<T>::apply_left(bool trans, int64_t ncols, T* C, int64_t ldc) const {
+    const int64_t K = int64_t(tau.size());
+    if (K == 0 || ncols <= 0) return;
+    const int64_t CB = 16;
+    #pragma omp parallel for schedule(dynamic)
+    for (int64_t c0 = 0; c0 < ncols; c0 += CB) {
+        int64_t c1 = std::min(ncols, c0 + CB);
+        for (int64_t t = 0; t < K; ++t) {
+            int64_t k = trans ? t : K - 1 - t;
+            T tk = trans ? cj(tau[k]) : tau[k];
+            if (tk == T(0)) continue;
+            const T* vk = v.data() + voff[k];
+            int64_t o = off[k], L = len[k];
+            for (int64_t j = c0; j < c1; ++j) {
+                T* cc = C + o + j * ldc;
+                T s = T(0);
+                for (int64_t i = 0; i < L; ++i) s += cj(vk[i]) * cc[i];
+                s *= tk;
+                for (int64_t i = 0; i < L; ++i) cc[i] -= vk[i] * s;
+            }
+        }
+    }
+}
+
+//------------------------------------------------------------------------------
+// hb2st: sweeps j = 0..n-3; each annihilates column j below the subdiagonal
+// with a reflector on rows [j+1, j+kd] and chases the bulge down the band by
+// annihilating its first column kd rows further each time.
+template <typename T>
+void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& d, std::vector<real_type<T>>& e,
+           Reflectors<T>& Q, std::vector<T>& phase) {
+    using R = real_type<T>;
+    auto a = [&](int64_t i, int64_t j) -> T& { return A[i + j * lda]; };
+    const int64_t b = std::max<int64_t>(kd, 1);
+    std::vector<T> v(b + 1), w(n);
+    auto two_sided = [&](int64_t k, int64_t s0, int64_t L, T tau) {
+        // H^H A H on the window [w0, w1] (column/row k set explicitly by the caller)
+        int64_t w0 = std::max<int64_t>(0, k - 2 * b), w1 = std::min<int64_t>(n - 1, s0 + L - 1 + 2 * b);
+        // left: rows J, columns in window (skip k)
+        for (int64_t c = w0; c <= w1; ++c) {
+            if (c == k) continue;
+            T s = T(0);
+            for (int64_t i = 0; i < L; ++i) s += cj(v[i]) * a(s0 + i, c);
+            s *= cj(tau);
+            if (s != T(0)) for (int64_t i = 0; i < L; ++i) a(s0 + i, c) -= v[i] * s;
+        }
+        // right: rows in window (skip k), columns J
+        for (int64_t r = w0; r <= w1; ++r) {
+            if (r == k) continue;
+            T s = T(0);
+            for (int64_t i = 0; i < L; ++i) s += a(r, s0 + i) * v[i];
+            s *= tau;
+            if (s != T(0)) for (int64_t i = 0; i < L; ++i) a(r, s0 + i) -= s * cj(v[i]);
+        }
+    };
+    for (int64_t j = 0; j + 2 < n && b > 1; ++j) {
+        int64_t k = j, s0 = j + 1, s1 = std::min(j + b, n - 1);
+        while (true) {
+            int64_t L = s1 - s0 + 1;
+            if (L < 2) break;
+            T alpha = a(s0, k);
+            for (int64_t i = 1; i < L; ++i) v[i] = a(s0 + i, k);
+            T tau;
+            larfg(L, alpha, v.data() + 1, 1, tau);
+            v[0] = T(1);
+            a(s0, k) = alpha;
+            a(k, s0) = cj(alpha);
+            for (int64_t i = 1; i < L; ++i) { a(s0 + i, k) = T(0); a(k, s0 + i) = T(0); }
+            if (tau != T(0)) {
+                two_sided(k, s0, L, tau);
+                Q.push(s0, L, tau, v.data());
+            }
+            // next bulge: column s0 below its band
+            int64_t ns0 = s0 + b, ns1 = std::min(s1 + b, n - 1);
+            if (ns0 >= n - 1 || ns1 <= ns0) break;
+            k = s0; s0 = ns0; s1 = ns1;
+        }
+    }
+    d.assign(n, R(0));
+    e.assign(std::max<int64_t>(n - 1, 0), R(0));
+    phase.assign(n, T(1));
+    for (int64_t i = 0; i < n; ++i) d[i] = std::real(a(i, i));
+    for (int64_t i = 0; i + 1 < n; ++i) {
+        T t = a(i + 1, i);
+        R at = std::abs(t);
+        e[i] = at;
+        phase[i + 1] = at > R(0) ? phase[i] * t / T(at) : phase[i];
+    }
+}
+
+//------------------------------------------------------------------------------
+// tb2bd: sweeps j = 0..n-2: a right reflector on columns [j+1, j+kd] clears
+// row j beyond the superdiagonal; the bulge below the diagonal is chased with
+// alternating left (column) and right (row) reflectors.
+template <typename T>
+void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& d,
+           std::vector<real_type<T>>& e, Reflectors<T>& QU, Reflectors<T>& QV, std::vector<T>& pu,
+           std::vector<T>& pv) {
+    using R = real_type<T>;
+    auto a = [&](int64_t i, int64_t j) -> T& { return A[i + j * lda]; };
+    const int64_t b = std::max<int64_t>(kd, 1);
+    std::vector<T> v(b + 1);
+    auto right = [&](int64_t r, int64_t c0, int64_t L, T tau) {
+        // rows in window (skip r): A[row, J] = A[row, J] H
+        int64_t w0 = std::max<int64_t>(0, c0 - 2 * b - 1), w1 = std::min<int64_t>(m - 1, c0 + L - 1 + 2 * b);
+        for (int64_t i = w0; i <= w1; ++i) {
+            if (i == r) continue;
+            T s = T(0);
+            for (int64_t t = 0; t < L; ++t) s += a(i, c0 + t) * v[t];
+            s *= tau;
+            if (s != T(0)) for (int64_t t = 0; t < L; ++t) a(i, c0 + t) -= s * cj(v[t]);
+        }
+    };
+    auto left = [&](int64_t c, int64_t r0, int64_t L, T tau) {
+        int64_t w0 = std::max<int64_t>(0, r0 - 2 * b - 1), w1 = std::min<int64_t>(n - 1, r0 + L - 1 + 2 * b);
+        for (int64_t jj = w0; jj <= w1; ++jj) {
+            if (jj == c) continue;
+            T s = T(0);
+            for (int64_t t = 0; t < L; ++t) s += cj(v[t]) * a(r0 + t, jj);
+            s *= cj(tau);
+            if (s != T(0)) for (int64_t t = 0; t < L; ++t) a(r0 + t, jj) -= v[t] * s;
+        }
+    };
+    for (int64_t j = 0; j + 1 < n; ++j) {
+        int64_t r = j, c0 = j + 1, c1 = std::min(j + b, n - 1);
+        while (true) {
+            // right reflector: row r, columns [c0, c1]
+            int64_t L = c1 - c0 + 1;
+            if (L >= 2) {
+                T alpha = cj(a(r, c0));
+                for (int64_t t = 1; t < L; ++t) v[t] = cj(a(r, c0 + t));
+                T tau;
+                larfg(L, alpha, v.data() + 1, 1, tau);
+                v[0] = T(1);
+                a(r, c0) = cj(alpha);
+                for (int64_t t = 1; t < L; ++t) a(r, c0 + t) = T(0);
+                if (tau != T(0)) { right(r, c0, L, tau); QV.push(c0, L, tau, v.data()); }
+            }
+            // left reflector: column c0, rows [c0, min(c1, m-1)]
+            int64_t r1 = std::min(c1, m - 1);
+            int64_t Ll = r1 - c0 + 1;
+            if (Ll >= 2) {
+                T alpha = a(c0, c0);
+                for (int64_t t = 1; t < Ll; ++t) v[t] = a(c0 + t, c0);
+                T tau;
+                larfg(Ll, alpha, v.data() + 1, 1, tau);
+                v[0] = T(1);
+                a(c0, c0) = alpha;
+                for (int64_t t = 1; t < Ll; ++t) a(c0 + t, c0) = T(0);
+                if (tau != T(0)) { left(c0, c0, Ll, tau); QU.push(c0, Ll, tau, v.data()); }
+            }
+            // next: row c0 beyond its band, columns [c0 + b, c1 + b]
+            int64_t nc0 = c0 + b, nc1 = std::min(c1 + b, n - 1);
+            if (nc0 >= n - 1 || nc1 <= nc0) break;
+            r = c0; c0 = nc0; c1 = nc1;
+        }
+    }
+    d.assign(n, R(0));
+    e.assign(std::max<int64_t>(n - 1, 0), R(0));
+    pu.assign(n, T(1));
+    pv.assign(n, T(1));
+    // B' = Du B Dv^H with real nonnegative B: v_0 = 1, u_i from d_i, v_{i+1} from e_i
+    for (int64_t i = 0; i < n; ++i) {
+        T di = a(i, i);
+        R ad = std::abs(di);
+        pu[i] = ad > R(0) ? di * pv[i] / T(ad) : pv[i];
+        d[i] = ad;
+        if (i + 1 < n) {
+            T ei = a(i, i + 1);
+            R ae = std::abs(ei);
+            e[i] = ae;
+            // conj(u_i) e_i v_{i+1} = |e_i|  =>  v_{i+1} = u_i |e_i| / e_i
+            pv[i + 1] = ae > R(0) ? pu[i] * cj(ei) / T(ae) : pu[i];
+        }
+    }
+}
+
+//------------------------------------------------------------------------------
+// Implicit QL (EISPACK tql2 formulation); Z columns are the eigenvectors.
+template <typename R, typename T>
+int64_t steqr(int64_t n, R* d, R* e_in, T* Z, int64_t ldz, int64_t zrows) {
+    if (n <= 0) return 0;
+    std::vector<R> e(n, R(0));
+    for (int64_t i = 0; i + 1 < n; ++i) e[i] = e_in[i];
+    const R eps = std::numeric_limits<R>::epsilon();
+    R f = 0, tst1 = 0;
+    int64_t unconverged = 0;
+    std::vector<Rot<R>> rots;
+    for (int64_t l = 0; l < n; ++l) {
+        tst1 = std::max(tst1, std::abs(d[l]) + std::abs(e[l]));
+        int64_t m = l;
+        while (m < n - 1 && std::abs(e[m]) > eps * tst1) ++m;
+        if (m > l) {
+            int iter = 0;
+            do {
+                if (++iter > 60) { ++unconverged; break; }
+                R g = d[l];
+                R p = (d[l + 1] - g) / (R(2) * e[l]);
+                R r = std::hypot(p, R(1));
+                if (p < 0) r = -r;
+                d[l] = e[l] / (p + r);
+                d[l + 1] = e[l] * (p + r);
+                R dl1 = d[l + 1];
+                R h = g - d[l];
+                for (int64_t i = l + 2; i < n; ++i) d[i] -= h;
+                f += h;
+                p = d[m];
+                R c = 1, c2 = 1, c3 = 1, el1 = e[l + 1], s = 0, s2 = 0;
+                rots.clear();
+                for (int64_t i = m - 1; i >= l; --i) {
+                    c3 = c2; c2 = c; s2 = s;
+                    g = c * e[i];
+                    h = c * p;
+                    r = std::hypot(p, e[i]);
+                    e[i + 1] = s * r;
+                    s = e[i] / r;
+                    c = p / r;
+                    p = c * d[i] - s * g;
+                    d[i + 1] = h + s * (c * g + s * d[i]);
+                    // Z(:, i+1) = s Z(:,i) + c Z(:,i+1); Z(:,i) = c Z(:,i) - s Z(:,i+1)
+                    rots.push_back({i, c, s});
+                }
+                apply_rots(rots, Z, ldz, zrows);
+                p = -s * s2 * c3 * el1 * e[l] / dl1;
+                e[l] = s * p;
+                d[l] = c * p;
+            } while (std::abs(e[l]) > eps * tst1);
+        }
+        d[l] += f;
+        e[l] = 0;
+    }
+    // sort ascending (selection sort keeps column swaps to n)
+    for (int64_t i = 0; i + 1 < n; ++i) {
+        int64_t k = i;
+        for (int64_t j = i + 1; j < n; ++j) if (d[j] < d[k]) k = j;
+        if (k != i) {
+            std::swap(d[i], d[k]);
+            if (Z) for (int64_t r = 0; r < zrows; ++r) std::swap(Z[r + i * ldz], Z[r + k * ldz]);
+        }
+    }
+    return unconverged;
+}
+
+template <typename R>
+int64_t sterf(int64_t n, R* d, R* e) {
+    return steqr<R, R>(n, d, e, nullptr, 1, 0);
+}
+
+//------------------------------------------------------------------------------
+// Divide and conquer (Cuppen; deflation as LAPACK laed2; Gu-Eisenstat vectors
+// as laed3).  Q receives the eigenvectors of the n x n tridiagonal.
+namespace {
+
+template <typename R>
+void stedc_rec(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
+    const int64_t SMALL = 32;
+    if (n <= SMALL) {
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < n; ++i) Q[i + j * ldq] = (i == j) ? R(1) : R(0);
+        steqr<R, R>(n, d, e, Q, ldq, n);
+        return;
+    }
+    const int64_t m = n / 2;
+    const R beta = e[m - 1];
+    const R rho0 = std::abs(beta);
+    d[m - 1] -= rho0;
+    d[m] -= rho0;
+    // subproblems, Q = diag(Q1, Q2)
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < n; ++i) Q[i + j * ldq] = R(0);
+    stedc_rec(m, d, e, Q, ldq);
+    stedc_rec(n - m, d + m, e + m, Q + m + m * ldq, ldq);
+    const R sgn = beta < 0 ? R(-1) : R(1);
+    // z = [last row of Q1, sgn * first row of Q2] / sqrt(2); rho = 2 |beta|
+    std::vector<R> z(n), D(d, d + n);
+    for (int64_t j = 0; j < m; ++j) z[j] = Q[(m - 1) + j * ldq];
+    for (int64_t j = m; j < n; ++j) z[j] = sgn * Q[m + j * ldq];
+    const R s2 = std::sqrt(R(2));
+    for (auto& x : z) x /= s2;
+    R rho = R(2) * rho0;
+    // sort D ascending (permutation of the columns of Q)
+    std::vector<int64_t> perm(n);
+    std::iota(perm.begin(), perm.end(), 0);
+    std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return D[a] < D[b]; });
+    std::vector<R> Ds(n), zs(n), Qp(size_t(n) * n);
+    for (int64_t j = 0; j < n; ++j) {
+        Ds[j] = D[perm[j]];
+        zs[j] = z[perm[j]];
+        std::copy(Q + perm[j] * ldq, Q + perm[j] * ldq + n, Qp.begin() + j * n);
+    }
+    const R eps = std::numeric_limits<R>::epsilon();
+    R dmax = 0, zmax = 0;
+    for (int64_t j = 0; j < n; ++j) { dmax = std::max(dmax, std::abs(Ds[j])); zmax = std::max(zmax, std::abs(zs[j])); }
+    const R tol = R(8) * eps * std::max(dmax, zmax * rho);
+    // deflation: tiny z, then close pairs via Givens rotations
+    std::vector<char> defl(n, 0);
+    for (int64_t j = 0; j < n; ++j) if (rho * std::abs(zs[j]) <= tol) defl[j] = 1;
+    int64_t last = -1;
+    for (int64_t j = 0; j < n; ++j) {
+        if (defl[j]) continue;
+        if (last >= 0) {
+            R t = std::hypot(zs[last], zs[j]);
+            R c = zs[j] / t, s = -zs[last] / t;
+            if (std::abs((Ds[j] - Ds[last]) * c * s) <= tol) {
+                // rotate columns last, j: zs[last] -> 0
+                R* ql = Qp.data() + last * n;
+                R* qj = Qp.data() + j * n;
+                for (int64_t i = 0; i < n; ++i) {
+                    R a = ql[i], b = qj[i];
+                    ql[i] = c * a + s * b;
+                    qj[i] = -s * a + c * b;
+                }
+                R dl = Ds[last], dj = Ds[j];
+                Ds[last] = dl * c * c + dj * s * s;
+                Ds[j] = dl * s * s + dj * c * c;
+                zs[j] = t;
+                zs[last] = 0;
+                defl[last] = 1;
+            }
+        }
+        last = j;
+    }
+    std::vector<int64_t> act;
+    for (int64_t j = 0; j < n; ++j) if (!defl[j]) act.push_back(j);
+    const int64_t k = int64_t(act.size());
+    std::vector<R> lam(n);
+    std::vector<R> Qout(size_t(n) * n, R(0));
+    if (k > 0) {
+        std::vector<R> dk(k), zk(k);
+        for (int64_t i = 0; i < k; ++i) { dk[i] = Ds[act[i]]; zk[i] = zs[act[i]]; }
+        // dk may be out of order after rotations: sort
+        std::vector<int64_t> o(k);
+        std::iota(o.begin(), o.end(), 0);
+        std::sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return dk[a] < dk[b]; });
+        std::vector<R> dd(k), zz(k);
+        std::vector<int64_t> actS(k);
+        for (int64_t i = 0; i < k; ++i) { dd[i] = dk[o[i]]; zz[i] = zk[o[i]]; actS[i] = act[o[i]]; }
+        R znorm2 = 0;
+        for (auto x : zz) znorm2 += x * x;
+        // roots: lambda_j = dd[org[j]] + tau[j]
+        std::vector<int64_t> org(k);
+        std::vector<R> tau(k);
+        #pragma omp parallel for schedule(dynamic, 8) if (k > 64)
+        for (int64_t j = 0; j < k; ++j) {
+            R lo_abs = dd[j];
+            R hi_abs = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2;
+            auto sec = [&](int64_t o2, R t) {   // f(dd[o2] + t)
+                R s = 0;
+                for (int64_t i = 0; i < k; ++i) s += zz[i] * zz[i] / ((dd[i] - dd[o2]) - t);
+                return R(1) + rho * s;
+            };
+            // which endpoint is closer: sign of f at the midpoint
+            R mid = (hi_abs - lo_abs) / R(2);
+            int64_t o2 = j;
+            R a = 0, b = mid;
+            if (j + 1 < k && sec(j, mid) < R(0)) { o2 = j + 1; a = -mid; b = 0; }
+            else if (j + 1 >= k) { a = 0; b = hi_abs - lo_abs; }
+            // bisection on t in (a, b) relative to dd[o2]; f increases with t
+            // bisection to full relative precision of t (the distance to the
+            // nearest pole), which the Gu-Eisenstat vectors need
+            for (int it = 0; it < 400; ++it) {
+                R t = (a + b) / R(2);
+                if (t == a || t == b) break;
+                R fv = sec(o2, t);
+                if (fv > R(0)) b = t; else a = t;
+                if (std::abs(b - a) <= R(2) * eps * std::min(std::abs(a), std::abs(b))) break;
+            }
+            org[j] = o2;
+            tau[j] = (a + b) / R(2);
+        }
+        // Gu-Eisenstat: recompute z from the computed roots
+        auto lam_minus_d = [&](int64_t j, int64_t i) { return (dd[org[j]] - dd[i]) + tau[j]; };
+        std::vector<R> zh(k);
+        for (int64_t i = 0; i < k; ++i) {
+            R p = lam_minus_d(k - 1, i) / rho;
+            for (int64_t j = 0; j < k - 1; ++j) {
+                R num = lam_minus_d(j, i);
+                R den = (j < i) ? (dd[j] - dd[i]) : (dd[j + 1] - dd[i]);
+                p *= num / den;
+            }
+            zh[i] = std::copysign(std::sqrt(std::abs(p)), zz[i]);
+        }
+        // eigenvectors of D + rho z z^T, then Q * U
+        std::vector<R> U(size_t(k) * k);
+        for (int64_t j = 0; j < k; ++j) {
+            R nrm = 0;
+            for (int64_t i = 0; i < k; ++i) {
+                R den = (dd[i] - dd[org[j]]) - tau[j];
+                R u = zh[i] / den;
+                U[i + j * k] = u;
+                nrm += u * u;
+            }
+            nrm = std::sqrt(nrm);
+            for (int64_t i = 0; i < k; ++i) U[i + j * k] /= nrm;
+            lam[j] = dd[org[j]] + tau[j];
+        }
+        std::vector<R> Qa(size_t(n) * k);
+        for (int64_t i = 0; i < k; ++i) std::copy(Qp.begin() + actS[i] * n, Qp.begin() + actS[i] * n + n, Qa.begin() + i * n);
+        gemm<R>(Op::NoTrans, Op::NoTrans, n, k, k, R(1), Qa.data(), n, U.data(), k, R(0), Qout.data(), n);
+    }
+    // deflated columns pass through
+    int64_t col = k;
+    for (int64_t j = 0; j < n; ++j) {
+        if (!defl[j]) continue;
+        lam[col] = Ds[j];
+        std::copy(Qp.begin() + j * n, Qp.begin() + j * n + n, Qout.begin() + col * n);
+        ++col;
+    }
+    // sort ascending into d, Q
+    std::vector<int64_t> o(n);
+    std::iota(o.begin(), o.end(), 0);
+    std::sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return lam[a] < lam[b]; });
+    for (int64_t j = 0; j < n; ++j) {
+        d[j] = lam[o[j]];
+        std::copy(Qout.begin() + o[j] * n, Qout.begin() + o[j] * n + n, Q + j * ldq);
+    }
+}
+
+}  // namespace
+
+template <typename R>
+int64_t stedc(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
+    if (n <= 0) return 0;
+    std::vector<R> ee(e, e + std::max<int64_t>(n - 1, 0));
+    ee.push_back(R(0));
+    stedc_rec<R>(n, d, ee.data(), Q, ldq);
+    return 0;
+}
+
+//------------------------------------------------------------------------------
+// Golub-Reinsch implicit-shift QR on the upper bidiagonal (EISPACK svd).
+template <typename R, typename T>
+int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, int64_t ldvt, int64_t vcols) {
+    if (n <= 0) return 0;
+    std::vector<R> rv1(n, R(0));
+    for (int64_t i = 1; i < n; ++i) rv1[i] = e[i - 1];
+    R anorm = 0;
+    for (int64_t i = 0; i < n; ++i) anorm = std::max(anorm, std::abs(w[i]) + std::abs(rv1[i]));
+    int64_t fail = 0;
+    auto colrot = [&](T* M, int64_t ld, int64_t rows, int64_t a, int64_t b, R c, R s) {
+        if (!M) return;
+        T* x = M + a * ld;
+        T* y = M + b * ld;
+        for (int64_t r = 0; r < rows; ++r) {
+            T ya = x[r], yb = y[r];
+            x[r] = ya * c + yb * s;
+            y[r] = yb * c - ya * s;
+        }
+    };
+    auto rowrot = [&](T* M, int64_t ld, int64_t cols, int64_t a, int64_t b, R c, R s) {
+        if (!M) return;
+        for (int64_t jj = 0; jj < cols; ++jj) {
+            T xa = M[a + jj * ld], xb = M[b + jj * ld];
+            M[a + jj * ld] = xa * c + xb * s;
+            M[b + jj * ld] = xb * c - xa * s;
+        }
+    };
+    for (int64_t k = n - 1; k >= 0; --k) {
+        for (int its = 0; its < 75; ++its) {
+            bool flag = true;
+            int64_t l = k, nm = 0;
+            for (; l >= 0; --l) {
+                nm = l - 1;
+                if (l == 0 || std::abs(rv1[l]) + anorm == anorm) { flag = false; break; }
+                if (std::abs(w[nm]) + anorm == anorm) break;
+            }
+            if (flag) {
+                R c = 0, s = 1;
+                for (int64_t i = l; i <= k; ++i) {
+                    R f = s * rv1[i];
+                    rv1[i] = c * rv1[i];
+                    if (std::abs(f) + anorm == anorm) break;
+                    R g = w[i];
+                    R h = std::hypot(f, g);
+                    w[i] = h;
+                    h = R(1) / h;
+                    c = g * h;
+                    s = -f * h;
+                    colrot(U, ldu, urows, nm, i, c, s);
+                }
+            }
+            R z = w[k];
+            if (l == k) {
+                if (z < R(0)) {
+                    w[k] = -z;
+                    if (VT) for (int64_t jj = 0; jj < vcols; ++jj) VT[k + jj * ldvt] = -VT[k + jj * ldvt];
+                }
+                break;
+            }
+            if (its == 74) { ++fail; break; }
+            R x = w[l];
+            nm = k - 1;
+            R y = w[nm], g = rv1[nm], h = rv1[k];
+            R f = ((y - z) * (y + z) + (g - h) * (g + h)) / (R(2) * h * y);
+            g = std::hypot(f, R(1));
+            f = ((x - z) * (x + z) + h * ((y / (f + std::copysign(g, f))) - h)) / x;
+            R c = 1, s = 1;
+            for (int64_t j = l; j <= nm; ++j) {
+                int64_t i = j + 1;
+                g = rv1[i];
+                y = w[i];
+                h = s * g;
+                g = c * g;
+                z = std::hypot(f, h);
+                rv1[j] = z;
+                c = f / z;
+                s = h / z;
+                f = x * c + g * s;
+                g = g * c - x * s;
+                h = y * s;
+                y *= c;
+                rowrot(VT, ldvt, vcols, j, i, c, s);
+                z = std::hypot(f, h);
+                w[j] = z;
+                if (z != R(0)) {
+                    z = R(1) / z;
+                    c = f * z;
+                    s = h * z;
+                }
+                f = c * g + s * y;
+                x = c * y - s * g;
+                colrot(U, ldu, urows, j, i, c, s);
+            }
+            rv1[l] = 0;
+            rv1[k] = f;
+            w[k] = x;
+        }
+    }
+    // sort descending
+    for (int64_t i = 0; i + 1 < n; ++i) {
+        int64_t kk = i;
+        for (int64_t j = i + 1; j < n; ++j) if (w[j] > w[kk]) kk = j;
+        if (kk != i) {
+            std::swap(w[i], w[kk]);
+            if (U) for (int64_t r = 0; r < urows; ++r) std::swap(U[r + i * ldu], U[r + kk * ldu]);
+            if (VT) for (int64_t jj = 0; jj < vcols; ++jj) std::swap(VT[i + jj * ldvt], VT[kk + jj * ldvt]);
+        }
+    }
+    return fail;
+}
+
+//------------------------------------------------------------------------------
+#define SLATE_EIGH_INST(T)                                                                              \
+    template struct Reflectors<T>;                                                                      \
+    template void hb2st<T>(int64_t, int64_t, T*, int64_t, std::vector<real_type<T>>&,                   \
+                           std::vector<real_type<T>>&, Reflectors<T>&, std::vector<T>&);                \
+    template void tb2bd<T>(int64_t, int64_t, int64_t, T*, int64_t, std::vector<real_type<T>>&,          \
+                           std::vector<real_type<T>>&, Reflectors<T>&, Reflectors<T>&, std::vector<T>&, \
+                           std::vector<T>&);                                                            \
+    template int64_t steqr<real_type<T>, T>(int64_t, real_type<T>*, real_type<T>*, T*, int64_t, int64_t); \
+    template int64_t bdsqr<real_type<T>, T>(int64_t, real_type<T>*, real_type<T>*, T*, int64_t, int64_t, \
+                                            T*, int64_t, int64_t);
+
+SLATE_EIGH_INST(float)
+SLATE_EIGH_INST(double)
+SLATE_EIGH_INST(std::complex<float>)
+SLATE_EIGH_INST(std::complex<double>)
+
+template int64_t sterf<float>(int64_t, float*, float*);
+template int64_t sterf<double>(int64_t, double*, double*);
+template int64_t stedc<float>(int64_t, float*, float*, float*, int64_t);
+template int64_t stedc<double>(int64_t, double*, double*, double*, int64_t);
+
+}  // namespace host
+}  // namespace slate

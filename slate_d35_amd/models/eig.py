@@ -8,12 +8,17 @@ __all__ = ["heev", "hegv", "hegst", "svd", "svd_vals", "eig", "eig_vals", "he2hb
 
 
 def heev(A, Z=None, target=None, **kw):
-    """Eigenvalues (and vectors into Z if given) of a Hermitian matrix."""
-    return call("heev", A, A, Z, target=target, **kw)
+    """Eigenvalues (ascending numpy array; vectors into Z if given) of a
+    Hermitian matrix.  method_eig="dc" (divide and conquer, default) or "qr"."""
+    import numpy as np
+    return np.asarray(call("heev", A, A, Z, target=target, **kw))
 
 
 def hegv(itype, A, B, Z=None, target=None, **kw):
-    return call("hegv", A, itype, A, B, Z, target=target, **kw)
+    """Generalized Hermitian-definite eigenproblem (itype 1: A x = l B x,
+    2: A B x = l x, 3: B A x = l x).  B is overwritten by its Cholesky factor."""
+    import numpy as np
+    return np.asarray(call("hegv", A, itype, A, B, Z, target=target, **kw))
 
 
 def hegst(itype, A, B, target=None, **kw):
@@ -21,7 +26,10 @@ def hegst(itype, A, B, target=None, **kw):
 
 
 def svd(A, U=None, VT=None, target=None, **kw):
-    return call("svd", A, A, U, VT, target=target, **kw)
+    """Singular values (descending numpy array); thin U (m x k) and VT
+    (k x n), k = min(m, n), filled when given."""
+    import numpy as np
+    return np.asarray(call("svd", A, A, U, VT, target=target, **kw))
 
 
 def svd_vals(A, target=None, **kw):
@@ -40,8 +48,11 @@ def he2hb(A, target=None, **kw):
     return call("he2hb", A, A, target=target, **kw)
 
 
-def hb2st(A, target=None, **kw):
-    return call("hb2st", A, A, target=target, **kw)
+def hb2st(a, kd):
+    """Band (dense numpy, Hermitian, bandwidth kd) -> (d, e) of the tridiagonal."""
+    import numpy as np
+    from .._core import native
+    return native("hb2st", np.asarray(a).dtype)(np.asarray(a), kd)
 
 
 def sterf(d, e, **kw):
@@ -63,8 +74,11 @@ def ge2tb(A, target=None, **kw):
     return call("ge2tb", A, A, target=target, **kw)
 
 
-def tb2bd(A, target=None, **kw):
-    return call("tb2bd", A, A, target=target, **kw)
+def tb2bd(a, kd):
+    """Upper band (dense numpy, bandwidth kd) -> (d, e) of the bidiagonal."""
+    import numpy as np
+    from .._core import native
+    return native("tb2bd", np.asarray(a).dtype)(np.asarray(a), kd)
 
 
 def bdsqr(d, e, **kw):

@@ -1,0 +1,141 @@
+"""Eigenvalue and SVD tests (reference test/test_heev.cc, test_hegv.cc,
+test_hegst.cc, test_svd.cc, test_sterf.cc, test_steqr2.cc, test_stedc.cc,
+test_bdsqr.cc, test_hb2st.cc, test_tb2bd.cc): eigen/singular values against
+numpy.linalg, and backward error / orthogonality of the vectors."""
+import numpy as np
+import pytest
+
+import slate_d35_amd as s
+from helpers import DTYPES, rnd
+
+
+def tol(dt):
+    return 1e-3 if dt in (np.float32, np.complex64) else 1e-10
+
+
+def herm(n, dt, seed):
+    a = rnd(n, n, dt, seed)
+    return ((a + a.conj().T) / 2).astype(dt)
+
+
+def test_sterf_steqr_stedc():
+    rng = np.random.default_rng(0)
+    for n in (1, 2, 5, 31, 33, 100, 257):
+        d = rng.standard_normal(n)
+        e = rng.standard_normal(max(n - 1, 0))
+        t = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+        ref = np.linalg.eigvalsh(t)
+        assert np.allclose(s.sterf(d, e), ref, atol=1e-12 * max(1, abs(ref).max()))
+        for fn in (lambda: s.steqr(d, e, True), lambda: s.stedc(d, e)):
+            w, z = fn()
+            w = np.asarray(w)
+            assert np.allclose(w, ref, atol=1e-11 * max(1, abs(ref).max()))
+            assert np.linalg.norm(t @ z - z * w) <= 1e-11 * n * max(1, abs(ref).max())
+            assert np.linalg.norm(z.T @ z - np.eye(n)) <= 1e-11 * n
+
+
+def test_stedc_clustered():
+    # glued Wilkinson-like matrix with many close eigenvalues (deflation paths)
+    n = 200
+    d = np.abs(np.arange(n) - n // 2).astype(float) / 10
+    e = np.full(n - 1, 1e-7)
+    w, z = s.stedc(d, e)
+    t = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    assert np.allclose(np.asarray(w), np.linalg.eigvalsh(t), atol=1e-12)
+    assert np.linalg.norm(z.T @ z - np.eye(n)) < 1e-10
+    assert np.linalg.norm(t @ z - z * np.asarray(w)) < 1e-10
+
+
+def test_bdsqr():
+    rng = np.random.default_rng(1)
+    for n in (1, 3, 40, 120):
+        d = rng.standard_normal(n)
+        e = rng.standard_normal(max(n - 1, 0))
+        b = np.diag(d) + np.diag(e, 1)
+        sv, u, vt = s.bdsqr(d, e)
+        sv = np.asarray(sv)
+        assert np.allclose(sv, np.linalg.svd(b, compute_uv=False), atol=1e-12 * max(1, sv.max()))
+        assert np.linalg.norm(u @ np.diag(sv) @ vt - b) < 1e-11 * n * max(1, sv.max())
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+def test_hb2st_tb2bd(dt):
+    n, kd = 90, 7
+    a = herm(n, dt, 3)
+    band = np.tril(np.triu(a, -kd), kd)
+    d, e = s.hb2st(band, kd)
+    t = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    ref = np.linalg.eigvalsh(band)
+    assert np.allclose(np.linalg.eigvalsh(t), ref, atol=tol(dt) * abs(ref).max())
+    g = rnd(n, n, dt, 4)
+    ub = np.triu(np.tril(g, kd))
+    d, e = s.tb2bd(ub, kd)
+    b = np.diag(d) + np.diag(e, 1)
+    sref = np.linalg.svd(ub, compute_uv=False)
+    assert np.allclose(np.linalg.svd(b, compute_uv=False), sref, atol=tol(dt) * sref.max())
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("method", ["dc", "qr"])
+def test_heev(dt, method):
+    n, nb = 130, 32
+    a = herm(n, dt, 5)
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb))
+    Z = s.from_numpy(np.zeros((n, n), dt), nb=nb)
+    w = s.heev(A, Z, method_eig=method)
+    ref = np.linalg.eigvalsh(a.astype(np.complex128))
+    assert np.allclose(w, ref, atol=tol(dt) * abs(ref).max())
+    z = s.to_numpy(Z)
+    assert np.linalg.norm(a @ z - z * w) / (np.linalg.norm(a) * n) < tol(dt)
+    assert np.linalg.norm(z.conj().T @ z - np.eye(n)) / n < tol(dt)
+    # values only
+    A2 = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb))
+    assert np.allclose(s.heev(A2), ref, atol=tol(dt) * abs(ref).max())
+
+
+def test_heev_upper():
+    n, nb = 70, 16
+    a = herm(n, np.complex128, 6)
+    A = s.HermitianMatrix(s.Uplo.Upper, s.from_numpy(a, nb=nb))
+    assert np.allclose(s.heev(A), np.linalg.eigvalsh(a), atol=1e-10)
+
+
+@pytest.mark.parametrize("itype", [1, 2, 3])
+def test_hegv(itype):
+    n, nb = 80, 16
+    a = herm(n, np.float64, 7)
+    c = rnd(n, n, np.float64, 8)
+    b = c @ c.T + n * np.eye(n)
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb))
+    B = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(b, nb=nb))
+    Z = s.from_numpy(np.zeros((n, n)), nb=nb)
+    w = s.hegv(itype, A, B, Z)
+    z = s.to_numpy(Z)
+    if itype == 1:
+        r = a @ z - b @ z * w
+    elif itype == 2:
+        r = a @ b @ z - z * w
+    else:
+        r = b @ a @ z - z * w
+    assert np.linalg.norm(r) / (np.linalg.norm(a) * np.linalg.norm(b) * n) < 1e-12
+
+
+@pytest.mark.parametrize("dt", DTYPES)
+@pytest.mark.parametrize("mn", [(150, 100), (100, 100), (90, 140)])
+def test_svd(dt, mn):
+    m, n = mn
+    nb = 32
+    a = rnd(m, n, dt, 9)
+    k = min(m, n)
+    A = s.from_numpy(a, nb=nb)
+    U = s.from_numpy(np.zeros((m, k), dt), nb=nb)
+    VT = s.from_numpy(np.zeros((k, n), dt), nb=nb)
+    sv = s.svd(A, U, VT)
+    ref = np.linalg.svd(a.astype(np.complex128), compute_uv=False)
+    assert np.allclose(sv, ref, atol=tol(dt) * ref.max())
+    u, vt = s.to_numpy(U), s.to_numpy(VT)
+    assert np.linalg.norm(u @ np.diag(sv) @ vt - a) / (np.linalg.norm(a) * k) < tol(dt)
+    assert np.linalg.norm(u.conj().T @ u - np.eye(k)) / k < tol(dt)
+    assert np.linalg.norm(vt @ vt.conj().T - np.eye(k)) / k < tol(dt)
+    A2 = s.from_numpy(a, nb=nb)
+    assert np.allclose(s.svd_vals(A2), ref, atol=tol(dt) * ref.max())

@@ -318,3 +318,45 @@ def test_gemm_splitk_kernel(ta):
     s.ops.gemm(ta, "N", 2.0, tA, tB, 0.5, tC)
     opa = a if ta == "N" else a.T
     assert relerr(tC.cpu().numpy().T, 2.0 * opa @ b + 0.5 * c) < 1e-12
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_heev_device(dtype):
+    n, nb = 300, 64
+    a = rnd(n, n, dtype, 31)
+    a = (a + a.conj().T) / 2
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb, target="d"))
+    Z = s.from_numpy(np.zeros((n, n), dtype), nb=nb, target="d")
+    w = s.heev(A, Z, target="d")
+    assert np.allclose(w, np.linalg.eigvalsh(a), atol=1e-10 * n)
+    z = s.to_numpy(Z)
+    assert np.linalg.norm(a @ z - z * w) / (np.linalg.norm(a) * n) < 1e-12
+
+
+def test_svd_device():
+    m, n, nb = 320, 200, 64
+    a = rnd(m, n, np.float64, 32)
+    A = s.from_numpy(a, nb=nb, target="d")
+    U = s.from_numpy(np.zeros((m, n)), nb=nb, target="d")
+    VT = s.from_numpy(np.zeros((n, n)), nb=nb, target="d")
+    sv = s.svd(A, U, VT, target="d")
+    assert np.allclose(sv, np.linalg.svd(a, compute_uv=False), atol=1e-10 * n)
+    u, vt = s.to_numpy(U), s.to_numpy(VT)
+    assert np.linalg.norm(u @ np.diag(sv) @ vt - a) / (np.linalg.norm(a) * n) < 1e-12
+
+
+def test_condest_gmres_device():
+    n, nb = 256, 64
+    a = rnd(n, n, np.float64, 33) + n * np.eye(n)
+    A = s.from_numpy(a, nb=nb, target="d")
+    anorm = s.norm(s.Norm.One, A, target="d")
+    info, _ = s.getrf(A, target="d")
+    rc = s.gecondest(s.Norm.One, A, anorm, target="d")
+    ref = 1 / np.linalg.cond(a, 1)
+    assert ref * 0.999 <= rc <= 10 * ref
+    b = rnd(n, 1, np.float64, 34)
+    A2, B = s.from_numpy(a, nb=nb, target="d"), s.from_numpy(b, nb=nb, target="d")
+    X = s.from_numpy(np.zeros_like(b), nb=nb, target="d")
+    info, _, it = s.gesv_mixed_gmres(A2, B, X, target="d")
+    assert info == 0 and it >= 0
+    assert np.linalg.norm(a @ s.to_numpy(X) - b) / np.linalg.norm(b) < 1e-13
