@@ -544,7 +544,7 @@ void larfb(Ctx const& c, Side side, Op op, int64_t m, int64_t n, int64_t k, T co
         T* W = sc.alloc<T>(size_t(k) * n);
         T* W2 = sc.alloc<T>(size_t(k) * n);
         // W = V^H C (k x n, K = m): tall-skinny when n small
-        if (n <= 64 && k <= 32) {
+        if (n <= 32 && k <= 32) {   // tsip handles m, n <= 32
             T* work = sc.alloc<T>(size_t(1) << 20);
             kd::tsip(m, int(k), int(n), dval(T(1)), dptr(Vx), mv, dptr(C), ldc, dval(T(0)), dptr(W), k,
                      dptr(work), int64_t(1) << 20, s);

@@ -167,7 +167,7 @@ def test_getrf_panel_tournament_singular():
     assert info == 6
 
 
-@pytest.mark.parametrize("m,n", [(1000, 64), (2048, 256), (500, 100)])
+@pytest.mark.parametrize("m,n", [(1000, 64), (2048, 256), (500, 100), (8, 64), (20, 100), (64, 130), (33, 40)])
 def test_geqrf_panel_kernel(m, n):
     torch = _torch()
     a = rnd(m, n, np.float64, 9)
