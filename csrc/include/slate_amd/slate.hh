@@ -174,6 +174,38 @@ template <typename T>
 void hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_type<T>>& Lambda,
           Matrix<T>& Z, Options const& opts = {});
 
+//------------------------------------------------------------------------------
+// Band (reference gbtrf.cc, gbtrs.cc, gbsv.cc, pbtrf.cc, pbtrs.cc, pbsv.cc,
+// gbmm.cc, hbmm.cc, tbsm.cc)
+template <typename T>
+int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts = {});
+template <typename T>
+void gbtrs(BandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t gbsv(BandMatrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t pbtrf(HermitianBandMatrix<T>& A, Options const& opts = {});
+template <typename T>
+void pbtrs(HermitianBandMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+void gbmm(T alpha, BandMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts = {});
+template <typename T>
+void hbmm(Side side, T alpha, HermitianBandMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
+          Options const& opts = {});
+template <typename T>
+void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Hermitian indefinite (reference hetrf.cc, hetrs.cc, hesv.cc); LAPACK ipiv.
+template <typename T>
+int64_t hetrf(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Options const& opts = {});
+template <typename T>
+void hetrs(HermitianMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t hesv(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Options const& opts = {});
+
 /// Wait for all device work of this process (drivers already synchronize).
 void sync();
 

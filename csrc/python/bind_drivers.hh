@@ -178,6 +178,41 @@ void bind_drivers(py::module_& m, std::string const& s) {
     DEF("cholqr", [](Matrix<T>& A, Matrix<T>& R, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; return cholqr(A, R, op); });
 
+    // ---- band
+    DEF("gbtrf", [=](BandMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); Pivots P; int64_t info;
+        { py::gil_scoped_release r; info = gbtrf(A, P, op); }
+        return py::make_tuple(info, piv_out(P)); });
+    DEF("gbtrs", [=](BandMatrix<T> const& A, py::list piv, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; gbtrs(A, P, B, op); });
+    DEF("gbsv", [=](BandMatrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P; int64_t info;
+        { py::gil_scoped_release r; info = gbsv(A, P, B, op); }
+        return py::make_tuple(info, piv_out(P)); });
+    DEF("pbtrf", [](HermitianBandMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return pbtrf(A, op); });
+    DEF("pbtrs", [](HermitianBandMatrix<T> const& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; pbtrs(A, B, op); });
+    DEF("pbsv", [](HermitianBandMatrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return pbsv(A, B, op); });
+    DEF("gbmm", [](T a, BandMatrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; gbmm(a, A, B, b, C, op); });
+    DEF("hbmm", [](Side sd, T a, HermitianBandMatrix<T> const& A, Matrix<T> const& B, T b, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; hbmm(sd, a, A, B, b, C, op); });
+    DEF("tbsm", [](Side sd, T a, TriangularBandMatrix<T> const& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; tbsm(sd, a, A, B, op); });
+    // ---- Hermitian indefinite (LAPACK-style ipiv list)
+    DEF("hetrf", [](HermitianMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); std::vector<int64_t> ip; int64_t info;
+        { py::gil_scoped_release r; info = hetrf(A, ip, op); }
+        return py::make_tuple(info, ip); });
+    DEF("hetrs", [](HermitianMatrix<T> const& A, std::vector<int64_t> ip, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; hetrs(A, ip, B, op); });
+    DEF("hesv", [](HermitianMatrix<T>& A, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); std::vector<int64_t> ip; int64_t info;
+        { py::gil_scoped_release r; info = hesv(A, ip, B, op); }
+        return py::make_tuple(info, ip); });
+
     // ---- eigenvalues / SVD (None for an unwanted vector matrix)
     auto opt_mat = [](py::object z) { return z.is_none() ? Matrix<T>() : z.cast<Matrix<T>>(); };
     DEF("heev", [=](HermitianMatrix<T>& A, py::object z, py::dict o) {

@@ -2,7 +2,7 @@
 her2k.cc, syr2k.cc, trmm.cc, trsm*.cc)."""
 from ._wrap import call
 
-__all__ = ["gemm", "gemmA", "gemmC", "hemm", "symm", "herk", "syrk", "her2k", "syr2k",
+__all__ = ["gbmm", "hbmm", "tbsm", "gemm", "gemmA", "gemmC", "hemm", "symm", "herk", "syrk", "her2k", "syr2k",
            "trmm", "trsm", "multiply", "triangular_multiply", "triangular_solve",
            "rank_k_update", "rank_2k_update"]
 
@@ -91,3 +91,18 @@ def rank_2k_update(alpha, A, B, beta, C, **kw):
     if type(C).__name__.startswith("HermitianMatrix"):
         return her2k(alpha, A, B, beta, C, **kw)
     return syr2k(alpha, A, B, beta, C, **kw)
+
+
+def gbmm(alpha, A, B, beta, C, target=None, **kw):
+    """C = alpha A B + beta C with A a BandMatrix (reference src/gbmm.cc)."""
+    call("gbmm", A, alpha, A, B, beta, C, target=target, **kw)
+
+
+def hbmm(side, alpha, A, B, beta, C, target=None, **kw):
+    """C = alpha A B + beta C (or B A) with A a HermitianBandMatrix (src/hbmm.cc)."""
+    call("hbmm", A, side, alpha, A, B, beta, C, target=target, **kw)
+
+
+def tbsm(side, alpha, A, B, target=None, **kw):
+    """Solve op(A) X = alpha B with A a TriangularBandMatrix (src/tbsm.cc)."""
+    call("tbsm", A, side, alpha, A, B, target=target, **kw)
