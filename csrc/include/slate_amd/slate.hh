@@ -206,6 +206,15 @@ void hetrs(HermitianMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix
 template <typename T>
 int64_t hesv(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Options const& opts = {});
 
+/// Out-of-place inverse from getrf factors (reference getriOOP.cc).
+template <typename T>
+int64_t getri(Matrix<T>& A, Pivots const& pivots, Matrix<T>& B, Options const& opts);
+/// Random butterfly transform A := U^T A V and the RBT solver (gerbt.cc, gesv_rbt.cc).
+template <typename T>
+void gerbt(Matrix<T>& A, int depth, uint64_t seed_u, uint64_t seed_v, Options const& opts = {});
+template <typename T>
+int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
+
 /// Wait for all device work of this process (drivers already synchronize).
 void sync();
 

@@ -178,6 +178,14 @@ void bind_drivers(py::module_& m, std::string const& s) {
     DEF("cholqr", [](Matrix<T>& A, Matrix<T>& R, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; return cholqr(A, R, op); });
 
+    DEF("getri_oop", [=](Matrix<T>& A, py::list piv, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; return getri(A, P, B, op); });
+    DEF("gesv_rbt", [](Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, py::dict o) {
+        Options op = to_options(o); int iter = 0; int64_t info;
+        { py::gil_scoped_release r; info = gesv_rbt(A, B, X, iter, op); }
+        return py::make_tuple(info, iter); });
+    DEF("gerbt", [](Matrix<T>& A, int depth, uint64_t su, uint64_t sv, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; gerbt(A, depth, su, sv, op); });
     // ---- band
     DEF("gbtrf", [=](BandMatrix<T>& A, py::dict o) {
         Options op = to_options(o); Pivots P; int64_t info;

@@ -282,6 +282,15 @@ int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter,
     return 0;
 }
 
+/// Out-of-place inverse from the LU factors: B = A^{-1} (reference getriOOP.cc).
+template <typename T>
+int64_t getri(Matrix<T>& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("getriOOP");
+    set(T(0), T(1), B, opts);
+    getrs(A, pivots, B, opts);
+    return 0;
+}
+
 //------------------------------------------------------------------------------
 #define SLATE_SOLVE_INST(T)                                                                     \
     template void getrs<T>(Matrix<T> const&, Pivots const&, Matrix<T>&, Options const&);       \
@@ -293,7 +302,8 @@ int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter,
     template int64_t trtri<T>(TriangularMatrix<T>&, Options const&);                           \
     template void trtrm<T>(TriangularMatrix<T>&, Options const&);                              \
     template int64_t potri<T>(HermitianMatrix<T>&, Options const&);                            \
-    template int64_t getri<T>(Matrix<T>&, Pivots const&, Options const&);
+    template int64_t getri<T>(Matrix<T>&, Pivots const&, Options const&);                         \
+    template int64_t getri<T>(Matrix<T>&, Pivots const&, Matrix<T>&, Options const&);
 
 SLATE_SOLVE_INST(float)
 SLATE_SOLVE_INST(double)

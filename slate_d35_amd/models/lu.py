@@ -3,7 +3,7 @@ gecondest.cc, trtri.cc, trtrm.cc, trcondest.cc)."""
 from ._wrap import call
 
 __all__ = ["getrf", "getrf_nopiv", "getrf_tntpiv", "getrs", "getrs_nopiv", "gesv", "gesv_nopiv",
-           "gesv_mixed", "gesv_mixed_gmres", "gesv_rbt", "getri", "gecondest", "trtri", "trtrm",
+           "gesv_mixed", "gesv_mixed_gmres", "gesv_rbt", "gerbt", "getri", "gecondest", "trtri", "trtrm",
            "trcondest", "lu_factor", "lu_solve", "lu_solve_using_factor", "lu_inverse_using_factor",
            "lu_factor_nopiv", "lu_solve_nopiv", "lu_solve_using_factor_nopiv", "lu_rcondest_using_factor",
            "triangular_rcondest", "gbtrf", "gbtrs", "gbsv", "pbtrf", "pbtrs", "pbsv", "hetrf", "hetrs", "hesv",
@@ -52,11 +52,20 @@ def gesv_mixed_gmres(A, B, X, target=None, **kw):
 
 
 def gesv_rbt(A, B, X, target=None, **kw):
+    """Random-butterfly LU without pivoting + refinement; returns (info, iterations)."""
     return call("gesv_rbt", A, A, B, X, target=target, **kw)
 
 
-def getri(A, pivots, target=None, **kw):
+def getri(A, pivots, B=None, target=None, **kw):
+    """Inverse from the LU factors: in place, or out of place into B."""
+    if B is not None:
+        return call("getri_oop", A, A, pivots, B, target=target, **kw)
     return call("getri", A, A, pivots, target=target, **kw)
+
+
+def gerbt(A, depth=2, seed_u=0x5eed0001, seed_v=0x5eed0002, target=None, **kw):
+    """A := U^T A V with random butterflies of the given depth."""
+    return call("gerbt", A, A, depth, seed_u, seed_v, target=target, **kw)
 
 
 def gecondest(norm, A, anorm, target=None, **kw):

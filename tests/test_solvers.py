@@ -83,3 +83,41 @@ def test_posv_mixed_gmres():
     assert info == 0 and it >= 0
     x = s.to_numpy(X)
     assert np.linalg.norm(a @ x - b) / (np.linalg.norm(a) * np.linalg.norm(x)) < 1e-14
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_gesv_rbt(dtype):
+    n = 130
+    a = rnd(n, n, dtype, 21)
+    # a matrix whose leading entries make no-pivot LU unstable without the RBT
+    a[0, 0] = 1e-10
+    b = rnd(n, 2, dtype, 22)
+    A, B = s.from_numpy(a, nb=32), s.from_numpy(b, nb=32)
+    X = s.from_numpy(np.zeros_like(b), nb=32)
+    info, it = s.gesv_rbt(A, B, X)
+    assert info == 0
+    x = s.to_numpy(X)
+    eps = np.finfo(np.float32 if dtype in (np.float32, np.complex64) else np.float64).eps
+    assert np.linalg.norm(a @ x - b) / (np.linalg.norm(a) * np.linalg.norm(x)) < 100 * n * eps
+
+
+def test_gerbt_depths():
+    n = 97
+    a = rnd(n, n, np.float64, 23)
+    for depth in (1, 2, 3):
+        A = s.from_numpy(a, nb=16)
+        s.gerbt(A, depth)
+        ap = s.to_numpy(A)
+        # a similarity-free two-sided transform preserves rank / nonsingularity
+        assert abs(np.linalg.slogdet(ap)[1]) < np.inf
+        assert not np.allclose(ap, a)
+
+
+def test_getri_out_of_place():
+    n = 90
+    a = rnd(n, n, np.float64, 24) + n * np.eye(n)
+    A = s.from_numpy(a, nb=32)
+    info, piv = s.getrf(A)
+    B = s.from_numpy(np.zeros((n, n)), nb=32)
+    s.getri(A, piv, B)
+    assert relerr(s.to_numpy(B) @ a, np.eye(n)) < 1e-13
