@@ -28,8 +28,10 @@ HDRS      := $(wildcard csrc/include/slate_amd/*.hh) $(wildcard csrc/kernels/*.h
 LIB       := $(PKG)/libslate_amd.so
 PYMOD     := $(PKG)/_slate$(PY_EXT)
 TESTER    := build/slate_tester
+LAPACK_API    := $(PKG)/libslate_lapack_api.so
+SCALAPACK_API := $(PKG)/libslate_scalapack_api.so
 
-all: $(LIB) $(PYMOD)
+all: $(LIB) $(PYMOD) $(LAPACK_API) $(SCALAPACK_API)
 
 $(BUILD):
 	mkdir -p $(BUILD)
@@ -49,11 +51,20 @@ $(BUILD)/bind.o: csrc/python/bind.cc $(HDRS) | $(BUILD)
 $(PYMOD): $(BUILD)/bind.o $(LIB)
 	$(CXX) -shared -o $@ $(BUILD)/bind.o -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
 
+$(BUILD)/api_%.o: csrc/api/%.cc $(HDRS) | $(BUILD)
+	$(CXX) $(CXXFLAGS) -c $< -o $@
+
+$(LAPACK_API): $(BUILD)/api_lapack_api.o $(LIB)
+	$(CXX) -shared -o $@ $(BUILD)/api_lapack_api.o -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
+
+$(SCALAPACK_API): $(BUILD)/api_scalapack_api.o $(LIB)
+	$(CXX) -shared -o $@ $(BUILD)/api_scalapack_api.o -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
+
 tester: $(TESTER)
 $(TESTER): csrc/tools/tester.cc $(LIB)
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDLIBS)
 
 clean:
-	rm -rf build $(LIB) $(PYMOD)
+	rm -rf build $(LIB) $(PYMOD) $(LAPACK_API) $(SCALAPACK_API)
 
 .PHONY: all clean tester

@@ -277,7 +277,7 @@ public:
     static Matrix fromLAPACK(int64_t m, int64_t n, T* A, int64_t lda, int64_t nb, Loc loc = Loc::Host);
     /// Wrap a ScaLAPACK local array (2D block-cyclic on `grid`).
     static Matrix fromScaLAPACK(int64_t m, int64_t n, T* A, int64_t lld, int64_t mb, int64_t nb,
-                                GridPtr grid, Loc loc = Loc::Host);
+                                GridPtr grid, Loc loc = Loc::Host, int rsrc = 0, int csrc = 0);
     /// Wrap a device-resident local array (reference fromDevices).
     static Matrix fromDevices(int64_t m, int64_t n, T* dA, int64_t lld, int64_t mb, int64_t nb, GridPtr grid) {
         return fromScaLAPACK(m, n, dA, lld, mb, nb, grid, Loc::Device);

@@ -206,6 +206,9 @@ void hetrs(HermitianMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix
 template <typename T>
 int64_t hesv(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Options const& opts = {});
 
+/// op(A) X = B with getrf factors (op = NoTrans, Trans, ConjTrans).
+template <typename T>
+void getrs(Op trans, Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts = {});
 /// Out-of-place inverse from getrf factors (reference getriOOP.cc).
 template <typename T>
 int64_t getri(Matrix<T>& A, Pivots const& pivots, Matrix<T>& B, Options const& opts);

@@ -1,0 +1,240 @@
+// C API implementation (see slate_amd/c_api.h).  Reference capability:
+// src/c_api/wrappers.cc (generated there; hand-written here over the
+// simplified-API names).
+#include "slate_amd/c_api.h"
+#include "slate_amd/slate.hh"
+#include "slate_amd/device.hh"
+
+#include <complex>
+#include <cstring>
+#include <string>
+
+namespace {
+
+thread_local std::string g_last_error;
+
+template <typename F>
+auto guarded(F&& f, decltype(f()) fail) -> decltype(f()) {
+    try {
+        g_last_error.clear();
+        return f();
+    } catch (std::exception const& e) {
+        g_last_error = e.what();
+    } catch (...) {
+        g_last_error = "unknown exception";
+    }
+    return fail;
+}
+
+slate::Options to_opts(int n, slate_Options const* o) {
+    slate::Options r;
+    for (int i = 0; i < n; ++i) {
+        auto key = slate::Option(o[i].option);
+        if (key == slate::Option::Tolerance || key == slate::Option::PivotThreshold)
+            r[key] = slate::OptionValue(o[i].dvalue);
+        else
+            r[key] = slate::OptionValue(int64_t(o[i].ivalue));
+    }
+    return r;
+}
+
+template <typename T> struct CType;
+template <> struct CType<float> { using type = float; };
+template <> struct CType<double> { using type = double; };
+template <> struct CType<std::complex<float>> { using type = _slate_c32; };
+template <> struct CType<std::complex<double>> { using type = _slate_c64; };
+
+template <typename T>
+T from_c(typename CType<T>::type v) { T r; std::memcpy(&r, &v, sizeof(T)); return r; }
+
+}  // namespace
+
+struct slate_Pivots_struct { slate::Pivots p; };
+
+extern "C" {
+
+const char* slate_version(void) { return slate::version(); }
+const char* slate_last_error(void) { return g_last_error.c_str(); }
+int slate_device_available(void) { return slate::device::available() ? 1 : 0; }
+int slate_grid_size(void) { return slate::default_grid()->size(); }
+
+slate_Pivots slate_Pivots_create(void) { return new slate_Pivots_struct(); }
+void slate_Pivots_destroy(slate_Pivots p) { delete p; }
+int64_t slate_Pivots_size(slate_Pivots p) { return int64_t(p->p.size()); }
+
+}  // extern "C"
+
+#define SLATE_C_API_DEFINE(X, T)                                                                           \
+struct slate_Matrix_##X##_struct { slate::Matrix<T> A; };                                                  \
+struct slate_TriangularFactors_##X##_struct { slate::TriangularFactors<T> T_; };                           \
+extern "C" {                                                                                               \
+using X##_s = CType<T>::type;                                                                              \
+using X##_r = slate::real_type<T>;                                                                         \
+slate_Matrix_##X slate_Matrix_create_##X(int64_t m, int64_t n, int64_t nb) {                               \
+    return guarded([&]() -> slate_Matrix_##X {                                                             \
+        return new slate_Matrix_##X##_struct{slate::Matrix<T>(m, n, nb, nb, slate::default_grid())}; },   \
+        nullptr); }                                                                                        \
+slate_Matrix_##X slate_Matrix_create_fromLAPACK_##X(int64_t m, int64_t n, X##_s* A, int64_t lda, int64_t nb) { \
+    return guarded([&]() -> slate_Matrix_##X {                                                             \
+        return new slate_Matrix_##X##_struct{slate::Matrix<T>::fromLAPACK(m, n, (T*)A, lda, nb)}; }, nullptr); } \
+slate_Matrix_##X slate_Matrix_create_fromScaLAPACK_##X(int64_t m, int64_t n, X##_s* A, int64_t lld,        \
+                                                       int64_t mb, int64_t nb) {                           \
+    return guarded([&]() -> slate_Matrix_##X {                                                             \
+        return new slate_Matrix_##X##_struct{                                                              \
+            slate::Matrix<T>::fromScaLAPACK(m, n, (T*)A, lld, mb, nb, slate::default_grid())}; }, nullptr); } \
+void slate_Matrix_destroy_##X(slate_Matrix_##X A) { delete A; }                                           \
+void slate_Matrix_insertLocalTiles_##X(slate_Matrix_##X A, slate_Target t) {                              \
+    guarded([&]() { A->A.insertLocalTiles(slate::Target(t)); return 0; }, 0); }                           \
+void slate_Matrix_tileUpdateAllOrigin_##X(slate_Matrix_##X A) {                                           \
+    guarded([&]() { A->A.tileUpdateAllOrigin(); return 0; }, 0); }                                        \
+int64_t slate_Matrix_m_##X(slate_Matrix_##X A) { return A->A.m(); }                                       \
+int64_t slate_Matrix_n_##X(slate_Matrix_##X A) { return A->A.n(); }                                       \
+int64_t slate_Matrix_mt_##X(slate_Matrix_##X A) { return A->A.mt(); }                                     \
+int64_t slate_Matrix_nt_##X(slate_Matrix_##X A) { return A->A.nt(); }                                     \
+slate_Matrix_##X slate_Matrix_transpose_##X(slate_Matrix_##X A) {                                         \
+    return new slate_Matrix_##X##_struct{slate::transpose(A->A)}; }                                       \
+slate_Matrix_##X slate_Matrix_conj_transpose_##X(slate_Matrix_##X A) {                                    \
+    return new slate_Matrix_##X##_struct{slate::conj_transpose(A->A)}; }                                  \
+slate_Matrix_##X slate_Matrix_sub_##X(slate_Matrix_##X A, int64_t i1, int64_t i2, int64_t j1, int64_t j2) { \
+    return guarded([&]() -> slate_Matrix_##X {                                                             \
+        return new slate_Matrix_##X##_struct{A->A.sub(i1, i2, j1, j2)}; }, nullptr); }                     \
+int slate_Matrix_get_##X(slate_Matrix_##X A, X##_s* out, int64_t ld) {                                    \
+    return guarded([&]() {                                                                                 \
+        std::vector<T> full; slate::gather(A->A, full);                                                    \
+        for (int64_t j = 0; j < A->A.n(); ++j)                                                             \
+            for (int64_t i = 0; i < A->A.m(); ++i) ((T*)out)[i + j * ld] = full[i + j * A->A.m()];        \
+        return 0; }, -1); }                                                                                \
+int slate_Matrix_set_##X(slate_Matrix_##X A, X##_s const* in, int64_t ld) {                               \
+    return guarded([&]() {                                                                                 \
+        T const* p = (T const*)in;                                                                         \
+        slate::set<T>(std::function<T(int64_t, int64_t)>([&](int64_t i, int64_t j) { return p[i + j * ld]; }), \
+                      A->A, slate::Options{{slate::Option::Target, slate::Target::Host}});                 \
+        return 0; }, -1); }                                                                                \
+slate_TriangularFactors_##X slate_TriangularFactors_create_##X(void) {                                    \
+    return new slate_TriangularFactors_##X##_struct(); }                                                   \
+void slate_TriangularFactors_destroy_##X(slate_TriangularFactors_##X T_) { delete T_; }                    \
+int slate_multiply_##X(X##_s alpha, slate_Matrix_##X A, slate_Matrix_##X B, X##_s beta, slate_Matrix_##X C, \
+                       int no, slate_Options const* o) {                                                   \
+    return guarded([&]() { slate::gemm(from_c<T>(alpha), A->A, B->A, from_c<T>(beta), C->A, to_opts(no, o)); \
+                           return 0; }, -1); }                                                             \
+int slate_hermitian_multiply_##X(slate_Side side, X##_s alpha, slate_Uplo uplo, slate_Matrix_##X A,        \
+                                 slate_Matrix_##X B, X##_s beta, slate_Matrix_##X C, int no,               \
+                                 slate_Options const* o) {                                                 \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        slate::hemm(slate::Side(side), from_c<T>(alpha), H, B->A, from_c<T>(beta), C->A, to_opts(no, o));  \
+        return 0; }, -1); }                                                                                \
+int slate_rank_k_update_##X(X##_r alpha, slate_Matrix_##X A, X##_r beta, slate_Uplo uplo,                 \
+                            slate_Matrix_##X C, int no, slate_Options const* o) {                          \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), C->A);                          \
+        slate::herk(alpha, A->A, beta, H, to_opts(no, o)); return 0; }, -1); }                             \
+int slate_rank_2k_update_##X(X##_s alpha, slate_Matrix_##X A, slate_Matrix_##X B, X##_r beta,             \
+                             slate_Uplo uplo, slate_Matrix_##X C, int no, slate_Options const* o) {        \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), C->A);                          \
+        slate::her2k(from_c<T>(alpha), A->A, B->A, beta, H, to_opts(no, o)); return 0; }, -1); }           \
+int slate_triangular_multiply_##X(slate_Side side, X##_s alpha, slate_Uplo uplo, slate_Diag diag,         \
+                                  slate_Matrix_##X A, slate_Matrix_##X B, int no, slate_Options const* o) { \
+    return guarded([&]() { slate::TriangularMatrix<T> Tm(slate::Uplo(uplo), slate::Diag(diag), A->A);    \
+        slate::trmm(slate::Side(side), from_c<T>(alpha), Tm, B->A, to_opts(no, o)); return 0; }, -1); }   \
+int slate_triangular_solve_##X(slate_Side side, X##_s alpha, slate_Uplo uplo, slate_Diag diag,            \
+                               slate_Matrix_##X A, slate_Matrix_##X B, int no, slate_Options const* o) {   \
+    return guarded([&]() { slate::TriangularMatrix<T> Tm(slate::Uplo(uplo), slate::Diag(diag), A->A);    \
+        slate::trsm(slate::Side(side), from_c<T>(alpha), Tm, B->A, to_opts(no, o)); return 0; }, -1); }   \
+X##_r slate_norm_##X(slate_Norm nm, slate_Matrix_##X A, int no, slate_Options const* o) {                \
+    return guarded([&]() { return slate::norm(slate::Norm(nm), A->A, to_opts(no, o)); }, X##_r(-1)); }   \
+int64_t slate_lu_factor_##X(slate_Matrix_##X A, slate_Pivots P, int no, slate_Options const* o) {         \
+    return guarded([&]() { return slate::getrf(A->A, P->p, to_opts(no, o)); }, int64_t(-1)); }            \
+int64_t slate_lu_solve_##X(slate_Matrix_##X A, slate_Matrix_##X B, int no, slate_Options const* o) {      \
+    return guarded([&]() { slate::Pivots P; return slate::gesv(A->A, P, B->A, to_opts(no, o)); }, int64_t(-1)); } \
+int slate_lu_solve_using_factor_##X(slate_Matrix_##X A, slate_Pivots P, slate_Matrix_##X B, int no,       \
+                                    slate_Options const* o) {                                              \
+    return guarded([&]() { slate::getrs(A->A, P->p, B->A, to_opts(no, o)); return 0; }, -1); }            \
+int64_t slate_lu_inverse_using_factor_##X(slate_Matrix_##X A, slate_Pivots P, int no, slate_Options const* o) { \
+    return guarded([&]() { return slate::getri(A->A, P->p, to_opts(no, o)); }, int64_t(-1)); }            \
+X##_r slate_lu_rcondest_using_factor_##X(slate_Norm nm, slate_Matrix_##X A, X##_r anorm, int no,          \
+                                         slate_Options const* o) {                                         \
+    return guarded([&]() { return slate::gecondest(slate::Norm(nm), A->A, anorm, to_opts(no, o)); }, X##_r(-1)); } \
+int64_t slate_lu_factor_nopiv_##X(slate_Matrix_##X A, int no, slate_Options const* o) {                   \
+    return guarded([&]() { return slate::getrf_nopiv(A->A, to_opts(no, o)); }, int64_t(-1)); }            \
+int64_t slate_chol_factor_##X(slate_Uplo uplo, slate_Matrix_##X A, int no, slate_Options const* o) {      \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        return slate::potrf(H, to_opts(no, o)); }, int64_t(-1)); }                                         \
+int64_t slate_chol_solve_##X(slate_Uplo uplo, slate_Matrix_##X A, slate_Matrix_##X B, int no,             \
+                             slate_Options const* o) {                                                     \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        return slate::posv(H, B->A, to_opts(no, o)); }, int64_t(-1)); }                                    \
+int slate_chol_solve_using_factor_##X(slate_Uplo uplo, slate_Matrix_##X A, slate_Matrix_##X B, int no,    \
+                                      slate_Options const* o) {                                            \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        slate::potrs(H, B->A, to_opts(no, o)); return 0; }, -1); }                                         \
+int64_t slate_chol_inverse_using_factor_##X(slate_Uplo uplo, slate_Matrix_##X A, int no,                  \
+                                            slate_Options const* o) {                                      \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        return slate::potri(H, to_opts(no, o)); }, int64_t(-1)); }                                         \
+X##_r slate_chol_rcondest_using_factor_##X(slate_Norm nm, slate_Uplo uplo, slate_Matrix_##X A,            \
+                                           X##_r anorm, int no, slate_Options const* o) {                  \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        return slate::pocondest(slate::Norm(nm), H, anorm, to_opts(no, o)); }, X##_r(-1)); }               \
+int64_t slate_indefinite_solve_##X(slate_Uplo uplo, slate_Matrix_##X A, slate_Matrix_##X B, int no,       \
+                                   slate_Options const* o) {                                               \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        std::vector<int64_t> ip; return slate::hesv(H, ip, B->A, to_opts(no, o)); }, int64_t(-1)); }       \
+int slate_qr_factor_##X(slate_Matrix_##X A, slate_TriangularFactors_##X T_, int no, slate_Options const* o) { \
+    return guarded([&]() { slate::geqrf(A->A, T_->T_, to_opts(no, o)); return 0; }, -1); }               \
+int slate_qr_multiply_by_q_##X(slate_Side side, slate_Op op, slate_Matrix_##X A,                          \
+                               slate_TriangularFactors_##X T_, slate_Matrix_##X C, int no,                 \
+                               slate_Options const* o) {                                                   \
+    return guarded([&]() { slate::unmqr(slate::Side(side), slate::Op(op), A->A, T_->T_, C->A,            \
+                                        to_opts(no, o)); return 0; }, -1); }                               \
+int slate_lq_factor_##X(slate_Matrix_##X A, slate_TriangularFactors_##X T_, int no, slate_Options const* o) { \
+    return guarded([&]() { slate::gelqf(A->A, T_->T_, to_opts(no, o)); return 0; }, -1); }               \
+int slate_lq_multiply_by_q_##X(slate_Side side, slate_Op op, slate_Matrix_##X A,                          \
+                               slate_TriangularFactors_##X T_, slate_Matrix_##X C, int no,                 \
+                               slate_Options const* o) {                                                   \
+    return guarded([&]() { slate::unmlq(slate::Side(side), slate::Op(op), A->A, T_->T_, C->A,            \
+                                        to_opts(no, o)); return 0; }, -1); }                               \
+int slate_least_squares_solve_##X(slate_Matrix_##X A, slate_Matrix_##X BX, int no, slate_Options const* o) { \
+    return guarded([&]() { slate::TriangularFactors<T> Tf; slate::gels(A->A, Tf, BX->A, to_opts(no, o)); \
+                           return 0; }, -1); }                                                             \
+int slate_hermitian_eig_##X(slate_Uplo uplo, slate_Matrix_##X A, X##_r* Lambda, slate_Matrix_##X Z, int no, \
+                            slate_Options const* o) {                                                      \
+    return guarded([&]() { slate::HermitianMatrix<T> H(slate::Uplo(uplo), A->A);                          \
+        std::vector<X##_r> L; slate::Matrix<T> Zm = Z ? Z->A : slate::Matrix<T>();                         \
+        slate::heev(H, L, Zm, to_opts(no, o)); std::copy(L.begin(), L.end(), Lambda); return 0; }, -1); }  \
+int slate_svd_##X(slate_Matrix_##X A, X##_r* Sigma, slate_Matrix_##X U, slate_Matrix_##X VT, int no,      \
+                  slate_Options const* o) {                                                                \
+    return guarded([&]() { std::vector<X##_r> S;                                                          \
+        slate::Matrix<T> Um = U ? U->A : slate::Matrix<T>(), Vm = VT ? VT->A : slate::Matrix<T>();        \
+        slate::svd(A->A, S, Um, Vm, to_opts(no, o)); std::copy(S.begin(), S.end(), Sigma); return 0; }, -1); } \
+int slate_copy_##X(slate_Matrix_##X A, slate_Matrix_##X B, int no, slate_Options const* o) {              \
+    return guarded([&]() { slate::copy<T, T>(A->A, B->A, to_opts(no, o)); return 0; }, -1); }             \
+int slate_add_##X(X##_s alpha, slate_Matrix_##X A, X##_s beta, slate_Matrix_##X B, int no,                \
+                  slate_Options const* o) {                                                                \
+    return guarded([&]() { slate::add(from_c<T>(alpha), A->A, from_c<T>(beta), B->A, to_opts(no, o));     \
+                           return 0; }, -1); }                                                             \
+int slate_scale_##X(X##_r numer, X##_r denom, slate_Matrix_##X A, int no, slate_Options const* o) {       \
+    return guarded([&]() { slate::scale(numer, denom, A->A, to_opts(no, o)); return 0; }, -1); }          \
+int slate_set_##X(X##_s offdiag, X##_s diag, slate_Matrix_##X A, int no, slate_Options const* o) {        \
+    return guarded([&]() { slate::set(from_c<T>(offdiag), from_c<T>(diag), A->A, to_opts(no, o)); return 0; }, -1); } \
+}
+
+SLATE_C_API_DEFINE(r32, float)
+SLATE_C_API_DEFINE(r64, double)
+SLATE_C_API_DEFINE(c32, std::complex<float>)
+SLATE_C_API_DEFINE(c64, std::complex<double>)
+
+extern "C" {
+int64_t slate_lu_solve_mixed_r64(slate_Matrix_r64 A, slate_Matrix_r64 B, slate_Matrix_r64 X, int* iter, int no,
+                                 slate_Options const* o) {
+    return guarded([&]() { slate::Pivots P; int it = 0;
+        int64_t info = slate::gesv_mixed(A->A, P, B->A, X->A, it, to_opts(no, o));
+        if (iter) *iter = it;
+        return info; }, int64_t(-1));
+}
+int64_t slate_chol_solve_mixed_r64(slate_Uplo uplo, slate_Matrix_r64 A, slate_Matrix_r64 B, slate_Matrix_r64 X,
+                                   int* iter, int no, slate_Options const* o) {
+    return guarded([&]() { slate::HermitianMatrix<double> H(slate::Uplo(uplo), A->A); int it = 0;
+        int64_t info = slate::posv_mixed(H, B->A, X->A, it, to_opts(no, o));
+        if (iter) *iter = it;
+        return info; }, int64_t(-1));
+}
+}  // extern "C"

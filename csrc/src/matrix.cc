@@ -237,8 +237,8 @@ Matrix<T> Matrix<T>::fromLAPACK(int64_t m, int64_t n, T* A, int64_t lda, int64_t
 
 template <typename T>
 Matrix<T> Matrix<T>::fromScaLAPACK(int64_t m, int64_t n, T* A, int64_t lld, int64_t mb, int64_t nb,
-                                   GridPtr grid, Loc loc) {
-    Matrix<T> M(m, n, mb, nb, grid ? grid : default_grid());
+                                   GridPtr grid, Loc loc, int rsrc, int csrc) {
+    Matrix<T> M(m, n, mb, nb, grid ? grid : default_grid(), rsrc, csrc);
     M.storage_->attach(A, lld, loc);
     return M;
 }

@@ -36,6 +36,25 @@ void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const
     trsm(Side::Left, T(1), tri<T>(Uplo::Upper, Diag::NonUnit, A), B, opts);
 }
 
+/// op(A) X = B with the getrf factors; op = Trans / ConjTrans:
+/// A^H = U^H L^H P  =>  X = P^T L^{-H} U^{-H} B.
+template <typename T>
+void getrs(Op trans, Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
+    if (trans == Op::NoTrans) { getrs(A, pivots, B, opts); return; }
+    trace::Block tb("getrs_trans");
+    Target target = resolve_target(opts);
+    auto L = tri<T>(Uplo::Lower, Diag::Unit, A);
+    auto U = tri<T>(Uplo::Upper, Diag::NonUnit, A);
+    if (trans == Op::Trans) {
+        trsm(Side::Left, T(1), transpose(U), B, opts);
+        trsm(Side::Left, T(1), transpose(L), B, opts);
+    } else {
+        trsm(Side::Left, T(1), conj_transpose(U), B, opts);
+        trsm(Side::Left, T(1), conj_transpose(L), B, opts);
+    }
+    apply_pivots(pivots, A, B, target, false);
+}
+
 template <typename T>
 void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("getrs_nopiv");
@@ -294,6 +313,7 @@ int64_t getri(Matrix<T>& A, Pivots const& pivots, Matrix<T>& B, Options const& o
 //------------------------------------------------------------------------------
 #define SLATE_SOLVE_INST(T)                                                                     \
     template void getrs<T>(Matrix<T> const&, Pivots const&, Matrix<T>&, Options const&);       \
+    template void getrs<T>(Op, Matrix<T> const&, Pivots const&, Matrix<T>&, Options const&);   \
     template void getrs_nopiv<T>(Matrix<T> const&, Matrix<T>&, Options const&);                \
     template int64_t gesv<T>(Matrix<T>&, Pivots&, Matrix<T>&, Options const&);                 \
     template int64_t gesv_nopiv<T>(Matrix<T>&, Matrix<T>&, Options const&);                    \
