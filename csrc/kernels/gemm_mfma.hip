@@ -232,26 +232,41 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         __syncthreads();
     }
 
-    // epilogue: lane&15 runs along M (contiguous in column-major C)
+    // epilogue: lane&15 runs along M (contiguous in column-major C).  For
+    // beta != 0 the 16 C values of one accumulator row are loaded together
+    // before any store so the loads overlap instead of serializing.
     const bool beta_zero = (beta == T(0));
+    constexpr int JB = 2;      // accumulator columns per load batch (8 values)
+    auto inside = [&](int64_t gm, int64_t gn) {
+        bool in = gm < m && gn < n;
+        if constexpr (TRI == 'L') in = in && gm >= gn;
+        if constexpr (TRI == 'U') in = in && gm <= gn;
+        return in;
+    };
     #pragma unroll
     for (int i = 0; i < TM; ++i) {
         const int64_t gm = m0 + wm * WTM + i * 16 + (lane & 15);
         #pragma unroll
-        for (int j = 0; j < TN; ++j) {
+        for (int j0 = 0; j0 < TN; j0 += JB) {
+            T cv[JB][4];
             #pragma unroll
-            for (int r = 0; r < 4; ++r) {
-                const int64_t gn = n0 + wn * WTN + j * 16 + M::row(lane, r);
-                bool in = gm < m && gn < n;
-                if constexpr (TRI == 'L') in = in && gm >= gn;
-                if constexpr (TRI == 'U') in = in && gm <= gn;
-                if (in) {
-                    T* c = C + gm + gn * ldc;
-                    T v = alpha * acc[i][j][r];
-                    if (!beta_zero) v += beta * (*c);
-                    *c = v;
+            for (int j = 0; j < JB; ++j)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gn = n0 + wn * WTN + (j0 + j) * 16 + M::row(lane, r);
+                    cv[j][r] = (!beta_zero && inside(gm, gn)) ? C[gm + gn * ldc] : T(0);
                 }
-            }
+            #pragma unroll
+            for (int j = 0; j < JB; ++j)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gn = n0 + wn * WTN + (j0 + j) * 16 + M::row(lane, r);
+                    if (inside(gm, gn)) {
+                        T v = alpha * acc[i][j0 + j][r];
+                        if (!beta_zero) v += beta * cv[j][r];
+                        C[gm + gn * ldc] = v;
+                    }
+                }
         }
     }
 }
