@@ -21,6 +21,8 @@
 #include "device_common.hh"
 #include "kernels.hh"
 
+#include <cstdlib>
+
 namespace slate_amd {
 namespace dev {
 
@@ -46,12 +48,12 @@ template <> struct Mfma<float> {
 
 // Load a BX x BK operand tile into registers. Element (x, kk) of the operand
 // lives at X[x*sx + kk*sk]; KCONTIG means sk == 1 (else sx == 1).
-template <typename T, int BX, int BK, bool KCONTIG>
+template <typename T, int BX, int BK, bool KCONTIG, int NTHR = 256>
 struct TileLoader {
     static constexpr int VEC = 16 / sizeof(T);
     static constexpr int NV  = BX * BK / VEC;   // vectors per tile
-    static constexpr int NVT = NV / 256;        // vectors per thread
-    static_assert(NV % 256 == 0, "tile must split evenly over 256 threads");
+    static constexpr int NVT = NV / NTHR;       // vectors per thread
+    static_assert(NV % NTHR == 0, "tile must split evenly over the workgroup");
     T r[NVT][VEC];
 
     __device__ inline void coords(int v, int& x, int& kk) const {
@@ -73,7 +75,7 @@ struct TileLoader {
             #pragma unroll
             for (int i = 0; i < NVT; ++i) {
                 int x, kk;
-                coords(tid + 256 * i, x, kk);
+                coords(tid + NTHR * i, x, kk);
                 const T* p = KCONTIG ? X + (k0 + kk) + (x0 + x) * ld
                                      : X + (x0 + x) + (k0 + kk) * ld;
                 if constexpr (sizeof(T) == 8) {
@@ -90,7 +92,7 @@ struct TileLoader {
             #pragma unroll
             for (int i = 0; i < NVT; ++i) {
                 int x, kk;
-                coords(tid + 256 * i, x, kk);
+                coords(tid + NTHR * i, x, kk);
                 #pragma unroll
                 for (int e = 0; e < VEC; ++e) {
                     int64_t gx = x0 + x + (KCONTIG ? 0 : e);
@@ -109,7 +111,7 @@ struct TileLoader {
         #pragma unroll
         for (int i = 0; i < NVT; ++i) {
             int x, kk;
-            coords(tid + 256 * i, x, kk);
+            coords(tid + NTHR * i, x, kk);
             if constexpr (KCONTIG) {
                 #pragma unroll
                 for (int e = 0; e < VEC; ++e)
@@ -123,10 +125,71 @@ struct TileLoader {
     }
 };
 
+// Epilogue shared by the MFMA GEMM kernels: lane&15 runs along M (contiguous
+// in column-major C).  For beta != 0 the C values of two accumulator columns
+// are loaded together before any store so the loads overlap.
+template <typename T, int TM, int TN, char TRI>
+__device__ inline void gemm_epilogue(typename Mfma<T>::acc_t (&acc)[TM][TN], int64_t m, int64_t n, T alpha,
+                                     T beta, T* __restrict__ C, int64_t ldc, int64_t wm0, int64_t wn0, int lane) {
+    using M = Mfma<T>;
+    const bool beta_zero = (beta == T(0));
+    constexpr int JB = 2;
+    auto inside = [&](int64_t gm, int64_t gn) {
+        bool in = gm < m && gn < n;
+        if constexpr (TRI == 'L') in = in && gm >= gn;
+        if constexpr (TRI == 'U') in = in && gm <= gn;
+        return in;
+    };
+    #pragma unroll
+    for (int i = 0; i < TM; ++i) {
+        const int64_t gm = wm0 + i * 16 + (lane & 15);
+        #pragma unroll
+        for (int j0 = 0; j0 < TN; j0 += JB) {
+            T cv[JB][4];
+            #pragma unroll
+            for (int j = 0; j < JB; ++j)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gn = wn0 + (j0 + j) * 16 + M::row(lane, r);
+                    cv[j][r] = (!beta_zero && inside(gm, gn)) ? C[gm + gn * ldc] : T(0);
+                }
+            #pragma unroll
+            for (int j = 0; j < JB; ++j)
+                #pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gn = wn0 + (j0 + j) * 16 + M::row(lane, r);
+                    if (inside(gm, gn)) {
+                        T v = alpha * acc[i][j0 + j][r];
+                        if (!beta_zero) v += beta * cv[j][r];
+                        C[gm + gn * ldc] = v;
+                    }
+                }
+        }
+    }
+}
+
+// Tile order: XCD-aware bijective remap, then GROUP tile-rows at a time.
+__device__ inline void gemm_tile_coords(int64_t m, int64_t n, int BM, int BN, int& tm, int& tn) {
+    const int mt = (int)((m + BM - 1) / BM), nt = (int)((n + BN - 1) / BN);
+    const int nblk = mt * nt;
+    int bid = xcd_remap(blockIdx.x, nblk);
+    constexpr int GROUP = 8;
+    int group = bid / (GROUP * nt);
+    int first_m = group * GROUP;
+    int gsize = min(mt - first_m, GROUP);
+    int within = bid % (GROUP * nt);
+    tm = first_m + within % gsize;
+    tn = within / gsize;
+}
+
 // TRI: 0 = full C; 'L' / 'U' = only the lower / upper triangle of a square C
 // is computed (tiles outside it are never launched; diagonal tiles are masked).
-template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI>
-__global__ __launch_bounds__(256, 2)
+// NTHR = 64 * (BM/64) * (BN/64): one wave per 64 x 64 sub-tile.  128 x 128
+// (4 waves, 2 workgroups per CU) or 256 x 128 (8 waves, 1 workgroup per CU:
+// 25% less operand traffic per flop for large C).
+template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI, int WTN_ = 64>
+__global__ __launch_bounds__(64 * (BM / 64) * (BN / WTN_),
+    (2 * BK * (BM + BN + 32) * sizeof(T) > 81920) ? 1 : 512 / (64 * (BM / 64) * (BN / WTN_)))
 void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
                       const T* __restrict__ A, int64_t lda, int64_t sA,
                       const T* __restrict__ B, int64_t ldb, int64_t sB,
@@ -137,7 +200,9 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     using acc_t = typename M::acc_t;
     constexpr int PAD = 16;
     constexpr int LDA_S = BM + PAD, LDB_S = BN + PAD;
-    constexpr int WTM = BM / 2, WTN = BN / 2;       // per-wave tile (2x2 waves)
+    constexpr int WTM = 64, WTN = WTN_;             // per-wave tile
+    constexpr int WN = BN / WTN;                     // waves along N
+    constexpr int NTHR = 64 * (BM / WTM) * WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;     // MFMA tiles per wave
     constexpr int A_ELEMS = BK * LDA_S, B_ELEMS = BK * LDB_S;
 
@@ -174,7 +239,7 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
 
     const int lane = threadIdx.x & 63;
     const int wid  = threadIdx.x >> 6;
-    const int wm = wid >> 1, wn = wid & 1;
+    const int wm = wid / WN, wn = wid % WN;
 
     acc_t acc[TM][TN];
     #pragma unroll
@@ -183,8 +248,8 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         for (int j = 0; j < TN; ++j)
             acc[i][j] = acc_t{0, 0, 0, 0};
 
-    TileLoader<T, BM, BK, A_KC> la;
-    TileLoader<T, BN, BK, B_KC> lb;
+    TileLoader<T, BM, BK, A_KC, NTHR> la;
+    TileLoader<T, BN, BK, B_KC, NTHR> lb;
     const bool mfull = (m0 + BM <= m), nfull = (n0 + BN <= n);
 
     const int KT = (int)((k + BK - 1) / BK);
@@ -232,43 +297,32 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         __syncthreads();
     }
 
-    // epilogue: lane&15 runs along M (contiguous in column-major C).  For
-    // beta != 0 the 16 C values of one accumulator row are loaded together
-    // before any store so the loads overlap instead of serializing.
-    const bool beta_zero = (beta == T(0));
-    constexpr int JB = 2;      // accumulator columns per load batch (8 values)
-    auto inside = [&](int64_t gm, int64_t gn) {
-        bool in = gm < m && gn < n;
-        if constexpr (TRI == 'L') in = in && gm >= gn;
-        if constexpr (TRI == 'U') in = in && gm <= gn;
-        return in;
-    };
-    #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-        const int64_t gm = m0 + wm * WTM + i * 16 + (lane & 15);
-        #pragma unroll
-        for (int j0 = 0; j0 < TN; j0 += JB) {
-            T cv[JB][4];
-            #pragma unroll
-            for (int j = 0; j < JB; ++j)
-                #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t gn = n0 + wn * WTN + (j0 + j) * 16 + M::row(lane, r);
-                    cv[j][r] = (!beta_zero && inside(gm, gn)) ? C[gm + gn * ldc] : T(0);
-                }
-            #pragma unroll
-            for (int j = 0; j < JB; ++j)
-                #pragma unroll
-                for (int r = 0; r < 4; ++r) {
-                    const int64_t gn = n0 + wn * WTN + (j0 + j) * 16 + M::row(lane, r);
-                    if (inside(gm, gn)) {
-                        T v = alpha * acc[i][j0 + j][r];
-                        if (!beta_zero) v += beta * cv[j][r];
-                        C[gm + gn * ldc] = v;
-                    }
-                }
-        }
-    }
+    gemm_epilogue<T, TM, TN, TRI>(acc, m, n, alpha, beta, C, ldc, m0 + wm * WTM, n0 + wn * WTN, lane);
+}
+
+template <typename T, bool A_KC, bool B_KC, char TRI, int BM, int BN, int BK = 16, int WTN = 64>
+static void launch_tile(int64_t m, int64_t n, int64_t k, T alpha,
+                        const T* A, int64_t lda, int64_t sA,
+                        const T* B, int64_t ldb, int64_t sB,
+                        T beta, T* C, int64_t ldc, int64_t sC,
+                        int64_t batch, bool aligned, hipStream_t stream)
+{
+    constexpr int NTHR = 64 * (BM / 64) * (BN / WTN);
+    int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
+    int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
+    dim3 grid((unsigned)nblk, (unsigned)batch);
+    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN>), grid, dim3(NTHR), 0, stream,
+                       m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+}
+
+// fp32 only: 256 x 128 tiles (8 waves, 1 workgroup per CU) cut operand
+// traffic per flop by 25%, worth +5% for large sgemm; measured neutral-to-worse
+// for fp64, whose 64-cycle MFMA leaves the 128 x 128 tile compute-bound.
+static bool big_tiles(int64_t m, int64_t n, int64_t batch) {
+    static int env = [] { const char* e = std::getenv("SLATE_GEMM_BIG"); return e ? std::atoi(e) : 1; }();
+    if (!env) return false;
+    // only when they still give >= 2 waves of workgroups over 256 CUs
+    return m >= 512 && ((m + 255) / 256) * ((n + 127) / 128) * batch >= 512;
 }
 
 template <typename T, bool A_KC, bool B_KC, char TRI = 0>
@@ -278,16 +332,19 @@ static void launch_gemm(int64_t m, int64_t n, int64_t k, T alpha,
                         T beta, T* C, int64_t ldc, int64_t sC,
                         int64_t batch, hipStream_t stream)
 {
-    constexpr int BM = 128, BN = 128, BK = 16;
     constexpr int VEC = 16 / sizeof(T);
     auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };
     bool aligned = al(A) && al(B) && (lda % VEC == 0) && (ldb % VEC == 0)
                 && (batch == 1 || (sA % VEC == 0 && sB % VEC == 0));
-    int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
-    int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
-    dim3 grid((unsigned)nblk, (unsigned)batch);
-    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI>), grid, dim3(256), 0, stream,
-                       m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+    if constexpr (TRI == 0 && sizeof(T) == 4) {
+        if (big_tiles(m, n, batch)) {
+            launch_tile<T, A_KC, B_KC, TRI, 256, 128>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                                                      batch, aligned, stream);
+            return;
+        }
+    }
+    launch_tile<T, A_KC, B_KC, TRI, 128, 128>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+                                                  batch, aligned, stream);
 }
 
 template <typename T>
