@@ -278,6 +278,20 @@ __global__ void permute_rows_kernel(int64_t n, T* A, int64_t lda, const int64_t*
     }
 }
 
+// Row gather / scatter between a column strip of A and a packed buffer
+// (buf is count x n, column-major, ld = count): gather buf(t, :) = A(idx[t], :),
+// scatter A(idx[t], :) = buf(t, :).  Used by the distributed row exchange.
+template <typename T>
+__global__ void rows_pack_kernel(int64_t n, T* A, int64_t lda, const int64_t* idx, int count, T* buf,
+                                 int scatter) {
+    const int64_t j = blockIdx.y;
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= count || j >= n) return;
+    T* a = A + idx[t] + j * lda;
+    T* b = buf + t + j * (int64_t)count;
+    if (scatter) *a = *b; else *b = *a;
+}
+
 // Sequential interchanges applied to a column strip (LAPACK laswp semantics,
 // ipiv 0-based absolute rows), used when the pivot count is tiny.
 template <typename T>
@@ -354,6 +368,13 @@ void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_
 }
 
 template <typename T>
+void rows_pack(int64_t n, T* A, int64_t lda, const int64_t* idx, int count, T* buf, bool scatter, hipStream_t s) {
+    if (n <= 0 || count <= 0) return;
+    dim3 grid((unsigned)((count + 63) / 64), (unsigned)n);
+    hipLaunchKernelGGL(rows_pack_kernel<T>, grid, dim3(64), 0, s, n, A, lda, idx, count, buf, scatter ? 1 : 0);
+}
+
+template <typename T>
 void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* ipiv, int64_t ipiv_offset, hipStream_t s) {
     if (n <= 0 || k2 <= k1) return;
     hipLaunchKernelGGL(laswp_kernel<T>, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, n, A, lda, k1, k2, ipiv, ipiv_offset);
@@ -367,7 +388,8 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void trtri_diag<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t);   \
     template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \
     template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
-    template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);
+    template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);  \
+    template void rows_pack<T>(int64_t, T*, int64_t, const int64_t*, int, T*, bool, hipStream_t);
 
 SLATE_INST_AUX(float)
 SLATE_INST_AUX(double)

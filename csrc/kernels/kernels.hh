@@ -52,6 +52,10 @@ void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset
 template <typename T>
 void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
                   const int* npairs, int max_pairs, hipStream_t s);
+/// buf(t, :) = A(idx[t], :) (gather) or A(idx[t], :) = buf(t, :) (scatter);
+/// buf is count x n column-major; idx device array.
+template <typename T>
+void rows_pack(int64_t n, T* A, int64_t lda, const int64_t* idx, int count, T* buf, bool scatter, hipStream_t s);
 template <typename T>
 void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* ipiv, int64_t ipiv_offset, hipStream_t s);
 

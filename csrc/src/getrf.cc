@@ -78,9 +78,6 @@ void permute_rows_dist(BaseMatrix<T> const& A, RowPairs const& P, int64_t c0, in
         else if (os == me) send_src[od].push_back(P.src[t]);
         else if (od == me) recv_dst[os].push_back(P.dst[t]);
     }
-    if (ncols <= 0) {
-        // still participate in the exchange with zero-size messages
-    }
     size_t nsend = 0, nrecv = 0;
     for (int r = 0; r < p; ++r) { nsend += send_src[r].size(); nrecv += recv_dst[r].size(); }
     size_t nloc = loc_src.size();
@@ -88,33 +85,82 @@ void permute_rows_dist(BaseMatrix<T> const& A, RowPairs const& P, int64_t c0, in
     T* sb = buf.data();
     T* lb_ = sb + nsend * ncols;
     T* rb = lb_ + nloc * ncols;
-    // gather rows (each row: ncols elements with stride ld -> contiguous)
-    auto grab = [&](int64_t gr, T* dst) {
-        lb::copy2d(c, 1, ncols, la.ptr + lrow(gr) + c0 * la.ld, la.ld, dst, 1);
-    };
-    auto put = [&](int64_t gr, T const* src) {
-        lb::copy2d(c, 1, ncols, src, 1, la.ptr + lrow(gr) + c0 * la.ld, la.ld);
-    };
-    size_t k = 0;
-    for (int r = 0; r < p; ++r) for (int64_t gr : send_src[r]) grab(gr, sb + (k++) * ncols);
-    for (size_t t = 0; t < nloc; ++t) grab(loc_src[t], lb_ + t * ncols);
-    if (p > 1) {
-        std::vector<Comm::P2P> ops;
-        size_t so = 0, ro = 0;
-        for (int r = 0; r < p; ++r) {
-            if (!send_src[r].empty()) ops.push_back({sb + so * ncols, send_src[r].size() * ncols, r, true});
-            so += send_src[r].size();
+    // row lists: send rows (grouped by destination), local moves, received rows
+    std::vector<int64_t> snd, lsrc, ldst, rcv;
+    for (int r = 0; r < p; ++r) for (int64_t gr : send_src[r]) snd.push_back(lrow(gr));
+    for (size_t t = 0; t < nloc; ++t) { lsrc.push_back(lrow(loc_src[t])); ldst.push_back(lrow(loc_dst[t])); }
+    for (int r = 0; r < p; ++r) for (int64_t gr : recv_dst[r]) rcv.push_back(lrow(gr));
+    T* Ablk = la.ptr + c0 * la.ld;
+    // packed buffers are (rows x ncols) with ld = rows: message r is then not
+    // contiguous, so pack per destination / source block into its own slab
+    if (c.dev()) {
+        Work<int64_t> didx(Target::Devices, std::max<size_t>(1, snd.size() + 2 * nloc + rcv.size()));
+        std::vector<int64_t> all;
+        all.insert(all.end(), snd.begin(), snd.end());
+        all.insert(all.end(), lsrc.begin(), lsrc.end());
+        all.insert(all.end(), ldst.begin(), ldst.end());
+        all.insert(all.end(), rcv.begin(), rcv.end());
+        if (!all.empty()) device::memcpy_async(didx.data(), all.data(), all.size() * sizeof(int64_t), c.stream);
+        int64_t* d_snd = didx.data();
+        int64_t* d_lsrc = d_snd + snd.size();
+        int64_t* d_ldst = d_lsrc + nloc;
+        int64_t* d_rcv = d_ldst + nloc;
+        using DT = slate_amd::dev::dev_t<T>;
+        auto pk = [&](int64_t* idx, size_t cnt, T* buf, bool scat) {
+            if (cnt) slate_amd::dev::rows_pack<DT>(ncols, slate_amd::dev::dptr(Ablk), la.ld, idx, int(cnt),
+                                                   slate_amd::dev::dptr(buf), scat, c.stream);
+        };
+        // per-peer slabs so each message is contiguous
+        size_t so = 0;
+        for (int r = 0; r < p; ++r) { pk(d_snd + so, send_src[r].size(), sb + so * ncols, false); so += send_src[r].size(); }
+        pk(d_lsrc, nloc, lb_, false);
+        if (p > 1 && ncols > 0) {
+            std::vector<Comm::P2P> ops;
+            size_t s2 = 0, r2 = 0;
+            for (int r = 0; r < p; ++r) {
+                if (!send_src[r].empty()) ops.push_back({sb + s2 * ncols, send_src[r].size() * ncols, r, true});
+                s2 += send_src[r].size();
+            }
+            for (int r = 0; r < p; ++r) {
+                if (!recv_dst[r].empty()) ops.push_back({rb + r2 * ncols, recv_dst[r].size() * ncols, r, false});
+                r2 += recv_dst[r].size();
+            }
+            g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
         }
-        for (int r = 0; r < p; ++r) {
-            if (!recv_dst[r].empty()) ops.push_back({rb + ro * ncols, recv_dst[r].size() * ncols, r, false});
-            ro += recv_dst[r].size();
-        }
-        if (ncols > 0) g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+        pk(d_ldst, nloc, lb_, true);
+        size_t ro = 0;
+        for (int r = 0; r < p; ++r) { pk(d_rcv + ro, recv_dst[r].size(), rb + ro * ncols, true); ro += recv_dst[r].size(); }
+        slate_hip_call(hipStreamSynchronize(c.stream));
+        return;
     }
-    for (size_t t = 0; t < nloc; ++t) put(loc_dst[t], lb_ + t * ncols);
-    k = 0;
-    for (int r = 0; r < p; ++r) for (int64_t gr : recv_dst[r]) put(gr, rb + (k++) * ncols);
-    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    // host: same slab layout, plain loops
+    auto hpk = [&](int64_t const* idx, size_t cnt, T* buf, bool scat) {
+        for (int64_t j = 0; j < ncols; ++j)
+            for (size_t t = 0; t < cnt; ++t) {
+                T& a = Ablk[idx[t] + j * la.ld];
+                T& b = buf[t + j * cnt];
+                if (scat) a = b; else b = a;
+            }
+    };
+    size_t so = 0;
+    for (int r = 0; r < p; ++r) { hpk(snd.data() + so, send_src[r].size(), sb + so * ncols, false); so += send_src[r].size(); }
+    hpk(lsrc.data(), nloc, lb_, false);
+    if (p > 1 && ncols > 0) {
+        std::vector<Comm::P2P> ops;
+        size_t s2 = 0, r2 = 0;
+        for (int r = 0; r < p; ++r) {
+            if (!send_src[r].empty()) ops.push_back({sb + s2 * ncols, send_src[r].size() * ncols, r, true});
+            s2 += send_src[r].size();
+        }
+        for (int r = 0; r < p; ++r) {
+            if (!recv_dst[r].empty()) ops.push_back({rb + r2 * ncols, recv_dst[r].size() * ncols, r, false});
+            r2 += recv_dst[r].size();
+        }
+        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+    }
+    hpk(ldst.data(), nloc, lb_, true);
+    size_t ro = 0;
+    for (int r = 0; r < p; ++r) { hpk(rcv.data() + ro, recv_dst[r].size(), rb + ro * ncols, true); ro += recv_dst[r].size(); }
 }
 
 enum class PanelMode { Partial, Tournament, NoPiv };
