@@ -34,6 +34,7 @@ from slate_d35_amd.utils import flops as F  # noqa: E402
 
 METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
 ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
+EXTRA = ["dgesv_mixed"]  # BASELINE config 5; run with --routines dgesv_mixed
 
 
 def parse():
@@ -41,8 +42,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--dim", "--n", dest="n", type=int, default=65536)
     ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("--nb-per", default="", help="per-routine nb overrides, e.g. dgeqrf=256,dgetrf=512")
     ap.add_argument("--routines", default=",".join(ALL))
     ap.add_argument("--p", type=int, default=0)
     ap.add_argument("--q", type=int, default=0)
@@ -63,7 +65,8 @@ def main():
     target = "d" if s.device_available() else "h"
     p, q = (a.p, a.q) if a.p and a.q else s.choose_grid(world)
     grid = s.init_grid(p, q)
-    n, nb = a.n, a.nb
+    n = a.n
+    nb_per = {k: int(v) for k, v in (kv.split("=") for kv in a.nb_per.split(",") if kv)}
     opts = dict(target=target, lookahead=a.lookahead)
 
     def barrier_sync():
@@ -84,6 +87,7 @@ def main():
     routines = [r.strip() for r in a.routines.split(",") if r.strip()]
     for rname in routines:
         mats = {}
+        nb = nb_per.get(rname, a.nb)
         if rname == "dgemm":
             for key, seed in (("A", 1), ("B", 2), ("C", 3)):
                 M = s.Matrix(n, n, nb, np.float64, grid)
@@ -91,6 +95,17 @@ def main():
                 s._slate.generate_matrix_d("rands", M, seed, -1.0, s.opts(target))
                 mats[key] = M
             flops = F.gemm_flops(n, n, n)
+        elif rname == "dgesv_mixed":
+            # fp32 LU + fp64 refinement; flops counted as the fp64 LU (tester convention)
+            for key, seed in (("B", 7), ("X", 0)):
+                M = s.Matrix(n, 1, nb, np.float64, grid)
+                M.insertLocalTiles(s.target_of(target))
+                s._slate.generate_matrix_d("rands", M, seed + 1, -1.0, s.opts(target))
+                mats[key] = M
+            M = s.Matrix(n, n, nb, np.float64, grid)
+            M.insertLocalTiles(s.target_of(target))
+            mats["A"] = M
+            flops = F.getrf_flops(n)
         else:
             M = s.Matrix(n, n, nb, np.float64, grid)
             M.insertLocalTiles(s.target_of(target))
@@ -99,7 +114,8 @@ def main():
         times = []
         for step in range(a.warmup + a.steps):
             if rname != "dgemm":
-                kind = "spd" if rname == "dpotrf" else "rands"
+                # diagonally dominant for dgesv_mixed so fp32 LU + refinement converges
+                kind = "spd" if rname == "dpotrf" else ("diag_dominant" if rname == "dgesv_mixed" else "rands")
                 s._slate.generate_matrix_d(kind, mats["A"], 100 + step, -1.0, s.opts(target))
             barrier_sync()
             if a.trace and step == a.warmup:
@@ -118,6 +134,9 @@ def main():
                 assert info == 0, f"dgetrf info={info}"
             elif rname == "dgeqrf":
                 s.geqrf(mats["A"], **opts)
+            elif rname == "dgesv_mixed":
+                info, _, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], **opts)
+                assert info == 0 and iters >= 0, f"dgesv_mixed info={info} iters={iters}"
             barrier_sync()
             dt = time.perf_counter() - t0
             if a.trace and step == a.warmup:
@@ -129,7 +148,7 @@ def main():
                 print(f"# {rname} step {step} {'warm' if step < a.warmup else 'timed'}: {dt*1e3:.1f} ms "
                       f"{flops/dt/1e12:.2f} TFLOP/s", file=sys.stderr, flush=True)
         t = max_over_ranks(float(np.mean(times)))
-        results[rname] = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops}
+        results[rname] = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb}
         del mats
         s.sync()
         s._slate.release_cache()
@@ -151,7 +170,7 @@ def main():
         "dtype": "fp64",
         "data": "synthetic (counter-hash uniform[-1,1); SPD = symmetric + n*I for dpotrf)",
         "config": {
-            "model": "+".join(results.keys()) + f" n={n} nb={nb}",
+            "model": "+".join(f"{k}(nb={v['nb']})" for k, v in results.items()) + f" n={n}",
             "global_batch": 1,
             "seq_len": n,
             "parallelism": f"2d-block-cyclic {p}x{q} (one process per GPU, RCCL)" if world > 1 else "1x1",
@@ -162,6 +181,9 @@ def main():
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
+    if world > 1:
+        del grid
+        s.finalize()
 
 
 if __name__ == "__main__":

@@ -11,6 +11,7 @@
 #include <hip/hip_runtime_api.h>
 #include <cstdint>
 #include "dev_types.hh"
+#include "matgen_entry.hh"
 
 namespace slate_amd {
 namespace dev {
@@ -65,10 +66,15 @@ template <typename T>
 void genorm_partial(char kind, char uplo, char diag, int64_t m, int64_t n, const T* A, int64_t lda,
                     int64_t goff_row, int64_t goff_col, rt<T>* out, hipStream_t s);
 
-// ---- matgen (matgen.hip): fill a block-cyclic local array from a counter hash
+// ---- matgen (matgen.hip): fill a block-cyclic local array (view block at
+// absolute local (rb, cb), global offset (row0, col0)) from matgen_entry.hh
 template <typename T>
-void generate(char kind, int64_t mloc, int64_t nloc, T* A, int64_t lda, int64_t mb, int p, int rrel, int64_t row0,
-              int64_t nb, int q, int crel, int64_t col0, uint64_t seed, double shift, hipStream_t s);
+void generate(gen::Spec const& spec, int64_t mloc, int64_t nloc, T* A, int64_t lda, int64_t mb, int p, int rrel,
+              int64_t rb, int64_t row0, int64_t nb, int q, int crel, int64_t cb, int64_t col0, hipStream_t s);
+/// diagonal post-op on a block-cyclic local array: 'R' zero imaginary parts, 'S' add shift
+template <typename T>
+void gen_diag(char op, double shift, int64_t mloc, int64_t nloc, T* A, int64_t lda, int64_t mb, int p, int rrel,
+              int64_t rb, int64_t row0, int64_t nb, int q, int crel, int64_t cb, int64_t col0, hipStream_t s);
 
 // ---- panels (panel.hip)
 template <typename T>

@@ -337,6 +337,7 @@ PYBIND11_MODULE(_slate, m) {
         .def_property_readonly("world", &Grid::world_ptr)
         .def_property_readonly("row_comm", &Grid::row_ptr)
         .def_property_readonly("col_comm", &Grid::col_ptr);
+    m.def("generate_matrix_usage", &slate::generate_matrix_usage);
     m.def("default_grid", &default_grid);
     m.def("set_default_grid", &set_default_grid);
 

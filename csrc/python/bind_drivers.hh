@@ -73,6 +73,23 @@ void bind_drivers(py::module_& m, std::string const& s) {
 
     DEF("generate_matrix", [](std::string kind, BaseMatrix<T>& A, uint64_t seed, double shift, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; generate_matrix(kind, A, seed, shift, op); });
+    // full generator (MatgenParams): returns (Sigma, cond_actual); sigma_in used by the _specified distribution
+    DEF("matgen", [](std::string kind, Matrix<T>& A, int64_t seed, double cond, double condD,
+                     std::vector<R> sigma_in, py::dict o) {
+        Options op = to_options(o);
+        MatgenParams p; p.kind = kind; p.seed = seed; p.cond_request = cond; p.condD = condD;
+        std::vector<R> S = sigma_in;
+        { py::gil_scoped_release r; generate_matrix(p, A, S, op); }
+        return py::make_tuple(S, p.cond_actual);
+    });
+    DEF("matgen_tz", [](std::string kind, BaseTrapezoidMatrix<T>& A, int64_t seed, double cond, double condD,
+                        py::dict o) {
+        Options op = to_options(o);
+        MatgenParams p; p.kind = kind; p.seed = seed; p.cond_request = cond; p.condD = condD;
+        std::vector<R> S;
+        { py::gil_scoped_release r; generate_matrix(p, A, S, op); }
+        return py::make_tuple(S, p.cond_actual);
+    });
 
     // ---- Cholesky
     DEF("potrf", [](HermitianMatrix<T>& A, py::dict o) {

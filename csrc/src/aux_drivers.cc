@@ -46,6 +46,49 @@ inline bool is_trapezoid_kind(MatrixKind k) {
            k == MatrixKind::Symmetric || k == MatrixKind::Hermitian;
 }
 
+/// Calls fn(uplo, r, c, m, n) for the parts of an mb x nb tile whose (0, 0)
+/// element is view element (ri, cj) that lie in trapezoid `u` of the view
+/// (Lower keeps i >= j, Upper i <= j).  Handles views whose diagonal does not
+/// run through tile corners (slices with row0 != col0): at most one General
+/// strip plus one triangular sub-block per tile.
+template <typename F>
+void tz_tile_parts(Uplo u, int64_t ri, int64_t cj, int64_t mb, int64_t nb, F&& fn) {
+    if (u == Uplo::General) { fn(Uplo::General, 0, 0, mb, nb); return; }
+    const int64_t k = cj - ri;  // tile element (r, c) is on the view diagonal iff r - c == k
+    if (u == Uplo::Upper) {
+        if (k >= 0) {
+            if (k > 0) fn(Uplo::General, 0, 0, std::min(k, mb), nb);
+            if (k < mb) fn(Uplo::Upper, k, 0, mb - k, nb);
+        } else if (-k < nb) {
+            fn(Uplo::Upper, 0, -k, mb, nb + k);
+        }
+    } else {
+        if (k >= 0) {
+            if (k < mb) fn(Uplo::Lower, k, 0, mb - k, nb);
+        } else {
+            fn(Uplo::General, 0, 0, mb, std::min(-k, nb));
+            if (-k < nb) fn(Uplo::Lower, 0, -k, mb, nb + k);
+        }
+    }
+}
+
+/// Visit the local tiles of storage-oriented view A (NoTrans) that touch its
+/// trapezoid `u`, with each tile's view element origin.
+template <typename T, typename F>
+void for_tz_tiles(BaseMatrix<T> const& A, Uplo u, F&& fn) {
+    std::vector<int64_t> r0(A.mt() + 1, 0), c0(A.nt() + 1, 0);
+    for (int64_t i = 0; i < A.mt(); ++i) r0[i + 1] = r0[i] + A.tileMb(i);
+    for (int64_t j = 0; j < A.nt(); ++j) c0[j + 1] = c0[j] + A.tileNb(j);
+    for (int64_t j = 0; j < A.nt(); ++j)
+        for (int64_t i = 0; i < A.mt(); ++i) {
+            if (!A.tileIsLocal(i, j)) continue;
+            // skip tiles entirely outside the trapezoid
+            if (u == Uplo::Lower && r0[i + 1] - 1 < c0[j]) continue;
+            if (u == Uplo::Upper && r0[i] > c0[j + 1] - 1) continue;
+            fn(i, j, r0[i], c0[j]);
+        }
+}
+
 /// iterate over the local tiles of a view (logical indices), giving storage pointers
 template <typename T, typename F>
 void for_local_tiles(BaseMatrix<T> const& A, Loc loc, F f) {
@@ -189,14 +232,17 @@ void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     A.storage()->get(loc, false);
     B.storage()->get(loc, true);
-    Uplo u = B.uplo_physical();
-    for (int64_t j = 0; j < A.nt(); ++j)
-        for (int64_t i = 0; i < A.mt(); ++i) {
-            if (!A.tileIsLocal(i, j)) continue;
-            if (u == Uplo::Lower ? i < j : i > j) continue;
-            Tile<T> ta = A.tile(i, j, loc), tbt = B.tile(i, j, loc);
-            lb::add(c, i == j ? u : Uplo::General, ta.mb, ta.nb, alpha, ta.data, ta.stride, beta, tbt.data, tbt.stride);
-        }
+    // storage orientation: both views share op (same_layout)
+    BaseMatrix<T> As = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
+    BaseMatrix<T> Bs = B.op() == Op::NoTrans ? BaseMatrix<T>(B) : B.transpose_view(B.op() == Op::ConjTrans);
+    Uplo u = Bs.uplo();
+    for_tz_tiles(Bs, u, [&](int64_t i, int64_t j, int64_t ri, int64_t cj) {
+        Tile<T> ta = As.tile(i, j, loc), tbt = Bs.tile(i, j, loc);
+        tz_tile_parts(u, ri, cj, ta.mb, ta.nb, [&](Uplo pu, int64_t r, int64_t cc, int64_t m, int64_t n) {
+            lb::add(c, pu, m, n, alpha, ta.data + r + cc * ta.stride, ta.stride, beta,
+                    tbt.data + r + cc * tbt.stride, tbt.stride);
+        });
+    });
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
     B.storage()->update_origin();
 }
@@ -209,19 +255,18 @@ void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options con
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     bool trap = is_trapezoid_kind(A.matrix_kind());
     A.storage()->get(loc, true);
-    if (!trap || A.grid()->size() == 1) {
+    if (!trap || (A.grid()->size() == 1 && A.row0() == A.col0())) {
         LocalBlock<T> la = A.local_raw(loc);
         lb::scale(c, trap ? A.uplo_physical() : Uplo::General, la.m, la.n, numer, denom, la.ptr, la.ld);
     } else {
-        Uplo u = A.uplo_physical();
-        for (int64_t j = 0; j < A.nt(); ++j)
-            for (int64_t i = 0; i < A.mt(); ++i) {
-                if (!A.tileIsLocal(i, j)) continue;
-                int64_t si = A.op() == Op::NoTrans ? i : j, sj = A.op() == Op::NoTrans ? j : i;
-                if (u == Uplo::Lower ? si < sj : si > sj) continue;
-                Tile<T> t = A.tile(i, j, loc);
-                lb::scale(c, si == sj ? u : Uplo::General, t.mb, t.nb, numer, denom, t.data, t.stride);
-            }
+        BaseMatrix<T> As = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
+        Uplo u = As.uplo();
+        for_tz_tiles(As, u, [&](int64_t i, int64_t j, int64_t ri, int64_t cj) {
+            Tile<T> t = As.tile(i, j, loc);
+            tz_tile_parts(u, ri, cj, t.mb, t.nb, [&](Uplo pu, int64_t r, int64_t cc, int64_t m, int64_t n) {
+                lb::scale(c, pu, m, n, numer, denom, t.data + r + cc * t.stride, t.stride);
+            });
+        });
     }
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
     A.storage()->update_origin();
@@ -267,18 +312,31 @@ void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     bool trap = is_trapezoid_kind(A.matrix_kind());
-    Uplo u = trap ? A.uplo_physical() : Uplo::General;
     A.storage()->get(loc, true);
-    for (int64_t j = 0; j < A.nt(); ++j)
-        for (int64_t i = 0; i < A.mt(); ++i) {
-            if (!A.tileIsLocal(i, j)) continue;
-            int64_t si = A.op() == Op::NoTrans ? i : j, sj = A.op() == Op::NoTrans ? j : i;
-            if (u == Uplo::Lower && si < sj) continue;
-            if (u == Uplo::Upper && si > sj) continue;
-            Tile<T> t = A.tile(i, j, loc);
-            if (si == sj) lb::set(c, u, t.mb, t.nb, offdiag, diag, t.data, t.stride);
-            else lb::set(c, Uplo::General, t.mb, t.nb, offdiag, offdiag, t.data, t.stride);
+    // storage orientation; a transposed view stores op(value) (set is symmetric
+    // in i, j, but conj_transpose views store conjugated values)
+    bool cj_ = A.op() == Op::ConjTrans;
+    BaseMatrix<T> As = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(cj_);
+    if (cj_) { offdiag = slate::conj(offdiag); diag = slate::conj(diag); }
+    Uplo u = trap ? As.uplo() : Uplo::General;
+    for_tz_tiles(As, u, [&](int64_t i, int64_t j, int64_t ri, int64_t cj) {
+        Tile<T> t = As.tile(i, j, loc);
+        if (u == Uplo::General) {
+            // whole tile, then the diagonal run r - c == cj - ri (if any) through a sub-block
+            const int64_t k = cj - ri, r = std::max<int64_t>(k, 0), cc = std::max<int64_t>(-k, 0);
+            bool has_diag = r < t.mb && cc < t.nb;
+            if (!has_diag || !(diag == offdiag))
+                lb::set(c, Uplo::General, t.mb, t.nb, offdiag, offdiag, t.data, t.stride);
+            if (has_diag)
+                lb::set(c, Uplo::General, t.mb - r, t.nb - cc, offdiag, diag, t.data + r + cc * t.stride, t.stride);
+            return;
         }
+        // trapezoid: General strips hold no diagonal element; triangular parts
+        // have the view diagonal as their own
+        tz_tile_parts(u, ri, cj, t.mb, t.nb, [&](Uplo pu, int64_t r, int64_t cc, int64_t m, int64_t n) {
+            lb::set(c, pu, m, n, offdiag, pu == Uplo::General ? offdiag : diag, t.data + r + cc * t.stride, t.stride);
+        });
+    });
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
     A.storage()->update_origin();
 }

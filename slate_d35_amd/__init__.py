@@ -22,7 +22,7 @@ from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid, 
                     BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general,
                     from_numpy, to_numpy, empty_like, local_tensor, transpose, conj_transpose,
                     version, suffix_of, dtype_of, opts, target_of)
-from .parallel import init_grid, choose_grid, TorchHostComm, current_grid  # noqa: F401
+from .parallel import init_grid, choose_grid, TorchHostComm, current_grid, finalize  # noqa: F401
 from .models import *  # noqa: F401,F403
 from . import utils  # noqa: F401
 from . import ops  # noqa: F401

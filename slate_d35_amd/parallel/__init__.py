@@ -200,5 +200,20 @@ def init_grid(p: int | None = None, q: int | None = None, order=GridOrder.Col, t
     return _GRID
 
 
+def finalize():
+    """Tear down the grid and the torch.distributed process group (the
+    reference's MPI_Finalize point).  Call before exit in multi-process runs:
+    destroying gloo groups during interpreter shutdown can abort."""
+    global _GRID
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
+    _slate.set_default_grid(_slate.Grid.self())
+    _GRID = None
+    _KEEP.clear()
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
+
+
 def current_grid():
     return _GRID if _GRID is not None else _slate.default_grid()

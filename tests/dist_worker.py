@@ -126,6 +126,7 @@ def main():
                 continue
             for nb in (32, 48):
                 fn(tg, dt, nb)
+    parallel.finalize()
     if parallel.world_rank() == 0:
         print("DIST_OK", p, q, tg, names, flush=True)
 

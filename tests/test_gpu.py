@@ -238,6 +238,20 @@ def test_generate_matrix_device_matches_host():
         np.testing.assert_array_equal(s.to_numpy(A), s.to_numpy(B))
 
 
+@pytest.mark.parametrize("kind", ["randn", "rand_dominant", "chebspec", "orthog", "kms", "riemann", "gfpp",
+                                  "diag_geo", "svd_arith", "heev", "poev_cluster0", "geev"])
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_matgen_kinds_device_match_host(kind, dtype):
+    from slate_d35_amd.utils import matgen as mg
+    out = []
+    for tg in ("d", "h"):
+        A = s.Matrix(260, 260, 64, dtype); A.insertLocalTiles(s.target_of(tg))
+        S, _ = mg.generate_matrix(kind, A, seed=3, cond=1e3, target=tg)
+        out.append((s.to_numpy(A), S))
+    np.testing.assert_allclose(out[0][0], out[1][0], rtol=1e-10, atol=1e-12)
+    np.testing.assert_allclose(out[0][1], out[1][1], rtol=1e-14)
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("mn", [(700, 700), (900, 500), (500, 900)])
 def test_getrf_driver_device(dtype, mn):
