@@ -22,6 +22,15 @@
 #include "kernels.hh"
 
 #include <cstdlib>
+#include <type_traits>
+
+// lab switches (A/B builds of the standalone harness)
+#ifndef GEMM_SPLIT
+#define GEMM_SPLIT 1
+#endif
+#ifndef GEMM_FDB
+#define GEMM_FDB false
+#endif
 
 namespace slate_amd {
 namespace dev {
@@ -45,6 +54,19 @@ template <> struct Mfma<float> {
     // C/D layout of v_mfma_f32_16x16x4_f32: col = lane&15, row = 4*(lane>>4) + reg
     __device__ static inline int row(int lane, int r) { return 4 * (lane >> 4) + r; }
 };
+
+// LDS row skew: row r of an operand image starts at r*LD + lds_skew(r).  A
+// K-contiguous operand is transposed on its way into LDS; with a plain row
+// stride (BM+16, a multiple of 32 dwords) the BK/VEC lanes that share a column
+// write rows on the same bank (ds_write: bank = (addr/4)%32) - an 8-way (fp64)
+// / 4-way (fp32) store conflict.  The skew spreads those rows over distinct
+// banks while keeping the two rows an MFMA operand read touches per 32-lane
+// group (r, r+1 with r even / r%4 < 2) on disjoint bank halves, and it is a
+// per-row constant, so operand reads keep immediate address offsets.
+template <typename T>
+__device__ __forceinline__ constexpr int lds_skew(int r) {
+    return sizeof(T) == 8 ? (r & ~1) : 8 * (r >> 2);
+}
 
 // Load a BX x BK operand tile into registers. Element (x, kk) of the operand
 // lives at X[x*sx + kk*sk]; KCONTIG means sk == 1 (else sx == 1).
@@ -72,22 +94,7 @@ struct TileLoader {
                                 int64_t xdim, int64_t kdim, bool fast) {
         const int tid = threadIdx.x;
         if (fast) {
-            #pragma unroll
-            for (int i = 0; i < NVT; ++i) {
-                int x, kk;
-                coords(tid + NTHR * i, x, kk);
-                const T* p = KCONTIG ? X + (k0 + kk) + (x0 + x) * ld
-                                     : X + (x0 + x) + (k0 + kk) * ld;
-                if constexpr (sizeof(T) == 8) {
-                    using v2 = double __attribute__((ext_vector_type(2)));
-                    v2 t = *reinterpret_cast<const v2*>(p);
-                    r[i][0] = t[0]; r[i][1] = t[1];
-                } else {
-                    using v4 = float __attribute__((ext_vector_type(4)));
-                    v4 t = *reinterpret_cast<const v4*>(p);
-                    r[i][0] = t[0]; r[i][1] = t[1]; r[i][2] = t[2]; r[i][3] = t[3];
-                }
-            }
+            load_fast(X, ld, x0, k0);
         } else {
             #pragma unroll
             for (int i = 0; i < NVT; ++i) {
@@ -104,7 +111,30 @@ struct TileLoader {
         }
     }
 
-    // store into LDS image L[kk][x], row stride LD elements
+    /// Vector loads only (tile fully inside the operand, 16-B aligned).
+    __device__ inline void load_fast(const T* __restrict__ X, int64_t ld, int64_t x0, int64_t k0) {
+        const int tid = threadIdx.x;
+        {
+            #pragma unroll
+            for (int i = 0; i < NVT; ++i) {
+                int x, kk;
+                coords(tid + NTHR * i, x, kk);
+                const T* p = KCONTIG ? X + (k0 + kk) + (x0 + x) * ld
+                                     : X + (x0 + x) + (k0 + kk) * ld;
+                if constexpr (sizeof(T) == 8) {
+                    using v2 = double __attribute__((ext_vector_type(2)));
+                    v2 t = *reinterpret_cast<const v2*>(p);
+                    r[i][0] = t[0]; r[i][1] = t[1];
+                } else {
+                    using v4 = float __attribute__((ext_vector_type(4)));
+                    v4 t = *reinterpret_cast<const v4*>(p);
+                    r[i][0] = t[0]; r[i][1] = t[1]; r[i][2] = t[2]; r[i][3] = t[3];
+                }
+            }
+        }
+    }
+
+    // store into LDS image row kk at kk*LD + lds_skew(kk), column x
     template <int LD>
     __device__ inline void store(T* L) const {
         const int tid = threadIdx.x;
@@ -115,11 +145,12 @@ struct TileLoader {
             if constexpr (KCONTIG) {
                 #pragma unroll
                 for (int e = 0; e < VEC; ++e)
-                    L[(kk + e) * LD + x] = r[i][e];
+                    L[(kk + e) * LD + lds_skew<T>(kk + e) + x] = r[i][e];
             } else {
+                // the skew is a multiple of VEC: the vector stays aligned
                 #pragma unroll
                 for (int e = 0; e < VEC; ++e)
-                    L[kk * LD + x + e] = r[i][e];
+                    L[kk * LD + lds_skew<T>(kk) + x + e] = r[i][e];
             }
         }
     }
@@ -187,9 +218,10 @@ __device__ inline void gemm_tile_coords(int64_t m, int64_t n, int BM, int BN, in
 // NTHR = 64 * (BM/64) * (BN/64): one wave per 64 x 64 sub-tile.  128 x 128
 // (4 waves, 2 workgroups per CU) or 256 x 128 (8 waves, 1 workgroup per CU:
 // 25% less operand traffic per flop for large C).
-template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI, int WTN_ = 64>
-__global__ __launch_bounds__(64 * (BM / 64) * (BN / WTN_),
-    (2 * BK * (BM + BN + 32) * sizeof(T) > 81920) ? 1 : 512 / (64 * (BM / 64) * (BN / WTN_)))
+template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI, int WTN_ = 64, int WTM_ = 64,
+          bool FDB = false>
+__global__ __launch_bounds__(64 * (BM / WTM_) * (BN / WTN_),
+    (2 * BK * (BM + BN + 32) * sizeof(T) > 81920) ? 1 : 512 / (64 * (BM / WTM_) * (BN / WTN_)))
 void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
                       const T* __restrict__ A, int64_t lda, int64_t sA,
                       const T* __restrict__ B, int64_t ldb, int64_t sB,
@@ -200,11 +232,11 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     using acc_t = typename M::acc_t;
     constexpr int PAD = 16;
     constexpr int LDA_S = BM + PAD, LDB_S = BN + PAD;
-    constexpr int WTM = 64, WTN = WTN_;             // per-wave tile
+    constexpr int WTM = WTM_, WTN = WTN_;           // per-wave tile
     constexpr int WN = BN / WTN;                     // waves along N
     constexpr int NTHR = 64 * (BM / WTM) * WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;     // MFMA tiles per wave
-    constexpr int A_ELEMS = BK * LDA_S, B_ELEMS = BK * LDB_S;
+    constexpr int A_ELEMS = BK * LDA_S + 32, B_ELEMS = BK * LDB_S + 32;  // + max skew
 
     __shared__ T smem[2 * (A_ELEMS + B_ELEMS)];
 
@@ -253,41 +285,75 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     const bool mfull = (m0 + BM <= m), nfull = (n0 + BN <= n);
 
     const int KT = (int)((k + BK - 1) / BK);
+    // Interior tiles (the common case) run a K loop with vector loads only;
+    // edge tiles take the bounds-checked loop.  Keeping the two apart keeps
+    // the checked path's 64-bit index math out of the hot loop's registers.
+    auto kloop = [&](auto interior_tag) {
+    constexpr bool INTERIOR = decltype(interior_tag)::value;
+    auto load_a = [&](int64_t k0, bool kfull) {
+        if constexpr (INTERIOR) la.load_fast(A, lda, m0, k0);
+        else la.load(A, lda, m0, k0, m, k, aligned && mfull && kfull);
+    };
+    auto load_b = [&](int64_t k0, bool kfull) {
+        if constexpr (INTERIOR) lb.load_fast(B, ldb, n0, k0);
+        else lb.load(B, ldb, n0, k0, n, k, aligned && nfull && kfull);
+    };
     if (KT > 0) {
         bool kfull = (BK <= k);
-        la.load(A, lda, m0, 0, m, k, aligned && mfull && kfull);
-        lb.load(B, ldb, n0, 0, n, k, aligned && nfull && kfull);
+        load_a(0, kfull);
+        load_b(0, kfull);
         la.template store<LDA_S>(smem);
         lb.template store<LDB_S>(smem + A_ELEMS);
         __syncthreads();
     }
 
+    // MFMA operand fragments are double-buffered in registers: the LDS reads
+    // of k-step s+1 are issued before the MFMAs of step s, so the LDS latency
+    // hides behind 16 MFMAs instead of stalling every step.
+    auto frag = [&](const T* As, const T* Bs, int s, T (&a)[TM], T (&b)[TN]) {
+        const int kr = s * 4 + (lane >> 4);
+        const int sk = lds_skew<T>(kr);
+        #pragma unroll
+        for (int i = 0; i < TM; ++i)
+            a[i] = As[kr * LDA_S + sk + wm * WTM + i * 16 + (lane & 15)];
+        #pragma unroll
+        for (int j = 0; j < TN; ++j)
+            b[j] = Bs[kr * LDB_S + sk + wn * WTN + j * 16 + (lane & 15)];
+    };
     for (int kt = 0; kt < KT; ++kt) {
         const int cur = kt & 1;
         const bool more = (kt + 1 < KT);
         if (more) {
             int64_t k0 = (int64_t)(kt + 1) * BK;
             bool kfull = (k0 + BK <= k);
-            la.load(A, lda, m0, k0, m, k, aligned && mfull && kfull);
-            lb.load(B, ldb, n0, k0, n, k, aligned && nfull && kfull);
+            load_a(k0, kfull);
+            load_b(k0, kfull);
         }
         const T* As = smem + cur * (A_ELEMS + B_ELEMS);
         const T* Bs = As + A_ELEMS;
+        if constexpr (FDB) {
+        T a[2][TM], b[2][TN];
+        frag(As, Bs, 0, a[0], b[0]);
         #pragma unroll
         for (int s = 0; s < BK / 4; ++s) {
-            const int kr = s * 4 + (lane >> 4);
-            T a[TM], b[TN];
+            if (s + 1 < BK / 4) frag(As, Bs, s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
             #pragma unroll
             for (int i = 0; i < TM; ++i)
-                a[i] = As[kr * LDA_S + wm * WTM + i * 16 + (lane & 15)];
-            #pragma unroll
-            for (int j = 0; j < TN; ++j)
-                b[j] = Bs[kr * LDB_S + wn * WTN + j * 16 + (lane & 15)];
+                #pragma unroll
+                for (int j = 0; j < TN; ++j)
+                    acc[i][j] = M::run(b[s & 1][j], a[s & 1][i], acc[i][j]);
+        }
+        } else {
+        #pragma unroll
+        for (int s = 0; s < BK / 4; ++s) {
+            T a[TM], b[TN];
+            frag(As, Bs, s, a, b);
             #pragma unroll
             for (int i = 0; i < TM; ++i)
                 #pragma unroll
                 for (int j = 0; j < TN; ++j)
                     acc[i][j] = M::run(b[j], a[i], acc[i][j]);
+        }
         }
         if (more) {
             T* Asn = smem + (cur ^ 1) * (A_ELEMS + B_ELEMS);
@@ -296,22 +362,26 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         }
         __syncthreads();
     }
+    };
+    if (GEMM_SPLIT && aligned && mfull && nfull && k % BK == 0) kloop(std::true_type{});
+    else kloop(std::false_type{});
 
     gemm_epilogue<T, TM, TN, TRI>(acc, m, n, alpha, beta, C, ldc, m0 + wm * WTM, n0 + wn * WTN, lane);
 }
 
-template <typename T, bool A_KC, bool B_KC, char TRI, int BM, int BN, int BK = 16, int WTN = 64>
+template <typename T, bool A_KC, bool B_KC, char TRI, int BM, int BN, int BK = 16, int WTN = 64, int WTM = 64,
+          bool FDB = GEMM_FDB>
 static void launch_tile(int64_t m, int64_t n, int64_t k, T alpha,
                         const T* A, int64_t lda, int64_t sA,
                         const T* B, int64_t ldb, int64_t sB,
                         T beta, T* C, int64_t ldc, int64_t sC,
                         int64_t batch, bool aligned, hipStream_t stream)
 {
-    constexpr int NTHR = 64 * (BM / 64) * (BN / WTN);
+    constexpr int NTHR = 64 * (BM / WTM) * (BN / WTN);
     int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
     int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
     dim3 grid((unsigned)nblk, (unsigned)batch);
-    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN>), grid, dim3(NTHR), 0, stream,
+    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, FDB>), grid, dim3(NTHR), 0, stream,
                        m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
 }
 
