@@ -17,6 +17,7 @@
 #include "func.hh"
 #include "method.hh"
 #include "matgen.hh"
+#include "init.hh"
 
 #include <vector>
 

@@ -28,6 +28,9 @@
 #ifndef GEMM_SPLIT
 #define GEMM_SPLIT 1
 #endif
+#ifndef GEMM_JB
+#define GEMM_JB 2
+#endif
 #ifndef GEMM_FDB
 #define GEMM_FDB false
 #endif
@@ -164,7 +167,7 @@ __device__ inline void gemm_epilogue(typename Mfma<T>::acc_t (&acc)[TM][TN], int
                                      T beta, T* __restrict__ C, int64_t ldc, int64_t wm0, int64_t wn0, int lane) {
     using M = Mfma<T>;
     const bool beta_zero = (beta == T(0));
-    constexpr int JB = 2;
+    constexpr int JB = GEMM_JB;
     auto inside = [&](int64_t gm, int64_t gn) {
         bool in = gm < m && gn < n;
         if constexpr (TRI == 'L') in = in && gm >= gn;

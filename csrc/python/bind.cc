@@ -323,6 +323,16 @@ PYBIND11_MODULE(_slate, m) {
         return rccl_split(parent, color, key);
     });
 
+    // native bootstrap + TCP host transport (csrc/src/tcp_comm.cc)
+    m.def("make_tcp_world", [](double timeout) { return make_tcp_world(timeout); },
+          py::arg("timeout") = 120.0, py::call_guard<py::gil_scoped_release>());
+    m.def("tcp_split", [](CommPtr parent, int color, int key) { return tcp_split(parent, color, key); },
+          py::call_guard<py::gil_scoped_release>());
+    m.def("native_init_grid", [](int p, int q, GridOrder order, std::string transport) {
+        return slate::init_grid(p, q, order, transport); },
+          py::arg("p") = 0, py::arg("q") = 0, py::arg("order") = GridOrder::Col, py::arg("transport") = "auto",
+          py::call_guard<py::gil_scoped_release>());
+    m.def("native_finalize", &slate::finalize, py::call_guard<py::gil_scoped_release>());
     py::class_<Grid, std::shared_ptr<Grid>>(m, "Grid")
         .def(py::init<int, int, GridOrder, CommPtr, CommPtr, CommPtr>())
         .def_static("self", &Grid::self)

@@ -11,6 +11,9 @@ tile, include/slate/BaseMatrix.hh:1999-2212).  Two transports:
   buffers are staged through pinned host memory (the reference's
   non-GPU-aware-MPI path).  Used for CPU multi-process tests and for
   multi-rank runs sharing one GPU.
+* ``tcp``   - the native C++ socket-mesh transport (csrc/src/tcp_comm.cc,
+  no torch needed; the same one standalone C++/C/Fortran programs use
+  through slate::init_grid).  Host buffers, staged like ``host``.
 
 ``init_grid(p, q)`` returns the Grid and installs it as the default grid.
 """
@@ -151,7 +154,7 @@ def init_grid(p: int | None = None, q: int | None = None, order=GridOrder.Col, t
     """Create the p x q process grid over all ranks and make it the default.
 
     transport: 'auto' (rccl when a GPU is visible and world > 1, else host),
-    'rccl', or 'host'.
+    'rccl', 'host' (torch.distributed/gloo) or 'tcp' (native socket mesh).
     """
     global _GRID
     n = world_size()
@@ -162,6 +165,9 @@ def init_grid(p: int | None = None, q: int | None = None, order=GridOrder.Col, t
     if n == 1:
         _GRID = _slate.Grid.self()
         _slate.set_default_grid(_GRID)
+        return _GRID
+    if transport == "tcp":
+        _GRID = _slate.native_init_grid(p, q, order, "tcp")
         return _GRID
     dist = _ensure_dist("gloo")
     rank = dist.get_rank()
@@ -206,6 +212,11 @@ def finalize():
     destroying gloo groups during interpreter shutdown can abort."""
     global _GRID
     import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()):
+        _slate.native_finalize()
+        _GRID = None
+        _KEEP.clear()
+        return
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
     _slate.set_default_grid(_slate.Grid.self())

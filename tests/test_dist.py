@@ -43,6 +43,13 @@ def test_dist_host(p, q):
     run_workers(p, q, "h")
 
 
+@pytest.mark.parametrize("p,q", [(1, 2), (2, 2)])
+def test_dist_native_tcp(p, q):
+    """Same drivers over the native C++ socket-mesh transport (tcp_comm.cc),
+    the one standalone C++/C programs get from slate::init_grid."""
+    run_workers(p, q, "h", env_extra={"SLATE_TRANSPORT": "tcp"})
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("p,q", [(1, 2), (2, 1)])
 def test_dist_device_shared_gpu(p, q):
