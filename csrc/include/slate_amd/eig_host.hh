@@ -67,6 +67,34 @@ int64_t sterf(int64_t n, R* d, R* e);
 template <typename R>
 int64_t stedc(int64_t n, R* d, R* e, R* Q, int64_t ldq);
 
+// ---- the stages of stedc (reference stedc_solve.cc, stedc_z_vector.cc,
+// stedc_sort.cc, stedc_deflate.cc, stedc_secular.cc, stedc_merge.cc)
+
+/// Recursive D&C on the n x n tridiagonal (d, e[0:n-1]); Q gets its eigenvectors.
+template <typename R>
+void stedc_solve(int64_t n, R* d, R* e, R* Q, int64_t ldq);
+/// Rank-one coupling vector z = [last row of Q1, sgn * first row of Q2] / sqrt(2)
+/// of Q = diag(Q1 (n1 x n1), Q2).
+template <typename R>
+void stedc_z_vector(int64_t n1, int64_t n, R const* Q, int64_t ldq, R sgn, R* z);
+/// Sort D ascending, permuting z and the columns of Q into Qp; perm[j] = source column.
+template <typename R>
+void stedc_sort(int64_t n, R* D, R* z, R const* Q, int64_t ldq, R* Qp, int64_t ldqp, int64_t* perm);
+/// Deflation of D + rho z z^T: tiny z components and close D pairs (Givens on
+/// Qp's columns).  deflated[j] = 1 marks deflated columns; returns the rest.
+template <typename R>
+int64_t stedc_deflate(int64_t n, R rho, R* D, R* z, R* Qp, int64_t ldqp, char* deflated);
+/// Secular equation of D + rho z z^T (k x k, D ascending): eigenvalues lam
+/// and orthonormal eigenvectors U (Gu-Eisenstat).
+template <typename R>
+void stedc_secular(int64_t k, R rho, R const* D, R const* z, R* lam, R* U, int64_t ldu);
+
+/// Merge-product offload: C (m x n) = A (m x k) * B (k x n), element size
+/// esize (4 or 8); installed by the device layer when a GPU is attached.
+using StedcGemm = void (*)(size_t esize, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
+                           const void* B, int64_t ldb, void* C, int64_t ldc);
+void set_stedc_gemm(StedcGemm f);
+
 /// Bidiagonal SVD: B = diag(d) + superdiag(e) (n x n, upper).  Singular
 /// values descending in d; U (urows x n) := U * Ub, VT (n x vcols) := Vb^T VT.
 template <typename R, typename T>

@@ -18,6 +18,7 @@
 #include "method.hh"
 #include "matgen.hh"
 #include "init.hh"
+#include "eig_host.hh"
 
 #include <vector>
 
@@ -218,6 +219,99 @@ template <typename T>
 void gerbt(Matrix<T>& A, int depth, uint64_t seed_u, uint64_t seed_v, Options const& opts = {});
 template <typename T>
 int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Two-stage reduction building blocks (reference slate.hh:1050-1334).
+/// Householder reflectors of a bulge-chasing stage (hb2st / tb2bd) plus the
+/// diagonal phase that makes the condensed form real; replicated on every
+/// rank (the reference keeps them in a distributed Matrix V).
+template <typename T>
+struct BandReflectors {
+    host::Reflectors<T> Q;
+    std::vector<T> phase;
+};
+
+/// Band Hermitian -> real symmetric tridiagonal (D, E); A = Q T Q^H with
+/// Q = V.Q diag(V.phase).
+template <typename T>
+void hb2st(HermitianBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E,
+           BandReflectors<T>& V, Options const& opts = {});
+/// C = op(Q) C (Side::Left) or C op(Q) (Side::Right) with Q from hb2st.
+template <typename T>
+void unmtr_hb2st(Side side, Op op, BandReflectors<T> const& V, Matrix<T>& C, Options const& opts = {});
+/// C = op(Q1) C / C op(Q1) with Q1 the he2hb reflectors (stored below the band of A).
+template <typename T>
+void unmtr_he2hb(Side side, Op op, Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Matrix<T>& C,
+                 Options const& opts = {});
+/// Upper triangular band -> real upper bidiagonal: A = U B V^H.
+template <typename T>
+void tb2bd(TriangularBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E,
+           BandReflectors<T>& U, BandReflectors<T>& V, Options const& opts = {});
+/// Apply the tb2bd reflectors U or V: C = op(Q) C or C op(Q).
+template <typename T>
+void unmbr_tb2bd(Side side, Op op, BandReflectors<T> const& V, Matrix<T>& C, Options const& opts = {});
+/// Apply the ge2tb reflectors: Side::Left with the QR factors TU (C = op(U1) C),
+/// Side::Right with the LQ factors TV (C = C op(V1^H)).
+template <typename T>
+void unmbr_ge2tb(Side side, Op op, Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Matrix<T>& C,
+                 Options const& opts = {});
+
+/// Tridiagonal eigenvalues only (root-free QL).
+template <typename R>
+void sterf(std::vector<R>& D, std::vector<R>& E, Options const& opts = {});
+/// Tridiagonal QL/QR; with jobz = Vec, Z := Z * (eigenvectors).
+template <typename T>
+void steqr2(Job jobz, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E, Matrix<T>& Z,
+            Options const& opts = {});
+/// Tridiagonal divide and conquer: eigenvalues ascending in D, vectors in Q.
+template <typename R>
+void stedc(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const& opts = {});
+/// D&C stages (reference stedc_solve.cc, stedc_z_vector.cc, stedc_sort.cc,
+/// stedc_deflate.cc, stedc_secular.cc, stedc_merge.cc).
+template <typename R>
+void stedc_solve(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const& opts = {});
+template <typename R>
+void stedc_z_vector(Matrix<R>& Q, int64_t n1, R sgn, std::vector<R>& z, Options const& opts = {});
+template <typename R>
+void stedc_sort(std::vector<R>& D, std::vector<R>& z, Matrix<R>& Q, Matrix<R>& Qout, std::vector<int64_t>& perm,
+                Options const& opts = {});
+template <typename R>
+int64_t stedc_deflate(R rho, std::vector<R>& D, std::vector<R>& z, Matrix<R>& Q, std::vector<char>& deflated,
+                      Options const& opts = {});
+template <typename R>
+void stedc_secular(R rho, std::vector<R> const& D, std::vector<R> const& z, std::vector<R>& Lambda, Matrix<R>& U,
+                   Options const& opts = {});
+template <typename R>
+void stedc_merge(Matrix<R>& Q, Matrix<R>& U, Matrix<R>& Qout, Options const& opts = {});
+/// Bidiagonal SVD: D descending singular values; U := U Ub, VT := Vb^H VT.
+template <typename T>
+void bdsqr(Job jobu, Job jobvt, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E, Matrix<T>& U,
+           Matrix<T>& VT, Options const& opts = {});
+
+//------------------------------------------------------------------------------
+// Real-symmetric aliases (real types only) and compatibility names.
+template <typename T>
+void syev(SymmetricMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts = {});
+template <typename T>
+void sygst(int64_t itype, SymmetricMatrix<T>& A, SymmetricMatrix<T> const& B, Options const& opts = {});
+template <typename T>
+void sygv(int64_t itype, SymmetricMatrix<T>& A, SymmetricMatrix<T>& B, std::vector<real_type<T>>& Lambda,
+          Matrix<T>& Z, Options const& opts = {});
+template <typename T>
+int64_t sytrf(SymmetricMatrix<T>& A, std::vector<int64_t>& ipiv, Options const& opts = {});
+template <typename T>
+void sytrs(SymmetricMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+int64_t sysv(SymmetricMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Options const& opts = {});
+template <typename T>
+void svd_vals(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Options const& opts = {});
+template <typename T>
+void gesvd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts = {});
+template <typename T>
+void gels_qr(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options const& opts = {});
+/// Least squares via CholeskyQR (m >= n): A := Q, R upper n x n.
+template <typename T>
+void gels_cholqr(Matrix<T>& A, Matrix<T>& R, Matrix<T>& BX, Options const& opts = {});
 
 /// Wait for all device work of this process (drivers already synchronize).
 void sync();

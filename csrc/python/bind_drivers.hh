@@ -262,6 +262,61 @@ void bind_drivers(py::module_& m, std::string const& s) {
         Options op = to_options(o); std::vector<TriangularFactors<T>> TU, TV;
         { py::gil_scoped_release r; ge2tb(A, TU, TV, op); }
         return py::make_tuple(TU, TV); });
+    // ---- stage-level two-stage API on distributed matrices (eig_stages.cc)
+    py::class_<BandReflectors<T>>(m, ("BandReflectors_" + s).c_str())
+        .def("size", [](BandReflectors<T> const& V) { return V.Q.size(); });
+    DEF("hb2st_band", [](HermitianBandMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); std::vector<R> D, E; BandReflectors<T> V;
+        { py::gil_scoped_release r; hb2st(A, D, E, V, op); }
+        return py::make_tuple(D, E, V); });
+    DEF("unmtr_hb2st", [](Side sd, Op op_, BandReflectors<T> const& V, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; unmtr_hb2st(sd, op_, V, C, op); });
+    DEF("unmtr_he2hb", [](Side sd, Op op_, Matrix<T>& A, std::vector<TriangularFactors<T>> Ts, Matrix<T>& C,
+                          py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; unmtr_he2hb(sd, op_, A, Ts, C, op); });
+    DEF("tb2bd_band", [](TriangularBandMatrix<T>& A, py::dict o) {
+        Options op = to_options(o); std::vector<R> D, E; BandReflectors<T> U, V;
+        { py::gil_scoped_release r; tb2bd(A, D, E, U, V, op); }
+        return py::make_tuple(D, E, U, V); });
+    DEF("unmbr_tb2bd", [](Side sd, Op op_, BandReflectors<T> const& V, Matrix<T>& C, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; unmbr_tb2bd(sd, op_, V, C, op); });
+    DEF("unmbr_ge2tb", [](Side sd, Op op_, Matrix<T>& A, std::vector<TriangularFactors<T>> Ts, Matrix<T>& C,
+                          py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; unmbr_ge2tb(sd, op_, A, Ts, C, op); });
+    DEF("steqr2", [](Job jobz, std::vector<R> D, std::vector<R> E, Matrix<T>& Z, py::dict o) {
+        Options op = to_options(o);
+        { py::gil_scoped_release r; steqr2(jobz, D, E, Z, op); }
+        return D; });
+    DEF("bdsqr_mat", [=](Job ju, Job jv, std::vector<R> D, std::vector<R> E, py::object u, py::object vt,
+                         py::dict o) {
+        Options op = to_options(o); Matrix<T> U = opt_mat(u), VT = opt_mat(vt);
+        { py::gil_scoped_release r; bdsqr(ju, jv, D, E, U, VT, op); }
+        return D; });
+    DEF("gels_cholqr", [](Matrix<T>& A, Matrix<T>& Rm, Matrix<T>& BX, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; gels_cholqr(A, Rm, BX, op); });
+    DEF("gels_qr", [](Matrix<T>& A, Matrix<T>& BX, py::dict o) {
+        Options op = to_options(o); TriangularFactors<T> Tf;
+        { py::gil_scoped_release r; gels_qr(A, Tf, BX, op); }
+        return Tf; });
+    if constexpr (!is_complex_v<T>) {
+        DEF("stedc_mat", [](std::vector<T> D, std::vector<T> E, Matrix<T>& Q, py::dict o) {
+            Options op = to_options(o);
+            { py::gil_scoped_release r; stedc(D, E, Q, op); }
+            return D; });
+        DEF("syev", [=](SymmetricMatrix<T>& A, py::object z, py::dict o) {
+            Options op = to_options(o); Matrix<T> Z = opt_mat(z); std::vector<R> L;
+            { py::gil_scoped_release r; syev(A, L, Z, op); }
+            return L; });
+        DEF("sygv", [=](int64_t itype, SymmetricMatrix<T>& A, SymmetricMatrix<T>& B, py::object z, py::dict o) {
+            Options op = to_options(o); Matrix<T> Z = opt_mat(z); std::vector<R> L;
+            { py::gil_scoped_release r; sygv(itype, A, B, L, Z, op); }
+            return L; });
+        DEF("sysv", [](SymmetricMatrix<T>& A, Matrix<T>& B, py::dict o) {
+            Options op = to_options(o); std::vector<int64_t> ip; int64_t info;
+            { py::gil_scoped_release r; info = sysv(A, ip, B, op); }
+            return py::make_tuple(info, ip); });
+    }
+
     // host stage-2 kernels on dense numpy arrays (column-major copies)
     DEF("hb2st", [](py::array_t<T, py::array::f_style | py::array::forcecast> a, int64_t kd) {
         auto b = a.request();

@@ -297,11 +297,141 @@ int64_t sterf(int64_t n, R* d, R* e) {
 
 //------------------------------------------------------------------------------
 // Divide and conquer (Cuppen; deflation as LAPACK laed2; Gu-Eisenstat vectors
-// as laed3).  Q receives the eigenvectors of the n x n tridiagonal.
-namespace {
+// as laed3), split into the reference's stages (stedc_solve.cc, stedc_merge.cc,
+// stedc_z_vector.cc, stedc_sort.cc, stedc_deflate.cc, stedc_secular.cc).
 
 template <typename R>
-void stedc_rec(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
+void stedc_z_vector(int64_t n1, int64_t n, R const* Q, int64_t ldq, R sgn, R* z) {
+    const R s2 = std::sqrt(R(2));
+    for (int64_t j = 0; j < n1; ++j) z[j] = Q[(n1 - 1) + j * ldq] / s2;
+    for (int64_t j = n1; j < n; ++j) z[j] = sgn * Q[n1 + j * ldq] / s2;
+}
+
+template <typename R>
+void stedc_sort(int64_t n, R* D, R* z, R const* Q, int64_t ldq, R* Qp, int64_t ldqp, int64_t* perm) {
+    std::iota(perm, perm + n, int64_t(0));
+    std::stable_sort(perm, perm + n, [&](int64_t a, int64_t b) { return D[a] < D[b]; });
+    std::vector<R> Ds(n), zs(n);
+    for (int64_t j = 0; j < n; ++j) {
+        Ds[j] = D[perm[j]];
+        zs[j] = z[perm[j]];
+        std::copy(Q + perm[j] * ldq, Q + perm[j] * ldq + n, Qp + j * ldqp);
+    }
+    std::copy(Ds.begin(), Ds.end(), D);
+    std::copy(zs.begin(), zs.end(), z);
+}
+
+template <typename R>
+int64_t stedc_deflate(int64_t n, R rho, R* D, R* z, R* Qp, int64_t ldqp, char* deflated) {
+    const R eps = std::numeric_limits<R>::epsilon();
+    R dmax = 0, zmax = 0;
+    for (int64_t j = 0; j < n; ++j) { dmax = std::max(dmax, std::abs(D[j])); zmax = std::max(zmax, std::abs(z[j])); }
+    const R tol = R(8) * eps * std::max(dmax, zmax * rho);
+    // tiny components of z
+    for (int64_t j = 0; j < n; ++j) deflated[j] = (rho * std::abs(z[j]) <= tol) ? 1 : 0;
+    // close pairs of D: a Givens rotation of the two Q columns moves all of
+    // z onto one of them
+    int64_t last = -1;
+    for (int64_t j = 0; j < n; ++j) {
+        if (deflated[j]) continue;
+        if (last >= 0) {
+            R t = std::hypot(z[last], z[j]);
+            R c = z[j] / t, sn = -z[last] / t;
+            if (std::abs((D[j] - D[last]) * c * sn) <= tol) {
+                R* ql = Qp + last * ldqp;
+                R* qj = Qp + j * ldqp;
+                for (int64_t i = 0; i < n; ++i) {
+                    R x = ql[i], y = qj[i];
+                    ql[i] = c * x + sn * y;
+                    qj[i] = -sn * x + c * y;
+                }
+                R dl = D[last], dj = D[j];
+                D[last] = dl * c * c + dj * sn * sn;
+                D[j] = dl * sn * sn + dj * c * c;
+                z[j] = t;
+                z[last] = 0;
+                deflated[last] = 1;
+            }
+        }
+        last = j;
+    }
+    int64_t k = 0;
+    for (int64_t j = 0; j < n; ++j) k += !deflated[j];
+    return k;
+}
+
+template <typename R>
+void stedc_secular(int64_t k, R rho, R const* dd, R const* zz, R* lam, R* U, int64_t ldu) {
+    if (k <= 0) return;
+    const R eps = std::numeric_limits<R>::epsilon();
+    R znorm2 = 0;
+    for (int64_t i = 0; i < k; ++i) znorm2 += zz[i] * zz[i];
+    // roots: lambda_j = dd[org[j]] + tau[j], tau relative to the closer pole
+    std::vector<int64_t> org(k);
+    std::vector<R> tau(k);
+    #pragma omp parallel for schedule(dynamic, 8) if (k > 64)
+    for (int64_t j = 0; j < k; ++j) {
+        R lo_abs = dd[j];
+        R hi_abs = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2;
+        auto sec = [&](int64_t o2, R t) {   // f(dd[o2] + t)
+            R sum = 0;
+            for (int64_t i = 0; i < k; ++i) sum += zz[i] * zz[i] / ((dd[i] - dd[o2]) - t);
+            return R(1) + rho * sum;
+        };
+        R mid = (hi_abs - lo_abs) / R(2);
+        int64_t o2 = j;
+        R a = 0, b = mid;
+        if (j + 1 < k && sec(j, mid) < R(0)) { o2 = j + 1; a = -mid; b = 0; }
+        else if (j + 1 >= k) { a = 0; b = hi_abs - lo_abs; }
+        // bisection to full relative precision of t (the distance to the
+        // nearest pole), which the Gu-Eisenstat vectors need
+        for (int it = 0; it < 400; ++it) {
+            R t = (a + b) / R(2);
+            if (t == a || t == b) break;
+            R fv = sec(o2, t);
+            if (fv > R(0)) b = t; else a = t;
+            if (std::abs(b - a) <= R(2) * eps * std::min(std::abs(a), std::abs(b))) break;
+        }
+        org[j] = o2;
+        tau[j] = (a + b) / R(2);
+    }
+    // Gu-Eisenstat: recompute z from the computed roots
+    auto lam_minus_d = [&](int64_t j, int64_t i) { return (dd[org[j]] - dd[i]) + tau[j]; };
+    std::vector<R> zh(k);
+    for (int64_t i = 0; i < k; ++i) {
+        R pr = lam_minus_d(k - 1, i) / rho;
+        for (int64_t j = 0; j < k - 1; ++j) {
+            R num = lam_minus_d(j, i);
+            R den = (j < i) ? (dd[j] - dd[i]) : (dd[j + 1] - dd[i]);
+            pr *= num / den;
+        }
+        zh[i] = std::copysign(std::sqrt(std::abs(pr)), zz[i]);
+    }
+    // eigenvectors of D + rho z z^T
+    #pragma omp parallel for schedule(static) if (k > 256)
+    for (int64_t j = 0; j < k; ++j) {
+        R nrm = 0;
+        for (int64_t i = 0; i < k; ++i) {
+            R u = zh[i] / ((dd[i] - dd[org[j]]) - tau[j]);
+            U[i + j * ldu] = u;
+            nrm += u * u;
+        }
+        nrm = std::sqrt(nrm);
+        for (int64_t i = 0; i < k; ++i) U[i + j * ldu] /= nrm;
+        lam[j] = dd[org[j]] + tau[j];
+    }
+}
+
+namespace {
+/// Merge-product hook: C = A * B on the GPU when one is attached (set by the
+/// device layer); the host blocked gemm otherwise.
+StedcGemm g_stedc_gemm = nullptr;
+}
+
+void set_stedc_gemm(StedcGemm f) { g_stedc_gemm = f; }
+
+template <typename R>
+void stedc_solve(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
     const int64_t SMALL = 32;
     if (n <= SMALL) {
         for (int64_t j = 0; j < n; ++j)
@@ -309,155 +439,54 @@ void stedc_rec(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
         steqr<R, R>(n, d, e, Q, ldq, n);
         return;
     }
+    // divide: T = diag(T1, T2) + |beta| v v^T with the coupling removed
     const int64_t m = n / 2;
     const R beta = e[m - 1];
     const R rho0 = std::abs(beta);
     d[m - 1] -= rho0;
     d[m] -= rho0;
-    // subproblems, Q = diag(Q1, Q2)
     for (int64_t j = 0; j < n; ++j)
         for (int64_t i = 0; i < n; ++i) Q[i + j * ldq] = R(0);
-    stedc_rec(m, d, e, Q, ldq);
-    stedc_rec(n - m, d + m, e + m, Q + m + m * ldq, ldq);
-    const R sgn = beta < 0 ? R(-1) : R(1);
-    // z = [last row of Q1, sgn * first row of Q2] / sqrt(2); rho = 2 |beta|
-    std::vector<R> z(n), D(d, d + n);
-    for (int64_t j = 0; j < m; ++j) z[j] = Q[(m - 1) + j * ldq];
-    for (int64_t j = m; j < n; ++j) z[j] = sgn * Q[m + j * ldq];
-    const R s2 = std::sqrt(R(2));
-    for (auto& x : z) x /= s2;
-    R rho = R(2) * rho0;
-    // sort D ascending (permutation of the columns of Q)
+    stedc_solve(m, d, e, Q, ldq);
+    stedc_solve(n - m, d + m, e + m, Q + m + m * ldq, ldq);
+    // conquer
+    std::vector<R> z(n), Qp(size_t(n) * n);
     std::vector<int64_t> perm(n);
-    std::iota(perm.begin(), perm.end(), 0);
-    std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return D[a] < D[b]; });
-    std::vector<R> Ds(n), zs(n), Qp(size_t(n) * n);
-    for (int64_t j = 0; j < n; ++j) {
-        Ds[j] = D[perm[j]];
-        zs[j] = z[perm[j]];
-        std::copy(Q + perm[j] * ldq, Q + perm[j] * ldq + n, Qp.begin() + j * n);
-    }
-    const R eps = std::numeric_limits<R>::epsilon();
-    R dmax = 0, zmax = 0;
-    for (int64_t j = 0; j < n; ++j) { dmax = std::max(dmax, std::abs(Ds[j])); zmax = std::max(zmax, std::abs(zs[j])); }
-    const R tol = R(8) * eps * std::max(dmax, zmax * rho);
-    // deflation: tiny z, then close pairs via Givens rotations
-    std::vector<char> defl(n, 0);
-    for (int64_t j = 0; j < n; ++j) if (rho * std::abs(zs[j]) <= tol) defl[j] = 1;
-    int64_t last = -1;
-    for (int64_t j = 0; j < n; ++j) {
-        if (defl[j]) continue;
-        if (last >= 0) {
-            R t = std::hypot(zs[last], zs[j]);
-            R c = zs[j] / t, s = -zs[last] / t;
-            if (std::abs((Ds[j] - Ds[last]) * c * s) <= tol) {
-                // rotate columns last, j: zs[last] -> 0
-                R* ql = Qp.data() + last * n;
-                R* qj = Qp.data() + j * n;
-                for (int64_t i = 0; i < n; ++i) {
-                    R a = ql[i], b = qj[i];
-                    ql[i] = c * a + s * b;
-                    qj[i] = -s * a + c * b;
-                }
-                R dl = Ds[last], dj = Ds[j];
-                Ds[last] = dl * c * c + dj * s * s;
-                Ds[j] = dl * s * s + dj * c * c;
-                zs[j] = t;
-                zs[last] = 0;
-                defl[last] = 1;
-            }
-        }
-        last = j;
-    }
-    std::vector<int64_t> act;
-    for (int64_t j = 0; j < n; ++j) if (!defl[j]) act.push_back(j);
-    const int64_t k = int64_t(act.size());
-    std::vector<R> lam(n);
-    std::vector<R> Qout(size_t(n) * n, R(0));
+    stedc_z_vector<R>(m, n, Q, ldq, beta < 0 ? R(-1) : R(1), z.data());
+    const R rho = R(2) * rho0;
+    stedc_sort<R>(n, d, z.data(), Q, ldq, Qp.data(), n, perm.data());
+    std::vector<char> defl(n);
+    const int64_t k = stedc_deflate<R>(n, rho, d, z.data(), Qp.data(), n, defl.data());
+    std::vector<R> lam(n), Qout(size_t(n) * n, R(0));
     if (k > 0) {
-        std::vector<R> dk(k), zk(k);
-        for (int64_t i = 0; i < k; ++i) { dk[i] = Ds[act[i]]; zk[i] = zs[act[i]]; }
-        // dk may be out of order after rotations: sort
-        std::vector<int64_t> o(k);
-        std::iota(o.begin(), o.end(), 0);
-        std::sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return dk[a] < dk[b]; });
-        std::vector<R> dd(k), zz(k);
-        std::vector<int64_t> actS(k);
-        for (int64_t i = 0; i < k; ++i) { dd[i] = dk[o[i]]; zz[i] = zk[o[i]]; actS[i] = act[o[i]]; }
-        R znorm2 = 0;
-        for (auto x : zz) znorm2 += x * x;
-        // roots: lambda_j = dd[org[j]] + tau[j]
-        std::vector<int64_t> org(k);
-        std::vector<R> tau(k);
-        #pragma omp parallel for schedule(dynamic, 8) if (k > 64)
-        for (int64_t j = 0; j < k; ++j) {
-            R lo_abs = dd[j];
-            R hi_abs = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2;
-            auto sec = [&](int64_t o2, R t) {   // f(dd[o2] + t)
-                R s = 0;
-                for (int64_t i = 0; i < k; ++i) s += zz[i] * zz[i] / ((dd[i] - dd[o2]) - t);
-                return R(1) + rho * s;
-            };
-            // which endpoint is closer: sign of f at the midpoint
-            R mid = (hi_abs - lo_abs) / R(2);
-            int64_t o2 = j;
-            R a = 0, b = mid;
-            if (j + 1 < k && sec(j, mid) < R(0)) { o2 = j + 1; a = -mid; b = 0; }
-            else if (j + 1 >= k) { a = 0; b = hi_abs - lo_abs; }
-            // bisection on t in (a, b) relative to dd[o2]; f increases with t
-            // bisection to full relative precision of t (the distance to the
-            // nearest pole), which the Gu-Eisenstat vectors need
-            for (int it = 0; it < 400; ++it) {
-                R t = (a + b) / R(2);
-                if (t == a || t == b) break;
-                R fv = sec(o2, t);
-                if (fv > R(0)) b = t; else a = t;
-                if (std::abs(b - a) <= R(2) * eps * std::min(std::abs(a), std::abs(b))) break;
-            }
-            org[j] = o2;
-            tau[j] = (a + b) / R(2);
-        }
-        // Gu-Eisenstat: recompute z from the computed roots
-        auto lam_minus_d = [&](int64_t j, int64_t i) { return (dd[org[j]] - dd[i]) + tau[j]; };
-        std::vector<R> zh(k);
+        std::vector<int64_t> act;
+        for (int64_t j = 0; j < n; ++j) if (!defl[j]) act.push_back(j);
+        // the rotations may leave the active D out of order
+        std::sort(act.begin(), act.end(), [&](int64_t a, int64_t b) { return d[a] < d[b]; });
+        std::vector<R> dd(k), zz(k), U(size_t(k) * k), Qa(size_t(n) * k);
         for (int64_t i = 0; i < k; ++i) {
-            R p = lam_minus_d(k - 1, i) / rho;
-            for (int64_t j = 0; j < k - 1; ++j) {
-                R num = lam_minus_d(j, i);
-                R den = (j < i) ? (dd[j] - dd[i]) : (dd[j + 1] - dd[i]);
-                p *= num / den;
-            }
-            zh[i] = std::copysign(std::sqrt(std::abs(p)), zz[i]);
+            dd[i] = d[act[i]];
+            zz[i] = z[act[i]];
+            std::copy(Qp.begin() + act[i] * n, Qp.begin() + act[i] * n + n, Qa.begin() + i * n);
         }
-        // eigenvectors of D + rho z z^T, then Q * U
-        std::vector<R> U(size_t(k) * k);
-        for (int64_t j = 0; j < k; ++j) {
-            R nrm = 0;
-            for (int64_t i = 0; i < k; ++i) {
-                R den = (dd[i] - dd[org[j]]) - tau[j];
-                R u = zh[i] / den;
-                U[i + j * k] = u;
-                nrm += u * u;
-            }
-            nrm = std::sqrt(nrm);
-            for (int64_t i = 0; i < k; ++i) U[i + j * k] /= nrm;
-            lam[j] = dd[org[j]] + tau[j];
-        }
-        std::vector<R> Qa(size_t(n) * k);
-        for (int64_t i = 0; i < k; ++i) std::copy(Qp.begin() + actS[i] * n, Qp.begin() + actS[i] * n + n, Qa.begin() + i * n);
-        gemm<R>(Op::NoTrans, Op::NoTrans, n, k, k, R(1), Qa.data(), n, U.data(), k, R(0), Qout.data(), n);
+        stedc_secular<R>(k, rho, dd.data(), zz.data(), lam.data(), U.data(), k);
+        // merge product: Qout(:, 0:k) = Qa * U
+        if (g_stedc_gemm && n * k >= 512 * 512)
+            g_stedc_gemm(sizeof(R), n, k, k, Qa.data(), n, U.data(), k, Qout.data(), n);
+        else
+            gemm<R>(Op::NoTrans, Op::NoTrans, n, k, k, R(1), Qa.data(), n, U.data(), k, R(0), Qout.data(), n);
     }
     // deflated columns pass through
     int64_t col = k;
     for (int64_t j = 0; j < n; ++j) {
         if (!defl[j]) continue;
-        lam[col] = Ds[j];
+        lam[col] = d[j];
         std::copy(Qp.begin() + j * n, Qp.begin() + j * n + n, Qout.begin() + col * n);
         ++col;
     }
     // sort ascending into d, Q
     std::vector<int64_t> o(n);
-    std::iota(o.begin(), o.end(), 0);
+    std::iota(o.begin(), o.end(), int64_t(0));
     std::sort(o.begin(), o.end(), [&](int64_t a, int64_t b) { return lam[a] < lam[b]; });
     for (int64_t j = 0; j < n; ++j) {
         d[j] = lam[o[j]];
@@ -465,14 +494,12 @@ void stedc_rec(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
     }
 }
 
-}  // namespace
-
 template <typename R>
 int64_t stedc(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
     if (n <= 0) return 0;
     std::vector<R> ee(e, e + std::max<int64_t>(n - 1, 0));
     ee.push_back(R(0));
-    stedc_rec<R>(n, d, ee.data(), Q, ldq);
+    stedc_solve<R>(n, d, ee.data(), Q, ldq);
     return 0;
 }
 
@@ -609,6 +636,14 @@ template int64_t sterf<float>(int64_t, float*, float*);
 template int64_t sterf<double>(int64_t, double*, double*);
 template int64_t stedc<float>(int64_t, float*, float*, float*, int64_t);
 template int64_t stedc<double>(int64_t, double*, double*, double*, int64_t);
+#define SLATE_STEDC_INST(R)                                                                           \
+    template void stedc_z_vector<R>(int64_t, int64_t, R const*, int64_t, R, R*);                      \
+    template void stedc_sort<R>(int64_t, R*, R*, R const*, int64_t, R*, int64_t, int64_t*);            \
+    template int64_t stedc_deflate<R>(int64_t, R, R*, R*, R*, int64_t, char*);                       \
+    template void stedc_secular<R>(int64_t, R, R const*, R const*, R*, R*, int64_t);                  \
+    template void stedc_solve<R>(int64_t, R*, R*, R*, int64_t);
+SLATE_STEDC_INST(float)
+SLATE_STEDC_INST(double)
 
 }  // namespace host
 }  // namespace slate

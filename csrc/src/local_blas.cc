@@ -2,6 +2,7 @@
 #include "slate_amd/local_blas.hh"
 #include "slate_amd/host_blas.hh"
 #include "../kernels/kernels.hh"
+#include "slate_amd/eig_host.hh"
 
 #include <map>
 #include <mutex>
@@ -839,6 +840,35 @@ SLATE_LB_COPY(std::complex<float>, std::complex<float>)
 SLATE_LB_COPY(std::complex<double>, std::complex<double>)
 SLATE_LB_COPY(std::complex<float>, std::complex<double>)
 SLATE_LB_COPY(std::complex<double>, std::complex<float>)
+
+//------------------------------------------------------------------------------
+// Divide-and-conquer merge products (host::stedc_solve) on the GPU.
+namespace {
+template <typename R>
+void stedc_gemm_dev_t(int64_t m, int64_t n, int64_t k, const R* A, int64_t lda, const R* B, int64_t ldb,
+                      R* C, int64_t ldc) {
+    Ctx c = Ctx::device(device::kTrailQueue);
+    device::Buffer<R> dA(size_t(m) * k), dB(size_t(k) * n), dC(size_t(m) * n);
+    device::memcpy2d_async(dA.data(), m * sizeof(R), A, lda * sizeof(R), m * sizeof(R), k, c.stream);
+    device::memcpy2d_async(dB.data(), k * sizeof(R), B, ldb * sizeof(R), k * sizeof(R), n, c.stream);
+    gemm<R>(c, Op::NoTrans, Op::NoTrans, m, n, k, R(1), dA.data(), m, dB.data(), k, R(0), dC.data(), m);
+    device::memcpy2d_async(C, ldc * sizeof(R), dC.data(), m * sizeof(R), m * sizeof(R), n, c.stream);
+    slate_hip_call(hipStreamSynchronize(c.stream));
+}
+void stedc_gemm_dev(size_t esize, int64_t m, int64_t n, int64_t k, const void* A, int64_t lda,
+                    const void* B, int64_t ldb, void* C, int64_t ldc) {
+    if (!device::available()) {
+        if (esize == 8) host::gemm<double>(Op::NoTrans, Op::NoTrans, m, n, k, 1.0, (const double*)A, lda,
+                                           (const double*)B, ldb, 0.0, (double*)C, ldc);
+        else host::gemm<float>(Op::NoTrans, Op::NoTrans, m, n, k, 1.0f, (const float*)A, lda,
+                               (const float*)B, ldb, 0.0f, (float*)C, ldc);
+        return;
+    }
+    if (esize == 8) stedc_gemm_dev_t<double>(m, n, k, (const double*)A, lda, (const double*)B, ldb, (double*)C, ldc);
+    else stedc_gemm_dev_t<float>(m, n, k, (const float*)A, lda, (const float*)B, ldb, (float*)C, ldc);
+}
+struct StedcHook { StedcHook() { host::set_stedc_gemm(&stedc_gemm_dev); } } g_stedc_hook;
+}  // namespace
 
 }  // namespace lb
 }  // namespace slate

@@ -17,7 +17,7 @@ try:
 except Exception:  # torch is optional for the native library
     _torch = None
 from . import _slate
-from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid,  # noqa: F401
+from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid, Job,  # noqa: F401
                     Matrix, HermitianMatrix, SymmetricMatrix, TriangularMatrix, TrapezoidMatrix,
                     BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general,
                     from_numpy, to_numpy, empty_like, local_tensor, transpose, conj_transpose,

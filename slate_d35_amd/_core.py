@@ -13,6 +13,7 @@ from . import _slate
 Target = _slate.Target
 Op = _slate.Op
 Uplo = _slate.Uplo
+Job = _slate.Job
 Diag = _slate.Diag
 Side = _slate.Side
 Norm = _slate.Norm

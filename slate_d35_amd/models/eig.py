@@ -3,8 +3,9 @@ he2hb.cc, hb2st.cc, sterf.cc, steqr2.cc, stedc*.cc, svd.cc, ge2tb.cc,
 tb2bd.cc, bdsqr.cc)."""
 from ._wrap import call
 
-__all__ = ["heev", "hegv", "hegst", "svd", "svd_vals", "eig", "eig_vals", "he2hb", "hb2st", "sterf",
-           "steqr", "stedc", "ge2tb", "tb2bd", "bdsqr"]
+__all__ = ["heev", "hegv", "hegst", "svd", "svd_vals", "gesvd", "eig", "eig_vals", "he2hb", "hb2st", "sterf",
+           "steqr", "stedc", "ge2tb", "tb2bd", "bdsqr", "syev", "sygv", "hb2st_band", "unmtr_hb2st",
+           "unmtr_he2hb", "tb2bd_band", "unmbr_tb2bd", "unmbr_ge2tb", "steqr2", "stedc_matrix", "bdsqr_matrix"]
 
 
 def heev(A, Z=None, target=None, **kw):
@@ -84,3 +85,65 @@ def tb2bd(a, kd):
 def bdsqr(d, e, **kw):
     from .. import _slate
     return _slate.bdsqr(list(d), list(e))
+
+
+def gesvd(A, U=None, VT=None, target=None, **kw):
+    """Compatibility name of svd (reference slate.hh gesvd)."""
+    return svd(A, U, VT, target=target, **kw)
+
+
+def syev(A, Z=None, target=None, **kw):
+    """Real symmetric eigenproblem (A a SymmetricMatrix of a real type)."""
+    import numpy as np
+    return np.asarray(call("syev", A, A, Z, target=target, **kw))
+
+
+def sygv(itype, A, B, Z=None, target=None, **kw):
+    import numpy as np
+    return np.asarray(call("sygv", A, itype, A, B, Z, target=target, **kw))
+
+
+# ---- stage-level API on distributed matrices (reference slate.hh:1050-1334)
+def hb2st_band(A, target=None, **kw):
+    """HermitianBandMatrix -> (d, e, V): the real tridiagonal and the
+    bulge-chasing reflectors (apply with unmtr_hb2st)."""
+    return call("hb2st_band", A, A, target=target, **kw)
+
+
+def unmtr_hb2st(side, op, V, C, target=None, **kw):
+    return call("unmtr_hb2st", C, side, op, V, C, target=target, **kw)
+
+
+def unmtr_he2hb(side, op, A, Ts, C, target=None, **kw):
+    return call("unmtr_he2hb", C, side, op, A, Ts, C, target=target, **kw)
+
+
+def tb2bd_band(A, target=None, **kw):
+    """Upper TriangularBandMatrix -> (d, e, U, V) of A = U B V^H."""
+    return call("tb2bd_band", A, A, target=target, **kw)
+
+
+def unmbr_tb2bd(side, op, V, C, target=None, **kw):
+    return call("unmbr_tb2bd", C, side, op, V, C, target=target, **kw)
+
+
+def unmbr_ge2tb(side, op, A, Ts, C, target=None, **kw):
+    return call("unmbr_ge2tb", C, side, op, A, Ts, C, target=target, **kw)
+
+
+def steqr2(jobz, d, e, Z, target=None, **kw):
+    """Tridiagonal QL with Z := Z * eigenvectors (jobz = Job.Vec)."""
+    import numpy as np
+    return np.asarray(call("steqr2", Z, jobz, list(d), list(e), Z, target=target, **kw))
+
+
+def stedc_matrix(d, e, Q, target=None, **kw):
+    """Tridiagonal divide and conquer into a distributed Q."""
+    import numpy as np
+    return np.asarray(call("stedc_mat", Q, list(d), list(e), Q, target=target, **kw))
+
+
+def bdsqr_matrix(jobu, jobvt, d, e, U=None, VT=None, target=None, **kw):
+    import numpy as np
+    key = U if U is not None else VT
+    return np.asarray(call("bdsqr_mat", key, jobu, jobvt, list(d), list(e), U, VT, target=target, **kw))

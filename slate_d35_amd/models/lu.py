@@ -7,7 +7,7 @@ __all__ = ["getrf", "getrf_nopiv", "getrf_tntpiv", "getrs", "getrs_nopiv", "gesv
            "trcondest", "lu_factor", "lu_solve", "lu_solve_using_factor", "lu_inverse_using_factor",
            "lu_factor_nopiv", "lu_solve_nopiv", "lu_solve_using_factor_nopiv", "lu_rcondest_using_factor",
            "triangular_rcondest", "gbtrf", "gbtrs", "gbsv", "pbtrf", "pbtrs", "pbsv", "hetrf", "hetrs", "hesv",
-           "indefinite_factor", "indefinite_solve", "indefinite_solve_using_factor"]
+           "indefinite_factor", "indefinite_solve", "indefinite_solve_using_factor", "sysv"]
 
 
 def getrf(A, target=None, **kw):
@@ -132,3 +132,9 @@ triangular_rcondest = trcondest
 indefinite_factor = hetrf
 indefinite_solve = hesv
 indefinite_solve_using_factor = hetrs
+
+
+def sysv(A, B, target=None, **kw):
+    """Real symmetric indefinite solve (A a SymmetricMatrix of a real type);
+    returns (info, ipiv)."""
+    return call("sysv", A, A, B, target=target, **kw)

@@ -3,7 +3,7 @@ unmlq.cc, gels*.cc, cholqr.cc)."""
 from ._wrap import call
 
 __all__ = ["geqrf", "unmqr", "gelqf", "unmlq", "gels", "cholqr", "qr_factor", "qr_multiply_by_q",
-           "lq_factor", "lq_multiply_by_q", "least_squares_solve"]
+           "lq_factor", "lq_multiply_by_q", "least_squares_solve", "gels_qr", "gels_cholqr"]
 
 
 def geqrf(A, target=None, **kw):
@@ -29,6 +29,15 @@ def gels(A, BX, target=None, **kw):
 
 def cholqr(A, R, target=None, **kw):
     return call("cholqr", A, A, R, target=target, **kw)
+
+
+def gels_qr(A, BX, target=None, **kw):
+    return call("gels_qr", A, A, BX, target=target, **kw)
+
+
+def gels_cholqr(A, R, BX, target=None, **kw):
+    """Least squares via CholeskyQR (m >= n): A := Q, R (n x n) upper."""
+    return call("gels_cholqr", A, A, R, BX, target=target, **kw)
 
 
 qr_factor = geqrf
