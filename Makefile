@@ -64,7 +64,15 @@ tester: $(TESTER)
 $(TESTER): csrc/tools/tester.cc $(LIB)
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDLIBS)
 
+# C++ examples (reference examples/ex01-ex15), linked against the library
+EX_SRC    := $(wildcard examples/cpp/ex*.cc)
+EX_BIN    := $(patsubst examples/cpp/%.cc,build/examples/%,$(EX_SRC))
+examples: $(EX_BIN)
+build/examples/%: examples/cpp/%.cc examples/cpp/util.hh $(LIB) $(HDRS)
+	@mkdir -p build/examples
+	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../../$(PKG)' $(LDLIBS)
+
 clean:
 	rm -rf build $(LIB) $(PYMOD) $(LAPACK_API) $(SCALAPACK_API)
 
-.PHONY: all clean tester
+.PHONY: all clean tester examples

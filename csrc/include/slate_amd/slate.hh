@@ -313,7 +313,24 @@ void gels_qr(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options cons
 template <typename T>
 void gels_cholqr(Matrix<T>& A, Matrix<T>& R, Matrix<T>& BX, Options const& opts = {});
 
+//------------------------------------------------------------------------------
+// Printing (reference include/slate/print.hh).  Collective; rank 0 prints a
+// MATLAB-style `label = [ ... ];` block.  Options PrintVerbose (0-4, default
+// 2 = edges), PrintEdgeItems (16), PrintWidth (10), PrintPrecision (4).
+template <typename T>
+void print(const char* label, BaseMatrix<T> const& A, Options const& opts = {});
+/// Vector x[0:n:incx] (rank 0 only).
+template <typename T>
+void print(const char* label, int64_t n, T const* x, int64_t incx = 1, Options const& opts = {});
+/// What print() writes on rank 0, as a string (empty elsewhere).
+template <typename T>
+std::string print_to_string(const char* label, BaseMatrix<T> const& A, Options const& opts = {});
+template <typename R>
+int snprintf_value(char* buf, size_t len, int width, int precision, R value);
+
 /// Wait for all device work of this process (drivers already synchronize).
 void sync();
 
 }  // namespace slate
+
+#include "simplified_api.hh"

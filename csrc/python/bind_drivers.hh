@@ -262,6 +262,8 @@ void bind_drivers(py::module_& m, std::string const& s) {
         Options op = to_options(o); std::vector<TriangularFactors<T>> TU, TV;
         { py::gil_scoped_release r; ge2tb(A, TU, TV, op); }
         return py::make_tuple(TU, TV); });
+    DEF("print", [](std::string label, BaseMatrix<T> const& A, py::dict o) {
+        Options op = to_options(o); py::gil_scoped_release r; return print_to_string(label.c_str(), A, op); });
     // ---- stage-level two-stage API on distributed matrices (eig_stages.cc)
     py::class_<BandReflectors<T>>(m, ("BandReflectors_" + s).c_str())
         .def("size", [](BandReflectors<T> const& V) { return V.Q.size(); });

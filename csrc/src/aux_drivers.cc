@@ -5,6 +5,8 @@
 // colNorms.cc, internal_reduce_info.cc.
 #include "internal.hh"
 
+#include <algorithm>
+
 #include <cstring>
 #include <functional>
 #include <numeric>
@@ -99,39 +101,71 @@ void for_local_tiles(BaseMatrix<T> const& A, Loc loc, F f) {
 
 }  // namespace
 
-/// B = op(A) tile by tile over p2p (generic redistribution).
+/// B = op(A) over p2p for any pair of distributions AND tilings (reference
+/// redistribute.cc).  The unit of transfer is a cell of the union of both
+/// tile grids: each cell lies in exactly one tile of A and one tile of B, so
+/// with equal tilings cells are tiles (one message per tile).  For a
+/// triangular mask the row and column breakpoints are merged so diagonal
+/// cells are square blocks on the diagonal.
 template <typename Ts, typename Td>
 void redistribute_any(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Target target, Uplo mask) {
     slate_error_if_msg(A.m() != B.m() || A.n() != B.n(), "redistribute: dimension mismatch");
-    slate_error_if_msg(A.mt() != B.mt() || A.nt() != B.nt(), "redistribute: tile grids differ");
-    for (int64_t i = 0; i < A.mt(); ++i) slate_error_if_msg(A.tileMb(i) != B.tileMb(i), "redistribute: tile sizes differ");
-    for (int64_t j = 0; j < A.nt(); ++j) slate_error_if_msg(A.tileNb(j) != B.tileNb(j), "redistribute: tile sizes differ");
     Comm& world = A.grid()->world();
+    slate_error_if_msg(!A.grid()->same_processes(*B.grid()) && world.size() > 1,
+                       "redistribute: A and B must live on the same processes");
     const int me = world.rank();
     const Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     A.storage()->get(loc, false);
     B.storage()->get(loc, true);
-    // tile list in a deterministic order; buffers: one dense tile per transfer
-    struct Xfer { int64_t i, j; int src, dst; size_t off; int64_t mb, nb; };
+    // tile boundaries (logical, op applied) and their union
+    auto bounds = [](int64_t nt, auto size) {
+        std::vector<int64_t> v(1, 0);
+        for (int64_t t = 0; t < nt; ++t) v.push_back(v.back() + size(t));
+        return v;
+    };
+    std::vector<int64_t> ar = bounds(A.mt(), [&](int64_t t) { return A.tileMb(t); });
+    std::vector<int64_t> ac = bounds(A.nt(), [&](int64_t t) { return A.tileNb(t); });
+    std::vector<int64_t> br = bounds(B.mt(), [&](int64_t t) { return B.tileMb(t); });
+    std::vector<int64_t> bc = bounds(B.nt(), [&](int64_t t) { return B.tileNb(t); });
+    auto merge = [](std::vector<std::vector<int64_t> const*> const& lists, int64_t lim) {
+        std::vector<int64_t> u;
+        for (auto* l : lists) for (int64_t x : *l) if (x <= lim) u.push_back(x);
+        u.push_back(lim);
+        std::sort(u.begin(), u.end());
+        u.erase(std::unique(u.begin(), u.end()), u.end());
+        return u;
+    };
+    std::vector<int64_t> ur, uc;
+    if (mask == Uplo::General) { ur = merge({&ar, &br}, A.m()); uc = merge({&ac, &bc}, A.n()); }
+    else { ur = merge({&ar, &br, &ac, &bc}, A.m()); uc = merge({&ar, &br, &ac, &bc}, A.n()); }
+    auto tile_of = [](std::vector<int64_t> const& b, int64_t x) {
+        return int64_t(std::upper_bound(b.begin(), b.end(), x) - b.begin()) - 1;
+    };
+    // sub-block (rows r0.., cols c0..) of an op-applied tile view
+    auto sub = [](auto const& t, int64_t r, int64_t cc) {
+        return t.op == Op::NoTrans ? t.data + r + cc * t.stride : t.data + cc + r * t.stride;
+    };
+    struct Xfer { int64_t r0, c0, mb, nb; int peer; size_t off; bool diag; };
     std::vector<Xfer> sends, recvs;
     size_t soff = 0, roff = 0;
-    for (int64_t j = 0; j < B.nt(); ++j)
-        for (int64_t i = 0; i < B.mt(); ++i) {
-            if (mask == Uplo::Lower && i < j) continue;
-            if (mask == Uplo::Upper && i > j) continue;
-            int src = A.tileRank(i, j), dst = B.tileRank(i, j);
-            int64_t mb = B.tileMb(i), nb = B.tileNb(j);
+    for (size_t jc = 0; jc + 1 < uc.size(); ++jc)
+        for (size_t ic = 0; ic + 1 < ur.size(); ++ic) {
+            const int64_t r0 = ur[ic], c0 = uc[jc], mb = ur[ic + 1] - r0, nb = uc[jc + 1] - c0;
+            const bool diag = mask != Uplo::General && r0 == c0;
+            if (mask == Uplo::Lower && r0 < c0 && !diag) continue;
+            if (mask == Uplo::Upper && r0 > c0 && !diag) continue;
+            const int64_t ia = tile_of(ar, r0), ja = tile_of(ac, c0), ib = tile_of(br, r0), jb = tile_of(bc, c0);
+            const int src = A.tileRank(ia, ja), dst = B.tileRank(ib, jb);
             if (src == me && dst == me) {
-                Tile<Ts> ta = A.tile(i, j, loc);
-                Tile<Td> tb = B.tile(i, j, loc);
-                // tile of op(A): stored (ta.op != N ? transposed) tile
-                lb::copy(c, mask == Uplo::General || i != j ? Uplo::General : mask, ta.op,
-                         mb, nb, ta.data, ta.stride, tb.data, tb.stride);
+                Tile<Ts> ta = A.tile(ia, ja, loc);
+                Tile<Td> tb = B.tile(ib, jb, loc);
+                lb::copy(c, diag ? mask : Uplo::General, ta.op, mb, nb, sub(ta, r0 - ar[ia], c0 - ac[ja]), ta.stride,
+                         sub(tb, r0 - br[ib], c0 - bc[jb]), tb.stride);
             } else if (src == me) {
-                sends.push_back({i, j, src, dst, soff, mb, nb}); soff += size_t(mb) * nb;
+                sends.push_back({r0, c0, mb, nb, dst, soff, diag}); soff += size_t(mb) * nb;
             } else if (dst == me) {
-                recvs.push_back({i, j, src, dst, roff, mb, nb}); roff += size_t(mb) * nb;
+                recvs.push_back({r0, c0, mb, nb, src, roff, diag}); roff += size_t(mb) * nb;
             }
         }
     if (world.size() == 1) {
@@ -141,18 +175,21 @@ void redistribute_any(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Target target,
     Work<Ts> sbuf(target, std::max<size_t>(soff, 1));
     Work<Ts> rbuf(target, std::max<size_t>(roff, 1));
     for (auto& x : sends) {
-        Tile<Ts> ta = A.tile(x.i, x.j, loc);
-        // pack op(A) tile as dense mb x nb (storage-op applied)
-        lb::copy(c, Uplo::General, ta.op, x.mb, x.nb, ta.data, ta.stride, sbuf.data() + x.off, x.mb);
+        const int64_t ia = tile_of(ar, x.r0), ja = tile_of(ac, x.c0);
+        Tile<Ts> ta = A.tile(ia, ja, loc);
+        // pack the op(A) cell as a dense mb x nb block
+        lb::copy(c, Uplo::General, ta.op, x.mb, x.nb, sub(ta, x.r0 - ar[ia], x.c0 - ac[ja]), ta.stride,
+                 sbuf.data() + x.off, x.mb);
     }
     std::vector<Comm::P2P> ops;
-    for (auto& x : sends) ops.push_back({sbuf.data() + x.off, size_t(x.mb * x.nb), x.dst, true});
-    for (auto& x : recvs) ops.push_back({rbuf.data() + x.off, size_t(x.mb * x.nb), x.src, false});
+    for (auto& x : sends) ops.push_back({sbuf.data() + x.off, size_t(x.mb * x.nb), x.peer, true});
+    for (auto& x : recvs) ops.push_back({rbuf.data() + x.off, size_t(x.mb * x.nb), x.peer, false});
     world.exchange(ops, scalar_type<Ts>(), loc, c.stream);
     for (auto& x : recvs) {
-        Tile<Td> tb = B.tile(x.i, x.j, loc);
-        lb::copy(c, mask == Uplo::General || x.i != x.j ? Uplo::General : mask, Op::NoTrans, x.mb, x.nb,
-                 rbuf.data() + x.off, x.mb, tb.data, tb.stride);
+        const int64_t ib = tile_of(br, x.r0), jb = tile_of(bc, x.c0);
+        Tile<Td> tb = B.tile(ib, jb, loc);
+        lb::copy(c, x.diag ? mask : Uplo::General, Op::NoTrans, x.mb, x.nb, rbuf.data() + x.off, x.mb,
+                 sub(tb, x.r0 - br[ib], x.c0 - bc[jb]), tb.stride);
     }
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
 }

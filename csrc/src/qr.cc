@@ -236,8 +236,11 @@ void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
     slate_error_if_msg(T_.empty(), "unmqr: missing T factors");
     if (is_complex_v<T> == false && op == Op::ConjTrans) op = Op::Trans;
     if (side == Side::Left) {
+        // same processes in the same p x q arrangement (a transposed grid has
+        // the same processes and sizes but a different rank mapping)
         bool conform = C.op() == Op::NoTrans && C.aligned() && C.grid()->same_processes(*A.grid())
-                    && C.grid()->p() == A.grid()->p() && C.mt() == A.mt();
+                    && C.grid()->p() == A.grid()->p() && C.grid()->q() == A.grid()->q()
+                    && C.grid()->order() == A.grid()->order() && C.mt() == A.mt();
         if (conform)
             for (int64_t i = 0; i < A.mt(); ++i)
                 if (A.tileMb(i) != C.tileMb(i) || A.srow_owner(i) != C.srow_owner(i)) { conform = false; break; }

@@ -4,6 +4,8 @@
 #include <chrono>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
+#include <cstdio>
 #include <ctime>
 #include <map>
 #include <mutex>
@@ -192,11 +194,27 @@ std::string Trace::finish(Comm* comm, std::string const& basename) {
     return base;
 }
 
+namespace {
+/// SLATE_DEBUG_CALLS=1: every traced routine logs entry/exit to stderr with
+/// the world rank (reference Debug.cc-style diagnostics; finds the routine a
+/// multi-rank hang is stuck in).
+bool debug_calls() {
+    static bool on = [] { const char* e = std::getenv("SLATE_DEBUG_CALLS"); return e && *e && *e != '0'; }();
+    return on;
+}
+int debug_rank() {
+    const char* e = std::getenv("RANK");
+    return e ? std::atoi(e) : 0;
+}
+}  // namespace
+
 Block::Block(const char* name) : name_(name), start_(0), active_(Trace::is_on()) {
     if (active_) start_ = Trace::now();
+    if (debug_calls()) std::fprintf(stderr, "[rank %d] > %s\n", debug_rank(), name);
 }
 
 Block::~Block() {
+    if (debug_calls()) std::fprintf(stderr, "[rank %d] < %s\n", debug_rank(), name_);
     if (!active_) return;
     Event e{};
     std::strncpy(e.name, name_, sizeof(e.name) - 1);

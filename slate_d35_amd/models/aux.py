@@ -5,7 +5,7 @@ from .._core import suffix_of, opts
 from ._wrap import call
 
 __all__ = ["add", "tzadd", "copy", "scale", "scale_row_col", "set", "set_lambda", "redistribute",
-           "norm", "colNorms"]
+           "norm", "colNorms", "print_matrix", "print_to_string"]
 
 
 def add(alpha, A, beta, B, target=None, **kw):
@@ -53,3 +53,17 @@ def norm(kind, A, target=None, **kw):
 
 def colNorms(kind, A, target=None, **kw):
     return call("colNorms", A, kind, A, target=target, **kw)
+
+
+def print_to_string(label, A, target=None, **kw):
+    """What slate::print writes on rank 0 (MATLAB-style block; '' elsewhere).
+    Keywords: print_verbose (0-4, default 2), print_edge_items (16),
+    print_width (10), print_precision (4)."""
+    return call("print", A, label, A, target=target, **kw)
+
+
+def print_matrix(label, A, target=None, **kw):
+    """Collective print of a distributed matrix (reference slate::print)."""
+    out = print_to_string(label, A, target=target, **kw)
+    if out:
+        print(out, end="", flush=True)
