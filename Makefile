@@ -66,10 +66,12 @@ $(TESTER): csrc/tools/tester.cc $(LIB)
 
 # C++ examples (reference examples/ex01-ex15), linked against the library
 EX_SRC    := $(wildcard examples/cpp/ex*.cc)
-EX_BIN    := $(patsubst examples/cpp/%.cc,build/examples/%,$(EX_SRC))
+# Binaries go to examples/bin (shipped to GPU boxes with the tree); they only
+# depend on their sources so a tree without build/obj does not rebuild the library.
+EX_BIN    := $(patsubst examples/cpp/%.cc,examples/bin/%,$(EX_SRC))
 examples: $(EX_BIN)
-build/examples/%: examples/cpp/%.cc examples/cpp/util.hh $(LIB) $(HDRS)
-	@mkdir -p build/examples
+examples/bin/%: examples/cpp/%.cc examples/cpp/util.hh
+	@mkdir -p examples/bin
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../../$(PKG)' $(LDLIBS)
 
 clean:

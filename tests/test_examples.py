@@ -11,7 +11,7 @@ import subprocess
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-BIN = os.path.join(ROOT, "build", "examples")
+BIN = os.path.join(ROOT, "examples", "bin")
 EXAMPLES = sorted(os.path.basename(p)[:-3] for p in glob.glob(os.path.join(ROOT, "examples", "cpp", "ex*.cc")))
 MULTI = ["ex01_matrix", "ex04_norm", "ex05_blas", "ex06_linear_system_lu", "ex07_linear_system_cholesky",
          "ex09_least_squares", "ex11_hermitian_eig", "ex13_redistribute", "ex14_scalapack_gemm", "ex15_set_matrix"]
