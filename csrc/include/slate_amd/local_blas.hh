@@ -149,5 +149,9 @@ void norm_partial(Ctx const& c, char kind, Uplo uplo, Diag diag, int64_t m, int6
 template <typename T>
 void copy2d(Ctx const& c, int64_t m, int64_t n, T const* src, int64_t lds, T* dst, int64_t ldd);
 
+/// Throw if a persistent panel kernel reported a grid hand-off timeout since
+/// the last check (synchronizes with the device).
+void check_panel_errors();
+
 }  // namespace lb
 }  // namespace slate

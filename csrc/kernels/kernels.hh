@@ -125,5 +125,17 @@ void tsip(int64_t K, int m, int n, T alpha, const T* A, int64_t lda, const T* B,
 template <typename T>
 void larft_small(int k, const T* tau, T* Tm, int64_t ldt, hipStream_t s);
 
+/// Persistent narrow-block QR (qr_persistent.hip): Householder QR of columns
+/// [c0, c0+nn) (nn <= 32) of a panel over rows [c0, m) in ONE launch; tau[c0..]
+/// receives the scalars, A the reflectors (unit diagonal implicit) and R.
+/// part: qr_narrow_workspace_words(groups) 64-bit words; cnt: 32 counters
+/// (zeroed by the launcher); err: set non-zero if a grid hand-off timed out.
+template <typename T>
+int qr_narrow_groups(int64_t rows);
+size_t qr_narrow_workspace_words(int groups);
+template <typename T>
+void qr_narrow(int64_t m, int64_t c0, int nn, T* A, int64_t lda, T* tau, unsigned long long* part,
+               unsigned* cnt, unsigned* err, hipStream_t s);
+
 }  // namespace dev
 }  // namespace slate_amd

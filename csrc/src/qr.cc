@@ -225,6 +225,7 @@ void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
     Tf.insertLocalTiles(target);
     set(T(0), T(0), Tf, opts);
     geqrf_impl<T>(A, Tf, target, la);
+    if (target == Target::Devices) lb::check_panel_errors();
     T_.clear();
     T_.push_back(Tf);
 }
