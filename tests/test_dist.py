@@ -51,7 +51,7 @@ def test_dist_native_tcp(p, q):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("p,q", [(1, 2), (2, 1)])
+@pytest.mark.parametrize("p,q", [(1, 2), (2, 1), (2, 2)])
 def test_dist_device_shared_gpu(p, q):
     """Device target, 2 ranks on one GPU (host transport): covers the device
     code paths of the p x q drivers (panel gathers, row exchanges, U/L bcasts)."""
