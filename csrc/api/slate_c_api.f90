@@ -18,6 +18,26 @@ module slate_amd
             type(c_ptr) :: slate_version
         end function
 
+        ! process grid over a torchrun-style launch (RANK / WORLD_SIZE env)
+        function slate_grid_init(p, q) bind(c, name="slate_grid_init")
+            import :: c_int
+            integer(c_int), value :: p, q
+            integer(c_int) :: slate_grid_init
+        end function
+
+        function slate_grid_rank() bind(c, name="slate_grid_rank")
+            import :: c_int
+            integer(c_int) :: slate_grid_rank
+        end function
+
+        function slate_grid_size() bind(c, name="slate_grid_size")
+            import :: c_int
+            integer(c_int) :: slate_grid_size
+        end function
+
+        subroutine slate_finalize() bind(c, name="slate_finalize")
+        end subroutine
+
         function slate_Matrix_create_fromLAPACK_r64(m, n, A, lda, nb) &
                 bind(c, name="slate_Matrix_create_fromLAPACK_r64")
             import :: c_ptr, c_int64_t, c_double

@@ -47,6 +47,15 @@ int  slate_device_available(void);
 /* install a p x q grid over a single process (p = q = 1), or return the size
  * of the grid that the Python / C++ layer installed */
 int  slate_grid_size(void);
+/* Create the p x q process grid over all ranks of a torchrun-style launch
+ * (RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT in the environment; RCCL
+ * when a GPU is visible, the native TCP transport otherwise).  p = q = 0
+ * picks the most square grid.  Returns 0, or -1 (see slate_last_error). */
+int  slate_grid_init(int p, int q);
+/* This process's rank in the grid. */
+int  slate_grid_rank(void);
+/* Barrier and tear down the grid (MPI_Finalize analog). */
+void slate_finalize(void);
 
 slate_Pivots slate_Pivots_create(void);
 void    slate_Pivots_destroy(slate_Pivots p);
@@ -139,7 +148,10 @@ int slate_copy_##X(slate_Matrix_##X A, slate_Matrix_##X B, int nopts, slate_Opti
 int slate_add_##X(scalar_t alpha, slate_Matrix_##X A, scalar_t beta, slate_Matrix_##X B, int nopts,       \
                   slate_Options const* opts);                                                             \
 int slate_scale_##X(real_t numer, real_t denom, slate_Matrix_##X A, int nopts, slate_Options const* opts); \
-int slate_set_##X(scalar_t offdiag, scalar_t diag, slate_Matrix_##X A, int nopts, slate_Options const* opts);
+int slate_set_##X(scalar_t offdiag, scalar_t diag, slate_Matrix_##X A, int nopts, slate_Options const* opts); \
+/* test matrices (matgen kinds: "rand", "rands", "randn", "spd", "rands+n", ... ; shift < 0: default) */   \
+int slate_generate_matrix_##X(const char* kind, slate_Matrix_##X A, uint64_t seed, double shift,           \
+                              int nopts, slate_Options const* opts);
 
 #ifdef __cplusplus
 #define SLATE_C32 _slate_c32

@@ -57,6 +57,11 @@ const char* slate_version(void) { return slate::version(); }
 const char* slate_last_error(void) { return g_last_error.c_str(); }
 int slate_device_available(void) { return slate::device::available() ? 1 : 0; }
 int slate_grid_size(void) { return slate::default_grid()->size(); }
+int slate_grid_rank(void) { return slate::default_grid()->rank(); }
+int slate_grid_init(int p, int q) {
+    return int(guarded([&] { slate::init_grid(p, q); return int64_t(0); }, int64_t(-1)));
+}
+void slate_finalize(void) { slate::finalize(); }
 
 slate_Pivots slate_Pivots_create(void) { return new slate_Pivots_struct(); }
 void slate_Pivots_destroy(slate_Pivots p) { delete p; }
@@ -215,6 +220,12 @@ int slate_scale_##X(X##_r numer, X##_r denom, slate_Matrix_##X A, int no, slate_
     return guarded([&]() { slate::scale(numer, denom, A->A, to_opts(no, o)); return 0; }, -1); }          \
 int slate_set_##X(X##_s offdiag, X##_s diag, slate_Matrix_##X A, int no, slate_Options const* o) {        \
     return guarded([&]() { slate::set(from_c<T>(offdiag), from_c<T>(diag), A->A, to_opts(no, o)); return 0; }, -1); } \
+int slate_generate_matrix_##X(const char* kind, slate_Matrix_##X A, uint64_t seed, double shift, int no,  \
+                              slate_Options const* o) {                                                    \
+    return guarded([&]() { slate::Options op = to_opts(no, o);                                            \
+        A->A.insertLocalTiles(slate::get_target(op, slate::Target::HostTask));                                                 \
+        slate::BaseMatrix<T>& b = A->A; slate::generate_matrix(std::string(kind), b, seed, shift, op);     \
+        return 0; }, -1); }                                                                                \
 }
 
 SLATE_C_API_DEFINE(r32, float)

@@ -42,6 +42,27 @@ def ptr(a):
     return a.ctypes.data_as(C.c_void_p)
 
 
+@pytest.mark.parametrize("nprocs", [1, 2, 4])
+def test_c_api_grid_example(tmp_path, nprocs):
+    """C program on a p x q grid bootstrapped by slate_grid_init from the
+    torchrun-style environment (native TCP transport here)."""
+    import socket
+    exe = tmp_path / "ex_c_api_grid"
+    subprocess.run(["gcc", "-std=c11", f"-I{ROOT}/csrc/include", f"{ROOT}/examples/ex_c_api_grid.c", f"-L{PKG}",
+                    "-lslate_amd", f"-Wl,-rpath,{PKG}", "-lm", "-o", str(exe)], check=True)
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    procs = [subprocess.Popen([str(exe)], stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True,
+                              env=dict(ENV, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs),
+                                       MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), SLATE_MASTER_PORT=str(port),
+                                       SLATE_COMM="host", OMP_NUM_THREADS="2"))
+             for r in range(nprocs)]
+    outs = [p.communicate(timeout=300)[0] for p in procs]
+    assert all(p.returncode == 0 for p in procs), "\n".join(outs)
+    assert "info=0" in outs[0] and f"{nprocs} ranks" in outs[0]
+
+
 def test_c_api_example(tmp_path):
     exe = tmp_path / "ex_c_api"
     subprocess.run(["gcc", "-std=c11", f"-I{ROOT}/csrc/include", f"{ROOT}/examples/ex_c_api.c", f"-L{PKG}",
