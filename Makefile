@@ -27,7 +27,7 @@ HDRS      := $(wildcard csrc/include/slate_amd/*.hh) $(wildcard csrc/kernels/*.h
 
 LIB       := $(PKG)/libslate_amd.so
 PYMOD     := $(PKG)/_slate$(PY_EXT)
-TESTER    := build/slate_tester
+TESTER    := bin/slate_tester
 LAPACK_API    := $(PKG)/libslate_lapack_api.so
 SCALAPACK_API := $(PKG)/libslate_scalapack_api.so
 
@@ -61,7 +61,10 @@ $(SCALAPACK_API): $(BUILD)/api_scalapack_api.o $(LIB)
 	$(CXX) -shared -o $@ $(BUILD)/api_scalapack_api.o -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN' $(LDLIBS)
 
 tester: $(TESTER)
-$(TESTER): csrc/tools/tester.cc $(LIB)
+# native tester (reference test/tester); like the examples it only depends on
+# its source, so a tree without build/obj does not rebuild the library
+$(TESTER): csrc/tools/tester.cc
+	@mkdir -p bin
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDLIBS)
 
 # C++ examples (reference examples/ex01-ex15), linked against the library

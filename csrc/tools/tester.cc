@@ -1,0 +1,687 @@
+// Native command-line tester and benchmark (reference test/test.cc and
+// test/test_*.cc): for each routine x type x dim x nb
+// it generates grid-independent test matrices, times the driver between a
+// barrier + device synchronization (MAX over ranks), and checks the result
+// with DISTRIBUTED backward-error residuals (no gather of the operands, so the
+// check scales with the run):
+//   BLAS-3:   C X == op-expression applied to X, X random (reference test_gemm.cc:138-211)
+//   solvers:  ||B - A X||_1 / (n ||A||_1 ||X||_1)         (test_gesv.cc:330-377)
+//   QR / LQ:  ||A - Q R||_1 / (m ||A||_1)                  (test_geqrf.cc:155-216)
+//   eig/svd:  ||A Z - Z Lambda||_1 / (n ||A||_1), ||A - U S V^H||_1 / (n ||A||_1)
+// and reports "error <= tol * eps" as pass / FAILED, one table row per case.
+//
+//   slate_tester gemm,potrf,getrf --type d,z --dim 1000:4000:1000 --nb 256 --target d
+//   python -m torch.distributed.run --nproc-per-node 8 --master-addr 127.0.0.1 \
+//       bin/slate_tester getrf_tntpiv --dim 65536 --nb 512 --grid 2x4 --check n
+#include "slate_amd/slate.hh"
+#include "slate_amd/trace.hh"
+
+#include <array>
+#include <chrono>
+#include <cmath>
+#include <complex>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <limits>
+#include <map>
+#include <sstream>
+#include <string>
+#include <vector>
+
+using namespace slate;
+
+namespace {
+
+struct Params {
+    std::string types = "d";
+    std::vector<std::array<int64_t, 3>> dims{{500, 500, 500}};
+    std::vector<int64_t> nbs{256};
+    int p = 0, q = 0;
+    Target target = device::available() ? Target::Devices : Target::HostTask;
+    int64_t lookahead = 1;
+    int64_t nrhs = 10;
+    bool check = true;
+    double tol = 50;
+    int repeat = 1;
+    bool trace = false;
+};
+
+std::vector<int64_t> parse_list(std::string const& s) {
+    std::vector<int64_t> out;
+    std::stringstream ss(s);
+    std::string part;
+    while (std::getline(ss, part, ',')) {
+        size_t c1 = part.find(':');
+        if (c1 == std::string::npos) { out.push_back(std::stoll(part)); continue; }
+        size_t c2 = part.find(':', c1 + 1);
+        int64_t a = std::stoll(part.substr(0, c1));
+        int64_t b = std::stoll(part.substr(c1 + 1, c2 == std::string::npos ? std::string::npos : c2 - c1 - 1));
+        int64_t st = c2 == std::string::npos ? a : std::stoll(part.substr(c2 + 1));
+        for (int64_t v = a; v <= b; v += st) out.push_back(v);
+    }
+    return out;
+}
+
+std::vector<std::array<int64_t, 3>> parse_dims(std::string const& s) {
+    std::vector<std::array<int64_t, 3>> out;
+    std::stringstream ss(s);
+    std::string part;
+    while (std::getline(ss, part, ',')) {
+        if (part.find('x') != std::string::npos) {
+            std::vector<int64_t> v;
+            std::stringstream ps(part);
+            std::string t;
+            while (std::getline(ps, t, 'x')) v.push_back(std::stoll(t));
+            out.push_back({v[0], v.size() > 1 ? v[1] : v[0], v.size() > 2 ? v[2] : (v.size() > 1 ? v[1] : v[0])});
+        } else {
+            for (int64_t n : parse_list(part)) out.push_back({n, n, n});
+        }
+    }
+    return out;
+}
+
+int rank() { return default_grid()->rank(); }
+
+template <typename T>
+using R_ = real_type<T>;
+
+/// One test case: matrices on the default grid, options, timing helpers.
+template <typename T>
+struct Case {
+    Params const& P;
+    int64_t m, n, k, nb;
+    uint64_t seed = 1;
+    Options opts;
+    Case(Params const& p, std::array<int64_t, 3> d, int64_t nb_)
+        : P(p), m(d[0]), n(d[1]), k(d[2]), nb(nb_) {
+        opts = {{Option::Target, P.target}, {Option::Lookahead, P.lookahead}};
+    }
+    Matrix<T> mat(int64_t rows, int64_t cols, const char* kind = "rands", double shift = -1) {
+        Matrix<T> A(rows, cols, nb, default_grid());
+        A.insertLocalTiles(P.target);
+        BaseMatrix<T>& b = A;
+        generate_matrix(std::string(kind), b, seed++, shift, opts);
+        return A;
+    }
+    Matrix<T> zeros(int64_t rows, int64_t cols) {
+        Matrix<T> A(rows, cols, nb, default_grid());
+        A.insertLocalTiles(P.target);
+        set(T(0), T(0), A, opts);
+        return A;
+    }
+    Matrix<T> copy_of(BaseMatrix<T> const& A) {
+        Matrix<T> B(A.m(), A.n(), nb, default_grid());
+        B.insertLocalTiles(P.target);
+        copy<T, T>(A, B, opts);
+        return B;
+    }
+    double nrm(BaseMatrix<T> const& A) { return double(norm(Norm::One, A, opts)); }
+    /// seconds, MAX over ranks, bracketed by barrier + device sync
+    double timed(std::function<void()> f) {
+        auto& w = default_grid()->world();
+        slate::sync();
+        w.barrier();
+        auto t0 = std::chrono::steady_clock::now();
+        f();
+        slate::sync();
+        w.barrier();
+        double t = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return w.allreduce_scalar<double>(t, ReduceOp::Max);
+    }
+    /// ||B0 - A X||_1 / (n ||A||_1 ||X||_1) for a general A
+    double solve_resid(Matrix<T> const& A0, Matrix<T> const& X, Matrix<T> const& B0) {
+        auto Rm = copy_of(B0);
+        gemm(T(-1), A0, X, T(1), Rm, opts);
+        return nrm(Rm) / (double(A0.n()) * nrm(A0) * nrm(X));
+    }
+};
+
+struct Result { double time = NAN, error = NAN; double flops = 0; bool skipped = false; std::string note; };
+
+template <typename T> double cfac() { return is_complex_v<T> ? 4.0 : 1.0; }
+template <typename T> double gemm_fl(double m, double n, double k) { return cfac<T>() * 2 * m * n * k; }
+
+//------------------------------------------------------------------------------
+// Routines
+template <typename T>
+Result r_gemm(Case<T>& c) {
+    auto A = c.mat(c.m, c.k), B = c.mat(c.k, c.n), C = c.mat(c.m, c.n);
+    auto C0 = c.copy_of(C);
+    T alpha(1.5), beta(-0.5);
+    Result r;
+    r.time = c.timed([&] { gemm(alpha, A, B, beta, C, c.opts); });
+    r.flops = gemm_fl<T>(c.m, c.n, c.k);
+    if (c.P.check) {
+        auto X = c.mat(c.n, 4), BX = c.zeros(c.k, 4), CX = c.zeros(c.m, 4), Y = c.zeros(c.m, 4);
+        gemm(T(1), C, X, T(0), CX, c.opts);          // C X
+        gemm(T(1), B, X, T(0), BX, c.opts);
+        gemm(T(1), C0, X, T(0), Y, c.opts);
+        gemm(alpha, A, BX, beta, Y, c.opts);         // alpha A (B X) + beta C0 X
+        add(T(-1), CX, T(1), Y, c.opts);
+        r.error = c.nrm(Y) / ((std::abs(alpha) * c.nrm(A) * c.nrm(B) + std::abs(beta) * c.nrm(C0)) * c.nrm(X));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_herk(Case<T>& c) {
+    auto A = c.mat(c.n, c.k), Cg = c.mat(c.n, c.n, "spd", 0.0);
+    auto C0g = c.copy_of(Cg);
+    HermitianMatrix<T> C(Uplo::Lower, Cg), C0(Uplo::Lower, C0g);
+    R_<T> alpha(2), beta(-1);
+    Result r;
+    r.time = c.timed([&] { herk(alpha, A, beta, C, c.opts); });
+    r.flops = cfac<T>() * double(c.k) * c.n * (c.n + 1);
+    if (c.P.check) {
+        auto X = c.mat(c.n, 4), CX = c.zeros(c.n, 4), Y = c.zeros(c.n, 4), AX = c.zeros(c.k, 4);
+        hemm(Side::Left, T(1), C, X, T(0), CX, c.opts);
+        hemm(Side::Left, T(beta), C0, X, T(0), Y, c.opts);
+        gemm(T(1), conj_transpose(A), X, T(0), AX, c.opts);
+        gemm(T(alpha), A, AX, T(1), Y, c.opts);
+        add(T(-1), CX, T(1), Y, c.opts);
+        r.error = c.nrm(Y) / ((double(alpha) * c.nrm(A) * c.nrm(A) + std::abs(double(beta)) * c.nrm(C0g)) * c.nrm(X));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_hemm(Case<T>& c) {
+    auto Ag = c.mat(c.m, c.m, "spd", 0.0), B = c.mat(c.m, c.n), C = c.mat(c.m, c.n);
+    auto C0 = c.copy_of(C);
+    HermitianMatrix<T> A(Uplo::Lower, Ag);
+    T alpha(1), beta(0.5);
+    Result r;
+    r.time = c.timed([&] { hemm(Side::Left, alpha, A, B, beta, C, c.opts); });
+    r.flops = gemm_fl<T>(c.m, c.n, c.m);
+    if (c.P.check) {
+        auto X = c.mat(c.n, 4), CX = c.zeros(c.m, 4), BX = c.zeros(c.m, 4), Y = c.zeros(c.m, 4);
+        gemm(T(1), C, X, T(0), CX, c.opts);
+        gemm(T(1), B, X, T(0), BX, c.opts);
+        gemm(beta, C0, X, T(0), Y, c.opts);
+        hemm(Side::Left, alpha, A, BX, T(1), Y, c.opts);
+        add(T(-1), CX, T(1), Y, c.opts);
+        r.error = c.nrm(Y) / ((c.nrm(Ag) * c.nrm(B) + std::abs(beta) * c.nrm(C0)) * c.nrm(X));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_trsm(Case<T>& c) {
+    auto Tg = c.mat(c.m, c.m, "rands+n"), B = c.mat(c.m, c.n);
+    auto B0 = c.copy_of(B);
+    TriangularMatrix<T> L(Uplo::Lower, Diag::NonUnit, Tg);
+    T alpha(2);
+    Result r;
+    r.time = c.timed([&] { trsm(Side::Left, alpha, L, B, c.opts); });
+    r.flops = cfac<T>() * double(c.m) * c.m * c.n;
+    if (c.P.check) {
+        auto X = c.copy_of(B);
+        trmm(Side::Left, T(1), L, X, c.opts);          // L X
+        add(-alpha, B0, T(1), X, c.opts);              // L X - alpha B0
+        r.error = c.nrm(X) / (c.nrm(Tg) * c.nrm(B) * double(c.m));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_trmm(Case<T>& c) {
+    auto Tg = c.mat(c.m, c.m, "rands+n"), B = c.mat(c.m, c.n);
+    auto B0 = c.copy_of(B);
+    TriangularMatrix<T> U(Uplo::Upper, Diag::NonUnit, Tg);
+    Result r;
+    r.time = c.timed([&] { trmm(Side::Left, T(1), U, B, c.opts); });
+    r.flops = cfac<T>() * double(c.m) * c.m * c.n;
+    if (c.P.check) {
+        auto X = c.copy_of(B);
+        trsm(Side::Left, T(1), U, X, c.opts);           // U^{-1} (U B0) = B0
+        add(T(-1), B0, T(1), X, c.opts);
+        r.error = c.nrm(X) / (c.nrm(B0) * double(c.m));
+    }
+    return r;
+}
+
+// factor / solve family: run(A, B) factors and solves in place, residual vs A0
+template <typename T>
+Result solve_case(Case<T>& c, const char* kind, std::function<int64_t(Matrix<T>&, Matrix<T>&)> run,
+                  double flops) {
+    auto A = c.mat(c.n, c.n, kind), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(B);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = run(A, B); });
+    r.flops = flops;
+    if (info != 0) { r.error = INFINITY; r.note = "info=" + std::to_string(info); return r; }
+    if (c.P.check) r.error = c.solve_resid(A0, B, B0);
+    return r;
+}
+
+template <typename T> double getrf_fl(double n) { return cfac<T>() * (2.0 / 3 * n * n * n - 0.5 * n * n + 5.0 / 6 * n); }
+template <typename T> double potrf_fl(double n) { return cfac<T>() * (n * n * n / 3 + n * n / 2 + n / 6); }
+
+/// factorization timed alone; the solve for the check runs afterwards
+template <typename T>
+Result r_getrf_m(Case<T>& c, int64_t method) {
+    auto A = c.mat(c.n, c.n), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(B);
+    Pivots piv;
+    Options o = c.opts;
+    o[Option::MethodLU] = method;
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = getrf(A, piv, o); });
+    r.flops = getrf_fl<T>(c.n);
+    if (info) { r.error = INFINITY; r.note = "info=" + std::to_string(info); return r; }
+    if (c.P.check) {
+        getrs(A, piv, B, c.opts);
+        r.error = c.solve_resid(A0, B, B0);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_getrf_nopiv(Case<T>& c) {
+    auto A = c.mat(c.n, c.n, "rands+n"), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(B);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = getrf_nopiv(A, c.opts); });
+    r.flops = getrf_fl<T>(c.n);
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {
+        getrs_nopiv(A, B, c.opts);
+        r.error = c.solve_resid(A0, B, B0);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_gesv(Case<T>& c) {
+    return solve_case<T>(c, "rands", [&](Matrix<T>& A, Matrix<T>& B) { Pivots piv; return gesv(A, piv, B, c.opts); },
+                         getrf_fl<T>(c.n) + cfac<T>() * 2.0 * c.n * c.n * c.P.nrhs);
+}
+
+template <typename T>
+Result r_gesv_mixed_v(Case<T>& c, int variant) {
+    if constexpr (!std::is_same_v<T, double> && !std::is_same_v<T, std::complex<double>>) {
+        Result r; r.skipped = true; r.note = "double precisions only"; return r;
+    } else {
+        const int64_t nrhs = variant == 1 ? 1 : c.P.nrhs;   // GMRES-IR: one right-hand side
+        auto A = c.mat(c.n, c.n, variant == 2 ? "spd" : "rands+n"), B = c.mat(c.n, nrhs);
+        auto A0 = c.copy_of(A), X = c.zeros(c.n, nrhs);
+        Result r;
+        int64_t info = 0;
+        int iter = 0;
+        r.time = c.timed([&] {
+            Pivots piv;
+            if (variant == 0) info = gesv_mixed(A, piv, B, X, iter, c.opts);
+            else if (variant == 1) info = gesv_mixed_gmres(A, piv, B, X, iter, c.opts);
+            else {
+                HermitianMatrix<T> H(Uplo::Lower, A);
+                info = posv_mixed(H, B, X, iter, c.opts);
+            }
+        });
+        r.flops = variant == 2 ? potrf_fl<T>(c.n) : getrf_fl<T>(c.n);
+        r.note = "iter=" + std::to_string(iter);
+        if (info) { r.error = INFINITY; return r; }
+        if (c.P.check) r.error = c.solve_resid(A0, X, B);
+        return r;
+    }
+}
+
+template <typename T>
+Result r_posv(Case<T>& c, bool factor_only) {
+    auto Ag = c.mat(c.n, c.n, "spd"), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(Ag), B0 = c.copy_of(B);
+    HermitianMatrix<T> A(Uplo::Lower, Ag);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = factor_only ? potrf(A, c.opts) : posv(A, B, c.opts); });
+    r.flops = potrf_fl<T>(c.n);
+    if (info) { r.error = INFINITY; r.note = "info=" + std::to_string(info); return r; }
+    if (c.P.check) {
+        if (factor_only) potrs(A, B, c.opts);
+        r.error = c.solve_resid(A0, B, B0);   // "spd" is generated as a full Hermitian matrix
+    }
+    return r;
+}
+
+template <typename T>
+Result r_getri(Case<T>& c) {
+    auto A = c.mat(c.n, c.n, "rands+n");
+    auto A0 = c.copy_of(A);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] {
+        Pivots piv;
+        info = getrf(A, piv, c.opts);
+        if (!info) info = getri(A, piv, c.opts);
+    });
+    r.flops = getrf_fl<T>(c.n) + cfac<T>() * 4.0 / 3 * double(c.n) * c.n * c.n;
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {
+        auto I = c.zeros(c.n, c.n);
+        set(T(0), T(1), I, c.opts);
+        gemm(T(1), A0, A, T(-1), I, c.opts);
+        r.error = c.nrm(I) / (double(c.n) * c.nrm(A0) * c.nrm(A));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_trtri(Case<T>& c) {
+    auto Tg = c.mat(c.n, c.n, "rands+n");
+    auto T0g = c.copy_of(Tg);
+    TriangularMatrix<T> L(Uplo::Lower, Diag::NonUnit, Tg), L0(Uplo::Lower, Diag::NonUnit, T0g);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = trtri(L, c.opts); });
+    r.flops = cfac<T>() * double(c.n) * c.n * c.n / 3;
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {
+        // L0 * inv(L) = I, inv(L) materialized as a general lower matrix
+        auto Li = c.zeros(c.n, c.n);
+        BaseTrapezoidMatrix<T> Ls(Uplo::Lower, Tg, MatrixKind::Trapezoid), Ld(Uplo::Lower, Li, MatrixKind::Trapezoid);
+        copy<T, T>(Ls, Ld, c.opts);
+        trmm(Side::Left, T(1), L0, Li, c.opts);
+        auto I = c.zeros(c.n, c.n);
+        set(T(0), T(1), I, c.opts);
+        add(T(-1), I, T(1), Li, c.opts);
+        r.error = c.nrm(Li) / double(c.n);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_geqrf(Case<T>& c) {
+    auto A = c.mat(c.m, c.n);
+    auto A0 = c.copy_of(A);
+    TriangularFactors<T> Tf;
+    Result r;
+    r.time = c.timed([&] { geqrf(A, Tf, c.opts); });
+    double m = double(c.m), n = double(c.n);
+    r.flops = cfac<T>() * (c.m >= c.n ? 2 * m * n * n - 2.0 / 3 * n * n * n : 2 * n * m * m - 2.0 / 3 * m * m * m);
+    if (c.P.check) {
+        // Q R with R = triu(A) (m x n), Q applied by unmqr
+        auto QR = c.zeros(c.m, c.n);
+        BaseTrapezoidMatrix<T> Rt(Uplo::Upper, A, MatrixKind::Trapezoid), Qt(Uplo::Upper, QR, MatrixKind::Trapezoid);
+        copy<T, T>(Rt, Qt, c.opts);
+        unmqr(Side::Left, Op::NoTrans, A, Tf, QR, c.opts);
+        add(T(-1), A0, T(1), QR, c.opts);
+        r.error = c.nrm(QR) / (double(c.m) * c.nrm(A0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_gelqf(Case<T>& c) {
+    auto A = c.mat(c.m, c.n);
+    auto A0 = c.copy_of(A);
+    TriangularFactors<T> Tf;
+    Result r;
+    r.time = c.timed([&] { gelqf(A, Tf, c.opts); });
+    double m = double(c.m), n = double(c.n);
+    r.flops = cfac<T>() * (c.n >= c.m ? 2 * n * m * m - 2.0 / 3 * m * m * m : 2 * m * n * n - 2.0 / 3 * n * n * n);
+    if (c.P.check) {
+        auto LQ = c.zeros(c.m, c.n);
+        BaseTrapezoidMatrix<T> Lt(Uplo::Lower, A, MatrixKind::Trapezoid), Qt(Uplo::Lower, LQ, MatrixKind::Trapezoid);
+        copy<T, T>(Lt, Qt, c.opts);
+        unmlq(Side::Right, Op::NoTrans, A, Tf, LQ, c.opts);
+        add(T(-1), A0, T(1), LQ, c.opts);
+        r.error = c.nrm(LQ) / (double(c.n) * c.nrm(A0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_gels(Case<T>& c) {
+    auto A = c.mat(c.m, c.n), BX = c.mat(std::max(c.m, c.n), c.P.nrhs);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(BX);
+    TriangularFactors<T> Tf;
+    Result r;
+    r.time = c.timed([&] { gels(A, Tf, BX, c.opts); });
+    r.flops = cfac<T>() * 2.0 * c.m * c.n * std::min(c.m, c.n);
+    if (c.P.check) {
+        Matrix<T> X = BX.slice(0, c.n - 1, 0, c.P.nrhs - 1);
+        auto Rr = c.copy_of(B0.slice(0, c.m - 1, 0, c.P.nrhs - 1));
+        gemm(T(-1), A0, X, T(1), Rr, c.opts);
+        if (c.m >= c.n) {
+            auto G = c.zeros(c.n, c.P.nrhs);
+            gemm(T(1), conj_transpose(A0), Rr, T(0), G, c.opts);        // A^H (b - A x) = 0
+            r.error = c.nrm(G) / (c.nrm(A0) * c.nrm(A0) * c.nrm(X) * double(c.n));
+        } else {
+            r.error = c.nrm(Rr) / (c.nrm(A0) * c.nrm(X) * double(c.n));
+        }
+    }
+    return r;
+}
+
+template <typename T>
+Result r_heev(Case<T>& c) {
+    auto Ag = c.mat(c.n, c.n, "spd", 0.0);
+    auto A0 = c.copy_of(Ag);
+    HermitianMatrix<T> A(Uplo::Lower, Ag);
+    auto Z = c.zeros(c.n, c.n);
+    std::vector<R_<T>> L;
+    Result r;
+    r.time = c.timed([&] { heev(A, L, Z, c.opts); });
+    r.flops = cfac<T>() * 4.0 / 3 * double(c.n) * c.n * c.n;
+    if (c.P.check) {
+        auto AZ = c.zeros(c.n, c.n), ZL = c.copy_of(Z);
+        gemm(T(1), A0, Z, T(0), AZ, c.opts);
+        std::vector<R_<T>> ones(c.n, R_<T>(1));
+        scale_row_col(Equed::Col, ones, L, ZL, c.opts);
+        add(T(-1), ZL, T(1), AZ, c.opts);
+        r.error = c.nrm(AZ) / (double(c.n) * c.nrm(A0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_svd(Case<T>& c) {
+    auto A = c.mat(c.m, c.n);
+    auto A0 = c.copy_of(A);
+    int64_t k = std::min(c.m, c.n);
+    auto U = c.zeros(c.m, k), VT = c.zeros(k, c.n);
+    std::vector<R_<T>> S;
+    Result r;
+    r.time = c.timed([&] { svd(A, S, U, VT, c.opts); });
+    r.flops = cfac<T>() * 8.0 / 3 * double(k) * k * k;
+    if (c.P.check) {
+        std::vector<R_<T>> ones(c.m, R_<T>(1));
+        scale_row_col(Equed::Col, ones, S, U, c.opts);
+        double a0 = c.nrm(A0);
+        gemm(T(1), U, VT, T(-1), A0, c.opts);
+        r.error = c.nrm(A0) / (double(k) * a0);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_hesv(Case<T>& c) {
+    auto Ag = c.mat(c.n, c.n, "spd", 0.0), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(Ag), B0 = c.copy_of(B);
+    HermitianMatrix<T> A(Uplo::Lower, Ag);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { std::vector<int64_t> ipiv; info = hesv(A, ipiv, B, c.opts); });
+    r.flops = cfac<T>() * double(c.n) * c.n * c.n / 3;
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) r.error = c.solve_resid(A0, B, B0);
+    return r;
+}
+
+template <typename T>
+Result r_gbsv(Case<T>& c) {
+    int64_t kl = std::max<int64_t>(1, c.nb / 4), ku = kl;
+    auto Ag = c.mat(c.n, c.n, "rands+n"), B = c.mat(c.n, c.P.nrhs);
+    auto A0g = c.copy_of(Ag), B0 = c.copy_of(B);
+    BandMatrix<T> A(kl, ku, Ag), A0(kl, ku, A0g);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { Pivots piv; info = gbsv(A, piv, B, c.opts); });
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {
+        auto Rm = c.copy_of(B0);
+        gbmm(T(-1), A0, B, T(1), Rm, c.opts);
+        r.error = c.nrm(Rm) / (double(c.n) * c.nrm(B0) * c.nrm(B));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_genorm(Case<T>& c) {
+    auto A = c.mat(c.m, c.n);
+    Result r;
+    R_<T> v1 = 0;
+    r.time = c.timed([&] { v1 = norm(Norm::One, A, c.opts); });
+    r.flops = double(c.m) * c.n;
+    if (c.P.check) {
+        // one-norm of A == inf-norm of A^H (materialized)
+        auto AH = c.zeros(c.n, c.m);
+        copy<T, T>(conj_transpose(A), AH, c.opts);
+        R_<T> v2 = norm(Norm::Inf, AH, c.opts);
+        r.error = std::abs(double(v1 - v2)) / double(v1);
+    }
+    return r;
+}
+
+template <typename T>
+using Fn = std::function<Result(Case<T>&)>;
+
+template <typename T>
+std::map<std::string, Fn<T>> routines() {
+    return {
+        {"gemm", r_gemm<T>}, {"herk", r_herk<T>}, {"hemm", r_hemm<T>}, {"trsm", r_trsm<T>}, {"trmm", r_trmm<T>},
+        {"getrf", [](Case<T>& c) { return r_getrf_m<T>(c, MethodLU::PartialPiv); }},
+        {"getrf_tntpiv", [](Case<T>& c) { return r_getrf_m<T>(c, MethodLU::CALU); }},
+        {"getrf_nopiv", r_getrf_nopiv<T>}, {"gesv", r_gesv<T>},
+        {"gesv_mixed", [](Case<T>& c) { return r_gesv_mixed_v<T>(c, 0); }},
+        {"gesv_mixed_gmres", [](Case<T>& c) { return r_gesv_mixed_v<T>(c, 1); }},
+        {"posv_mixed", [](Case<T>& c) { return r_gesv_mixed_v<T>(c, 2); }},
+        {"potrf", [](Case<T>& c) { return r_posv<T>(c, true); }},
+        {"posv", [](Case<T>& c) { return r_posv<T>(c, false); }},
+        {"getri", r_getri<T>}, {"trtri", r_trtri<T>},
+        {"geqrf", r_geqrf<T>}, {"gelqf", r_gelqf<T>}, {"gels", r_gels<T>},
+        {"heev", r_heev<T>}, {"svd", r_svd<T>}, {"hesv", r_hesv<T>}, {"gbsv", r_gbsv<T>}, {"genorm", r_genorm<T>},
+    };
+}
+
+template <typename T>
+double eps_of() { return double(std::numeric_limits<R_<T>>::epsilon()); }
+
+template <typename T>
+int run_type(Params const& P, char tc, std::string const& name) {
+    auto table = routines<T>();
+    auto it = table.find(name);
+    if (it == table.end()) {
+        if (rank() == 0) std::fprintf(stderr, "unknown routine %s\n", name.c_str());
+        return 1;
+    }
+    int fails = 0;
+    auto g = default_grid();
+    for (auto const& d : P.dims)
+        for (int64_t nb : P.nbs)
+            for (int rep = 0; rep < P.repeat; ++rep) {
+                Case<T> c(P, d, nb);
+                Result r;
+                std::string status;
+                try {
+                    r = it->second(c);
+                    if (r.skipped) status = "skip (" + r.note + ")";
+                    else {
+                        bool ok = !P.check || r.error <= P.tol * eps_of<T>();
+                        status = ok ? "pass" : "FAILED";
+                        fails += !ok;
+                    }
+                } catch (std::exception const& e) {
+                    status = std::string("FAILED: ") + e.what();
+                    ++fails;
+                }
+                if (rank() == 0) {
+                    char es[32];
+                    if (P.check && !r.skipped && !std::isnan(r.error)) std::snprintf(es, sizeof(es), "%10.2e", r.error);
+                    else std::snprintf(es, sizeof(es), "%10s", "NA");
+                    double gf = (r.time > 0 && r.flops > 0) ? r.flops / r.time / 1e9 : NAN;
+                    std::printf("%-16s %-4c %7lld %7lld %7lld %5lld %2d %2d %s %10.4f %11.2f  %s%s%s\n", name.c_str(), tc,
+                                (long long)c.m, (long long)c.n, (long long)c.k, (long long)nb, g->p(), g->q(), es,
+                                r.time, gf, status.c_str(), r.note.empty() ? "" : "  ", r.note.c_str());
+                    std::fflush(stdout);
+                }
+            }
+    return fails;
+}
+
+void usage() {
+    std::printf(
+        "usage: slate_tester ROUTINE[,ROUTINE...]|all [--type d,s,z,c] [--dim N|A:B:STEP|MxNxK,...]\n"
+        "       [--nb NB,...] [--grid PxQ] [--target d|h] [--lookahead LA] [--nrhs K]\n"
+        "       [--check y|n] [--tol T] [--repeat R] [--trace y|n]\n"
+        "routines:");
+    for (auto const& kv : routines<double>()) std::printf(" %s", kv.first.c_str());
+    std::printf("\n");
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    Params P;
+    std::string rlist;
+    for (int i = 1; i < argc; ++i) {
+        std::string a = argv[i];
+        auto val = [&]() -> std::string {
+            if (i + 1 >= argc) { usage(); std::exit(2); }
+            return argv[++i];
+        };
+        if (a == "-h" || a == "--help") { usage(); return 0; }
+        else if (a == "--type") P.types = val();
+        else if (a == "--dim") P.dims = parse_dims(val());
+        else if (a == "--nb") P.nbs = parse_list(val());
+        else if (a == "--grid") {
+            std::string g = val();
+            P.p = std::stoi(g.substr(0, g.find('x')));
+            P.q = std::stoi(g.substr(g.find('x') + 1));
+        }
+        else if (a == "--target") { std::string t = val(); P.target = (t[0] == 'd' || t[0] == 'D') ? Target::Devices : Target::HostTask; }
+        else if (a == "--lookahead" || a == "--la") P.lookahead = std::stoll(val());
+        else if (a == "--nrhs") P.nrhs = std::stoll(val());
+        else if (a == "--check") P.check = val()[0] == 'y';
+        else if (a == "--tol") P.tol = std::stod(val());
+        else if (a == "--repeat") P.repeat = std::stoi(val());
+        else if (a == "--trace") P.trace = val()[0] == 'y';
+        else if (!a.empty() && a[0] != '-') rlist = rlist.empty() ? a : rlist + "," + a;
+        else { usage(); return 2; }
+    }
+    if (rlist.empty()) { usage(); return 2; }
+    init_grid(P.p, P.q);
+    if (rlist == "all") {
+        rlist.clear();
+        for (auto const& kv : routines<double>()) rlist += (rlist.empty() ? "" : ",") + kv.first;
+    }
+    if (rank() == 0) {
+        std::printf("# slate %s tester: %d process(es), grid %dx%d, target %s\n", version(), default_grid()->size(),
+                    default_grid()->p(), default_grid()->q(), P.target == Target::Devices ? "devices" : "host");
+        std::printf("%-16s %-4s %7s %7s %7s %5s %2s %2s %10s %10s %11s  %s\n", "routine", "type", "m", "n", "k", "nb",
+                    "p", "q", "error", "time(s)", "gflop/s", "status");
+    }
+    if (P.trace) trace::Trace::on();
+    int fails = 0;
+    std::stringstream rs(rlist);
+    std::string name;
+    while (std::getline(rs, name, ','))
+        for (char tc : P.types) {
+            switch (tc) {
+                case 's': fails += run_type<float>(P, tc, name); break;
+                case 'd': fails += run_type<double>(P, tc, name); break;
+                case 'c': fails += run_type<std::complex<float>>(P, tc, name); break;
+                case 'z': fails += run_type<std::complex<double>>(P, tc, name); break;
+                default: break;
+            }
+        }
+    if (P.trace) trace::Trace::finish(&default_grid()->world());
+    int total = int(default_grid()->world().allreduce_scalar<int32_t>(fails, ReduceOp::Sum));
+    if (rank() == 0) std::printf(total ? "# %d failed\n" : "# all tests passed\n", total);
+    finalize();
+    return total ? 1 : 0;
+}
