@@ -31,8 +31,8 @@
 #ifndef GEMM_JB
 #define GEMM_JB 2
 #endif
-#ifndef GEMM_FDB
-#define GEMM_FDB false
+#ifndef GEMM_ROT
+#define GEMM_ROT true
 #endif
 
 namespace slate_amd {
@@ -137,6 +137,9 @@ struct TileLoader {
         }
     }
 
+    static constexpr int elems(int LD) { return BK * LD + 32; }   // + max skew
+    __device__ static inline int at(int LD, int x, int kr) { return kr * LD + lds_skew<T>(kr) + x; }
+
     // store into LDS image row kk at kk*LD + lds_skew(kk), column x
     template <int LD>
     __device__ inline void store(T* L) const {
@@ -222,7 +225,7 @@ __device__ inline void gemm_tile_coords(int64_t m, int64_t n, int BM, int BN, in
 // (4 waves, 2 workgroups per CU) or 256 x 128 (8 waves, 1 workgroup per CU:
 // 25% less operand traffic per flop for large C).
 template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI, int WTN_ = 64, int WTM_ = 64,
-          bool FDB = false>
+          bool ROT = false>
 __global__ __launch_bounds__(64 * (BM / WTM_) * (BN / WTN_),
     (2 * BK * (BM + BN + 32) * sizeof(T) > 81920) ? 1 : 512 / (64 * (BM / WTM_) * (BN / WTN_)))
 void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
@@ -239,9 +242,11 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     constexpr int WN = BN / WTN;                     // waves along N
     constexpr int NTHR = 64 * (BM / WTM) * WN;
     constexpr int TM = WTM / 16, TN = WTN / 16;     // MFMA tiles per wave
-    constexpr int A_ELEMS = BK * LDA_S + 32, B_ELEMS = BK * LDB_S + 32;  // + max skew
+    using LA = TileLoader<T, BM, BK, A_KC, NTHR>;
+    using LB = TileLoader<T, BN, BK, B_KC, NTHR>;
+    constexpr int A_ELEMS = LA::elems(LDA_S), B_ELEMS = LB::elems(LDB_S);
 
-    __shared__ T smem[2 * (A_ELEMS + B_ELEMS)];
+    __shared__ __attribute__((aligned(16))) T smem[2 * (A_ELEMS + B_ELEMS)];
 
     // batch offset
     const int64_t bz = blockIdx.y;
@@ -283,8 +288,8 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         for (int j = 0; j < TN; ++j)
             acc[i][j] = acc_t{0, 0, 0, 0};
 
-    TileLoader<T, BM, BK, A_KC, NTHR> la;
-    TileLoader<T, BN, BK, B_KC, NTHR> lb;
+    LA la;
+    LB lb;
     const bool mfull = (m0 + BM <= m), nfull = (n0 + BN <= n);
 
     const int KT = (int)((k + BK - 1) / BK);
@@ -315,14 +320,57 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     // hides behind 16 MFMAs instead of stalling every step.
     auto frag = [&](const T* As, const T* Bs, int s, T (&a)[TM], T (&b)[TN]) {
         const int kr = s * 4 + (lane >> 4);
-        const int sk = lds_skew<T>(kr);
         #pragma unroll
         for (int i = 0; i < TM; ++i)
-            a[i] = As[kr * LDA_S + sk + wm * WTM + i * 16 + (lane & 15)];
+            a[i] = As[LA::at(LDA_S, wm * WTM + i * 16 + (lane & 15), kr)];
         #pragma unroll
         for (int j = 0; j < TN; ++j)
-            b[j] = Bs[kr * LDB_S + sk + wn * WTN + j * 16 + (lane & 15)];
+            b[j] = Bs[LB::at(LDB_S, wn * WTN + j * 16 + (lane & 15), kr)];
     };
+    auto mfma_step = [&](const T (&a)[TM], const T (&b)[TN]) {
+        #pragma unroll
+        for (int i = 0; i < TM; ++i)
+            #pragma unroll
+            for (int j = 0; j < TN; ++j)
+                acc[i][j] = M::run(b[j], a[i], acc[i][j]);
+    };
+    if constexpr (ROT) {
+        // Rotated pipeline: the last k-step's MFMAs of tile kt are issued
+        // AFTER the barrier, behind the LDS reads of tile kt+1's first step,
+        // so the post-barrier LDS latency hides under 16 MFMAs instead of
+        // idling the matrix pipe once per K-tile.
+        T fa[2][TM], fb[2][TN];
+        if (KT > 0) frag(smem, smem + A_ELEMS, 0, fa[0], fb[0]);
+        for (int kt = 0; kt < KT; ++kt) {
+            const int cur = kt & 1;
+            const bool more = (kt + 1 < KT);
+            if (more) {
+                int64_t k0 = (int64_t)(kt + 1) * BK;
+                bool kfull = (k0 + BK <= k);
+                load_a(k0, kfull);
+                load_b(k0, kfull);
+            }
+            const T* As = smem + cur * (A_ELEMS + B_ELEMS);
+            const T* Bs = As + A_ELEMS;
+            #pragma unroll
+            for (int s = 0; s < BK / 4 - 1; ++s) {
+                frag(As, Bs, s + 1, fa[(s + 1) & 1], fb[(s + 1) & 1]);
+                mfma_step(fa[s & 1], fb[s & 1]);
+            }
+            constexpr int LAST = (BK / 4 - 1) & 1;
+            if (more) {
+                T* Asn = smem + (cur ^ 1) * (A_ELEMS + B_ELEMS);
+                la.template store<LDA_S>(Asn);
+                lb.template store<LDB_S>(Asn + A_ELEMS);
+            }
+            __syncthreads();
+            if (more) {
+                const T* An = smem + (cur ^ 1) * (A_ELEMS + B_ELEMS);
+                frag(An, An + A_ELEMS, 0, fa[LAST ^ 1], fb[LAST ^ 1]);
+            }
+            mfma_step(fa[LAST], fb[LAST]);
+        }
+    } else {
     for (int kt = 0; kt < KT; ++kt) {
         const int cur = kt & 1;
         const bool more = (kt + 1 < KT);
@@ -334,29 +382,11 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         }
         const T* As = smem + cur * (A_ELEMS + B_ELEMS);
         const T* Bs = As + A_ELEMS;
-        if constexpr (FDB) {
-        T a[2][TM], b[2][TN];
-        frag(As, Bs, 0, a[0], b[0]);
-        #pragma unroll
-        for (int s = 0; s < BK / 4; ++s) {
-            if (s + 1 < BK / 4) frag(As, Bs, s + 1, a[(s + 1) & 1], b[(s + 1) & 1]);
-            #pragma unroll
-            for (int i = 0; i < TM; ++i)
-                #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = M::run(b[s & 1][j], a[s & 1][i], acc[i][j]);
-        }
-        } else {
         #pragma unroll
         for (int s = 0; s < BK / 4; ++s) {
             T a[TM], b[TN];
             frag(As, Bs, s, a, b);
-            #pragma unroll
-            for (int i = 0; i < TM; ++i)
-                #pragma unroll
-                for (int j = 0; j < TN; ++j)
-                    acc[i][j] = M::run(b[j], a[i], acc[i][j]);
-        }
+            mfma_step(a, b);
         }
         if (more) {
             T* Asn = smem + (cur ^ 1) * (A_ELEMS + B_ELEMS);
@@ -364,6 +394,7 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
             lb.template store<LDB_S>(Asn + A_ELEMS);
         }
         __syncthreads();
+    }
     }
     };
     if (GEMM_SPLIT && aligned && mfull && nfull && k % BK == 0) kloop(std::true_type{});
@@ -373,7 +404,7 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
 }
 
 template <typename T, bool A_KC, bool B_KC, char TRI, int BM, int BN, int BK = 16, int WTN = 64, int WTM = 64,
-          bool FDB = GEMM_FDB>
+          bool ROT = (GEMM_ROT && sizeof(T) == 8)>
 static void launch_tile(int64_t m, int64_t n, int64_t k, T alpha,
                         const T* A, int64_t lda, int64_t sA,
                         const T* B, int64_t ldb, int64_t sB,
@@ -384,7 +415,7 @@ static void launch_tile(int64_t m, int64_t n, int64_t k, T alpha,
     int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
     int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
     dim3 grid((unsigned)nblk, (unsigned)batch);
-    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, FDB>), grid, dim3(NTHR), 0, stream,
+    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, ROT>), grid, dim3(NTHR), 0, stream,
                        m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
 }
 

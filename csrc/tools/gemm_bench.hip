@@ -8,6 +8,7 @@
 #include <vector>
 #include <cmath>
 #include <chrono>
+#include <algorithm>
 
 using namespace slate_amd::dev;
 
@@ -81,30 +82,41 @@ double check(char ta, char tb, int64_t m, int64_t n, int64_t k, int64_t pad) {
 }
 
 template <typename T>
-void timeit(char ta, char tb, int64_t n, int64_t k, int reps) {
+void timeit(char ta, char tb, int64_t n, int64_t k, int reps, int64_t pad = 0) {
     T *A, *B, *C;
-    CHECK(hipMalloc(&A, n * k * sizeof(T))); CHECK(hipMalloc(&B, n * k * sizeof(T))); CHECK(hipMalloc(&C, n * n * sizeof(T)));
-    double* tmp; CHECK(hipMalloc(&tmp, n * k * 8));
-    fill<<<(n * k + 255) / 256, 256>>>(tmp, n * k, 5);
-    if constexpr (sizeof(T) == 8) { CHECK(hipMemcpy(A, tmp, n * k * 8, hipMemcpyDeviceToDevice)); CHECK(hipMemcpy(B, tmp, n * k * 8, hipMemcpyDeviceToDevice)); }
-    else { tofloat<<<(n * k + 255) / 256, 256>>>(tmp, (float*)A, n * k); tofloat<<<(n * k + 255) / 256, 256>>>(tmp, (float*)B, n * k); }
-    CHECK(hipMemset(C, 0, n * n * sizeof(T)));
-    int64_t lda = ta == 'N' ? n : k, ldb = tb == 'N' ? k : n;
-    gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, n, 0, 1, 0);
+    const int64_t ne = (std::max(n, k) + pad) * std::max(n, k);   // operand storage incl. padded ld
+    CHECK(hipMalloc(&A, ne * sizeof(T))); CHECK(hipMalloc(&B, ne * sizeof(T))); CHECK(hipMalloc(&C, (n + pad) * n * sizeof(T)));
+    double* tmp; CHECK(hipMalloc(&tmp, ne * 8));
+    fill<<<(ne + 255) / 256, 256>>>(tmp, ne, 5);
+    if constexpr (sizeof(T) == 8) { CHECK(hipMemcpy(A, tmp, ne * 8, hipMemcpyDeviceToDevice)); CHECK(hipMemcpy(B, tmp, ne * 8, hipMemcpyDeviceToDevice)); }
+    else { tofloat<<<(ne + 255) / 256, 256>>>(tmp, (float*)A, ne); tofloat<<<(ne + 255) / 256, 256>>>(tmp, (float*)B, ne); }
+    CHECK(hipMemset(C, 0, (n + pad) * n * sizeof(T)));
+    int64_t lda = (ta == 'N' ? n : k) + pad, ldb = (tb == 'N' ? k : n) + pad;
+    const int64_t ldc = n + pad;
+    gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, ldc, 0, 1, 0);
     CHECK(hipDeviceSynchronize());
     hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
     hipEventRecord(e0);
     for (int r = 0; r < reps; ++r)
-        gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, n, 0, 1, 0);
+        gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, ldc, 0, 1, 0);
     hipEventRecord(e1); hipEventSynchronize(e1);
     float ms; hipEventElapsedTime(&ms, e0, e1);
     double tf = 2.0 * n * n * k * reps / (ms * 1e-3) / 1e12;
-    printf("%s %c%c n=%ld k=%ld : %.3f ms/call  %.2f TFLOP/s\n", sizeof(T) == 8 ? "dgemm" : "sgemm", ta, tb, n, k, ms / reps, tf);
+    printf("%s %c%c n=%ld k=%ld ldpad=%ld : %.3f ms/call  %.2f TFLOP/s\n", sizeof(T) == 8 ? "dgemm" : "sgemm", ta, tb, n, k, pad, ms / reps, tf);
     hipFree(A); hipFree(B); hipFree(C); hipFree(tmp);
 }
 
 int main(int argc, char** argv) {
     const char ops[2] = {'N', 'T'};
+    if (argc > 2) {   // gemm_bench N K pad [reps]: leading-dimension padding study only
+        int64_t N = atoll(argv[1]), K = atoll(argv[2]), pad = argc > 3 ? atoll(argv[3]) : 0;
+        int reps = argc > 4 ? atoi(argv[4]) : 1;
+        timeit<double>('N', 'N', N, K, 1, pad);   // warm
+        timeit<double>('N', 'N', N, K, reps, pad);
+        timeit<double>('N', 'T', N, K, reps, pad);
+        timeit<double>('T', 'N', N, K, reps, pad);
+        return 0;
+    }
     int64_t shapes[][3] = {{1, 1, 1}, {17, 33, 5}, {128, 128, 16}, {129, 131, 67}, {300, 257, 513}, {1000, 999, 77}};
     bool ok = true;
     for (auto& s : shapes)
