@@ -17,11 +17,22 @@
 // the panel's nb x nb upper-triangular T).
 #include "internal.hh"
 
+#include <cstdlib>
+
 namespace slate {
 
 using namespace internal;
 
 namespace {
+
+/// K-chunk (rows) of the trailing update's W = V^H C; SLATE_QR_KCHUNK, 0 = off
+inline int64_t qr_kchunk() {
+    static int64_t v = [] {
+        const char* e = std::getenv("SLATE_QR_KCHUNK");
+        return e ? std::atoll(e) : int64_t(8192);
+    }();
+    return v;
+}
 
 template <typename T>
 void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
@@ -146,7 +157,17 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
             T* W = Wk + c0 * kb;
             T* W2 = W2k + c0 * kb;
             // W = V^H C  (kb x nc), all-reduced over the process column
-            if (mr > 0) lb::gemm(c, cT, Op::NoTrans, kb, nc, mr, T(1), Vk, ldv, Cc, lda, T(0), W, kb);
+            // On a wide trailing block this GEMM's K (= mr rows) is long, so
+            // without chunking each workgroup lives for milliseconds and the
+            // next panel's short kernels (high-priority stream) find no free
+            // CU until it drains.  K chunks of kch rows, accumulated in W,
+            // bound the workgroup lifetime.
+            const int64_t kch = qr_kchunk();
+            if (mr > 0 && kch > 0 && mr > kch && nc >= 4 * kb) {
+                for (int64_t r0 = 0; r0 < mr; r0 += kch)
+                    lb::gemm(c, cT, Op::NoTrans, kb, nc, std::min(kch, mr - r0), T(1), Vk + r0, ldv, Cc + r0, lda,
+                             r0 ? T(1) : T(0), W, kb);
+            } else if (mr > 0) lb::gemm(c, cT, Op::NoTrans, kb, nc, mr, T(1), Vk, ldv, Cc, lda, T(0), W, kb);
             else lb::set(c, Uplo::General, kb, nc, T(0), T(0), W, kb);
             if (p > 1) g.col().allreduce(W, W, size_t(kb * nc), scalar_type<T>(), ReduceOp::Sum, c.loc(), c.stream);
             lb::gemm(c, cT, Op::NoTrans, kb, nc, kb, T(1), Tk, kb, W, kb, T(0), W2, kb);

@@ -10,6 +10,7 @@ import sys
 import pytest
 
 HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
 WORKER = os.path.join(HERE, "dist_worker.py")
 CASES = "gemm,herk,trsm,potrf,getrf,geqrf,norm,mixed"
 
@@ -56,3 +57,17 @@ def test_dist_device_shared_gpu(p, q):
     """Device target, 2 ranks on one GPU (host transport): covers the device
     code paths of the p x q drivers (panel gathers, row exchanges, U/L bcasts)."""
     run_workers(p, q, "d", env_extra={"LOCAL_RANK": "0"})
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,grid", [(2, "1x2"), (4, "2x2")])
+def test_rccl_multirank_one_gpu(nprocs, grid):
+    """The real RCCL transport with several ranks on one GPU: each rank gets
+    its own NCCL_HOSTID so RCCL treats them as separate hosts (socket
+    transport over loopback) instead of refusing a duplicate device.  The
+    tester's distributed residual checks validate the results."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), str(nprocs),
+                        "gemm,potrf,getrf_tntpiv,geqrf,gels,heev", "--type", "d", "--dim", "400", "--nb", "64",
+                        "--grid", grid, "--target", "d"], capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
+    assert "Duplicate GPU" not in r.stdout
