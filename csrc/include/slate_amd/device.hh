@@ -68,6 +68,10 @@ void  release_cache();
 /// Bytes held in use / cached.
 size_t bytes_in_use();
 size_t bytes_cached();
+/// Blocks handed out / parked in the cache; pinned host bytes handed out.
+size_t blocks_in_use();
+size_t blocks_cached();
+size_t host_bytes_in_use();
 
 void memcpy_async(void* dst, const void* src, size_t bytes, hipStream_t s);
 void memcpy2d_async(void* dst, size_t dpitch, const void* src, size_t spitch,

@@ -19,6 +19,7 @@
 #include "matgen.hh"
 #include "init.hh"
 #include "eig_host.hh"
+#include "debug.hh"
 
 #include <vector>
 

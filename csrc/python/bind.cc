@@ -359,6 +359,12 @@ PYBIND11_MODULE(_slate, m) {
     m.def("sync", &slate::sync, py::call_guard<py::gil_scoped_release>());
     m.def("release_cache", &device::release_cache);
     m.def("bytes_in_use", &device::bytes_in_use);
+    m.def("debug_on", &Debug::on);
+    m.def("debug_off", &Debug::off);
+    m.def("debug_enabled", &Debug::enabled);
+    m.def("debug_mem_report", &Debug::printNumFreeMemBlocks);
+    m.def("debug_device_leaks", &Debug::checkDeviceMemoryLeaks);
+    m.def("debug_host_leaks", &Debug::checkHostMemoryLeaks);
     m.def("version", &slate::version);
     // tridiagonal / bidiagonal host solvers (fp64): return numpy arrays
     using VD = std::vector<double>;

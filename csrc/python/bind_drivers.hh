@@ -264,6 +264,19 @@ void bind_drivers(py::module_& m, std::string const& s) {
         return py::make_tuple(TU, TV); });
     DEF("print", [](std::string label, BaseMatrix<T> const& A, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; return print_to_string(label.c_str(), A, op); });
+    // ---- Debug (debug.hh)
+    DEF("debug_print_tiles", [](BaseMatrix<T> const& A) { return Debug::printTiles(A); });
+    DEF("debug_check_tiles_lives", [](BaseMatrix<T> const& A) { return Debug::checkTilesLives(A); });
+    DEF("debug_check_tiles_layout", [](BaseMatrix<T> const& A) { return Debug::checkTilesLayout(A); });
+    DEF("debug_diff_lapack", [](py::array_t<T, py::array::f_style | py::array::forcecast> a,
+                                py::array_t<T, py::array::f_style | py::array::forcecast> b, int64_t mb, int64_t nb,
+                                double tol) {
+        slate_error_if_msg(a.ndim() != 2 || b.ndim() != 2 || a.shape(0) != b.shape(0) || a.shape(1) != b.shape(1),
+                           "debug_diff_lapack: shapes differ");
+        std::string map;
+        int64_t nd = Debug::diffLapackMatrices<T>(a.shape(0), a.shape(1), a.data(), std::max<int64_t>(1, a.shape(0)),
+                                                  b.data(), std::max<int64_t>(1, b.shape(0)), mb, nb, tol, &map);
+        return py::make_tuple(nd, map); });
     // ---- stage-level two-stage API on distributed matrices (eig_stages.cc)
     py::class_<BandReflectors<T>>(m, ("BandReflectors_" + s).c_str())
         .def("size", [](BandReflectors<T> const& V) { return V.Q.size(); });

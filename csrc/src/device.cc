@@ -21,6 +21,8 @@ struct State {
     std::multimap<size_t, void*> free_blocks;
     std::map<void*, size_t> live;
     size_t in_use = 0, cached = 0;
+    std::map<void*, size_t> host_live;   // pinned host blocks
+    size_t host_in_use = 0;
 };
 
 State& st() {
@@ -210,15 +212,41 @@ void release_cache() {
 
 size_t bytes_in_use() { return st().in_use; }
 size_t bytes_cached() { return st().cached; }
+size_t blocks_in_use() {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    return s.live.size();
+}
+size_t blocks_cached() {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    return s.free_blocks.size();
+}
+size_t host_bytes_in_use() { return st().host_in_use; }
 
 void* malloc_host(size_t bytes) {
     void* p = nullptr;
-    slate_hip_call(hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault));
+    bytes = std::max<size_t>(bytes, 1);
+    slate_hip_call(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    s.host_live[p] = bytes;
+    s.host_in_use += bytes;
     return p;
 }
 
 void free_host(void* ptr) {
-    if (ptr) (void)hipHostFree(ptr);
+    if (!ptr) return;
+    {
+        auto& s = st();
+        std::lock_guard<std::mutex> g(s.mtx);
+        auto it = s.host_live.find(ptr);
+        if (it != s.host_live.end()) {
+            s.host_in_use -= it->second;
+            s.host_live.erase(it);
+        }
+    }
+    (void)hipHostFree(ptr);
 }
 
 void memcpy_async(void* dst, const void* src, size_t bytes, hipStream_t s) {

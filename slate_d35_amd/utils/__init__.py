@@ -2,3 +2,4 @@
 test-matrix generation (reference matgen/)."""
 from .flops import *   # noqa: F401,F403
 from .matgen import *  # noqa: F401,F403
+from . import debug  # noqa: F401
