@@ -10,7 +10,12 @@
 //    4x4 MFMA tiles = 16 independent accumulator chains, so one wave per SIMD
 //    already issues back-to-back.
 //  * 256-thread workgroup (4 waves, 2x2) per 128x128 C tile, BK=16, LDS
-//    double buffer with register prefetch (one barrier per K-tile).
+//    double buffer with register prefetch (one barrier per K-tile).  fp64
+//    products with a K-contiguous operand use 8 waves of 64x32 instead
+//    (4 waves per SIMD at <= 128 VGPRs; see launch_gemm).
+//  * Interior-only instantiation when every tile is full (no bounds-checked
+//    path competing for registers); rotated K pipeline for fp64 (the last
+//    k-step's MFMAs issue after the barrier, behind the next LDS reads).
 //  * LDS image is [k][m] with row stride BM+16 elements: the MFMA operand
 //    read (lanes 0-15 consecutive m, lanes 16-31 next k) then lands the two
 //    16-lane halves on disjoint bank halves (ds_read_b64: bank=(a/4)%64).
@@ -140,23 +145,37 @@ struct TileLoader {
     static constexpr int elems(int LD) { return BK * LD + 32; }   // + max skew
     __device__ static inline int at(int LD, int x, int kr) { return kr * LD + lds_skew<T>(kr) + x; }
 
-    // store into LDS image row kk at kk*LD + lds_skew(kk), column x
+    // LDS image offsets of this thread's vectors (element units), computed
+    // once: row kk at kk*LD + lds_skew(kk), column x.  A K-contiguous vector
+    // spans VEC rows, all with the same skew (kk is a multiple of VEC), so
+    // its elements sit at soff + e*LD.  Keeping one register per vector
+    // (instead of re-deriving x, kk and the skew each K-tile) keeps the
+    // 8-wave kernel within its 128-VGPR budget.
+    int soff[NVT];
     template <int LD>
-    __device__ inline void store(T* L) const {
+    __device__ inline void init_store() {
         const int tid = threadIdx.x;
         #pragma unroll
         for (int i = 0; i < NVT; ++i) {
             int x, kk;
             coords(tid + NTHR * i, x, kk);
+            soff[i] = kk * LD + lds_skew<T>(kk) + x;
+        }
+    }
+
+    template <int LD>
+    __device__ inline void store(T* L) const {
+        #pragma unroll
+        for (int i = 0; i < NVT; ++i) {
             if constexpr (KCONTIG) {
                 #pragma unroll
                 for (int e = 0; e < VEC; ++e)
-                    L[(kk + e) * LD + lds_skew<T>(kk + e) + x] = r[i][e];
+                    L[soff[i] + e * LD] = r[i][e];
             } else {
                 // the skew is a multiple of VEC: the vector stays aligned
                 #pragma unroll
                 for (int e = 0; e < VEC; ++e)
-                    L[kk * LD + lds_skew<T>(kk) + x + e] = r[i][e];
+                    L[soff[i] + e] = r[i][e];
             }
         }
     }
@@ -225,9 +244,11 @@ __device__ inline void gemm_tile_coords(int64_t m, int64_t n, int BM, int BN, in
 // (4 waves, 2 workgroups per CU) or 256 x 128 (8 waves, 1 workgroup per CU:
 // 25% less operand traffic per flop for large C).
 template <typename T, int BM, int BN, int BK, bool A_KC, bool B_KC, char TRI, int WTN_ = 64, int WTM_ = 64,
-          bool ROT = false>
+          bool ROT = false, bool IONLY = false>
 __global__ __launch_bounds__(64 * (BM / WTM_) * (BN / WTN_),
-    (2 * BK * (BM + BN + 32) * sizeof(T) > 81920) ? 1 : 512 / (64 * (BM / WTM_) * (BN / WTN_)))
+    (2 * BK * (BM + BN + 32) * sizeof(T) > 81920) ? 1
+        : (BM == 128 && BN == 128 && 64 * (BM / WTM_) * (BN / WTN_) == 512) ? 4
+        : 512 / (64 * (BM / WTM_) * (BN / WTN_)))
 void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
                       const T* __restrict__ A, int64_t lda, int64_t sA,
                       const T* __restrict__ B, int64_t ldb, int64_t sB,
@@ -290,6 +311,8 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
 
     LA la;
     LB lb;
+    la.template init_store<LDA_S>();
+    lb.template init_store<LDB_S>();
     const bool mfull = (m0 + BM <= m), nfull = (n0 + BN <= n);
 
     const int KT = (int)((k + BK - 1) / BK);
@@ -397,7 +420,8 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     }
     }
     };
-    if (GEMM_SPLIT && aligned && mfull && nfull && k % BK == 0) kloop(std::true_type{});
+    if constexpr (IONLY) kloop(std::true_type{});
+    else if (GEMM_SPLIT && aligned && mfull && nfull && k % BK == 0) kloop(std::true_type{});
     else kloop(std::false_type{});
 
     gemm_epilogue<T, TM, TN, TRI>(acc, m, n, alpha, beta, C, ldc, m0 + wm * WTM, n0 + wn * WTN, lane);
@@ -415,8 +439,15 @@ static void launch_tile(int64_t m, int64_t n, int64_t k, T alpha,
     int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
     int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
     dim3 grid((unsigned)nblk, (unsigned)batch);
-    hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, ROT>), grid, dim3(NTHR), 0, stream,
-                       m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+    // every tile interior (the common case for nb-multiple trailing updates):
+    // a kernel without the bounds-checked path, whose registers then go to
+    // the hot loop alone
+    if (aligned && m % BM == 0 && n % BN == 0 && k % BK == 0 && k > 0)
+        hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, ROT, true>), grid, dim3(NTHR),
+                           0, stream, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+    else
+        hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, ROT, false>), grid, dim3(NTHR),
+                           0, stream, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
 }
 
 // fp32 only: 256 x 128 tiles (8 waves, 1 workgroup per CU) cut operand
@@ -447,8 +478,20 @@ static void launch_gemm(int64_t m, int64_t n, int64_t k, T alpha,
             return;
         }
     }
-    launch_tile<T, A_KC, B_KC, TRI, 128, 128>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
+    if constexpr (TRI == 0 && sizeof(T) == 8 && (A_KC || B_KC)) {
+        // fp64 with a K-contiguous operand: 8 waves of 64 x 32 per 128 x 128
+        // tile (4 waves per SIMD at <= 128 VGPRs, so one wave's barrier or
+        // LDS wait is covered by three others).  Measured on 16384^2 x 16384
+        // against the 4-wave 64 x 64 tile: NN 68.5 vs 66.9, TN 69.5 vs 67.0
+        // TFLOP/s (rotated pipeline on TN only: it spills NN); NT keeps the
+        // 4-wave rotated tile (70.4).
+        constexpr bool ROT8 = A_KC && B_KC;
+        launch_tile<T, A_KC, B_KC, TRI, 128, 128, 16, 32, 64, ROT8>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C,
+                                                                    ldc, sC, batch, aligned, stream);
+    } else {
+        launch_tile<T, A_KC, B_KC, TRI, 128, 128>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,
                                                   batch, aligned, stream);
+    }
 }
 
 template <typename T>

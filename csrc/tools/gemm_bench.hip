@@ -92,6 +92,7 @@ void timeit(char ta, char tb, int64_t n, int64_t k, int reps, int64_t pad = 0) {
     else { tofloat<<<(ne + 255) / 256, 256>>>(tmp, (float*)A, ne); tofloat<<<(ne + 255) / 256, 256>>>(tmp, (float*)B, ne); }
     CHECK(hipMemset(C, 0, (n + pad) * n * sizeof(T)));
     int64_t lda = (ta == 'N' ? n : k) + pad, ldb = (tb == 'N' ? k : n) + pad;
+    if (getenv("GEMM_LD0")) { lda = 0; ldb = 0; }   // lab: operands always cache-resident
     const int64_t ldc = n + pad;
     gemm_real<T>(ta, tb, n, n, k, T(1), A, lda, 0, B, ldb, 0, T(1), C, ldc, 0, 1, 0);
     CHECK(hipDeviceSynchronize());
