@@ -344,6 +344,15 @@ __device__ inline void qr_block_reflector(int nparts, const real_t<T>* psum, con
     beta = sh[0]; tau = sh[1]; scal = sh[2];
 }
 
+// Each (row block, column group) workgroup handles QR_CPB trailing columns:
+// the reflector (a reduction over the norm partials, done redundantly by every
+// workgroup) and the v column are then read once per QR_CPB columns instead
+// of once per column.  Still thousands of short workgroups per launch, which
+// is what lets the panel slot into the CUs a concurrent trailing GEMM frees
+// (one workgroup per 256 rows looping over all columns measured 20% slower
+// at n = 65536).
+constexpr int QR_CPB = 4;
+
 template <typename T>
 __global__ void qr_dots2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                  int nparts_norm, const real_t<T>* psum, const T* alpha_in,
@@ -351,9 +360,9 @@ __global__ void qr_dots2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, 
     using R = real_t<T>;
     T beta, tau, scal;
     qr_block_reflector(nparts_norm, psum, alpha_in, beta, tau, scal);
-    const int j = blockIdx.y;
+    const int y = blockIdx.y;
     const int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
-    if (j == 0) {
+    if (y == 0) {
         if (blockIdx.x == 0 && threadIdx.x == 0) { tau_out[c] = tau; scal_buf[c] = scal; A[r + c * lda] = beta; }
         if (scale_prev && i < m) {
             T sp = scal_buf[c - 1];
@@ -361,22 +370,28 @@ __global__ void qr_dots2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, 
         }
         return;
     }
-    const int64_t cc = c + j;
-    T prod = zero<T>();
-    if (i < m) {
-        T v = (i == r) ? one<T>() : A[i + c * lda] * scal;
-        prod = conj(v) * A[i + cc * lda];
+    const int j0 = 1 + (y - 1) * QR_CPB;                 // first column offset of this group
+    const int ncol = (int)min<int64_t>(QR_CPB, cend - c - j0);
+    T v = zero<T>();
+    if (i < m) v = (i == r) ? one<T>() : A[i + c * lda] * scal;
+    __shared__ R wr[QR_CPB][PT / 64], wi[QR_CPB][PT / 64];
+    #pragma unroll
+    for (int t = 0; t < QR_CPB; ++t) {
+        if (t >= ncol) break;
+        T prod = (i < m) ? conj(v) * A[i + (c + j0 + t) * lda] : zero<T>();
+        R pr = wave_sum(real(prod));
+        R pim = 0;
+        if constexpr (is_cplx<T>::value) pim = wave_sum(imag(prod));
+        if ((threadIdx.x & 63) == 0) { wr[t][threadIdx.x >> 6] = pr; wi[t][threadIdx.x >> 6] = pim; }
     }
-    R pr = wave_sum(real(prod)), pim = wave_sum(imag(prod));
-    __shared__ R wr[PT / 64], wi[PT / 64];
-    if ((threadIdx.x & 63) == 0) { wr[threadIdx.x >> 6] = pr; wi[threadIdx.x >> 6] = pim; }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        R a = 0, b = 0;
-        for (int w = 0; w < PT / 64; ++w) { a += wr[w]; b += wi[w]; }
-        T t;
-        if constexpr (is_cplx<T>::value) t = T(a, b); else t = a;
-        pdots[(int64_t)blockIdx.x * 64 + (j - 1)] = t;
+    if (threadIdx.x < ncol) {
+        const int t = threadIdx.x;
+        R a = 0, bi = 0;
+        for (int w = 0; w < PT / 64; ++w) { a += wr[t][w]; bi += wi[t][w]; }
+        T tt;
+        if constexpr (is_cplx<T>::value) tt = T(a, bi); else tt = a;
+        pdots[(int64_t)blockIdx.x * 64 + (j0 - 1 + t)] = tt;
     }
 }
 
@@ -385,38 +400,46 @@ __global__ void qr_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend
                                    int nparts, const T* pdots, const T* tau_buf, const T* scal_buf,
                                    real_t<T>* psum_next, T* alpha_next) {
     using R = real_t<T>;
-    const int j = blockIdx.y + 1;
-    const int64_t cc = c + j;
-    __shared__ T zsh;
-    if (threadIdx.x < 64) {
-        // wave 0 reduces this column's dot partials (lane-strided, DPP sum)
-        R tr = 0, ti = 0;
-        for (int b = threadIdx.x; b < nparts; b += 64) {
-            T t = pdots[(int64_t)b * 64 + (j - 1)];
-            tr += real(t); ti += imag(t);
-        }
-        tr = wave_sum(tr);
-        if constexpr (is_cplx<T>::value) ti = wave_sum(ti);
-        if (threadIdx.x == 0) {
-            T t;
-            if constexpr (is_cplx<T>::value) t = T(tr, ti); else t = tr;
-            zsh = conj(tau_buf[c]) * t;
+    const int j0 = 1 + blockIdx.y * QR_CPB;
+    const int ncol = (int)min<int64_t>(QR_CPB, cend - c - j0);
+    __shared__ T zsh[QR_CPB];
+    {
+        // wave t reduces the dot partials of column j0 + t (lane-strided)
+        const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+        if (w < ncol) {
+            R tr = 0, ti = 0;
+            for (int b = lane; b < nparts; b += 64) {
+                T t = pdots[(int64_t)b * 64 + (j0 - 1 + w)];
+                tr += real(t); ti += imag(t);
+            }
+            tr = wave_sum(tr);
+            if constexpr (is_cplx<T>::value) ti = wave_sum(ti);
+            if (lane == 0) {
+                T t;
+                if constexpr (is_cplx<T>::value) t = T(tr, ti); else t = tr;
+                zsh[w] = conj(tau_buf[c]) * t;
+            }
         }
     }
     __syncthreads();
-    const T z = zsh, scal = scal_buf[c];
+    const T scal = scal_buf[c];
     const int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
     R s = 0;
     if (i < m) {
-        T v = (i == r) ? one<T>() : A[i + c * lda] * scal;
-        T a = A[i + cc * lda] - v * z;
-        A[i + cc * lda] = a;
-        if (j == 1) {
-            if (i > r + 1) s = real(a) * real(a) + imag(a) * imag(a);
-            if (i == r + 1) *alpha_next = a;
+        const T v = (i == r) ? one<T>() : A[i + c * lda] * scal;
+        #pragma unroll
+        for (int t = 0; t < QR_CPB; ++t) {
+            if (t >= ncol) break;
+            const int64_t cc = c + j0 + t;
+            T a = A[i + cc * lda] - v * zsh[t];
+            A[i + cc * lda] = a;
+            if (j0 + t == 1) {
+                if (i > r + 1) s = real(a) * real(a) + imag(a) * imag(a);
+                if (i == r + 1) *alpha_next = a;
+            }
         }
     }
-    if (j == 1) {
+    if (blockIdx.y == 0) {
         s = wave_sum(s);
         __shared__ R sh[PT / 64];
         if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = s;
@@ -566,7 +589,8 @@ void qr_dots2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
     if (rows <= 0) return;
     int g = (int)((rows + PT - 1) / PT);
     int64_t nc = cend - c - 1;
-    hipLaunchKernelGGL(qr_dots2d_kernel<T>, dim3(g, (unsigned)(1 + nc)), dim3(PT), 0, s, m, r, c, cend, A, lda,
+    hipLaunchKernelGGL(qr_dots2d_kernel<T>, dim3(g, (unsigned)(1 + (nc + QR_CPB - 1) / QR_CPB)), dim3(PT), 0, s, m, r,
+                       c, cend, A, lda,
                        nparts_norm, psum, alpha_in, tau_out, scal_buf, pdots, scale_prev);
 }
 template <typename T>
@@ -576,7 +600,8 @@ void qr_update2d(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t ld
     int64_t nc = cend - c - 1;
     if (rows <= 0 || nc <= 0) return;
     int g = (int)((rows + PT - 1) / PT);
-    hipLaunchKernelGGL(qr_update2d_kernel<T>, dim3(g, (unsigned)nc), dim3(PT), 0, s, m, r, c, cend, A, lda,
+    hipLaunchKernelGGL(qr_update2d_kernel<T>, dim3(g, (unsigned)((nc + QR_CPB - 1) / QR_CPB)), dim3(PT), 0, s, m, r,
+                       c, cend, A, lda,
                        nparts, pdots, tau_buf, scal_buf, psum_next, alpha_next);
 }
 template <typename T>

@@ -104,8 +104,11 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
         // split-K for small outputs with a long K (e.g. V^H C in QR panels):
         // otherwise only a handful of 128x128 tiles would carry all the work
         const int64_t tiles = ceildiv(m, 128) * ceildiv(n, 128);
-        if (uplo == 'G' && tiles < 128 && k >= 4096) {
-            int64_t splits = std::min<int64_t>(ceildiv(k, 256), std::max<int64_t>(2, 1024 / tiles));
+        // (a handful of tiles with K >= 1024: the QR panel's V^H V and
+        // V^H A products at the tail, where one workgroup would otherwise walk
+        // all of K alone)
+        if (uplo == 'G' && tiles < 128 && k >= 1024) {
+            int64_t splits = std::min<int64_t>(ceildiv(k, 128), std::max<int64_t>(2, 1024 / tiles));
             int64_t kc = roundup(ceildiv(k, splits), 16);
             splits = ceildiv(k, kc);
             int64_t full = k / kc;                 // chunks of exactly kc
