@@ -15,7 +15,7 @@ PY_EXT    := $(shell $(PYTHON) -c "import sysconfig;print(sysconfig.get_config_v
 
 INC       := -Icsrc/include -Icsrc/kernels -I$(ROCM)/include
 DEFS      := -D__HIP_PLATFORM_AMD__ -DSLATE_AMD_VERSION=\"2026.10.0\"
-CXXFLAGS  := -std=c++17 -O3 -fPIC -fopenmp -march=x86-64-v3 -Wall -Wno-unused-function -Wno-sign-compare $(INC) $(DEFS)
+CXXFLAGS  := -std=c++17 -O3 -fPIC -fopenmp -march=x86-64-v3 -fcx-fortran-rules -Wall -Wno-unused-function -Wno-sign-compare $(INC) $(DEFS)
 HIPFLAGS  := -std=c++17 -O3 -fPIC --offload-arch=$(ARCH) -Wno-unused-result $(INC) $(DEFS)
 LDLIBS    := -L$(ROCM)/lib -Wl,-rpath,$(ROCM)/lib -lamdhip64 -lrccl -fopenmp
 

@@ -93,13 +93,21 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
             s *= cj(tau);
             if (s != T(0)) for (int64_t i = 0; i < L; ++i) a(s0 + i, c) -= v[i] * s;
         }
-        // right: rows in window (skip k), columns J
-        for (int64_t r = w0; r <= w1; ++r) {
-            if (r == k) continue;
-            T s = T(0);
-            for (int64_t i = 0; i < L; ++i) s += a(r, s0 + i) * v[i];
-            s *= tau;
-            if (s != T(0)) for (int64_t i = 0; i < L; ++i) a(r, s0 + i) -= s * cj(v[i]);
+        // right: rows in window (skip k), columns J; column-oriented so every
+        // inner loop runs down a contiguous column
+        const int64_t nr = w1 - w0 + 1;
+        std::fill(w.begin(), w.begin() + nr, T(0));
+        for (int64_t i = 0; i < L; ++i) {
+            const T* col = &a(w0, s0 + i);
+            const T vi = v[i];
+            for (int64_t r = 0; r < nr; ++r) w[r] += col[r] * vi;
+        }
+        for (int64_t i = 0; i < L; ++i) {
+            T* col = &a(w0, s0 + i);
+            const T f = tau * cj(v[i]);
+            const T keep = col[k - w0];  // row k is excluded
+            for (int64_t r = 0; r < nr; ++r) col[r] -= w[r] * f;
+            col[k - w0] = keep;
         }
     };
     for (int64_t j = 0; j + 2 < n && b > 1; ++j) {
@@ -148,16 +156,26 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
     using R = real_type<T>;
     auto a = [&](int64_t i, int64_t j) -> T& { return A[i + j * lda]; };
     const int64_t b = std::max<int64_t>(kd, 1);
-    std::vector<T> v(b + 1);
+    std::vector<T> v(b + 1), w(size_t(std::max<int64_t>(m, 1)));
     auto right = [&](int64_t r, int64_t c0, int64_t L, T tau) {
-        // rows in window (skip r): A[row, J] = A[row, J] H
+        // rows in window (skip r): A[row, J] = A[row, J] H, column-oriented
+        // (contiguous inner loops; the row-wise form strides by lda)
         int64_t w0 = std::max<int64_t>(0, c0 - 2 * b - 1), w1 = std::min<int64_t>(m - 1, c0 + L - 1 + 2 * b);
-        for (int64_t i = w0; i <= w1; ++i) {
-            if (i == r) continue;
-            T s = T(0);
-            for (int64_t t = 0; t < L; ++t) s += a(i, c0 + t) * v[t];
-            s *= tau;
-            if (s != T(0)) for (int64_t t = 0; t < L; ++t) a(i, c0 + t) -= s * cj(v[t]);
+        const int64_t nr = w1 - w0 + 1;
+        if (nr <= 0) return;
+        std::fill(w.begin(), w.begin() + nr, T(0));
+        for (int64_t t = 0; t < L; ++t) {
+            const T* col = &a(w0, c0 + t);
+            const T vt = v[t];
+            for (int64_t i = 0; i < nr; ++i) w[i] += col[i] * vt;
+        }
+        const bool skip = (r >= w0 && r <= w1);
+        for (int64_t t = 0; t < L; ++t) {
+            T* col = &a(w0, c0 + t);
+            const T f = tau * cj(v[t]);
+            const T keep = skip ? col[r - w0] : T(0);  // row r is excluded
+            for (int64_t i = 0; i < nr; ++i) col[i] -= w[i] * f;
+            if (skip) col[r - w0] = keep;
         }
     };
     auto left = [&](int64_t c, int64_t r0, int64_t L, T tau) {
@@ -523,14 +541,20 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
             y[r] = yb * c - ya * s;
         }
     };
-    auto rowrot = [&](T* M, int64_t ld, int64_t cols, int64_t a, int64_t b, R c, R s) {
-        if (!M) return;
-        for (int64_t jj = 0; jj < cols; ++jj) {
-            T xa = M[a + jj * ld], xb = M[b + jj * ld];
-            M[a + jj * ld] = xa * c + xb * s;
-            M[b + jj * ld] = xb * c - xa * s;
-        }
-    };
+    // VT is rotated by rows; rows of a column-major VT are ld-strided, so work
+    // on V^T-transposed storage (row j of VT = contiguous column j of Vt) and
+    // transpose back at the end.  The rotations of one implicit-shift sweep are
+    // recorded and applied afterwards by apply_rots (row blocks in parallel).
+    std::vector<T> Vt;
+    if (VT) {
+        Vt.resize(size_t(vcols) * n);
+        for (int64_t jj = 0; jj < vcols; ++jj)
+            for (int64_t j = 0; j < n; ++j) Vt[jj + j * vcols] = VT[j + jj * ldvt];
+    }
+    T* V = VT ? Vt.data() : nullptr;
+    // Rot convention of apply_rots: [x y] <- [c x - s y, s x + c y]; the sweep
+    // below rotates [x y] <- [c x + s y, c y - s x], i.e. (c, -s).
+    std::vector<Rot<R>> ru, rv;
     for (int64_t k = n - 1; k >= 0; --k) {
         for (int its = 0; its < 75; ++its) {
             bool flag = true;
@@ -559,7 +583,7 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
             if (l == k) {
                 if (z < R(0)) {
                     w[k] = -z;
-                    if (VT) for (int64_t jj = 0; jj < vcols; ++jj) VT[k + jj * ldvt] = -VT[k + jj * ldvt];
+                    if (V) for (int64_t jj = 0; jj < vcols; ++jj) V[jj + k * vcols] = -V[jj + k * vcols];
                 }
                 break;
             }
@@ -571,6 +595,7 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
             g = std::hypot(f, R(1));
             f = ((x - z) * (x + z) + h * ((y / (f + std::copysign(g, f))) - h)) / x;
             R c = 1, s = 1;
+            ru.clear(); rv.clear();
             for (int64_t j = l; j <= nm; ++j) {
                 int64_t i = j + 1;
                 g = rv1[i];
@@ -585,7 +610,7 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
                 g = g * c - x * s;
                 h = y * s;
                 y *= c;
-                rowrot(VT, ldvt, vcols, j, i, c, s);
+                rv.push_back(Rot<R>{j, c, -s});
                 z = std::hypot(f, h);
                 w[j] = z;
                 if (z != R(0)) {
@@ -595,8 +620,10 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
                 }
                 f = c * g + s * y;
                 x = c * y - s * g;
-                colrot(U, ldu, urows, j, i, c, s);
+                ru.push_back(Rot<R>{j, c, -s});
             }
+            apply_rots(rv, V, vcols, vcols);
+            apply_rots(ru, U, ldu, urows);
             rv1[l] = 0;
             rv1[k] = f;
             w[k] = x;
@@ -609,8 +636,12 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
         if (kk != i) {
             std::swap(w[i], w[kk]);
             if (U) for (int64_t r = 0; r < urows; ++r) std::swap(U[r + i * ldu], U[r + kk * ldu]);
-            if (VT) for (int64_t jj = 0; jj < vcols; ++jj) std::swap(VT[i + jj * ldvt], VT[kk + jj * ldvt]);
+            if (V) for (int64_t jj = 0; jj < vcols; ++jj) std::swap(V[jj + i * vcols], V[jj + kk * vcols]);
         }
+    }
+    if (VT) {
+        for (int64_t jj = 0; jj < vcols; ++jj)
+            for (int64_t j = 0; j < n; ++j) VT[j + jj * ldvt] = Vt[jj + j * vcols];
     }
     return fail;
 }
