@@ -8,6 +8,10 @@
 #include <complex>
 #include <limits>
 #include <numeric>
+#include <atomic>
+#include <memory>
+#include <thread>
+#include <omp.h>
 
 namespace slate {
 namespace host {
@@ -81,10 +85,14 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
     using R = real_type<T>;
     auto a = [&](int64_t i, int64_t j) -> T& { return A[i + j * lda]; };
     const int64_t b = std::max<int64_t>(kd, 1);
-    std::vector<T> v(b + 1), w(n);
-    auto two_sided = [&](int64_t k, int64_t s0, int64_t L, T tau) {
-        // H^H A H on the window [w0, w1] (column/row k set explicitly by the caller)
-        int64_t w0 = std::max<int64_t>(0, k - 2 * b), w1 = std::min<int64_t>(n - 1, s0 + L - 1 + 2 * b);
+    // per-thread scratch: v (reflector), w (window-length dot products)
+    auto two_sided = [&](int64_t k, int64_t s0, int64_t L, T tau, const T* v, T* w) {
+        // H^H A H on the window [w0, w1] (column/row k set explicitly by the
+        // caller).  Rows J = [s0, s0+L) hold nonzeros in columns [k, s0+L-1+b]:
+        // k is the bulge column (earlier columns are already tridiagonal) and
+        // the band reaches b past the diagonal; by symmetry the same rows are
+        // touched by the right update.
+        int64_t w0 = k, w1 = std::min<int64_t>(n - 1, s0 + L - 1 + b);
         // left: rows J, columns in window (skip k)
         for (int64_t c = w0; c <= w1; ++c) {
             if (c == k) continue;
@@ -96,7 +104,7 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
         // right: rows in window (skip k), columns J; column-oriented so every
         // inner loop runs down a contiguous column
         const int64_t nr = w1 - w0 + 1;
-        std::fill(w.begin(), w.begin() + nr, T(0));
+        std::fill(w, w + nr, T(0));
         for (int64_t i = 0; i < L; ++i) {
             const T* col = &a(w0, s0 + i);
             const T vi = v[i];
@@ -110,28 +118,60 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
             col[k - w0] = keep;
         }
     };
-    for (int64_t j = 0; j + 2 < n && b > 1; ++j) {
+    // Sweeps are pipelined over threads (the reference's hb2st.cc runs its
+    // bulge-chasing sweeps as OpenMP tasks the same way).  Step t of sweep j
+    // works on the window [s0 - b, s0 + 2b) with s0 = j + 1 + t b; it may run
+    // once sweep j-1 has finished its steps 0..t+3 (the last ones whose windows
+    // reach into it), and sweep j-1's later steps cannot reach back into it.
+    // Reflectors are collected per sweep and concatenated in sweep order:
+    // reflectors of different sweeps that ran out of order act on disjoint rows
+    // and commute.
+    const int64_t nsw = (b > 1 && n > 2) ? n - 2 : 0;
+    constexpr int64_t kLag = 4;
+    constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
+    std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
+    for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
+    std::vector<Reflectors<T>> Qs(nsw);
+    auto sweep = [&](int64_t j, T* v, T* w) {
         int64_t k = j, s0 = j + 1, s1 = std::min(j + b, n - 1);
-        while (true) {
+        for (int64_t t = 0;; ++t) {
+            if (j > 0) {
+                while (prog[j - 1].load(std::memory_order_acquire) < t + kLag) std::this_thread::yield();
+            }
             int64_t L = s1 - s0 + 1;
             if (L < 2) break;
             T alpha = a(s0, k);
             for (int64_t i = 1; i < L; ++i) v[i] = a(s0 + i, k);
             T tau;
-            larfg(L, alpha, v.data() + 1, 1, tau);
+            larfg(L, alpha, v + 1, 1, tau);
             v[0] = T(1);
             a(s0, k) = alpha;
             a(k, s0) = cj(alpha);
             for (int64_t i = 1; i < L; ++i) { a(s0 + i, k) = T(0); a(k, s0 + i) = T(0); }
             if (tau != T(0)) {
-                two_sided(k, s0, L, tau);
-                Q.push(s0, L, tau, v.data());
+                two_sided(k, s0, L, tau, v, w);
+                Qs[j].push(s0, L, tau, v);
             }
+            prog[j].store(t + 1, std::memory_order_release);
             // next bulge: column s0 below its band
             int64_t ns0 = s0 + b, ns1 = std::min(s1 + b, n - 1);
             if (ns0 >= n - 1 || ns1 <= ns0) break;
             k = s0; s0 = ns0; s1 = ns1;
         }
+        prog[j].store(kDone, std::memory_order_release);
+    };
+    const bool par = nsw >= 64 && n >= 8 * b;
+    #pragma omp parallel if (par)
+    {
+        std::vector<T> v(b + 1), w(n);
+        const int nth = par ? omp_get_num_threads() : 1, tid = par ? omp_get_thread_num() : 0;
+        // round-robin: sweep j-1 is always owned by another running thread (or
+        // finished earlier by this one), so every wait terminates
+        for (int64_t j = tid; j < nsw; j += nth) sweep(j, v.data(), w.data());
+    }
+    for (auto& q : Qs) {
+        for (size_t r = 0; r < q.size(); ++r) Q.push(q.off[r], q.len[r], q.tau[r], q.v.data() + q.voff[r]);
+        q = Reflectors<T>();
     }
     d.assign(n, R(0));
     e.assign(std::max<int64_t>(n - 1, 0), R(0));
