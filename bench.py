@@ -43,7 +43,7 @@ def parse():
     ap.add_argument("--steps", type=int, default=2)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--dim", "--n", dest="n", type=int, default=65536)
-    ap.add_argument("--nb", type=int, default=512)
+    ap.add_argument("--nb", type=int, default=0, help="tile size for every routine (default: per-routine table)")
     ap.add_argument("--nb-per", default="", help="per-routine nb overrides, e.g. dgeqrf=256,dgetrf=512")
     ap.add_argument("--routines", default=",".join(ALL))
     ap.add_argument("--p", type=int, default=0)
@@ -66,7 +66,17 @@ def main():
     p, q = (a.p, a.q) if a.p and a.q else s.choose_grid(world)
     grid = s.init_grid(p, q)
     n = a.n
-    nb_per = {k: int(v) for k, v in (kv.split("=") for kv in a.nb_per.split(",") if kv)}
+    # Default tiles: 512 everywhere, except on one GPU where dgetrf / dpotrf
+    # run 2-4% faster at nb = 1024 (profiles/nb_sweep_r1_n65536_1gpu.txt:
+    # getrf 50.3 -> 52.3, potrf 57.8 -> 58.6 TFLOP/s); dgeqrf stays at 512
+    # (384: 50.5, 512: 51.9).  Multi-GPU grids keep 512 so the 2-D cyclic
+    # distribution has enough block columns per process.
+    default_nb = {"dgetrf": 1024, "dpotrf": 1024} if world == 1 else {}
+    if a.nb:
+        default_nb = {}
+    a.nb = a.nb or 512
+    nb_per = dict(default_nb)
+    nb_per.update({k: int(v) for k, v in (kv.split("=") for kv in a.nb_per.split(",") if kv)})
     opts = dict(target=target, lookahead=a.lookahead)
 
     def barrier_sync():

@@ -196,14 +196,14 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
     using R = real_type<T>;
     auto a = [&](int64_t i, int64_t j) -> T& { return A[i + j * lda]; };
     const int64_t b = std::max<int64_t>(kd, 1);
-    std::vector<T> v(b + 1), w(size_t(std::max<int64_t>(m, 1)));
-    auto right = [&](int64_t r, int64_t c0, int64_t L, T tau) {
+    // v (reflector) and w (window dot products) are per-thread scratch
+    auto right = [&](int64_t r, int64_t c0, int64_t L, T tau, const T* v, T* w) {
         // rows in window (skip r): A[row, J] = A[row, J] H, column-oriented
         // (contiguous inner loops; the row-wise form strides by lda)
         int64_t w0 = std::max<int64_t>(0, c0 - 2 * b - 1), w1 = std::min<int64_t>(m - 1, c0 + L - 1 + 2 * b);
         const int64_t nr = w1 - w0 + 1;
         if (nr <= 0) return;
-        std::fill(w.begin(), w.begin() + nr, T(0));
+        std::fill(w, w + nr, T(0));
         for (int64_t t = 0; t < L; ++t) {
             const T* col = &a(w0, c0 + t);
             const T vt = v[t];
@@ -218,7 +218,7 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
             if (skip) col[r - w0] = keep;
         }
     };
-    auto left = [&](int64_t c, int64_t r0, int64_t L, T tau) {
+    auto left = [&](int64_t c, int64_t r0, int64_t L, T tau, const T* v) {
         int64_t w0 = std::max<int64_t>(0, r0 - 2 * b - 1), w1 = std::min<int64_t>(n - 1, r0 + L - 1 + 2 * b);
         for (int64_t jj = w0; jj <= w1; ++jj) {
             if (jj == c) continue;
@@ -228,20 +228,33 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
             if (s != T(0)) for (int64_t t = 0; t < L; ++t) a(r0 + t, jj) -= v[t] * s;
         }
     };
-    for (int64_t j = 0; j + 1 < n; ++j) {
+    // Sweeps pipelined over threads as in hb2st: step t of sweep j touches
+    // rows/columns [c0 - 2b - 1, c0 + 3b) with c0 = j + 1 + t b, so it may run
+    // once sweep j-1 has finished its steps 0..t+5; reflectors are kept per
+    // sweep and concatenated in sweep order (out-of-order ones commute).
+    const int64_t nsw = n > 1 ? n - 1 : 0;
+    constexpr int64_t kLag = 6;
+    constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
+    std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
+    for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
+    std::vector<Reflectors<T>> QUs(nsw), QVs(nsw);
+    auto sweep = [&](int64_t j, T* v, T* w) {
         int64_t r = j, c0 = j + 1, c1 = std::min(j + b, n - 1);
-        while (true) {
+        for (int64_t st = 0;; ++st) {
+            if (j > 0) {
+                while (prog[j - 1].load(std::memory_order_acquire) < st + kLag) std::this_thread::yield();
+            }
             // right reflector: row r, columns [c0, c1]
             int64_t L = c1 - c0 + 1;
             if (L >= 2) {
                 T alpha = cj(a(r, c0));
                 for (int64_t t = 1; t < L; ++t) v[t] = cj(a(r, c0 + t));
                 T tau;
-                larfg(L, alpha, v.data() + 1, 1, tau);
+                larfg(L, alpha, v + 1, 1, tau);
                 v[0] = T(1);
                 a(r, c0) = cj(alpha);
                 for (int64_t t = 1; t < L; ++t) a(r, c0 + t) = T(0);
-                if (tau != T(0)) { right(r, c0, L, tau); QV.push(c0, L, tau, v.data()); }
+                if (tau != T(0)) { right(r, c0, L, tau, v, w); QVs[j].push(c0, L, tau, v); }
             }
             // left reflector: column c0, rows [c0, min(c1, m-1)]
             int64_t r1 = std::min(c1, m - 1);
@@ -250,17 +263,34 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
                 T alpha = a(c0, c0);
                 for (int64_t t = 1; t < Ll; ++t) v[t] = a(c0 + t, c0);
                 T tau;
-                larfg(Ll, alpha, v.data() + 1, 1, tau);
+                larfg(Ll, alpha, v + 1, 1, tau);
                 v[0] = T(1);
                 a(c0, c0) = alpha;
                 for (int64_t t = 1; t < Ll; ++t) a(c0 + t, c0) = T(0);
-                if (tau != T(0)) { left(c0, c0, Ll, tau); QU.push(c0, Ll, tau, v.data()); }
+                if (tau != T(0)) { left(c0, c0, Ll, tau, v); QUs[j].push(c0, Ll, tau, v); }
             }
+            prog[j].store(st + 1, std::memory_order_release);
             // next: row c0 beyond its band, columns [c0 + b, c1 + b]
             int64_t nc0 = c0 + b, nc1 = std::min(c1 + b, n - 1);
             if (nc0 >= n - 1 || nc1 <= nc0) break;
             r = c0; c0 = nc0; c1 = nc1;
         }
+        prog[j].store(kDone, std::memory_order_release);
+    };
+    const bool par = nsw >= 64 && n >= 8 * b;
+    #pragma omp parallel if (par)
+    {
+        std::vector<T> v(b + 1), w(size_t(std::max<int64_t>(m, 1)));
+        const int nth = par ? omp_get_num_threads() : 1, tid = par ? omp_get_thread_num() : 0;
+        for (int64_t j = tid; j < nsw; j += nth) sweep(j, v.data(), w.data());
+    }
+    for (int64_t j = 0; j < nsw; ++j) {
+        for (size_t q = 0; q < QVs[j].size(); ++q)
+            QV.push(QVs[j].off[q], QVs[j].len[q], QVs[j].tau[q], QVs[j].v.data() + QVs[j].voff[q]);
+        for (size_t q = 0; q < QUs[j].size(); ++q)
+            QU.push(QUs[j].off[q], QUs[j].len[q], QUs[j].tau[q], QUs[j].v.data() + QUs[j].voff[q]);
+        QVs[j] = Reflectors<T>();
+        QUs[j] = Reflectors<T>();
     }
     d.assign(n, R(0));
     e.assign(std::max<int64_t>(n - 1, 0), R(0));
