@@ -71,7 +71,8 @@ def main():
     # getrf 50.3 -> 52.3, potrf 57.8 -> 58.6 TFLOP/s); dgeqrf stays at 512
     # (384: 50.5, 512: 51.9).  Multi-GPU grids keep 512 so the 2-D cyclic
     # distribution has enough block columns per process.
-    default_nb = {"dgetrf": 1024, "dpotrf": 1024} if world == 1 else {}
+    # dgesv_mixed likewise (fp32 LU: 2.49 -> 2.42 s, profiles/r1_gesv_mixed_n64k_norm_fix.txt).
+    default_nb = {"dgetrf": 1024, "dpotrf": 1024, "dgesv_mixed": 1024} if world == 1 else {}
     if a.nb:
         default_nb = {}
     a.nb = a.nb or 512
@@ -145,8 +146,13 @@ def main():
             elif rname == "dgeqrf":
                 s.geqrf(mats["A"], **opts)
             elif rname == "dgesv_mixed":
-                info, _, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], **opts)
+                s._slate.clear_timers()
+                lu = {"tntpiv": 2, "ppiv": 1}[a.method_lu]  # MethodLU::CALU / PartialPiv
+                info, _, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], method_lu=lu, **opts)
                 assert info == 0 and iters >= 0, f"dgesv_mixed info={info} iters={iters}"
+                if rank == 0:
+                    tm = {k: round(v * 1e3, 1) for k, v in s._slate.timers().items() if "gesv_mixed" in k}
+                    print(f"# dgesv_mixed iters={iters} phase ms: {tm}", file=sys.stderr, flush=True)
             barrier_sync()
             dt = time.perf_counter() - t0
             if a.trace and step == a.warmup:

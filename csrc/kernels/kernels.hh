@@ -64,7 +64,9 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
 // kind: 'M' max, '1' column sums, 'I' row sums, 'F' column (scale, sumsq)
 template <typename T>
 void genorm_partial(char kind, char uplo, char diag, int64_t m, int64_t n, const T* A, int64_t lda,
-                    int64_t goff_row, int64_t goff_col, rt<T>* out, hipStream_t s);
+                    int64_t goff_row, int64_t goff_col, rt<T>* out, hipStream_t s, rt<T>* work = nullptr);
+// elements of `work` genorm_partial uses for kind 'I' (column-chunk partial row sums)
+int64_t genorm_work_size(char kind, int64_t m, int64_t n);
 
 // ---- matgen (matgen.hip): fill a block-cyclic local array (view block at
 // absolute local (rb, cb), global offset (row0, col0)) from matgen_entry.hh

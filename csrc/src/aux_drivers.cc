@@ -467,6 +467,22 @@ void local_parts(BaseMatrix<T> const& A, Target target, char kind, Uplo mask, Di
     if (kind == '1') P.colsum.assign(N, 0);
     if (kind == 'I') P.rowsum.assign(M, 0);
     bool band = kl >= 0 || ku >= 0;
+    if (!band && mask == Uplo::General && diag == Diag::NonUnit && A.aligned()) {
+        // General matrix: the whole local block (ScaLAPACK-layout local array)
+        // in one kernel launch and one sync, instead of one of each per tile.
+        LocalBlock<T> la = A.local(loc, false);
+        if (la.empty()) return;
+        const int p = s.grid->p(), q = s.grid->q();
+        std::vector<R> out(kind == 'I' ? la.m : (kind == 'F' ? 2 * la.n : la.n));
+        lb::norm_partial(c, kind, Uplo::General, Diag::NonUnit, la.m, la.n, la.ptr, la.ld, 0, 0, out.data());
+        auto gcol = [&](int64_t jl) { return l2g(A.lcol_begin() + jl, s.nb, s.crel(), q) - A.col0(); };
+        auto grow = [&](int64_t il) { return l2g(A.lrow_begin() + il, s.mb, s.rrel(), p) - A.row0(); };
+        if (kind == 'M') for (R v : out) P.maxv = max_nan(P.maxv, v);
+        else if (kind == '1') for (int64_t jl = 0; jl < la.n; ++jl) P.colsum[gcol(jl)] += out[jl];
+        else if (kind == 'I') for (int64_t il = 0; il < la.m; ++il) P.rowsum[grow(il)] += out[il];
+        else for (int64_t jl = 0; jl < la.n; ++jl) combine_sumsq(P.scale, P.sumsq, out[2 * jl], out[2 * jl + 1]);
+        return;
+    }
     // per local tile (for trapezoid / band masks the global offsets matter)
     int64_t smt = A.op() == Op::NoTrans ? A.mt() : A.nt();
     int64_t snt = A.op() == Op::NoTrans ? A.nt() : A.mt();

@@ -842,7 +842,9 @@ void norm_partial(Ctx const& c, char kind, Uplo uplo, Diag diag, int64_t m, int6
     Scratch sc(c);
     int64_t cnt = kind == 'I' ? m : (kind == 'F' ? 2 * n : n);
     R* d = sc.alloc<R>(cnt);
-    kd::genorm_partial(kind, upc(uplo), char(diag), m, n, dptr(A), lda, goff_row, goff_col, d, c.stream);
+    int64_t nw = kd::genorm_work_size(kind, m, n);
+    R* w = nw > 0 ? sc.alloc<R>(nw) : nullptr;
+    kd::genorm_partial(kind, upc(uplo), char(diag), m, n, dptr(A), lda, goff_row, goff_col, d, c.stream, w);
     device::memcpy_async(out, d, cnt * sizeof(R), c.stream);
     slate_hip_call(hipStreamSynchronize(c.stream));
 }

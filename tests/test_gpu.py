@@ -229,6 +229,18 @@ def test_norm_device():
     assert s.norm(s.Norm.Max, A, target="d") == np.abs(a).max()
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128, np.float32])
+def test_norm_device_wide_block(dtype):
+    # local block wider than one column chunk: 2-D row-sum kernel + in-order chunk reduction
+    a = rnd(333, 1700, dtype, 12)
+    A = s.from_numpy(a, nb=96, target="d")
+    rt = 1e-5 if dtype == np.float32 else 1e-12
+    for kind, npk in [(s.Norm.One, 1), (s.Norm.Inf, np.inf), (s.Norm.Fro, "fro")]:
+        ref = np.linalg.norm(a.astype(np.complex128 if np.iscomplexobj(a) else np.float64), npk)
+        assert abs(s.norm(kind, A, target="d") - ref) < rt * ref, kind
+    assert abs(s.norm(s.Norm.Max, A, target="d") - np.abs(a).max()) <= rt * np.abs(a).max()
+
+
 def test_generate_matrix_device_matches_host():
     for kind in ("rands", "spd"):
         A = s.Matrix(300, 300, 64); A.insertLocalTiles(s.Target.Devices)
