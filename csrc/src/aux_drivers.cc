@@ -467,14 +467,17 @@ void local_parts(BaseMatrix<T> const& A, Target target, char kind, Uplo mask, Di
     if (kind == '1') P.colsum.assign(N, 0);
     if (kind == 'I') P.rowsum.assign(M, 0);
     bool band = kl >= 0 || ku >= 0;
-    if (!band && mask == Uplo::General && diag == Diag::NonUnit && A.aligned()) {
-        // General matrix: the whole local block (ScaLAPACK-layout local array)
-        // in one kernel launch and one sync, instead of one of each per tile.
+    const int p = s.grid->p(), q = s.grid->q();
+    // On a 1 x 1 grid the local block is the view itself, so trapezoid masks
+    // and unit diagonals apply to it directly (view-relative offsets 0, 0).
+    const bool whole = mask == Uplo::General && diag == Diag::NonUnit;
+    if (!band && (whole || (p == 1 && q == 1)) && A.aligned()) {
+        // the whole local block (ScaLAPACK-layout local array) in one kernel
+        // launch and one sync, instead of one of each per tile
         LocalBlock<T> la = A.local(loc, false);
         if (la.empty()) return;
-        const int p = s.grid->p(), q = s.grid->q();
         std::vector<R> out(kind == 'I' ? la.m : (kind == 'F' ? 2 * la.n : la.n));
-        lb::norm_partial(c, kind, Uplo::General, Diag::NonUnit, la.m, la.n, la.ptr, la.ld, 0, 0, out.data());
+        lb::norm_partial(c, kind, mask, diag, la.m, la.n, la.ptr, la.ld, 0, 0, out.data());
         auto gcol = [&](int64_t jl) { return l2g(A.lcol_begin() + jl, s.nb, s.crel(), q) - A.col0(); };
         auto grow = [&](int64_t il) { return l2g(A.lrow_begin() + il, s.mb, s.rrel(), p) - A.row0(); };
         if (kind == 'M') for (R v : out) P.maxv = max_nan(P.maxv, v);

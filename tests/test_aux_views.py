@@ -55,3 +55,14 @@ def test_general_set_diag_on_offset_view(off):
     blk[:] = 1.0
     np.fill_diagonal(blk, 5.0)
     np.testing.assert_array_equal(s.to_numpy(A), exp)
+
+
+@pytest.mark.parametrize("tg", ["h", pytest.param("d", marks=pytest.mark.gpu)])
+def test_masked_norms_whole_block(tg):
+    # Hermitian / unit-triangular norms on a 1 x 1 grid take the whole-block
+    # path (one launch with the trapezoid mask); checked against numpy
+    import subprocess, sys, os
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "masked_norm_check.py"), tg],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "masked norms ok" in r.stdout, r.stdout + r.stderr
