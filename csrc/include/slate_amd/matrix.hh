@@ -308,6 +308,9 @@ public:
     BaseTrapezoidMatrix(Uplo uplo, BaseMatrix<T> const& b, MatrixKind k, Diag d = Diag::NonUnit)
         : BaseMatrix<T>(b) {
         slate_error_if_msg(uplo == Uplo::General, "trapezoid matrix requires Upper or Lower");
+        // the diagonal of tile (i, i) is the matrix diagonal only for square
+        // tiles (reference BaseTrapezoidMatrix.hh:397 asserts tileMb == tileNb)
+        slate_error_if_msg(b.mb() != b.nb(), "trapezoid/triangular/Hermitian/symmetric matrix requires square tiles (mb == nb)");
         this->set_uplo(uplo); this->set_kind(k); this->set_diag(d);
     }
     Matrix<T> general() const { Matrix<T> r{BaseMatrix<T>(*this)}; r.set_uplo(Uplo::General); return r; }

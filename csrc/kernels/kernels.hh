@@ -18,6 +18,49 @@ namespace dev {
 
 template <typename T> using rt = typename real_type_t<T>::type;
 
+// ---- 2-D block-cyclic row distribution of a view, as seen by one process
+// (ScaLAPACK RSRC semantics: tile row ti lives on process row (ti + rsrc) % p).
+// gr = view-relative global row; li = row index in the view's local block.
+struct RowDist {
+    int64_t row0;        // storage row of view row 0
+    int64_t mb;          // tile rows
+    int64_t lrow_begin;  // first local row of the view in the local array
+    int p, rsrc, myrow, rrel;
+};
+SLATE_HD inline int rd_owner(RowDist const& d, int64_t gr) { return int(((d.row0 + gr) / d.mb + d.rsrc) % d.p); }
+SLATE_HD inline int64_t rd_lrow(RowDist const& d, int64_t gr) {
+    int64_t R = d.row0 + gr;
+    return (R / d.mb / d.p) * d.mb + R % d.mb - d.lrow_begin;
+}
+SLATE_HD inline int64_t rd_l2g(RowDist const& d, int64_t li) {
+    int64_t L = li + d.lrow_begin;
+    return ((L / d.mb) * d.p + d.rrel) * d.mb + L % d.mb - d.row0;
+}
+
+// ---- distributed LU row permutations (lu_dist.hip)
+/// out(i, :) = A(sel[i], :) for i < cnt (ncols columns); id_out[i] = id_in[sel[i]]
+/// when id_in is given, else the global row of local row li_base + sel[i].
+template <typename T>
+void gather_rows_ids(int64_t cnt, int64_t ncols, const int64_t* sel, const T* A, int64_t lda, T* out, int64_t ldo,
+                     const int64_t* id_in, int64_t* id_out, RowDist d, int64_t li_base, hipStream_t s);
+/// Row movements of `cnt` sequential interchanges at positions base..base+cnt-1.
+/// mode 0: in[t] + in_off = ORIGINAL row that ends at base+t (tournament winners);
+/// mode 1: in[t] + in_off = LAPACK ipiv (current position swapped with base+t).
+/// Emits ipiv_out[t] (LAPACK ipiv, global rows) and 2*cnt slots:
+/// slot t < cnt: dst base+t <- src (always filled); slot cnt+j: a row outside
+/// [base, base+cnt) that receives a displaced row (-1 if unused).  cnt <= 1024.
+void perm_slots(int mode, int64_t base, int cnt, const int64_t* in, int64_t in_off, int64_t* ipiv_out,
+                int64_t* slot_src, int64_t* slot_dst, hipStream_t s);
+/// buf(s - s0, j) = A(row slot_src[s], j) if this process owns that row, else
+/// 0, for slots [s0, s1) and ncols local columns (buf ld = ldb).
+template <typename T>
+void slots_pack(int s0, int s1, int64_t ncols, const int64_t* slot_src, const T* A, int64_t lda, RowDist d, T* buf,
+                int64_t ldb, hipStream_t s);
+/// A(row slot_dst[s], j) = buf(s - s0, j) for owned destination rows, slots [s0, s1).
+template <typename T>
+void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const T* buf, int64_t ldb, T* A,
+                  int64_t lda, RowDist d, hipStream_t s);
+
 // ---- GEMM (gemm_mfma.hip: real MFMA; gemm_cplx.hip: complex)
 template <typename T>
 void gemm_real(char transA, char transB, int64_t m, int64_t n, int64_t k,

@@ -1,0 +1,158 @@
+// Device side of the distributed LU row permutations (getrf / getrf_tntpiv on
+// a p x q grid with p > 1).
+//
+// Reference behaviour: the panel's pivots are broadcast to every rank
+// (src/getrf.cc:116, src/getrf_tntpiv.cc:185) and permuteRows<Devices>
+// (src/internal/internal_swap.cc:511-805) moves the pivot rows between the
+// ranks of each block column with MPI_Isend/Irecv sized from host-side pivot
+// counts, plus one blas::swap per pivot on the device.
+//
+// MI355X design: the host never learns the pivots inside the k-loop.  The
+// permutation of one panel touches at most 2*kd rows: the kd rows of the
+// diagonal block T and the winner rows outside T (which receive the displaced
+// rows of T).  Every row movement becomes a "slot" (src row -> dst row)
+// computed on the device (perm_slots); each process packs the source rows it
+// owns into a fixed 2*kd x ncols slot buffer (zeros elsewhere), one RCCL
+// all-reduce over the column communicator assembles every slot on every
+// process, and each process unpacks the rows it owns.  Message sizes are
+// therefore known on the host without a device->host copy, and the winner
+// slots (the new block row of U, before the triangular solve) arrive on
+// EVERY process of the column, which removes the separate U broadcast.
+#include "device_common.hh"
+#include "kernels.hh"
+
+namespace slate_amd {
+namespace dev {
+
+namespace {
+
+constexpr int kMaxSlots = 1024;   // kd <= 1024 (tile size)
+
+template <typename T>
+__global__ __launch_bounds__(64) void gather_rows_ids_kernel(int64_t cnt, int64_t ncols, const int64_t* sel,
+                                                             const T* A, int64_t lda, T* out, int64_t ldo,
+                                                             const int64_t* id_in, int64_t* id_out, RowDist d,
+                                                             int64_t li_base) {
+    const int64_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= cnt) return;
+    const int64_t r = sel[i];
+    if (blockIdx.y == 0 && id_out) id_out[i] = id_in ? id_in[r] : rd_l2g(d, li_base + r);
+    for (int64_t j = blockIdx.y; j < ncols; j += gridDim.y) out[i + j * ldo] = A[r + j * lda];
+}
+
+// One workgroup replays the cnt interchanges on a slot table in LDS:
+// pos[s] = row of slot s (slots 0..cnt-1 are base..base+cnt-1, the rest are
+// rows outside the block, registered on first touch), content[s] = slot whose
+// ORIGINAL row currently sits at pos[s].  Lookups are parallel over the
+// table; the swap itself is one thread (wave-uniform, a few LDS ops).
+__global__ __launch_bounds__(256) void perm_slots_kernel(int mode, int64_t base, int cnt, const int64_t* in,
+                                                         int64_t in_off, int64_t* ipiv_out, int64_t* slot_src,
+                                                         int64_t* slot_dst) {
+    __shared__ int64_t pos[2 * kMaxSlots];
+    __shared__ int content[2 * kMaxSlots];
+    __shared__ int s_found, s_n;
+    const int tid = threadIdx.x;
+    for (int s = tid; s < cnt; s += 256) { pos[s] = base + s; content[s] = s; }
+    if (tid == 0) s_n = cnt;
+    __syncthreads();
+    for (int t = 0; t < cnt; ++t) {
+        const int64_t key = in[t] + in_off;
+        if (tid == 0) s_found = -1;
+        __syncthreads();
+        const int n = s_n;
+        for (int s = tid; s < n; s += 256) {
+            bool hit = mode == 0 ? (pos[content[s]] == key) : (pos[s] == key);
+            if (hit) s_found = s;
+        }
+        __syncthreads();
+        if (tid == 0) {
+            int f = s_found;
+            if (f < 0) { f = s_n++; pos[f] = key; content[f] = f; }
+            ipiv_out[t] = pos[f];
+            int a = content[t];
+            content[t] = content[f];
+            content[f] = a;
+        }
+        __syncthreads();
+    }
+    const int n = s_n;
+    for (int s = tid; s < 2 * cnt; s += 256) {
+        if (s < n) { slot_src[s] = pos[content[s]]; slot_dst[s] = pos[s]; }
+        else { slot_src[s] = -1; slot_dst[s] = -1; }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void slots_pack_kernel(int s0, int s1, int64_t ncols, const int64_t* slot_src,
+                                                        const T* A, int64_t lda, RowDist d, T* buf, int64_t ldb) {
+    const int s = s0 + blockIdx.x * 64 + threadIdx.x;
+    if (s >= s1) return;
+    const int64_t src = slot_src[s];
+    const bool mine = src >= 0 && rd_owner(d, src) == d.myrow;
+    const int64_t lr = mine ? rd_lrow(d, src) : 0;
+    for (int64_t j = blockIdx.y; j < ncols; j += gridDim.y)
+        buf[(s - s0) + j * ldb] = mine ? A[lr + j * lda] : zero<T>();
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void slots_unpack_kernel(int s0, int s1, int64_t ncols, const int64_t* slot_dst,
+                                                          const T* buf, int64_t ldb, T* A, int64_t lda, RowDist d) {
+    const int s = s0 + blockIdx.x * 64 + threadIdx.x;
+    if (s >= s1) return;
+    const int64_t dst = slot_dst[s];
+    if (dst < 0 || rd_owner(d, dst) != d.myrow) return;
+    const int64_t lr = rd_lrow(d, dst);
+    for (int64_t j = blockIdx.y; j < ncols; j += gridDim.y) A[lr + j * lda] = buf[(s - s0) + j * ldb];
+}
+
+inline unsigned col_blocks(int64_t ncols) { return (unsigned)std::min<int64_t>(std::max<int64_t>(ncols, 1), 8192); }
+
+}  // namespace
+
+template <typename T>
+void gather_rows_ids(int64_t cnt, int64_t ncols, const int64_t* sel, const T* A, int64_t lda, T* out, int64_t ldo,
+                     const int64_t* id_in, int64_t* id_out, RowDist d, int64_t li_base, hipStream_t s) {
+    if (cnt <= 0) return;
+    dim3 g((unsigned)((cnt + 63) / 64), col_blocks(ncols));
+    hipLaunchKernelGGL(gather_rows_ids_kernel<T>, g, dim3(64), 0, s, cnt, ncols, sel, A, lda, out, ldo, id_in, id_out,
+                       d, li_base);
+}
+
+void perm_slots(int mode, int64_t base, int cnt, const int64_t* in, int64_t in_off, int64_t* ipiv_out,
+                int64_t* slot_src, int64_t* slot_dst, hipStream_t s) {
+    if (cnt <= 0) return;
+    hipLaunchKernelGGL(perm_slots_kernel, dim3(1), dim3(256), 0, s, mode, base, cnt, in, in_off, ipiv_out, slot_src,
+                       slot_dst);
+}
+
+template <typename T>
+void slots_pack(int s0, int s1, int64_t ncols, const int64_t* slot_src, const T* A, int64_t lda, RowDist d, T* buf,
+                int64_t ldb, hipStream_t s) {
+    if (s1 <= s0 || ncols <= 0) return;
+    dim3 g((unsigned)((s1 - s0 + 63) / 64), col_blocks(ncols));
+    hipLaunchKernelGGL(slots_pack_kernel<T>, g, dim3(64), 0, s, s0, s1, ncols, slot_src, A, lda, d, buf, ldb);
+}
+
+template <typename T>
+void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const T* buf, int64_t ldb, T* A,
+                  int64_t lda, RowDist d, hipStream_t s) {
+    if (s1 <= s0 || ncols <= 0) return;
+    dim3 g((unsigned)((s1 - s0 + 63) / 64), col_blocks(ncols));
+    hipLaunchKernelGGL(slots_unpack_kernel<T>, g, dim3(64), 0, s, s0, s1, ncols, slot_dst, buf, ldb, A, lda, d);
+}
+
+#define SLATE_INST_LUDIST(T)                                                                                       \
+    template void gather_rows_ids<T>(int64_t, int64_t, const int64_t*, const T*, int64_t, T*, int64_t,            \
+                                     const int64_t*, int64_t*, RowDist, int64_t, hipStream_t);                    \
+    template void slots_pack<T>(int, int, int64_t, const int64_t*, const T*, int64_t, RowDist, T*, int64_t,       \
+                                hipStream_t);                                                                      \
+    template void slots_unpack<T>(int, int, int64_t, const int64_t*, const T*, int64_t, T*, int64_t, RowDist,     \
+                                  hipStream_t);
+
+SLATE_INST_LUDIST(float)
+SLATE_INST_LUDIST(double)
+SLATE_INST_LUDIST(cplx<float>)
+SLATE_INST_LUDIST(cplx<double>)
+
+}  // namespace dev
+}  // namespace slate_amd

@@ -21,6 +21,7 @@
 // tournament over 256-row leaves on the device (kernels/tslu.hip), then
 // factors that block without further pivoting.
 #include "internal.hh"
+#include "lu_dist.hh"
 #include "../kernels/kernels.hh"
 
 #include <algorithm>
@@ -165,6 +166,395 @@ void permute_rows_dist(BaseMatrix<T> const& A, RowPairs const& P, int64_t c0, in
 
 enum class PanelMode { Partial, Tournament, NoPiv };
 
+//------------------------------------------------------------------------------
+/// LU on a p x q grid with p > 1.  No host synchronization inside the k-loop:
+/// every pivot-dependent quantity stays on the device and every message size
+/// is known on the host from the distribution alone.
+///
+/// Panel (process column qk, rows spread over the p process rows):
+///   Tournament (CALU, reference internal_getrf_tntpiv.cc:479-633): every
+///     process selects kd candidate rows from its local panel rows with the
+///     device tournament panel (a local LU on a copy); the candidates of
+///     process rows meet in a binary tree rooted at the diagonal process pk
+///     (ncclSend/Recv of kd x kb ORIGINAL rows + their global indices over the
+///     column communicator, partial-pivoting LU of the stacked 2kd x kb block);
+///     the root's final LU gives the winners and [L11\U11].  Winners and LU11
+///     go down the column; the panel rows are permuted (slot all-reduce) and
+///     L21 = A21 U11^{-1} is a local trsm on every process.
+///   Partial (PPLU): exact partial pivoting.  The panel's rows are gathered to
+///     pk over the column communicator (sizes known from the distribution),
+///     factored there by the device panel and scattered back; the LAPACK ipiv
+///     becomes the same device slots.
+///   NoPiv: pk factors the diagonal block, the column solves L21 locally.
+/// Row permutation of every other column range: lu_dist.hip slots (pack ->
+/// all-reduce over the column communicator -> unpack), which also delivers
+/// the (unsolved) U block row to every process of the column, so U12 =
+/// L11^{-1} (...) is computed redundantly instead of broadcast.  Trailing
+/// columns are processed in chunks so the all-reduce of chunk c+1 overlaps the
+/// GEMM of chunk c.  The interchanges of the left columns [0, k) are applied
+/// one step late, behind the next panel's messages on the comm queue.
+template <typename T>
+int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelMode mode, Target target) {
+    using namespace internal::ludist;
+    trace::Block tb("getrf_dist");
+    const int64_t la = get_option<int64_t>(opts, Option::Lookahead, 1);
+    auto& g = *A.grid();
+    const int p = g.p(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    const int64_t mt = A.mt(), nt = A.nt(), m = A.m(), n = A.n();
+    const int64_t kt = std::min(mt, nt), nb = A.nb();
+    slate_error_if_msg(nb > 1024, "getrf on a p > 1 grid: tile size above 1024");
+    LocalBlock<T> L = A.local(loc, true);
+    T* a = L.ptr;
+    const int64_t lda = L.ld, mloc = L.m, nloc = L.n;
+    const bool pivot = mode != PanelMode::NoPiv;
+    const RowDist rd = row_dist(A);
+    const int qC = device::kCommQueue, qP = 1;
+
+    Sched S(target);
+    const int R = int(std::max<int64_t>(3, la + 2));
+    std::vector<Work<T>> W(R), LU(R);
+    std::vector<Work<int64_t>> PV(R);        // [win nb | ipiv nb | slot_src 2nb | slot_dst 2nb]
+    for (int r = 0; r < R; ++r) {
+        W[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+        LU[r].resize(target, size_t(nb) * nb);
+        PV[r].resize(target, size_t(6 * nb));
+    }
+    const size_t ubn = size_t(2 * nb) * size_t(std::max<int64_t>(nloc, 1));
+    Work<T> UB(target, ubn), LB(pivot ? target : Target::HostTask, pivot ? ubn : 1), PB(target, size_t(nb) * nb);
+    // panel scratch
+    Work<T> Wsel(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+    Work<T> Cb(target, size_t(nb) * nb), Cr(target, size_t(nb) * nb), Sb(target, size_t(2 * nb) * nb),
+        Fb(target, size_t(2 * nb) * nb);
+    Work<int64_t> ids(target, nb), idr(target, nb), idS(target, 2 * nb),
+        perm(target, size_t(std::max<int64_t>(mloc, 2 * nb))), pip(target, nb);
+    Work<T> Gfull, Gr;
+    if (mode == PanelMode::Partial) {
+        Gfull.resize(target, size_t(std::max<int64_t>(m, 1)) * nb);
+        Gr.resize(target, size_t(std::max<int64_t>(m, 1)) * nb);
+    }
+    Work<int64_t> ipiv_all(target, size_t(std::max<int64_t>(kt, 1)) * nb);
+    Work<int> dinfo(target, 2);               // [info, dummy]
+    {
+        lb::Ctx c0 = S.ctx(qP);
+        if (c0.dev()) device::memset_async(dinfo.data(), 0, 2 * sizeof(int), c0.stream);
+        else dinfo.data()[0] = dinfo.data()[1] = 0;
+    }
+    int* info_real = dinfo.data();
+    int* info_dummy = dinfo.data() + 1;
+    auto lcols = [&](int64_t j0, int64_t j1) { return std::make_pair(lcol_of(A, j0), lcol_of(A, j1)); };
+    const int64_t tSel = Sched::tok(30, 0), tPB = Sched::tok(33, 0), tLeft = Sched::tok(34, 0);
+
+    // left-column interchanges of step k2 on tile columns [0, k2)
+    auto left = [&](int64_t k2) {
+        if (!pivot || k2 <= 0) return;
+        int64_t nc = lcol_of(A, k2);
+        if (nc <= 0) return;
+        const int s2 = int(k2 % R);
+        const int64_t kd2 = std::min(A.tileNb(k2), m - grow_of(A, k2));
+        int64_t* pv2 = PV[s2].data();
+        S.task(qC, {Sched::tok(31, s2), Sched::col(k2 - 1)}, {tLeft}, [&, nc, kd2, pv2](lb::Ctx const& c) {
+            trace::Block t2("getrf_left_swap");
+            const int ns = int(2 * kd2);
+            slots_pack(c, 0, ns, nc, pv2 + 2 * nb, a, lda, rd, LB.data(), ns);
+            g.col().allreduce(LB.data(), size_t(ns) * nc, ReduceOp::Sum, c.loc(), c.stream);
+            slots_unpack(c, 0, ns, nc, pv2 + 4 * nb, LB.data(), ns, a, lda, rd);
+        });
+    };
+
+    for (int64_t k = 0; k < kt; ++k) {
+        const int64_t kb = A.tileNb(k), kk = grow_of(A, k), M = m - kk, kd = std::min(kb, M);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const bool in_col = (mycol == qk), diag = (myrow == pk);
+        const int64_t lr_k = lrow_of(A, k);
+        // first local row below the diagonal block T = rows [kk, kk + kd) (on pk
+        // T starts tile k; kd < tileMb(k) in the last block column)
+        const int64_t lr_k1 = diag ? lr_k + kd : lr_k;
+        const int64_t lc_k = in_col ? lcol_of(A, k) : 0;
+        const int64_t mr = mloc - lr_k, ldw = std::max<int64_t>(mr, 1);
+        const int slot = int(k % R);
+        int64_t* pv = PV[slot].data();
+        int64_t* win = pv;
+        int64_t* ipv = pv + nb;
+        int64_t* ssrc = pv + 2 * nb;
+        int64_t* sdst = pv + 4 * nb;
+        T* LUk = LU[slot].data();
+        const int64_t ldlu = kd;
+        T* Wk = W[slot].data();
+        T* ap = a + lr_k + lc_k * lda;        // my panel rows (>= kk)
+        T* apc = a + lc_k * lda;               // panel column, local row 0
+        const int64_t tPV = Sched::tok(31, slot), tW = Sched::tok(32, slot);
+        // rows of the panel (global rows >= kk) per process row: host-known
+        std::vector<int64_t> rows_r(p, 0);
+        for (int64_t i = k; i < mt; ++i) rows_r[A.srow_owner(i)] += A.tileMb(i);
+
+        // ================================================================ panel
+        if (in_col && mode == PanelMode::Tournament) {
+            // tree over the process rows holding panel rows, rooted at pk
+            std::vector<int> part;
+            for (int d = 0; d < p; ++d) { int r = (pk + d) % p; if (rows_r[r] > 0) part.push_back(r); }
+            const int np = int(part.size());
+            std::vector<int64_t> cnt(np);
+            for (int i = 0; i < np; ++i) cnt[i] = std::min(rows_r[part[i]], kd);
+            int ix = -1;
+            for (int i = 0; i < np; ++i) if (part[i] == myrow) ix = i;
+            struct Round { bool recv; int peer; int64_t mine, theirs; bool final; };
+            std::vector<Round> rounds;
+            for (int l = 1; l < np; l *= 2) {
+                for (int i = 0; i + l < np; i += 2 * l) {
+                    if (i == ix) rounds.push_back({true, part[i + l], cnt[i], cnt[i + l], false});
+                    if (i + l == ix) rounds.push_back({false, part[i], cnt[i + l], 0, false});
+                    cnt[i] = std::min(cnt[i] + cnt[i + l], kd);
+                }
+            }
+            if (diag && !rounds.empty()) rounds.back().final = true;
+            const bool sel_final = diag && rounds.empty();
+            if (ix >= 0) {
+                const int64_t cme = std::min(mr, kd);
+                S.task(qP, {Sched::col(k)}, {tSel}, [&, ap, mr, kb, kk, cme, sel_final, lr_k](lb::Ctx const& c) {
+                    trace::Block t2("getrf_tnt_local");
+                    lb::copy2d(c, mr, kb, ap, lda, Wsel.data(), mr);
+                    lb::getrf_panel(c, mr, kb, Wsel.data(), mr, pip.data(), perm.data(),
+                                    sel_final ? info_real : info_dummy, kk, true, true);
+                    gather_rows_ids(c, cme, kb, perm.data(), ap, lda, Cb.data(), cme, (int64_t const*)nullptr,
+                                    ids.data(), rd, lr_k);
+                });
+                int64_t cur = cme;
+                T const* lastF = Wsel.data();
+                int64_t ldF = mr;
+                for (auto const& rd_ : rounds) {
+                    if (!rd_.recv) {
+                        S.task(qC, {tSel}, {tSel}, [&, rd_, kb](lb::Ctx const& c) {
+                            trace::Block t2("getrf_tnt_send");
+                            std::vector<Comm::P2P> ops{{Cb.data(), size_t(rd_.mine * kb), rd_.peer, true}};
+                            g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                            std::vector<Comm::P2P> ops2{{ids.data(), size_t(rd_.mine), rd_.peer, true}};
+                            g.col().exchange(ops2, scalar_type<int64_t>(), c.loc(), c.stream);
+                        });
+                        break;
+                    }
+                    S.task(qC, {}, {tSel}, [&, rd_, kb](lb::Ctx const& c) {
+                        trace::Block t2("getrf_tnt_recv");
+                        std::vector<Comm::P2P> ops{{Cr.data(), size_t(rd_.theirs * kb), rd_.peer, false}};
+                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                        std::vector<Comm::P2P> ops2{{idr.data(), size_t(rd_.theirs), rd_.peer, false}};
+                        g.col().exchange(ops2, scalar_type<int64_t>(), c.loc(), c.stream);
+                    });
+                    const int64_t ms = rd_.mine + rd_.theirs, c2 = std::min(ms, kd);
+                    S.task(qP, {}, {tSel}, [&, rd_, kb, kk, ms, c2](lb::Ctx const& c) {
+                        trace::Block t2("getrf_tnt_merge");
+                        // stacked originals S = [mine; theirs], F = LU(S) with partial pivoting
+                        lb::copy2d(c, rd_.mine, kb, Cb.data(), rd_.mine, Sb.data(), ms);
+                        lb::copy2d(c, rd_.theirs, kb, Cr.data(), rd_.theirs, Sb.data() + rd_.mine, ms);
+                        lb::copy2d(c, rd_.mine, int64_t(1), ids.data(), rd_.mine, idS.data(), ms);
+                        lb::copy2d(c, rd_.theirs, int64_t(1), idr.data(), rd_.theirs, idS.data() + rd_.mine, ms);
+                        lb::copy2d(c, ms, kb, Sb.data(), ms, Fb.data(), ms);
+                        lb::getrf_panel(c, ms, kb, Fb.data(), ms, pip.data(), perm.data(),
+                                        rd_.final ? info_real : info_dummy, kk, true, false);
+                        gather_rows_ids(c, c2, kb, perm.data(), Sb.data(), ms, Cb.data(), c2, idS.data(), ids.data(),
+                                        rd, 0);
+                    });
+                    cur = c2;
+                    lastF = Fb.data();
+                    ldF = ms;
+                }
+                if (diag) {
+                    S.task(qP, {tSel}, {tPV}, [&, lastF, ldF, kd, kb, LUk, win](lb::Ctx const& c) {
+                        lb::copy2d(c, kd, kb, lastF, ldF, LUk, kd);
+                        lb::copy2d(c, kd, int64_t(1), ids.data(), kd, win, kd);
+                    });
+                }
+                (void)cur;
+            }
+            // winners and [L11\U11] down the panel column
+            S.task(qC, {}, {tPV}, [&, kd, kb, pk, LUk, win](lb::Ctx const& c) {
+                trace::Block t2("getrf_bcast_winners");
+                bcast(g.col(), win, size_t(kd), pk, c);
+                bcast(g.col(), LUk, size_t(kd * kb), pk, c);
+            });
+            S.task(qP, {}, {tPV}, [&, k, kk, kd, win, ipv, ssrc, sdst](lb::Ctx const& c) {
+                perm_slots(c, 0, kk, int(kd), win, 0, ipv, ssrc, sdst);
+            });
+            // panel rows: displaced rows to the vacated winner positions
+            S.task(qC, {tPV}, {Sched::col(k), tPB}, [&, kd, kb, apc, ssrc, sdst](lb::Ctx const& c) {
+                trace::Block t2("getrf_panel_perm");
+                slots_pack(c, int(kd), int(2 * kd), kb, ssrc, apc, lda, rd, PB.data(), kd);
+                g.col().allreduce(PB.data(), size_t(kd * kb), ReduceOp::Sum, c.loc(), c.stream);
+                slots_unpack(c, int(kd), int(2 * kd), kb, sdst, PB.data(), kd, apc, lda, rd);
+            });
+        } else if (in_col && mode == PanelMode::Partial) {
+            // gather the panel rows to pk (global order is host-known), factor, scatter back
+            std::vector<int64_t> off_r(p, 0);
+            {
+                int64_t o = 0;
+                for (int r = 0; r < p; ++r) if (r != pk) { off_r[r] = o; o += rows_r[r]; }
+            }
+            S.task(qC, {Sched::col(k)}, {tSel}, [&, kb, ap, mr, pk, off_r, rows_r](lb::Ctx const& c) {
+                trace::Block t2("getrf_pp_gather");
+                std::vector<Comm::P2P> ops;
+                if (myrow == pk) {
+                    for (int r = 0; r < p; ++r)
+                        if (r != pk && rows_r[r] > 0)
+                            ops.push_back({Gr.data() + off_r[r] * kb, size_t(rows_r[r] * kb), r, false});
+                } else if (mr > 0) {
+                    lb::copy2d(c, mr, kb, ap, lda, Wsel.data(), mr);
+                    ops.push_back({Wsel.data(), size_t(mr * kb), pk, true});
+                }
+                g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+            });
+            if (diag) {
+                S.task(qP, {tSel, Sched::col(k)}, {tSel, tPV, Sched::col(k)},
+                       [&, k, kb, kk, M, kd, ap, pk, off_r, rows_r, LUk](lb::Ctx const& c) {
+                    trace::Block t2("getrf_pp_panel");
+                    // assemble / scatter in tile order: (own rows, or rank r's buffer at its running offset)
+                    auto walk = [&](bool to_full) {
+                        std::vector<int64_t> o(p, 0);
+                        for (int64_t i = k; i < mt; ++i) {
+                            int r = A.srow_owner(i);
+                            int64_t ib = A.tileMb(i), gi = grow_of(A, i) - kk;
+                            T* src = (r == pk) ? ap + o[r] : Gr.data() + off_r[r] * kb + o[r];
+                            int64_t lds = (r == pk) ? lda : rows_r[r];
+                            if (to_full) lb::copy2d(c, ib, kb, src, lds, Gfull.data() + gi, M);
+                            else lb::copy2d(c, ib, kb, Gfull.data() + gi, M, src, lds);
+                            o[r] += ib;
+                        }
+                    };
+                    walk(true);
+                    lb::getrf_panel(c, M, kb, Gfull.data(), M, pip.data(), (int64_t*)nullptr, info_real, kk, true, false);
+                    walk(false);
+                    lb::copy2d(c, kd, kb, Gfull.data(), M, LUk, kd);
+                });
+            }
+            S.task(qC, {tSel}, {tSel, Sched::col(k)}, [&, kb, ap, mr, pk, off_r, rows_r](lb::Ctx const& c) {
+                trace::Block t2("getrf_pp_scatter");
+                std::vector<Comm::P2P> ops;
+                if (myrow == pk) {
+                    for (int r = 0; r < p; ++r)
+                        if (r != pk && rows_r[r] > 0)
+                            ops.push_back({Gr.data() + off_r[r] * kb, size_t(rows_r[r] * kb), r, true});
+                } else if (mr > 0) {
+                    ops.push_back({Wsel.data(), size_t(mr * kb), pk, false});
+                }
+                g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                if (myrow != pk && mr > 0) lb::copy2d(c, mr, kb, Wsel.data(), mr, ap, lda);
+            });
+            S.task(qC, {tSel}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) {
+                trace::Block t2("getrf_bcast_piv");
+                bcast(g.col(), pip.data(), size_t(kd), pk, c);
+                bcast(g.col(), LUk, size_t(kd * kb), pk, c);
+            });
+            S.task(qP, {tSel}, {tPV}, [&, k, kk, kd, ipv, ssrc, sdst](lb::Ctx const& c) {
+                perm_slots(c, 1, kk, int(kd), pip.data(), kk, ipv, ssrc, sdst);
+            });
+        } else if (in_col) {
+            // no pivoting: pk factors the diagonal block
+            if (diag) {
+                S.task(qP, {Sched::col(k)}, {Sched::col(k), tPV}, [&, kk, kd, kb, ap, LUk](lb::Ctx const& c) {
+                    lb::getrf_panel(c, kd, kb, ap, lda, pip.data(), (int64_t*)nullptr, info_real, kk, false, false);
+                    lb::copy2d(c, kd, kb, ap, lda, LUk, kd);
+                });
+            }
+            S.task(qC, {}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) { bcast(g.col(), LUk, size_t(kd * kb), pk, c); });
+        }
+        // L21 = A21 U11^{-1} (tournament / no pivoting: the panel rows are still
+        // original; partial: already factored by pk) and the L panel for the row
+        if (in_col) {
+            const bool solve = (mode != PanelMode::Partial);
+            S.task(qP, {tPV, tPB}, {Sched::col(k), tW}, [&, solve, kd, kb, ap, mr, lr_k1, lc_k, LUk, Wk, diag](lb::Ctx const& c) {
+                trace::Block t2("getrf_l21");
+                if (solve) {
+                    if (diag && mode != PanelMode::NoPiv) lb::copy2d(c, kd, kb, LUk, kd, ap, lda);
+                    lb::trsm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, mloc - lr_k1, kd, T(1), LUk, kd,
+                             a + lr_k1 + lc_k * lda, lda);
+                }
+                if (mr > 0) pack(c, mr, kb, ap, lda, Wk);
+            });
+        }
+        // pivots + LU11 and the L panel along the process rows
+        S.task(qC, {}, {tPV}, [&, k, kd, kb, qk, pv, ipv, LUk](lb::Ctx const& c) {
+            trace::Block t2("getrf_bcast_row");
+            if (pivot) {
+                bcast(g.row(), pv, size_t(6 * nb), qk, c);
+                lb::copy2d(c, kd, int64_t(1), ipv, kd, ipiv_all.data() + k * nb, kd);
+            }
+            bcast(g.row(), LUk, size_t(kd * kb), qk, c);
+        });
+        S.task(qC, {}, {tW}, [&, kb, qk, mr, Wk](lb::Ctx const& c) {
+            trace::Block t2("getrf_bcast_L");
+            bcast(g.row(), Wk, size_t(mr * kb), qk, c);
+        });
+
+        // ============================================== column ranges: U + update
+        const int64_t ldu = pivot ? 2 * kd : kd;
+        auto range = [&, k, kd, kb, pk, diag, lr_k, lr_k1, ldu, ssrc, sdst, LUk, Wk, ldw, tPV, tW](int queue, int64_t j0,
+                                                                                                   int64_t j1) {
+            const auto cc = lcols(j0, j1);
+            const int64_t c0 = cc.first, nc = cc.second - cc.first;
+            if (nc <= 0) return;
+            std::vector<int64_t> cols;
+            for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
+            T* buf = UB.data() + c0 * ldu;
+            // permuted block row k of these columns -> buf (every process of the column)
+            S.task(qC, {tPV}, cols, [&, c0, nc, buf](lb::Ctx const& c) {
+                trace::Block t2("getrf_rows_exchange");
+                if (pivot) {
+                    slots_pack(c, 0, int(2 * kd), nc, ssrc, a + c0 * lda, lda, rd, buf, ldu);
+                    g.col().allreduce(buf, size_t(ldu * nc), ReduceOp::Sum, c.loc(), c.stream);
+                    slots_unpack(c, int(kd), int(2 * kd), nc, sdst, buf + kd, ldu, a + c0 * lda, lda, rd);
+                } else {
+                    if (diag) lb::copy2d(c, kd, nc, a + lr_k + c0 * lda, lda, buf, ldu);
+                    bcast(g.col(), buf, size_t(ldu * nc), pk, c);
+                }
+            });
+            std::vector<int64_t> in{tPV, tW};
+            S.task(queue, in, cols, [&, c0, nc, buf](lb::Ctx const& c) {
+                trace::Block t2("getrf_update");
+                lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, nc, T(1), LUk, kd, buf, ldu);
+                if (diag) lb::copy2d(c, kd, nc, buf, ldu, a + lr_k + c0 * lda, lda);
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, mloc - lr_k1, nc, kd, T(-1), Wk + (lr_k1 - lr_k), ldw,
+                         buf, ldu, T(1), a + lr_k1 + c0 * lda, lda);
+            });
+        };
+        const int64_t jla_end = std::min(nt, k + 1 + la);
+        for (int64_t j = k + 1; j < jla_end; ++j) range(device::kLookaheadQueue, j, j + 1);
+        if (jla_end < nt) {
+            const int64_t ntr = nt - jla_end;
+            const int64_t nch = std::min<int64_t>(4, ntr);
+            for (int64_t ch = 0; ch < nch; ++ch)
+                range(device::kTrailQueue, jla_end + ch * ntr / nch, jla_end + (ch + 1) * ntr / nch);
+        }
+        // interchanges of the previous step on its left columns
+        left(k - 1);
+    }
+    left(kt - 1);
+    S.wait_all();
+
+    // pivots -> Pivots (tile index relative to k, offset within the tile)
+    std::vector<int64_t> ip(size_t(std::max<int64_t>(kt, 1)) * nb, 0);
+    if (target == Target::Devices) {
+        if (pivot) device::memcpy_async(ip.data(), ipiv_all.data(), ip.size() * sizeof(int64_t), S.ctx(qP).stream);
+        slate_hip_call(hipStreamSynchronize(S.ctx(qP).stream));
+    } else if (pivot) {
+        std::copy(ipiv_all.data(), ipiv_all.data() + ip.size(), ip.begin());
+    }
+    pivots.assign(kt, {});
+    for (int64_t k = 0; k < kt; ++k) {
+        int64_t kk = grow_of(A, k), kd = std::min(A.tileNb(k), m - kk);
+        pivots[k].resize(kd);
+        for (int64_t t = 0; t < kd; ++t) {
+            int64_t r = pivot ? ip[k * nb + t] : kk + t;
+            int64_t ti = 0;
+            while (ti + k + 1 < mt && grow_of(A, k + ti + 1) <= r) ++ti;
+            pivots[k][t] = Pivot(ti, r - grow_of(A, k + ti));
+        }
+    }
+    int64_t info = fetch_info(target, info_real);
+    info = reduce_info(info, g.world());
+    A.storage()->update_origin();
+    (void)n;
+    return info;
+}
+
 template <typename T>
 int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMode mode) {
     trace::Block tb("getrf");
@@ -175,9 +565,12 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     slate_error_if_msg(A_in.mb() != A_in.nb(), "getrf: square tiles required");
     BaseMatrix<T> A = A_in;
     auto& g = *A.grid();
-    const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    if (g.p() > 1) return getrf_dist(A, pivots, opts, mode, target);
+    // ---- p == 1: the panel column is local to one process; pivots travel
+    // along the process row as device (dst, src) row pairs
+    const int q = g.q(), mycol = g.mycol();
     const Loc loc = loc_of(target);
-    const int64_t mt = A.mt(), nt = A.nt(), m = A.m(), n = A.n();
+    const int64_t mt = A.mt(), nt = A.nt(), m = A.m();
     const int64_t kt = std::min(mt, nt);
     const int64_t nb = A.nb();
     LocalBlock<T> L = A.local(loc, true);
@@ -197,22 +590,20 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     }
     Work<int64_t> perm(target, size_t(std::max<int64_t>(m, 1)));
     Work<int> dinfo(target, 1);
-    std::vector<int64_t> ipiv_all(std::min(m, n), 0);    // host copy (global rows)
-    std::vector<Work<int64_t>> ipiv_dev(kt);              // device per-step pivots (p == 1)
+    // every step's panel-relative pivots, copied to the host once at the end
+    Work<int64_t> ipiv_all(target, size_t(std::max<int64_t>(kt, 1)) * nb);
     {
         lb::Ctx c0 = S.ctx(1);
         if (c0.dev()) device::memset_async(dinfo.data(), 0, sizeof(int), c0.stream);
         else dinfo.data()[0] = 0;
     }
-    int host_info = 0;
-    std::vector<RowPairs> host_pairs(kt);
 
     for (int64_t k = 0; k < kt; ++k) {
         const int64_t kb = A.tileNb(k);
         const int64_t kk = grow_of(A, k);
         const int64_t M = m - kk;                         // panel rows (global)
         const int64_t kd = std::min(kb, M);                // pivots this step
-        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int qk = A.scol_owner(k);
         const bool in_col = (mycol == qk);
         const int64_t lr_k = lrow_of(A, k), lr_k1 = lrow_of(A, k + 1);
         const int64_t lc_k = in_col ? lcol_of(A, k) : 0;
@@ -224,121 +615,33 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         const int64_t tPanel = Sched::tok(6, slot), tBc = Sched::bcast(slot);
 
         // ------------------------------------------------------------ panel
-        if (p == 1) {
-            if (in_col) {
-                S.task(1, {}, {Sched::col(k), tPanel}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pv_dst, pv_src](lb::Ctx const& c) {
-                    trace::Block t2("getrf_panel");
-                    T* ap = a + lr_k + lc_k * lda;
-                    lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot, tnt);
-                    if (c.dev()) {
-                        slate_amd::dev::perm_pairs(kd, perm.data(), pv_ipiv, pv_dst, pv_src, c.stream);
-                    } else {
-                        // host: pairs from sequential pivots
-                        std::vector<int64_t> ip(pv_ipiv, pv_ipiv + kd);
-                        for (auto& x : ip) x += kk;
-                        RowPairs P = pairs_from_ipiv(kk, ip);
-                        int64_t cnt = int64_t(P.size());
-                        for (int64_t t = 0; t < 2 * kd; ++t) {
-                            pv_dst[t] = t < cnt ? P.dst[t] - kk : 0;
-                            pv_src[t] = t < cnt ? P.src[t] - kk : 0;
-                        }
-                        pv[5 * nb] = cnt;
+        if (in_col) {
+            S.task(1, {}, {Sched::col(k), tPanel}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pv_dst, pv_src](lb::Ctx const& c) {
+                trace::Block t2("getrf_panel");
+                T* ap = a + lr_k + lc_k * lda;
+                lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot, tnt);
+                if (c.dev()) {
+                    slate_amd::dev::perm_pairs(kd, perm.data(), pv_ipiv, pv_dst, pv_src, c.stream);
+                } else {
+                    // host: pairs from sequential pivots
+                    std::vector<int64_t> ip(pv_ipiv, pv_ipiv + kd);
+                    for (auto& x : ip) x += kk;
+                    RowPairs P = pairs_from_ipiv(kk, ip);
+                    int64_t cnt = int64_t(P.size());
+                    for (int64_t t = 0; t < 2 * kd; ++t) {
+                        pv_dst[t] = t < cnt ? P.dst[t] - kk : 0;
+                        pv_src[t] = t < cnt ? P.src[t] - kk : 0;
                     }
-                });
-            }
-        } else {
-            // p > 1: gather the panel to the diagonal process row, factor, scatter back
-            if (in_col) {
-                S.task(device::kCommQueue, {}, {Sched::col(k), tPanel}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pk](lb::Ctx const& c) {
-                    trace::Block t2("getrf_panel_gather");
-                    // local rows >= kk of the panel
-                    int64_t mr = mloc - lr_k;
-                    T* ap = a + lr_k + lc_k * lda;
-                    auto& st = *A.storage();
-                    // which global tile rows belong to which process row
-                    std::vector<std::vector<int64_t>> rows_of(p);   // global row starts of tiles
-                    std::vector<int64_t> cnt(p, 0);
-                    for (int64_t i = k; i < mt; ++i) {
-                        int r = A.srow_owner(i);
-                        rows_of[r].push_back(i);
-                        cnt[r] += A.tileMb(i);
-                    }
-                    Work<T> full(target, size_t(std::max<int64_t>(M, 1)) * kb);
-                    Work<T> mine(target, size_t(std::max<int64_t>(mr, 1)) * kb);
-                    pack(c, mr, kb, ap, lda, mine.data());
-                    // gather to pk
-                    std::vector<Comm::P2P> ops;
-                    std::vector<Work<T>> rbufs(p);
-                    if (myrow == pk) {
-                        for (int r = 0; r < p; ++r) {
-                            if (r == pk || cnt[r] == 0) continue;
-                            rbufs[r].resize(target, size_t(cnt[r]) * kb);
-                            ops.push_back({rbufs[r].data(), size_t(cnt[r] * kb), r, false});
-                        }
-                    } else if (mr > 0) {
-                        ops.push_back({mine.data(), size_t(mr * kb), pk, true});
-                    }
-                    g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                    if (myrow == pk) {
-                        // assemble in global order
-                        std::vector<int64_t> off(p, 0);
-                        for (int64_t i = k; i < mt; ++i) {
-                            int r = A.srow_owner(i);
-                            int64_t ib = A.tileMb(i);
-                            T const* src = (r == pk) ? mine.data() + off[r] : rbufs[r].data() + off[r];
-                            int64_t lds = (r == pk) ? std::max<int64_t>(mr, 1) : cnt[r];
-                            lb::copy2d(c, ib, kb, src, lds, full.data() + (grow_of(A, i) - kk), std::max<int64_t>(M, 1));
-                            off[r] += ib;
-                        }
-                        lb::getrf_panel(c, M, kb, full.data(), std::max<int64_t>(M, 1), pv_ipiv, nullptr,
-                                        dinfo.data(), kk, pivot, tnt);
-                        // scatter back (same layout)
-                        std::fill(off.begin(), off.end(), 0);
-                        for (int64_t i = k; i < mt; ++i) {
-                            int r = A.srow_owner(i);
-                            int64_t ib = A.tileMb(i);
-                            T* dst = (r == pk) ? mine.data() + off[r] : rbufs[r].data() + off[r];
-                            int64_t ldd = (r == pk) ? std::max<int64_t>(mr, 1) : cnt[r];
-                            lb::copy2d(c, ib, kb, full.data() + (grow_of(A, i) - kk), std::max<int64_t>(M, 1), dst, ldd);
-                            off[r] += ib;
-                        }
-                    }
-                    ops.clear();
-                    if (myrow == pk) {
-                        for (int r = 0; r < p; ++r)
-                            if (r != pk && cnt[r] > 0) ops.push_back({rbufs[r].data(), size_t(cnt[r] * kb), r, true});
-                    } else if (mr > 0) {
-                        ops.push_back({mine.data(), size_t(mr * kb), pk, false});
-                    }
-                    g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                    lb::copy2d(c, mr, kb, mine.data(), std::max<int64_t>(mr, 1), ap, lda);
-                    // pivots to every process of the column
-                    g.col().bcast(pv_ipiv, size_t(kd), scalar_type<int64_t>(), pk, c.loc(), c.stream);
-                    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-                    (void)st;
-                });
-            }
+                    pv[5 * nb] = cnt;
+                }
+            });
         }
 
-        // ------------------------------------------- pivots to every process
-        // p == 1: (ipiv, pairs) along the process row, stays on the device.
-        // p > 1: ipiv to every rank (world bcast from the diagonal owner), pairs
-        //        computed on the host (the row exchange needs host counts).
-        S.task(device::kCommQueue, {tPanel}, {tBc}, [&, k, kd, kk, qk, pk, pv_ipiv, slot](lb::Ctx const& c) {
+        // ------------------------------- (ipiv, pairs) along the process row
+        S.task(device::kCommQueue, {tPanel}, {tBc}, [&, k, kd, slot, pv_ipiv](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_piv");
-            if (p == 1) {
-                bcast(g.row(), PV[slot].data(), size_t(5 * nb + 8), qk, c);
-            } else {
-                int root = g.rank_of(pk, qk);
-                g.world().bcast(pv_ipiv, size_t(kd), scalar_type<int64_t>(), root, c.loc(), c.stream);
-                std::vector<int64_t> ip(kd);
-                if (c.dev()) {
-                    device::memcpy_async(ip.data(), pv_ipiv, kd * sizeof(int64_t), c.stream);
-                    slate_hip_call(hipStreamSynchronize(c.stream));
-                } else std::copy(pv_ipiv, pv_ipiv + kd, ip.begin());
-                for (auto& x : ip) x += kk;
-                host_pairs[k] = pairs_from_ipiv(kk, ip);
-            }
+            bcast(g.row(), PV[slot].data(), size_t(5 * nb + 8), qk, c);
+            if (pivot) lb::copy2d(c, kd, int64_t(1), pv_ipiv, kd, ipiv_all.data() + k * nb, kd);
         });
 
         // ----------------------------------------- L panel along process rows
@@ -353,25 +656,21 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
         // -------------------------------------- column ranges: permute, U, update
         // apply the step's row permutation to local columns [c0, c1)
-        auto permute = [&, k, kk, kd, slot](lb::Ctx const& c, int64_t c0, int64_t c1) {
+        auto permute = [&, kk, kd, slot](lb::Ctx const& c, int64_t c0, int64_t c1) {
             if (c1 <= c0 || !pivot) return;
-            if (p == 1) {
-                // rows: local == global; pairs relative to kk
-                int64_t* pvv = PV[slot].data();
-                if (c.dev()) {
-                    slate_amd::dev::permute_rows(c1 - c0, slate_amd::dev::dptr(a + kk + c0 * lda), lda,
-                                                 pvv + nb, pvv + 3 * nb, nullptr, int(2 * kd), c.stream);
-                } else {
-                    int64_t cnt = pvv[5 * nb];
-                    std::vector<T> tmp(cnt);
-                    for (int64_t j = c0; j < c1; ++j) {
-                        T* col = a + kk + j * lda;
-                        for (int64_t t = 0; t < cnt; ++t) tmp[t] = col[pvv[3 * nb + t]];
-                        for (int64_t t = 0; t < cnt; ++t) col[pvv[nb + t]] = tmp[t];
-                    }
-                }
+            // rows: local == global; pairs relative to kk
+            int64_t* pvv = PV[slot].data();
+            if (c.dev()) {
+                slate_amd::dev::permute_rows(c1 - c0, slate_amd::dev::dptr(a + kk + c0 * lda), lda,
+                                             pvv + nb, pvv + 3 * nb, nullptr, int(2 * kd), c.stream);
             } else {
-                permute_rows_dist(A, host_pairs[k], c0, c1, c);
+                int64_t cnt = pvv[5 * nb];
+                std::vector<T> tmp(cnt);
+                for (int64_t j = c0; j < c1; ++j) {
+                    T* col = a + kk + j * lda;
+                    for (int64_t t = 0; t < cnt; ++t) tmp[t] = col[pvv[3 * nb + t]];
+                    for (int64_t t = 0; t < cnt; ++t) col[pvv[nb + t]] = tmp[t];
+                }
             }
         };
         // columns of tiles [j0, j1) local to me
@@ -379,46 +678,35 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         T* WUk = WU[slot].data();
         // U row height is kd = tileMb(k) (< kb only for the last block row of a
         // wide matrix; rows beyond it are not part of the matrix)
-        auto urow = [&, k, kd, lr_k, pk, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
-            auto [c0, c1] = lcols(j0, j1);
+        auto urow = [&, kd, lr_k, Wk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+            auto cc = lcols(j0, j1);
+            int64_t c0 = cc.first, c1 = cc.second;
             if (c1 <= c0) return;
-            if (myrow == pk) {
-                // U(k, j0:j1) = L(k,k)^{-1} A(k, j0:j1); L(k,k) = top kd rows of W_k
-                lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, c1 - c0, T(1),
-                         Wk, std::max<int64_t>(mrows_k, 1), a + lr_k + c0 * lda, lda);
-            }
+            // U(k, j0:j1) = L(k,k)^{-1} A(k, j0:j1); L(k,k) = top kd rows of W_k
+            lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, c1 - c0, T(1),
+                     Wk, std::max<int64_t>(mrows_k, 1), a + lr_k + c0 * lda, lda);
         };
-        auto ubcast = [&, k, kb, kd, lr_k, pk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
-            auto [c0, c1] = lcols(j0, j1);
-            int64_t nc = c1 - c0;
-            if (nc <= 0) return;
-            T* dst = WUk + c0 * kb;
-            if (myrow == pk) lb::copy2d(c, kd, nc, a + lr_k + c0 * lda, lda, dst, kb);
-            if (p > 1) bcast(g.col(), dst, size_t(kb * nc), pk, c);
-        };
-        auto update = [&, k, kb, lr_k1, lr_k, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
-            auto [c0, c1] = lcols(j0, j1);
-            int64_t nc = c1 - c0, nr = mloc - lr_k1;
+        auto update = [&, kb, lr_k1, lr_k, Wk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+            auto cc = lcols(j0, j1);
+            int64_t c0 = cc.first, nc = cc.second - cc.first, nr = mloc - lr_k1;
             if (nc <= 0 || nr <= 0) return;
             trace::Block t2("getrf_update");
+            // U rows of these columns live in A itself (process row 0 owns them)
             lb::gemm(c, Op::NoTrans, Op::NoTrans, nr, nc, kb, T(-1), Wk + (lr_k1 - lr_k), std::max<int64_t>(mrows_k, 1),
-                     WUk + c0 * kb, kb, T(1), a + lr_k1 + c0 * lda, lda);
+                     a + lr_k + c0 * lda, lda, T(1), a + lr_k1 + c0 * lda, lda);
         };
+        (void)WUk;
 
         auto range_tasks = [&](int queue, int64_t j0, int64_t j1) {
             std::vector<int64_t> cols;
             for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
             std::vector<int64_t> in = {tBc, tL};
-            int pq = (p == 1) ? queue : device::kCommQueue;
-            S.task(pq, in, cols, [&, j0, j1](lb::Ctx const& c) {
-                auto [c0, c1] = lcols(j0, j1);
-                permute(c, c0, c1);
+            S.task(queue, in, cols, [&, j0, j1](lb::Ctx const& c) {
+                auto cc = lcols(j0, j1);
+                permute(c, cc.first, cc.second);
+                urow(c, j0, j1);
+                update(c, j0, j1);
             });
-            S.task(queue, in, cols, [&, urow, j0, j1](lb::Ctx const& c) { urow(c, j0, j1); });
-            const int64_t tU = Sched::tok(10 + queue, slot);
-            S.task(device::kCommQueue, cols, {tU}, [&, ubcast, j0, j1](lb::Ctx const& c) { ubcast(c, j0, j1); });
-            std::vector<int64_t> in2 = {tU, tL};
-            S.task(queue, in2, cols, [&, update, j0, j1](lb::Ctx const& c) { update(c, j0, j1); });
         };
         int64_t jla_end = std::min(nt, k + 1 + la);
         for (int64_t j = k + 1; j < jla_end; ++j)
@@ -427,31 +715,30 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
         // left columns [0, k): apply the step's interchanges (deferred queue)
         if (k > 0 && pivot) {
-            int lq = (p == 1) ? device::kTrailQueue : device::kCommQueue;
-            S.task(lq, {tBc}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
-                auto [c0, c1] = lcols(0, k);
-                permute(c, c0, c1);
+            S.task(device::kTrailQueue, {tBc}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
+                auto cc = lcols(0, k);
+                permute(c, cc.first, cc.second);
             });
         }
-        // host copy of this step's pivots (global rows)
-        S.task(device::kCommQueue, {tBc}, {}, [&, k, kk, kd, pv_ipiv](lb::Ctx const& c) {
-            std::vector<int64_t> ip(kd);
-            if (c.dev()) {
-                device::memcpy_async(ip.data(), pv_ipiv, kd * sizeof(int64_t), c.stream);
-                slate_hip_call(hipStreamSynchronize(c.stream));
-            } else std::copy(pv_ipiv, pv_ipiv + kd, ip.begin());
-            for (int64_t t = 0; t < kd; ++t) ipiv_all[kk + t] = ip[t] + (p == 1 ? kk : kk);
-        });
     }
     S.wait_all();
-    (void)host_info;
     // pivots -> reference Pivots structure: (tile index relative to k, offset)
+    std::vector<int64_t> ip(size_t(std::max<int64_t>(kt, 1)) * nb, 0);
+    if (pivot) {
+        if (target == Target::Devices) {
+            hipStream_t s1 = S.ctx(1).stream;
+            device::memcpy_async(ip.data(), ipiv_all.data(), ip.size() * sizeof(int64_t), s1);
+            slate_hip_call(hipStreamSynchronize(s1));
+        } else {
+            std::copy(ipiv_all.data(), ipiv_all.data() + ip.size(), ip.begin());
+        }
+    }
     pivots.assign(kt, {});
     for (int64_t k = 0; k < kt; ++k) {
         int64_t kk = grow_of(A, k), kd = std::min(A.tileNb(k), m - kk);
         pivots[k].resize(kd);
         for (int64_t t = 0; t < kd; ++t) {
-            int64_t r = ipiv_all[kk + t];
+            int64_t r = pivot ? ip[k * nb + t] + kk : kk + t;
             // tile index relative to k and offset within the tile
             int64_t ti = 0;
             while (ti + k + 1 < mt && grow_of(A, k + ti + 1) <= r) ++ti;

@@ -891,6 +891,7 @@ SLATE_LB_INST(float)
 SLATE_LB_INST(double)
 SLATE_LB_INST(std::complex<float>)
 SLATE_LB_INST(std::complex<double>)
+template void copy2d<int64_t>(Ctx const&, int64_t, int64_t, int64_t const*, int64_t, int64_t*, int64_t);
 
 #define SLATE_LB_COPY(Ts, Td) \
     template void copy<Ts, Td>(Ctx const&, Uplo, Op, int64_t, int64_t, Ts const*, int64_t, Td*, int64_t);

@@ -1,0 +1,104 @@
+// Host / device dispatch of the distributed LU row-permutation helpers
+// (device kernels: kernels/lu_dist.hip; see there for the slot scheme).
+#include "lu_dist.hh"
+
+#include <cstring>
+#include <vector>
+
+namespace slate {
+namespace internal {
+namespace ludist {
+
+namespace kd = slate_amd::dev;
+using kd::dptr;
+
+template <typename T>
+void gather_rows_ids(lb::Ctx const& c, int64_t cnt, int64_t ncols, int64_t const* sel, T const* A, int64_t lda,
+                     T* out, int64_t ldo, int64_t const* id_in, int64_t* id_out, RowDist const& d, int64_t li_base) {
+    if (cnt <= 0) return;
+    if (c.dev()) {
+        kd::gather_rows_ids(cnt, ncols, sel, dptr(A), lda, dptr(out), ldo, id_in, id_out, d, li_base, c.stream);
+        return;
+    }
+    for (int64_t i = 0; i < cnt; ++i) {
+        if (id_out) id_out[i] = id_in ? id_in[sel[i]] : kd::rd_l2g(d, li_base + sel[i]);
+        for (int64_t j = 0; j < ncols; ++j) out[i + j * ldo] = A[sel[i] + j * lda];
+    }
+}
+
+void perm_slots(lb::Ctx const& c, int mode, int64_t base, int cnt, int64_t const* in, int64_t in_off,
+                int64_t* ipiv_out, int64_t* slot_src, int64_t* slot_dst) {
+    if (cnt <= 0) return;
+    slate_error_if_msg(cnt > 1024, "distributed LU: tile size above 1024");
+    if (c.dev()) {
+        kd::perm_slots(mode, base, cnt, in, in_off, ipiv_out, slot_src, slot_dst, c.stream);
+        return;
+    }
+    // same replay as the kernel (slot table: pos[s], content[s])
+    std::vector<int64_t> pos(2 * cnt);
+    std::vector<int> content(2 * cnt);
+    int n = cnt;
+    for (int s = 0; s < cnt; ++s) { pos[s] = base + s; content[s] = s; }
+    for (int t = 0; t < cnt; ++t) {
+        int64_t key = in[t] + in_off;
+        int f = -1;
+        for (int s = 0; s < n && f < 0; ++s)
+            if (mode == 0 ? pos[content[s]] == key : pos[s] == key) f = s;
+        if (f < 0) { f = n++; pos[f] = key; content[f] = f; }
+        ipiv_out[t] = pos[f];
+        std::swap(content[t], content[f]);
+    }
+    for (int s = 0; s < 2 * cnt; ++s) {
+        slot_src[s] = s < n ? pos[content[s]] : -1;
+        slot_dst[s] = s < n ? pos[s] : -1;
+    }
+}
+
+template <typename T>
+void slots_pack(lb::Ctx const& c, int s0, int s1, int64_t ncols, int64_t const* slot_src, T const* A, int64_t lda,
+                RowDist const& d, T* buf, int64_t ldb) {
+    if (s1 <= s0 || ncols <= 0) return;
+    if (c.dev()) {
+        kd::slots_pack(s0, s1, ncols, slot_src, dptr(A), lda, d, dptr(buf), ldb, c.stream);
+        return;
+    }
+    for (int s = s0; s < s1; ++s) {
+        int64_t src = slot_src[s];
+        bool mine = src >= 0 && kd::rd_owner(d, src) == d.myrow;
+        int64_t lr = mine ? kd::rd_lrow(d, src) : 0;
+        for (int64_t j = 0; j < ncols; ++j) buf[(s - s0) + j * ldb] = mine ? A[lr + j * lda] : T(0);
+    }
+}
+
+template <typename T>
+void slots_unpack(lb::Ctx const& c, int s0, int s1, int64_t ncols, int64_t const* slot_dst, T const* buf,
+                  int64_t ldb, T* A, int64_t lda, RowDist const& d) {
+    if (s1 <= s0 || ncols <= 0) return;
+    if (c.dev()) {
+        kd::slots_unpack(s0, s1, ncols, slot_dst, dptr(buf), ldb, dptr(A), lda, d, c.stream);
+        return;
+    }
+    for (int s = s0; s < s1; ++s) {
+        int64_t dst = slot_dst[s];
+        if (dst < 0 || kd::rd_owner(d, dst) != d.myrow) continue;
+        int64_t lr = kd::rd_lrow(d, dst);
+        for (int64_t j = 0; j < ncols; ++j) A[lr + j * lda] = buf[(s - s0) + j * ldb];
+    }
+}
+
+#define SLATE_LUDIST_INST(T)                                                                                    \
+    template void gather_rows_ids<T>(lb::Ctx const&, int64_t, int64_t, int64_t const*, T const*, int64_t, T*,  \
+                                     int64_t, int64_t const*, int64_t*, RowDist const&, int64_t);              \
+    template void slots_pack<T>(lb::Ctx const&, int, int, int64_t, int64_t const*, T const*, int64_t,          \
+                                RowDist const&, T*, int64_t);                                                  \
+    template void slots_unpack<T>(lb::Ctx const&, int, int, int64_t, int64_t const*, T const*, int64_t, T*,    \
+                                  int64_t, RowDist const&);
+
+SLATE_LUDIST_INST(float)
+SLATE_LUDIST_INST(double)
+SLATE_LUDIST_INST(std::complex<float>)
+SLATE_LUDIST_INST(std::complex<double>)
+
+}  // namespace ludist
+}  // namespace internal
+}  // namespace slate

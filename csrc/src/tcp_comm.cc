@@ -77,14 +77,35 @@ std::string env_str(const char* name, const char* dflt) {
     return e && *e ? std::string(e) : std::string(dflt);
 }
 
-int listen_on(int port, int& bound_port) {
+/// True when every rank reaches the master over loopback (single-node jobs
+/// launched with MASTER_ADDR=127.0.0.1 / localhost): the listeners are then
+/// bound to 127.0.0.1 only instead of every interface.
+bool loopback_job(std::string const& master) {
+    return master == "localhost" || master.rfind("127.", 0) == 0;
+}
+
+/// Per-job handshake token: SLATE_JOB_TOKEN if set, else a hash of the
+/// launcher environment every rank of the job shares (torchrun run id,
+/// master address/port, world size).  Peers presenting another token are
+/// rejected, so a stray connection cannot pose as a rank of this job.
+uint64_t job_token() {
+    std::string k = env_str("SLATE_JOB_TOKEN", "");
+    if (k.empty())
+        k = env_str("TORCHELASTIC_RUN_ID", "") + "|" + env_str("MASTER_ADDR", "127.0.0.1") + "|" +
+            env_str("MASTER_PORT", "") + "|" + env_str("SLATE_MASTER_PORT", "") + "|" + env_str("WORLD_SIZE", "1");
+    uint64_t h = 1469598103934665603ull;   // FNV-1a
+    for (unsigned char c : k) { h ^= c; h *= 1099511628211ull; }
+    return h;
+}
+
+int listen_on(int port, int& bound_port, bool loopback) {
     int fd = ::socket(AF_INET, SOCK_STREAM, 0);
     if (fd < 0) sys_fail("socket");
     int one = 1;
     ::setsockopt(fd, SOL_SOCKET, SO_REUSEADDR, &one, sizeof(one));
     sockaddr_in a{};
     a.sin_family = AF_INET;
-    a.sin_addr.s_addr = htonl(INADDR_ANY);
+    a.sin_addr.s_addr = htonl(loopback ? INADDR_LOOPBACK : INADDR_ANY);
     a.sin_port = htons(uint16_t(port));
     if (::bind(fd, reinterpret_cast<sockaddr*>(&a), sizeof(a)) < 0) sys_fail("bind port " + std::to_string(port));
     if (::listen(fd, 256) < 0) sys_fail("listen");
@@ -140,26 +161,34 @@ public:
     void connect_mesh(std::string const& master, int master_port, double timeout_s) {
         if (size_ == 1) return;
         int my_port = 0;
-        int lfd = listen_on(0, my_port);
+        const bool lo = loopback_job(master);
+        const uint64_t token = job_token();
+        int lfd = listen_on(0, my_port, lo);
         // rendezvous at rank 0: gather (ip, port) of every rank, broadcast table
         std::vector<uint32_t> ips(size_, 0);
         std::vector<int32_t> ports(size_, 0);
         if (rank_ == 0) {
             int rport = 0;
-            int rfd = listen_on(master_port, rport);
+            int rfd = listen_on(master_port, rport, lo);
             ports[0] = my_port;
             ips[0] = 0;  // peers reach rank 0 through `master`
             std::vector<int> fds;
-            for (int n = 1; n < size_; ++n) {
+            std::vector<char> seen(size_, 0);
+            while (int(fds.size()) < size_ - 1) {
                 sockaddr_in a{};
                 socklen_t len = sizeof(a);
                 int fd = ::accept(rfd, reinterpret_cast<sockaddr*>(&a), &len);
                 if (fd < 0) sys_fail("accept (rendezvous)");
-                int32_t hdr[2];
-                if (!read_all(fd, hdr, sizeof(hdr))) sys_fail("rendezvous read");
-                slate_error_if_msg(hdr[0] <= 0 || hdr[0] >= size_, "tcp rendezvous: bad rank");
-                ips[hdr[0]] = a.sin_addr.s_addr;
-                ports[hdr[0]] = hdr[1];
+                Hello h{};
+                // wrong token, bad or duplicate rank: drop the connection
+                if (!read_all(fd, &h, sizeof(h)) || h.token != token || h.rank <= 0 || h.rank >= size_ ||
+                    seen[h.rank]) {
+                    ::close(fd);
+                    continue;
+                }
+                seen[h.rank] = 1;
+                ips[h.rank] = a.sin_addr.s_addr;
+                ports[h.rank] = h.port;
                 fds.push_back(fd);
             }
             for (int fd : fds) {
@@ -170,8 +199,8 @@ public:
             ::close(rfd);
         } else {
             int fd = connect_to(master, master_port, timeout_s);
-            int32_t hdr[2] = {rank_, my_port};
-            write_all(fd, hdr, sizeof(hdr));
+            Hello h{token, rank_, my_port};
+            write_all(fd, &h, sizeof(h));
             if (!read_all(fd, ips.data(), ips.size() * sizeof(uint32_t)) ||
                 !read_all(fd, ports.data(), ports.size() * sizeof(int32_t)))
                 sys_fail("rendezvous table");
@@ -187,19 +216,23 @@ public:
                 host = ::inet_ntop(AF_INET, &ia, buf, sizeof(buf));
             }
             int fd = connect_to(host, ports[j], timeout_s);
-            int32_t me = rank_;
-            write_all(fd, &me, sizeof(me));
+            Hello h{token, rank_, 0};
+            write_all(fd, &h, sizeof(h));
             peers_[j].fd = fd;
         }
-        for (int n = rank_ + 1; n < size_; ++n) {
+        for (int n = rank_ + 1; n < size_;) {
             int fd = ::accept(lfd, nullptr, nullptr);
             if (fd < 0) sys_fail("accept (mesh)");
             int one = 1;
             ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
-            int32_t who = -1;
-            if (!read_all(fd, &who, sizeof(who))) sys_fail("mesh handshake");
-            slate_error_if_msg(who <= rank_ || who >= size_, "tcp mesh: bad peer rank");
-            peers_[who].fd = fd;
+            Hello h{};
+            if (!read_all(fd, &h, sizeof(h)) || h.token != token || h.rank <= rank_ || h.rank >= size_ ||
+                peers_[h.rank].fd >= 0) {
+                ::close(fd);   // not a peer of this job (or a duplicate rank)
+                continue;
+            }
+            peers_[h.rank].fd = fd;
+            ++n;
         }
         ::close(lfd);
         for (int j = 0; j < size_; ++j)
@@ -245,6 +278,12 @@ public:
     }
 
 private:
+    /// Rendezvous / mesh handshake: job token, sender rank, listening port.
+    struct Hello {
+        uint64_t token;
+        int32_t rank;
+        int32_t port;
+    };
     struct Peer {
         int fd = -1;
         std::thread th;

@@ -77,6 +77,40 @@ def case_getrf(tg, dt, nb):
         assert relerr(a @ s.to_numpy(B), b) < 100 * tol(dt), method
 
 
+def ipiv_of(piv, nb):
+    """Reference Pivots (per block column k: (tile index rel. to k, offset)) ->
+    LAPACK-style 0-based sequential interchanges."""
+    return [(k + ti) * nb + off for k, blk in enumerate(piv) for (ti, off) in blk]
+
+
+def case_getrf_shapes(tg, dt, nb):
+    """Distributed LU on tall / wide / square shapes, lookahead 1 and 2, every
+    pivoting method: P A = L U reconstructed from the returned factors and
+    pivots (covers the cross-rank tournament tree, the gathered PPLU panel and
+    the device-side row-permutation slots, including left-column swaps)."""
+    for (m, n) in ((190, 190), (230, 120), (120, 200)):
+        a = rnd(m, n, dt, 21 + m + n)
+        if m == n:
+            a_np = (a + 4 * n * np.eye(n)).astype(dt)   # no-pivoting case needs a safe diagonal
+        for method, mlu in (("ppiv", 1), ("tntpiv", 2), ("nopiv", 3)):
+            if method == "nopiv" and m != n:
+                continue
+            src = a_np if method == "nopiv" else a
+            for la in (1, 2):
+                A = s.from_numpy(src, nb=nb, target=tg)
+                info, piv = s.getrf(A, target=tg, method_lu=mlu, lookahead=la)
+                assert info == 0, (method, m, n, info)
+                f = s.to_numpy(A)
+                k = min(m, n)
+                Lf = np.tril(f[:, :k], -1) + np.eye(m, k, dtype=dt)
+                Uf = np.triu(f[:k, :])
+                pa = src.copy()
+                for i, r in enumerate(ipiv_of(piv, nb) if method != "nopiv" else range(k)):
+                    if r != i:
+                        pa[[i, r]] = pa[[r, i]]
+                assert relerr(Lf @ Uf, pa) < 100 * tol(dt), (method, m, n, la)
+
+
 def case_geqrf(tg, dt, nb):
     m, n = 230, 120
     a = rnd(m, n, dt, 11)
