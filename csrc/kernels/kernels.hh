@@ -61,6 +61,12 @@ template <typename T>
 void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const T* buf, int64_t ldb, T* A,
                   int64_t lda, RowDist d, hipStream_t s);
 
+// ---- TSQR Householder reconstruction (tsqr.hip): narrow block (nn <= 32) of
+// the sign-modified LU without pivoting, rows [r, m), columns [r, r+nn) of A;
+// Utop = copy of the nn x nn top block (ld 32); sgn[r+j] receives s_j.
+template <typename T>
+void lu_sign_narrow(int64_t m, int64_t r, int nn, T* A, int64_t lda, const T* Utop, T* sgn, hipStream_t s);
+
 // ---- GEMM (gemm_mfma.hip: real MFMA; gemm_cplx.hip: complex)
 template <typename T>
 void gemm_real(char transA, char transB, int64_t m, int64_t n, int64_t k,

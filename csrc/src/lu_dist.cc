@@ -3,6 +3,7 @@
 #include "lu_dist.hh"
 
 #include <cstring>
+#include <functional>
 #include <vector>
 
 namespace slate {
@@ -86,13 +87,62 @@ void slots_unpack(lb::Ctx const& c, int s0, int s1, int64_t ncols, int64_t const
     }
 }
 
+namespace {
+template <typename T> T unit_phase(T b) {
+    if constexpr (is_complex_v<T>) {
+        auto a = std::abs(b);
+        return a == 0 ? T(1) : b / a;
+    } else {
+        return b < T(0) ? T(-1) : T(1);
+    }
+}
+}  // namespace
+
+template <typename T>
+void lu_sign(lb::Ctx const& c, int64_t n, T* A, int64_t lda, T* sgn) {
+    if (n <= 0) return;
+    if (!c.dev()) {
+        for (int64_t k = 0; k < n; ++k) {
+            T s = unit_phase(A[k + k * lda]);
+            A[k + k * lda] += s;
+            sgn[k] = s;
+            T d = A[k + k * lda];
+            for (int64_t i = k + 1; i < n; ++i) A[i + k * lda] /= d;
+            for (int64_t j = k + 1; j < n; ++j) {
+                T u = A[k + j * lda];
+                for (int64_t i = k + 1; i < n; ++i) A[i + j * lda] -= A[i + k * lda] * u;
+            }
+        }
+        return;
+    }
+    // right-looking recursion over 32-column narrow blocks (tsqr.hip)
+    lb::Scratch sc(c);
+    T* Utop = sc.alloc<T>(32 * 32);
+    std::function<void(int64_t, int64_t)> rec = [&](int64_t c0, int64_t nn) {
+        if (nn <= 32) {
+            lb::copy2d(c, nn, nn, A + c0 + c0 * lda, lda, Utop, int64_t(32));
+            kd::lu_sign_narrow(n, c0, int(nn), dptr(A), lda, dptr(Utop), dptr(sgn), c.stream);
+            return;
+        }
+        int64_t n1 = ((nn + 1) / 2 + 31) / 32 * 32, n2 = nn - n1;
+        rec(c0, n1);
+        lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, n1, n2, T(1), A + c0 + c0 * lda, lda,
+                 A + c0 + (c0 + n1) * lda, lda);
+        lb::gemm(c, Op::NoTrans, Op::NoTrans, n - c0 - n1, n2, n1, T(-1), A + (c0 + n1) + c0 * lda, lda,
+                 A + c0 + (c0 + n1) * lda, lda, T(1), A + (c0 + n1) + (c0 + n1) * lda, lda);
+        rec(c0 + n1, n2);
+    };
+    rec(0, n);
+}
+
 #define SLATE_LUDIST_INST(T)                                                                                    \
     template void gather_rows_ids<T>(lb::Ctx const&, int64_t, int64_t, int64_t const*, T const*, int64_t, T*,  \
                                      int64_t, int64_t const*, int64_t*, RowDist const&, int64_t);              \
     template void slots_pack<T>(lb::Ctx const&, int, int, int64_t, int64_t const*, T const*, int64_t,          \
                                 RowDist const&, T*, int64_t);                                                  \
     template void slots_unpack<T>(lb::Ctx const&, int, int, int64_t, int64_t const*, T const*, int64_t, T*,    \
-                                  int64_t, RowDist const&);
+                                  int64_t, RowDist const&);                                                    \
+    template void lu_sign<T>(lb::Ctx const&, int64_t, T*, int64_t, T*);
 
 SLATE_LUDIST_INST(float)
 SLATE_LUDIST_INST(double)

@@ -41,6 +41,12 @@ template <typename T>
 void slots_unpack(lb::Ctx const& c, int s0, int s1, int64_t ncols, int64_t const* slot_dst, T const* buf,
                   int64_t ldb, T* A, int64_t lda, RowDist const& d);
 
+/// Sign-modified LU without pivoting of the n x n block A (TSQR Householder
+/// reconstruction): for each column j the diagonal b gets s_j = b/|b| added
+/// (|pivot| = 1 + |b|); Y (unit lower) and U' overwrite A, sgn[j] = s_j.
+template <typename T>
+void lu_sign(lb::Ctx const& c, int64_t n, T* A, int64_t lda, T* sgn);
+
 }  // namespace ludist
 }  // namespace internal
 }  // namespace slate

@@ -16,6 +16,7 @@
 // T factors: T[0] is an nb x n matrix replicated on every rank (tile k holds
 // the panel's nb x nb upper-triangular T).
 #include "internal.hh"
+#include "lu_dist.hh"
 
 #include <cstdlib>
 
@@ -39,7 +40,7 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
     auto& g = *A.grid();
     const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
     const Loc loc = loc_of(target);
-    const int64_t mt = A.mt(), nt = A.nt(), m = A.m(), n = A.n();
+    const int64_t mt = A.mt(), nt = A.nt(), m = A.m();
     const int64_t kt = std::min(mt, nt);
     const int64_t nb = A.nb();
     LocalBlock<T> L = A.local(loc, true);
@@ -48,6 +49,7 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
     LocalBlock<T> LT = Tf.local(loc, true);   // replicated nb x n
     T* tm = LT.ptr;
     const int64_t ldt = LT.ld;
+    const int qC = device::kCommQueue, qP = 1;
 
     Sched S(target);
     const int R = int(std::max<int64_t>(2, la + 2));
@@ -59,7 +61,21 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         WW2[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         Wtau[r].resize(target, size_t(nb));
     }
-    Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+    // TSQR scratch (p > 1): local T, current / received R, E blocks of the
+    // explicit Q, per-level stacked factors, local Q rows, the sign-modified LU
+    const int maxr = 8;   // tree levels (p <= 256)
+    Work<T> Tloc, Rcur, Rrecv, Ecur, Etmp, Qloc, LUb, Ytmp, Dg, Tw, sgn, taul;
+    std::vector<Work<T>> Sst(p > 1 ? maxr : 0), Ttt(p > 1 ? maxr : 0);
+    if (p > 1) {
+        const size_t nn = size_t(nb) * nb;
+        Tloc.resize(target, nn); Rcur.resize(target, nn); Rrecv.resize(target, nn);
+        Ecur.resize(target, 2 * nn); Etmp.resize(target, 2 * nn); LUb.resize(target, nn); Ytmp.resize(target, nn);
+        Dg.resize(target, nn); Tw.resize(target, nn); sgn.resize(target, nb); taul.resize(target, 2 * nb);
+        Qloc.resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+        for (int r = 0; r < maxr; ++r) { Sst[r].resize(target, 2 * nn); Ttt[r].resize(target, nn); }
+    }
+    const int64_t tSel = Sched::tok(30, 0);
+    const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
 
     for (int64_t k = 0; k < kt; ++k) {
         const int64_t kb = A.tileNb(k);
@@ -67,101 +83,206 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         const int64_t M = m - kk;
         const int64_t kd = std::min(kb, M);
         const int pk = A.srow_owner(k), qk = A.scol_owner(k);
-        const bool in_col = (mycol == qk);
+        const bool in_col = (mycol == qk), diag = (myrow == pk);
         const int64_t lr_k = lrow_of(A, k);
         const int64_t lc_k = in_col ? lcol_of(A, k) : 0;
         const int64_t mr = mloc - lr_k;          // my rows >= kk
         const int slot = int(k % R);
         T* Tk = WT[slot].data();
         T* tau = Wtau[slot].data();
+        T* ap = a + lr_k + lc_k * lda;
         const int64_t tP = Sched::tok(6, slot), tB = Sched::bcast(slot);
 
-        // ---------------------------------------------------------- panel
-        if (in_col) {
-            int qq = (p == 1) ? 1 : device::kCommQueue;
-            S.task(qq, {}, {Sched::col(k), tP}, [&, k, kb, kk, M, kd, lr_k, lc_k, mr, pk, Tk, tau](lb::Ctx const& c) {
+        // ================================================================ panel
+        if (in_col && p == 1) {
+            S.task(qP, {}, {Sched::col(k), tP}, [&, kb, M, Tk, tau, ap](lb::Ctx const& c) {
                 trace::Block t2("geqrf_panel");
-                T* ap = a + lr_k + lc_k * lda;
-                if (p == 1) {
-                    lb::geqrf_panel(c, M, kb, ap, lda, tau, Tk, kb);
-                    return;
-                }
-                // gather rows >= kk of the panel to pk, factor, scatter back
-                std::vector<int64_t> cnt(p, 0);
-                for (int64_t i = k; i < mt; ++i) cnt[A.srow_owner(i)] += A.tileMb(i);
-                Work<T> full(target, size_t(std::max<int64_t>(M, 1)) * kb);
-                Work<T> mine(target, size_t(std::max<int64_t>(mr, 1)) * kb);
-                pack(c, mr, kb, ap, lda, mine.data());
-                std::vector<Work<T>> rb(p);
-                std::vector<Comm::P2P> ops;
-                if (myrow == pk) {
-                    for (int r = 0; r < p; ++r) if (r != pk && cnt[r]) {
-                        rb[r].resize(target, size_t(cnt[r]) * kb);
-                        ops.push_back({rb[r].data(), size_t(cnt[r] * kb), r, false});
-                    }
-                } else if (mr > 0) ops.push_back({mine.data(), size_t(mr * kb), pk, true});
-                g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                if (myrow == pk) {
-                    std::vector<int64_t> off(p, 0);
-                    for (int64_t i = k; i < mt; ++i) {
-                        int r = A.srow_owner(i); int64_t ib = A.tileMb(i);
-                        T* src = (r == pk) ? mine.data() + off[r] : rb[r].data() + off[r];
-                        int64_t lds = (r == pk) ? std::max<int64_t>(mr, 1) : cnt[r];
-                        lb::copy2d(c, ib, kb, src, lds, full.data() + (grow_of(A, i) - kk), std::max<int64_t>(M, 1));
-                        off[r] += ib;
-                    }
-                    lb::geqrf_panel(c, M, kb, full.data(), std::max<int64_t>(M, 1), tau, Tk, kb);
-                    std::fill(off.begin(), off.end(), 0);
-                    for (int64_t i = k; i < mt; ++i) {
-                        int r = A.srow_owner(i); int64_t ib = A.tileMb(i);
-                        T* dst = (r == pk) ? mine.data() + off[r] : rb[r].data() + off[r];
-                        int64_t ldd = (r == pk) ? std::max<int64_t>(mr, 1) : cnt[r];
-                        lb::copy2d(c, ib, kb, full.data() + (grow_of(A, i) - kk), std::max<int64_t>(M, 1), dst, ldd);
-                        off[r] += ib;
-                    }
-                }
-                ops.clear();
-                if (myrow == pk) {
-                    for (int r = 0; r < p; ++r) if (r != pk && cnt[r]) ops.push_back({rb[r].data(), size_t(cnt[r] * kb), r, true});
-                } else if (mr > 0) ops.push_back({mine.data(), size_t(mr * kb), pk, false});
-                g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                lb::copy2d(c, mr, kb, mine.data(), std::max<int64_t>(mr, 1), ap, lda);
-                if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+                lb::geqrf_panel(c, M, kb, ap, lda, tau, Tk, kb);
             });
+        } else if (in_col) {
+            // ---- TSQR over the process column (tree rooted at pk) + Householder
+            //      reconstruction of (V, T) (kernels/tsqr.hip)
+            std::vector<int64_t> rows_r(p, 0);
+            for (int64_t i = k; i < mt; ++i) rows_r[A.srow_owner(i)] += A.tileMb(i);
+            std::vector<int> part;
+            for (int d = 0; d < p; ++d) { int r = (pk + d) % p; if (rows_r[r] > 0) part.push_back(r); }
+            const int np = int(part.size());
+            std::vector<int64_t> cnt(np);
+            for (int i = 0; i < np; ++i) cnt[i] = std::min(rows_r[part[i]], kb);
+            int ix = -1;
+            for (int i = 0; i < np; ++i) if (part[i] == myrow) ix = i;
+            struct Round { bool recv; int peer; int64_t mine, theirs; int level; };
+            std::vector<Round> rounds;
+            int lev = 0;
+            for (int l = 1; l < np; l *= 2, ++lev) {
+                for (int i = 0; i + l < np; i += 2 * l) {
+                    if (i == ix) rounds.push_back({true, part[i + l], cnt[i], cnt[i + l], lev});
+                    if (i + l == ix) rounds.push_back({false, part[i], cnt[i + l], 0, lev});
+                    cnt[i] = std::min(cnt[i] + cnt[i + l], kb);
+                }
+            }
+            slate_error_if_msg(lev > maxr, "geqrf: process grid too tall for the TSQR tree");
+            const int64_t rr = std::min(mr, kb);     // rows of my local R
+            if (ix >= 0) {
+                // (a) local QR of my panel rows; R -> Rcur (rr x kb, ld rr, zeros below)
+                S.task(qP, {Sched::col(k)}, {Sched::col(k), tSel}, [&, ap, mr, kb, rr](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_local");
+                    lb::geqrf_panel(c, mr, kb, ap, lda, taul.data(), Tloc.data(), nb);
+                    lb::set(c, Uplo::General, rr, kb, T(0), T(0), Rcur.data(), rr);
+                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, rr, kb, ap, lda, Rcur.data(), rr);
+                });
+                // (b) reduction tree: QR of the stacked [R_a; R_b], factors kept per level
+                int64_t cur = rr;
+                int nrecv = 0;
+                for (auto const& r_ : rounds) {
+                    if (!r_.recv) {
+                        S.task(qC, {tSel}, {tSel}, [&, r_, kb](lb::Ctx const& c) {
+                            trace::Block t2("geqrf_tsqr_sendR");
+                            std::vector<Comm::P2P> ops{{Rcur.data(), size_t(r_.mine * kb), r_.peer, true}};
+                            g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                        });
+                        break;
+                    }
+                    const int64_t ms = r_.mine + r_.theirs, c2 = std::min(ms, kb);
+                    S.task(qC, {}, {tSel}, [&, r_, kb](lb::Ctx const& c) {
+                        trace::Block t2("geqrf_tsqr_recvR");
+                        std::vector<Comm::P2P> ops{{Rrecv.data(), size_t(r_.theirs * kb), r_.peer, false}};
+                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                    });
+                    T* Sb = Sst[r_.level].data();
+                    T* Tt = Ttt[r_.level].data();
+                    S.task(qP, {}, {tSel}, [&, r_, kb, ms, c2, Sb, Tt](lb::Ctx const& c) {
+                        trace::Block t2("geqrf_tsqr_merge");
+                        lb::copy2d(c, r_.mine, kb, Rcur.data(), r_.mine, Sb, ms);
+                        lb::copy2d(c, r_.theirs, kb, Rrecv.data(), r_.theirs, Sb + r_.mine, ms);
+                        lb::geqrf_panel(c, ms, kb, Sb, ms, taul.data(), Tt, nb);
+                        lb::set(c, Uplo::General, c2, kb, T(0), T(0), Rcur.data(), c2);
+                        lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, c2, kb, Sb, ms, Rcur.data(), c2);
+                    });
+                    cur = c2;
+                    ++nrecv;
+                }
+                // (c) explicit Q (first kd columns), top-down: E = [I; 0] at the root
+                const bool sender = !rounds.empty() && !rounds.back().recv;
+                int64_t ecnt = 0;                  // rows of my current E block (ld ecnt)
+                if (diag) {
+                    S.task(qP, {}, {tSel}, [&, cur, kd](lb::Ctx const& c) {
+                        lb::set(c, Uplo::General, cur, kd, T(0), T(1), Ecur.data(), cur);
+                    });
+                    ecnt = cur;
+                } else if (sender) {
+                    auto const r_ = rounds.back();
+                    S.task(qC, {}, {tSel}, [&, r_, kd](lb::Ctx const& c) {
+                        trace::Block t2("geqrf_tsqr_recvE");
+                        std::vector<Comm::P2P> ops{{Ecur.data(), size_t(r_.mine * kd), r_.peer, false}};
+                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                    });
+                    ecnt = r_.mine;
+                }
+                for (int t = nrecv - 1; t >= 0; --t) {
+                    auto const r_ = rounds[t];
+                    const int64_t ms = r_.mine + r_.theirs, c2 = std::min(ms, kb);
+                    T* Sb = Sst[r_.level].data();
+                    T* Tt = Ttt[r_.level].data();
+                    // E (c2 x kd) -> [E; 0] (ms x kd) -> Q_level [E; 0]
+                    S.task(qP, {}, {tSel}, [&, ms, c2, kd, Sb, Tt](lb::Ctx const& c) {
+                        trace::Block t2("geqrf_tsqr_qtree");
+                        lb::set(c, Uplo::General, ms, kd, T(0), T(0), Etmp.data(), ms);
+                        lb::copy2d(c, c2, kd, Ecur.data(), c2, Etmp.data(), ms);
+                        lb::larfb(c, Side::Left, Op::NoTrans, ms, kd, c2, Sb, ms, Tt, nb, Etmp.data(), ms);
+                    });
+                    // partner's rows go down the tree, mine stay (compacted to ld = mine)
+                    S.task(qC, {}, {tSel}, [&, r_, ms, kd](lb::Ctx const& c) {
+                        trace::Block t2("geqrf_tsqr_sendE");
+                        lb::copy2d(c, r_.theirs, kd, Etmp.data() + r_.mine, ms, Rrecv.data(), r_.theirs);
+                        std::vector<Comm::P2P> ops{{Rrecv.data(), size_t(r_.theirs * kd), r_.peer, true}};
+                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                    });
+                    S.task(qP, {}, {tSel}, [&, r_, ms, kd](lb::Ctx const& c) {
+                        lb::copy2d(c, r_.mine, kd, Etmp.data(), ms, Ecur.data(), r_.mine);
+                    });
+                    ecnt = r_.mine;
+                }
+                // (d) local rows of Q: Qloc = Q_local [E; 0]  (mr x kd)
+                S.task(qP, {tSel}, {tSel}, [&, ap, mr, rr, kd, ecnt](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_qlocal");
+                    lb::set(c, Uplo::General, mr, kd, T(0), T(0), Qloc.data(), mr);
+                    lb::copy2d(c, ecnt, kd, Ecur.data(), ecnt, Qloc.data(), mr);
+                    lb::larfb(c, Side::Left, Op::NoTrans, mr, kd, rr, ap, lda, Tloc.data(), nb, Qloc.data(), mr);
+                });
+            }
+            // (e) pk: sign-modified LU of [S - Q11]  ->  Y1, U', S
+            if (diag) {
+                S.task(qP, {tSel}, {tSel}, [&, mr, kd](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_hr_lu");
+                    lb::add(c, Uplo::General, kd, kd, T(-1), Qloc.data(), mr, T(0), LUb.data(), kd);
+                    internal::ludist::lu_sign(c, kd, LUb.data(), kd, sgn.data());
+                });
+            }
+            S.task(qC, {}, {tSel}, [&, kd, pk](lb::Ctx const& c) {
+                trace::Block t2("geqrf_tsqr_bcast_lu");
+                bcast(g.col(), LUb.data(), size_t(kd * kd), pk, c);
+                bcast(g.col(), sgn.data(), size_t(kd), pk, c);
+            });
+            // (f) V below T: Y2 = -Q21 U'^{-1}, written into the panel rows
+            const int64_t off = diag ? kd : 0, nbelow = std::max<int64_t>(mr - off, 0);
+            S.task(qP, {tSel}, {Sched::col(k), tSel}, [&, ap, mr, kd, off, nbelow](lb::Ctx const& c) {
+                trace::Block t2("geqrf_tsqr_hr_v");
+                lb::trsm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, nbelow, kd, T(-1), LUb.data(), kd,
+                         Qloc.data() + off, std::max<int64_t>(mr, 1));
+                lb::copy2d(c, nbelow, kd, Qloc.data() + off, std::max<int64_t>(mr, 1), ap + off, lda);
+            });
+            // (g) pk: R = S R_tsqr and Y1 into the diagonal block; T = U' S^H Y1^{-H}
+            if (diag) {
+                S.task(qP, {tSel}, {Sched::col(k), tSel, tP}, [&, ap, kb, kd, Tk](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_hr_t");
+                    // Dg = diag(s)
+                    lb::set(c, Uplo::General, kd, kd, T(0), T(0), Dg.data(), kd);
+                    lb::copy2d(c, int64_t(1), kd, sgn.data(), int64_t(1), Dg.data(), kd + 1);
+                    // A(T rows) = S R_tsqr (upper trapezoid) + strictly-lower Y1
+                    lb::gemm(c, Op::NoTrans, Op::NoTrans, kd, kb, kd, T(1), Dg.data(), kd, Rcur.data(), kd, T(0), ap,
+                             lda);
+                    lb::copy2d(c, kd, kd, LUb.data(), kd, Ytmp.data(), kd);
+                    lb::set(c, Uplo::Upper, kd, kd, T(0), T(0), Ytmp.data(), kd);
+                    lb::add(c, Uplo::Lower, kd, kd, T(1), Ytmp.data(), kd, T(1), ap, lda);
+                    // T = triu(U') S^H Y1^{-H}, padded to kb x kb
+                    lb::set(c, Uplo::General, kd, kd, T(0), T(0), Tw.data(), kd);
+                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, kd, kd, LUb.data(), kd, Tw.data(), kd);
+                    lb::set(c, Uplo::General, kb, kb, T(0), T(0), Tk, kb);
+                    lb::gemm(c, Op::NoTrans, Op::ConjTrans, kd, kd, kd, T(1), Tw.data(), kd, Dg.data(), kd, T(0), Tk, kb);
+                    lb::trsm(c, Side::Right, Uplo::Lower, Op::ConjTrans, Diag::Unit, kd, kd, T(1), LUb.data(), kd, Tk, kb);
+                });
+            }
         }
-        // -------------------- broadcast T_k (world, from the diagonal owner) and V
+
+        // ======================= T_k down the panel column, then (V, T_k) along rows
         T* Vk = WV[slot].data();
         const int64_t ldv = std::max<int64_t>(mr, 1);
-        S.task(device::kCommQueue, {tP, Sched::col(k)}, {tB}, [&, k, kb, kk, kd, lr_k, lc_k, mr, pk, qk, Tk, Vk, ldv](lb::Ctx const& c) {
+        S.task(qC, {tP, Sched::col(k)}, {tB}, [&, kb, kk, lr_k, lc_k, mr, pk, qk, Tk, Vk, ldv, in_col, diag](lb::Ctx const& c) {
             trace::Block t2("geqrf_bcast");
-            int root = g.rank_of(pk, qk);
-            g.world().bcast(Tk, size_t(kb * kb), scalar_type<T>(), root, c.loc(), c.stream);
-            if (mycol == qk) {
+            if (in_col) {
+                if (p > 1) bcast(g.col(), Tk, size_t(kb * kb), pk, c);
                 // explicit V: my rows >= kk; the diagonal process row has the unit upper part
                 pack(c, mr, kb, a + lr_k + lc_k * lda, lda, Vk);
-                if (myrow == pk) lb::set(c, Uplo::Upper, std::min<int64_t>(kb, mr), kb, T(0), T(1), Vk, ldv);
+                if (diag) lb::set(c, Uplo::Upper, std::min<int64_t>(kb, mr), kb, T(0), T(1), Vk, ldv);
             }
-            if (q > 1) bcast(g.row(), Vk, size_t(mr * kb), qk, c);
+            if (q > 1) {
+                bcast(g.row(), Tk, size_t(kb * kb), qk, c);
+                bcast(g.row(), Vk, size_t(mr * kb), qk, c);
+            }
             // keep T_k in the replicated factor matrix
             lb::copy2d(c, kb, kb, Tk, kb, tm + kk * ldt, ldt);
         });
 
-        // ---------------------------------------------------------- update
+        // ============================================================ update
         T* Wk = WW[slot].data();
         T* W2k = WW2[slot].data();
-        auto update = [&, k, kb, lr_k, mr, Tk, Vk, ldv, Wk, W2k, cT](lb::Ctx const& c, int64_t j0, int64_t j1) {
-            int64_t c0 = lcol_of(A, j0), c1 = lcol_of(A, j1), nc = c1 - c0;
-            if (nc <= 0) return;
-            trace::Block t2("geqrf_update");
+        // W = V^H C  (kb x nc); on a wide trailing block the GEMM's K (= mr rows)
+        // is long, so K chunks of kch rows bound each workgroup's lifetime and
+        // the next panel's short kernels (high-priority stream) find free CUs.
+        auto vhc = [&, kb, lr_k, mr, Vk, ldv, Wk](lb::Ctx const& c, int64_t c0, int64_t nc) {
             T* Cc = a + lr_k + c0 * lda;
             T* W = Wk + c0 * kb;
-            T* W2 = W2k + c0 * kb;
-            // W = V^H C  (kb x nc), all-reduced over the process column
-            // On a wide trailing block this GEMM's K (= mr rows) is long, so
-            // without chunking each workgroup lives for milliseconds and the
-            // next panel's short kernels (high-priority stream) find no free
-            // CU until it drains.  K chunks of kch rows, accumulated in W,
-            // bound the workgroup lifetime.
             const int64_t kch = qr_kchunk();
             if (mr > 0 && kch > 0 && mr > kch && nc >= 4 * kb) {
                 for (int64_t r0 = 0; r0 < mr; r0 += kch)
@@ -169,21 +290,42 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
                              r0 ? T(1) : T(0), W, kb);
             } else if (mr > 0) lb::gemm(c, cT, Op::NoTrans, kb, nc, mr, T(1), Vk, ldv, Cc, lda, T(0), W, kb);
             else lb::set(c, Uplo::General, kb, nc, T(0), T(0), W, kb);
-            if (p > 1) g.col().allreduce(W, W, size_t(kb * nc), scalar_type<T>(), ReduceOp::Sum, c.loc(), c.stream);
-            lb::gemm(c, cT, Op::NoTrans, kb, nc, kb, T(1), Tk, kb, W, kb, T(0), W2, kb);
-            if (mr > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, nc, kb, T(-1), Vk, ldv, W2, kb, T(1), Cc, lda);
         };
-        auto range = [&](int queue, int64_t j0, int64_t j1) {
+        // C -= V (T^H W)
+        auto apply = [&, kb, lr_k, mr, Tk, Vk, ldv, Wk, W2k](lb::Ctx const& c, int64_t c0, int64_t nc) {
+            T* Cc = a + lr_k + c0 * lda;
+            lb::gemm(c, cT, Op::NoTrans, kb, nc, kb, T(1), Tk, kb, Wk + c0 * kb, kb, T(0), W2k + c0 * kb, kb);
+            if (mr > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, nc, kb, T(-1), Vk, ldv, W2k + c0 * kb, kb, T(1), Cc, lda);
+        };
+        auto range = [&, kb, Wk](int queue, int64_t j0, int64_t j1) {
+            const int64_t c0 = lcol_of(A, j0), nc = lcol_of(A, j1) - c0;
+            if (nc <= 0) return;
             std::vector<int64_t> cols;
             for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
-            // with p > 1 the update contains an all-reduce: keep it on the comm queue
-            int qq = (p == 1) ? queue : device::kCommQueue;
-            S.task(qq, {tB}, cols, [&, update, j0, j1](lb::Ctx const& c) { update(c, j0, j1); });
+            if (p == 1) {
+                S.task(queue, {tB}, cols, [&, c0, nc](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_update");
+                    vhc(c, c0, nc);
+                    apply(c, c0, nc);
+                });
+                return;
+            }
+            // p > 1: the column all-reduce of W runs on the comm queue between
+            // the two halves, which stay on the compute queue
+            S.task(queue, {tB}, cols, [&, c0, nc](lb::Ctx const& c) { trace::Block t2("geqrf_update_w"); vhc(c, c0, nc); });
+            S.task(qC, {}, cols, [&, c0, nc, kb, Wk](lb::Ctx const& c) {
+                trace::Block t2("geqrf_update_allreduce");
+                g.col().allreduce(Wk + c0 * kb, size_t(kb * nc), ReduceOp::Sum, c.loc(), c.stream);
+            });
+            S.task(queue, {tB}, cols, [&, c0, nc](lb::Ctx const& c) { trace::Block t2("geqrf_update_c"); apply(c, c0, nc); });
         };
-        int64_t jla_end = std::min(nt, k + 1 + la);
+        const int64_t jla_end = std::min(nt, k + 1 + la);
         for (int64_t j = k + 1; j < jla_end; ++j) range(device::kLookaheadQueue, j, j + 1);
-        if (jla_end < nt) range(device::kTrailQueue, jla_end, nt);
-        (void)kd;
+        if (jla_end < nt) {
+            const int64_t ntr = nt - jla_end, nch = (p == 1) ? 1 : std::min<int64_t>(4, ntr);
+            for (int64_t ch = 0; ch < nch; ++ch)
+                range(device::kTrailQueue, jla_end + ch * ntr / nch, jla_end + (ch + 1) * ntr / nch);
+        }
     }
     S.wait_all();
     A.storage()->update_origin();

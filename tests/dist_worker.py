@@ -123,6 +123,32 @@ def case_geqrf(tg, dt, nb):
     assert relerr(x, ref) < 100 * tol(dt)
 
 
+def case_geqrf_shapes(tg, dt, nb):
+    """Distributed QR (TSQR tree + Householder reconstruction on p > 1) on
+    tall / square / wide shapes, lookahead 1 and 2: Q^H A = R through unmqr,
+    |R| against numpy's, and Q (Q^H C) = C."""
+    for (m, n) in ((230, 120), (150, 150), (100, 170)):
+        a = rnd(m, n, dt, 31 + m + n)
+        c = rnd(m, 5, dt, 32 + m)
+        for la in (1, 2):
+            A = s.from_numpy(a, nb=nb, target=tg)
+            T = s.geqrf(A, target=tg, lookahead=la)
+            f = s.to_numpy(A)
+            k = min(m, n)
+            r = np.triu(f[:k, :])
+            rref = np.linalg.qr(a, mode="r")[:k, :]
+            assert relerr(np.abs(r), np.abs(rref)) < 100 * tol(dt), ("R", m, n, la)
+            Aq = s.from_numpy(a, nb=nb, target=tg)
+            s.unmqr(s.Side.Left, s.Op.ConjTrans, A, T, Aq, target=tg)
+            qa = s.to_numpy(Aq)
+            assert relerr(np.triu(qa[:k]), r) < 100 * tol(dt), ("QhA", m, n, la)
+            assert np.abs(qa[k:]).max() <= 100 * tol(dt) * np.abs(a).max() * m if m > k else True
+            C = s.from_numpy(c, nb=nb, target=tg)
+            s.unmqr(s.Side.Left, s.Op.ConjTrans, A, T, C, target=tg)
+            s.unmqr(s.Side.Left, s.Op.NoTrans, A, T, C, target=tg)
+            assert relerr(s.to_numpy(C), c) < 100 * tol(dt), ("QQh", m, n, la)
+
+
 def case_norm(tg, dt, nb):
     a = rnd(170, 110, dt, 13)
     A = s.from_numpy(a, nb=nb, target=tg)

@@ -12,7 +12,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 WORKER = os.path.join(HERE, "dist_worker.py")
-CASES = "gemm,herk,trsm,potrf,getrf,getrf_shapes,geqrf,norm,mixed"
+CASES = "gemm,herk,trsm,potrf,getrf,getrf_shapes,geqrf,geqrf_shapes,norm,mixed"
 
 
 def _free_port():
@@ -74,21 +74,23 @@ def test_rccl_multirank_one_gpu(nprocs, grid):
 
 
 @pytest.mark.parametrize("p,q", [(3, 1), (4, 1), (3, 2)])
-def test_dist_lu_deep_trees(p, q):
-    """Tournament trees with 2 levels and uneven process rows (p = 3, 4):
-    distributed CALU / PPLU / no-pivoting LU reconstructed as P A = L U."""
-    run_workers(p, q, "h", cases="getrf_shapes,getrf", dtypes="float64,complex128")
+def test_dist_lu_qr_deep_trees(p, q):
+    """Tournament / TSQR trees with 2 levels and uneven process rows (p = 3, 4):
+    distributed CALU / PPLU / no-pivoting LU reconstructed as P A = L U, and
+    TSQR + Householder-reconstruction QR checked through unmqr."""
+    run_workers(p, q, "h", cases="getrf_shapes,getrf,geqrf_shapes,geqrf", dtypes="float64,complex128")
 
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("nprocs,grid", [(2, "2x1"), (4, "2x2")])
-def test_rccl_lu_p_gt_1(nprocs, grid):
-    """Device-resident distributed LU over real RCCL (ranks sharing one GPU):
-    cross-rank tournament, device pivot slots + column all-reduce, lookahead
-    1 and 2, at sizes with many panels (residual checks of the tester)."""
+def test_rccl_lu_qr_p_gt_1(nprocs, grid):
+    """Device-resident distributed LU and QR over real RCCL (ranks sharing one
+    GPU): cross-rank tournament, device pivot slots + column all-reduce, TSQR
+    tree + Householder reconstruction, lookahead 1 and 2, at sizes with many
+    panels (residual checks of the tester)."""
     for la in ("1", "2"):
         r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), str(nprocs),
-                            "getrf,getrf_tntpiv,getrf_nopiv,gesv", "--type", "d,z", "--dim", "1000,1536",
+                            "getrf,getrf_tntpiv,getrf_nopiv,gesv,geqrf,gels,gelqf", "--type", "d,z", "--dim", "1000,1536",
                             "--nb", "128", "--grid", grid, "--target", "d", "--lookahead", la],
                            capture_output=True, text=True, timeout=900)
         assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]

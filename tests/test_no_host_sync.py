@@ -19,6 +19,7 @@ DRIVERS = [
     ("csrc/src/getrf.cc", "getrf_dist"),
     ("csrc/src/getrf.cc", "getrf_impl"),
     ("csrc/src/potrf.cc", "potrf_lower"),
+    ("csrc/src/qr.cc", "geqrf_impl"),
 ]
 
 
