@@ -66,6 +66,12 @@ void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const 
 // Utop = copy of the nn x nn top block (ld 32); sgn[r+j] receives s_j.
 template <typename T>
 void lu_sign_narrow(int64_t m, int64_t r, int nn, T* A, int64_t lda, const T* Utop, T* sgn, hipStream_t s);
+/// On-chip TSQR + Householder reconstruction of a narrow panel block: rows x nn
+/// (nn <= 32) at A -> V below the diagonal, R on/above, the nn x nn T at Tm,
+/// tau[0..nn).  work: qr_tsqr_workspace(rows) scalars.
+int64_t qr_tsqr_workspace(int64_t rows);
+template <typename T>
+void qr_tsqr_narrow(int64_t rows, int nn, T* A, int64_t lda, T* Tm, int64_t ldt, T* tau, T* work, hipStream_t s);
 
 // ---- GEMM (gemm_mfma.hip: real MFMA; gemm_cplx.hip: complex)
 template <typename T>

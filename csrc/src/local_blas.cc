@@ -587,6 +587,7 @@ struct QrPanelDev {
     T* Tm; int64_t ldt;
     Ctx ctx;
     real_type<T>* psum; T* alpha; T* pdots; T* work; int64_t work_elems; T* scal;
+    T* tsqr_work = nullptr;
 
     // narrow block [c0, c0+nn): Householder columns + T block (nn x nn at Tm[c0, c0])
     void narrow(int64_t c0, int64_t nn) {
@@ -594,6 +595,13 @@ struct QrPanelDev {
         DT* A = dptr(A0);
         int64_t kmax = std::min(nn, m - c0);
         if (kmax <= 0) return;
+        if (use_tsqr(c0, nn)) {
+            // on-chip TSQR tree + Householder reconstruction (tsqr.hip): about
+            // 2 log8(rows/256) + 4 launches per narrow block instead of two per column
+            kd::qr_tsqr_narrow<DT>(m - c0, int(nn), A + c0 + c0 * lda, lda, dptr(Tm + c0 + c0 * ldt), ldt,
+                                   dptr(tau + c0), dptr(tsqr_work), s);
+            return;
+        }
         if (use_persistent(c0)) {
             // one launch for the whole block, LDS-resident (qr_persistent.hip)
             Scratch sc(ctx);
@@ -613,6 +621,18 @@ struct QrPanelDev {
     // point), and slower still under a concurrent trailing GEMM, which delays
     // co-residency of the 128 workgroups.  Kept for panels that do fit one
     // XCD / for future fused variants.
+    // SLATE_QR_PANEL=columns selects the column-at-a-time path (A/B runs)
+    static bool tsqr_enabled() {
+        static int on = [] { const char* e = std::getenv("SLATE_QR_PANEL"); return !(e && (std::string(e) == "columns" || std::string(e) == "persistent")); }();
+        return on;
+    }
+    // (rows > nn: a square last block keeps the column path, whose last
+    // reflector is the identity exactly as in LAPACK, so R's sign convention
+    // matches the host path on every block)
+    // (real types: the complex node kernel does not fit its block in VGPRs)
+    bool use_tsqr(int64_t c0, int64_t nn) const {
+        return is_real_v<T> && tsqr_enabled() && m - c0 > nn && nn <= 32;
+    }
     static bool persistent_enabled() {
         static int on = [] { const char* e = std::getenv("SLATE_QR_PANEL"); return e && std::string(e) == "persistent"; }();
         return on;
@@ -705,6 +725,7 @@ void geqrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, T* tau, 
     P.scal = sc.alloc<T>(size_t(k) + 1);
     P.work_elems = int64_t(1) << 20;
     P.work = sc.alloc<T>(P.work_elems);
+    P.tsqr_work = sc.alloc<T>(size_t(kd::qr_tsqr_workspace(m)));
     // zero all of T (n x n when the panel is wider than tall: the driver's
     // block update multiplies by the full nb x nb T)
     int64_t nt_ = std::min(n, ldt);

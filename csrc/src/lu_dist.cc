@@ -90,8 +90,7 @@ void slots_unpack(lb::Ctx const& c, int s0, int s1, int64_t ncols, int64_t const
 namespace {
 template <typename T> T unit_phase(T b) {
     if constexpr (is_complex_v<T>) {
-        auto a = std::abs(b);
-        return a == 0 ? T(1) : b / a;
+        return T(std::real(b) < 0 ? -1 : 1);   // real +-1: R keeps a real diagonal (tsqr.hip)
     } else {
         return b < T(0) ? T(-1) : T(1);
     }
