@@ -34,7 +34,14 @@ from slate_d35_amd.utils import flops as F  # noqa: E402
 
 METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
 ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
-EXTRA = ["dgesv_mixed"]  # BASELINE config 5; run with --routines dgesv_mixed
+# BASELINE.json configs beyond the 4-routine headline suite (run after it,
+# reported under "configs"): name -> (routine, n or None = --dim, nb, target)
+EXTRAS = {
+    "cfg1_dgemm_host_n2048_nb256": ("dgemm", 2048, 256, "h"),
+    "cfg2_dpotrf_n32768_nb512": ("dpotrf", -2, 512, None),       # -2: half of --dim (32768 at the default)
+    "cfg4_dgeqrf_nb256": ("dgeqrf", None, 256, None),
+    "cfg5_dgesv_mixed": ("dgesv_mixed", None, None, None),
+}
 
 
 def parse():
@@ -51,6 +58,9 @@ def parse():
     ap.add_argument("--lookahead", type=int, default=1)
     ap.add_argument("--method-lu", default="tntpiv", choices=["ppiv", "tntpiv"])
     ap.add_argument("--trace", default="")
+    ap.add_argument("--extras", default="all", help="BASELINE configs to add after the suite: all, none, or names")
+    ap.add_argument("--check", default="yes", choices=["yes", "no"],
+                    help="backward-error check of each routine after its timed steps (outside the timed region)")
     return ap.parse_args()
 
 
@@ -94,80 +104,160 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    results = {}
-    routines = [r.strip() for r in a.routines.split(",") if r.strip()]
-    for rname in routines:
+    def residual(rname, mats, kind, seed, nb, n_, tg):
+        """Backward error of the result just computed (reference tester
+        formulas, test/test_gesv.cc:330-377, test_posv.cc:302-343):
+        ||b - A x|| / (||A|| ||x|| n eps) for the solves, and
+        ||C x - A (B x)|| / (||A|| ||B|| ||x|| n eps) for gemm."""
+        eps = np.finfo(np.float64).eps
+        tgt = s.target_of(tg)
+
+        def vec(seed_):
+            V = s.Matrix(n_, 1, nb, np.float64, grid)
+            V.insertLocalTiles(tgt)
+            s._slate.generate_matrix_d("rands", V, seed_, -1.0, s.opts(tg))
+            return V
+
+        def inf(M):
+            return s.norm(s.Norm.Inf, M, target=tg)
+
+        o = dict(target=tg)
+        if rname == "dgemm":
+            x = vec(901)
+            y1, t, y2 = vec(0), vec(0), vec(0)
+            s.gemm(1.0, mats["C"], x, 0.0, y1, **o)
+            s.gemm(1.0, mats["B"], x, 0.0, t, **o)
+            s.gemm(1.0, mats["A"], t, 0.0, y2, **o)
+            s.add(-1.0, y2, 1.0, y1, **o)
+            return inf(y1) / (inf(mats["A"]) * inf(mats["B"]) * inf(x) * n_ * eps)
+        # original matrix (the generator is deterministic), right-hand side b
+        A0 = s.Matrix(n_, n_, nb, np.float64, grid)
+        A0.insertLocalTiles(tgt)
+        s._slate.generate_matrix_d(kind, A0, seed, -1.0, s.opts(tg))
+        b = vec(902)
+        if rname == "dgesv_mixed":
+            X = mats["X"]
+            b = mats["B"]
+        else:
+            X = vec(902)
+            if rname == "dpotrf":
+                s.potrs(s.HermitianMatrix(s.Uplo.Lower, mats["A"]), X, **o)
+            elif rname == "dgetrf":
+                s.getrs(mats["A"], mats["piv"], X, **o)
+            elif rname == "dgeqrf":
+                s.unmqr(s.Side.Left, s.Op.ConjTrans, mats["A"], mats["T"], X, **o)
+                R = s.TriangularMatrix(s.Uplo.Upper, s.Diag.NonUnit, mats["A"])
+                s.trsm(s.Side.Left, 1.0, R, X, **o)
+        # r = b - A0 X
+        r = vec(0)
+        s.gemm(-1.0, A0, X, 0.0, r, **o)
+        s.add(1.0, b, 1.0, r, **o)
+        err = inf(r) / (inf(A0) * inf(X) * n_ * eps)
+        del A0
+        return err
+
+    def run(rname, n_, nb, tg, label):
+        """W untimed + K timed steps of one routine; returns its result dict."""
         mats = {}
-        nb = nb_per.get(rname, a.nb)
+        tgt = s.target_of(tg)
+        o = dict(target=tg, lookahead=a.lookahead)
         if rname == "dgemm":
             for key, seed in (("A", 1), ("B", 2), ("C", 3)):
-                M = s.Matrix(n, n, nb, np.float64, grid)
-                M.insertLocalTiles(s.target_of(target))
-                s._slate.generate_matrix_d("rands", M, seed, -1.0, s.opts(target))
+                M = s.Matrix(n_, n_, nb, np.float64, grid)
+                M.insertLocalTiles(tgt)
+                s._slate.generate_matrix_d("rands", M, seed, -1.0, s.opts(tg))
                 mats[key] = M
-            flops = F.gemm_flops(n, n, n)
+            flops = F.gemm_flops(n_, n_, n_)
         elif rname == "dgesv_mixed":
-            # fp32 LU + fp64 refinement; flops counted as the fp64 LU (tester convention)
             for key, seed in (("B", 7), ("X", 0)):
-                M = s.Matrix(n, 1, nb, np.float64, grid)
-                M.insertLocalTiles(s.target_of(target))
-                s._slate.generate_matrix_d("rands", M, seed + 1, -1.0, s.opts(target))
+                M = s.Matrix(n_, 1, nb, np.float64, grid)
+                M.insertLocalTiles(tgt)
+                s._slate.generate_matrix_d("rands", M, seed + 1, -1.0, s.opts(tg))
                 mats[key] = M
-            M = s.Matrix(n, n, nb, np.float64, grid)
-            M.insertLocalTiles(s.target_of(target))
+            M = s.Matrix(n_, n_, nb, np.float64, grid)
+            M.insertLocalTiles(tgt)
             mats["A"] = M
-            flops = F.getrf_flops(n)
+            flops = F.getrf_flops(n_)   # tester convention: counted as the fp64 LU
         else:
-            M = s.Matrix(n, n, nb, np.float64, grid)
-            M.insertLocalTiles(s.target_of(target))
+            M = s.Matrix(n_, n_, nb, np.float64, grid)
+            M.insertLocalTiles(tgt)
             mats["A"] = M
-            flops = {"dpotrf": F.potrf_flops, "dgetrf": F.getrf_flops, "dgeqrf": F.geqrf_flops}[rname](n)
-        times = []
+            flops = {"dpotrf": F.potrf_flops, "dgetrf": F.getrf_flops, "dgeqrf": F.geqrf_flops}[rname](n_)
+        # random (rands) matrices everywhere, as the reference tester; SPD for potrf
+        kind = "spd" if rname == "dpotrf" else "rands"
+        times, extra = [], {}
+        seed = 0
         for step in range(a.warmup + a.steps):
+            seed = 100 + step
             if rname != "dgemm":
-                # diagonally dominant for dgesv_mixed so fp32 LU + refinement converges
-                kind = "spd" if rname == "dpotrf" else ("diag_dominant" if rname == "dgesv_mixed" else "rands")
-                s._slate.generate_matrix_d(kind, mats["A"], 100 + step, -1.0, s.opts(target))
+                s._slate.generate_matrix_d(kind, mats["A"], seed, -1.0, s.opts(tg))
             barrier_sync()
             if a.trace and step == a.warmup:
                 s.trace.on()
             t0 = time.perf_counter()
             if rname == "dgemm":
-                s.gemm(1.0, mats["A"], mats["B"], 0.0, mats["C"], **opts)
+                s.gemm(1.0, mats["A"], mats["B"], 0.0, mats["C"], **o)
             elif rname == "dpotrf":
-                info = s.potrf(s.HermitianMatrix(s.Uplo.Lower, mats["A"]), **opts)
+                info = s.potrf(s.HermitianMatrix(s.Uplo.Lower, mats["A"]), **o)
                 assert info == 0, f"dpotrf info={info}"
             elif rname == "dgetrf":
                 if a.method_lu == "tntpiv":
-                    info, _ = s.getrf_tntpiv(mats["A"], **opts)
+                    info, piv = s.getrf_tntpiv(mats["A"], **o)
                 else:
-                    info, _ = s.getrf(mats["A"], **opts)
+                    info, piv = s.getrf(mats["A"], **o)
+                mats["piv"] = piv
                 assert info == 0, f"dgetrf info={info}"
             elif rname == "dgeqrf":
-                s.geqrf(mats["A"], **opts)
+                mats["T"] = s.geqrf(mats["A"], **o)
             elif rname == "dgesv_mixed":
                 s._slate.clear_timers()
                 lu = {"tntpiv": 2, "ppiv": 1}[a.method_lu]  # MethodLU::CALU / PartialPiv
-                info, _, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], method_lu=lu, **opts)
-                assert info == 0 and iters >= 0, f"dgesv_mixed info={info} iters={iters}"
+                info, piv, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], method_lu=lu, **o)
+                mats["piv"] = piv
+                assert info == 0, f"dgesv_mixed info={info} iters={iters}"
+                extra["iterations"] = int(iters)
+                extra["fallback"] = bool(iters < 0)
                 if rank == 0:
                     tm = {k: round(v * 1e3, 1) for k, v in s._slate.timers().items() if "gesv_mixed" in k}
                     print(f"# dgesv_mixed iters={iters} phase ms: {tm}", file=sys.stderr, flush=True)
             barrier_sync()
             dt = time.perf_counter() - t0
             if a.trace and step == a.warmup:
-                s.trace.finish(grid.world, f"{a.trace}_{rname}")
+                s.trace.finish(grid.world, f"{a.trace}_{label}")
                 s.trace.off()
             if step >= a.warmup:
                 times.append(dt)
             if rank == 0:
-                print(f"# {rname} step {step} {'warm' if step < a.warmup else 'timed'}: {dt*1e3:.1f} ms "
+                print(f"# {label} step {step} {'warm' if step < a.warmup else 'timed'}: {dt*1e3:.1f} ms "
                       f"{flops/dt/1e12:.2f} TFLOP/s", file=sys.stderr, flush=True)
         t = max_over_ranks(float(np.mean(times)))
-        results[rname] = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb}
+        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_}
+        if a.check == "yes":
+            err = residual(rname, mats, kind, seed, nb, n_, tg)
+            res["backward_error"] = float(f"{err:.3e}")
+            res["check"] = "pass" if err < 50 else "FAIL"
+            if rank == 0:
+                print(f"# {label} backward error {err:.3e} ({res['check']})", file=sys.stderr, flush=True)
+        res.update(extra)
         del mats
         s.sync()
         s._slate.release_cache()
+        return res
+
+    results = {}
+    routines = [r.strip() for r in a.routines.split(",") if r.strip()]
+    for rname in routines:
+        results[rname] = run(rname, n, nb_per.get(rname, a.nb), target, rname)
+    configs = {}
+    extras = list(EXTRAS) if a.extras == "all" else ([] if a.extras == "none" else a.extras.split(","))
+    for name in extras:
+        rname, n_, nb_, tg_ = EXTRAS[name]
+        tg_ = tg_ or target
+        if tg_ == "h" and world > 1:
+            continue   # config 1 is a one-process host-target plumbing check
+        nb_ = nb_ or nb_per.get(rname, a.nb)
+        n_ = n if n_ is None else (n // 2 if n_ == -2 else n_)
+        configs[name] = run(rname, n_, nb_, tg_, name)
 
     tot_flops = sum(r["flops"] for r in results.values())
     tot_t = sum(r["ms"] for r in results.values()) / 1e3
@@ -184,7 +274,7 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "fp64",
-        "data": "synthetic (counter-hash uniform[-1,1); SPD = symmetric + n*I for dpotrf)",
+        "data": "synthetic random (rands: counter-hash uniform[-1,1); SPD = symmetric + n*I for dpotrf)",
         "config": {
             "model": "+".join(f"{k}(nb={v['nb']})" for k, v in results.items()) + f" n={n}",
             "global_batch": 1,
@@ -193,7 +283,10 @@ def main():
             "lookahead": a.lookahead,
             "lu_method": a.method_lu,
         },
-        "routines": {k: {"tflops": round(v["tflops"], 3), "ms": round(v["ms"], 2)} for k, v in results.items()},
+        "routines": {k: {kk: (round(vv, 4) if isinstance(vv, float) and kk != "backward_error" else vv)
+                         for kk, vv in v.items() if kk != "flops"} for k, v in results.items()},
+        "configs": {k: {kk: (round(vv, 4) if isinstance(vv, float) and kk != "backward_error" else vv)
+                        for kk, vv in v.items() if kk != "flops"} for k, v in configs.items()},
     }
     if rank == 0:
         print(json.dumps(line), flush=True)

@@ -539,9 +539,19 @@ __global__ void splitk_reduce_kernel(int64_t m, int64_t n, int splits, const T* 
     int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
     int64_t j = blockIdx.y;
     if (i >= m) return;
-    T s = 0;
+    // four independent partial sums keep several loads in flight
+    T s0 = 0, s1 = 0, s2 = 0, s3 = 0;
     const int64_t mn = m * n;
-    for (int b = 0; b < splits; ++b) s += P[b * mn + i + j * m];
+    const T* p = P + i + j * m;
+    int b = 0;
+    for (; b + 4 <= splits; b += 4) {
+        s0 += p[(b + 0) * mn];
+        s1 += p[(b + 1) * mn];
+        s2 += p[(b + 2) * mn];
+        s3 += p[(b + 3) * mn];
+    }
+    for (; b < splits; ++b) s0 += p[b * mn];
+    T s = (s0 + s1) + (s2 + s3);
     T* c = C + i + j * ldc;
     *c = (beta == T(0)) ? alpha * s : alpha * s + beta * (*c);
 }

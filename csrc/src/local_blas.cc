@@ -108,7 +108,9 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
         // V^H A products at the tail, where one workgroup would otherwise walk
         // all of K alone)
         if (uplo == 'G' && tiles < 128 && k >= 1024) {
-            int64_t splits = std::min<int64_t>(ceildiv(k, 128), std::max<int64_t>(2, 1024 / tiles));
+            // about 2 workgroups per CU in total and at most 64 partial
+            // products, so the reduction stays a short streaming pass
+            int64_t splits = std::min<int64_t>({ceildiv(k, 256), std::max<int64_t>(2, 512 / tiles), int64_t(64)});
             int64_t kc = roundup(ceildiv(k, splits), 16);
             splits = ceildiv(k, kc);
             int64_t full = k / kc;                 // chunks of exactly kc
