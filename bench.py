@@ -225,6 +225,7 @@ def main():
             if a.trace and step == a.warmup:
                 s.trace.finish(grid.world, f"{a.trace}_{label}")
                 s.trace.off()
+                s.trace.clear()
             if step >= a.warmup:
                 times.append(dt)
             if rank == 0:

@@ -38,6 +38,12 @@ public:
     static void clear();
 };
 
+/// Label of the Sched task being enqueued on this thread: the name of the
+/// first trace::Block opened between task_label_begin() and task_label_end()
+/// (null if none) -- the runtime's device spans of a task carry it.
+void task_label_begin();
+const char* task_label_end();
+
 /// RAII host span.
 class Block {
 public:

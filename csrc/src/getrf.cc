@@ -349,8 +349,10 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
                         lb::copy2d(c, rd_.mine, int64_t(1), ids.data(), rd_.mine, idS.data(), ms);
                         lb::copy2d(c, rd_.theirs, int64_t(1), idr.data(), rd_.theirs, idS.data() + rd_.mine, ms);
                         lb::copy2d(c, ms, kb, Sb.data(), ms, Fb.data(), ms);
+                        // tournament inside the merge too (tslu narrow blocks): a 2kd x kb
+                        // partial-pivoting LU would cost two launches per column
                         lb::getrf_panel(c, ms, kb, Fb.data(), ms, pip.data(), perm.data(),
-                                        rd_.final ? info_real : info_dummy, kk, true, false);
+                                        rd_.final ? info_real : info_dummy, kk, true, true);
                         gather_rows_ids(c, c2, kb, perm.data(), Sb.data(), ms, Cb.data(), c2, idS.data(), ids.data(),
                                         rd, 0);
                     });

@@ -35,7 +35,22 @@ void Sched::task(int queue, std::vector<int64_t> const& in, std::vector<int64_t>
         wait(st.writer);
         for (auto e : st.readers) wait(e);
     }
+    // tracing: one device span per task (timing events around its kernels),
+    // labeled by the task's first trace::Block, on lane 100 + queue
+    hipEvent_t ta = nullptr;
+    if (trace::Trace::is_on() && hipEventCreate(&ta) == hipSuccess) {
+        (void)hipEventRecord(ta, s);
+        trace::task_label_begin();
+    }
     fn(ctx(queue));
+    if (ta) {
+        const char* label = trace::task_label_end();
+        hipEvent_t tb = nullptr;
+        if (hipEventCreate(&tb) == hipSuccess) {
+            (void)hipEventRecord(tb, s);
+            trace::Trace::insert_device(label ? label : "task", queue, ta, tb);
+        }
+    }
     hipEvent_t e = device::event_get();
     events_.push_back(e);
     slate_hip_call(hipEventRecord(e, s));

@@ -208,7 +208,16 @@ int debug_rank() {
 }
 }  // namespace
 
+namespace {
+thread_local const char* t_task_label = nullptr;
+thread_local bool t_task_open = false;
+}  // namespace
+
+void task_label_begin() { t_task_open = true; t_task_label = nullptr; }
+const char* task_label_end() { t_task_open = false; const char* l = t_task_label; t_task_label = nullptr; return l; }
+
 Block::Block(const char* name) : name_(name), start_(0), active_(Trace::is_on()) {
+    if (t_task_open && !t_task_label) t_task_label = name;   // first span inside a Sched task labels it
     if (active_) start_ = Trace::now();
     if (debug_calls()) std::fprintf(stderr, "[rank %d] > %s\n", debug_rank(), name);
 }
