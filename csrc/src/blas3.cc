@@ -9,8 +9,10 @@
 // gemmA: stationary A (reference src/gemmA.cc:67-190): local partial
 //   products reduced across the process row (allreduce replaces listReduce).
 // trsm: block-row sweeps (reference src/work/work_trsm.cc:101-185).
-// herk/syrk/her2k/syr2k/hemm/symm/trmm: a single local call on 1x1 grids;
-//   on larger grids they are composed from gemmC on materialized operands.
+// herk/syrk/her2k/syr2k: a single local call on 1x1 grids; on larger grids a
+//   triangle-only SUMMA (tri_summa: diagonal tiles through the triangular MFMA
+//   GEMM, never the other triangle).  trmm (Left, NoTrans A): SUMMA that skips
+//   the zero part of each A panel.  hemm/symm: gemmC on the expanded operand.
 #include "internal.hh"
 
 #include <numeric>
@@ -361,6 +363,113 @@ void tri_axpby(T alpha, Matrix<T> const& G, T beta, BaseTrapezoidMatrix<T>& C, T
 
 }  // namespace
 
+namespace {
+
+/// C(uplo) = alpha * A * B + beta * C(uplo) on a p x q grid, touching only the
+/// stored triangle of C: the reference's herk/syrk/her2k updates do a
+/// triangular product on the diagonal tiles and a gemm on the off-diagonal
+/// ones and never form the other triangle (internal_herk.cc:491-515).  Here:
+/// SUMMA over k with gemmC's whole-panel broadcasts (A(:, k) along process
+/// rows, B(k, :) down process columns), and per local tile column J one
+/// triangular-output MFMA GEMM on the diagonal tile (when local) plus one
+/// GEMM over the local tiles strictly inside the triangle.
+template <typename T>
+void tri_summa(Uplo uplo, T alpha, BaseMatrix<T> const& A_in, BaseMatrix<T> const& B_in, T beta,
+               BaseMatrix<T> const& C, Options const& opts) {
+    Target target = resolve_target(opts);
+    const int64_t la = option_la(opts);
+    auto gC = C.grid();
+    BaseMatrix<T> A = A_in, B = B_in;
+    Matrix<T> Ac, Bc;
+    if (!rows_conform(A, C)) {
+        int64_t kb = A_in.nt() ? A_in.tileNb(0) : C.nb();
+        Ac = materialize<T>(A_in, target, gC, C.mb(), kb, row0_owner(C), 0);
+        A = Ac;
+    }
+    if (!cols_conform(B, C)) {
+        int64_t kb = A.nt() ? A.tileNb(0) : C.mb();
+        Bc = materialize<T>(B_in, target, gC, kb, C.nb(), 0, col0_owner(C));
+        B = Bc;
+    }
+    slate_error_if_msg(A.nt() != B.mt(), "tri_summa: inner tilings differ");
+    // scale the stored triangle by beta once
+    if (beta != T(1)) {
+        Options o = {{Option::Target, target}};
+        BaseTrapezoidMatrix<T> Ct(uplo, C, MatrixKind::Trapezoid);
+        add(T(0), Ct, beta, Ct, o);
+    }
+    const Loc loc = loc_of(target);
+    auto& g = *gC;
+    const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    LocalBlock<T> lc = C.local(loc, true);
+    LocalBlock<T> la_ = A.local(loc, false);
+    LocalBlock<T> lb_ = B.local(loc, false);
+    const int64_t kt = A.nt(), nt = C.nt();
+    Sched S(target);
+    const int R = int(std::max<int64_t>(2, la + 2));
+    int64_t kbmax = 0;
+    for (int64_t k = 0; k < kt; ++k) kbmax = std::max(kbmax, A.tileNb(k));
+    std::vector<Work<T>> WA(R), WB(R);
+    for (int r = 0; r < R; ++r) {
+        if (q > 1) WA[r].resize(target, size_t(std::max<int64_t>(lc.m, 1)) * std::max<int64_t>(kbmax, 1));
+        if (p > 1) WB[r].resize(target, size_t(std::max<int64_t>(kbmax, 1)) * std::max<int64_t>(lc.n, 1));
+    }
+    // my local tile columns of C
+    std::vector<int64_t> myJ;
+    for (int64_t J = 0; J < nt; ++J) if (C.scol_owner(J) == mycol) myJ.push_back(J);
+    for (int64_t k = 0; k < kt; ++k) {
+        const int slot = int(k % R);
+        const int64_t kb = A.tileNb(k);
+        const int qa = A.scol_owner(k), pb = B.srow_owner(k);
+        T* pa = (q > 1) ? WA[slot].data() : nullptr;
+        T* pbuf = (p > 1) ? WB[slot].data() : nullptr;
+        T const* Ak = (q == 1) ? la_.ptr + lcol_of(A, k) * la_.ld : pa;
+        const int64_t ldak = (q == 1) ? la_.ld : std::max<int64_t>(lc.m, 1);
+        T const* Bk = (p == 1) ? lb_.ptr + lrow_of(B, k) : pbuf;
+        const int64_t ldbk = (p == 1) ? lb_.ld : kb;
+        const int64_t tBc = Sched::bcast(slot);
+        S.task(device::kCommQueue, {}, {tBc}, [&, k, kb, qa, pb, pa, pbuf](lb::Ctx const& c) {
+            trace::Block t2("trisumma_bcast");
+            if (q > 1) {
+                if (mycol == qa) pack(c, lc.m, kb, la_.ptr + lcol_of(A, k) * la_.ld, la_.ld, pa);
+                bcast(g.row(), pa, size_t(lc.m * kb), qa, c);
+            }
+            if (p > 1) {
+                if (myrow == pb) lb::copy2d(c, kb, lc.n, lb_.ptr + lrow_of(B, k), lb_.ld, pbuf, kb);
+                bcast(g.col(), pbuf, size_t(kb * lc.n), pb, c);
+            }
+        });
+        S.task(0, {tBc}, {Sched::tok(9, 0)}, [&, Ak, ldak, Bk, ldbk, kb](lb::Ctx const& c) {
+            trace::Block t2("trisumma_update");
+            for (int64_t J : myJ) {
+                const int64_t c0 = lcol_of(C, J), nc = lcol_of(C, J + 1) - c0;
+                const int64_t r0 = lrow_of(C, J), r1 = lrow_of(C, J + 1);   // my rows of tile row J
+                const bool diag_local = (C.srow_owner(J) == myrow) && r1 > r0;
+                if (uplo == Uplo::Lower) {
+                    if (diag_local)
+                        lb::gemm_tri(c, Uplo::Lower, Op::NoTrans, Op::NoTrans, nc, kb, alpha, Ak + r0, ldak,
+                                     Bk + c0 * ldbk, ldbk, T(1), lc.ptr + r0 + c0 * lc.ld, lc.ld);
+                    const int64_t rs = diag_local ? r1 : r0;          // rows strictly below tile row J
+                    if (lc.m > rs)
+                        lb::gemm(c, Op::NoTrans, Op::NoTrans, lc.m - rs, nc, kb, alpha, Ak + rs, ldak,
+                                 Bk + c0 * ldbk, ldbk, T(1), lc.ptr + rs + c0 * lc.ld, lc.ld);
+                } else {
+                    if (diag_local)
+                        lb::gemm_tri(c, Uplo::Upper, Op::NoTrans, Op::NoTrans, nc, kb, alpha, Ak + r0, ldak,
+                                     Bk + c0 * ldbk, ldbk, T(1), lc.ptr + r0 + c0 * lc.ld, lc.ld);
+                    if (r0 > 0)                                        // rows strictly above tile row J
+                        lb::gemm(c, Op::NoTrans, Op::NoTrans, r0, nc, kb, alpha, Ak, ldak, Bk + c0 * ldbk, ldbk,
+                                 T(1), lc.ptr + c0 * lc.ld, lc.ld);
+                }
+            }
+        });
+    }
+    S.wait_all();
+    C.storage()->update_origin();
+}
+
+}  // namespace
+
 template <typename T>
 void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMatrix<T>& C, Options const& opts) {
     trace::Block tb("herk");
@@ -373,6 +482,10 @@ void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMa
         lb::herk(c, C.uplo(), op, lc.m, A.n(), alpha, la_.ptr, la_.ld, beta, lc.ptr, lc.ld);
         sync_ctx(c);
         C.storage()->update_origin();
+        return;
+    }
+    if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
+        tri_summa<T>(C.uplo(), T(alpha), A, conj_transpose(A), T(beta), C, opts);
         return;
     }
     Matrix<T> G = Matrix<T>(C).emptyLike();
@@ -393,6 +506,10 @@ void syrk(T alpha, Matrix<T> const& A, T beta, SymmetricMatrix<T>& C, Options co
         lb::syrk(c, C.uplo(), op, lc.m, A.n(), alpha, la_.ptr, la_.ld, beta, lc.ptr, lc.ld);
         sync_ctx(c);
         C.storage()->update_origin();
+        return;
+    }
+    if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
+        tri_summa<T>(C.uplo(), alpha, A, transpose(A), beta, C, opts);
         return;
     }
     Matrix<T> G = Matrix<T>(C).emptyLike();
@@ -416,6 +533,11 @@ void her2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, real_type<T> beta, H
         C.storage()->update_origin();
         return;
     }
+    if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
+        tri_summa<T>(C.uplo(), alpha, A, conj_transpose(B), T(beta), C, opts);
+        tri_summa<T>(C.uplo(), slate::conj(alpha), B, conj_transpose(A), T(1), C, opts);
+        return;
+    }
     Matrix<T> G = Matrix<T>(C).emptyLike();
     G.insertLocalTiles(target);
     gemmC(alpha, A, conj_transpose(B), T(0), G, opts);
@@ -437,6 +559,11 @@ void syr2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, SymmetricMat
         C.storage()->update_origin();
         return;
     }
+    if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
+        tri_summa<T>(C.uplo(), alpha, A, transpose(B), beta, C, opts);
+        tri_summa<T>(C.uplo(), alpha, B, transpose(A), T(1), C, opts);
+        return;
+    }
     Matrix<T> G = Matrix<T>(C).emptyLike();
     G.insertLocalTiles(target);
     gemmC(alpha, A, transpose(B), T(0), G, opts);
@@ -445,6 +572,81 @@ void syr2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, SymmetricMat
 }
 
 namespace {
+
+/// B := alpha A B, A triangular (NoTrans, conforming to B's rows and with
+/// square tiles), on a p x q grid: SUMMA over k where step k only touches
+/// the rows that A(:, k) reaches -- tile rows >= k (Lower) or <= k (Upper) --
+/// instead of a dense product with explicit zeros (reference src/trmm.cc +
+/// work::trmm).  B's old values are read from a copy; the diagonal tile of
+/// each broadcast panel is masked to its triangle (unit diagonal if asked).
+template <typename T>
+void trmm_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target,
+                       int64_t la) {
+    Options o = {{Option::Target, target}};
+    Matrix<T> B0 = B.emptyLike();
+    B0.insertLocalTiles(target);
+    slate::copy<T, T>(B, B0, o);
+    auto& g = *B.grid();
+    const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    LocalBlock<T> lbk = B.local(loc, true);
+    LocalBlock<T> lb0 = B0.local(loc, false);
+    LocalBlock<T> lA = A.local(loc, false);
+    const int64_t kt = A.nt();
+    Sched S(target);
+    const int R = int(std::max<int64_t>(2, la + 2));
+    const int64_t nb = B.mb();
+    std::vector<Work<T>> WA(R), WB(R);
+    for (int r = 0; r < R; ++r) {
+        WA[r].resize(target, size_t(std::max<int64_t>(lbk.m, 1)) * nb);
+        if (p > 1) WB[r].resize(target, size_t(nb) * std::max<int64_t>(lbk.n, 1));
+    }
+    const bool lower = (uplo == Uplo::Lower);
+    // Lower: panel k reaches rows >= k, so k = 0 touches every row first;
+    // Upper: rows <= k, so run k downwards
+    for (int64_t kk = 0; kk < kt; ++kk) {
+        const int64_t k = lower ? kk : kt - 1 - kk;
+        const int slot = int(kk % R);
+        const int64_t kb = A.tileNb(k);
+        const int qk = A.scol_owner(k), pk = B.srow_owner(k);
+        const int64_t r0 = lower ? lrow_of(B, k) : 0, r1 = lower ? lbk.m : lrow_of(B, k + 1);  // rows A(:, k) reaches
+        const int64_t rk = lrow_of(B, k);
+        T* WAk = WA[slot].data();
+        T* WBk = (p > 1) ? WB[slot].data() : nullptr;
+        const int64_t tBc = Sched::bcast(slot);
+        S.task(device::kCommQueue, {}, {tBc}, [&, k, kb, qk, pk, r0, r1, rk, WAk, WBk](lb::Ctx const& c) {
+            trace::Block t2("trmm_bcast");
+            const int64_t nr = r1 - r0;
+            if (nr > 0) {
+                if (mycol == qk) pack(c, nr, kb, lA.ptr + r0 + lcol_of(A, k) * lA.ld, lA.ld, WAk);
+                if (q > 1) bcast(g.row(), WAk, size_t(nr * kb), qk, c);
+                if (myrow == pk) {
+                    // diagonal tile sits at rows rk - r0 of the panel: keep its triangle only
+                    T* D = WAk + (rk - r0);
+                    if (kb > 1) {
+                        if (lower) lb::set(c, Uplo::Upper, kb - 1, kb - 1, T(0), T(0), D + nr, nr);
+                        else lb::set(c, Uplo::Lower, kb - 1, kb - 1, T(0), T(0), D + 1, nr);
+                    }
+                    if (diag == Diag::Unit) lb::set(c, Uplo::General, 1, kb, T(1), T(1), D, nr + 1);
+                }
+            }
+            if (p > 1) {
+                if (myrow == pk) lb::copy2d(c, kb, lb0.n, lb0.ptr + rk, lb0.ld, WBk, kb);
+                bcast(g.col(), WBk, size_t(kb * lb0.n), pk, c);
+            }
+        });
+        T const* Bk = (p > 1) ? WBk : lb0.ptr + rk;
+        const int64_t ldbk = (p > 1) ? kb : lb0.ld;
+        S.task(0, {tBc}, {Sched::tok(9, 0)}, [&, r0, r1, kb, WAk, Bk, ldbk, kk](lb::Ctx const& c) {
+            trace::Block t2("trmm_update");
+            const int64_t nr = r1 - r0;
+            if (nr > 0)
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, nr, lbk.n, kb, alpha, WAk, nr, Bk, ldbk, kk == 0 ? T(0) : T(1),
+                         lbk.ptr + r0, lbk.ld);
+        });
+    }
+    S.wait_all();
+}
 
 /// full (dense) copy of a symmetric/Hermitian matrix on the same layout
 template <typename T>
@@ -518,33 +720,31 @@ void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         B.storage()->update_origin();
         return;
     }
-    // dense op(A) with explicit zeros, then gemm into a copy
-    Options o = {{Option::Target, target}};
-    Matrix<T> F = Matrix<T>(BaseMatrix<T>(A)).emptyLike();
-    F.insertLocalTiles(target);
-    set(T(0), T(0), F, o);
-    Matrix<T> Ag{BaseMatrix<T>(A)};
-    Ag.set_uplo(Uplo::General);
-    BaseTrapezoidMatrix<T> At(A.uplo(), Ag, MatrixKind::Trapezoid);
-    BaseTrapezoidMatrix<T> Ft(A.uplo(), F, MatrixKind::Trapezoid);
-    slate::copy<T, T>(At, Ft, o);
-    if (A.diag() == Diag::Unit) {
-        TriangularMatrix<T> Fd(A.uplo(), Diag::NonUnit, F);
-        // set the diagonal to one: tiles on the diagonal
-        Matrix<T> Fg(F);
-        for (int64_t i = 0; i < std::min(Fg.mt(), Fg.nt()); ++i) {
-            if (!Fg.tileIsLocal(i, i)) continue;
-            Tile<T> t = Fg.tile(i, i, loc_of(target));
-            lb::Ctx c = ctx_for(target);
-            lb::set(c, Uplo::General, 1, std::min(t.mb, t.nb), T(1), T(1), t.data, t.stride + 1);
-            sync_ctx(c);
-        }
+    // distributed: reduce to Left with a NoTrans triangle conforming to B's
+    // rows (as trsm does), then a SUMMA that skips the zero part of A
+    auto gB = B.grid();
+    if (side == Side::Right) {
+        // B op(A) = (op(A)^H B^H)^H
+        bool conj = is_complex_v<T>;
+        Matrix<T> Bt = materialize<T>(conj ? conj_transpose(B) : transpose(B), target, gB, B.nb(), B.mb(), 0, 0);
+        TriangularMatrix<T> Ah = conj ? conj_transpose(A) : transpose(A);
+        TriangularMatrix<T> At(Ah.uplo(), A.diag(), Ah);
+        trmm(Side::Left, conj ? slate::conj(alpha) : alpha, At, Bt, opts);
+        slate::copy<T, T>(conj ? conj_transpose(Bt) : transpose(Bt), B, opts);
+        return;
     }
-    Matrix<T> Bc = B.emptyLike();
-    Bc.insertLocalTiles(target);
-    slate::copy<T, T>(B, Bc, o);
-    if (side == Side::Left) gemmC(alpha, F, Bc, T(0), B, opts);
-    else gemmC(alpha, Bc, F, T(0), B, opts);
+    BaseMatrix<T> Ause = A;
+    Matrix<T> Ac;
+    bool conform = A.op() == Op::NoTrans && rows_conform(BaseMatrix<T>(A), BaseMatrix<T>(B)) &&
+                   A.grid()->same_processes(*gB);
+    if (conform)
+        for (int64_t j = 0; j < A.nt(); ++j) if (A.tileNb(j) != B.tileMb(j)) conform = false;
+    if (!conform) {
+        Ac = materialize<T>(A, target, gB, B.mb(), B.mb(), row0_owner(B), 0);
+        Ause = Ac;
+    }
+    trmm_left_notrans<T>(A.uplo(), A.diag(), alpha, Ause, B, target, option_la(opts));
+    B.storage()->update_origin();
 }
 
 //------------------------------------------------------------------------------

@@ -42,6 +42,28 @@ def case_herk(tg, dt, nb):
     assert relerr(np.tril(s.to_numpy(C)), np.tril(ref)) < tol(dt)
 
 
+def case_rank2k(tg, dt, nb):
+    """syrk / her2k / syr2k on p x q grids (triangle-only SUMMA), both uplos, beta != 0."""
+    n, k = 140, 60
+    a, b = rnd(n, k, dt, 41), rnd(n, k, dt, 42)
+    c0 = rnd(n, n, dt, 43)
+    c0 = c0 + c0.conj().T
+    for uplo, tri in ((s.Uplo.Lower, np.tril), (s.Uplo.Upper, np.triu)):
+        C = s.from_numpy(c0, nb=nb, target=tg)
+        s.syrk(1.5, s.from_numpy(a, nb=nb, target=tg), 0.5, s.SymmetricMatrix(uplo, C), target=tg)
+        assert relerr(tri(s.to_numpy(C)), tri(1.5 * a @ a.T + 0.5 * c0)) < tol(dt), ("syrk", uplo)
+        C = s.from_numpy(c0, nb=nb, target=tg)
+        s.her2k(2.0, s.from_numpy(a, nb=nb, target=tg), s.from_numpy(b, nb=nb, target=tg), 0.5,
+                s.HermitianMatrix(uplo, C), target=tg)
+        ref = 2.0 * a @ b.conj().T + 2.0 * b @ a.conj().T + 0.5 * c0
+        assert relerr(tri(s.to_numpy(C)), tri(ref)) < tol(dt), ("her2k", uplo)
+        C = s.from_numpy(c0, nb=nb, target=tg)
+        s.syr2k(1.0, s.from_numpy(a, nb=nb, target=tg), s.from_numpy(b, nb=nb, target=tg), -1.0,
+                s.SymmetricMatrix(uplo, C), target=tg)
+        ref = a @ b.T + b @ a.T - c0
+        assert relerr(tri(s.to_numpy(C)), tri(ref)) < tol(dt), ("syr2k", uplo)
+
+
 def case_trsm(tg, dt, nb):
     n = 140
     t = (np.tril(rnd(n, n, dt, 5)) / n + 2 * np.eye(n)).astype(dt)
@@ -50,6 +72,30 @@ def case_trsm(tg, dt, nb):
     B = s.from_numpy(b, nb=nb, target=tg)
     s.trsm(s.Side.Left, 1.0, T, B, target=tg)
     assert relerr(t @ s.to_numpy(B), b) < tol(dt)
+
+
+def case_trmm(tg, dt, nb):
+    """Distributed trmm (triangle-skipping SUMMA) on every side / uplo / op / diag."""
+    m, n = 130, 70
+    for side in (s.Side.Left, s.Side.Right):
+        na = m if side == s.Side.Left else n
+        for uplo, tri in ((s.Uplo.Lower, np.tril), (s.Uplo.Upper, np.triu)):
+            t = rnd(na, na, dt, 51)
+            for diag in (s.Diag.NonUnit, s.Diag.Unit):
+                teff = tri(t).copy()
+                if diag == s.Diag.Unit:
+                    np.fill_diagonal(teff, 1)
+                for op in ("n", "c"):
+                    b = rnd(m, n, dt, 52)
+                    T = s.TriangularMatrix(uplo, diag, s.from_numpy(t, nb=nb, target=tg))
+                    opt = teff
+                    if op == "c":
+                        T = s.conj_transpose(T)
+                        opt = teff.conj().T
+                    B = s.from_numpy(b, nb=nb, target=tg)
+                    s.trmm(side, dt(1.5), T, B, target=tg)
+                    ref = 1.5 * (opt @ b if side == s.Side.Left else b @ opt)
+                    assert relerr(s.to_numpy(B), ref) < tol(dt), (side, uplo, diag, op)
 
 
 def case_potrf(tg, dt, nb):
