@@ -57,8 +57,10 @@ hipEvent_t event_get();
 void event_put(hipEvent_t e);
 
 /// Caching device allocator.  Blocks are bucketed by rounded size and reused;
-/// callers must ensure stream work using a block is complete before freeing
-/// it (drivers free their workspace only after syncing their streams).
+/// free is stream-ordered: the block is only handed out again once the work
+/// queued before the free on every queue (and the null stream) has completed,
+/// so early returns and exception paths cannot recycle memory under in-flight
+/// kernels.
 void* malloc(size_t bytes);
 void  free(void* ptr);
 void* malloc_host(size_t bytes);   // pinned host memory

@@ -261,8 +261,9 @@ int64_t potrf(Uplo uplo, int64_t n, T* A, int64_t lda) {
 
 /// LU with partial pivoting (right-looking, rank-1 updates, OpenMP over columns).
 /// ipiv[j] = 0-based row swapped with row j.  Returns info (1-based first zero pivot).
+/// thresh < 1: threshold pivoting, the diagonal stays pivot while |a_jj| >= thresh * max.
 template <typename T>
-int64_t getrf(int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, bool pivot = true) {
+int64_t getrf(int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, bool pivot = true, double thresh = 1.0) {
     int64_t info = 0;
     int64_t mn = std::min(m, n);
     for (int64_t j = 0; j < mn; ++j) {
@@ -273,6 +274,7 @@ int64_t getrf(int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, bool pivot
                 real_type<T> v = cabs1(A[i + j * lda]);
                 if (v > best) { best = v; p = i; }
             }
+            if (thresh < 1.0 && p != j && cabs1(A[j + j * lda]) >= real_type<T>(thresh) * best) p = j;
         }
         ipiv[j] = p;
         if (p != j)

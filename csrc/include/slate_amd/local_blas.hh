@@ -100,9 +100,12 @@ void lauum(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda);
 /// (row t of the result is row perm[t] of the input) when non-null.
 /// pivot=false gives LU without pivoting; tournament=true selects the pivots
 /// of every 32-column narrow block by tournament (CALU) instead of per column.
+/// pivot_threshold in (0, 1] (Option::PivotThreshold) keeps the diagonal entry
+/// as pivot when |a_jj| >= threshold * max_i |a_ij| (1 = partial pivoting).
 template <typename T>
 void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, int64_t* perm,
-                 int* info, int64_t info_offset, bool pivot = true, bool tournament = false);
+                 int* info, int64_t info_offset, bool pivot = true, bool tournament = false,
+                 double pivot_threshold = 1.0);
 
 /// Apply a row permutation produced by getrf_panel (perm over the first m
 /// rows, pivots ipiv[0..k)) to n columns of B.

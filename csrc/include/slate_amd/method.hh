@@ -43,7 +43,14 @@ inline Method str2method(std::string s) {
 
 namespace MethodHemm {
 const Method Error = baseMethodError, Auto = baseMethodAuto, HemmA = 1, HemmC = 2;
+inline Method str2method(std::string s) {
+    std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+    if (s == "auto") return Auto;
+    if (s == "a" || s == "hemma") return HemmA;
+    if (s == "c" || s == "hemmc") return HemmC;
+    throw Exception("unknown hemm method");
 }
+}  // namespace MethodHemm
 
 namespace MethodCholQR {
 const Method Error = baseMethodError, Auto = baseMethodAuto, GemmA = 1, GemmC = 2, HerkA = 3, HerkC = 4;

@@ -140,7 +140,7 @@ void lu_colmax(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c, rt<T>* 
 template <typename T>
 void lu_pivot(int nparts, const rt<T>* pval, const int64_t* pidx, int64_t r, int64_t c, T* A, int64_t lda,
               int64_t ncols, int64_t* ipiv, int64_t ipiv_base, int64_t* perm, int* info, int64_t info_offset,
-              int64_t* piv_out, hipStream_t s);
+              int64_t* piv_out, hipStream_t s, double thresh = 1.0);
 template <typename T>
 void lu_update(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, rt<T>* pval, int64_t* pidx,
                hipStream_t s);

@@ -63,7 +63,7 @@ template <typename T>
 __global__ void lu_pivot_kernel(int nparts, const real_t<T>* pval, const int64_t* pidx,
                                 int64_t r, int64_t c, T* A, int64_t lda, int64_t ncols,
                                 int64_t* ipiv, int64_t ipiv_base, int64_t* perm,
-                                int* info, int64_t info_offset, int64_t* piv_out) {
+                                int* info, int64_t info_offset, int64_t* piv_out, real_t<T> thresh) {
     using R = real_t<T>;
     R v = -1; int64_t idx = INT64_MAX;
     for (int k = threadIdx.x; k < nparts; k += PT) {
@@ -74,6 +74,8 @@ __global__ void lu_pivot_kernel(int nparts, const real_t<T>* pval, const int64_t
     __shared__ int64_t p_sh;
     if (threadIdx.x == 0) {
         int64_t p = (idx == INT64_MAX) ? r : idx;
+        // threshold pivoting: keep the diagonal when |a_rc| >= thresh * max
+        if (thresh < R(1) && p != r && abs1(A[r + c * lda]) >= thresh * v) p = r;
         p_sh = p;
         ipiv[r] = ipiv_base + p;
         if (piv_out) *piv_out = p;
@@ -554,9 +556,9 @@ void lu_colmax(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c, real_t<
 template <typename T>
 void lu_pivot(int nparts, const real_t<T>* pval, const int64_t* pidx, int64_t r, int64_t c, T* A, int64_t lda,
               int64_t ncols, int64_t* ipiv, int64_t ipiv_base, int64_t* perm, int* info, int64_t info_offset,
-              int64_t* piv_out, hipStream_t s) {
+              int64_t* piv_out, hipStream_t s, double thresh) {
     hipLaunchKernelGGL(lu_pivot_kernel<T>, dim3(1), dim3(PT), 0, s, nparts, pval, pidx, r, c, A, lda, ncols,
-                       ipiv, ipiv_base, perm, info, info_offset, piv_out);
+                       ipiv, ipiv_base, perm, info, info_offset, piv_out, real_t<T>(thresh));
 }
 template <typename T>
 void lu_update(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda, real_t<T>* pval, int64_t* pidx,
@@ -661,7 +663,7 @@ void larft_small(int k, const T* tau, T* Tm, int64_t ldt, hipStream_t s) {
 #define SLATE_INST_PANEL(T)                                                                                 \
     template void lu_colmax<T>(int64_t, int64_t, const T*, int64_t, int64_t, real_t<T>*, int64_t*, int, hipStream_t); \
     template void lu_pivot<T>(int, const real_t<T>*, const int64_t*, int64_t, int64_t, T*, int64_t, int64_t,  \
-                              int64_t*, int64_t, int64_t*, int*, int64_t, int64_t*, hipStream_t);             \
+                              int64_t*, int64_t, int64_t*, int*, int64_t, int64_t*, hipStream_t, double);     \
     template void lu_update<T>(int64_t, int64_t, int64_t, int64_t, T*, int64_t, real_t<T>*, int64_t*, hipStream_t); \
     template void qr_colnorm<T>(int64_t, int64_t, const T*, int64_t, int64_t, real_t<T>*, T*, int, hipStream_t); \
     template void qr_reflect_dots<T>(int64_t, int64_t, int64_t, int64_t, T*, int64_t, int, const real_t<T>*,  \

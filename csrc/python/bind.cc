@@ -130,6 +130,10 @@ py::capsule export_local(BaseMatrix<T> const& A, Loc loc) {
 //------------------------------------------------------------------------------
 Options to_options(py::dict d) {
     Options o;
+    auto meth = [](py::handle v, Method (*parse)(std::string)) -> OptionValue {
+        if (py::isinstance<py::str>(v)) return OptionValue(int64_t(parse(v.cast<std::string>())));
+        return OptionValue(v.cast<int64_t>());
+    };
     for (auto kv : d) {
         std::string k = py::str(kv.first);
         py::handle v = kv.second;
@@ -147,12 +151,13 @@ Options to_options(py::dict d) {
         else if (k == "pivot_threshold") o[Option::PivotThreshold] = v.cast<double>();
         else if (k == "hold_local_workspace") o[Option::HoldLocalWorkspace] = v.cast<bool>();
         else if (k == "depth") o[Option::Depth] = v.cast<int64_t>();
-        else if (k == "method_gemm") o[Option::MethodGemm] = v.cast<int64_t>();
-        else if (k == "method_lu") o[Option::MethodLU] = v.cast<int64_t>();
-        else if (k == "method_trsm") o[Option::MethodTrsm] = v.cast<int64_t>();
-        else if (k == "method_gels") o[Option::MethodGels] = v.cast<int64_t>();
+        // methods: an int or the reference's names ("trsmA", "hemmC", "calu", ...)
+        else if (k == "method_gemm") o[Option::MethodGemm] = meth(v, MethodGemm::str2method);
+        else if (k == "method_lu") o[Option::MethodLU] = meth(v, MethodLU::str2method);
+        else if (k == "method_trsm") o[Option::MethodTrsm] = meth(v, MethodTrsm::str2method);
+        else if (k == "method_gels") o[Option::MethodGels] = meth(v, MethodGels::str2method);
         else if (k == "method_cholqr") o[Option::MethodCholQR] = v.cast<int64_t>();
-        else if (k == "method_hemm") o[Option::MethodHemm] = v.cast<int64_t>();
+        else if (k == "method_hemm") o[Option::MethodHemm] = meth(v, MethodHemm::str2method);
         else if (k == "method_eig") o[Option::MethodEig] = OptionValue(int64_t(v.cast<std::string>()[0]));
         else if (k == "print_verbose") o[Option::PrintVerbose] = v.cast<int64_t>();
         else if (k == "print_edge_items") o[Option::PrintEdgeItems] = v.cast<int64_t>();

@@ -212,6 +212,7 @@ using namespace internal;
 template <typename Ts, typename Td>
 void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
     trace::Block tb("copy");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -238,7 +239,7 @@ void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
     } else {
         redistribute_any<Ts, Td>(A, B, target, mask);
     }
-    B.storage()->update_origin();
+    internal::finish_origin(B, opts);
 }
 
 template <typename T>
@@ -249,6 +250,7 @@ void redistribute(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts) {
     trace::Block tb("add");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     slate_error_if_msg(!same_layout(A, B) || A.op() != B.op(), "add: matrices must share a layout");
@@ -257,12 +259,13 @@ void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts)
     LocalBlock<T> lbk = B.local(loc, true);
     lb::add(c, Uplo::General, la.m, la.n, alpha, la.ptr, la.ld, beta, lbk.ptr, lbk.ld);
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    B.storage()->update_origin();
+    internal::finish_origin(B, opts);
 }
 
 template <typename T>
 void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T>& B, Options const& opts) {
     trace::Block tb("tzadd");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     slate_error_if_msg(!same_layout(A, B), "add: matrices must share a layout");
@@ -281,12 +284,13 @@ void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T
         });
     });
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    B.storage()->update_origin();
+    internal::finish_origin(B, opts);
 }
 
 template <typename T>
 void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options const& opts) {
     trace::Block tb("scale");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -306,13 +310,14 @@ void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options con
         });
     }
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    A.storage()->update_origin();
+    internal::finish_origin(A, opts);
 }
 
 template <typename T>
 void scale_row_col(Equed equed, std::vector<real_type<T>> const& R, std::vector<real_type<T>> const& C,
                    Matrix<T>& A, Options const& opts) {
     trace::Block tb("scale_row_col");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -339,12 +344,13 @@ void scale_row_col(Equed equed, std::vector<real_type<T>> const& R, std::vector<
     } else {
         lb::scale_row_col(c, la.m, la.n, r.data(), cs.data(), la.ptr, la.ld);
     }
-    A.storage()->update_origin();
+    internal::finish_origin(A, opts);
 }
 
 template <typename T>
 void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
     trace::Block tb("set");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -375,12 +381,13 @@ void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
         });
     });
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    A.storage()->update_origin();
+    internal::finish_origin(A, opts);
 }
 
 template <typename T>
 void set(std::function<T(int64_t, int64_t)> const& value, BaseMatrix<T>& A, Options const&) {
     trace::Block tb("set_lambda");
+    internal::DriverScope ds_;
     // evaluated on the host instance, then marked modified
     auto& s = *A.storage();
     T* base = s.get(Loc::Host, true);
@@ -402,6 +409,7 @@ void set(std::function<T(int64_t, int64_t)> const& value, BaseMatrix<T>& A, Opti
 template <typename T>
 void gather(BaseMatrix<T> const& A, std::vector<T>& full, Options const& opts) {
     trace::Block tb("gather");
+    internal::DriverScope ds_;
     (void)opts;
     int64_t m = A.m(), n = A.n();
     full.assign(size_t(m) * n, T(0));
@@ -567,6 +575,7 @@ real_type<T> finish_norm(BaseMatrix<T> const& A, char kind, NormParts<T>& P) {
 template <typename T>
 real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
     trace::Block tb("norm");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     Target target = resolve_target(opts);
     // normalize: work in storage orientation; One<->Inf swap for transposed views
@@ -659,6 +668,7 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
 template <typename T>
 void colNorms(Norm in_norm, Matrix<T> const& A, real_type<T>* values, Options const& opts) {
     trace::Block tb("colNorms");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     Target target = resolve_target(opts);
     slate_error_if_msg(in_norm != Norm::Max, "colNorms: only Norm::Max is supported (as the reference)");

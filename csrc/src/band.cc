@@ -250,6 +250,7 @@ Matrix<T> band_dense(BaseMatrix<T> const& A, int64_t kl, int64_t ku, Options con
 template <typename T>
 int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts) {
     trace::Block tb("gbtrf");
+    internal::DriverScope ds_;
     const int64_t n = A.n(), kl = A.lowerBandwidth(), ku = A.upperBandwidth();
     slate_error_if_msg(A.m() != n, "gbtrf: square band matrix required");
     const int64_t ldab = 2 * kl + ku + 1, kv = kl + ku;
@@ -269,6 +270,7 @@ int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts) {
 template <typename T>
 void gbtrs(BandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
     trace::Block tb("gbtrs");
+    internal::DriverScope ds_;
     const int64_t n = A.n(), kl = A.lowerBandwidth(), ku_f = A.upperBandwidth();
     // after gbtrf the stored upper bandwidth is kl + ku (fill)
     const int64_t ku = std::max<int64_t>(ku_f - kl, 0);
@@ -284,6 +286,7 @@ void gbtrs(BandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options c
 template <typename T>
 int64_t gbsv(BandMatrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
     trace::Block tb("gbsv");
+    internal::DriverScope ds_;
     int64_t info = gbtrf(A, pivots, opts);
     if (info == 0) gbtrs(A, pivots, B, opts);
     return info;
@@ -292,6 +295,7 @@ int64_t gbsv(BandMatrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts
 template <typename T>
 int64_t pbtrf(HermitianBandMatrix<T>& A, Options const& opts) {
     trace::Block tb("pbtrf");
+    internal::DriverScope ds_;
     const int64_t n = A.n(), kd = A.bandwidth();
     const bool upper = A.uplo() == Uplo::Upper;
     // lower band storage ab(i - j, j) = L(i, j); an Upper matrix is read as U^H
@@ -306,6 +310,7 @@ int64_t pbtrf(HermitianBandMatrix<T>& A, Options const& opts) {
 template <typename T>
 void pbtrs(HermitianBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("pbtrs");
+    internal::DriverScope ds_;
     const int64_t n = A.n(), kd = A.bandwidth();
     const bool upper = A.uplo() == Uplo::Upper;
     std::vector<T> ab = upper ? gather_band<T>(A, 0, kd, 0, kd + 1, true) : gather_band<T>(A, kd, 0, 0, kd + 1);
@@ -318,6 +323,7 @@ void pbtrs(HermitianBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("pbsv");
+    internal::DriverScope ds_;
     int64_t info = pbtrf(A, opts);
     if (info == 0) pbtrs(A, B, opts);
     return info;
@@ -327,6 +333,7 @@ int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 void gbmm(T alpha, BandMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts) {
     trace::Block tb("gbmm");
+    internal::DriverScope ds_;
     Matrix<T> D = band_dense<T>(A, A.lowerBandwidth(), A.upperBandwidth(), opts);
     gemm(alpha, D, B, beta, C, opts);
 }
@@ -335,6 +342,7 @@ template <typename T>
 void hbmm(Side side, T alpha, HermitianBandMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
           Options const& opts) {
     trace::Block tb("hbmm");
+    internal::DriverScope ds_;
     const int64_t kd = A.bandwidth();
     Matrix<T> D = band_dense<T>(A, kd, kd, opts, true, A.uplo());
     if (side == Side::Left) gemm(alpha, D, B, beta, C, opts);
@@ -344,6 +352,7 @@ void hbmm(Side side, T alpha, HermitianBandMatrix<T> const& A, Matrix<T> const& 
 template <typename T>
 void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("tbsm");
+    internal::DriverScope ds_;
     Matrix<T> D = band_dense<T>(A, A.kl(), A.ku(), opts);
     TriangularMatrix<T> Tm(A.uplo(), A.diag(), D);
     trsm(side, alpha, Tm, B, opts);

@@ -12,7 +12,11 @@
 // herk/syrk/her2k/syr2k: a single local call on 1x1 grids; on larger grids a
 //   triangle-only SUMMA (tri_summa: diagonal tiles through the triangular MFMA
 //   GEMM, never the other triangle).  trmm (Left, NoTrans A): SUMMA that skips
-//   the zero part of each A panel.  hemm/symm: gemmC on the expanded operand.
+//   the zero part of each A panel.  hemm/symm: hemmC (SUMMA over the stored
+//   triangle, partial A^H B products reduced down process columns) or hemmA
+//   (stationary A, narrow B replicated, one world reduction); MethodHemm.
+// gemmA / trsmA / hemmA replicate the narrow operand on the device instead of
+//   moving A (reference method.hh select_algo: B.nt() < 2).
 #include "internal.hh"
 
 #include <numeric>
@@ -53,6 +57,54 @@ bool rows_conform(BaseMatrix<T> const& A, BaseMatrix<T> const& C) {
         if (A.tileMb(i) != C.tileMb(i) || A.srow_owner(i) != C.srow_owner(i)) return false;
     return true;
 }
+inline lb::Ctx ctx_for(Target t) { return t == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host(); }
+inline void sync_ctx(lb::Ctx const& c) { if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream)); }
+
+/// in-place sum over `comm` of a contiguous buffer (stream-ordered)
+template <typename T>
+inline void allreduce_sum(Comm& comm, T* buf, size_t count, lb::Ctx const& c) {
+    if (comm.size() == 1 || count == 0) return;
+    comm.allreduce(buf, buf, count, scalar_type<T>(), ReduceOp::Sum, c.loc(), c.stream);
+}
+
+/// Stationary-A building block: every process of the grid gets the whole
+/// (narrow) NoTrans matrix X in G (X.m() x X.n(), ld X.m()) -- zero fill,
+/// local tiles written at their global positions, one world allreduce --
+/// O(m n) traffic on the device, no host gather.
+template <typename T>
+void replicate(lb::Ctx const& c, BaseMatrix<T> const& X, T* G) {
+    const int64_t ldg = std::max<int64_t>(X.m(), 1);
+    lb::set(c, Uplo::General, X.m(), X.n(), T(0), T(0), G, ldg);
+    LocalBlock<T> lx = X.local(c.loc(), false);
+    auto& g = *X.grid();
+    for (int64_t i = 0; i < X.mt(); ++i) {
+        if (X.srow_owner(i) != g.myrow()) continue;
+        for (int64_t j = 0; j < X.nt(); ++j)
+            if (X.scol_owner(j) == g.mycol())
+                lb::copy2d(c, X.tileMb(i), X.tileNb(j), lx.ptr + lrow_of(X, i) + lcol_of(X, j) * lx.ld, lx.ld,
+                           G + grow_of(X, i) + gcol_of(X, j) * ldg, ldg);
+    }
+    allreduce_sum(g.world(), G, size_t(ldg) * X.n(), c);
+}
+
+/// rows of a replicated global G (ld ldg, n columns) at A's local row tiles
+/// (by_cols: at A's local column tiles) -> W (ld ldw); add = true adds W back
+/// into G instead (W -> G, G += W).
+template <typename T>
+void gather_local(lb::Ctx const& c, BaseMatrix<T> const& A, bool by_cols, T* G, int64_t ldg, int64_t n, T* W,
+                  int64_t ldw, bool add) {
+    auto& g = *A.grid();
+    const int64_t nt = by_cols ? A.nt() : A.mt();
+    for (int64_t t = 0; t < nt; ++t) {
+        if ((by_cols ? A.scol_owner(t) : A.srow_owner(t)) != (by_cols ? g.mycol() : g.myrow())) continue;
+        const int64_t sz = by_cols ? A.tileNb(t) : A.tileMb(t);
+        T* gp = G + (by_cols ? gcol_of(A, t) : grow_of(A, t));
+        T* wp = W + (by_cols ? lcol_of(A, t) : lrow_of(A, t));
+        if (add) lb::add(c, Uplo::General, sz, n, T(1), wp, ldw, T(1), gp, ldg);
+        else lb::copy2d(c, sz, n, gp, ldg, wp, ldw);
+    }
+}
+
 template <typename T>
 bool cols_conform(BaseMatrix<T> const& B, BaseMatrix<T> const& C) {
     if (B.op() != Op::NoTrans || !B.aligned() || !B.grid()->same_processes(*C.grid())) return false;
@@ -69,6 +121,7 @@ bool cols_conform(BaseMatrix<T> const& B, BaseMatrix<T> const& C) {
 template <typename T>
 void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix<T>& C, Options const& opts) {
     trace::Block tb("gemmC");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const int64_t la = option_la(opts);
     slate_error_if_msg(A_in.m() != C.m() || B_in.n() != C.n() || A_in.n() != B_in.m(), "gemm: dimension mismatch");
@@ -110,7 +163,7 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
                      beta, lc.ptr, lc.ld);
         });
         S.wait_all();
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
     if (kt == 0) {
@@ -120,7 +173,7 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
             lb::add(c, Uplo::General, lc.m, lc.n, T(0), lc.ptr, lc.ld, beta, lc.ptr, lc.ld);
             if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
         }
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
     const int R = int(std::max<int64_t>(2, la + 2));
@@ -163,57 +216,57 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
         });
     }
     S.wait_all();
-    C.storage()->update_origin();
+    internal::finish_origin(C, opts);
 }
 
 template <typename T>
 void gemmA(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix<T>& C, Options const& opts) {
     trace::Block tb("gemmA");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     auto gC = C.grid();
     if (gC->size() == 1) { gemmC(alpha, A_in, B_in, beta, C, opts); return; }
-    // stationary A: A conforms to C's rows; every process multiplies its
-    // local A block by the matching rows of B (B gathered, it is narrow),
-    // partial sums are reduced across the process row.
+    // stationary A: A conforms to C's rows; B (narrow) is replicated on the
+    // device with one world allreduce, every process multiplies its local A
+    // block by the rows of B matching its local columns, and the partial
+    // products are summed across the process row (reference src/gemmA.cc).
     BaseMatrix<T> A = A_in;
-    Matrix<T> Ac;
+    Matrix<T> Ac, Bc;
     if (!rows_conform(A, C)) {
         int64_t kb = A_in.nt() ? A_in.tileNb(0) : C.nb();
         Ac = materialize<T>(A_in, target, gC, C.mb(), kb, row0_owner(C), 0);
         A = Ac;
     }
-    std::vector<T> Bfull;
-    gather(B_in, Bfull, opts);
+    BaseMatrix<T> B = B_in;
+    if (B_in.op() != Op::NoTrans || !B_in.grid()->same_processes(*gC)) {
+        Bc = materialize<T>(B_in, target, gC, B_in.m() ? std::min<int64_t>(B_in.m(), A.mb()) : 1,
+                            std::max<int64_t>(B_in.n(), 1), 0, 0);
+        B = Bc;
+    }
     const int64_t k = A.n(), n = C.n();
     auto& g = *gC;
     const Loc loc = loc_of(target);
-    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    lb::Ctx c = ctx_for(target);
     LocalBlock<T> la_ = A.local(loc, false);
-    auto& sa = *A.storage();
-    // rows of B matching my local columns of A
-    std::vector<T> Bl(size_t(std::max<int64_t>(la_.n, 1)) * n);
-    for (int64_t jl = 0; jl < la_.n; ++jl) {
-        int64_t kg = l2g(A.lcol_begin() + jl, sa.nb, sa.crel(), g.q()) - A.col0();
-        for (int64_t j = 0; j < n; ++j) Bl[jl + j * la_.n] = Bfull[kg + j * k];
-    }
-    // partial P (my local rows x n) in host or device memory
-    Work<T> P(target, size_t(std::max<int64_t>(la_.m, 1)) * n), Bd(target, Bl.size());
-    if (c.dev()) device::memcpy_async(Bd.data(), Bl.data(), Bl.size() * sizeof(T), c.stream);
-    else std::copy(Bl.begin(), Bl.end(), Bd.data());
-    lb::gemm(c, Op::NoTrans, Op::NoTrans, la_.m, n, la_.n, T(1), la_.ptr, la_.ld,
-             Bd.data(), std::max<int64_t>(la_.n, 1), T(0), P.data(), std::max<int64_t>(la_.m, 1));
-    if (la_.n == 0) lb::set(c, Uplo::General, la_.m, n, T(0), T(0), P.data(), std::max<int64_t>(la_.m, 1));
-    g.row().allreduce(P.data(), P.data(), size_t(la_.m) * n, scalar_type<T>(), ReduceOp::Sum, loc, c.stream);
-    // owners of C's columns add alpha * P(:, their cols) + beta C
+    const int64_t ldbl = std::max<int64_t>(la_.n, 1), ldp = std::max<int64_t>(la_.m, 1);
+    Work<T> G(target, size_t(std::max<int64_t>(k, 1)) * std::max<int64_t>(n, 1));
+    Work<T> Bl(target, size_t(ldbl) * std::max<int64_t>(n, 1)), P(target, size_t(ldp) * std::max<int64_t>(n, 1));
+    replicate(c, B, G.data());
+    gather_local(c, A, true, G.data(), std::max<int64_t>(k, 1), n, Bl.data(), ldbl, false);
+    if (la_.n > 0)
+        lb::gemm(c, Op::NoTrans, Op::NoTrans, la_.m, n, la_.n, T(1), la_.ptr, la_.ld, Bl.data(), ldbl, T(0),
+                 P.data(), ldp);
+    else
+        lb::set(c, Uplo::General, la_.m, n, T(0), T(0), P.data(), ldp);
+    allreduce_sum(g.row(), P.data(), size_t(ldp) * n, c);
+    // owners of C's column tiles: C = alpha P(:, their cols) + beta C
     LocalBlock<T> lc = C.local(loc, true);
-    auto& sc = *C.storage();
-    for (int64_t jl = 0; jl < lc.n; ++jl) {
-        int64_t jg = l2g(C.lcol_begin() + jl, sc.nb, sc.crel(), g.q()) - C.col0();
-        lb::add(c, Uplo::General, lc.m, 1, alpha, P.data() + jg * std::max<int64_t>(la_.m, 1),
-                std::max<int64_t>(la_.m, 1), beta, lc.ptr + jl * lc.ld, lc.ld);
-    }
-    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    C.storage()->update_origin();
+    for (int64_t j = 0; j < C.nt(); ++j)
+        if (C.scol_owner(j) == g.mycol())
+            lb::add(c, Uplo::General, lc.m, C.tileNb(j), alpha, P.data() + gcol_of(C, j) * ldp, ldp, beta,
+                    lc.ptr + lcol_of(C, j) * lc.ld, lc.ld);
+    sync_ctx(c);
+    internal::finish_origin(C, opts);
 }
 
 template <typename T>
@@ -296,11 +349,83 @@ void trsm_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Ma
     S.wait_all();
 }
 
+/// Stationary-A triangular solve for narrow B (reference src/work/work_trsmA.cc):
+/// A never moves.  Each process keeps a partial-sum block W (its local rows x
+/// all columns of B); step k sums block row k of W across process row pk,
+/// the owner of A(k,k) solves it, broadcasts X(k) down its process column, and
+/// that column updates W(i) -= A(i,k) X(k) for its local rows.  Traffic per
+/// step is kb x n, instead of trsmB's A panel of (local rows) x kb.
+template <typename T>
+void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target) {
+    auto& g = *B.grid();
+    const int myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    LocalBlock<T> lbk = B.local(loc, true);
+    LocalBlock<T> lA = A.local(loc, false);
+    const int64_t mt = B.mt(), n = B.n(), mloc = lbk.m, ldw = std::max<int64_t>(mloc, 1);
+    Sched S(target);
+    Work<T> W(target, size_t(ldw) * std::max<int64_t>(n, 1)), X(target, size_t(ldw) * std::max<int64_t>(n, 1));
+    Work<T> WX(target, size_t(B.mb()) * std::max<int64_t>(n, 1));
+    const int64_t tW = Sched::tok(9, 0), tX = Sched::tok(8, 0);
+    // W = alpha B at B's global columns (zero elsewhere), X = 0
+    S.task(0, {}, {tW, tX}, [&](lb::Ctx const& c) {
+        lb::set(c, Uplo::General, mloc, n, T(0), T(0), W.data(), ldw);
+        lb::set(c, Uplo::General, mloc, n, T(0), T(0), X.data(), ldw);
+        for (int64_t j = 0; j < B.nt(); ++j)
+            if (B.scol_owner(j) == mycol)
+                lb::add(c, Uplo::General, mloc, B.tileNb(j), alpha, lbk.ptr + lcol_of(B, j) * lbk.ld, lbk.ld, T(1),
+                        W.data() + gcol_of(B, j) * ldw, ldw);
+    });
+    const bool lower = (uplo == Uplo::Lower);
+    for (int64_t t = 0; t < mt; ++t) {
+        const int64_t k = lower ? t : mt - 1 - t;
+        const int64_t kb = B.tileMb(k);
+        const int pk = B.srow_owner(k), qk = A.scol_owner(k);
+        const int64_t lrk = lrow_of(B, k);
+        S.task(device::kCommQueue, {tW}, {tW}, [&, kb, pk, lrk](lb::Ctx const& c) {
+            trace::Block t2("trsmA_reduce");
+            if (myrow != pk) return;
+            pack(c, kb, n, W.data() + lrk, ldw, WX.data());
+            allreduce_sum(g.row(), WX.data(), size_t(kb) * n, c);
+        });
+        S.task(0, {tW}, {tX}, [&, k, kb, pk, qk, lrk](lb::Ctx const& c) {
+            if (myrow != pk || mycol != qk) return;
+            lb::trsm(c, Side::Left, uplo, Op::NoTrans, diag, kb, n, T(1),
+                     lA.ptr + lrow_of(A, k) + lcol_of(A, k) * lA.ld, lA.ld, WX.data(), kb);
+            lb::copy2d(c, kb, n, WX.data(), kb, X.data() + lrk, ldw);
+        });
+        S.task(device::kCommQueue, {tX}, {tX}, [&, kb, pk, qk](lb::Ctx const& c) {
+            trace::Block t2("trsmA_bcast");
+            if (mycol == qk) bcast(g.col(), WX.data(), size_t(kb) * n, pk, c);
+        });
+        S.task(0, {tX}, {tW}, [&, k, kb, qk, lrk](lb::Ctx const& c) {
+            if (mycol != qk) return;
+            const int64_t r0 = lower ? lrow_of(B, k + 1) : 0, r1 = lower ? mloc : lrk;
+            if (r1 > r0)
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + r0 + lcol_of(A, k) * lA.ld,
+                         lA.ld, WX.data(), kb, T(1), W.data() + r0, ldw);
+        });
+    }
+    // X(k) sits on process column qk of block row k: sum across the process
+    // row, then each process keeps its own columns of B
+    S.task(device::kCommQueue, {tW}, {tX}, [&](lb::Ctx const& c) {
+        allreduce_sum(g.row(), X.data(), size_t(ldw) * n, c);
+    });
+    S.task(0, {tX}, {tW}, [&](lb::Ctx const& c) {
+        for (int64_t j = 0; j < B.nt(); ++j)
+            if (B.scol_owner(j) == mycol)
+                lb::copy2d(c, mloc, B.tileNb(j), X.data() + gcol_of(B, j) * ldw, ldw,
+                           lbk.ptr + lcol_of(B, j) * lbk.ld, lbk.ld);
+    });
+    S.wait_all();
+}
+
 }  // namespace
 
 template <typename T>
 void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("trsm");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     auto gB = B.grid();
@@ -311,9 +436,14 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         // A's logical op applied to its physical triangle
         lb::trsm(c, side, A.uplo_physical(), A.op(), A.diag(), lbk.m, lbk.n, alpha, lA.ptr, lA.ld, lbk.ptr, lbk.ld);
         if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-        B.storage()->update_origin();
+        internal::finish_origin(B, opts);
         return;
     }
+    // MethodTrsm (reference include/slate/method.hh:35-45): stationary A for a
+    // single block column of right-hand sides, else the trsmB sweep
+    Method method = get_option<int64_t>(opts, Option::MethodTrsm, MethodTrsm::Auto);
+    if (method == MethodTrsm::Auto) method = B.nt() < 2 ? MethodTrsm::TrsmA : MethodTrsm::TrsmB;
+    slate_error_if_msg(method != MethodTrsm::TrsmA && method != MethodTrsm::TrsmB, "trsm: unknown MethodTrsm");
     // distributed: reduce to Left, NoTrans, A conforming to B's rows
     if (side == Side::Right) {
         // X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T (use conj for ConjTrans pairs)
@@ -322,7 +452,9 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
                                       0, 0);
         TriangularMatrix<T> Ah = conj ? conj_transpose(A) : transpose(A);
         TriangularMatrix<T> At(Ah.uplo(), A.diag(), Ah);
-        trsm(Side::Left, conj ? slate::conj(alpha) : alpha, At, Bt, opts);
+        Options o2 = opts;
+        o2[Option::MethodTrsm] = method;
+        trsm(Side::Left, conj ? slate::conj(alpha) : alpha, At, Bt, o2);
         slate::copy<T, T>(conj ? conj_transpose(Bt) : transpose(Bt), B, opts);
         return;
     }
@@ -339,8 +471,9 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         Ac = materialize<T>(A, target, gB, B.mb(), B.mb(), row0_owner(B), 0);
         Ause = Ac;
     }
-    trsm_left_notrans(u, A.diag(), alpha, Ause, B, target, option_la(opts));
-    B.storage()->update_origin();
+    if (method == MethodTrsm::TrsmA) trsmA_left_notrans(u, A.diag(), alpha, Ause, B, target);
+    else trsm_left_notrans(u, A.diag(), alpha, Ause, B, target, option_la(opts));
+    internal::finish_origin(B, opts);
 }
 
 //------------------------------------------------------------------------------
@@ -350,8 +483,6 @@ namespace {
 template <typename T>
 bool local_only(BaseMatrix<T> const& A) { return A.grid()->size() == 1; }
 
-inline lb::Ctx ctx_for(Target t) { return t == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host(); }
-inline void sync_ctx(lb::Ctx const& c) { if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream)); }
 
 /// C(uplo) = alpha * G + beta * C(uplo) with G general (same layout as C)
 template <typename T>
@@ -465,7 +596,7 @@ void tri_summa(Uplo uplo, T alpha, BaseMatrix<T> const& A_in, BaseMatrix<T> cons
         });
     }
     S.wait_all();
-    C.storage()->update_origin();
+    internal::finish_origin(C, opts);
 }
 
 }  // namespace
@@ -473,6 +604,7 @@ void tri_summa(Uplo uplo, T alpha, BaseMatrix<T> const& A_in, BaseMatrix<T> cons
 template <typename T>
 void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMatrix<T>& C, Options const& opts) {
     trace::Block tb("herk");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(C) && local_only(A) && C.op() == Op::NoTrans) {
@@ -481,7 +613,7 @@ void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMa
         Op op = A.op() == Op::NoTrans ? Op::NoTrans : Op::ConjTrans;
         lb::herk(c, C.uplo(), op, lc.m, A.n(), alpha, la_.ptr, la_.ld, beta, lc.ptr, lc.ld);
         sync_ctx(c);
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
     if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
@@ -497,6 +629,7 @@ void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMa
 template <typename T>
 void syrk(T alpha, Matrix<T> const& A, T beta, SymmetricMatrix<T>& C, Options const& opts) {
     trace::Block tb("syrk");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(C) && local_only(A) && C.op() == Op::NoTrans) {
@@ -505,7 +638,7 @@ void syrk(T alpha, Matrix<T> const& A, T beta, SymmetricMatrix<T>& C, Options co
         Op op = A.op() == Op::NoTrans ? Op::NoTrans : Op::Trans;
         lb::syrk(c, C.uplo(), op, lc.m, A.n(), alpha, la_.ptr, la_.ld, beta, lc.ptr, lc.ld);
         sync_ctx(c);
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
     if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
@@ -522,6 +655,7 @@ template <typename T>
 void her2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, real_type<T> beta, HermitianMatrix<T>& C,
            Options const& opts) {
     trace::Block tb("her2k");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(C) && local_only(A) && local_only(B) && C.op() == Op::NoTrans && A.op() == B.op()) {
@@ -530,7 +664,7 @@ void her2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, real_type<T> beta, H
         Op op = A.op() == Op::NoTrans ? Op::NoTrans : Op::ConjTrans;
         lb::her2k(c, C.uplo(), op, lc.m, A.n(), alpha, la_.ptr, la_.ld, lbk.ptr, lbk.ld, beta, lc.ptr, lc.ld);
         sync_ctx(c);
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
     if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
@@ -548,6 +682,7 @@ void her2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, real_type<T> beta, H
 template <typename T>
 void syr2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, SymmetricMatrix<T>& C, Options const& opts) {
     trace::Block tb("syr2k");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(C) && local_only(A) && local_only(B) && C.op() == Op::NoTrans && A.op() == B.op()) {
@@ -556,7 +691,7 @@ void syr2k(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, SymmetricMat
         Op op = A.op() == Op::NoTrans ? Op::NoTrans : Op::Trans;
         lb::syr2k(c, C.uplo(), op, lc.m, A.n(), alpha, la_.ptr, la_.ld, lbk.ptr, lbk.ld, beta, lc.ptr, lc.ld);
         sync_ctx(c);
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
     if (C.op() == Op::NoTrans && C.aligned() && C.mb() == C.nb()) {
@@ -648,20 +783,192 @@ void trmm_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Ma
     S.wait_all();
 }
 
-/// full (dense) copy of a symmetric/Hermitian matrix on the same layout
+/// C = beta C, with beta = 0 overwriting (NaN-safe)
 template <typename T>
-Matrix<T> expand_sym(BaseTrapezoidMatrix<T> const& A, bool herm, Target target) {
-    Options o = {{Option::Target, target}};
-    Matrix<T> F = Matrix<T>(BaseMatrix<T>(A)).emptyLike();
-    F.insertLocalTiles(target);
-    // mirror: F = op(A) fully, then overwrite the stored triangle
-    Matrix<T> Ag{BaseMatrix<T>(A)};
-    Ag.set_uplo(Uplo::General);
-    slate::copy<T, T>(herm ? conj_transpose(Ag) : transpose(Ag), F, o);
-    BaseTrapezoidMatrix<T> Ft(A.uplo(), F, MatrixKind::Trapezoid);
-    BaseTrapezoidMatrix<T> At(A.uplo(), Ag, MatrixKind::Trapezoid);
-    slate::copy<T, T>(At, Ft, o);
-    return F;
+inline void scale_c(lb::Ctx const& c, T beta, int64_t m, int64_t n, T* C, int64_t ldc) {
+    if (beta == T(0)) lb::set(c, Uplo::General, m, n, T(0), T(0), C, ldc);
+    else if (beta != T(1)) lb::add(c, Uplo::General, m, n, T(0), C, ldc, beta, C, ldc);
+}
+
+/// hemmC / symmC, Left (reference src/hemmC.cc): SUMMA over the STORED
+/// triangle only.  With A = L + L_s^H (Lower; Upper mirrors it), step k
+/// broadcasts the stored part of column k along process rows and B(k,:) down
+/// process columns, then
+///   C(i,:) += A(i,k) B(k,:)           rows strictly inside the triangle,
+///   C(k,:) += hemm(A(k,k)) B(k,:)     diagonal tile,
+///   C(k,:) += sum_j A(j,k)^H B(j,:)   partial products on every process,
+///                                     summed over the process column.
+/// No n x n temporary and no transposed copy of A.  A: rows conform to C,
+/// column tiles = C's row tiles; B conforms to C.
+template <typename T>
+void hemmC_left(Uplo uplo, bool herm, T alpha, BaseMatrix<T> const& A, BaseMatrix<T> const& B, T beta,
+                Matrix<T>& C, Target target, int64_t la) {
+    auto& g = *C.grid();
+    const int myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    LocalBlock<T> lc = C.local(loc, true), lB = B.local(loc, false), lA = A.local(loc, false);
+    const int64_t kt = A.nt(), nloc = lc.n, mloc = lc.m, nb = C.mb();
+    const bool lower = (uplo == Uplo::Lower);
+    const Op opH = herm ? Op::ConjTrans : Op::Trans;
+    Sched S(target);
+    const int64_t tC = Sched::tok(9, 0);
+    S.task(0, {}, {tC}, [&](lb::Ctx const& c) { scale_c(c, beta, mloc, nloc, lc.ptr, lc.ld); });
+    const int R = int(std::max<int64_t>(2, la + 2));
+    std::vector<Work<T>> WA(R), WB(R), WP(R);
+    for (int r = 0; r < R; ++r) {
+        WA[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+        WB[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
+        WP[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
+    }
+    for (int64_t k = 0; k < kt; ++k) {
+        const int slot = int(k % R);
+        const int64_t kb = A.tileNb(k);
+        const int qk = A.scol_owner(k), pk = C.srow_owner(k);
+        const int64_t rk = lrow_of(C, k), rk1 = lrow_of(C, k + 1);
+        const int64_t lo = lower ? rk : 0, hi = lower ? mloc : rk1;   // stored rows of column k
+        const int64_t rs = lower ? rk1 : 0, re = lower ? mloc : rk;   // strictly off-diagonal rows
+        const int64_t nr = hi - lo, ldw = std::max<int64_t>(nr, 1);
+        T* WAk = WA[slot].data();
+        T* WBk = WB[slot].data();
+        T* WPk = WP[slot].data();
+        const int64_t tBc = Sched::bcast(slot), tP = Sched::tok(7, slot);
+        S.task(device::kCommQueue, {}, {tBc}, [&, k, kb, qk, pk, rk, lo, nr, WAk, WBk](lb::Ctx const& c) {
+            trace::Block t2("hemm_bcast");
+            if (nr > 0) {
+                if (mycol == qk) pack(c, nr, kb, lA.ptr + lo + lcol_of(A, k) * lA.ld, lA.ld, WAk);
+                bcast(g.row(), WAk, size_t(nr * kb), qk, c);
+            }
+            if (nloc > 0) {
+                if (myrow == pk) lb::copy2d(c, kb, nloc, lB.ptr + rk, lB.ld, WBk, kb);
+                bcast(g.col(), WBk, size_t(kb * nloc), pk, c);
+            }
+        });
+        S.task(0, {tBc}, {tC, tP}, [&, kb, pk, rk, lo, rs, re, ldw, WAk, WBk, WPk](lb::Ctx const& c) {
+            trace::Block t2("hemm_update");
+            if (nloc == 0) return;
+            if (myrow == pk)
+                lb::hemm(c, Side::Left, uplo, kb, nloc, alpha, WAk + (rk - lo), ldw, WBk, kb, T(1), lc.ptr + rk, lc.ld,
+                         herm);
+            if (re > rs) {
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, re - rs, nloc, kb, alpha, WAk + (rs - lo), ldw, WBk, kb, T(1),
+                         lc.ptr + rs, lc.ld);
+                lb::gemm(c, opH, Op::NoTrans, kb, nloc, re - rs, T(1), WAk + (rs - lo), ldw, lB.ptr + rs, lB.ld, T(0),
+                         WPk, kb);
+            } else {
+                lb::set(c, Uplo::General, kb, nloc, T(0), T(0), WPk, kb);
+            }
+        });
+        S.task(device::kCommQueue, {tP}, {tP}, [&, kb, WPk](lb::Ctx const& c) {
+            trace::Block t2("hemm_reduce");
+            allreduce_sum(g.col(), WPk, size_t(kb * nloc), c);
+        });
+        S.task(0, {tP}, {tC}, [&, kb, pk, rk, WPk](lb::Ctx const& c) {
+            if (myrow == pk && nloc > 0) lb::add(c, Uplo::General, kb, nloc, alpha, WPk, kb, T(1), lc.ptr + rk, lc.ld);
+        });
+    }
+    S.wait_all();
+}
+
+/// hemmA / symmA, Left (reference src/hemmA.cc): A stays where it is.  B
+/// (narrow) is replicated on the device; every process multiplies its stored
+/// tiles by the matching rows of B, both as A(i,j) B(j,:) into row i and as
+/// A(i,j)^H B(i,:) into row j, and one world allreduce sums the partial rows.
+/// C, B: any distribution (NoTrans); A: aligned, square diagonal tiles.
+template <typename T>
+void hemmA_left(Uplo uplo, bool herm, T alpha, BaseMatrix<T> const& A, BaseMatrix<T> const& B, T beta,
+                Matrix<T>& C, Target target) {
+    auto& g = *C.grid();
+    const int myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    lb::Ctx c = ctx_for(target);
+    LocalBlock<T> lA = A.local(loc, false), lc = C.local(loc, true);
+    const int64_t n = C.m(), nrhs = C.n(), mloc = lA.m, nloc = lA.n;
+    const int64_t ldg = std::max<int64_t>(n, 1), ldr = std::max<int64_t>(mloc, 1), ldq = std::max<int64_t>(nloc, 1);
+    const size_t w = size_t(std::max<int64_t>(nrhs, 1));
+    const bool lower = (uplo == Uplo::Lower);
+    const Op opH = herm ? Op::ConjTrans : Op::Trans;
+    Work<T> G(target, ldg * w), Br(target, ldr * w), Wr(target, ldr * w), Bq(target, ldq * w), Wq(target, ldq * w);
+    replicate(c, B, G.data());
+    gather_local(c, A, false, G.data(), ldg, nrhs, Br.data(), ldr, false);
+    gather_local(c, A, true, G.data(), ldg, nrhs, Bq.data(), ldq, false);
+    lb::set(c, Uplo::General, mloc, nrhs, T(0), T(0), Wr.data(), ldr);
+    lb::set(c, Uplo::General, nloc, nrhs, T(0), T(0), Wq.data(), ldq);
+    for (int64_t j = 0; j < A.nt(); ++j) {
+        if (A.scol_owner(j) != mycol) continue;
+        const int64_t cj = lcol_of(A, j), nbj = A.tileNb(j), rj = lrow_of(A, j), rj1 = lrow_of(A, j + 1);
+        T const* Aj = lA.ptr + cj * lA.ld;
+        if (A.srow_owner(j) == myrow)
+            lb::hemm(c, Side::Left, uplo, nbj, nrhs, T(1), Aj + rj, lA.ld, Bq.data() + cj, ldq, T(1),
+                     Wr.data() + rj, ldr, herm);
+        const int64_t rs = lower ? rj1 : 0, re = lower ? mloc : rj;
+        if (re > rs) {
+            lb::gemm(c, Op::NoTrans, Op::NoTrans, re - rs, nrhs, nbj, T(1), Aj + rs, lA.ld, Bq.data() + cj, ldq, T(1),
+                     Wr.data() + rs, ldr);
+            lb::gemm(c, opH, Op::NoTrans, nbj, nrhs, re - rs, T(1), Aj + rs, lA.ld, Br.data() + rs, ldr, T(1),
+                     Wq.data() + cj, ldq);
+        }
+    }
+    lb::set(c, Uplo::General, n, nrhs, T(0), T(0), G.data(), ldg);
+    gather_local(c, A, false, G.data(), ldg, nrhs, Wr.data(), ldr, true);
+    gather_local(c, A, true, G.data(), ldg, nrhs, Wq.data(), ldq, true);
+    allreduce_sum(g.world(), G.data(), ldg * size_t(nrhs), c);
+    for (int64_t i = 0; i < C.mt(); ++i) {
+        if (C.srow_owner(i) != myrow) continue;
+        for (int64_t j = 0; j < C.nt(); ++j) {
+            if (C.scol_owner(j) != mycol) continue;
+            T* cp = lc.ptr + lrow_of(C, i) + lcol_of(C, j) * lc.ld;
+            scale_c(c, beta, C.tileMb(i), C.tileNb(j), cp, lc.ld);
+            lb::add(c, Uplo::General, C.tileMb(i), C.tileNb(j), alpha, G.data() + grow_of(C, i) + gcol_of(C, j) * ldg,
+                    ldg, T(1), cp, lc.ld);
+        }
+    }
+    sync_ctx(c);
+}
+
+/// distributed hemm / symm: MethodHemm picks hemmA (narrow B) or hemmC;
+/// Right is reduced to Left on (conj-)transposed copies of B and C.
+template <typename T>
+void hemm_dist(Side side, bool herm, T alpha, BaseTrapezoidMatrix<T> const& A, Matrix<T> const& B, T beta,
+               Matrix<T>& C, Options const& opts) {
+    Target target = resolve_target(opts);
+    Method method = get_option<int64_t>(opts, Option::MethodHemm, MethodHemm::Auto);
+    if (method == MethodHemm::Auto) method = B.nt() < 2 ? MethodHemm::HemmA : MethodHemm::HemmC;
+    slate_error_if_msg(method != MethodHemm::HemmA && method != MethodHemm::HemmC, "hemm: unknown MethodHemm");
+    auto gC = C.grid();
+    if (side == Side::Right) {
+        // C = a B A + b C  <=>  C^H = conj(a) A B^H + conj(b) C^H (A = A^H), C^T = a A B^T + b C^T (A = A^T)
+        Matrix<T> Ct = materialize<T>(herm ? conj_transpose(C) : transpose(C), target, gC, C.nb(), C.mb(), 0, 0);
+        Matrix<T> Bt = materialize<T>(herm ? conj_transpose(B) : transpose(B), target, gC, C.nb(), C.mb(), 0, 0);
+        Options o2 = opts;
+        o2[Option::MethodHemm] = method;
+        hemm_dist(Side::Left, herm, herm ? slate::conj(alpha) : alpha, A, Bt, herm ? slate::conj(beta) : beta, Ct, o2);
+        slate::copy<T, T>(herm ? conj_transpose(Ct) : transpose(Ct), C, opts);
+        return;
+    }
+    // C must be a NoTrans aligned view; B and A conform to it (else copies)
+    Matrix<T> Cx, Bx, Ax;
+    Matrix<T>* Cu = &C;
+    const bool cdirect = C.op() == Op::NoTrans && C.aligned();
+    if (!cdirect) {
+        Cx = materialize<T>(C, target, gC, C.mb(), C.nb(), 0, 0);
+        Cu = &Cx;
+    }
+    BaseMatrix<T> Bu = B;
+    if (!(rows_conform(BaseMatrix<T>(B), BaseMatrix<T>(*Cu)) && cols_conform(BaseMatrix<T>(B), BaseMatrix<T>(*Cu)))) {
+        Bx = materialize<T>(B, target, gC, Cu->mb(), Cu->nb(), row0_owner(*Cu), col0_owner(*Cu));
+        Bu = Bx;
+    }
+    BaseMatrix<T> Au = A;
+    bool aconf = A.op() == Op::NoTrans && rows_conform(BaseMatrix<T>(A), BaseMatrix<T>(*Cu)) && A.nt() == Cu->mt();
+    if (aconf)
+        for (int64_t j = 0; j < A.nt(); ++j) if (A.tileNb(j) != Cu->tileMb(j)) aconf = false;
+    if (!aconf) {
+        Ax = materialize<T>(A, target, gC, Cu->mb(), Cu->mb(), row0_owner(*Cu), 0);
+        Au = Ax;
+    }
+    if (method == MethodHemm::HemmA) hemmA_left(A.uplo(), herm, alpha, Au, Bu, beta, *Cu, target);
+    else hemmC_left(A.uplo(), herm, alpha, Au, Bu, beta, *Cu, target, option_la(opts));
+    if (!cdirect) slate::copy<T, T>(Cx, C, opts);
 }
 
 }  // namespace
@@ -670,6 +977,7 @@ template <typename T>
 void hemm(Side side, T alpha, HermitianMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
           Options const& opts) {
     trace::Block tb("hemm");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(C) && local_only(A) && local_only(B) && C.op() == Op::NoTrans && B.op() == Op::NoTrans) {
@@ -678,18 +986,18 @@ void hemm(Side side, T alpha, HermitianMatrix<T> const& A, Matrix<T> const& B, T
         lb::hemm(c, side, A.uplo_physical(), lc.m, lc.n, alpha, la_.ptr, la_.ld, lbk.ptr, lbk.ld, beta,
                  lc.ptr, lc.ld, true);
         sync_ctx(c);
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
-    Matrix<T> F = expand_sym<T>(A, true, target);
-    if (side == Side::Left) gemmC(alpha, F, B, beta, C, opts);
-    else gemmC(alpha, B, F, beta, C, opts);
+    hemm_dist<T>(side, true, alpha, A, B, beta, C, opts);
+    internal::finish_origin(C, opts);
 }
 
 template <typename T>
 void symm(Side side, T alpha, SymmetricMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
           Options const& opts) {
     trace::Block tb("symm");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(C) && local_only(A) && local_only(B) && C.op() == Op::NoTrans && B.op() == Op::NoTrans) {
@@ -698,17 +1006,17 @@ void symm(Side side, T alpha, SymmetricMatrix<T> const& A, Matrix<T> const& B, T
         lb::hemm(c, side, A.uplo_physical(), lc.m, lc.n, alpha, la_.ptr, la_.ld, lbk.ptr, lbk.ld, beta,
                  lc.ptr, lc.ld, false);
         sync_ctx(c);
-        C.storage()->update_origin();
+        internal::finish_origin(C, opts);
         return;
     }
-    Matrix<T> F = expand_sym<T>(A, false, target);
-    if (side == Side::Left) gemmC(alpha, F, B, beta, C, opts);
-    else gemmC(alpha, B, F, beta, C, opts);
+    hemm_dist<T>(side, false, alpha, A, B, beta, C, opts);
+    internal::finish_origin(C, opts);
 }
 
 template <typename T>
 void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("trmm");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (local_only(B) && local_only(A) && B.op() == Op::NoTrans) {
@@ -717,7 +1025,7 @@ void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         lb::trmm(c, side, A.uplo_physical(), A.op(), A.diag(), lbk.m, lbk.n, alpha, la_.ptr, la_.ld,
                  lbk.ptr, lbk.ld);
         sync_ctx(c);
-        B.storage()->update_origin();
+        internal::finish_origin(B, opts);
         return;
     }
     // distributed: reduce to Left with a NoTrans triangle conforming to B's
@@ -744,7 +1052,7 @@ void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         Ause = Ac;
     }
     trmm_left_notrans<T>(A.uplo(), A.diag(), alpha, Ause, B, target, option_la(opts));
-    B.storage()->update_origin();
+    internal::finish_origin(B, opts);
 }
 
 //------------------------------------------------------------------------------

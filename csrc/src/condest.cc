@@ -111,6 +111,7 @@ int row0_src(BaseMatrix<T> const& A) { return A.srow_owner(0); }
 template <typename T>
 real_type<T> gecondest(Norm in_norm, Matrix<T>& A, real_type<T> Anorm, Options const& opts) {
     trace::Block tb("gecondest");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     slate_error_if_msg(in_norm != Norm::One && in_norm != Norm::Inf, "gecondest: norm must be One or Inf");
     const int64_t n = A.n();
@@ -142,6 +143,7 @@ real_type<T> gecondest(Norm in_norm, Matrix<T>& A, real_type<T> Anorm, Options c
 template <typename T>
 real_type<T> pocondest(Norm in_norm, HermitianMatrix<T>& A, real_type<T> Anorm, Options const& opts) {
     trace::Block tb("pocondest");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     slate_error_if_msg(in_norm != Norm::One && in_norm != Norm::Inf, "pocondest: norm must be One or Inf");
     const int64_t n = A.n();
@@ -164,6 +166,7 @@ real_type<T> pocondest(Norm in_norm, HermitianMatrix<T>& A, real_type<T> Anorm, 
 template <typename T>
 real_type<T> trcondest(Norm in_norm, TriangularMatrix<T>& A, Options const& opts) {
     trace::Block tb("trcondest");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     slate_error_if_msg(in_norm != Norm::One && in_norm != Norm::Inf, "trcondest: norm must be One or Inf");
     const int64_t n = A.n();

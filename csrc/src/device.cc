@@ -3,6 +3,7 @@
 
 #include <cstdlib>
 #include <algorithm>
+#include <deque>
 #include <string>
 
 namespace slate {
@@ -21,6 +22,10 @@ struct State {
     std::multimap<size_t, void*> free_blocks;
     std::map<void*, size_t> live;
     size_t in_use = 0, cached = 0;
+    // stream-ordered frees: a freed block is reusable once the work queued
+    // before the free on every queue (and the null stream) has drained
+    struct Pending { void* p; size_t b; std::vector<hipEvent_t> ev; };
+    std::deque<Pending> pending;
     std::map<void*, size_t> host_live;   // pinned host blocks
     size_t host_in_use = 0;
 };
@@ -96,6 +101,36 @@ void ensure_streams_locked(State& s) {
     s.streams_ready = true;
 }
 
+hipEvent_t event_get_locked(State& s) {
+    if (!s.events.empty()) {
+        hipEvent_t e = s.events.back();
+        s.events.pop_back();
+        return e;
+    }
+    hipEvent_t e;
+    slate_hip_call(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    return e;
+}
+
+/// move pending frees whose events have completed to the free lists
+/// (wait: block until all of them have)
+void reclaim_locked(State& s, bool wait) {
+    for (auto it = s.pending.begin(); it != s.pending.end();) {
+        bool done = true;
+        for (hipEvent_t e : it->ev) {
+            if (wait) { slate_hip_call(hipEventSynchronize(e)); continue; }
+            hipError_t r = hipEventQuery(e);
+            if (r == hipErrorNotReady) { done = false; break; }
+            slate_hip_call(r);
+        }
+        if (!done) { ++it; continue; }
+        for (hipEvent_t e : it->ev) s.events.push_back(e);
+        s.free_blocks.emplace(it->b, it->p);
+        s.cached += it->b;
+        it = s.pending.erase(it);
+    }
+}
+
 }  // namespace
 
 int reserved_cus() { return st().reserved_cus; }
@@ -146,14 +181,7 @@ hipEvent_t event_get() {
     auto& s = st();
     std::lock_guard<std::mutex> g(s.mtx);
     ensure_device_locked(s);
-    if (!s.events.empty()) {
-        hipEvent_t e = s.events.back();
-        s.events.pop_back();
-        return e;
-    }
-    hipEvent_t e;
-    slate_hip_call(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    return e;
+    return event_get_locked(s);
 }
 
 void event_put(hipEvent_t e) {
@@ -166,6 +194,7 @@ void* malloc(size_t bytes) {
     auto& s = st();
     std::lock_guard<std::mutex> g(s.mtx);
     ensure_device_locked(s);
+    if (!s.pending.empty()) reclaim_locked(s, false);
     size_t b = bucket(bytes);
     auto it = s.free_blocks.find(b);
     void* p = nullptr;
@@ -178,6 +207,7 @@ void* malloc(size_t bytes) {
         if (e != hipSuccess) {
             // release the cache and retry once
             (void)hipGetLastError();
+            reclaim_locked(s, true);
             for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
             s.free_blocks.clear();
             s.cached = 0;
@@ -198,13 +228,28 @@ void free(void* ptr) {
     size_t b = it->second;
     s.live.erase(it);
     s.in_use -= b;
-    s.free_blocks.emplace(b, ptr);
-    s.cached += b;
+    if (!s.streams_ready) {
+        // no queue ever ran: only synchronous (null-stream) use is possible
+        slate_hip_call(hipStreamSynchronize(nullptr));
+        s.free_blocks.emplace(b, ptr);
+        s.cached += b;
+        return;
+    }
+    // free on events: work already queued on any queue may still read the block
+    State::Pending pd{ptr, b, {}};
+    pd.ev.reserve(kNumQueues + 1);
+    for (int i = 0; i <= kNumQueues; ++i) {
+        hipEvent_t e = event_get_locked(s);
+        slate_hip_call(hipEventRecord(e, i < kNumQueues ? s.streams[i] : nullptr));
+        pd.ev.push_back(e);
+    }
+    s.pending.push_back(std::move(pd));
 }
 
 void release_cache() {
     auto& s = st();
     std::lock_guard<std::mutex> g(s.mtx);
+    reclaim_locked(s, true);
     for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
     s.free_blocks.clear();
     s.cached = 0;

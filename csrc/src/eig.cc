@@ -54,6 +54,7 @@ bool wanted(Matrix<T> const& M) { return M.m() > 0 && M.n() > 0; }
 template <typename T>
 void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& opts) {
     trace::Block tb("he2hb");
+    internal::DriverScope ds_;
     const int64_t nt = A.nt();
     Ts.assign(std::max<int64_t>(nt - 1, 0), {});
     for (int64_t k = 0; k + 1 < nt; ++k) {
@@ -68,6 +69,7 @@ void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& o
 template <typename T>
 void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts) {
     trace::Block tb("heev");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     const int64_t n = A.n(), nb = A.nb(), nt = A.nt();
     Lambda.assign(n, R(0));
@@ -141,6 +143,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
 template <typename T>
 void hegst(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T> const& B, Options const& opts) {
     trace::Block tb("hegst");
+    internal::DriverScope ds_;
     slate_error_if_msg(itype < 1 || itype > 3, "hegst: itype must be 1, 2 or 3");
     Target target = resolve_target(opts);
     Matrix<T> F = hermitian_full(A, opts);
@@ -170,6 +173,7 @@ template <typename T>
 void hegv(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_type<T>>& Lambda,
           Matrix<T>& Z, Options const& opts) {
     trace::Block tb("hegv");
+    internal::DriverScope ds_;
     int64_t info = potrf(B, opts);
     slate_error_if_msg(info != 0, "hegv: B is not positive definite");
     hegst(itype, A, B, opts);
@@ -190,6 +194,7 @@ template <typename T>
 void ge2tb(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<TriangularFactors<T>>& TV,
            Options const& opts) {
     trace::Block tb("ge2tb");
+    internal::DriverScope ds_;
     const int64_t mt = A.mt(), nt = A.nt();
     TU.assign(nt, {});
     TV.assign(std::max<int64_t>(nt - 1, 0), {});
@@ -212,6 +217,7 @@ void ge2tb(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<Tria
 template <typename T>
 void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts) {
     trace::Block tb("svd");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     Target target = resolve_target(opts);
     const int64_t m = A.m(), n = A.n();

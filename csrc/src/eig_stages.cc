@@ -79,6 +79,7 @@ template <typename T>
 void hb2st(HermitianBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E,
            BandReflectors<T>& V, Options const& opts) {
     trace::Block tb("hb2st");
+    internal::DriverScope ds_;
     const int64_t n = A.n(), kd = A.bandwidth();
     std::vector<T> full = replicate(A, opts);
     const bool lower = A.uplo() == Uplo::Lower;
@@ -97,6 +98,7 @@ void hb2st(HermitianBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector<
 template <typename T>
 void unmtr_hb2st(Side side, Op op, BandReflectors<T> const& V, Matrix<T>& C, Options const& opts) {
     trace::Block tb("unmtr_hb2st");
+    internal::DriverScope ds_;
     apply_band_reflectors(side, op, V, C, opts);
 }
 
@@ -104,6 +106,7 @@ template <typename T>
 void unmtr_he2hb(Side side, Op op, Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Matrix<T>& C,
                  Options const& opts) {
     trace::Block tb("unmtr_he2hb");
+    internal::DriverScope ds_;
     const int64_t nt = A.nt();
     // Q = Q_0 Q_1 ... Q_{nt-2}; Q_k acts on block rows k+1..nt-1
     auto apply = [&](int64_t k, Op o) {
@@ -125,6 +128,7 @@ template <typename T>
 void tb2bd(TriangularBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E,
            BandReflectors<T>& U, BandReflectors<T>& V, Options const& opts) {
     trace::Block tb("tb2bd");
+    internal::DriverScope ds_;
     slate_error_if_msg(A.uplo() != Uplo::Upper, "tb2bd: A must be upper triangular band");
     const int64_t m = A.m(), n = A.n(), kd = A.bandwidth();
     std::vector<T> full = replicate(A, opts);
@@ -139,6 +143,7 @@ void tb2bd(TriangularBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector
 template <typename T>
 void unmbr_tb2bd(Side side, Op op, BandReflectors<T> const& V, Matrix<T>& C, Options const& opts) {
     trace::Block tb("unmbr_tb2bd");
+    internal::DriverScope ds_;
     apply_band_reflectors(side, op, V, C, opts);
 }
 
@@ -146,6 +151,7 @@ template <typename T>
 void unmbr_ge2tb(Side side, Op op, Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Matrix<T>& C,
                  Options const& opts) {
     trace::Block tb("unmbr_ge2tb");
+    internal::DriverScope ds_;
     const int64_t mt = A.mt(), nt = A.nt();
     if (side == Side::Left) {
         // U = QU_0 ... QU_{nt-1}; QU_k = block-column k's QR reflectors
@@ -173,6 +179,7 @@ void unmbr_ge2tb(Side side, Op op, Matrix<T>& A, std::vector<TriangularFactors<T
 template <typename R>
 void sterf(std::vector<R>& D, std::vector<R>& E, Options const&) {
     trace::Block tb("sterf");
+    internal::DriverScope ds_;
     host::sterf<R>(int64_t(D.size()), D.data(), E.data());
 }
 
@@ -180,6 +187,7 @@ template <typename T>
 void steqr2(Job jobz, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E, Matrix<T>& Z,
             Options const& opts) {
     trace::Block tb("steqr2");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     const int64_t n = int64_t(D.size());
     if (jobz == Job::NoVec || !wanted(Z)) {
@@ -198,6 +206,7 @@ void steqr2(Job jobz, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E
 template <typename R>
 void stedc(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const&) {
     trace::Block tb("stedc");
+    internal::DriverScope ds_;
     const int64_t n = int64_t(D.size());
     std::vector<R> h(size_t(n) * n);
     host::stedc<R>(n, D.data(), E.data(), h.data(), n);
@@ -207,6 +216,7 @@ void stedc(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const&) {
 template <typename R>
 void stedc_solve(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const& opts) {
     trace::Block tb("stedc_solve");
+    internal::DriverScope ds_;
     const int64_t n = int64_t(D.size());
     std::vector<R> ee(E.begin(), E.end());
     ee.resize(std::max<int64_t>(n, 1), R(0));
@@ -265,6 +275,7 @@ template <typename T>
 void bdsqr(Job jobu, Job jobvt, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E, Matrix<T>& U,
            Matrix<T>& VT, Options const& opts) {
     trace::Block tb("bdsqr");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     const int64_t n = int64_t(D.size());
     const bool wu = jobu != Job::NoVec && wanted(U), wv = jobvt != Job::NoVec && wanted(VT);
@@ -346,6 +357,7 @@ void gels_qr(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options cons
 template <typename T>
 void gels_cholqr(Matrix<T>& A, Matrix<T>& R, Matrix<T>& BX, Options const& opts) {
     trace::Block tb("gels_cholqr");
+    internal::DriverScope ds_;
     // A = Q R with CholeskyQR; X = R^{-1} (Q^H B)   (m >= n)
     const int64_t m = A.m(), n = A.n(), nrhs = BX.n();
     slate_error_if_msg(m < n, "gels_cholqr: requires m >= n");

@@ -193,11 +193,21 @@ enum class PanelMode { Partial, Tournament, NoPiv };
 /// columns are processed in chunks so the all-reduce of chunk c+1 overlaps the
 /// GEMM of chunk c.  The interchanges of the left columns [0, k) are applied
 /// one step late, behind the next panel's messages on the comm queue.
+/// Option::PivotThreshold in (0, 1] (reference src/getrf.cc:39): partial
+/// pivoting keeps the diagonal while |a_jj| >= threshold * column max
+inline double pivot_threshold(Options const& opts) {
+    double t = get_option<double>(opts, Option::PivotThreshold, 1.0);
+    slate_error_if_msg(!(t > 0.0 && t <= 1.0), "PivotThreshold must be in (0, 1]");
+    return t;
+}
+
 template <typename T>
 int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelMode mode, Target target) {
     using namespace internal::ludist;
     trace::Block tb("getrf_dist");
+    internal::DriverScope ds_;
     const int64_t la = get_option<int64_t>(opts, Option::Lookahead, 1);
+    const double thresh = pivot_threshold(opts);
     auto& g = *A.grid();
     const int p = g.p(), myrow = g.myrow(), mycol = g.mycol();
     const Loc loc = loc_of(target);
@@ -422,7 +432,7 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
                         }
                     };
                     walk(true);
-                    lb::getrf_panel(c, M, kb, Gfull.data(), M, pip.data(), (int64_t*)nullptr, info_real, kk, true, false);
+                    lb::getrf_panel(c, M, kb, Gfull.data(), M, pip.data(), (int64_t*)nullptr, info_real, kk, true, false, thresh);
                     walk(false);
                     lb::copy2d(c, kd, kb, Gfull.data(), M, LUk, kd);
                 });
@@ -552,7 +562,7 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
     }
     int64_t info = fetch_info(target, info_real);
     info = reduce_info(info, g.world());
-    A.storage()->update_origin();
+    internal::finish_origin(A, opts);
     (void)n;
     return info;
 }
@@ -560,8 +570,10 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
 template <typename T>
 int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMode mode) {
     trace::Block tb("getrf");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const int64_t la = get_option<int64_t>(opts, Option::Lookahead, 1);
+    const double thresh = pivot_threshold(opts);
     slate_error_if_msg(A_in.op() != Op::NoTrans, "getrf: NoTrans view required");
     slate_error_if_msg(!A_in.aligned(), "getrf: tile-aligned matrix required");
     slate_error_if_msg(A_in.mb() != A_in.nb(), "getrf: square tiles required");
@@ -621,7 +633,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             S.task(1, {}, {Sched::col(k), tPanel}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pv_dst, pv_src](lb::Ctx const& c) {
                 trace::Block t2("getrf_panel");
                 T* ap = a + lr_k + lc_k * lda;
-                lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot, tnt);
+                lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot, tnt, thresh);
                 if (c.dev()) {
                     slate_amd::dev::perm_pairs(kd, perm.data(), pv_ipiv, pv_dst, pv_src, c.stream);
                 } else {
@@ -749,7 +761,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     }
     int64_t info = fetch_info(target, dinfo.data());
     info = reduce_info(info, g.world());
-    A.storage()->update_origin();
+    internal::finish_origin(A, opts);
     return info;
 }
 

@@ -151,6 +151,7 @@ bool gmres_ir(int64_t n, std::vector<T> const& b, std::vector<T>& x, real_type<T
 template <typename T>
 int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
     trace::Block tb("gesv_mixed_gmres");
+    internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;
     slate_error_if_msg(B.n() != 1, "gesv_mixed_gmres: one right-hand side");
     Target target = resolve_target(opts);
@@ -198,6 +199,7 @@ int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& 
 template <typename T>
 int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
     trace::Block tb("posv_mixed_gmres");
+    internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;
     slate_error_if_msg(B.n() != 1, "posv_mixed_gmres: one right-hand side");
     Target target = resolve_target(opts);

@@ -176,6 +176,7 @@ std::vector<T> gather_lower(HermitianMatrix<T> const& A, Options const& opts) {
 template <typename T>
 int64_t hetrf(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Options const& opts) {
     trace::Block tb("hetrf");
+    internal::DriverScope ds_;
     const int64_t n = A.n();
     std::vector<T> a = gather_lower(A, opts);
     ipiv.assign(n, 0);
@@ -196,6 +197,7 @@ int64_t hetrf(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Options const& 
 template <typename T>
 void hetrs(HermitianMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix<T>& B, Options const& opts) {
     trace::Block tb("hetrs");
+    internal::DriverScope ds_;
     const int64_t n = A.n(), nrhs = B.n();
     std::vector<T> a = gather_lower(A, opts);
     std::vector<T> b;
@@ -209,6 +211,7 @@ void hetrs(HermitianMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix
 template <typename T>
 int64_t hesv(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Options const& opts) {
     trace::Block tb("hesv");
+    internal::DriverScope ds_;
     int64_t info = hetrf(A, ipiv, opts);
     if (info == 0) hetrs(A, ipiv, B, opts);
     return info;

@@ -97,6 +97,28 @@ inline Target resolve_target(Options const& opts) {
     return t;
 }
 
+/// Driver nesting depth on this thread.  Option::HoldLocalWorkspace = false
+/// (the default, reference src/potrf.cc:42,198) frees a matrix's non-origin
+/// instance -- the device copy of a host-origin matrix, i.e. SLATE's
+/// workspace tiles -- when the OUTERMOST driver finishes, so composite drivers
+/// (gesv = getrf + getrs, posv, gels, ...) keep it between their stages.
+inline int& driver_depth() { thread_local int d = 0; return d; }
+struct DriverScope {
+    DriverScope() { ++driver_depth(); }
+    ~DriverScope() { --driver_depth(); }
+    DriverScope(DriverScope const&) = delete;
+    DriverScope& operator=(DriverScope const&) = delete;
+};
+
+/// End of a driver for an output matrix: write back to the origin instance
+/// (tileUpdateAllOrigin) and release the workspace instance unless held.
+template <typename T>
+inline void finish_origin(BaseMatrix<T> const& A, Options const& opts) {
+    A.storage()->update_origin();
+    if (driver_depth() <= 1 && !get_option<bool>(opts, Option::HoldLocalWorkspace, false))
+        A.storage()->release_workspace();
+}
+
 /// Broadcast a contiguous buffer over `comm` from `root` (stream-ordered).
 template <typename T>
 inline void bcast(Comm& comm, T* buf, size_t count, int root, lb::Ctx const& c) {

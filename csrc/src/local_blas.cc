@@ -421,6 +421,7 @@ struct LuPanelDev {
     int* info; int64_t info_offset;
     real_type<T>* pval; int64_t* pidx;
     bool pivot, tournament;
+    double thresh;
     int64_t* tws;
     Ctx ctx;
 
@@ -438,7 +439,7 @@ struct LuPanelDev {
         for (int64_t j = 0; j < kmax; ++j) {
             int64_t col = c0 + j;
             kd::lu_pivot<DT>(pivot ? nparts : 0, pval, pidx, col, col, A, lda, ncols, ipiv, 0, perm, info,
-                             info_offset, nullptr, s);
+                             info_offset, nullptr, s, thresh);
             // update columns (col, c0+nn); deferred scaling of column col-1
             kd::lu_update2d<DT>(m, col, col, c0 + nn, A, lda, pval, pidx, j > 0 ? 1 : 0, s);
             nparts = int(ceildiv(m - col, 256));
@@ -467,11 +468,11 @@ struct LuPanelDev {
 
 template <typename T>
 void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t* ipiv, int64_t* perm,
-                 int* info, int64_t info_offset, bool pivot, bool tournament) {
+                 int* info, int64_t info_offset, bool pivot, bool tournament, double pivot_threshold) {
     if (m <= 0 || n <= 0) return;
     if (!c.dev()) {
         std::vector<int64_t> piv(std::min(m, n));
-        int64_t r = host::getrf(m, n, A, lda, piv.data(), pivot);
+        int64_t r = host::getrf(m, n, A, lda, piv.data(), pivot, pivot_threshold);
         if (r != 0 && info && *info == 0) *info = int(info_offset + r);
         for (size_t j = 0; j < piv.size(); ++j) ipiv[j] = piv[j];
         if (perm) {
@@ -484,6 +485,7 @@ void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t*
     LuPanelDev<T> P;
     P.s = c.stream; P.m = m; P.ncols = n; P.A0 = A; P.lda = lda; P.ipiv = ipiv; P.perm = perm;
     P.info = info; P.info_offset = info_offset; P.pivot = pivot; P.tournament = tournament; P.ctx = c;
+    P.thresh = pivot_threshold;
     P.tws = tournament ? sc.alloc<int64_t>(size_t(kd::tslu_workspace(m))) : nullptr;
     int64_t np = ceildiv(m, 256) + 1;
     P.pval = sc.alloc<real_type<T>>(np);
@@ -898,7 +900,7 @@ void copy2d(Ctx const& c, int64_t m, int64_t n, T const* src, int64_t lds, T* ds
     template void trtri<T>(Ctx const&, Uplo, Diag, int64_t, T*, int64_t);                                 \
     template void trtri_to<T>(Ctx const&, Uplo, Diag, int64_t, T const*, int64_t, T*, int64_t);           \
     template void lauum<T>(Ctx const&, Uplo, int64_t, T*, int64_t);                                        \
-    template void getrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, int64_t*, int64_t*, int*, int64_t, bool, bool); \
+    template void getrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, int64_t*, int64_t*, int*, int64_t, bool, bool, double); \
     template void apply_perm<T>(Ctx const&, int64_t, int64_t const*, int64_t const*, int64_t, T*, int64_t); \
     template void geqrf_panel<T>(Ctx const&, int64_t, int64_t, T*, int64_t, T*, T*, int64_t);             \
     template void larfb<T>(Ctx const&, Side, Op, int64_t, int64_t, int64_t, T const*, int64_t, T const*, int64_t, T*, int64_t); \

@@ -281,6 +281,7 @@ template <typename T>
 void generate_matrix(MatgenParams& params, Matrix<T>& A, std::vector<real_type<T>>& Sigma, Options const& opts) {
     using R = real_type<T>;
     trace::Block tb("generate_matrix");
+    internal::DriverScope ds_;
     Target target = internal::resolve_target(opts);
     Decoded d = decode<R>(params, A.m(), A.n());
     const int64_t m = A.m(), n = A.n(), k = std::min(m, n);
@@ -414,6 +415,7 @@ void generate_matrix(MatgenParams& params, BaseTrapezoidMatrix<T>& A, std::vecto
 template <typename T>
 void generate_matrix(std::string const& kind, BaseMatrix<T>& A, uint64_t seed, double shift, Options const& opts) {
     trace::Block tb("generate_matrix");
+    internal::DriverScope ds_;
     Target target = internal::resolve_target(opts);
     gen::Spec sp = base_spec(gen::Rands, seed);
     if (shift < 0) shift = double(std::max(A.m(), A.n()));

@@ -197,6 +197,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
 template <typename T>
 int64_t potrf(HermitianMatrix<T>& A_in, Options const& opts) {
     trace::Block tb("potrf");
+    internal::DriverScope ds_;
     Target target = internal::resolve_target(opts);
     int64_t la = get_option<int64_t>(opts, Option::Lookahead, 1);
     BaseMatrix<T> A = A_in;
@@ -214,7 +215,7 @@ int64_t potrf(HermitianMatrix<T>& A_in, Options const& opts) {
         Matrix<T> Ad(A);
         slate::copy<T, T>(conj_transpose(Ah), Ad, opts);
     }
-    A.storage()->update_origin();
+    internal::finish_origin(A, opts);
     return info;
 }
 

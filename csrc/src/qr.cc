@@ -380,6 +380,7 @@ void unmqr_left(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Targe
 template <typename T>
 void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
     trace::Block tb("geqrf");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     int64_t la = get_option<int64_t>(opts, Option::Lookahead, 1);
     slate_error_if_msg(A.op() != Op::NoTrans || !A.aligned() || A.mb() != A.nb(),
@@ -389,6 +390,7 @@ void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
     set(T(0), T(0), Tf, opts);
     geqrf_impl<T>(A, Tf, target, la);
     if (target == Target::Devices) lb::check_panel_errors();
+    internal::finish_origin(A, opts);
     T_.clear();
     T_.push_back(Tf);
 }
@@ -396,6 +398,7 @@ void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
 template <typename T>
 void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C, Options const& opts) {
     trace::Block tb("unmqr");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     slate_error_if_msg(T_.empty(), "unmqr: missing T factors");
     if (is_complex_v<T> == false && op == Op::ConjTrans) op = Op::Trans;
@@ -410,6 +413,7 @@ void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
                 if (A.tileMb(i) != C.tileMb(i) || A.srow_owner(i) != C.srow_owner(i)) { conform = false; break; }
         if (conform) {
             unmqr_left<T>(op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans, A, T_[0], C, target);
+            internal::finish_origin(C, opts);
         } else {
             Matrix<T> Cx(C.m(), C.n(), A.mb(), C.nb(), A.grid(), A.mt() ? A.srow_owner(0) : 0, 0);
             Cx.insertLocalTiles(target);
@@ -435,6 +439,7 @@ void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
 template <typename T>
 void gelqf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
     trace::Block tb("gelqf");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     Matrix<T> Ah = A.emptyLike(0, 0, Op::ConjTrans);
     Ah.insertLocalTiles(target);
@@ -446,6 +451,7 @@ void gelqf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
 template <typename T>
 void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C, Options const& opts) {
     trace::Block tb("unmlq");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     // Q = Q'^H where Q' is the QR factor of A^H
     Matrix<T> Ah = A.emptyLike(0, 0, Op::ConjTrans);
@@ -458,6 +464,7 @@ void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
 template <typename T>
 void gels(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options const& opts) {
     trace::Block tb("gels");
+    internal::DriverScope ds_;
     const int64_t m = A.m(), n = A.n(), nrhs = BX.n();
     Method method = get_option<int64_t>(opts, Option::MethodGels, MethodGels::Geqrf);
     if (m >= n) {
@@ -500,6 +507,7 @@ void gels(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options const& 
 template <typename T>
 int64_t cholqr(Matrix<T>& A, Matrix<T>& R, Options const& opts) {
     trace::Block tb("cholqr");
+    internal::DriverScope ds_;
     // R^H R = A^H A ; Q = A R^{-1} (reference src/cholqr.cc)
     Target target = resolve_target(opts);
     (void)target;

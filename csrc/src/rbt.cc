@@ -86,6 +86,7 @@ Matrix<T> butterfly_matrix(int64_t n, int64_t nb, GridPtr grid, int depth, uint6
 template <typename T>
 void gerbt(Matrix<T>& A, int depth, uint64_t seed_u, uint64_t seed_v, Options const& opts) {
     trace::Block tb("gerbt");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const int64_t n = A.n();
     Matrix<T> U = butterfly_matrix<T>(A.m(), A.mb(), A.grid(), depth, seed_u, target);
@@ -99,6 +100,7 @@ void gerbt(Matrix<T>& A, int depth, uint64_t seed_u, uint64_t seed_v, Options co
 template <typename T>
 int64_t gesv_rbt(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
     trace::Block tb("gesv_rbt");
+    internal::DriverScope ds_;
     using R = real_type<T>;
     Target target = resolve_target(opts);
     const int depth = int(get_option<int64_t>(opts, Option::Depth, 2));

@@ -30,6 +30,7 @@ TriangularMatrix<T> tri(Uplo u, Diag d, BaseMatrix<T> const& A) {
 template <typename T>
 void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
     trace::Block tb("getrs");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     apply_pivots(pivots, A, B, target, true);
     trsm(Side::Left, T(1), tri<T>(Uplo::Lower, Diag::Unit, A), B, opts);
@@ -42,6 +43,7 @@ template <typename T>
 void getrs(Op trans, Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
     if (trans == Op::NoTrans) { getrs(A, pivots, B, opts); return; }
     trace::Block tb("getrs_trans");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     auto L = tri<T>(Uplo::Lower, Diag::Unit, A);
     auto U = tri<T>(Uplo::Upper, Diag::NonUnit, A);
@@ -58,6 +60,7 @@ void getrs(Op trans, Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Opt
 template <typename T>
 void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("getrs_nopiv");
+    internal::DriverScope ds_;
     trsm(Side::Left, T(1), tri<T>(Uplo::Lower, Diag::Unit, A), B, opts);
     trsm(Side::Left, T(1), tri<T>(Uplo::Upper, Diag::NonUnit, A), B, opts);
 }
@@ -65,6 +68,7 @@ void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 int64_t gesv(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
     trace::Block tb("gesv");
+    internal::DriverScope ds_;
     int64_t info = getrf(A, pivots, opts);
     if (info == 0) getrs(A, pivots, B, opts);
     return info;
@@ -73,6 +77,7 @@ int64_t gesv(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
 template <typename T>
 int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("gesv_nopiv");
+    internal::DriverScope ds_;
     int64_t info = getrf_nopiv(A, opts);
     if (info == 0) getrs_nopiv(A, B, opts);
     return info;
@@ -81,6 +86,7 @@ int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("potrs");
+    internal::DriverScope ds_;
     // A = L L^H (lower) or U^H U (upper) in the physical triangle
     BaseMatrix<T> Ap = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
     Uplo u = A.uplo_physical();
@@ -97,6 +103,7 @@ void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("posv");
+    internal::DriverScope ds_;
     int64_t info = potrf(A, opts);
     if (info == 0) potrs(A, B, opts);
     return info;
@@ -107,6 +114,7 @@ int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, Options const& opts) {
 template <typename T>
 int64_t trtri(TriangularMatrix<T>& A, Options const& opts) {
     trace::Block tb("trtri");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (A.grid()->size() == 1 && A.op() == Op::NoTrans) {
@@ -114,7 +122,7 @@ int64_t trtri(TriangularMatrix<T>& A, Options const& opts) {
         LocalBlock<T> la = A.local(loc, true);
         lb::trtri(c, A.uplo(), A.diag(), la.m, la.ptr, la.ld);
         if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-        A.storage()->update_origin();
+        internal::finish_origin(A, opts);
         return 0;
     }
     // distributed: solve A X = I
@@ -130,6 +138,7 @@ int64_t trtri(TriangularMatrix<T>& A, Options const& opts) {
 template <typename T>
 void trtrm(TriangularMatrix<T>& A, Options const& opts) {
     trace::Block tb("trtrm");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     if (A.grid()->size() == 1 && A.op() == Op::NoTrans) {
@@ -137,7 +146,7 @@ void trtrm(TriangularMatrix<T>& A, Options const& opts) {
         LocalBlock<T> la = A.local(loc, true);
         lb::lauum(c, A.uplo(), la.m, la.ptr, la.ld);
         if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-        A.storage()->update_origin();
+        internal::finish_origin(A, opts);
         return;
     }
     // distributed: L^H L via a dense copy of L and herk-style gemm
@@ -157,6 +166,7 @@ void trtrm(TriangularMatrix<T>& A, Options const& opts) {
 template <typename T>
 int64_t potri(HermitianMatrix<T>& A, Options const& opts) {
     trace::Block tb("potri");
+    internal::DriverScope ds_;
     int64_t info = 0;
     BaseMatrix<T> Ap = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
     TriangularMatrix<T> Tm = tri<T>(A.uplo_physical(), Diag::NonUnit, Ap);
@@ -168,6 +178,7 @@ int64_t potri(HermitianMatrix<T>& A, Options const& opts) {
 template <typename T>
 int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts) {
     trace::Block tb("getri");
+    internal::DriverScope ds_;
     Target target = resolve_target(opts);
     // A^{-1} = U^{-1} L^{-1} P: solve (L U) X = P^T ... via X = A^{-1} I
     Matrix<T> X = A.emptyLike();
@@ -260,6 +271,7 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
 template <typename T>
 int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
     trace::Block tb("gesv_mixed");
+    internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;
     if constexpr (std::is_same_v<Lo, T>) {
         slate_error("gesv_mixed requires a double-precision type");
@@ -277,6 +289,7 @@ int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int
 template <typename T>
 int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
     trace::Block tb("posv_mixed");
+    internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;
     if constexpr (std::is_same_v<Lo, T>) {
         slate_error("posv_mixed requires a double-precision type");
@@ -305,6 +318,7 @@ int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter,
 template <typename T>
 int64_t getri(Matrix<T>& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
     trace::Block tb("getriOOP");
+    internal::DriverScope ds_;
     set(T(0), T(1), B, opts);
     getrs(A, pivots, B, opts);
     return 0;

@@ -98,6 +98,62 @@ def case_trmm(tg, dt, nb):
                     assert relerr(s.to_numpy(B), ref) < tol(dt), (side, uplo, diag, op)
 
 
+def case_hemm(tg, dt, nb):
+    """Distributed hemm / symm: hemmC (stored-triangle SUMMA) and hemmA
+    (stationary A), Left / Right, Lower / Upper, narrow and wide B."""
+    n = 130
+    a = rnd(n, n, dt, 71)
+    h = a + a.conj().T
+    sy = a + a.T
+    for ncol in (20, 90):
+        for side in (s.Side.Left, s.Side.Right):
+            shp = (n, ncol) if side == s.Side.Left else (ncol, n)
+            b, c0 = rnd(*shp, dt, 72), rnd(*shp, dt, 73)
+            for uplo, tri in ((s.Uplo.Lower, np.tril), (s.Uplo.Upper, np.triu)):
+                for meth in ("hemmA", "hemmC"):
+                    for herm, full, fn, cls in ((True, h, s.hemm, s.HermitianMatrix),
+                                                (False, sy, s.symm, s.SymmetricMatrix)):
+                        # only the stored triangle is valid: garbage in the other one
+                        st = tri(full) + (np.triu(rnd(n, n, dt, 74), 1) if uplo == s.Uplo.Lower
+                                          else np.tril(rnd(n, n, dt, 74), -1))
+                        A = cls(uplo, s.from_numpy(st, nb=nb, target=tg))
+                        B = s.from_numpy(b, nb=nb, target=tg)
+                        C = s.from_numpy(c0, nb=nb, target=tg)
+                        fn(side, 1.5, A, B, 0.5, C, target=tg, method_hemm=meth)
+                        ref = 1.5 * (full @ b if side == s.Side.Left else b @ full) + 0.5 * c0
+                        assert relerr(s.to_numpy(C), ref) < tol(dt), (ncol, side, uplo, meth, herm)
+
+
+def case_stationary(tg, dt, nb):
+    """gemmA and trsmA (stationary A, narrow operand replicated on the device)
+    against gemmC / trsmB on every side / uplo / op."""
+    m, k = 140, 110
+    a, b, c0 = rnd(m, k, dt, 81), rnd(k, 30, dt, 82), rnd(m, 30, dt, 83)
+    for meth in ("gemmA", "gemmC"):
+        C = s.from_numpy(c0, nb=nb, target=tg)
+        s.gemm(2.0, s.from_numpy(a, nb=nb, target=tg), s.from_numpy(b, nb=nb, target=tg), -1.0, C,
+               target=tg, method_gemm=meth)
+        assert relerr(s.to_numpy(C), 2.0 * a @ b - c0) < tol(dt), meth
+    n = 130
+    t = (rnd(n, n, dt, 84) / n + 2 * np.eye(n)).astype(dt)
+    for side in (s.Side.Left, s.Side.Right):
+        for uplo, tri in ((s.Uplo.Lower, np.tril), (s.Uplo.Upper, np.triu)):
+            for op in ("n", "c"):
+                for meth in ("trsmA", "trsmB"):
+                    shp = (n, 25) if side == s.Side.Left else (25, n)
+                    b = rnd(*shp, dt, 85)
+                    T = s.TriangularMatrix(uplo, s.Diag.NonUnit, s.from_numpy(t, nb=nb, target=tg))
+                    opt = tri(t)
+                    if op == "c":
+                        T = s.conj_transpose(T)
+                        opt = opt.conj().T
+                    B = s.from_numpy(b, nb=nb, target=tg)
+                    s.trsm(side, 2.0, T, B, target=tg, method_trsm=meth)
+                    x = s.to_numpy(B)
+                    lhs = opt @ x if side == s.Side.Left else x @ opt
+                    assert relerr(lhs, 2.0 * b) < 10 * tol(dt), (side, uplo, op, meth)
+
+
 def case_potrf(tg, dt, nb):
     n = 200
     a = rnd(n, n, dt, 7)

@@ -386,3 +386,45 @@ def test_condest_gmres_device():
     info, _, it = s.gesv_mixed_gmres(A2, B, X, target="d")
     assert info == 0 and it >= 0
     assert np.linalg.norm(a @ s.to_numpy(X) - b) / np.linalg.norm(b) < 1e-13
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("thresh", [0.5, 0.1])
+def test_getrf_pivot_threshold_device(thresh):
+    """PivotThreshold in the device PPLU panel kernel (lu_pivot_kernel): |L| <= 1/threshold,
+    P A = L U, and fewer interchanges than partial pivoting."""
+    n, nb = 600, 128
+    a = rnd(n, n, np.float64, 63) + 1.5 * np.eye(n)
+
+    def run(**kw):
+        A = s.from_numpy(a, nb=nb, target="d")
+        info, piv = s.getrf(A, target="d", **kw)
+        f = s.to_numpy(A)
+        L = np.tril(f, -1) + np.eye(n)
+        U = np.triu(f)
+        ip = [kk * nb + ti * nb + off for kk, pv in enumerate(piv) for (ti, off) in pv]
+        pa = a.copy()
+        for j, p_ in enumerate(ip):
+            pa[[j, p_]] = pa[[p_, j]]
+        return info, relerr(L @ U, pa), np.abs(L).max(), sum(1 for j, p_ in enumerate(ip) if p_ != j)
+    info, err, lmax, mv = run(pivot_threshold=thresh)
+    _, _, _, mv1 = run()
+    assert info == 0 and err < 1e-12 and lmax <= 1 / thresh + 1e-12 and mv < mv1
+
+
+@pytest.mark.gpu
+def test_hold_local_workspace_device():
+    """Option::HoldLocalWorkspace (reference src/potrf.cc:42,198): a host-origin
+    matrix factored on the device keeps its device copy only when held."""
+    from slate_d35_amd import _slate
+    n, nb = 512, 128
+    a = rnd(n, n, np.float64, 64)
+    a = a @ a.T + n * np.eye(n)
+    for hold in (False, True):
+        H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb))   # host origin
+        before = _slate.bytes_in_use()
+        assert s.potrf(H, target="d", hold_local_workspace=hold) == 0
+        grown = _slate.bytes_in_use() - before
+        assert (grown >= n * n * 8) == hold, (hold, grown)
+        L = np.tril(s.to_numpy(H))
+        assert relerr(L @ L.T, a) < 1e-13

@@ -121,3 +121,41 @@ def test_getri_out_of_place():
     B = s.from_numpy(np.zeros((n, n)), nb=32)
     s.getri(A, piv, B)
     assert relerr(s.to_numpy(B) @ a, np.eye(n)) < 1e-13
+
+
+def _lu_residual(a, f, piv, nb):
+    m, n = a.shape
+    k = min(m, n)
+    L = np.tril(f[:, :k], -1) + np.eye(m, k)
+    U = np.triu(f[:k, :])
+    pa = a.copy()
+    for j, p_ in enumerate(kk * nb + ti * nb + off for kk, pv in enumerate(piv) for (ti, off) in pv):
+        pa[[j, p_]] = pa[[p_, j]]
+    return relerr(L @ U, pa), np.abs(L).max()
+
+
+@pytest.mark.parametrize("thresh", [1.0, 0.5, 0.1])
+def test_getrf_pivot_threshold(thresh):
+    """Option::PivotThreshold (reference src/getrf.cc:39): the diagonal stays
+    pivot while |a_jj| >= threshold * column max, so |L| <= 1 / threshold and
+    fewer rows move as the threshold drops."""
+    n, nb = 120, 32
+    a = rnd(n, n, np.float64, 61) + 1.5 * np.eye(n)
+
+    def moved(piv):
+        return sum(1 for blk in piv for j, (ti, off) in enumerate(blk) if (ti, off) != (0, j))
+    A = s.from_numpy(a, nb=nb)
+    info, piv = s.getrf(A, pivot_threshold=thresh)
+    err, lmax = _lu_residual(a, s.to_numpy(A), piv, nb)
+    assert info == 0 and err < 1e-12
+    assert lmax <= 1.0 / thresh + 1e-12
+    if thresh < 1.0:
+        A1 = s.from_numpy(a, nb=nb)
+        _, piv1 = s.getrf(A1)
+        assert moved(piv) < moved(piv1), (moved(piv), moved(piv1))
+
+
+def test_getrf_pivot_threshold_invalid():
+    A = s.from_numpy(rnd(40, 40, np.float64, 62), nb=16)
+    with pytest.raises(Exception):
+        s.getrf(A, pivot_threshold=1.5)
