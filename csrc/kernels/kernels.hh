@@ -61,6 +61,17 @@ template <typename T>
 void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const T* buf, int64_t ldb, T* A,
                   int64_t lda, RowDist d, hipStream_t s);
 
+// ---- butterfly transforms (rbt.hip)
+/// by_rows: buf(t, j) = A(idx[t], j) for t < cnt, j < len (scatter: the reverse);
+/// by columns: buf(i, t) = A(i, idx[t]) for i < len.
+template <typename T>
+void rbt_gather(bool by_rows, bool scatter, int64_t cnt, int64_t len, const int64_t* idx, T* A, int64_t lda, T* buf,
+                int64_t ldb, hipStream_t s);
+/// A(i, j) = ca[r] A(i, j) + cp[r] P(i, j) with r = i (by_rows) or j.
+template <typename T>
+void rbt_combine(bool by_rows, int64_t m, int64_t n, T* A, int64_t lda, const T* P, int64_t ldp, const rt<T>* ca,
+                 const rt<T>* cp, hipStream_t s);
+
 // ---- TSQR Householder reconstruction (tsqr.hip): narrow block (nn <= 32) of
 // the sign-modified LU without pivoting, rows [r, m), columns [r, r+nn) of A;
 // Utop = copy of the nn x nn top block (ld 32); sgn[r+j] receives s_j.

@@ -18,7 +18,7 @@ sys.path.insert(0, HERE)
 import torch  # noqa: F401,E402  (HIP runtime first)
 import slate_d35_amd as s  # noqa: E402
 from slate_d35_amd import parallel  # noqa: E402
-from helpers import rnd, relerr  # noqa: E402
+from helpers import rnd, relerr, butterfly_dense  # noqa: E402
 
 
 def tol(dt):
@@ -152,6 +152,24 @@ def case_stationary(tg, dt, nb):
                     x = s.to_numpy(B)
                     lhs = opt @ x if side == s.Side.Left else x @ opt
                     assert relerr(lhs, 2.0 * b) < 10 * tol(dt), (side, uplo, op, meth)
+
+
+def case_rbt(tg, dt, nb):
+    """Butterfly levels with partner rows / columns on other processes
+    (grouped exchange) against the dense U^T A V, and gesv_rbt."""
+    m, n = 150, 130
+    a = rnd(m, n, dt, 91)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    s.gerbt(A, 2, 1, 2, target=tg)
+    ref = butterfly_dense(m, 2, 1).T @ a @ butterfly_dense(n, 2, 2)
+    assert relerr(s.to_numpy(A), ref) < tol(dt)
+    a = rnd(n, n, dt, 92) + 2 * np.eye(n, dtype=dt)
+    b = rnd(n, 3, dt, 93)
+    A, B = s.from_numpy(a, nb=nb, target=tg), s.from_numpy(b, nb=nb, target=tg)
+    X = s.from_numpy(np.zeros_like(b), nb=nb, target=tg)
+    info, it = s.gesv_rbt(A, B, X, target=tg)
+    assert info == 0
+    assert relerr(a @ s.to_numpy(X), b) < 100 * tol(dt)
 
 
 def case_potrf(tg, dt, nb):

@@ -17,3 +17,33 @@ def relerr(x, ref):
     d = np.linalg.norm(np.asarray(x) - np.asarray(ref))
     r = np.linalg.norm(np.asarray(ref))
     return d / max(r, 1e-300)
+
+
+def rbt_rand(seed, level, idx):
+    M = (1 << 64) - 1
+    z = (seed * 0x9E3779B97F4A7C15 + level * 0xBF58476D1CE4E5B9 + idx * 0x94D049BB133111EB) & M
+    z ^= z >> 30
+    z = (z * 0xBF58476D1CE4E5B9) & M
+    z ^= z >> 27
+    z = (z * 0x94D049BB133111EB) & M
+    z ^= z >> 31
+    return np.exp(((z >> 11) * (1.0 / 9007199254740992.0) - 0.5) / 10.0)
+
+
+def butterfly_dense(n, depth, seed):
+    """Dense W = L_{d-1} ... L_0 of the butterfly definition in csrc/src/rbt.cc."""
+    W = np.eye(n)
+    s2 = 1 / np.sqrt(2)
+    for lev in range(depth):
+        L = np.eye(n)
+        nblk = 1 << lev
+        for b in range(nblk):
+            r0, r1 = n * b // nblk, n * (b + 1) // nblk
+            h = (r1 - r0) // 2
+            for r in range(h):
+                i = r0 + r
+                R0, R1 = rbt_rand(seed, lev, 2 * i), rbt_rand(seed, lev, 2 * i + 1)
+                L[i, i], L[i, i + h] = s2 * R0, s2 * R1
+                L[i + h, i], L[i + h, i + h] = s2 * R0, -s2 * R1
+        W = L @ W
+    return W

@@ -4,7 +4,7 @@ import numpy as np
 import pytest
 
 import slate_d35_amd as s
-from helpers import DTYPES, rnd, relerr
+from helpers import DTYPES, rnd, relerr, butterfly_dense as _butterfly
 
 
 def _ill(n, dt, seed, cond=1e4):
@@ -159,3 +159,15 @@ def test_getrf_pivot_threshold_invalid():
     A = s.from_numpy(rnd(40, 40, np.float64, 62), nb=16)
     with pytest.raises(Exception):
         s.getrf(A, pivot_threshold=1.5)
+
+
+@pytest.mark.parametrize("depth", [1, 2, 3])
+def test_gerbt_matches_dense_butterflies(depth):
+    """gerbt applies the O(n^2 d) butterfly levels: equal to U^T A V with the
+    dense butterflies (seeds of gerbt's defaults)."""
+    m, n, nb = 75, 61, 16
+    a = rnd(m, n, np.float64, 25)
+    A = s.from_numpy(a, nb=nb)
+    s.gerbt(A, depth, 1, 2)
+    U, V = _butterfly(m, depth, 1), _butterfly(n, depth, 2)
+    assert relerr(s.to_numpy(A), U.T @ a @ V) < 1e-14
