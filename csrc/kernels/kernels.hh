@@ -61,6 +61,23 @@ template <typename T>
 void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const T* buf, int64_t ldb, T* A,
                   int64_t lda, RowDist d, hipStream_t s);
 
+// ---- distributed partial-pivoting panel, one column per call (lu_dist.hip)
+/// elements of T per process in the per-column all-gather: header + 2 rows
+template <typename T>
+int64_t pplu_entry(int64_t kb);
+/// my candidate (max |ap(r, j)|, r in [r0, mr)) and, on the diagonal process,
+/// row j -> buf (one all-gather entry)
+template <typename T>
+void pplu_cand(int64_t mr, int64_t j, int64_t r0, const T* ap, int64_t lda, int64_t kb, RowDist d, int64_t lr_k,
+               bool is_pk, T* buf, hipStream_t s);
+/// winner from the gathered entries (np of them, diagonal process pk), swap of
+/// row kk+j with the pivot row over the panel width kb, scaling of column j and
+/// rank-1 update of columns (j, cend) on local rows [r_upd0, mr); pip[j] = piv - kk
+template <typename T>
+void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int64_t mr, int64_t r_upd0, T* ap,
+                int64_t lda, RowDist d, int64_t lr_k, int64_t kk, int pk, double thresh, bool is_pk, int64_t* pip,
+                int* info, int64_t info_off, hipStream_t s);
+
 // ---- butterfly transforms (rbt.hip)
 /// by_rows: buf(t, j) = A(idx[t], j) for t < cnt, j < len (scatter: the reverse);
 /// by columns: buf(i, t) = A(i, idx[t]) for i < len.

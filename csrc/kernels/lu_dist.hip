@@ -107,6 +107,123 @@ __global__ __launch_bounds__(64) void slots_unpack_kernel(int s0, int s1, int64_
 
 inline unsigned col_blocks(int64_t ncols) { return (unsigned)std::min<int64_t>(std::max<int64_t>(ncols, 1), 8192); }
 
+// ---- distributed partial pivoting (PPLU on a p > 1 grid), one column j of
+// the panel at a time.  Every process of the panel column contributes an entry
+// [ header(16 B: max |a|, global row) | its candidate row (kb) | row kk+j (kb,
+// from the diagonal process) ] to one all-gather; every process then picks the
+// same winner and applies the swap + rank-1 update to the rows it owns.
+template <typename T>
+__device__ inline rt<T>& pp_val(T* e) { return *reinterpret_cast<rt<T>*>(e); }
+template <typename T>
+__device__ inline int64_t& pp_gid(T* e) { return *reinterpret_cast<int64_t*>(reinterpret_cast<char*>(e) + 8); }
+template <typename T>
+__device__ inline rt<T> pp_val(const T* e) { return *reinterpret_cast<const rt<T>*>(e); }
+template <typename T>
+__device__ inline int64_t pp_gid(const T* e) { return *reinterpret_cast<const int64_t*>(reinterpret_cast<const char*>(e) + 8); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void pplu_cand_kernel(int64_t mr, int64_t j, int64_t r0, const T* ap, int64_t lda,
+                                                        int64_t kb, RowDist d, int64_t lr_k, int is_pk, T* buf,
+                                                        int hdr) {
+    using R = rt<T>;
+    __shared__ R sv[256];
+    __shared__ int64_t si[256];
+    R best = R(-1);
+    int64_t bi = INT64_MAX;
+    for (int64_t r = r0 + threadIdx.x; r < mr; r += 256) {
+        const R v = abs1(ap[r + j * lda]);
+        if (v > best) { best = v; bi = r; }          // rows ascending per thread: first max kept
+    }
+    sv[threadIdx.x] = best;
+    si[threadIdx.x] = bi;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) {
+            const R ov = sv[threadIdx.x + w];
+            const int64_t oi = si[threadIdx.x + w];
+            if (ov > sv[threadIdx.x] || (ov == sv[threadIdx.x] && oi < si[threadIdx.x])) {
+                sv[threadIdx.x] = ov;
+                si[threadIdx.x] = oi;
+            }
+        }
+        __syncthreads();
+    }
+    const int64_t r = si[0];
+    const bool have = (r != INT64_MAX);
+    if (threadIdx.x == 0) {
+        pp_val(buf) = have ? sv[0] : R(-1);
+        pp_gid(buf) = have ? rd_l2g(d, lr_k + r) : int64_t(-1);
+    }
+    T* cand = buf + hdr;
+    T* cur = buf + hdr + kb;
+    for (int64_t c = threadIdx.x; c < kb; c += 256) {
+        cand[c] = have ? ap[r + c * lda] : T();
+        cur[c] = is_pk ? ap[j + c * lda] : T();
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void pplu_apply_kernel(int np, const T* gbuf, int64_t E, int hdr, int64_t kb,
+                                                         int64_t j, int64_t cend, int64_t mr, int64_t r_upd0, T* ap,
+                                                         int64_t lda, RowDist d, int64_t lr_k, int64_t kk, int pk,
+                                                         rt<T> thresh, int is_pk, int64_t* pip, int* info,
+                                                         int64_t info_off) {
+    using R = rt<T>;
+    __shared__ int64_t s_piv;
+    __shared__ int s_w;
+    __shared__ T u[64];
+    const T* crow = gbuf + pk * E + hdr + kb;
+    if (threadIdx.x == 0) {
+        R best = R(-1);
+        int64_t bg = INT64_MAX;
+        int w = -1;
+        for (int e = 0; e < np; ++e) {
+            const T* en = gbuf + e * E;
+            const R v = pp_val(en);
+            const int64_t gi = pp_gid(en);
+            if (gi < 0) continue;
+            if (v > best || (v == best && gi < bg)) { best = v; bg = gi; w = e; }
+        }
+        int64_t piv = (w < 0) ? kk + j : bg;
+        // threshold pivoting: keep row kk+j while |a| >= thresh * max
+        if (w >= 0 && thresh < R(1) && piv != kk + j && abs1(crow[j]) >= thresh * best) { piv = kk + j; w = -1; }
+        s_piv = piv;
+        s_w = w;
+        if (blockIdx.x == 0) {
+            pip[j] = piv - kk;
+            if (info && best == R(0) && *info == 0) *info = (int)(info_off + j + 1);
+        }
+    }
+    __syncthreads();
+    const int64_t piv = s_piv;
+    const T* prow = (s_w >= 0) ? gbuf + s_w * E + hdr : crow;
+    const int64_t nc = cend - j;                 // narrow-block columns j .. cend-1 (<= 64)
+    if (threadIdx.x < nc) u[threadIdx.x] = prow[j + threadIdx.x];
+    __syncthreads();
+    const bool swap = (piv != kk + j);
+    const int64_t lp = (swap && rd_owner(d, piv) == d.myrow) ? rd_lrow(d, piv) - lr_k : int64_t(-1);
+    if (blockIdx.x == 0) {
+        // row kk+j (local row j on the diagonal process) becomes the pivot row,
+        // full panel width; the vacated pivot row gets the old row outside [j, cend)
+        for (int64_t c = threadIdx.x; c < kb; c += 256) {
+            if (is_pk) ap[j + c * lda] = prow[c];
+            if (lp >= 0 && (c < j || c >= cend)) ap[lp + c * lda] = crow[c];
+        }
+    }
+    const T ujj = u[0];
+    const bool nz = !is_zero(ujj);
+    for (int64_t r = r_upd0 + blockIdx.x * 256 + threadIdx.x; r < mr; r += 256 * (int64_t)gridDim.x) {
+        const bool isp = (r == lp);
+        const T s0 = isp ? crow[j] : ap[r + j * lda];
+        const T l = nz ? s0 / ujj : s0;
+        ap[r + j * lda] = l;
+        for (int64_t c = 1; c < nc; ++c) {
+            const T x = isp ? crow[j + c] : ap[r + (j + c) * lda];
+            ap[r + (j + c) * lda] = x - l * u[c];
+        }
+    }
+}
+
 }  // namespace
 
 template <typename T>
@@ -141,13 +258,42 @@ void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const 
     hipLaunchKernelGGL(slots_unpack_kernel<T>, g, dim3(64), 0, s, s0, s1, ncols, slot_dst, buf, ldb, A, lda, d);
 }
 
+template <typename T>
+constexpr int pp_hdr() { return int((16 + sizeof(T) - 1) / sizeof(T)); }
+
+template <typename T>
+int64_t pplu_entry(int64_t kb) { return pp_hdr<T>() + 2 * kb; }
+
+template <typename T>
+void pplu_cand(int64_t mr, int64_t j, int64_t r0, const T* ap, int64_t lda, int64_t kb, RowDist d, int64_t lr_k,
+               bool is_pk, T* buf, hipStream_t s) {
+    hipLaunchKernelGGL(pplu_cand_kernel<T>, dim3(1), dim3(256), 0, s, mr, j, r0, ap, lda, kb, d, lr_k, int(is_pk), buf,
+                       pp_hdr<T>());
+}
+
+template <typename T>
+void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int64_t mr, int64_t r_upd0, T* ap,
+                int64_t lda, RowDist d, int64_t lr_k, int64_t kk, int pk, double thresh, bool is_pk, int64_t* pip,
+                int* info, int64_t info_off, hipStream_t s) {
+    const int64_t rows = std::max<int64_t>(mr - r_upd0, 1);
+    const unsigned nblk = (unsigned)std::min<int64_t>((rows + 255) / 256, 1024);
+    hipLaunchKernelGGL(pplu_apply_kernel<T>, dim3(nblk), dim3(256), 0, s, np, gbuf, pplu_entry<T>(kb), pp_hdr<T>(),
+                       kb, j, cend, mr, r_upd0, ap, lda, d, lr_k, kk, pk, rt<T>(thresh), int(is_pk), pip, info,
+                       info_off);
+}
+
 #define SLATE_INST_LUDIST(T)                                                                                       \
     template void gather_rows_ids<T>(int64_t, int64_t, const int64_t*, const T*, int64_t, T*, int64_t,            \
                                      const int64_t*, int64_t*, RowDist, int64_t, hipStream_t);                    \
     template void slots_pack<T>(int, int, int64_t, const int64_t*, const T*, int64_t, RowDist, T*, int64_t,       \
                                 hipStream_t);                                                                      \
     template void slots_unpack<T>(int, int, int64_t, const int64_t*, const T*, int64_t, T*, int64_t, RowDist,     \
-                                  hipStream_t);
+                                  hipStream_t);                                                                    \
+    template int64_t pplu_entry<T>(int64_t);                                                                       \
+    template void pplu_cand<T>(int64_t, int64_t, int64_t, const T*, int64_t, int64_t, RowDist, int64_t, bool, T*,  \
+                               hipStream_t);                                                                       \
+    template void pplu_apply<T>(int, const T*, int64_t, int64_t, int64_t, int64_t, int64_t, T*, int64_t, RowDist, \
+                                int64_t, int64_t, int, double, bool, int64_t*, int*, int64_t, hipStream_t);
 
 SLATE_INST_LUDIST(float)
 SLATE_INST_LUDIST(double)

@@ -238,10 +238,11 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
         Fb(target, size_t(2 * nb) * nb);
     Work<int64_t> ids(target, nb), idr(target, nb), idS(target, 2 * nb),
         perm(target, size_t(std::max<int64_t>(mloc, 2 * nb))), pip(target, nb);
-    Work<T> Gfull, Gr;
+    Work<T> PPe, PPg, U12;     // partial pivoting: all-gather entry / gathered entries / U12 rows
     if (mode == PanelMode::Partial) {
-        Gfull.resize(target, size_t(std::max<int64_t>(m, 1)) * nb);
-        Gr.resize(target, size_t(std::max<int64_t>(m, 1)) * nb);
+        PPe.resize(target, size_t(pplu_entry<T>(nb)));
+        PPg.resize(target, size_t(p) * pplu_entry<T>(nb));
+        U12.resize(target, size_t(32) * nb);
     }
     Work<int64_t> ipiv_all(target, size_t(std::max<int64_t>(kt, 1)) * nb);
     Work<int> dinfo(target, 2);               // [info, dummy]
@@ -289,7 +290,6 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
         int64_t* ssrc = pv + 2 * nb;
         int64_t* sdst = pv + 4 * nb;
         T* LUk = LU[slot].data();
-        const int64_t ldlu = kd;
         T* Wk = W[slot].data();
         T* ap = a + lr_k + lc_k * lda;        // my panel rows (>= kk)
         T* apc = a + lc_k * lda;               // panel column, local row 0
@@ -395,67 +395,54 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
                 slots_unpack(c, int(kd), int(2 * kd), kb, sdst, PB.data(), kd, apc, lda, rd);
             });
         } else if (in_col && mode == PanelMode::Partial) {
-            // gather the panel rows to pk (global order is host-known), factor, scatter back
-            std::vector<int64_t> off_r(p, 0);
-            {
-                int64_t o = 0;
-                for (int r = 0; r < p; ++r) if (r != pk) { off_r[r] = o; o += rows_r[r]; }
-            }
-            S.task(qC, {Sched::col(k)}, {tSel}, [&, kb, ap, mr, pk, off_r, rows_r](lb::Ctx const& c) {
-                trace::Block t2("getrf_pp_gather");
-                std::vector<Comm::P2P> ops;
-                if (myrow == pk) {
-                    for (int r = 0; r < p; ++r)
-                        if (r != pk && rows_r[r] > 0)
-                            ops.push_back({Gr.data() + off_r[r] * kb, size_t(rows_r[r] * kb), r, false});
-                } else if (mr > 0) {
-                    lb::copy2d(c, mr, kb, ap, lda, Wsel.data(), mr);
-                    ops.push_back({Wsel.data(), size_t(mr * kb), pk, true});
+            // distributed partial pivoting (reference Tile_getrf.hh:270): column
+            // by column, ONE all-gather over the panel column of every process's
+            // {max |a|, row id, candidate row, row kk+j}; each process then picks
+            // the same pivot and swaps / scales / updates the rows it owns.
+            // Narrow blocks of 32 columns; the rest of the panel is updated by
+            // U12 = L11^{-1} A12 (pk, broadcast down the column) and a GEMM.
+            const int64_t E = pplu_entry<T>(kb);
+            for (int64_t c0 = 0; c0 < kd; c0 += 32) {
+                const int64_t cend = std::min<int64_t>(c0 + 32, kd), nn = cend - c0;
+                for (int64_t j = c0; j < cend; ++j) {
+                    S.task(qC, {Sched::col(k)}, {Sched::col(k)}, [&, j, cend, kb, kk, E, mr, diag, pk, ap, lr_k](lb::Ctx const& c) {
+                        trace::Block t2("getrf_pp_column");
+                        pplu_cand(c, mr, j, diag ? j : 0, ap, lda, kb, rd, lr_k, diag, PPe.data());
+                        g.col().allgather(PPe.data(), PPg.data(), size_t(E), scalar_type<T>(), c.loc(), c.stream);
+                        pplu_apply(c, p, PPg.data(), kb, j, cend, mr, diag ? j + 1 : 0, ap, lda, rd, lr_k, kk, pk, thresh,
+                                   diag, pip.data(), diag ? info_real : info_dummy, kk);
+                    });
                 }
-                g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-            });
-            if (diag) {
-                S.task(qP, {tSel, Sched::col(k)}, {tSel, tPV, Sched::col(k)},
-                       [&, k, kb, kk, M, kd, ap, pk, off_r, rows_r, LUk](lb::Ctx const& c) {
-                    trace::Block t2("getrf_pp_panel");
-                    // assemble / scatter in tile order: (own rows, or rank r's buffer at its running offset)
-                    auto walk = [&](bool to_full) {
-                        std::vector<int64_t> o(p, 0);
-                        for (int64_t i = k; i < mt; ++i) {
-                            int r = A.srow_owner(i);
-                            int64_t ib = A.tileMb(i), gi = grow_of(A, i) - kk;
-                            T* src = (r == pk) ? ap + o[r] : Gr.data() + off_r[r] * kb + o[r];
-                            int64_t lds = (r == pk) ? lda : rows_r[r];
-                            if (to_full) lb::copy2d(c, ib, kb, src, lds, Gfull.data() + gi, M);
-                            else lb::copy2d(c, ib, kb, Gfull.data() + gi, M, src, lds);
-                            o[r] += ib;
+                if (cend < kb) {
+                    const int64_t rest = kb - cend;
+                    S.task(qC, {Sched::col(k)}, {Sched::col(k)}, [&, c0, nn, cend, rest, diag, pk, ap](lb::Ctx const& c) {
+                        trace::Block t2("getrf_pp_u12");
+                        if (diag) {
+                            lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, nn, rest, T(1),
+                                     ap + c0 + c0 * lda, lda, ap + c0 + cend * lda, lda);
+                            lb::copy2d(c, nn, rest, ap + c0 + cend * lda, lda, U12.data(), nn);
                         }
-                    };
-                    walk(true);
-                    lb::getrf_panel(c, M, kb, Gfull.data(), M, pip.data(), (int64_t*)nullptr, info_real, kk, true, false, thresh);
-                    walk(false);
-                    lb::copy2d(c, kd, kb, Gfull.data(), M, LUk, kd);
-                });
-            }
-            S.task(qC, {tSel}, {tSel, Sched::col(k)}, [&, kb, ap, mr, pk, off_r, rows_r](lb::Ctx const& c) {
-                trace::Block t2("getrf_pp_scatter");
-                std::vector<Comm::P2P> ops;
-                if (myrow == pk) {
-                    for (int r = 0; r < p; ++r)
-                        if (r != pk && rows_r[r] > 0)
-                            ops.push_back({Gr.data() + off_r[r] * kb, size_t(rows_r[r] * kb), r, true});
-                } else if (mr > 0) {
-                    ops.push_back({Wsel.data(), size_t(mr * kb), pk, false});
+                        bcast(g.col(), U12.data(), size_t(nn * rest), pk, c);
+                    });
+                    S.task(qP, {Sched::col(k)}, {Sched::col(k)}, [&, c0, nn, cend, rest, diag, mr, ap](lb::Ctx const& c) {
+                        trace::Block t2("getrf_pp_a22");
+                        const int64_t r0 = diag ? cend : 0;
+                        if (mr > r0)
+                            lb::gemm(c, Op::NoTrans, Op::NoTrans, mr - r0, rest, nn, T(-1), ap + r0 + c0 * lda, lda,
+                                     U12.data(), nn, T(1), ap + r0 + cend * lda, lda);
+                    });
                 }
-                g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                if (myrow != pk && mr > 0) lb::copy2d(c, mr, kb, Wsel.data(), mr, ap, lda);
-            });
-            S.task(qC, {tSel}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) {
-                trace::Block t2("getrf_bcast_piv");
-                bcast(g.col(), pip.data(), size_t(kd), pk, c);
+            }
+            if (diag)
+                S.task(qP, {Sched::col(k)}, {tPV}, [&, kd, kb, ap, LUk](lb::Ctx const& c) {
+                    lb::copy2d(c, kd, kb, ap, lda, LUk, kd);
+                });
+            S.task(qC, {}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) {
+                trace::Block t2("getrf_bcast_lu11");
                 bcast(g.col(), LUk, size_t(kd * kb), pk, c);
             });
-            S.task(qP, {tSel}, {tPV}, [&, k, kk, kd, ipv, ssrc, sdst](lb::Ctx const& c) {
+            // pip is replicated by the per-column all-gathers
+            S.task(qP, {Sched::col(k)}, {tPV}, [&, k, kk, kd, ipv, ssrc, sdst](lb::Ctx const& c) {
                 perm_slots(c, 1, kk, int(kd), pip.data(), kk, ipv, ssrc, sdst);
             });
         } else if (in_col) {

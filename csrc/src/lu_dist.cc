@@ -134,7 +134,90 @@ void lu_sign(lb::Ctx const& c, int64_t n, T* A, int64_t lda, T* sgn) {
     rec(0, n);
 }
 
+template <typename T>
+int64_t pplu_entry(int64_t kb) { return kd::pplu_entry<kd::dev_t<T>>(kb); }
+
+namespace {
+template <typename T>
+inline int64_t pp_hdr(int64_t kb) { return pplu_entry<T>(kb) - 2 * kb; }
+template <typename T>
+inline real_type<T>& pp_val(T* e) { return *reinterpret_cast<real_type<T>*>(e); }
+template <typename T>
+inline int64_t& pp_gid(T* e) { return *reinterpret_cast<int64_t*>(reinterpret_cast<char*>(e) + 8); }
+}  // namespace
+
+template <typename T>
+void pplu_cand(lb::Ctx const& c, int64_t mr, int64_t j, int64_t r0, T const* ap, int64_t lda, int64_t kb,
+               RowDist const& d, int64_t lr_k, bool is_pk, T* buf) {
+    if (c.dev()) {
+        kd::pplu_cand(mr, j, r0, dptr(ap), lda, kb, d, lr_k, is_pk, dptr(buf), c.stream);
+        return;
+    }
+    using R = real_type<T>;
+    R best = R(-1);
+    int64_t bi = -1;
+    for (int64_t r = r0; r < mr; ++r) {
+        R v = std::abs(std::real(ap[r + j * lda])) + std::abs(std::imag(ap[r + j * lda]));
+        if (v > best) { best = v; bi = r; }
+    }
+    const int64_t hdr = pp_hdr<T>(kb);
+    std::fill(buf, buf + hdr, T(0));
+    pp_val(buf) = best;
+    pp_gid(buf) = bi >= 0 ? kd::rd_l2g(d, lr_k + bi) : -1;
+    for (int64_t cc = 0; cc < kb; ++cc) {
+        buf[hdr + cc] = bi >= 0 ? ap[bi + cc * lda] : T(0);
+        buf[hdr + kb + cc] = is_pk ? ap[j + cc * lda] : T(0);
+    }
+}
+
+template <typename T>
+void pplu_apply(lb::Ctx const& c, int np, T const* gbuf, int64_t kb, int64_t j, int64_t cend, int64_t mr,
+                int64_t r_upd0, T* ap, int64_t lda, RowDist const& d, int64_t lr_k, int64_t kk, int pk, double thresh,
+                bool is_pk, int64_t* pip, int* info, int64_t info_off) {
+    if (c.dev()) {
+        kd::pplu_apply(np, dptr(gbuf), kb, j, cend, mr, r_upd0, dptr(ap), lda, d, lr_k, kk, pk, thresh, is_pk, pip,
+                       info, info_off, c.stream);
+        return;
+    }
+    using R = real_type<T>;
+    const int64_t E = pplu_entry<T>(kb), hdr = pp_hdr<T>(kb);
+    T const* crow = gbuf + pk * E + hdr + kb;
+    R best = R(-1);
+    int64_t bg = -1;
+    int w = -1;
+    for (int e = 0; e < np; ++e) {
+        T* en = const_cast<T*>(gbuf + e * E);
+        R v = pp_val(en);
+        int64_t gi = pp_gid(en);
+        if (gi < 0) continue;
+        if (v > best || (v == best && gi < bg)) { best = v; bg = gi; w = e; }
+    }
+    int64_t piv = w < 0 ? kk + j : bg;
+    auto a1 = [](T x) { return std::abs(std::real(x)) + std::abs(std::imag(x)); };
+    if (w >= 0 && thresh < 1.0 && piv != kk + j && a1(crow[j]) >= R(thresh) * best) { piv = kk + j; w = -1; }
+    pip[j] = piv - kk;
+    if (info && best == R(0) && *info == 0) *info = int(info_off + j + 1);
+    T const* prow = w >= 0 ? gbuf + w * E + hdr : crow;
+    std::vector<T> pr(prow, prow + kb), cr(crow, crow + kb);   // gbuf rows may alias nothing, copy anyway
+    const bool swap = piv != kk + j;
+    const int64_t lp = (swap && kd::rd_owner(d, piv) == d.myrow) ? kd::rd_lrow(d, piv) - lr_k : -1;
+    if (is_pk) for (int64_t cc = 0; cc < kb; ++cc) ap[j + cc * lda] = pr[cc];
+    if (lp >= 0) for (int64_t cc = 0; cc < kb; ++cc) ap[lp + cc * lda] = cr[cc];
+    const T ujj = pr[j];
+    for (int64_t r = r_upd0; r < mr; ++r) {
+        T l = ujj != T(0) ? ap[r + j * lda] / ujj : ap[r + j * lda];
+        ap[r + j * lda] = l;
+        for (int64_t cc = j + 1; cc < cend; ++cc) ap[r + cc * lda] -= l * pr[cc];
+    }
+}
+
 #define SLATE_LUDIST_INST(T)                                                                                    \
+    template int64_t pplu_entry<T>(int64_t);                                                                   \
+    template void pplu_cand<T>(lb::Ctx const&, int64_t, int64_t, int64_t, T const*, int64_t, int64_t,        \
+                               RowDist const&, int64_t, bool, T*);                                             \
+    template void pplu_apply<T>(lb::Ctx const&, int, T const*, int64_t, int64_t, int64_t, int64_t, int64_t, T*, \
+                                int64_t, RowDist const&, int64_t, int64_t, int, double, bool, int64_t*, int*,  \
+                                int64_t);                                                                      \
     template void gather_rows_ids<T>(lb::Ctx const&, int64_t, int64_t, int64_t const*, T const*, int64_t, T*,  \
                                      int64_t, int64_t const*, int64_t*, RowDist const&, int64_t);              \
     template void slots_pack<T>(lb::Ctx const&, int, int, int64_t, int64_t const*, T const*, int64_t,          \

@@ -41,6 +41,20 @@ template <typename T>
 void slots_unpack(lb::Ctx const& c, int s0, int s1, int64_t ncols, int64_t const* slot_dst, T const* buf,
                   int64_t ldb, T* A, int64_t lda, RowDist const& d);
 
+/// Distributed partial pivoting, one panel column per call (reference
+/// Tile_getrf.hh:270 MAXLOC + row exchange): elements of T per process in the
+/// per-column all-gather, the local candidate entry, and the replicated
+/// winner selection + swap + rank-1 update (see kernels/lu_dist.hip).
+template <typename T>
+int64_t pplu_entry(int64_t kb);
+template <typename T>
+void pplu_cand(lb::Ctx const& c, int64_t mr, int64_t j, int64_t r0, T const* ap, int64_t lda, int64_t kb,
+               RowDist const& d, int64_t lr_k, bool is_pk, T* buf);
+template <typename T>
+void pplu_apply(lb::Ctx const& c, int np, T const* gbuf, int64_t kb, int64_t j, int64_t cend, int64_t mr,
+                int64_t r_upd0, T* ap, int64_t lda, RowDist const& d, int64_t lr_k, int64_t kk, int pk, double thresh,
+                bool is_pk, int64_t* pip, int* info, int64_t info_off);
+
 /// Sign-modified LU without pivoting of the n x n block A (TSQR Householder
 /// reconstruction): for each column j the diagonal b gets s_j = b/|b| added
 /// (|pivot| = 1 + |b|); Y (unit lower) and U' overwrite A, sgn[j] = s_j.

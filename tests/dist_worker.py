@@ -197,6 +197,26 @@ def case_getrf(tg, dt, nb):
         assert relerr(a @ s.to_numpy(B), b) < 100 * tol(dt), method
 
 
+def case_getrf_thresh(tg, dt, nb):
+    """PivotThreshold in the distributed per-column pivot search: P A = L U
+    and |L| <= 1 / threshold."""
+    n = 170
+    a = rnd(n, n, dt, 95) + 1.5 * np.eye(n, dtype=dt)
+    for thresh in (0.5, 0.1):
+        A = s.from_numpy(a, nb=nb, target=tg)
+        info, piv = s.getrf(A, target=tg, pivot_threshold=thresh)
+        assert info == 0
+        f = s.to_numpy(A)
+        Lf = np.tril(f, -1) + np.eye(n, dtype=dt)
+        pa = a.copy()
+        for i, r in enumerate(ipiv_of(piv, nb)):
+            if r != i:
+                pa[[i, r]] = pa[[r, i]]
+        assert relerr(Lf @ np.triu(f), pa) < 100 * tol(dt), thresh
+        bound = (np.sqrt(2) if np.iscomplexobj(a) else 1) / thresh   # pivots chosen by |re| + |im|
+        assert np.abs(Lf).max() <= bound * (1 + 1e-5), (thresh, np.abs(Lf).max())
+
+
 def ipiv_of(piv, nb):
     """Reference Pivots (per block column k: (tile index rel. to k, offset)) ->
     LAPACK-style 0-based sequential interchanges."""
