@@ -29,9 +29,11 @@ namespace host {
 template <typename T>
 struct Reflectors {
     std::vector<int64_t> off, len, voff;
+    std::vector<int64_t> tag;   // producer's label (hb2st: the sweep), -1 if none
     std::vector<T> tau, v;
-    void push(int64_t o, int64_t l, T t, T const* vec) {
+    void push(int64_t o, int64_t l, T t, T const* vec, int64_t tg = -1) {
         off.push_back(o); len.push_back(l); voff.push_back(int64_t(v.size())); tau.push_back(t);
+        tag.push_back(tg);
         v.insert(v.end(), vec, vec + l);
     }
     size_t size() const { return tau.size(); }
@@ -39,9 +41,12 @@ struct Reflectors {
     void apply_left(bool trans, int64_t ncols, T* C, int64_t ldc) const;
 };
 
-/// Hermitian band (lower, bandwidth kd, full dense storage n x n in A) to real
-/// symmetric tridiagonal (d, e).  Reflectors and the diagonal phase (so that
-/// A = Q diag(phase) T diag(phase)^H Q^H) are returned for the back-transform.
+/// Hermitian band (lower, bandwidth kd) to real symmetric tridiagonal (d, e).
+/// A is addressed as A[i + j lda] for |i - j| <= 2 kd only, so either dense
+/// n x n storage or general band storage with kl = ku = 2 kd works (through
+/// the skew A = ab + 2 kd, lda = ldab - 1).  Reflectors (tagged with their
+/// sweep) and the diagonal phase (A = Q diag(phase) T diag(phase)^H Q^H) are
+/// returned for the back-transform.
 template <typename T>
 void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& d, std::vector<real_type<T>>& e,
            Reflectors<T>& Q, std::vector<T>& phase);

@@ -78,6 +78,11 @@ void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int6
                 int64_t lda, RowDist d, int64_t lr_k, int64_t kk, int pk, double thresh, bool is_pk, int64_t* pip,
                 int* info, int64_t info_off, hipStream_t s);
 
+// ---- eigensolver back-transform (eig.hip)
+/// G (k x k Gram V^H V) -> T^{-1} = striu(G) + diag(1 / tau) in place.
+template <typename T>
+void tinv_from_gram(int64_t k, T* G, int64_t ldg, const T* tau, hipStream_t s);
+
 // ---- butterfly transforms (rbt.hip)
 /// by_rows: buf(t, j) = A(idx[t], j) for t < cnt, j < len (scatter: the reverse);
 /// by columns: buf(i, t) = A(i, idx[t]) for i < len.

@@ -13,8 +13,11 @@
 // the stage-1 back-transform runs distributed (unmqr / unmlq on Z, U, VT).
 #include "internal.hh"
 #include "slate_amd/eig_host.hh"
+#include "../kernels/kernels.hh"
 
+#include <algorithm>
 #include <cmath>
+#include <map>
 
 namespace slate {
 
@@ -46,24 +49,220 @@ void fill_from_host(Matrix<T>& M, std::vector<T> const& h, int64_t ldh) {
 template <typename T>
 bool wanted(Matrix<T> const& M) { return M.m() > 0 && M.n() > 0; }
 
+/// Band of a distributed matrix (reference heev.cc he2hbGather, but onto every
+/// process): only the tiles (k, k) and (k+1, k) (lower) or (k, k+1) (upper)
+/// move, and only their entries with 0 <= i - j <= kd (lower) or 0 <= j - i
+/// <= kd (upper), into general band storage with kl = ku = 2 kd (room for the
+/// bulge chase): (i, j) at ab[2 kd + i - j + j ldab], ldab = 4 kd + 1.  One
+/// world all-reduce of O(n kd) data; no n x n array anywhere.  Hermitian
+/// (mirror = true): the other half is filled with the conjugate.
+template <typename T>
+std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, bool lower, bool mirror, Options const& opts) {
+    trace::Block tb("gather_band");
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
+    auto& g = *A.grid();
+    const int64_t n = std::min(A.m(), A.n()), ldab = 4 * kd + 1;
+    std::vector<T> ab(size_t(ldab) * std::max<int64_t>(n, 1), T(0));
+    LocalBlock<T> la = A.local(loc, false);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    const int64_t mb = A.mb(), nbt = A.nb();
+    Work<T> dt(target, size_t(mb) * nbt);
+    std::vector<T> ht(size_t(mb) * nbt);
+    auto take = [&](int64_t i, int64_t j) {
+        if (i < 0 || j < 0 || i >= A.mt() || j >= A.nt()) return;
+        if (A.srow_owner(i) != g.myrow() || A.scol_owner(j) != g.mycol()) return;
+        const int64_t tm = A.tileMb(i), tn = A.tileNb(j), gi0 = grow_of(A, i), gj0 = gcol_of(A, j);
+        T const* src = la.ptr + lrow_of(A, i) + lcol_of(A, j) * la.ld;
+        if (c.dev()) {
+            lb::copy2d(c, tm, tn, src, la.ld, dt.data(), tm);
+            device::memcpy_async(ht.data(), dt.data(), size_t(tm) * tn * sizeof(T), c.stream);
+            slate_hip_call(hipStreamSynchronize(c.stream));
+        } else {
+            for (int64_t jj = 0; jj < tn; ++jj)
+                for (int64_t ii = 0; ii < tm; ++ii) ht[ii + jj * tm] = src[ii + jj * la.ld];
+        }
+        for (int64_t jj = 0; jj < tn; ++jj)
+            for (int64_t ii = 0; ii < tm; ++ii) {
+                const int64_t gi = gi0 + ii, gj = gj0 + jj, off = lower ? gi - gj : gj - gi;
+                if (off < 0 || off > kd || gi >= n || gj >= n) continue;
+                ab[size_t(2 * kd + gi - gj + gj * ldab)] = ht[ii + jj * tm];
+            }
+    };
+    for (int64_t k = 0; k < std::min(A.mt(), A.nt()); ++k) {
+        take(k, k);
+        if (lower) take(k + 1, k);
+        else take(k, k + 1);
+    }
+    internal::allreduce_host(g.world(), ab.data(), ab.size(), ReduceOp::Sum);
+    if (mirror) {
+        for (int64_t j = 0; j < n; ++j) {
+            for (int64_t i = j + 1; i <= std::min(n - 1, j + kd); ++i) {
+                T& lo = ab[size_t(2 * kd + i - j + j * ldab)];
+                T& up = ab[size_t(2 * kd + j - i + i * ldab)];
+                if (lower) up = slate::conj(lo); else lo = slate::conj(up);
+            }
+            T& dd = ab[size_t(2 * kd + j * ldab)];
+            dd = T(std::real(dd));
+        }
+    }
+    return ab;
+}
+
 }  // namespace
 
 //------------------------------------------------------------------------------
-/// he2hb: A (dense Hermitian, general storage) -> band of width nb; the
-/// reflectors stay below the band, their T factors in Ts.
+/// he2hb: A (Hermitian, lower triangle referenced) -> band of width nb; the
+/// reflectors stay below the band, their T factors in Ts.  Per block column
+/// (reference src/he2hb.cc:401-572): geqrf of the panel, then the two-sided
+/// update A22 := Q^H A22 Q as  W = A22 V T  (hemm),  Y = W - V (T^H V^H W)/2
+/// (local, one column all-reduce of the nb x nb V^H W),  A22 -= V Y^H + Y V^H
+/// (her2k on the lower triangle only) -- half the flops of applying Q from
+/// both sides to the full square.
 template <typename T>
 void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& opts) {
     trace::Block tb("he2hb");
     internal::DriverScope ds_;
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
     const int64_t nt = A.nt();
+    auto gA = A.grid();
     Ts.assign(std::max<int64_t>(nt - 1, 0), {});
     for (int64_t k = 0; k + 1 < nt; ++k) {
         Matrix<T> panel = A.sub(k + 1, nt - 1, k, k);
         geqrf(panel, Ts[k], opts);
-        Matrix<T> A22 = A.sub(k + 1, nt - 1, k + 1, nt - 1);
-        unmqr(Side::Left, Op::ConjTrans, panel, Ts[k], A22, opts);
-        unmqr(Side::Right, Op::NoTrans, panel, Ts[k], A22, opts);
+        const int64_t m = panel.m(), kb = panel.n();
+        // explicit unit-lower V on the panel's layout
+        Matrix<T> V(m, kb, A.mb(), kb, gA, panel.srow_owner(0), panel.scol_owner(0));
+        V.insertLocalTiles(target);
+        slate::copy<T, T>(panel, V, opts);
+        {
+            TrapezoidMatrix<T> V0(Uplo::Upper, Diag::NonUnit, V.sub(0, 0, 0, 0));
+            set(T(0), T(1), V0, opts);
+        }
+        HermitianMatrix<T> A22(Uplo::Lower, A.sub(k + 1, nt - 1, k + 1, nt - 1));
+        Matrix<T> W = V.emptyLike();
+        W.insertLocalTiles(target);
+        hemm(Side::Left, T(1), A22, V, T(0), W, opts);
+        {
+            trace::Block t2("he2hb_wy");
+            LocalBlock<T> lv = V.local(loc, false), lw = W.local(loc, true);
+            LocalBlock<T> lt = Ts[k][0].local(loc, false);
+            if (lw.n > 0) {
+                lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+                Work<T> X(target, size_t(kb) * kb);
+                lb::trmm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, lw.m, kb, T(1), lt.ptr, lt.ld,
+                         lw.ptr, lw.ld);
+                if (lw.m > 0)
+                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, kb, kb, lw.m, T(1), lv.ptr, lv.ld, lw.ptr, lw.ld, T(0),
+                             X.data(), kb);
+                else
+                    lb::set(c, Uplo::General, kb, kb, T(0), T(0), X.data(), kb);
+                if (gA->col().size() > 1)
+                    gA->col().allreduce(X.data(), size_t(kb) * kb, ReduceOp::Sum, loc, c.stream);
+                lb::trmm(c, Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, kb, kb, T(1), lt.ptr, lt.ld,
+                         X.data(), kb);
+                if (lw.m > 0)
+                    lb::gemm(c, Op::NoTrans, Op::NoTrans, lw.m, kb, kb, T(-0.5), lv.ptr, lv.ld, X.data(), kb, T(1),
+                             lw.ptr, lw.ld);
+                if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+            }
+            W.storage()->modified(loc);
+        }
+        her2k(T(-1), V, W, real_type<T>(1), A22, opts);
     }
+}
+
+/// Z := Q2 Z on the device for the hb2st reflectors (reference
+/// unmtr_hb2st.cc).  The reflectors of GS consecutive sweeps J GS .. J GS +
+/// GS - 1 at the same bulge step t act on rows r0 + i .. r0 + i + kd - 1
+/// (r0 = J GS + t kd + 1, i = sweep - J GS): one (GS + kd) x GS block V with
+/// H_{J GS} ... H_{J GS + GS - 1} = I - V T V^H.  Reflector (j, t) only has to
+/// precede the overlapping (j + d, t) and (j + d, t - 1), (j + d, t - 2) of
+/// later sweeps, and two reflectors of one sweep touch disjoint rows, so Q2 is
+/// the product over J ascending, t DEScending of the blocks, and Z is updated
+/// for J descending, t ascending:  W = V^H Z_r,  W := T W (triangular solve
+/// with T^{-1} = striu(V^H V) + diag(1/tau)),  Z_r -= V W.  GS = 4 kd keeps
+/// the GEMMs large (about 2 n^2 / (GS kd) blocks).  Z holds all n rows of its
+/// columns (1-D column layout).  Host and device run the same blocked
+/// sequence (lb:: dispatch), so the CPU tests check the ordering.
+template <typename T>
+void unmtr_hb2st_blocked(host::Reflectors<T> const& Q, int64_t n, int64_t kd, T* Z, int64_t ldz, int64_t ncols,
+                        lb::Ctx const& c) {
+    trace::Block tb("unmtr_hb2st_blocked");
+    namespace kd_ = slate_amd::dev;
+    if (Q.size() == 0 || ncols <= 0) return;
+    const int64_t GS = 4 * kd;
+    std::map<std::pair<int64_t, int64_t>, std::vector<size_t>> groups;
+    for (size_t r = 0; r < Q.size(); ++r) {
+        const int64_t j = Q.tag[r];
+        slate_assert(j >= 0);
+        groups[{j / GS, (Q.off[r] - j - 1) / kd}].push_back(r);
+    }
+    std::vector<std::pair<int64_t, int64_t>> keys;
+    for (auto& kv : groups) keys.push_back(kv.first);
+    std::sort(keys.begin(), keys.end(), [](auto const& a, auto const& b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    const int64_t vr = GS + kd, VB = vr * GS;
+    const size_t ng = keys.size();
+    std::vector<T> hV(ng * VB, T(0)), ht(ng * GS, T(0));
+    std::vector<int64_t> r0s(ng), ws(ng);
+    #pragma omp parallel for schedule(dynamic)
+    for (size_t gi = 0; gi < ng; ++gi) {
+        const int64_t J = keys[gi].first, t = keys[gi].second, r0 = J * GS + t * kd + 1;
+        r0s[gi] = r0;
+        int64_t w = 0;
+        for (size_t r : groups.at(keys[gi])) {
+            const int64_t i = Q.tag[r] - J * GS;
+            slate_assert(Q.off[r] - r0 == i && i + Q.len[r] <= vr);
+            T const* v = Q.v.data() + Q.voff[r];
+            for (int64_t ii = 0; ii < Q.len[r]; ++ii) hV[gi * VB + (i + ii) + i * vr] = v[ii];
+            ht[gi * GS + i] = Q.tau[r];
+            w = std::max(w, i + 1);
+        }
+        ws[gi] = w;
+    }
+    const Target tg = c.dev() ? Target::Devices : Target::HostTask;
+    Work<T> dV, dt;
+    if (c.dev()) {
+        dV.resize(tg, hV.size());
+        dt.resize(tg, ht.size());
+        device::memcpy_async(dV.data(), hV.data(), hV.size() * sizeof(T), c.stream);
+        device::memcpy_async(dt.data(), ht.data(), ht.size() * sizeof(T), c.stream);
+    }
+    T const* Vall = c.dev() ? dV.data() : hV.data();
+    T const* tall = c.dev() ? dt.data() : ht.data();
+    Work<T> G(tg, size_t(GS) * GS), W(tg, size_t(GS) * ncols);
+    auto tinv = [&](int64_t w, T* Gm, T const* tau) {
+        if (c.dev()) { kd_::tinv_from_gram(w, kd_::dptr(Gm), GS, kd_::dptr(tau), c.stream); return; }
+        for (int64_t j = 0; j < w; ++j)
+            for (int64_t i = 0; i < w; ++i) {
+                T& x = Gm[i + j * GS];
+                if (i > j) x = T(0);
+                else if (i == j) x = tau[i] == T(0) ? T(1) : T(1) / tau[i];
+            }
+    };
+    for (size_t gi = 0; gi < ng; ++gi) {
+        const int64_t r0 = r0s[gi], w = ws[gi];                 // w: columns in use
+        const int64_t rows = std::min(w - 1 + kd, n - r0);
+        if (rows <= 0 || w <= 0) continue;
+        T const* V = Vall + gi * VB;
+        T* Zr = Z + r0;
+        lb::gemm(c, Op::ConjTrans, Op::NoTrans, w, w, rows, T(1), V, vr, V, vr, T(0), G.data(), GS);
+        tinv(w, G.data(), tall + gi * GS);
+        lb::gemm(c, Op::ConjTrans, Op::NoTrans, w, ncols, rows, T(1), V, vr, Zr, ldz, T(0), W.data(), GS);
+        lb::trsm(c, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, w, ncols, T(1), G.data(), GS, W.data(), GS);
+        lb::gemm(c, Op::NoTrans, Op::NoTrans, rows, ncols, w, T(-1), V, vr, W.data(), GS, T(1), Zr, ldz);
+    }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+}
+
+/// 1 x P grid over the processes of g (every row local: 1-D column layout)
+inline GridPtr row_grid(GridPtr const& g) {
+    if (g->p() == 1) return g;
+    return std::make_shared<Grid>(1, g->size(), GridOrder::Col, g->world_ptr(), g->world_ptr(),
+                                  std::make_shared<SelfComm>());
 }
 
 template <typename T>
@@ -71,29 +270,38 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     trace::Block tb("heev");
     internal::DriverScope ds_;
     using R = real_type<T>;
-    const int64_t n = A.n(), nb = A.nb(), nt = A.nt();
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
+    const int64_t n = A.n();
     Lambda.assign(n, R(0));
     if (n == 0) return;
-    Matrix<T> F = hermitian_full(A, opts);
+    // band width of the two-stage reduction: the bulge chase costs O(n^2 kd)
+    // on the host, the first stage is memory-bound either way, so large tiles
+    // are re-tiled to kd <= 64 (reference uses the tile size)
+    const int64_t kd = std::min<int64_t>(A.nb(), 64);
+    auto gA = A.grid();
+    Matrix<T> F(n, n, kd, kd, gA);
+    F.insertLocalTiles(target);
+    {
+        Matrix<T> Ag(A);
+        Ag.set_uplo(Uplo::General);
+        BaseTrapezoidMatrix<T> At(A.uplo(), Ag, MatrixKind::Trapezoid);
+        BaseTrapezoidMatrix<T> Fl(Uplo::Lower, F, MatrixKind::Trapezoid);
+        if (A.uplo() == Uplo::Lower) slate::copy<T, T>(At, Fl, opts);
+        else slate::copy<T, T>(conj_transpose(Ag), F, opts);   // upper: mirror into the lower triangle
+    }
+    const int64_t nt = F.nt();
     std::vector<TriangularFactors<T>> Ts;
     he2hb(F, Ts, opts);
-    // stage 2 on the host: band (lower, width nb) -> tridiagonal
-    std::vector<T> full;
-    gather(F, full, opts);
-    std::vector<T> B(size_t(n) * n, T(0));
-    for (int64_t j = 0; j < n; ++j)
-        for (int64_t i = j; i <= std::min(n - 1, j + nb); ++i) {
-            B[i + j * n] = full[i + j * n];
-            B[j + i * n] = slate::conj(full[i + j * n]);
-        }
-    for (int64_t i = 0; i < n; ++i) B[i + i * n] = T(std::real(B[i + i * n]));
-    full.clear(); full.shrink_to_fit();
+    // stage 2 on the host: band (lower, width kd) -> tridiagonal, in band
+    // storage (the bulge chase stays within 2 kd of the diagonal)
+    std::vector<T> B = gather_band(F, kd, true, true, opts);
     std::vector<R> d, e;
     host::Reflectors<T> Q2;
     std::vector<T> phase;
     {
         trace::Block t2("hb2st");
-        host::hb2st<T>(n, nb, B.data(), n, d, e, Q2, phase);
+        host::hb2st<T>(n, kd, B.data() + 2 * kd, 4 * kd, d, e, Q2, phase);
     }
     B.clear(); B.shrink_to_fit();
     if (!wanted(Z)) {
@@ -115,25 +323,47 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         }
     }
     Lambda = d;
-    std::vector<T> Zc(size_t(n) * n);
-    for (int64_t j = 0; j < n; ++j)
-        for (int64_t i = 0; i < n; ++i) Zc[i + j * n] = phase[i] * T(Zr[i + j * n]);
-    Zr.clear(); Zr.shrink_to_fit();
+    // Z1 (1-D column layout, kd-wide column tiles): my columns of
+    // diag(phase) Zr, then Q2 applied to all rows of them
+    Matrix<T> Z1(n, n, n, kd, row_grid(gA));
+    Z1.insertLocalTiles(target);
     {
         trace::Block t2("unmtr_hb2st");
-        Q2.apply_left(false, n, Zc.data(), n);
+        LocalBlock<T> lz = Z1.local(loc, true);
+        std::vector<T> hz(size_t(n) * std::max<int64_t>(lz.n, 1));
+        for (int64_t j = 0; j < Z1.nt(); ++j) {
+            if (Z1.scol_owner(j) != Z1.grid()->mycol()) continue;
+            const int64_t lc = lcol_of(Z1, j), gc = gcol_of(Z1, j);
+            for (int64_t jj = 0; jj < Z1.tileNb(j); ++jj)
+                for (int64_t i = 0; i < n; ++i) hz[i + (lc + jj) * n] = phase[i] * T(Zr[i + (gc + jj) * n]);
+        }
+        Zr.clear(); Zr.shrink_to_fit();
+        if (lz.n > 0) {
+            lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+            if (c.dev())
+                device::memcpy2d_async(lz.ptr, lz.ld * sizeof(T), hz.data(), n * sizeof(T), n * sizeof(T), lz.n,
+                                       c.stream);
+            else
+                for (int64_t j = 0; j < lz.n; ++j)
+                    std::copy(hz.begin() + j * n, hz.begin() + (j + 1) * n, lz.ptr + j * lz.ld);
+            unmtr_hb2st_blocked(Q2, n, kd, lz.ptr, lz.ld, lz.n, c);
+        }
     }
-    fill_from_host(Z, Zc, n);
-    Target target = resolve_target(opts);
-    if (target == Target::Devices) Z.insertLocalTiles(Target::Devices);
-    // stage-1 back-transform (unmtr_he2hb)
-    trace::Block t3("unmtr_he2hb");
-    const int64_t znt = Z.nt();
-    for (int64_t k = nt - 2; k >= 0; --k) {
-        Matrix<T> panel = F.sub(k + 1, nt - 1, k, k);
-        Matrix<T> Zk = Z.sub(k + 1, nt - 1, 0, znt - 1);
-        unmqr(Side::Left, Op::NoTrans, panel, Ts[k], Zk, opts);
+    // stage-1 back-transform (unmtr_he2hb) on F's layout, then into Z
+    Matrix<T> Zw(n, n, kd, kd, gA);
+    Zw.insertLocalTiles(target);
+    slate::copy<T, T>(Z1, Zw, opts);
+    {
+        trace::Block t3("unmtr_he2hb");
+        const int64_t znt = Zw.nt();
+        for (int64_t k = nt - 2; k >= 0; --k) {
+            Matrix<T> panel = F.sub(k + 1, nt - 1, k, k);
+            Matrix<T> Zk = Zw.sub(k + 1, nt - 1, 0, znt - 1);
+            unmqr(Side::Left, Op::NoTrans, panel, Ts[k], Zk, opts);
+        }
     }
+    slate::copy<T, T>(Zw, Z, opts);
+    (void)loc;
 }
 
 //------------------------------------------------------------------------------

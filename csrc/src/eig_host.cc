@@ -150,7 +150,7 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
             for (int64_t i = 1; i < L; ++i) { a(s0 + i, k) = T(0); a(k, s0 + i) = T(0); }
             if (tau != T(0)) {
                 two_sided(k, s0, L, tau, v, w);
-                Qs[j].push(s0, L, tau, v);
+                Qs[j].push(s0, L, tau, v, j);
             }
             prog[j].store(t + 1, std::memory_order_release);
             // next bulge: column s0 below its band
@@ -170,7 +170,7 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
         for (int64_t j = tid; j < nsw; j += nth) sweep(j, v.data(), w.data());
     }
     for (auto& q : Qs) {
-        for (size_t r = 0; r < q.size(); ++r) Q.push(q.off[r], q.len[r], q.tau[r], q.v.data() + q.voff[r]);
+        for (size_t r = 0; r < q.size(); ++r) Q.push(q.off[r], q.len[r], q.tau[r], q.v.data() + q.voff[r], q.tag[r]);
         q = Reflectors<T>();
     }
     d.assign(n, R(0));

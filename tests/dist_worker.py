@@ -172,6 +172,23 @@ def case_rbt(tg, dt, nb):
     assert relerr(a @ s.to_numpy(X), b) < 100 * tol(dt)
 
 
+def case_heev(tg, dt, nb):
+    """Two-stage heev on the grid (he2hb two-sided update, band-only gather,
+    distributed back-transforms): eigenvalues vs numpy and ||H Z - Z L||."""
+    n = 150
+    a = rnd(n, n, dt, 97)
+    h = (a + a.conj().T).astype(dt)
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+    Z = s.from_numpy(np.zeros((n, n), dt), nb=nb, target=tg)
+    lam = s.heev(H, Z, target=tg)
+    ref = np.linalg.eigvalsh(h)
+    assert np.abs(np.sort(lam) - ref).max() <= 100 * tol(dt) * np.abs(ref).max(), "eigenvalues"
+    z = s.to_numpy(Z)
+    assert np.linalg.norm(h @ z - z * lam) <= 100 * tol(dt) * np.linalg.norm(h) * np.sqrt(n), "vectors"
+    sv = s.svd_vals(s.from_numpy(a, nb=nb, target=tg), target=tg)
+    assert np.abs(np.sort(sv)[::-1] - np.linalg.svd(a, compute_uv=False)).max() <= 100 * tol(dt) * sv.max()
+
+
 def case_potrf(tg, dt, nb):
     n = 200
     a = rnd(n, n, dt, 7)
