@@ -105,5 +105,30 @@ void set_stedc_gemm(StedcGemm f);
 template <typename R, typename T>
 int64_t bdsqr(int64_t n, R* d, R* e, T* U, int64_t ldu, int64_t urows, T* VT, int64_t ldvt, int64_t vcols);
 
+/// Plane rotation on columns (i, i+1): [x y] <- [c x - s y, s x + c y].
+template <typename R>
+struct PlaneRot { int64_t i; R c, s; };
+
+/// Where bdsqr's transformations go: U (rows x n) and Vt = VT^T (rows x n)
+/// are only ever changed through these calls, so a device backend can batch
+/// the sweeps and apply them on the GPU while the host iterates on (d, e).
+template <typename R>
+struct RotSink {
+    virtual ~RotSink() = default;
+    /// one implicit-shift QR sweep: adjacent rotations, ascending, on U (ru) and Vt (rv)
+    virtual void sweep(std::vector<PlaneRot<R>> const& ru, std::vector<PlaneRot<R>> const& rv) = 0;
+    /// cancellation rotation on U columns (a, b): [x y] <- [x c + y s, y c - x s]
+    virtual void rot_u(int64_t a, int64_t b, R c, R s) = 0;
+    /// Vt column k *= -1
+    virtual void negate_v(int64_t k) = 0;
+    /// final ordering: new column i = old column perm[i] (U and Vt)
+    virtual void permute(std::vector<int64_t> const& perm) = 0;
+};
+
+/// bdsqr on (d, e) with every transformation sent to `sink` (may be null:
+/// values only).  Returns the number of unconverged values.
+template <typename R>
+int64_t bdsqr_core(int64_t n, R* d, R* e, RotSink<R>* sink);
+
 }  // namespace host
 }  // namespace slate

@@ -82,6 +82,17 @@ void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int6
 /// G (k x k Gram V^H V) -> T^{-1} = striu(G) + diag(1 / tau) in place.
 template <typename T>
 void tinv_from_gram(int64_t k, T* G, int64_t ldg, const T* tau, hipStream_t s);
+/// sweeps per rot_sweeps call
+constexpr int kRotBatch = 16;
+/// Apply kRotBatch QR sweeps of plane rotations to the columns [p0, p1) of
+/// every row of M (rows x n): sweep s rotates columns (j, j+1) with
+/// (C[s n + j], S[s n + j]), [x y] <- [c x - s y, s x + c y], j ascending.
+template <typename T>
+void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t n, int64_t p0, int64_t p1, const rt<T>* C, const rt<T>* S,
+                hipStream_t s);
+/// One rotation on columns (a, b): [x y] <- [x c + y s, y c - x s].
+template <typename T>
+void rot_cols(int64_t rows, T* M, int64_t ld, int64_t a, int64_t b, rt<T> c, rt<T> sn, hipStream_t s);
 
 // ---- butterfly transforms (rbt.hip)
 /// by_rows: buf(t, j) = A(idx[t], j) for t < cnt, j < len (scatter: the reverse);

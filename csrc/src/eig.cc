@@ -52,17 +52,17 @@ bool wanted(Matrix<T> const& M) { return M.m() > 0 && M.n() > 0; }
 /// Band of a distributed matrix (reference heev.cc he2hbGather, but onto every
 /// process): only the tiles (k, k) and (k+1, k) (lower) or (k, k+1) (upper)
 /// move, and only their entries with 0 <= i - j <= kd (lower) or 0 <= j - i
-/// <= kd (upper), into general band storage with kl = ku = 2 kd (room for the
-/// bulge chase): (i, j) at ab[2 kd + i - j + j ldab], ldab = 4 kd + 1.  One
-/// world all-reduce of O(n kd) data; no n x n array anywhere.  Hermitian
-/// (mirror = true): the other half is filled with the conjugate.
+/// <= kd (upper), into general band storage with kl = ku = M (room for the
+/// bulge chase: M = 2 kd for hb2st, 3 kd + 2 for tb2bd): (i, j) at
+/// ab[M + i - j + j ldab], ldab = 2 M + 1.  One world all-reduce of O(n kd)
+/// data; no n x n array anywhere.  Hermitian (mirror = true): the other half is filled with the conjugate.
 template <typename T>
-std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, bool lower, bool mirror, Options const& opts) {
+std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, int64_t M, bool lower, bool mirror, Options const& opts) {
     trace::Block tb("gather_band");
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     auto& g = *A.grid();
-    const int64_t n = std::min(A.m(), A.n()), ldab = 4 * kd + 1;
+    const int64_t n = std::min(A.m(), A.n()), ldab = 2 * M + 1;
     std::vector<T> ab(size_t(ldab) * std::max<int64_t>(n, 1), T(0));
     LocalBlock<T> la = A.local(loc, false);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -86,7 +86,7 @@ std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, bool lower, bool mirr
             for (int64_t ii = 0; ii < tm; ++ii) {
                 const int64_t gi = gi0 + ii, gj = gj0 + jj, off = lower ? gi - gj : gj - gi;
                 if (off < 0 || off > kd || gi >= n || gj >= n) continue;
-                ab[size_t(2 * kd + gi - gj + gj * ldab)] = ht[ii + jj * tm];
+                ab[size_t(M + gi - gj + gj * ldab)] = ht[ii + jj * tm];
             }
     };
     for (int64_t k = 0; k < std::min(A.mt(), A.nt()); ++k) {
@@ -98,11 +98,11 @@ std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, bool lower, bool mirr
     if (mirror) {
         for (int64_t j = 0; j < n; ++j) {
             for (int64_t i = j + 1; i <= std::min(n - 1, j + kd); ++i) {
-                T& lo = ab[size_t(2 * kd + i - j + j * ldab)];
-                T& up = ab[size_t(2 * kd + j - i + i * ldab)];
+                T& lo = ab[size_t(M + i - j + j * ldab)];
+                T& up = ab[size_t(M + j - i + i * ldab)];
                 if (lower) up = slate::conj(lo); else lo = slate::conj(up);
             }
-            T& dd = ab[size_t(2 * kd + j * ldab)];
+            T& dd = ab[size_t(M + j * ldab)];
             dd = T(std::real(dd));
         }
     }
@@ -265,6 +265,186 @@ inline GridPtr row_grid(GridPtr const& g) {
                                   std::make_shared<SelfComm>());
 }
 
+/// P x 1 grid over the processes of g (all columns local: 1-D row layout)
+inline GridPtr col_grid(GridPtr const& g) {
+    if (g->q() == 1) return g;
+    return std::make_shared<Grid>(g->size(), 1, GridOrder::Col, g->world_ptr(), std::make_shared<SelfComm>(),
+                                  g->world_ptr());
+}
+
+/// bdsqr transformations on the local rows of U and Vt (row layout: rows are
+/// independent under column rotations, so no communication).  Device: QR
+/// sweeps are batched kRotBatch at a time into pinned (C, S) buffers and
+/// applied by the register-window wavefront kernel (double-buffered, the host
+/// keeps iterating on (d, e) meanwhile); host: loops.
+template <typename T>
+struct RowRotSink : host::RotSink<real_type<T>> {
+    using R = real_type<T>;
+    static constexpr int K = slate_amd::dev::kRotBatch;
+    lb::Ctx c;
+    int64_t n = 0;
+    T* U = nullptr; int64_t ldu = 0, urows = 0;
+    T* V = nullptr; int64_t ldv = 0, vrows = 0;
+    // batch staging: [Cu | Su | Cv | Sv], K x n each
+    R* hb[2] = {nullptr, nullptr};
+    Work<R> db[2];
+    hipEvent_t ev[2] = {nullptr, nullptr};
+    int cur = 0, ns = 0;
+    int64_t ulo = 0, uhi = 0, vlo = 0, vhi = 0;   // union of the batch's rotation ranges
+
+    RowRotSink(lb::Ctx const& c_, int64_t n_) : c(c_), n(n_) {
+        if (c.dev()) {
+            for (int b = 0; b < 2; ++b) {
+                hb[b] = static_cast<R*>(device::malloc_host(sizeof(R) * 4 * K * size_t(n)));
+                db[b].resize(Target::Devices, size_t(4) * K * n);
+                ev[b] = device::event_get();
+                slate_hip_call(hipEventRecord(ev[b], c.stream));
+            }
+        }
+    }
+    ~RowRotSink() override {
+        if (c.dev()) {
+            (void)hipStreamSynchronize(c.stream);
+            for (int b = 0; b < 2; ++b) { device::free_host(hb[b]); device::event_put(ev[b]); }
+        }
+    }
+    R* Cs(int which) { return hb[cur] + size_t(which) * K * n; }
+    void rot_host(T* M, int64_t ld, int64_t rows, std::vector<host::PlaneRot<R>> const& rs) {
+        if (!M) return;
+        for (auto const& g : rs) {
+            T* x = M + g.i * ld;
+            T* y = M + (g.i + 1) * ld;
+            for (int64_t r = 0; r < rows; ++r) {
+                T a = x[r], b = y[r];
+                x[r] = g.c * a - g.s * b;
+                y[r] = g.s * a + g.c * b;
+            }
+        }
+    }
+    void flush() {
+        if (!c.dev() || ns == 0) return;
+        namespace kd_ = slate_amd::dev;
+        // identity rows for unused sweeps of this batch
+        for (int q = ns; q < K; ++q)
+            for (int w = 0; w < 4; w += 2) {
+                R* C = hb[cur] + size_t(w) * K * n + size_t(q) * n;
+                R* S = hb[cur] + size_t(w + 1) * K * n + size_t(q) * n;
+                const int64_t lo = w == 0 ? ulo : vlo, hi = w == 0 ? uhi : vhi;
+                for (int64_t j = lo; j < hi; ++j) { C[j] = R(1); S[j] = R(0); }
+            }
+        device::memcpy_async(db[cur].data(), hb[cur], sizeof(R) * 4 * K * size_t(n), c.stream);
+        R const* d0 = db[cur].data();
+        if (U && uhi > ulo)
+            kd_::rot_sweeps(urows, kd_::dptr(U), ldu, n, ulo, uhi + 1, d0, d0 + size_t(K) * n, c.stream);
+        if (V && vhi > vlo)
+            kd_::rot_sweeps(vrows, kd_::dptr(V), ldv, n, vlo, vhi + 1, d0 + size_t(2) * K * n, d0 + size_t(3) * K * n,
+                            c.stream);
+        slate_hip_call(hipEventRecord(ev[cur], c.stream));
+        cur ^= 1;
+        ns = 0;
+        slate_hip_call(hipEventSynchronize(ev[cur]));   // the other staging buffer is free again
+    }
+    void fill(int which, std::vector<host::PlaneRot<R>> const& rs, int64_t& lo, int64_t& hi) {
+        R* C = Cs(which) + size_t(ns) * n;
+        R* S = Cs(which + 1) + size_t(ns) * n;
+        // identity over the batch's union range, then this sweep's rotations
+        for (int64_t j = lo; j < hi; ++j) { C[j] = R(1); S[j] = R(0); }
+        if (rs.empty()) return;
+        const int64_t a = rs.front().i, b = rs.back().i + 1;
+        if (ns == 0) { lo = a; hi = b; }
+        else {
+            // widen the union: earlier sweeps of the batch need identity on the new part
+            for (int q = 0; q < ns; ++q) {
+                R* Cq = Cs(which) + size_t(q) * n;
+                R* Sq = Cs(which + 1) + size_t(q) * n;
+                for (int64_t j = a; j < lo; ++j) { Cq[j] = R(1); Sq[j] = R(0); }
+                for (int64_t j = hi; j < b; ++j) { Cq[j] = R(1); Sq[j] = R(0); }
+            }
+            for (int64_t j = std::min(a, lo); j < lo; ++j) { C[j] = R(1); S[j] = R(0); }
+            for (int64_t j = hi; j < std::max(b, hi); ++j) { C[j] = R(1); S[j] = R(0); }
+            lo = std::min(lo, a);
+            hi = std::max(hi, b);
+        }
+        for (auto const& g : rs) { C[g.i] = g.c; S[g.i] = g.s; }
+    }
+    void sweep(std::vector<host::PlaneRot<R>> const& ru, std::vector<host::PlaneRot<R>> const& rv) override {
+        if (!c.dev()) { rot_host(U, ldu, urows, ru); rot_host(V, ldv, vrows, rv); return; }
+        if (ns == K) flush();
+        if (ns == 0) { ulo = uhi = vlo = vhi = 0; }
+        fill(0, ru, ulo, uhi);
+        fill(2, rv, vlo, vhi);
+        ++ns;
+    }
+    void rot_u(int64_t a, int64_t b, R cc, R sn) override {
+        if (!U) return;
+        if (!c.dev()) {
+            T* x = U + a * ldu;
+            T* y = U + b * ldu;
+            for (int64_t r = 0; r < urows; ++r) {
+                T p = x[r], q = y[r];
+                x[r] = p * cc + q * sn;
+                y[r] = q * cc - p * sn;
+            }
+            return;
+        }
+        flush();
+        slate_amd::dev::rot_cols(urows, slate_amd::dev::dptr(U), ldu, a, b, cc, sn, c.stream);
+    }
+    void negate_v(int64_t k) override {
+        if (!V) return;
+        flush();
+        lb::scale(c, Uplo::General, vrows, int64_t(1), R(-1), R(1), V + k * ldv, ldv);
+    }
+    void permute(std::vector<int64_t> const& perm) override {
+        flush();
+        auto pc = [&](T* M, int64_t ld, int64_t rows) {
+            if (!M || rows <= 0) return;
+            Work<T> tmp(c.dev() ? Target::Devices : Target::HostTask, size_t(rows) * n);
+            if (c.dev()) {
+                Work<int64_t> dp(Target::Devices, perm.size());
+                device::memcpy_async(dp.data(), perm.data(), perm.size() * sizeof(int64_t), c.stream);
+                slate_amd::dev::rbt_gather(false, false, n, rows, dp.data(), slate_amd::dev::dptr(M), ld,
+                                           slate_amd::dev::dptr(tmp.data()), rows, c.stream);
+                lb::copy2d(c, rows, n, tmp.data(), rows, M, ld);
+                slate_hip_call(hipStreamSynchronize(c.stream));
+            } else {
+                for (int64_t i = 0; i < n; ++i)
+                    for (int64_t r = 0; r < rows; ++r) tmp.data()[r + i * rows] = M[r + perm[i] * ld];
+                for (int64_t i = 0; i < n; ++i)
+                    for (int64_t r = 0; r < rows; ++r) M[r + i * ld] = tmp.data()[r + i * rows];
+            }
+        };
+        pc(U, ldu, urows);
+        pc(V, ldv, vrows);
+    }
+    void finish() {
+        flush();
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    }
+};
+
+/// Local rows of a P x 1 row-layout n x n matrix set to diag(dg) (host build, one upload).
+template <typename T>
+void set_diag_rows(Matrix<T>& M, std::vector<T> const& dg, Target target) {
+    const Loc loc = loc_of(target);
+    LocalBlock<T> lm = M.local(loc, true);
+    const int64_t n = M.n();
+    std::vector<T> h(size_t(std::max<int64_t>(lm.m, 1)) * n, T(0));
+    for (int64_t i = 0; i < M.mt(); ++i) {
+        if (M.srow_owner(i) != M.grid()->myrow()) continue;
+        const int64_t lr = lrow_of(M, i), gr = grow_of(M, i);
+        for (int64_t ii = 0; ii < M.tileMb(i); ++ii) h[(lr + ii) + (gr + ii) * lm.m] = dg[gr + ii];
+    }
+    if (lm.m == 0) return;
+    if (target == Target::Devices) {
+        device::memcpy2d_async(lm.ptr, lm.ld * sizeof(T), h.data(), lm.m * sizeof(T), lm.m * sizeof(T), n,
+                               device::queue(0));
+        slate_hip_call(hipStreamSynchronize(device::queue(0)));
+    } else {
+        for (int64_t j = 0; j < n; ++j) std::copy(h.begin() + j * lm.m, h.begin() + (j + 1) * lm.m, lm.ptr + j * lm.ld);
+    }
+}
+
 template <typename T>
 void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts) {
     trace::Block tb("heev");
@@ -295,7 +475,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     he2hb(F, Ts, opts);
     // stage 2 on the host: band (lower, width kd) -> tridiagonal, in band
     // storage (the bulge chase stays within 2 kd of the diagonal)
-    std::vector<T> B = gather_band(F, kd, true, true, opts);
+    std::vector<T> B = gather_band(F, kd, 2 * kd, true, true, opts);
     std::vector<R> d, e;
     host::Reflectors<T> Q2;
     std::vector<T> phase;
@@ -464,65 +644,101 @@ void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>
         if (wanted(VT)) slate::copy<T, T>(conj_transpose(Uh), VT, opts);
         return;
     }
-    const int64_t nb = A.nb();
-    Matrix<T> W = A.emptyLike();
+    // stage 1 on kd-wide tiles (see heev)
+    const int64_t kd = std::min<int64_t>(A.nb(), 64);
+    auto gA = A.grid();
+    Matrix<T> W(m, n, kd, kd, gA);
     W.insertLocalTiles(target);
     slate::copy<T, T>(A, W, opts);
     std::vector<TriangularFactors<T>> TU, TV;
     ge2tb(W, TU, TV, opts);
-    std::vector<T> full;
-    gather(W, full, opts);
-    std::vector<T> Bd(size_t(n) * n, T(0));
-    for (int64_t j = 0; j < n; ++j)
-        for (int64_t i = std::max<int64_t>(0, j - nb); i <= j; ++i) Bd[i + j * n] = full[i + j * m];
-    full.clear(); full.shrink_to_fit();
+    // stage 2 on the host, band storage: tb2bd's windows reach 3 kd + 1 off the diagonal
+    const int64_t Mg = 3 * kd + 2;
     std::vector<R> d, e;
     host::Reflectors<T> QU2, QV2;
     std::vector<T> pu, pv;
     {
+        std::vector<T> Bb = gather_band(W, kd, Mg, false, false, opts);
         trace::Block t2("tb2bd");
-        host::tb2bd<T>(n, n, nb, Bd.data(), n, d, e, QU2, QV2, pu, pv);
+        host::tb2bd<T>(n, n, kd, Bb.data() + Mg, 2 * Mg, d, e, QU2, QV2, pu, pv);
     }
-    Bd.clear(); Bd.shrink_to_fit();
     const bool wu = wanted(U), wv = wanted(VT);
-    std::vector<T> U2, VT2;
-    if (wu) { U2.assign(size_t(n) * n, T(0)); for (int64_t i = 0; i < n; ++i) U2[i + i * n] = pu[i]; }
-    if (wv) { VT2.assign(size_t(n) * n, T(0)); for (int64_t i = 0; i < n; ++i) VT2[i + i * n] = slate::conj(pv[i]); }
+    if (!wu && !wv) {
+        trace::Block t2("bdsqr");
+        host::bdsqr_core<R>(n, d.data(), e.data(), nullptr);
+        Sigma = d;
+        return;
+    }
+    // bdsqr: U2 and Vt = VT2^T in the row layout (rotations mix columns)
+    GridPtr gr = col_grid(gA), gc = row_grid(gA);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    Matrix<T> U2(n, n, kd, n, gr), V2(n, n, kd, n, gr);
+    U2.insertLocalTiles(target);
+    V2.insertLocalTiles(target);
+    {
+        std::vector<T> cpv(n);
+        for (int64_t i = 0; i < n; ++i) cpv[i] = slate::conj(pv[i]);
+        set_diag_rows(U2, pu, target);
+        set_diag_rows(V2, cpv, target);
+    }
     {
         trace::Block t2("bdsqr");
-        host::bdsqr<R, T>(n, d.data(), e.data(), wu ? U2.data() : nullptr, n, n, wv ? VT2.data() : nullptr, n, n);
+        LocalBlock<T> lu = U2.local(loc_of(target), true), lv = V2.local(loc_of(target), true);
+        RowRotSink<T> sink(c, n);
+        sink.U = wu ? lu.ptr : nullptr; sink.ldu = lu.ld; sink.urows = lu.m;
+        sink.V = wv ? lv.ptr : nullptr; sink.ldv = lv.ld; sink.vrows = lv.m;
+        host::bdsqr_core<R>(n, d.data(), e.data(), &sink);
+        sink.finish();
     }
     Sigma = d;
     if (wu) {
-        QU2.apply_left(false, n, U2.data(), n);
-        std::vector<T> Uh(size_t(m) * n, T(0));
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = 0; i < n; ++i) Uh[i + j * m] = U2[i + j * n];
-        fill_from_host(U, Uh, m);
-        if (target == Target::Devices) U.insertLocalTiles(Target::Devices);
-        const int64_t mt = W.mt(), unt = U.nt();
+        // U = [QU2 U2; 0], then the stage-1 reflectors
+        Matrix<T> U1(n, n, n, kd, gc);
+        U1.insertLocalTiles(target);
+        slate::copy<T, T>(U2, U1, opts);
+        {
+            LocalBlock<T> l1 = U1.local(loc_of(target), true);
+            if (l1.n > 0) unmtr_hb2st_blocked(QU2, n, kd, l1.ptr, l1.ld, l1.n, c);
+        }
+        Matrix<T> Uw(m, n, kd, kd, gA);
+        Uw.insertLocalTiles(target);
+        set(T(0), T(0), Uw, opts);
+        {
+            Matrix<T> Ut = Uw.slice(0, n - 1, 0, n - 1);
+            slate::copy<T, T>(U1, Ut, opts);
+        }
+        trace::Block t3("unmbr_ge2tb_u");
+        const int64_t mt = W.mt(), unt = Uw.nt();
         for (int64_t k = W.nt() - 1; k >= 0; --k) {
             Matrix<T> cp = W.sub(k, mt - 1, k, k);
-            Matrix<T> Uk = U.sub(k, U.mt() - 1, 0, unt - 1);
+            Matrix<T> Uk = Uw.sub(k, Uw.mt() - 1, 0, unt - 1);
             unmqr(Side::Left, Op::NoTrans, cp, TU[k], Uk, opts);
         }
+        slate::copy<T, T>(Uw, U, opts);
     }
     if (wv) {
-        // VT2 := VT2 QV2^H  computed as (QV2 VT2^H)^H
-        std::vector<T> Vh(size_t(n) * n);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = 0; i < n; ++i) Vh[i + j * n] = slate::conj(VT2[j + i * n]);
-        QV2.apply_left(false, n, Vh.data(), n);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = 0; i < n; ++i) VT2[i + j * n] = slate::conj(Vh[j + i * n]);
-        fill_from_host(VT, VT2, n);
-        if (target == Target::Devices) VT.insertLocalTiles(Target::Devices);
-        const int64_t nt = W.nt(), vmt = VT.mt();
+        // VT2 := VT2 QV2^H  <=>  Vt := conj(QV2) Vt  (Vt = VT2^T), then the stage-1 reflectors
+        host::Reflectors<T> QV2c = QV2;
+        for (auto& x : QV2c.v) x = slate::conj(x);
+        for (auto& x : QV2c.tau) x = slate::conj(x);
+        Matrix<T> V1(n, n, n, kd, gc);
+        V1.insertLocalTiles(target);
+        slate::copy<T, T>(V2, V1, opts);
+        {
+            LocalBlock<T> l1 = V1.local(loc_of(target), true);
+            if (l1.n > 0) unmtr_hb2st_blocked(QV2c, n, kd, l1.ptr, l1.ld, l1.n, c);
+        }
+        Matrix<T> VTw(n, n, kd, kd, gA);
+        VTw.insertLocalTiles(target);
+        slate::copy<T, T>(transpose(V1), VTw, opts);
+        trace::Block t3("unmbr_ge2tb_v");
+        const int64_t nt = W.nt(), vmt = VTw.mt();
         for (int64_t k = nt - 2; k >= 0; --k) {
             Matrix<T> rp = W.sub(k, k, k + 1, nt - 1);
-            Matrix<T> Vk = VT.sub(0, vmt - 1, k + 1, VT.nt() - 1);
+            Matrix<T> Vk = VTw.sub(0, vmt - 1, k + 1, VTw.nt() - 1);
             unmlq(Side::Right, Op::NoTrans, rp, TV[k], Vk, opts);
         }
+        slate::copy<T, T>(VTw, VT, opts);
     }
 }
 

@@ -254,7 +254,7 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
                 v[0] = T(1);
                 a(r, c0) = cj(alpha);
                 for (int64_t t = 1; t < L; ++t) a(r, c0 + t) = T(0);
-                if (tau != T(0)) { right(r, c0, L, tau, v, w); QVs[j].push(c0, L, tau, v); }
+                if (tau != T(0)) { right(r, c0, L, tau, v, w); QVs[j].push(c0, L, tau, v, j); }
             }
             // left reflector: column c0, rows [c0, min(c1, m-1)]
             int64_t r1 = std::min(c1, m - 1);
@@ -267,7 +267,7 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
                 v[0] = T(1);
                 a(c0, c0) = alpha;
                 for (int64_t t = 1; t < Ll; ++t) a(c0 + t, c0) = T(0);
-                if (tau != T(0)) { left(c0, c0, Ll, tau, v); QUs[j].push(c0, Ll, tau, v); }
+                if (tau != T(0)) { left(c0, c0, Ll, tau, v); QUs[j].push(c0, Ll, tau, v, j); }
             }
             prog[j].store(st + 1, std::memory_order_release);
             // next: row c0 beyond its band, columns [c0 + b, c1 + b]
@@ -286,9 +286,9 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
     }
     for (int64_t j = 0; j < nsw; ++j) {
         for (size_t q = 0; q < QVs[j].size(); ++q)
-            QV.push(QVs[j].off[q], QVs[j].len[q], QVs[j].tau[q], QVs[j].v.data() + QVs[j].voff[q]);
+            QV.push(QVs[j].off[q], QVs[j].len[q], QVs[j].tau[q], QVs[j].v.data() + QVs[j].voff[q], j);
         for (size_t q = 0; q < QUs[j].size(); ++q)
-            QU.push(QUs[j].off[q], QUs[j].len[q], QUs[j].tau[q], QUs[j].v.data() + QUs[j].voff[q]);
+            QU.push(QUs[j].off[q], QUs[j].len[q], QUs[j].tau[q], QUs[j].v.data() + QUs[j].voff[q], j);
         QVs[j] = Reflectors<T>();
         QUs[j] = Reflectors<T>();
     }
@@ -593,38 +593,17 @@ int64_t stedc(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
 
 //------------------------------------------------------------------------------
 // Golub-Reinsch implicit-shift QR on the upper bidiagonal (EISPACK svd).
-template <typename R, typename T>
-int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, int64_t ldvt, int64_t vcols) {
+template <typename R>
+int64_t bdsqr_core(int64_t n, R* w, R* e, RotSink<R>* sink) {
     if (n <= 0) return 0;
     std::vector<R> rv1(n, R(0));
     for (int64_t i = 1; i < n; ++i) rv1[i] = e[i - 1];
     R anorm = 0;
     for (int64_t i = 0; i < n; ++i) anorm = std::max(anorm, std::abs(w[i]) + std::abs(rv1[i]));
     int64_t fail = 0;
-    auto colrot = [&](T* M, int64_t ld, int64_t rows, int64_t a, int64_t b, R c, R s) {
-        if (!M) return;
-        T* x = M + a * ld;
-        T* y = M + b * ld;
-        for (int64_t r = 0; r < rows; ++r) {
-            T ya = x[r], yb = y[r];
-            x[r] = ya * c + yb * s;
-            y[r] = yb * c - ya * s;
-        }
-    };
-    // VT is rotated by rows; rows of a column-major VT are ld-strided, so work
-    // on V^T-transposed storage (row j of VT = contiguous column j of Vt) and
-    // transpose back at the end.  The rotations of one implicit-shift sweep are
-    // recorded and applied afterwards by apply_rots (row blocks in parallel).
-    std::vector<T> Vt;
-    if (VT) {
-        Vt.resize(size_t(vcols) * n);
-        for (int64_t jj = 0; jj < vcols; ++jj)
-            for (int64_t j = 0; j < n; ++j) Vt[jj + j * vcols] = VT[j + jj * ldvt];
-    }
-    T* V = VT ? Vt.data() : nullptr;
-    // Rot convention of apply_rots: [x y] <- [c x - s y, s x + c y]; the sweep
+    // Rot convention of the sink: [x y] <- [c x - s y, s x + c y]; the sweep
     // below rotates [x y] <- [c x + s y, c y - s x], i.e. (c, -s).
-    std::vector<Rot<R>> ru, rv;
+    std::vector<PlaneRot<R>> ru, rv;
     for (int64_t k = n - 1; k >= 0; --k) {
         for (int its = 0; its < 75; ++its) {
             bool flag = true;
@@ -646,14 +625,14 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
                     h = R(1) / h;
                     c = g * h;
                     s = -f * h;
-                    colrot(U, ldu, urows, nm, i, c, s);
+                    if (sink) sink->rot_u(nm, i, c, s);
                 }
             }
             R z = w[k];
             if (l == k) {
                 if (z < R(0)) {
                     w[k] = -z;
-                    if (V) for (int64_t jj = 0; jj < vcols; ++jj) V[jj + k * vcols] = -V[jj + k * vcols];
+                    if (sink) sink->negate_v(k);
                 }
                 break;
             }
@@ -680,7 +659,7 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
                 g = g * c - x * s;
                 h = y * s;
                 y *= c;
-                rv.push_back(Rot<R>{j, c, -s});
+                rv.push_back(PlaneRot<R>{j, c, -s});
                 z = std::hypot(f, h);
                 w[j] = z;
                 if (z != R(0)) {
@@ -690,25 +669,88 @@ int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, in
                 }
                 f = c * g + s * y;
                 x = c * y - s * g;
-                ru.push_back(Rot<R>{j, c, -s});
+                ru.push_back(PlaneRot<R>{j, c, -s});
             }
-            apply_rots(rv, V, vcols, vcols);
-            apply_rots(ru, U, ldu, urows);
+            if (sink) sink->sweep(ru, rv);
             rv1[l] = 0;
             rv1[k] = f;
             w[k] = x;
         }
     }
-    // sort descending
+    // sort descending (selection sort: the permutation goes to the sink)
+    std::vector<int64_t> perm(n);
+    for (int64_t i = 0; i < n; ++i) perm[i] = i;
+    bool moved = false;
     for (int64_t i = 0; i + 1 < n; ++i) {
         int64_t kk = i;
         for (int64_t j = i + 1; j < n; ++j) if (w[j] > w[kk]) kk = j;
-        if (kk != i) {
-            std::swap(w[i], w[kk]);
-            if (U) for (int64_t r = 0; r < urows; ++r) std::swap(U[r + i * ldu], U[r + kk * ldu]);
-            if (V) for (int64_t jj = 0; jj < vcols; ++jj) std::swap(V[jj + i * vcols], V[jj + kk * vcols]);
+        if (kk != i) { std::swap(w[i], w[kk]); std::swap(perm[i], perm[kk]); moved = true; }
+    }
+    if (sink && moved) sink->permute(perm);
+    return fail;
+}
+
+namespace {
+
+/// host backend: U and Vt = VT^T in host memory (row blocks of the
+/// rotations in parallel, apply_rots)
+template <typename R, typename T>
+struct HostRotSink : RotSink<R> {
+    T* U; int64_t ldu, urows;
+    T* V; int64_t vcols;
+    std::vector<Rot<R>> tu, tv;
+    void sweep(std::vector<PlaneRot<R>> const& ru, std::vector<PlaneRot<R>> const& rv) override {
+        tv.clear(); tu.clear();
+        for (auto const& r : rv) tv.push_back(Rot<R>{r.i, r.c, r.s});
+        for (auto const& r : ru) tu.push_back(Rot<R>{r.i, r.c, r.s});
+        apply_rots(tv, V, vcols, vcols);
+        apply_rots(tu, U, ldu, urows);
+    }
+    void rot_u(int64_t a, int64_t b, R c, R s) override {
+        if (!U) return;
+        T* x = U + a * ldu;
+        T* y = U + b * ldu;
+        for (int64_t r = 0; r < urows; ++r) {
+            T ya = x[r], yb = y[r];
+            x[r] = ya * c + yb * s;
+            y[r] = yb * c - ya * s;
         }
     }
+    void negate_v(int64_t k) override {
+        if (V) for (int64_t jj = 0; jj < vcols; ++jj) V[jj + k * vcols] = -V[jj + k * vcols];
+    }
+    void permute(std::vector<int64_t> const& perm) override {
+        const int64_t n = int64_t(perm.size());
+        auto perm_cols = [&](T* M, int64_t ld, int64_t rows) {
+            if (!M) return;
+            std::vector<T> tmp(size_t(rows) * n);
+            for (int64_t i = 0; i < n; ++i)
+                for (int64_t r = 0; r < rows; ++r) tmp[r + i * rows] = M[r + perm[i] * ld];
+            for (int64_t i = 0; i < n; ++i)
+                for (int64_t r = 0; r < rows; ++r) M[r + i * ld] = tmp[r + i * rows];
+        };
+        perm_cols(U, ldu, urows);
+        perm_cols(V, vcols, vcols);
+    }
+};
+
+}  // namespace
+
+template <typename R, typename T>
+int64_t bdsqr(int64_t n, R* w, R* e, T* U, int64_t ldu, int64_t urows, T* VT, int64_t ldvt, int64_t vcols) {
+    if (n <= 0) return 0;
+    // VT is rotated by rows; rows of a column-major VT are ld-strided, so work
+    // on Vt = VT^T (row j of VT = contiguous column j of Vt) and transpose back
+    std::vector<T> Vt;
+    if (VT) {
+        Vt.resize(size_t(vcols) * n);
+        for (int64_t jj = 0; jj < vcols; ++jj)
+            for (int64_t j = 0; j < n; ++j) Vt[jj + j * vcols] = VT[j + jj * ldvt];
+    }
+    HostRotSink<R, T> sink;
+    sink.U = U; sink.ldu = ldu; sink.urows = urows;
+    sink.V = VT ? Vt.data() : nullptr; sink.vcols = vcols;
+    int64_t fail = bdsqr_core<R>(n, w, e, (U || VT) ? &sink : nullptr);
     if (VT) {
         for (int64_t jj = 0; jj < vcols; ++jj)
             for (int64_t j = 0; j < n; ++j) VT[j + jj * ldvt] = Vt[jj + j * vcols];
@@ -733,6 +775,8 @@ SLATE_EIGH_INST(double)
 SLATE_EIGH_INST(std::complex<float>)
 SLATE_EIGH_INST(std::complex<double>)
 
+template int64_t bdsqr_core<float>(int64_t, float*, float*, RotSink<float>*);
+template int64_t bdsqr_core<double>(int64_t, double*, double*, RotSink<double>*);
 template int64_t sterf<float>(int64_t, float*, float*);
 template int64_t sterf<double>(int64_t, double*, double*);
 template int64_t stedc<float>(int64_t, float*, float*, float*, int64_t);

@@ -187,6 +187,16 @@ def case_heev(tg, dt, nb):
     assert np.linalg.norm(h @ z - z * lam) <= 100 * tol(dt) * np.linalg.norm(h) * np.sqrt(n), "vectors"
     sv = s.svd_vals(s.from_numpy(a, nb=nb, target=tg), target=tg)
     assert np.abs(np.sort(sv)[::-1] - np.linalg.svd(a, compute_uv=False)).max() <= 100 * tol(dt) * sv.max()
+    for (m2, n2) in ((170, 120), (110, 160)):
+        b2 = rnd(m2, n2, dt, 98)
+        k2 = min(m2, n2)
+        U = s.from_numpy(np.zeros((m2, k2), dt), nb=nb, target=tg)
+        VT = s.from_numpy(np.zeros((k2, n2), dt), nb=nb, target=tg)
+        sv = s.svd(s.from_numpy(b2, nb=nb, target=tg), U, VT, target=tg)
+        u, vt = s.to_numpy(U), s.to_numpy(VT)
+        assert relerr((u * sv) @ vt, b2) < 100 * tol(dt), ("svd", m2, n2)
+        assert np.abs(u.conj().T @ u - np.eye(k2)).max() < 100 * tol(dt) * k2
+        assert np.abs(vt @ vt.conj().T - np.eye(k2)).max() < 100 * tol(dt) * k2
 
 
 def case_potrf(tg, dt, nb):
