@@ -29,41 +29,52 @@ __global__ __launch_bounds__(256) void tinv_from_gram_kernel(int64_t k, T* G, in
 
 // ---- bdsqr rotations on the device.  Every row of M is independent; one
 // thread owns one row and walks the columns once per batch of K QR sweeps
-// with a register window of K + 1 columns: at step tau, sweep s applies its
-// rotation at column pair (tau - s, tau - s + 1), sweeps in ascending order,
-// which is exactly the sequential order (sweep s at j only needs sweep s - 1
-// to be done with column j + 1).  Each column is read and written once per
-// batch instead of once per sweep.  C, S: K x n, identity outside a sweep's
-// range; rotations [x y] <- [c x - s y, s x + c y] on columns [p0, p1).
+// with a register window of 2K columns: at step tau, sweep s applies its
+// rotation at column pair (j, j + 1), j = tau - 2 s.  Sweep s at j only needs
+// sweep s - 1 to be done with column j + 1, which happened at step tau - 1,
+// so the K rotations of one step touch disjoint pairs and are independent
+// (ILP instead of a K-long dependency chain).  Each column is read and
+// written once per batch instead of once per sweep.  D holds the rotations in
+// step order: D[2 (tau - p0) K + 2 s + {0, 1}] = (c, s) of sweep s at step
+// tau (identity where sweep s has no rotation), so a step reads 2K
+// consecutive reals (prefetched one step ahead).  [x y] <- [c x - s y,
+// s x + c y] on columns [p0, p1).
 template <typename T, typename R, int K>
-__global__ __launch_bounds__(64) void rot_sweeps_kernel(int64_t rows, T* M, int64_t ld, int64_t n, int64_t p0,
-                                                        int64_t p1, const R* C, const R* S) {
+__global__ __launch_bounds__(64) void rot_sweeps_kernel(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1,
+                                                        const R* D) {
     const int64_t r = blockIdx.x * 64 + threadIdx.x;
     if (r >= rows) return;
     T* row = M + r;
-    T w[K + 1];
+    T w[2 * K];
     #pragma unroll
-    for (int i = 0; i < K + 1; ++i) w[i] = T();
-    w[K - 1] = row[p0 * ld];
-    w[K] = (p0 + 1 < p1) ? row[(p0 + 1) * ld] : T();
-    const int64_t tend = p1 - 2 + K - 1;
+    for (int i = 0; i < 2 * K; ++i) w[i] = T();
+    w[2 * K - 2] = row[p0 * ld];
+    w[2 * K - 1] = (p0 + 1 < p1) ? row[(p0 + 1) * ld] : T();
+    const int64_t tend = p1 - 2 + 2 * (K - 1);
+    R cs[2 * K], nx[2 * K];
+    #pragma unroll
+    for (int i = 0; i < 2 * K; ++i) cs[i] = D[i];
     for (int64_t tau = p0; tau <= tend; ++tau) {
+        const R* Dn = D + 2 * K * (tau + 1 - p0);
+        if (tau < tend) {
+            #pragma unroll
+            for (int i = 0; i < 2 * K; ++i) nx[i] = Dn[i];
+        }
         #pragma unroll
         for (int s = 0; s < K; ++s) {
-            const int64_t j = tau - s;
-            if (j >= p0 && j <= p1 - 2) {
-                const R c = C[s * n + j], sn = S[s * n + j];
-                const T x = w[K - 1 - s], y = w[K - s];
-                w[K - 1 - s] = x * c - y * sn;
-                w[K - s] = x * sn + y * c;
-            }
+            const R c = cs[2 * s], sn = cs[2 * s + 1];
+            const T x = w[2 * K - 2 - 2 * s], y = w[2 * K - 1 - 2 * s];
+            w[2 * K - 2 - 2 * s] = x * c - y * sn;
+            w[2 * K - 1 - 2 * s] = x * sn + y * c;
         }
-        const int64_t cr = tau - K + 1;
+        const int64_t cr = tau - 2 * K + 2;
         if (cr >= p0) row[cr * ld] = w[0];
         #pragma unroll
-        for (int i = 0; i < K; ++i) w[i] = w[i + 1];
+        for (int i = 0; i < 2 * K - 1; ++i) w[i] = w[i + 1];
         const int64_t cn = tau + 2;
-        w[K] = (cn < p1) ? row[cn * ld] : T();
+        w[2 * K - 1] = (cn < p1) ? row[cn * ld] : T();
+        #pragma unroll
+        for (int i = 0; i < 2 * K; ++i) cs[i] = nx[i];
     }
     if (p1 - 1 >= p0) row[(p1 - 1) * ld] = w[0];
 }
@@ -82,11 +93,10 @@ __global__ __launch_bounds__(256) void rot_cols_kernel(int64_t rows, T* M, int64
 }  // namespace
 
 template <typename T>
-void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t n, int64_t p0, int64_t p1, const rt<T>* C, const rt<T>* S,
-                hipStream_t s) {
+void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, const rt<T>* D, hipStream_t s) {
     if (rows <= 0 || p1 - p0 < 2) return;
     hipLaunchKernelGGL((rot_sweeps_kernel<T, rt<T>, kRotBatch>), dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s,
-                       rows, M, ld, n, p0, p1, C, S);
+                       rows, M, ld, p0, p1, D);
 }
 
 template <typename T>
@@ -105,8 +115,7 @@ void tinv_from_gram(int64_t k, T* G, int64_t ldg, const T* tau, hipStream_t s) {
 
 #define SLATE_INST_EIG(T)                                                                                          \
     template void tinv_from_gram<T>(int64_t, T*, int64_t, const T*, hipStream_t);                                 \
-    template void rot_sweeps<T>(int64_t, T*, int64_t, int64_t, int64_t, int64_t, const rt<T>*, const rt<T>*,        \
-                                hipStream_t);                                                                      \
+    template void rot_sweeps<T>(int64_t, T*, int64_t, int64_t, int64_t, const rt<T>*, hipStream_t);             \
     template void rot_cols<T>(int64_t, T*, int64_t, int64_t, int64_t, rt<T>, rt<T>, hipStream_t);
 
 SLATE_INST_EIG(float)

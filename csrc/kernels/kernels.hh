@@ -85,11 +85,12 @@ void tinv_from_gram(int64_t k, T* G, int64_t ldg, const T* tau, hipStream_t s);
 /// sweeps per rot_sweeps call
 constexpr int kRotBatch = 16;
 /// Apply kRotBatch QR sweeps of plane rotations to the columns [p0, p1) of
-/// every row of M (rows x n): sweep s rotates columns (j, j+1) with
-/// (C[s n + j], S[s n + j]), [x y] <- [c x - s y, s x + c y], j ascending.
+/// every row of M: sweep s rotates columns (j, j+1), j ascending, [x y] <-
+/// [c x - s y, s x + c y], with (c, s) at D[2 (j + 2 s - p0) kRotBatch + 2 s]
+/// (step-ordered table, identity where a sweep has no rotation; steps
+/// p0 .. p1 - 2 + 2 (kRotBatch - 1)).
 template <typename T>
-void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t n, int64_t p0, int64_t p1, const rt<T>* C, const rt<T>* S,
-                hipStream_t s);
+void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, const rt<T>* D, hipStream_t s);
 /// One rotation on columns (a, b): [x y] <- [x c + y s, y c - x s].
 template <typename T>
 void rot_cols(int64_t rows, T* M, int64_t ld, int64_t a, int64_t b, rt<T> c, rt<T> sn, hipStream_t s);

@@ -218,6 +218,20 @@ void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     Uplo mask = Uplo::General;
     if (is_trapezoid_kind(B.matrix_kind())) mask = B.uplo();
+    if (A.grid()->size() == 1 && B.grid()->size() == 1 &&
+        (B.op() == Op::NoTrans || (A.op() == Op::NoTrans && mask == Uplo::General))) {
+        // one process holds both: one (transposing) device copy of the local
+        // blocks instead of the tile-by-tile redistribution
+        LocalBlock<Ts> la = A.local(loc, false);
+        LocalBlock<Td> lbk = B.local(loc, true);
+        if (B.op() == Op::NoTrans)
+            lb::copy(c, mask, A.op(), B.m(), B.n(), la.ptr, la.ld, lbk.ptr, lbk.ld);
+        else   // B_storage = op_B(A) for a transposed destination view
+            lb::copy(c, Uplo::General, B.op(), B.n(), B.m(), la.ptr, la.ld, lbk.ptr, lbk.ld);
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+        internal::finish_origin(B, opts);
+        return;
+    }
     if (A.op() == Op::NoTrans && B.op() == Op::NoTrans && same_layout(A, B) && A.aligned() && B.aligned()) {
         LocalBlock<Ts> la = A.local(loc, false);
         LocalBlock<Td> lbk = B.local(loc, true);

@@ -274,29 +274,31 @@ inline GridPtr col_grid(GridPtr const& g) {
 
 /// bdsqr transformations on the local rows of U and Vt (row layout: rows are
 /// independent under column rotations, so no communication).  Device: QR
-/// sweeps are batched kRotBatch at a time into pinned (C, S) buffers and
-/// applied by the register-window wavefront kernel (double-buffered, the host
-/// keeps iterating on (d, e) meanwhile); host: loops.
+/// sweeps are batched kRotBatch at a time into step-ordered (c, s) tables
+/// (pinned, double-buffered) and applied by the register-window wavefront
+/// kernel while the host keeps iterating on (d, e); host: loops.
 template <typename T>
 struct RowRotSink : host::RotSink<real_type<T>> {
     using R = real_type<T>;
+    using Rots = std::vector<host::PlaneRot<R>>;
     static constexpr int K = slate_amd::dev::kRotBatch;
     lb::Ctx c;
     int64_t n = 0;
     T* U = nullptr; int64_t ldu = 0, urows = 0;
     T* V = nullptr; int64_t ldv = 0, vrows = 0;
-    // batch staging: [Cu | Su | Cv | Sv], K x n each
+    size_t tsz = 0;                                // reals per table (one matrix)
     R* hb[2] = {nullptr, nullptr};
     Work<R> db[2];
     hipEvent_t ev[2] = {nullptr, nullptr};
-    int cur = 0, ns = 0;
-    int64_t ulo = 0, uhi = 0, vlo = 0, vhi = 0;   // union of the batch's rotation ranges
+    int cur = 0;
+    std::vector<Rots> bu, bv;                      // the batch's sweeps
 
     RowRotSink(lb::Ctx const& c_, int64_t n_) : c(c_), n(n_) {
         if (c.dev()) {
+            tsz = size_t(2 * K) * size_t(n + 2 * K);
             for (int b = 0; b < 2; ++b) {
-                hb[b] = static_cast<R*>(device::malloc_host(sizeof(R) * 4 * K * size_t(n)));
-                db[b].resize(Target::Devices, size_t(4) * K * n);
+                hb[b] = static_cast<R*>(device::malloc_host(sizeof(R) * 2 * tsz));
+                db[b].resize(Target::Devices, 2 * tsz);
                 ev[b] = device::event_get();
                 slate_hip_call(hipEventRecord(ev[b], c.stream));
             }
@@ -308,75 +310,85 @@ struct RowRotSink : host::RotSink<real_type<T>> {
             for (int b = 0; b < 2; ++b) { device::free_host(hb[b]); device::event_put(ev[b]); }
         }
     }
-    R* Cs(int which) { return hb[cur] + size_t(which) * K * n; }
-    void rot_host(T* M, int64_t ld, int64_t rows, std::vector<host::PlaneRot<R>> const& rs) {
-        if (!M) return;
-        for (auto const& g : rs) {
-            T* x = M + g.i * ld;
-            T* y = M + (g.i + 1) * ld;
-            for (int64_t r = 0; r < rows; ++r) {
-                T a = x[r], b = y[r];
-                x[r] = g.c * a - g.s * b;
-                y[r] = g.s * a + g.c * b;
+    /// host twin of the rot_sweeps kernel (same table, same step order), so
+    /// the CPU tests check the batching
+    static void sweeps_host(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, R const* D) {
+        if (p1 - p0 < 2) return;
+        const int64_t tend = p1 - 2 + 2 * (K - 1);
+        #pragma omp parallel for schedule(static) if (rows > 64)
+        for (int64_t r = 0; r < rows; ++r) {
+            T w[2 * K];
+            for (int i = 0; i < 2 * K; ++i) w[i] = T(0);
+            w[2 * K - 2] = M[r + p0 * ld];
+            w[2 * K - 1] = (p0 + 1 < p1) ? M[r + (p0 + 1) * ld] : T(0);
+            for (int64_t tau = p0; tau <= tend; ++tau) {
+                R const* cs = D + 2 * K * (tau - p0);
+                for (int q = 0; q < K; ++q) {
+                    const R cc = cs[2 * q], sn = cs[2 * q + 1];
+                    const T x = w[2 * K - 2 - 2 * q], y = w[2 * K - 1 - 2 * q];
+                    w[2 * K - 2 - 2 * q] = x * cc - y * sn;
+                    w[2 * K - 1 - 2 * q] = x * sn + y * cc;
+                }
+                const int64_t cr = tau - 2 * K + 2;
+                if (cr >= p0) M[r + cr * ld] = w[0];
+                for (int i = 0; i < 2 * K - 1; ++i) w[i] = w[i + 1];
+                w[2 * K - 1] = (tau + 2 < p1) ? M[r + (tau + 2) * ld] : T(0);
             }
+            M[r + (p1 - 1) * ld] = w[0];
         }
+    }
+    static std::pair<int64_t, int64_t> build(std::vector<Rots> const& b, R* D) {
+        int64_t p0 = INT64_MAX, p1 = -1;
+        for (auto const& rs : b)
+            if (!rs.empty()) { p0 = std::min(p0, rs.front().i); p1 = std::max(p1, rs.back().i + 2); }
+        if (p1 < 0) return {0, 0};
+        const int64_t steps = p1 - p0 + 2 * K - 3;
+        for (int64_t t = 0; t < steps; ++t)
+            for (int q = 0; q < K; ++q) { D[2 * (t * K + q)] = R(1); D[2 * (t * K + q) + 1] = R(0); }
+        for (size_t q = 0; q < b.size(); ++q)
+            for (auto const& g : b[q]) {
+                const int64_t t = g.i + 2 * int64_t(q) - p0;
+                D[2 * (t * K + q)] = g.c;
+                D[2 * (t * K + q) + 1] = g.s;
+            }
+        return {p0, p1};
     }
     void flush() {
-        if (!c.dev() || ns == 0) return;
+        if (bu.empty()) return;
+        if (!c.dev()) {
+            std::vector<R> D(size_t(2 * K) * size_t(n + 2 * K));
+            auto ru = build(bu, D.data());
+            if (U) sweeps_host(urows, U, ldu, ru.first, ru.second, D.data());
+            auto rv = build(bv, D.data());
+            if (V) sweeps_host(vrows, V, ldv, rv.first, rv.second, D.data());
+            bu.clear();
+            bv.clear();
+            return;
+        }
         namespace kd_ = slate_amd::dev;
-        // identity rows for unused sweeps of this batch
-        for (int q = ns; q < K; ++q)
-            for (int w = 0; w < 4; w += 2) {
-                R* C = hb[cur] + size_t(w) * K * n + size_t(q) * n;
-                R* S = hb[cur] + size_t(w + 1) * K * n + size_t(q) * n;
-                const int64_t lo = w == 0 ? ulo : vlo, hi = w == 0 ? uhi : vhi;
-                for (int64_t j = lo; j < hi; ++j) { C[j] = R(1); S[j] = R(0); }
-            }
-        device::memcpy_async(db[cur].data(), hb[cur], sizeof(R) * 4 * K * size_t(n), c.stream);
-        R const* d0 = db[cur].data();
-        if (U && uhi > ulo)
-            kd_::rot_sweeps(urows, kd_::dptr(U), ldu, n, ulo, uhi + 1, d0, d0 + size_t(K) * n, c.stream);
-        if (V && vhi > vlo)
-            kd_::rot_sweeps(vrows, kd_::dptr(V), ldv, n, vlo, vhi + 1, d0 + size_t(2) * K * n, d0 + size_t(3) * K * n,
-                            c.stream);
+        R* Du = hb[cur];
+        R* Dv = hb[cur] + tsz;
+        auto ru = build(bu, Du), rv = build(bv, Dv);
+        const size_t su = size_t(std::max<int64_t>(ru.second - ru.first + 2 * K - 3, 0)) * 2 * K;
+        const size_t sv = size_t(std::max<int64_t>(rv.second - rv.first + 2 * K - 3, 0)) * 2 * K;
+        if (su) device::memcpy_async(db[cur].data(), Du, su * sizeof(R), c.stream);
+        if (sv) device::memcpy_async(db[cur].data() + tsz, Dv, sv * sizeof(R), c.stream);
+        if (U && su) kd_::rot_sweeps(urows, kd_::dptr(U), ldu, ru.first, ru.second, db[cur].data(), c.stream);
+        if (V && sv) kd_::rot_sweeps(vrows, kd_::dptr(V), ldv, rv.first, rv.second, db[cur].data() + tsz, c.stream);
         slate_hip_call(hipEventRecord(ev[cur], c.stream));
         cur ^= 1;
-        ns = 0;
+        bu.clear();
+        bv.clear();
         slate_hip_call(hipEventSynchronize(ev[cur]));   // the other staging buffer is free again
     }
-    void fill(int which, std::vector<host::PlaneRot<R>> const& rs, int64_t& lo, int64_t& hi) {
-        R* C = Cs(which) + size_t(ns) * n;
-        R* S = Cs(which + 1) + size_t(ns) * n;
-        // identity over the batch's union range, then this sweep's rotations
-        for (int64_t j = lo; j < hi; ++j) { C[j] = R(1); S[j] = R(0); }
-        if (rs.empty()) return;
-        const int64_t a = rs.front().i, b = rs.back().i + 1;
-        if (ns == 0) { lo = a; hi = b; }
-        else {
-            // widen the union: earlier sweeps of the batch need identity on the new part
-            for (int q = 0; q < ns; ++q) {
-                R* Cq = Cs(which) + size_t(q) * n;
-                R* Sq = Cs(which + 1) + size_t(q) * n;
-                for (int64_t j = a; j < lo; ++j) { Cq[j] = R(1); Sq[j] = R(0); }
-                for (int64_t j = hi; j < b; ++j) { Cq[j] = R(1); Sq[j] = R(0); }
-            }
-            for (int64_t j = std::min(a, lo); j < lo; ++j) { C[j] = R(1); S[j] = R(0); }
-            for (int64_t j = hi; j < std::max(b, hi); ++j) { C[j] = R(1); S[j] = R(0); }
-            lo = std::min(lo, a);
-            hi = std::max(hi, b);
-        }
-        for (auto const& g : rs) { C[g.i] = g.c; S[g.i] = g.s; }
-    }
-    void sweep(std::vector<host::PlaneRot<R>> const& ru, std::vector<host::PlaneRot<R>> const& rv) override {
-        if (!c.dev()) { rot_host(U, ldu, urows, ru); rot_host(V, ldv, vrows, rv); return; }
-        if (ns == K) flush();
-        if (ns == 0) { ulo = uhi = vlo = vhi = 0; }
-        fill(0, ru, ulo, uhi);
-        fill(2, rv, vlo, vhi);
-        ++ns;
+    void sweep(Rots const& ru, Rots const& rv) override {
+        bu.push_back(ru);
+        bv.push_back(rv);
+        if (int(bu.size()) == K) flush();
     }
     void rot_u(int64_t a, int64_t b, R cc, R sn) override {
         if (!U) return;
+        flush();
         if (!c.dev()) {
             T* x = U + a * ldu;
             T* y = U + b * ldu;
