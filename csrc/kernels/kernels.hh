@@ -95,6 +95,11 @@ void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, const rt
 template <typename T>
 void rot_cols(int64_t rows, T* M, int64_t ld, int64_t a, int64_t b, rt<T> c, rt<T> sn, hipStream_t s);
 
+/// Band LU: undo the panel's interchanges to the left of each pivot (columns
+/// c < jj of the w-column panel, jj = w-1 .. c+1), LAPACK gbtrs convention.
+template <typename T>
+void undo_left_swaps(int64_t w, T* A, int64_t lda, const int64_t* ipiv, hipStream_t s);
+
 // ---- butterfly transforms (rbt.hip)
 /// by_rows: buf(t, j) = A(idx[t], j) for t < cnt, j < len (scatter: the reverse);
 /// by columns: buf(i, t) = A(i, idx[t]) for i < len.

@@ -258,6 +258,31 @@ void slots_unpack(int s0, int s1, int64_t ncols, const int64_t* slot_dst, const 
     hipLaunchKernelGGL(slots_unpack_kernel<T>, g, dim3(64), 0, s, s0, s1, ncols, slot_dst, buf, ldb, A, lda, d);
 }
 
+// ---- band LU (gbtrf): the blocked panel applies its row interchanges over
+// the whole panel width (getrf convention); LAPACK's band solve (gbtrs) wants
+// each column's multipliers as computed, i.e. without the later swaps.  Undo
+// them column by column (one thread per column, later pivots first), as
+// LAPACK dgbtrf does after each panel.
+template <typename T>
+__global__ __launch_bounds__(64) void undo_left_swaps_kernel(int64_t w, T* A, int64_t lda, const int64_t* ipiv) {
+    const int64_t c = blockIdx.x * 64 + threadIdx.x;
+    if (c >= w) return;
+    for (int64_t jj = w - 1; jj > c; --jj) {
+        const int64_t p = ipiv[jj];
+        if (p != jj) {
+            const T t = A[jj + c * lda];
+            A[jj + c * lda] = A[p + c * lda];
+            A[p + c * lda] = t;
+        }
+    }
+}
+
+template <typename T>
+void undo_left_swaps(int64_t w, T* A, int64_t lda, const int64_t* ipiv, hipStream_t s) {
+    if (w <= 1) return;
+    hipLaunchKernelGGL(undo_left_swaps_kernel<T>, dim3((unsigned)((w + 63) / 64)), dim3(64), 0, s, w, A, lda, ipiv);
+}
+
 template <typename T>
 constexpr int pp_hdr() { return int((16 + sizeof(T) - 1) / sizeof(T)); }
 
@@ -290,6 +315,7 @@ void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int6
     template void slots_unpack<T>(int, int, int64_t, const int64_t*, const T*, int64_t, T*, int64_t, RowDist,     \
                                   hipStream_t);                                                                    \
     template int64_t pplu_entry<T>(int64_t);                                                                       \
+    template void undo_left_swaps<T>(int64_t, T*, int64_t, const int64_t*, hipStream_t);                           \
     template void pplu_cand<T>(int64_t, int64_t, int64_t, const T*, int64_t, int64_t, RowDist, int64_t, bool, T*,  \
                                hipStream_t);                                                                       \
     template void pplu_apply<T>(int, const T*, int64_t, int64_t, int64_t, int64_t, int64_t, T*, int64_t, RowDist, \

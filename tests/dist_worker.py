@@ -199,6 +199,37 @@ def case_heev(tg, dt, nb):
         assert np.abs(vt @ vt.conj().T - np.eye(k2)).max() < 100 * tol(dt) * k2
 
 
+def band_of(a, kl, ku):
+    i, j = np.indices(a.shape)
+    return np.where((i - j <= kl) & (j - i <= ku), a, 0).astype(a.dtype)
+
+
+def case_band(tg, dt, nb):
+    """Distributed blocked gbtrf / pbtrf (block-column slabs, one broadcast per
+    panel) through gbsv / pbsv; bandwidths below and above the tile size."""
+    n = 170
+    for kl, ku in ((3, 2), (20, 35), (60, 10)):
+        a = band_of(rnd(n, n, dt, 101 + kl), kl, ku)
+        b = rnd(n, 2, dt, 102)
+        A = s.BandMatrix(kl, ku, s.from_numpy(a, nb=nb, target=tg))
+        B = s.from_numpy(b, nb=nb, target=tg)
+        info, piv = s.gbsv(A, B, target=tg)
+        assert info == 0
+        x = s.to_numpy(B)
+        assert np.linalg.norm(a @ x - b) / (np.linalg.norm(a) * np.linalg.norm(x)) < 100 * tol(dt), (kl, ku)
+    for kd in (4, 50):
+        for uplo in (s.Uplo.Lower, s.Uplo.Upper):
+            c0 = band_of(rnd(n, n, dt, 103 + kd), kd, kd)
+            h = (c0 + c0.conj().T + 4 * kd * np.eye(n)).astype(dt)
+            st = np.tril(h) if uplo == s.Uplo.Lower else np.triu(h)
+            b = rnd(n, 3, dt, 104)
+            A = s.HermitianBandMatrix(uplo, kd, s.from_numpy(st, nb=nb, target=tg))
+            B = s.from_numpy(b, nb=nb, target=tg)
+            assert s.pbsv(A, B, target=tg) == 0
+            x = s.to_numpy(B)
+            assert relerr(h @ x, b) < 100 * tol(dt), (kd, uplo)
+
+
 def case_potrf(tg, dt, nb):
     n = 200
     a = rnd(n, n, dt, 7)
