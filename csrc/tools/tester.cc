@@ -46,6 +46,13 @@ struct Params {
     double tol = 50;
     int repeat = 1;
     bool trace = false;
+    std::string matrix;          // --matrix: matgen kind of the main operand (default per routine)
+    int64_t method_lu = -1, method_trsm = -1, method_gemm = -1, method_hemm = -1;
+    char origin = 'x';           // --origin h|d: where the operands are generated (x: the target)
+    int timer_level = 1;         // --timer-level 2: per-driver trace timers after each case
+    int64_t itermax = -1;
+    int fallback = -1;
+    double pivot_threshold = -1;
 };
 
 std::vector<int64_t> parse_list(std::string const& s) {
@@ -97,12 +104,40 @@ struct Case {
     Case(Params const& p, std::array<int64_t, 3> d, int64_t nb_)
         : P(p), m(d[0]), n(d[1]), k(d[2]), nb(nb_) {
         opts = {{Option::Target, P.target}, {Option::Lookahead, P.lookahead}};
+        if (P.method_lu >= 0) opts[Option::MethodLU] = P.method_lu;
+        if (P.method_trsm >= 0) opts[Option::MethodTrsm] = P.method_trsm;
+        if (P.method_gemm >= 0) opts[Option::MethodGemm] = P.method_gemm;
+        if (P.method_hemm >= 0) opts[Option::MethodHemm] = P.method_hemm;
+        if (P.itermax >= 0) opts[Option::MaxIterations] = P.itermax;
+        if (P.fallback >= 0) opts[Option::UseFallbackSolver] = int64_t(P.fallback);
+        if (P.pivot_threshold > 0) opts[Option::PivotThreshold] = P.pivot_threshold;
     }
-    Matrix<T> mat(int64_t rows, int64_t cols, const char* kind = "rands", double shift = -1) {
+    /// where operands are generated: --origin h puts them on the host (the
+    /// drivers then move them to the target and back, reference --origin)
+    Target gen_target() const {
+        return P.origin == 'h' ? Target::HostTask : (P.origin == 'd' ? Target::Devices : P.target);
+    }
+    Matrix<T> mat(int64_t rows, int64_t cols, const char* kind = "rands", double shift = -1, bool main = false) {
         Matrix<T> A(rows, cols, nb, default_grid());
-        A.insertLocalTiles(P.target);
+        const Target gt = gen_target();
+        A.insertLocalTiles(gt);
         BaseMatrix<T>& b = A;
-        generate_matrix(std::string(kind), b, seed++, shift, opts);
+        Options go = opts;
+        go[Option::Target] = gt;
+        if (main && !P.matrix.empty()) {
+            // --matrix: any matgen kind (element kinds, or spectral ones such as svd / poev / geev)
+            try {
+                generate_matrix(P.matrix, b, seed, shift, go);
+            } catch (std::exception const&) {
+                MatgenParams mp;
+                mp.kind = P.matrix;
+                mp.seed = int64_t(seed);
+                generate_matrix(mp, A, go);
+            }
+            ++seed;
+            return A;
+        }
+        generate_matrix(std::string(kind), b, seed++, shift, go);
         return A;
     }
     Matrix<T> zeros(int64_t rows, int64_t cols) {
@@ -246,7 +281,7 @@ Result r_trmm(Case<T>& c) {
 template <typename T>
 Result solve_case(Case<T>& c, const char* kind, std::function<int64_t(Matrix<T>&, Matrix<T>&)> run,
                   double flops) {
-    auto A = c.mat(c.n, c.n, kind), B = c.mat(c.n, c.P.nrhs);
+    auto A = c.mat(c.n, c.n, kind, -1, true), B = c.mat(c.n, c.P.nrhs);
     auto A0 = c.copy_of(A), B0 = c.copy_of(B);
     Result r;
     int64_t info = 0;
@@ -263,11 +298,11 @@ template <typename T> double potrf_fl(double n) { return cfac<T>() * (n * n * n 
 /// factorization timed alone; the solve for the check runs afterwards
 template <typename T>
 Result r_getrf_m(Case<T>& c, int64_t method) {
-    auto A = c.mat(c.n, c.n), B = c.mat(c.n, c.P.nrhs);
+    auto A = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
     auto A0 = c.copy_of(A), B0 = c.copy_of(B);
     Pivots piv;
     Options o = c.opts;
-    o[Option::MethodLU] = method;
+    if (c.P.method_lu < 0) o[Option::MethodLU] = method;
     Result r;
     int64_t info = 0;
     r.time = c.timed([&] { info = getrf(A, piv, o); });
@@ -547,6 +582,531 @@ Result r_genorm(Case<T>& c) {
     return r;
 }
 
+
+//------------------------------------------------------------------------------
+// Breadth: the rest of the reference tester's routine list (test/test.cc:83-295)
+template <typename T>
+Result blas3_check(Case<T>& c, Matrix<T>& Cn, std::function<void(Matrix<T> const& X, Matrix<T>& Y)> expect,
+                   double scale) {
+    // C_new X == expect(X) for a random X
+    auto X = c.mat(Cn.n(), 4), CX = c.zeros(Cn.m(), 4), Y = c.zeros(Cn.m(), 4);
+    gemm(T(1), Cn, X, T(0), CX, c.opts);
+    expect(X, Y);
+    add(T(-1), CX, T(1), Y, c.opts);
+    return Result{NAN, c.nrm(Y) / (scale * c.nrm(X)), 0, false, ""};
+}
+
+template <typename T>
+Matrix<T> full_of(Case<T>& c, BaseTrapezoidMatrix<T> const& S, bool herm) {
+    // dense copy of a Hermitian / symmetric matrix stored in one triangle
+    auto F = c.zeros(S.n(), S.n());
+    Matrix<T> G(S);
+    G.set_uplo(Uplo::General);
+    copy<T, T>(herm ? conj_transpose(G) : transpose(G), F, c.opts);
+    BaseTrapezoidMatrix<T> Fs(S.uplo(), F, MatrixKind::Trapezoid), Gs(S.uplo(), G, MatrixKind::Trapezoid);
+    copy<T, T>(Gs, Fs, c.opts);
+    return F;
+}
+
+template <typename T>
+Result r_rankk(Case<T>& c, int kind) {   // 0 syrk, 1 her2k, 2 syr2k
+    auto A = c.mat(c.n, c.k), B = c.mat(c.n, c.k), Cg = c.mat(c.n, c.n, "spd", 0.0);
+    auto C0 = c.copy_of(Cg);
+    const bool herm = kind == 1;
+    T alpha(1.5), beta(0.5);
+    Result r;
+    if (kind == 0) { SymmetricMatrix<T> C(Uplo::Lower, Cg); r.time = c.timed([&] { syrk(alpha, A, beta, C, c.opts); }); }
+    else if (kind == 1) { HermitianMatrix<T> C(Uplo::Lower, Cg); r.time = c.timed([&] { her2k(alpha, A, B, R_<T>(0.5), C, c.opts); }); }
+    else { SymmetricMatrix<T> C(Uplo::Lower, Cg); r.time = c.timed([&] { syr2k(alpha, A, B, beta, C, c.opts); }); }
+    r.flops = cfac<T>() * double(c.k) * c.n * (c.n + 1) * (kind == 0 ? 1 : 2);
+    if (c.P.check) {
+        BaseTrapezoidMatrix<T> Cs(Uplo::Lower, Cg, MatrixKind::Trapezoid), C0s(Uplo::Lower, C0, MatrixKind::Trapezoid);
+        auto Cn = full_of(c, Cs, herm), Cz = full_of(c, C0s, herm);
+        auto res = blas3_check<T>(c, Cn, [&](Matrix<T> const& X, Matrix<T>& Y) {
+            auto AX = c.zeros(c.k, 4), BX = c.zeros(c.k, 4);
+            auto opA = herm ? conj_transpose(A) : transpose(A);
+            auto opB = herm ? conj_transpose(B) : transpose(B);
+            gemm(beta, Cz, X, T(0), Y, c.opts);
+            if (kind == 0) { gemm(T(1), opA, X, T(0), AX, c.opts); gemm(alpha, A, AX, T(1), Y, c.opts); }
+            else {
+                gemm(T(1), opB, X, T(0), BX, c.opts); gemm(alpha, A, BX, T(1), Y, c.opts);
+                gemm(T(1), opA, X, T(0), AX, c.opts); gemm(herm ? slate::conj(alpha) : alpha, B, AX, T(1), Y, c.opts);
+            }
+        }, c.nrm(A) * c.nrm(B) * 3 + c.nrm(C0));
+        r.error = res.error;
+    }
+    return r;
+}
+
+template <typename T>
+Result r_symm(Case<T>& c) {
+    auto Ag = c.mat(c.m, c.m), B = c.mat(c.m, c.n), C = c.mat(c.m, c.n);
+    auto C0 = c.copy_of(C);
+    SymmetricMatrix<T> A(Uplo::Lower, Ag);
+    T alpha(1), beta(0.5);
+    Result r;
+    r.time = c.timed([&] { symm(Side::Left, alpha, A, B, beta, C, c.opts); });
+    r.flops = gemm_fl<T>(c.m, c.n, c.m);
+    if (c.P.check) {
+        BaseTrapezoidMatrix<T> As(Uplo::Lower, Ag, MatrixKind::Trapezoid);
+        auto F = full_of(c, As, false);
+        auto res = blas3_check<T>(c, C, [&](Matrix<T> const& X, Matrix<T>& Y) {
+            auto BX = c.zeros(c.m, 4);
+            gemm(T(1), B, X, T(0), BX, c.opts);
+            gemm(beta, C0, X, T(0), Y, c.opts);
+            gemm(alpha, F, BX, T(1), Y, c.opts);
+        }, c.nrm(F) * c.nrm(B) + c.nrm(C0));
+        r.error = res.error;
+    }
+    return r;
+}
+
+template <typename T>
+Result r_gemm_m(Case<T>& c, int64_t method) {
+    Options o = c.opts;
+    o[Option::MethodGemm] = method;
+    auto A = c.mat(c.m, c.k), B = c.mat(c.k, c.n), C = c.mat(c.m, c.n);
+    auto C0 = c.copy_of(C);
+    Result r;
+    r.time = c.timed([&] { gemm(T(1), A, B, T(-1), C, o); });
+    r.flops = gemm_fl<T>(c.m, c.n, c.k);
+    if (c.P.check) {
+        auto res = blas3_check<T>(c, C, [&](Matrix<T> const& X, Matrix<T>& Y) {
+            auto BX = c.zeros(c.k, 4);
+            gemm(T(1), B, X, T(0), BX, c.opts);
+            gemm(T(-1), C0, X, T(0), Y, c.opts);
+            gemm(T(1), A, BX, T(1), Y, c.opts);
+        }, c.nrm(A) * c.nrm(B) + c.nrm(C0));
+        r.error = res.error;
+    }
+    return r;
+}
+
+template <typename T>
+Result r_getrs(Case<T>& c) {
+    auto A = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(B);
+    Pivots piv;
+    int64_t info = getrf(A, piv, c.opts);
+    Result r;
+    if (info) { r.error = INFINITY; return r; }
+    r.time = c.timed([&] { getrs(A, piv, B, c.opts); });
+    r.flops = cfac<T>() * 2.0 * c.n * c.n * c.P.nrhs;
+    if (c.P.check) r.error = c.solve_resid(A0, B, B0);
+    return r;
+}
+
+template <typename T>
+Result r_potrs(Case<T>& c, int variant) {   // 0 potrs, 1 potri
+    auto Ag = c.mat(c.n, c.n, "spd"), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(Ag), B0 = c.copy_of(B);
+    HermitianMatrix<T> A(Uplo::Lower, Ag);
+    Result r;
+    if (potrf(A, c.opts)) { r.error = INFINITY; return r; }
+    if (variant == 0) {
+        r.time = c.timed([&] { potrs(A, B, c.opts); });
+        r.flops = cfac<T>() * 2.0 * c.n * c.n * c.P.nrhs;
+        if (c.P.check) r.error = c.solve_resid(A0, B, B0);
+    } else {
+        int64_t info = 0;
+        r.time = c.timed([&] { info = potri(A, c.opts); });
+        r.flops = cfac<T>() * 2.0 / 3 * double(c.n) * c.n * c.n;
+        if (info) { r.error = INFINITY; return r; }
+        if (c.P.check) {
+            BaseTrapezoidMatrix<T> As(Uplo::Lower, Ag, MatrixKind::Trapezoid);
+            auto Ai = full_of(c, As, true);
+            auto I = c.zeros(c.n, c.n);
+            set(T(0), T(1), I, c.opts);
+            gemm(T(1), A0, Ai, T(-1), I, c.opts);
+            r.error = c.nrm(I) / (double(c.n) * c.nrm(A0) * c.nrm(Ai));
+        }
+    }
+    return r;
+}
+
+template <typename T>
+Result r_gesv_v(Case<T>& c, int variant) {   // 0 nopiv, 1 tntpiv, 2 rbt
+    if (variant == 0)
+        return solve_case<T>(c, "rands+n", [&](Matrix<T>& A, Matrix<T>& B) { return gesv_nopiv(A, B, c.opts); },
+                             getrf_fl<T>(c.n));
+    if (variant == 1) {
+        Options o = c.opts;
+        o[Option::MethodLU] = int64_t(MethodLU::CALU);
+        return solve_case<T>(c, "rands", [&, o](Matrix<T>& A, Matrix<T>& B) { Pivots piv; return gesv(A, piv, B, o); },
+                             getrf_fl<T>(c.n));
+    }
+    auto A = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(A), X = c.zeros(c.n, c.P.nrhs);
+    Result r;
+    int iter = 0;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = gesv_rbt(A, B, X, iter, c.opts); });
+    r.flops = getrf_fl<T>(c.n);
+    r.note = "iter=" + std::to_string(iter);
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) r.error = c.solve_resid(A0, X, B);
+    return r;
+}
+
+template <typename T>
+Result r_condest(Case<T>& c, int variant) {   // 0 gecondest, 1 pocondest, 2 trcondest
+    Result r;
+    auto A = c.mat(c.n, c.n, variant == 1 ? "spd" : "rands+n");
+    const double anorm = c.nrm(A);
+    R_<T> rc = 0;
+    if (variant == 0) {
+        Pivots piv;
+        getrf(A, piv, c.opts);
+        r.time = c.timed([&] { rc = gecondest(Norm::One, A, R_<T>(anorm), c.opts); });
+    } else if (variant == 1) {
+        HermitianMatrix<T> H(Uplo::Lower, A);
+        potrf(H, c.opts);
+        r.time = c.timed([&] { rc = pocondest(Norm::One, H, R_<T>(anorm), c.opts); });
+    } else {
+        TriangularMatrix<T> L(Uplo::Lower, Diag::NonUnit, A);
+        r.time = c.timed([&] { rc = trcondest(Norm::One, L, c.opts); });
+    }
+    r.flops = cfac<T>() * 4.0 * c.n * c.n;
+    r.error = (rc > 0 && rc <= 1) ? 0.0 : INFINITY;   // an estimate: only its range is checked
+    char b[48];
+    std::snprintf(b, sizeof(b), "rcond=%.3e", double(rc));
+    r.note = b;
+    return r;
+}
+
+template <typename T>
+Result r_unmqr(Case<T>& c, bool lq) {
+    auto A = c.mat(c.m, c.n), C = c.mat(lq ? c.n : c.m, c.P.nrhs);
+    auto C0 = c.copy_of(C);
+    TriangularFactors<T> Tf;
+    if (lq) gelqf(A, Tf, c.opts); else geqrf(A, Tf, c.opts);
+    Result r;
+    r.time = c.timed([&] {
+        if (lq) unmlq(Side::Left, Op::ConjTrans, A, Tf, C, c.opts);
+        else unmqr(Side::Left, Op::ConjTrans, A, Tf, C, c.opts);
+    });
+    r.flops = cfac<T>() * 4.0 * c.m * c.n * c.P.nrhs;
+    if (c.P.check) {   // Q (Q^H C) = C
+        if (lq) unmlq(Side::Left, Op::NoTrans, A, Tf, C, c.opts);
+        else unmqr(Side::Left, Op::NoTrans, A, Tf, C, c.opts);
+        add(T(-1), C0, T(1), C, c.opts);
+        r.error = c.nrm(C) / (c.nrm(C0) * double(c.m));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_cholqr(Case<T>& c) {
+    if (c.m < c.n) { Result r; r.skipped = true; r.note = "m >= n"; return r; }
+    auto A = c.mat(c.m, c.n);
+    auto A0 = c.copy_of(A), Rm = c.zeros(c.n, c.n);
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = cholqr(A, Rm, c.opts); });
+    r.flops = cfac<T>() * (2.0 * c.m * c.n * c.n + double(c.n) * c.n * c.n / 3);
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {   // Q R = A0
+        TriangularMatrix<T> Rt(Uplo::Upper, Diag::NonUnit, Rm);
+        auto QR = c.copy_of(A);
+        trmm(Side::Right, T(1), Rt, QR, c.opts);
+        add(T(-1), A0, T(1), QR, c.opts);
+        r.error = c.nrm(QR) / (double(c.m) * c.nrm(A0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbtrs, 3 gbmm, 4 hbmm, 5 tbsm
+    const int64_t kd = std::max<int64_t>(1, c.nb / 2);
+    Result r;
+    if (variant == 1 || variant == 2 || variant == 4) {
+        auto Ag = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+        // Hermitian band with a dominant diagonal: H = band(A + A^H) + 4 kd I
+        auto F = c.zeros(c.n, c.n);
+        copy<T, T>(conj_transpose(Ag), F, c.opts);
+        add(T(1), Ag, T(1), F, c.opts);
+        BandMatrix<T> Fb(kd, kd, F);
+        auto D = c.zeros(c.n, c.n);
+        set(T(0), T(4 * kd + 4), D, c.opts);
+        add(T(1), D, T(1), F, c.opts);
+        auto Fz = c.zeros(c.n, c.n);   // dense band copy for the residual
+        {
+            auto Tmp = c.copy_of(F);
+            BandMatrix<T> Tb(kd, kd, Tmp);
+            auto I = c.zeros(c.n, c.n);
+            set(T(0), T(1), I, c.opts);
+            gbmm(T(1), Tb, I, T(0), Fz, c.opts);
+        }
+        auto B0 = c.copy_of(B);
+        HermitianBandMatrix<T> H(Uplo::Lower, kd, F);
+        if (variant == 4) {
+            auto C = c.zeros(c.n, c.P.nrhs);
+            r.time = c.timed([&] { hbmm(Side::Left, T(1), H, B, T(0), C, c.opts); });
+            r.flops = cfac<T>() * 2.0 * c.n * (2 * kd + 1) * c.P.nrhs;
+            if (c.P.check) {
+                gemm(T(-1), Fz, B, T(1), C, c.opts);
+                r.error = c.nrm(C) / (c.nrm(Fz) * c.nrm(B) * double(c.n));
+            }
+            return r;
+        }
+        int64_t info = 0;
+        r.time = c.timed([&] {
+            if (variant == 1) info = pbsv(H, B, c.opts);
+            else { info = pbtrf(H, c.opts); if (!info) pbtrs(H, B, c.opts); }
+        });
+        r.flops = cfac<T>() * double(c.n) * kd * kd;
+        if (info) { r.error = INFINITY; return r; }
+        if (c.P.check) r.error = c.solve_resid(Fz, B, B0);
+        return r;
+    }
+    auto Ag = c.mat(c.n, c.n, "rands+n", -1, true), B = c.mat(c.n, c.P.nrhs);
+    auto A0g = c.copy_of(Ag), B0 = c.copy_of(B);
+    BandMatrix<T> A(kd, kd / 2 + 1, Ag), A0(kd, kd / 2 + 1, A0g);
+    if (variant == 3) {
+        auto C = c.zeros(c.n, c.P.nrhs);
+        r.time = c.timed([&] { gbmm(T(1), A0, B, T(0), C, c.opts); });
+        r.flops = cfac<T>() * 2.0 * c.n * (1.5 * kd + 2) * c.P.nrhs;
+        if (c.P.check) {   // (A0 B) X via the band multiply twice
+            auto C2 = c.zeros(c.n, c.P.nrhs);
+            gbmm(T(1), A0, B, T(0), C2, c.opts);
+            add(T(-1), C, T(1), C2, c.opts);
+            r.error = c.nrm(C2) / std::max(1e-300, c.nrm(C));
+        }
+        return r;
+    }
+    if (variant == 5) {
+        TriangularBandMatrix<T> L(Uplo::Lower, Diag::NonUnit, kd, Ag);
+        auto X = c.copy_of(B);
+        r.time = c.timed([&] { tbsm(Side::Left, T(1), L, X, c.opts); });
+        r.flops = cfac<T>() * double(c.n) * kd * c.P.nrhs;
+        if (c.P.check) {   // L X == B through the dense triangle of the band
+            auto D = c.zeros(c.n, c.n);
+            BaseTrapezoidMatrix<T> Ls(Uplo::Lower, A0g, MatrixKind::Trapezoid), Ds(Uplo::Lower, D, MatrixKind::Trapezoid);
+            copy<T, T>(Ls, Ds, c.opts);
+            BandMatrix<T> Db(kd, 0, D);
+            auto LX = c.zeros(c.n, c.P.nrhs);
+            gbmm(T(1), Db, X, T(0), LX, c.opts);
+            add(T(-1), B0, T(1), LX, c.opts);
+            r.error = c.nrm(LX) / (c.nrm(B0) * double(c.n));
+        }
+        return r;
+    }
+    int64_t info = 0;
+    r.time = c.timed([&] { Pivots piv; info = gbtrf(A, piv, c.opts); if (!info) gbtrs(A, piv, B, c.opts); });
+    r.flops = cfac<T>() * 2.0 * c.n * kd * (1.5 * kd + 1);
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {
+        auto Rm = c.copy_of(B0);
+        gbmm(T(-1), A0, B, T(1), Rm, c.opts);
+        r.error = c.nrm(Rm) / (double(c.n) * c.nrm(B0) * c.nrm(B));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_hetrf(Case<T>& c) {
+    auto Ag = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+    // indefinite Hermitian: A + A^H
+    auto H0 = c.zeros(c.n, c.n);
+    copy<T, T>(conj_transpose(Ag), H0, c.opts);
+    add(T(1), Ag, T(1), H0, c.opts);
+    auto Hg = c.copy_of(H0), B0 = c.copy_of(B);
+    HermitianMatrix<T> H(Uplo::Lower, Hg);
+    std::vector<int64_t> ipiv;
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = hetrf(H, ipiv, c.opts); });
+    r.flops = cfac<T>() * double(c.n) * c.n * c.n / 3;
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) {
+        hetrs(H, ipiv, B, c.opts);
+        r.error = c.solve_resid(H0, B, B0);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_vals(Case<T>& c, int variant) {   // 0 heev values, 1 svd values, 2 hegv
+    Result r;
+    if (variant == 1) {
+        auto A = c.mat(c.m, c.n, "rands", -1, true);
+        auto A0 = c.copy_of(A);
+        std::vector<R_<T>> S;
+        r.time = c.timed([&] { svd_vals(A, S, c.opts); });
+        r.flops = cfac<T>() * 8.0 / 3 * double(std::min(c.m, c.n)) * c.m * c.n;
+        // sum of squares of the singular values == ||A||_F^2
+        double ss = 0;
+        for (auto v : S) ss += double(v) * double(v);
+        double f = double(norm(Norm::Fro, A0, c.opts));
+        r.error = std::abs(ss - f * f) / (f * f * double(c.n));
+        return r;
+    }
+    auto Ag = c.mat(c.n, c.n, "spd", 0.0);
+    auto A0 = c.copy_of(Ag);
+    HermitianMatrix<T> A(Uplo::Lower, Ag);
+    std::vector<R_<T>> L;
+    if (variant == 0) {
+        Matrix<T> none;
+        r.time = c.timed([&] { heev(A, L, none, c.opts); });
+        r.flops = cfac<T>() * 4.0 / 3 * double(c.n) * c.n * c.n;
+        if (c.P.check) {   // the values-only path against the vectors path
+            auto Ag2 = c.copy_of(A0);
+            HermitianMatrix<T> A2(Uplo::Lower, Ag2);
+            auto Z = c.zeros(c.n, c.n);
+            std::vector<R_<T>> L2;
+            heev(A2, L2, Z, c.opts);
+            double mx = 0;
+            for (int64_t i = 0; i < c.n; ++i) mx = std::max(mx, std::abs(double(L[i]) - double(L2[i])));
+            r.error = mx / (double(c.n) * c.nrm(A0));
+        }
+        return r;
+    }
+    auto Bg = c.mat(c.n, c.n, "spd");
+    HermitianMatrix<T> B(Uplo::Lower, Bg);
+    auto B0 = c.copy_of(Bg);
+    auto Z = c.zeros(c.n, c.n);
+    r.time = c.timed([&] { hegv(1, A, B, L, Z, c.opts); });
+    r.flops = cfac<T>() * 3.0 * double(c.n) * c.n * c.n;
+    if (c.P.check) {   // A Z = B Z Lambda
+        auto AZ = c.zeros(c.n, c.n), BZ = c.zeros(c.n, c.n);
+        gemm(T(1), A0, Z, T(0), AZ, c.opts);
+        gemm(T(1), B0, Z, T(0), BZ, c.opts);
+        std::vector<R_<T>> ones(c.n, R_<T>(1));
+        scale_row_col(Equed::Col, ones, L, BZ, c.opts);
+        add(T(-1), BZ, T(1), AZ, c.opts);
+        r.error = c.nrm(AZ) / (double(c.n) * c.nrm(A0) * c.nrm(Z));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_tridiag(Case<T>& c, int variant) {   // 0 sterf, 1 steqr2, 2 stedc (via heev method dc on a tridiagonal)
+    using R = R_<T>;
+    const int64_t n = c.n;
+    std::vector<R> d(n), e(std::max<int64_t>(n - 1, 0));
+    for (int64_t i = 0; i < n; ++i) d[i] = R(2) + R(i % 7) / R(10);
+    for (int64_t i = 0; i + 1 < n; ++i) e[i] = R(-1) + R(i % 5) / R(20);
+    auto d0 = d;
+    auto e0 = e;
+    Result r;
+    if (variant == 0) {
+        r.time = c.timed([&] { sterf<R>(d, e, c.opts); });
+        double s0 = 0, s1 = 0;
+        for (auto v : d0) s0 += double(v);
+        for (auto v : d) s1 += double(v);
+        r.error = std::abs(s0 - s1) / (std::abs(s0) * double(n));   // trace preserved
+        r.flops = 30.0 * n * n;
+        return r;
+    }
+    auto Z = c.zeros(n, n);
+    set(T(0), T(1), Z, c.opts);
+    r.time = c.timed([&] { steqr2(Job::Vec, d, e, Z, c.opts); });
+    r.flops = 6.0 * double(n) * n * n;
+    if (c.P.check) {
+        // T Z = Z diag(d) with T built as a dense tridiagonal
+        auto Tm = c.zeros(n, n);
+        std::function<T(int64_t, int64_t)> tv = [&](int64_t i, int64_t j) -> T {
+            if (i == j) return T(d0[i]);
+            if (i == j + 1) return T(e0[j]);
+            if (j == i + 1) return T(e0[i]);
+            return T(0);
+        };
+        set(tv, Tm, c.opts);
+        auto TZ = c.zeros(n, n), ZL = c.copy_of(Z);
+        gemm(T(1), Tm, Z, T(0), TZ, c.opts);
+        std::vector<R> ones(n, R(1));
+        scale_row_col(Equed::Col, ones, d, ZL, c.opts);
+        add(T(-1), ZL, T(1), TZ, c.opts);
+        r.error = c.nrm(TZ) / (double(n) * c.nrm(Tm));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_aux(Case<T>& c, int variant) {   // 0 add, 1 copy, 2 scale, 3 set, 4 trtrm, 5 colnorms, 6 henorm, 7 redistribute
+    auto A = c.mat(c.m, c.n, "rands", -1, true), B = c.mat(c.m, c.n);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(B);
+    Result r;
+    r.flops = double(c.m) * c.n;
+    switch (variant) {
+        case 0:
+            r.time = c.timed([&] { add(T(2), A, T(-1), B, c.opts); });
+            if (c.P.check) { add(T(-2), A0, T(1), B, c.opts); add(T(1), B0, T(1), B, c.opts); r.error = c.nrm(B) / c.nrm(B0); }
+            break;
+        case 1:
+            r.time = c.timed([&] { copy<T, T>(A, B, c.opts); });
+            if (c.P.check) { add(T(-1), A0, T(1), B, c.opts); r.error = c.nrm(B); }
+            break;
+        case 2:
+            r.time = c.timed([&] { scale(R_<T>(3), R_<T>(2), A, c.opts); });
+            if (c.P.check) { add(T(-1.5), A0, T(1), A, c.opts); r.error = c.nrm(A) / c.nrm(A0); }
+            break;
+        case 3:
+            r.time = c.timed([&] { set(T(0.5), T(2), A, c.opts); });
+            if (c.P.check) {
+                double e = double(norm(Norm::Max, A, c.opts));
+                r.error = std::abs(e - 2.0) / 2.0;
+            }
+            break;
+        case 4: {
+            if (c.m != c.n) { r.skipped = true; r.note = "square only"; break; }
+            TriangularMatrix<T> L(Uplo::Lower, Diag::NonUnit, A);
+            r.time = c.timed([&] { trtrm(L, c.opts); });
+            r.flops = cfac<T>() * double(c.n) * c.n * c.n / 3;
+            if (c.P.check) {   // L^H L from the original lower triangle
+                auto Lg = c.zeros(c.n, c.n);
+                BaseTrapezoidMatrix<T> Ls(Uplo::Lower, A0, MatrixKind::Trapezoid), Ld(Uplo::Lower, Lg, MatrixKind::Trapezoid);
+                copy<T, T>(Ls, Ld, c.opts);
+                auto P = c.zeros(c.n, c.n);
+                gemm(T(1), conj_transpose(Lg), Lg, T(0), P, c.opts);
+                BaseTrapezoidMatrix<T> Rs(Uplo::Lower, A, MatrixKind::Trapezoid), Ps(Uplo::Lower, P, MatrixKind::Trapezoid);
+                add(T(-1), Rs, T(1), Ps, c.opts);
+                r.error = double(norm(Norm::Max, Ps, c.opts)) / (c.nrm(Lg) * c.nrm(Lg));
+            }
+            break;
+        }
+        case 5: {
+            std::vector<R_<T>> v(c.n);
+            r.time = c.timed([&] { colNorms(Norm::Max, A, v.data(), c.opts); });
+            if (c.P.check) {
+                double mx = 0;
+                for (auto x : v) mx = std::max(mx, double(x));
+                const double am = double(norm(Norm::Max, A, c.opts));
+                r.error = std::abs(mx - am) / am;   // max over the column maxima == max norm
+            }
+            break;
+        }
+        case 6: {
+            if (c.m != c.n) { r.skipped = true; r.note = "square only"; break; }
+            HermitianMatrix<T> H(Uplo::Lower, A);
+            R_<T> v1 = 0;
+            r.time = c.timed([&] { v1 = norm(Norm::One, H, c.opts); });
+            if (c.P.check) {
+                BaseTrapezoidMatrix<T> Hs(Uplo::Lower, A, MatrixKind::Trapezoid);
+                auto F = full_of(c, Hs, true);
+                r.error = std::abs(double(v1) - c.nrm(F)) / c.nrm(F);
+            }
+            break;
+        }
+        case 7: {
+            // 2D block-cyclic -> transposed-grid layout with another tile size and back
+            auto g = default_grid();
+            Matrix<T> Bt(c.m, c.n, std::max<int64_t>(1, c.nb / 2 + 3), g->transposed());
+            Bt.insertLocalTiles(c.P.target);
+            r.time = c.timed([&] { redistribute(A, Bt, c.opts); });
+            if (c.P.check) {
+                auto Back = c.zeros(c.m, c.n);
+                redistribute(Bt, Back, c.opts);
+                add(T(-1), A0, T(1), Back, c.opts);
+                r.error = c.nrm(Back) / c.nrm(A0);
+            }
+            break;
+        }
+        default: break;
+    }
+    return r;
+}
+
 template <typename T>
 using Fn = std::function<Result(Case<T>&)>;
 
@@ -565,6 +1125,44 @@ std::map<std::string, Fn<T>> routines() {
         {"getri", r_getri<T>}, {"trtri", r_trtri<T>},
         {"geqrf", r_geqrf<T>}, {"gelqf", r_gelqf<T>}, {"gels", r_gels<T>},
         {"heev", r_heev<T>}, {"svd", r_svd<T>}, {"hesv", r_hesv<T>}, {"gbsv", r_gbsv<T>}, {"genorm", r_genorm<T>},
+        {"syrk", [](Case<T>& c) { return r_rankk<T>(c, 0); }},
+        {"her2k", [](Case<T>& c) { return r_rankk<T>(c, 1); }},
+        {"syr2k", [](Case<T>& c) { return r_rankk<T>(c, 2); }},
+        {"symm", r_symm<T>},
+        {"gemmA", [](Case<T>& c) { return r_gemm_m<T>(c, MethodGemm::GemmA); }},
+        {"gemmC", [](Case<T>& c) { return r_gemm_m<T>(c, MethodGemm::GemmC); }},
+        {"getrs", r_getrs<T>},
+        {"potrs", [](Case<T>& c) { return r_potrs<T>(c, 0); }},
+        {"potri", [](Case<T>& c) { return r_potrs<T>(c, 1); }},
+        {"gesv_nopiv", [](Case<T>& c) { return r_gesv_v<T>(c, 0); }},
+        {"gesv_tntpiv", [](Case<T>& c) { return r_gesv_v<T>(c, 1); }},
+        {"gesv_rbt", [](Case<T>& c) { return r_gesv_v<T>(c, 2); }},
+        {"gecondest", [](Case<T>& c) { return r_condest<T>(c, 0); }},
+        {"pocondest", [](Case<T>& c) { return r_condest<T>(c, 1); }},
+        {"trcondest", [](Case<T>& c) { return r_condest<T>(c, 2); }},
+        {"unmqr", [](Case<T>& c) { return r_unmqr<T>(c, false); }},
+        {"unmlq", [](Case<T>& c) { return r_unmqr<T>(c, true); }},
+        {"cholqr", r_cholqr<T>},
+        {"gbtrf", [](Case<T>& c) { return r_band<T>(c, 0); }},
+        {"pbsv", [](Case<T>& c) { return r_band<T>(c, 1); }},
+        {"pbtrf", [](Case<T>& c) { return r_band<T>(c, 2); }},
+        {"gbmm", [](Case<T>& c) { return r_band<T>(c, 3); }},
+        {"hbmm", [](Case<T>& c) { return r_band<T>(c, 4); }},
+        {"tbsm", [](Case<T>& c) { return r_band<T>(c, 5); }},
+        {"hetrf", r_hetrf<T>},
+        {"heev_vals", [](Case<T>& c) { return r_vals<T>(c, 0); }},
+        {"svd_vals", [](Case<T>& c) { return r_vals<T>(c, 1); }},
+        {"hegv", [](Case<T>& c) { return r_vals<T>(c, 2); }},
+        {"sterf", [](Case<T>& c) { return r_tridiag<T>(c, 0); }},
+        {"steqr2", [](Case<T>& c) { return r_tridiag<T>(c, 1); }},
+        {"add", [](Case<T>& c) { return r_aux<T>(c, 0); }},
+        {"copy", [](Case<T>& c) { return r_aux<T>(c, 1); }},
+        {"scale", [](Case<T>& c) { return r_aux<T>(c, 2); }},
+        {"set", [](Case<T>& c) { return r_aux<T>(c, 3); }},
+        {"trtrm", [](Case<T>& c) { return r_aux<T>(c, 4); }},
+        {"colnorms", [](Case<T>& c) { return r_aux<T>(c, 5); }},
+        {"henorm", [](Case<T>& c) { return r_aux<T>(c, 6); }},
+        {"redistribute", [](Case<T>& c) { return r_aux<T>(c, 7); }},
     };
 }
 
@@ -609,6 +1207,15 @@ int run_type(Params const& P, char tc, std::string const& name) {
                                 r.time, gf, status.c_str(), r.note.empty() ? "" : "  ", r.note.c_str());
                     std::fflush(stdout);
                 }
+                if (P.timer_level >= 2) {
+                    // per-driver wall time of this case from the host trace (reference --timer-level 2)
+                    std::map<std::string, double> tot;
+                    for (auto const& e : trace::Trace::events())
+                        if (e.lane < 100) tot[e.name] += e.stop - e.start;
+                    if (rank() == 0)
+                        for (auto const& kv : tot) std::printf("#   %-24s %10.4f s\n", kv.first.c_str(), kv.second);
+                    trace::Trace::clear();
+                }
             }
     return fails;
 }
@@ -618,6 +1225,9 @@ void usage() {
         "usage: slate_tester ROUTINE[,ROUTINE...]|all [--type d,s,z,c] [--dim N|A:B:STEP|MxNxK,...]\n"
         "       [--nb NB,...] [--grid PxQ] [--target d|h] [--lookahead LA] [--nrhs K]\n"
         "       [--check y|n] [--tol T] [--repeat R] [--trace y|n]\n"
+        "       [--matrix KIND] [--method-lu ppiv|calu|nopiv] [--method-trsm auto|A|B]\n"
+        "       [--method-gemm auto|A|C] [--method-hemm auto|A|C] [--origin h|d]\n"
+        "       [--timer-level 1|2] [--itermax N] [--fallback y|n] [--pivot-threshold X]\n"
         "routines:");
     for (auto const& kv : routines<double>()) std::printf(" %s", kv.first.c_str());
     std::printf("\n");
@@ -650,6 +1260,16 @@ int main(int argc, char** argv) {
         else if (a == "--tol") P.tol = std::stod(val());
         else if (a == "--repeat") P.repeat = std::stoi(val());
         else if (a == "--trace") P.trace = val()[0] == 'y';
+        else if (a == "--matrix") P.matrix = val();
+        else if (a == "--method-lu") P.method_lu = MethodLU::str2method(val());
+        else if (a == "--method-trsm") P.method_trsm = MethodTrsm::str2method(val());
+        else if (a == "--method-gemm") P.method_gemm = MethodGemm::str2method(val());
+        else if (a == "--method-hemm") P.method_hemm = MethodHemm::str2method(val());
+        else if (a == "--origin") P.origin = char(std::tolower(val()[0]));
+        else if (a == "--timer-level") P.timer_level = std::stoi(val());
+        else if (a == "--itermax") P.itermax = std::stoll(val());
+        else if (a == "--fallback") P.fallback = val()[0] == 'y' ? 1 : 0;
+        else if (a == "--pivot-threshold") P.pivot_threshold = std::stod(val());
         else if (!a.empty() && a[0] != '-') rlist = rlist.empty() ? a : rlist + "," + a;
         else { usage(); return 2; }
     }
@@ -665,7 +1285,7 @@ int main(int argc, char** argv) {
         std::printf("%-16s %-4s %7s %7s %7s %5s %2s %2s %10s %10s %11s  %s\n", "routine", "type", "m", "n", "k", "nb",
                     "p", "q", "error", "time(s)", "gflop/s", "status");
     }
-    if (P.trace) trace::Trace::on();
+    if (P.trace || P.timer_level >= 2) trace::Trace::on();
     int fails = 0;
     std::stringstream rs(rlist);
     std::string name;

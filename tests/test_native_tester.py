@@ -41,7 +41,7 @@ def launch(args, nprocs=1, timeout=600, target="h"):
 def test_all_routines_single_process():
     codes, outs = launch(["all", "--type", "d,z", "--dim", "200", "--nb", "48"])
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
-    assert outs[0].count("pass") >= 40
+    assert outs[0].count("pass") >= 110       # ~62 routines x 2 types
 
 
 @pytest.mark.parametrize("nprocs,grid", [(2, "1x2"), (4, "2x2")])
@@ -56,8 +56,30 @@ def test_rectangular_and_sweeps():
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
 
 
+def test_breadth_distributed_2x2():
+    """The breadth additions (rank-2k, stationary-A, condest, unm*, cholqr,
+    band, indefinite, generalized eig, tridiagonal, aux) on a 2x2 grid."""
+    codes, outs = launch(["syrk,her2k,syr2k,symm,gemmA,gemmC,getrs,potrs,potri,gesv_nopiv,gesv_tntpiv,gesv_rbt,"
+                          "gecondest,pocondest,unmqr,unmlq,cholqr,gbtrf,pbsv,gbmm,hbmm,tbsm,hetrf,heev_vals,svd_vals,"
+                          "hegv,steqr2,add,copy,scale,set,trtrm,colnorms,henorm,redistribute",
+                          "--type", "d,z", "--dim", "150", "--nb", "32", "--grid", "2x2"], 4)
+    assert codes == [0] * 4 and "all tests passed" in outs[0], "\n".join(o[-2500:] for o in outs)
+
+
+def test_tester_flags():
+    """--matrix (element and spectral matgen kinds), --method-lu/trsm/gemm,
+    --origin h, --timer-level 2 (per-driver times), --pivot-threshold."""
+    codes, outs = launch(["getrf,gesv,trsm,gemm,geqrf", "--type", "d", "--dim", "160", "--nb", "32", "--matrix", "svd",
+                          "--method-lu", "calu", "--method-trsm", "A", "--method-gemm", "A", "--origin", "h",
+                          "--timer-level", "2", "--pivot-threshold", "0.5"])
+    assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
+    assert "#   getrf" in outs[0]
+
+
 @pytest.mark.gpu
 def test_device_routines():
-    codes, outs = launch(["gemm,herk,trsm,potrf,getrf,getrf_tntpiv,geqrf,gesv_mixed,posv_mixed,heev,svd",
+    codes, outs = launch(["gemm,herk,trsm,potrf,getrf,getrf_tntpiv,geqrf,gesv_mixed,posv_mixed,heev,svd,"
+                          "syr2k,symm,gemmA,getrs,potri,gesv_rbt,unmqr,unmlq,cholqr,gbtrf,pbsv,hbmm,tbsm,heev_vals,"
+                          "svd_vals,hegv,steqr2,redistribute",
                           "--type", "d,z", "--dim", "1000", "--nb", "128"], target="d")
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
