@@ -63,17 +63,19 @@ $(SCALAPACK_API): $(BUILD)/api_scalapack_api.o $(LIB)
 tester: $(TESTER)
 # native tester (reference test/tester); like the examples it only depends on
 # its source, so a tree without build/obj does not rebuild the library
-$(TESTER): csrc/tools/tester.cc
+$(TESTER): csrc/tools/tester.cc $(wildcard csrc/include/slate_amd/*.hh)
 	@mkdir -p bin
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../$(PKG)' $(LDLIBS)
 
 # C++ examples (reference examples/ex01-ex15), linked against the library
 EX_SRC    := $(wildcard examples/cpp/ex*.cc)
 # Binaries go to examples/bin (shipped to GPU boxes with the tree); they only
-# depend on their sources so a tree without build/obj does not rebuild the library.
+# depend on their sources and the public headers (inline classes such as
+# MatrixStorage) so a tree without build/obj does not rebuild the library.
 EX_BIN    := $(patsubst examples/cpp/%.cc,examples/bin/%,$(EX_SRC))
 examples: $(EX_BIN)
-examples/bin/%: examples/cpp/%.cc examples/cpp/util.hh
+PUB_HDR   := $(wildcard csrc/include/slate_amd/*.hh)
+examples/bin/%: examples/cpp/%.cc examples/cpp/util.hh $(PUB_HDR)
 	@mkdir -p examples/bin
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../../$(PKG)' $(LDLIBS)
 

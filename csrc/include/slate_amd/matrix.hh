@@ -23,6 +23,7 @@
 
 #include <functional>
 #include <memory>
+#include <tuple>
 
 namespace slate {
 
@@ -62,6 +63,22 @@ public:
     /// rsrc/csrc: process row/column owning the first tile row/column
     /// (ScaLAPACK descriptor RSRC/CSRC).
     MatrixStorage(int64_t m, int64_t n, int64_t mb, int64_t nb, GridPtr grid, int rsrc = 0, int csrc = 0);
+
+    /// Arbitrary distribution (reference Matrix.hh:207-212 lambda constructor):
+    /// tile row/column sizes and the owning world rank of every tile.  The
+    /// tiles a process owns are packed column-major one after another (ld =
+    /// tile rows) in one host / device buffer.
+    struct Layout {
+        int64_t mt = 0, nt = 0;
+        std::vector<int64_t> rs, cs;       // tile row / column starts (mt + 1, nt + 1)
+        std::vector<int> owner;            // world rank of tile (i, j) at i + j mt
+        std::vector<int64_t> toff;         // my tiles: element offset in the local buffer, else -1
+    };
+    MatrixStorage(int64_t m, int64_t n, std::function<int64_t(int64_t)> const& tile_mb,
+                  std::function<int64_t(int64_t)> const& tile_nb,
+                  std::function<int(int64_t, int64_t)> const& tile_rank, GridPtr grid);
+    std::shared_ptr<Layout> layout;
+    bool general() const { return layout != nullptr; }
     ~MatrixStorage();
     MatrixStorage(MatrixStorage const&) = delete;
     MatrixStorage& operator=(MatrixStorage const&) = delete;
@@ -150,9 +167,12 @@ public:
     /// rank owning logical tile (i, j)
     int tileRank(int64_t i, int64_t j) const {
         int64_t si, sj; to_storage(i, j, si, sj);
+        if (storage_->general()) return storage_->layout->owner[si + sj * storage_->layout->mt];
         auto& g = *storage_->grid;
         return g.rank_of(storage_->row_owner(stile_r(si)), storage_->col_owner(stile_c(sj)));
     }
+    /// arbitrary (lambda) distribution: drivers work on a block-cyclic copy
+    bool arbitrary_layout() const { return storage_ && storage_->general(); }
     bool tileIsLocal(int64_t i, int64_t j) const { return tileRank(i, j) == mpiRank(); }
     int tileDevice(int64_t i, int64_t j) const { return tileIsLocal(i, j) ? 0 : HostNum; }
     /// process row / column owning storage tile-row/col (storage orientation)
@@ -234,14 +254,28 @@ protected:
     int64_t stile_c0() const { return c0_ / storage_->nb; }
     int64_t stile_r(int64_t si) const { return stile_r0() + si; }
     int64_t stile_c(int64_t sj) const { return stile_c0() + sj; }
-    int64_t smt() const { return m_ == 0 ? 0 : (r0_ + m_ - 1) / storage_->mb - stile_r0() + 1; }
-    int64_t snt() const { return n_ == 0 ? 0 : (c0_ + n_ - 1) / storage_->nb - stile_c0() + 1; }
-    int64_t srow_start(int64_t si) const { return std::max(r0_, stile_r(si) * storage_->mb); }
-    int64_t scol_start(int64_t sj) const { return std::max(c0_, stile_c(sj) * storage_->nb); }
+    int64_t smt() const {
+        if (storage_->general()) return storage_->layout->mt;
+        return m_ == 0 ? 0 : (r0_ + m_ - 1) / storage_->mb - stile_r0() + 1;
+    }
+    int64_t snt() const {
+        if (storage_->general()) return storage_->layout->nt;
+        return n_ == 0 ? 0 : (c0_ + n_ - 1) / storage_->nb - stile_c0() + 1;
+    }
+    int64_t srow_start(int64_t si) const {
+        if (storage_->general()) return storage_->layout->rs[si];
+        return std::max(r0_, stile_r(si) * storage_->mb);
+    }
+    int64_t scol_start(int64_t sj) const {
+        if (storage_->general()) return storage_->layout->cs[sj];
+        return std::max(c0_, stile_c(sj) * storage_->nb);
+    }
     int64_t srow_size(int64_t si) const {
+        if (storage_->general()) return storage_->layout->rs[si + 1] - storage_->layout->rs[si];
         return std::min(r0_ + m_, (stile_r(si) + 1) * storage_->mb) - srow_start(si);
     }
     int64_t scol_size(int64_t sj) const {
+        if (storage_->general()) return storage_->layout->cs[sj + 1] - storage_->layout->cs[sj];
         return std::min(c0_ + n_, (stile_c(sj) + 1) * storage_->nb) - scol_start(sj);
     }
 
@@ -272,6 +306,17 @@ public:
     Matrix(int64_t m, int64_t n, int64_t mb, int64_t nb, GridPtr grid, int rsrc = 0, int csrc = 0)
         : BaseMatrix<T>(std::make_shared<MatrixStorage<T>>(m, n, mb, nb, grid ? grid : default_grid(), rsrc, csrc)) {}
     explicit Matrix(BaseMatrix<T> const& b) : BaseMatrix<T>(b) { this->set_kind(MatrixKind::General); }
+    /// Arbitrary distribution with non-uniform tiles (reference Matrix.hh:
+    /// 207-212): tileMb(i), tileNb(j), tileRank({i, j}) (world rank),
+    /// tileDevice (one GPU per process here, accepted for API parity).  The
+    /// grid supplies the communicators; drivers run on a block-cyclic copy.
+    Matrix(int64_t m, int64_t n, std::function<int64_t(int64_t)> tileMb, std::function<int64_t(int64_t)> tileNb,
+           std::function<int(std::tuple<int64_t, int64_t>)> tileRank,
+           std::function<int(std::tuple<int64_t, int64_t>)> tileDevice, GridPtr grid = nullptr)
+        : BaseMatrix<T>(std::make_shared<MatrixStorage<T>>(
+              m, n, tileMb, tileNb,
+              [tileRank](int64_t i, int64_t j) { return tileRank(std::make_tuple(i, j)); },
+              grid ? grid : default_grid())) { (void)tileDevice; }
 
     /// Wrap a column-major LAPACK array (1 x 1 grid or replicated-rank use).
     static Matrix fromLAPACK(int64_t m, int64_t n, T* A, int64_t lda, int64_t nb, Loc loc = Loc::Host);

@@ -254,6 +254,20 @@ void bind_type(py::module_& m, const char* sfx) {
             return Matrix<T>(mm, n, mb, nb, g ? g : default_grid());
         }), py::arg("m"), py::arg("n"), py::arg("mb"), py::arg("nb"), py::arg("grid") = nullptr)
         .def(py::init([](BaseMatrix<T> const& b) { return Matrix<T>(b); }))
+        // arbitrary distribution (reference lambda constructor): tile row /
+        // column sizes and the owning world rank of every tile (mt x nt list)
+        .def_static("with_layout", [](int64_t mm, int64_t n, std::vector<int64_t> rsz, std::vector<int64_t> csz,
+                                      std::vector<std::vector<int>> owner, GridPtr g) {
+            auto tmb = [rsz](int64_t i) { return i < int64_t(rsz.size()) ? rsz[i] : rsz.back(); };
+            auto tnb = [csz](int64_t j) { return j < int64_t(csz.size()) ? csz[j] : csz.back(); };
+            auto trk = [owner](std::tuple<int64_t, int64_t> ij) {
+                return owner.at(std::get<0>(ij)).at(std::get<1>(ij));
+            };
+            auto tdv = [](std::tuple<int64_t, int64_t>) { return 0; };
+            return Matrix<T>(mm, n, tmb, tnb, trk, tdv, g ? g : default_grid());
+        }, py::arg("m"), py::arg("n"), py::arg("row_sizes"), py::arg("col_sizes"), py::arg("owner"),
+           py::arg("grid") = nullptr)
+        .def("arbitrary_layout", &BaseMatrix<T>::arbitrary_layout)
         .def_static("fromDevicePointer", [](int64_t mm, int64_t n, uintptr_t ptr, int64_t lld, int64_t mb,
                                               int64_t nb, GridPtr g) {
             return Matrix<T>::fromScaLAPACK(mm, n, reinterpret_cast<T*>(ptr), lld, mb, nb, g, Loc::Device);

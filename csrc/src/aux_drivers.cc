@@ -218,7 +218,7 @@ void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     Uplo mask = Uplo::General;
     if (is_trapezoid_kind(B.matrix_kind())) mask = B.uplo();
-    if (A.grid()->size() == 1 && B.grid()->size() == 1 &&
+    if (A.grid()->size() == 1 && B.grid()->size() == 1 && !A.arbitrary_layout() && !B.arbitrary_layout() &&
         (B.op() == Op::NoTrans || (A.op() == Op::NoTrans && mask == Uplo::General))) {
         // one process holds both: one (transposing) device copy of the local
         // blocks instead of the tile-by-tile redistribution
@@ -232,7 +232,8 @@ void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
         internal::finish_origin(B, opts);
         return;
     }
-    if (A.op() == Op::NoTrans && B.op() == Op::NoTrans && same_layout(A, B) && A.aligned() && B.aligned()) {
+    if (A.op() == Op::NoTrans && B.op() == Op::NoTrans && !A.arbitrary_layout() && !B.arbitrary_layout() && same_layout(A, B) &&
+        A.aligned() && B.aligned()) {
         LocalBlock<Ts> la = A.local(loc, false);
         LocalBlock<Td> lbk = B.local(loc, true);
         if (mask == Uplo::General || A.grid()->size() == 1) {
@@ -263,6 +264,12 @@ void redistribute(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts) {
+    if (A.arbitrary_layout() || B.arbitrary_layout()) {
+        Matrix<T> Ab = bc_operand(A, opts), Bb = block_cyclic(B, opts);
+        add(alpha, Ab, beta, Bb, opts);
+        slate::copy<T, T>(Bb, B, opts);
+        return;
+    }
     trace::Block tb("add");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -303,6 +310,13 @@ void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T
 
 template <typename T>
 void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> B = block_cyclic(A, opts);
+        BaseMatrix<T>& Bb = B;
+        scale(numer, denom, Bb, opts);
+        slate::copy<T, T>(B, A, opts);
+        return;
+    }
     trace::Block tb("scale");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -363,6 +377,14 @@ void scale_row_col(Equed equed, std::vector<real_type<T>> const& R, std::vector<
 
 template <typename T>
 void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> B = block_cyclic(A, opts);
+        B.set_uplo(A.uplo());
+        BaseMatrix<T>& Bb = B;
+        set(offdiag, diag, Bb, opts);
+        slate::copy<T, T>(B, A, opts);
+        return;
+    }
     trace::Block tb("set");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -588,6 +610,14 @@ real_type<T> finish_norm(BaseMatrix<T> const& A, char kind, NormParts<T>& P) {
 
 template <typename T>
 real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> B = block_cyclic(A, opts);
+        B.set_kind(A.matrix_kind());
+        B.set_uplo(A.uplo());
+        B.set_diag(A.diag());
+        B.set_band(A.kl(), A.ku());
+        return norm(in_norm, BaseMatrix<T>(B), opts);
+    }
     trace::Block tb("norm");
     internal::DriverScope ds_;
     using R = real_type<T>;

@@ -271,6 +271,12 @@ void gemmA(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
 
 template <typename T>
 void gemm(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts) {
+    if (A.arbitrary_layout() || B.arbitrary_layout() || C.arbitrary_layout()) {
+        Matrix<T> Ab = bc_operand(A, opts), Bb = bc_operand(B, opts), Cb = block_cyclic(C, opts);
+        gemm(alpha, Ab, Bb, beta, Cb, opts);
+        slate::copy<T, T>(Cb, C, opts);
+        return;
+    }
     Method m = get_option<int64_t>(opts, Option::MethodGemm, MethodGemm::Auto);
     if (m == MethodGemm::Auto) m = MethodGemm::select_algo(A, B, opts);
     if (m == MethodGemm::GemmA) gemmA(alpha, A, B, beta, C, opts);
@@ -424,6 +430,13 @@ void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, M
 
 template <typename T>
 void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    if (A.arbitrary_layout() || B.arbitrary_layout()) {
+        TriangularMatrix<T> Ab(A.uplo(), A.diag(), bc_operand(A, opts));
+        Matrix<T> Bb = block_cyclic(B, opts);
+        trsm(side, alpha, Ab, Bb, opts);
+        slate::copy<T, T>(Bb, B, opts);
+        return;
+    }
     trace::Block tb("trsm");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);

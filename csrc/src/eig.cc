@@ -459,6 +459,13 @@ void set_diag_rows(Matrix<T>& M, std::vector<T> const& dg, Target target) {
 
 template <typename T>
 void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts) {
+    if (A.arbitrary_layout() || Z.arbitrary_layout()) {
+        HermitianMatrix<T> Ab(A.uplo(), bc_operand(A, opts));
+        Matrix<T> Zb = wanted(Z) ? block_cyclic(Z, opts) : Z;
+        heev(Ab, Lambda, Zb, opts);
+        if (wanted(Z)) slate::copy<T, T>(Zb, Z, opts);
+        return;
+    }
     trace::Block tb("heev");
     internal::DriverScope ds_;
     using R = real_type<T>;
@@ -638,6 +645,14 @@ void ge2tb(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<Tria
 
 template <typename T>
 void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts) {
+    if (A.arbitrary_layout() || U.arbitrary_layout() || VT.arbitrary_layout()) {
+        Matrix<T> Ab = bc_operand(A, opts);
+        Matrix<T> Ub = wanted(U) ? block_cyclic(U, opts) : U, Vb = wanted(VT) ? block_cyclic(VT, opts) : VT;
+        svd(Ab, Sigma, Ub, Vb, opts);
+        if (wanted(U)) slate::copy<T, T>(Ub, U, opts);
+        if (wanted(VT)) slate::copy<T, T>(Vb, VT, opts);
+        return;
+    }
     trace::Block tb("svd");
     internal::DriverScope ds_;
     using R = real_type<T>;

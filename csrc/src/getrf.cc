@@ -756,6 +756,12 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
 template <typename T>
 int64_t getrf(Matrix<T>& A, Pivots& pivots, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> Ab = internal::block_cyclic(A, opts);
+        int64_t info = getrf(Ab, pivots, opts);
+        slate::copy<T, T>(Ab, A, opts);
+        return info;
+    }
     Method m = get_option<int64_t>(opts, Option::MethodLU, MethodLU::PartialPiv);
     return getrf_impl(A, pivots, opts, m == MethodLU::NoPiv ? PanelMode::NoPiv :
                       (m == MethodLU::CALU ? PanelMode::Tournament : PanelMode::Partial));

@@ -119,6 +119,25 @@ inline void finish_origin(BaseMatrix<T> const& A, Options const& opts) {
         A.storage()->release_workspace();
 }
 
+/// Block-cyclic working copy of an arbitrary-distribution (lambda
+/// constructor) matrix or of a view of one: the drivers' contiguous local
+/// arrays need the 2-D block-cyclic layout, while the reference drivers
+/// consume any layout tile by tile.  Same processes; the largest tile of A
+/// becomes the uniform tile.  The copy is the tile-by-tile redistribution.
+template <typename T>
+Matrix<T> block_cyclic(BaseMatrix<T> const& A, Options const& opts) {
+    const int64_t b = std::max<int64_t>(1, std::max(A.storage()->mb, A.storage()->nb));
+    Matrix<T> B(A.m(), A.n(), b, b, A.grid());
+    B.insertLocalTiles(resolve_target(opts));
+    slate::copy<T, T>(A, B, opts);
+    return B;
+}
+/// A itself, or its block-cyclic copy when A has an arbitrary distribution
+template <typename T>
+Matrix<T> bc_operand(BaseMatrix<T> const& A, Options const& opts) {
+    return A.arbitrary_layout() ? block_cyclic(A, opts) : Matrix<T>(A);
+}
+
 /// Broadcast a contiguous buffer over `comm` from `root` (stream-ordered).
 template <typename T>
 inline void bcast(Comm& comm, T* buf, size_t count, int root, lb::Ctx const& c) {

@@ -32,6 +32,51 @@ MatrixStorage<T>::MatrixStorage(int64_t m_, int64_t n_, int64_t mb_, int64_t nb_
 }
 
 template <typename T>
+MatrixStorage<T>::MatrixStorage(int64_t m_, int64_t n_, std::function<int64_t(int64_t)> const& tile_mb,
+                                std::function<int64_t(int64_t)> const& tile_nb,
+                                std::function<int(int64_t, int64_t)> const& tile_rank, GridPtr g)
+    : m(m_), n(n_), mb(1), nb(1), grid(g), rsrc(0), csrc(0)
+{
+    slate_error_if_msg(m < 0 || n < 0, "negative matrix dimension");
+    auto L = std::make_shared<Layout>();
+    L->rs.push_back(0);
+    while (L->rs.back() < m) {
+        int64_t b = tile_mb(int64_t(L->rs.size()) - 1);
+        slate_error_if_msg(b <= 0, "tileMb must be positive");
+        L->rs.push_back(std::min(m, L->rs.back() + b));
+        mb = std::max(mb, b);
+    }
+    L->cs.push_back(0);
+    while (L->cs.back() < n) {
+        int64_t b = tile_nb(int64_t(L->cs.size()) - 1);
+        slate_error_if_msg(b <= 0, "tileNb must be positive");
+        L->cs.push_back(std::min(n, L->cs.back() + b));
+        nb = std::max(nb, b);
+    }
+    L->mt = int64_t(L->rs.size()) - 1;
+    L->nt = int64_t(L->cs.size()) - 1;
+    L->owner.resize(size_t(L->mt * L->nt));
+    L->toff.assign(size_t(L->mt * L->nt), -1);
+    int64_t off = 0;
+    const int me = g->rank();
+    for (int64_t j = 0; j < L->nt; ++j)
+        for (int64_t i = 0; i < L->mt; ++i) {
+            int r = tile_rank(i, j);
+            slate_error_if_msg(r < 0 || r >= g->size(), "tileRank out of range");
+            L->owner[i + j * L->mt] = r;
+            if (r == me) {
+                L->toff[i + j * L->mt] = off;
+                off += (L->rs[i + 1] - L->rs[i]) * (L->cs[j + 1] - L->cs[j]);
+            }
+        }
+    layout = L;
+    // the packed local tiles as one column (allocate / copy_instance unchanged)
+    mloc = off;
+    nloc = off > 0 ? 1 : 0;
+    lld = std::max<int64_t>(off, 1);
+}
+
+template <typename T>
 MatrixStorage<T>::~MatrixStorage() {
     if (host_owned_ && host_) std::free(host_);
     if (dev_owned_ && dev_) {
@@ -133,6 +178,8 @@ BaseMatrix<T> BaseMatrix<T>::sub(int64_t i1, int64_t i2, int64_t j1, int64_t j2)
     int64_t si1, si2, sj1, sj2;
     if (op_ == Op::NoTrans) { si1 = i1; si2 = i2; sj1 = j1; sj2 = j2; }
     else { si1 = j1; si2 = j2; sj1 = i1; sj2 = i2; }
+    slate_error_if_msg(storage_->general() && !(si1 == 0 && sj1 == 0 && si2 == smt() - 1 && sj2 == snt() - 1),
+                       "sub: views of an arbitrary-distribution matrix are whole-matrix only");
     BaseMatrix r = *this;
     // empty ranges allowed (i2 = i1 - 1)
     slate_error_if_msg(si1 < 0 || sj1 < 0 || si2 >= std::max<int64_t>(smt(), si1) ||
@@ -158,6 +205,8 @@ BaseMatrix<T> BaseMatrix<T>::slice(int64_t r1, int64_t r2, int64_t c1, int64_t c
     else { sr1 = c1; sr2 = c2; sc1 = r1; sc2 = r2; }
     slate_error_if_msg(sr1 < 0 || sc1 < 0 || sr2 >= m_ || sc2 >= n_ || sr2 < sr1 - 1 || sc2 < sc1 - 1,
                        "slice: index out of range");
+    slate_error_if_msg(storage_->general() && !(sr1 == 0 && sc1 == 0 && sr2 == m_ - 1 && sc2 == n_ - 1),
+                       "slice: views of an arbitrary-distribution matrix are whole-matrix only");
     BaseMatrix r = *this;
     r.r0_ = r0_ + sr1; r.m_ = sr2 - sr1 + 1;
     r.c0_ = c0_ + sc1; r.n_ = sc2 - sc1 + 1;
@@ -183,6 +232,9 @@ int64_t BaseMatrix<T>::lcol_end() const {
 
 template <typename T>
 LocalBlock<T> BaseMatrix<T>::local_raw(Loc loc) const {
+    slate_error_if_msg(storage_->general(),
+                       "arbitrary-distribution matrix: no block-cyclic local array (copy / redistribute it into a "
+                       "block-cyclic Matrix, as the drivers do)");
     LocalBlock<T> b;
     int64_t rb = lrow_begin(), re = lrow_end(), cb = lcol_begin(), ce = lcol_end();
     b.m = re - rb; b.n = ce - cb;
@@ -202,6 +254,17 @@ template <typename T>
 Tile<T> BaseMatrix<T>::tile(int64_t i, int64_t j, Loc loc) const {
     slate_error_if_msg(!tileIsLocal(i, j), "tile: not local");
     int64_t si, sj; to_storage(i, j, si, sj);
+    if (storage_->general()) {
+        auto const& L = *storage_->layout;
+        T* base = storage_->raw(loc);
+        slate_error_if_msg(!base, "tile: storage not allocated at location");
+        Tile<T> t;
+        t.mb = srow_size(si); t.nb = scol_size(sj); t.stride = std::max<int64_t>(t.mb, 1);
+        t.data = base + L.toff[si + sj * L.mt];
+        t.op = op_; t.uplo = uplo_physical();
+        t.device = loc == Loc::Host ? HostNum : 0;
+        return t;
+    }
     auto& g = *storage_->grid;
     int64_t gr = srow_start(si), gc = scol_start(sj);
     int64_t lr = g2l(gr, storage_->mb, g.p()), lc = g2l(gc, storage_->nb, g.q());

@@ -196,6 +196,12 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
 
 template <typename T>
 int64_t potrf(HermitianMatrix<T>& A_in, Options const& opts) {
+    if (A_in.arbitrary_layout()) {
+        HermitianMatrix<T> Ab(A_in.uplo(), internal::block_cyclic(A_in, opts));
+        int64_t info = potrf(Ab, opts);
+        slate::copy<T, T>(Ab, A_in, opts);
+        return info;
+    }
     trace::Block tb("potrf");
     internal::DriverScope ds_;
     Target target = internal::resolve_target(opts);

@@ -379,6 +379,12 @@ void unmqr_left(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Targe
 
 template <typename T>
 void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> Ab = internal::block_cyclic(A, opts);
+        geqrf(Ab, T_, opts);
+        slate::copy<T, T>(Ab, A, opts);
+        return;
+    }
     trace::Block tb("geqrf");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);

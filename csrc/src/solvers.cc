@@ -67,6 +67,13 @@ void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 int64_t gesv(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
+    if (A.arbitrary_layout() || B.arbitrary_layout()) {
+        Matrix<T> Ab = internal::block_cyclic(A, opts), Bb = internal::block_cyclic(B, opts);
+        int64_t info = gesv(Ab, pivots, Bb, opts);
+        slate::copy<T, T>(Ab, A, opts);
+        slate::copy<T, T>(Bb, B, opts);
+        return info;
+    }
     trace::Block tb("gesv");
     internal::DriverScope ds_;
     int64_t info = getrf(A, pivots, opts);
@@ -102,6 +109,14 @@ void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, Options const& opts) {
+    if (A.arbitrary_layout() || B.arbitrary_layout()) {
+        HermitianMatrix<T> Ab(A.uplo(), internal::block_cyclic(A, opts));
+        Matrix<T> Bb = internal::block_cyclic(B, opts);
+        int64_t info = posv(Ab, Bb, opts);
+        slate::copy<T, T>(Ab, A, opts);
+        slate::copy<T, T>(Bb, B, opts);
+        return info;
+    }
     trace::Block tb("posv");
     internal::DriverScope ds_;
     int64_t info = potrf(A, opts);

@@ -20,7 +20,7 @@ from . import _slate
 from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid, Job,  # noqa: F401
                     Matrix, HermitianMatrix, SymmetricMatrix, TriangularMatrix, TrapezoidMatrix,
                     BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general,
-                    from_numpy, to_numpy, empty_like, local_tensor, transpose, conj_transpose,
+                    from_numpy, to_numpy, matrix_layout, empty_like, local_tensor, transpose, conj_transpose,
                     version, suffix_of, dtype_of, opts, target_of)
 from .parallel import init_grid, choose_grid, TorchHostComm, current_grid, finalize  # noqa: F401
 from .models import *  # noqa: F401,F403

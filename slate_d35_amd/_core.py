@@ -132,6 +132,27 @@ def from_numpy(full: np.ndarray, nb=256, grid=None, target=None, dtype=None, mb=
     return A
 
 
+def matrix_layout(m, n, tile_mb, tile_nb, tile_rank, dtype=np.float64, grid=None, target=None):
+    """Matrix with an arbitrary distribution and non-uniform tiles (reference
+    Matrix(m, n, tileMb, tileNb, tileRank, tileDevice, comm)): tile_mb(i) /
+    tile_nb(j) give tile sizes (or lists), tile_rank(i, j) the owning world
+    rank (or an mt x nt list).  Drivers run on a block-cyclic copy."""
+    def sizes(f, total):
+        out, acc = [], 0
+        while acc < total:
+            b = int(f[len(out)] if not callable(f) else f(len(out)))
+            out.append(b)
+            acc += b
+        return out
+    rs, cs = sizes(tile_mb, m), sizes(tile_nb, n)
+    own = tile_rank if not callable(tile_rank) else [[int(tile_rank(i, j)) for j in range(len(cs))]
+                                                     for i in range(len(rs))]
+    cls = getattr(_slate, "Matrix_" + _SUFFIX[np.dtype(dtype)])
+    A = cls.with_layout(m, n, rs, cs, own, grid)
+    A.insertLocalTiles(target_of(target) if target is not None else Target.Host)
+    return A
+
+
 def to_numpy(A) -> np.ndarray:
     """Gather a distributed matrix (logical view) to a full numpy array on every rank."""
     return A.gather()

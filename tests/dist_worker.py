@@ -230,6 +230,45 @@ def case_band(tg, dt, nb):
             assert relerr(h @ x, b) < 100 * tol(dt), (kd, uplo)
 
 
+def case_layout(tg, dt, nb):
+    """Arbitrary distribution + non-uniform tiles (reference lambda
+    constructor): drivers on lambda-layout operands (block-cyclic working
+    copies), results read back through the tile-by-tile redistribution."""
+    P = int(os.environ.get("WORLD_SIZE", "1"))
+    n = 150
+    rs = [17, 40, 23, 31, 39]
+    cs = [33, 12, 50, 28, 27]
+    own = lambda i, j: (3 * i + j) % P
+    a = rnd(n, n, dt, 111)
+    bm = rnd(n, 40, dt, 112)
+
+    def lay(x, rows, cols):
+        L = s.matrix_layout(x.shape[0], x.shape[1], rows, cols, own, dtype=dt, target=tg)
+        s.copy(s.from_numpy(x, nb=nb, target=tg), L, target=tg)
+        return L
+
+    def back(L):
+        B = s.from_numpy(np.zeros((L.m, L.n), dt), nb=nb, target=tg)
+        s.copy(L, B, target=tg)
+        return s.to_numpy(B)
+    A = lay(a, rs, cs)
+    assert A.arbitrary_layout()
+    assert relerr(back(A), a) == 0
+    C = lay(np.zeros((n, 40), dt), rs, [40])
+    s.gemm(1.0, A, lay(bm, cs, [15, 25]), 0.0, C, target=tg)
+    assert relerr(back(C), a @ bm) < tol(dt)
+    assert abs(s.norm(s.Norm.One, A, target=tg) - np.linalg.norm(a, 1)) <= 1e-4 * np.linalg.norm(a, 1)
+    h = (a @ a.conj().T + n * np.eye(n)).astype(dt)
+    H = s.HermitianMatrix(s.Uplo.Lower, lay(h, rs, rs))
+    B = lay(bm, rs, [40])
+    assert s.posv(H, B, target=tg) == 0
+    assert relerr(h @ back(B), bm) < 10 * tol(dt)
+    G = lay(a + n * np.eye(n, dtype=dt), cs, rs)
+    B = lay(bm, cs, [20, 20])
+    info, _ = s.gesv(G, B, target=tg)
+    assert info == 0 and relerr((a + n * np.eye(n)) @ back(B), bm) < 10 * tol(dt)
+
+
 def case_potrf(tg, dt, nb):
     n = 200
     a = rnd(n, n, dt, 7)
