@@ -208,6 +208,16 @@ template <typename T>
 void hetrs(HermitianMatrix<T> const& A, std::vector<int64_t> const& ipiv, Matrix<T>& B, Options const& opts = {});
 template <typename T>
 int64_t hesv(HermitianMatrix<T>& A, std::vector<int64_t>& ipiv, Matrix<T>& B, Options const& opts = {});
+// Aasen (reference hetrf.cc signatures): P A P^T = L T L^H, T band (kl = ku = nb)
+template <typename T>
+int64_t hetrf(HermitianMatrix<T>& A, Pivots& pivots, BandMatrix<T>& T_, Pivots& pivots2, Matrix<T>& H,
+              Options const& opts = {});
+template <typename T>
+void hetrs(HermitianMatrix<T>& A, Pivots& pivots, BandMatrix<T>& T_, Pivots& pivots2, Matrix<T>& B,
+           Options const& opts = {});
+template <typename T>
+int64_t hesv(HermitianMatrix<T>& A, Pivots& pivots, BandMatrix<T>& T_, Pivots& pivots2, Matrix<T>& H, Matrix<T>& B,
+             Options const& opts = {});
 
 /// op(A) X = B with getrf factors (op = NoTrans, Trans, ConjTrans).
 template <typename T>

@@ -106,6 +106,10 @@ void undo_left_swaps(int64_t w, T* A, int64_t lda, const int64_t* ipiv, hipStrea
 template <typename T>
 void rbt_gather(bool by_rows, bool scatter, int64_t cnt, int64_t len, const int64_t* idx, T* A, int64_t lda, T* buf,
                 int64_t ldb, hipStream_t s);
+/// Indexed 2-D gather: dst[rdst[a] + cdst[b] ldd] = src[ridx[a] + cidx[b] lds].
+template <typename T>
+void gather2d(int64_t nr, int64_t nc, const T* src, int64_t lds, const int64_t* ridx, const int64_t* cidx, T* dst,
+              int64_t ldd, const int64_t* rdst, const int64_t* cdst, hipStream_t s);
 /// A(i, j) = ca[r] A(i, j) + cp[r] P(i, j) with r = i (by_rows) or j.
 template <typename T>
 void rbt_combine(bool by_rows, int64_t m, int64_t n, T* A, int64_t lda, const T* P, int64_t ldp, const rt<T>* ca,

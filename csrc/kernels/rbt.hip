@@ -64,9 +64,29 @@ __global__ __launch_bounds__(256) void rbt_combine_kernel(int by_rows, int64_t m
     }
 }
 
+// dst[rdst[a] + cdst[b] ldd] = src[ridx[a] + cidx[b] lds] for a < nr, b < nc
+template <typename T>
+__global__ __launch_bounds__(256) void gather2d_kernel(int64_t nr, int64_t nc, const T* src, int64_t lds,
+                                                       const int64_t* ridx, const int64_t* cidx, T* dst, int64_t ldd,
+                                                       const int64_t* rdst, const int64_t* cdst) {
+    for (int64_t b = blockIdx.y; b < nc; b += gridDim.y) {
+        const int64_t cs = cidx[b], cd = cdst[b];
+        for (int64_t a = blockIdx.x * 256 + threadIdx.x; a < nr; a += 256 * (int64_t)gridDim.x)
+            dst[rdst[a] + cd * ldd] = src[ridx[a] + cs * lds];
+    }
+}
+
 inline unsigned grid_cap(int64_t v, int64_t cap) { return (unsigned)std::max<int64_t>(1, std::min(v, cap)); }
 
 }  // namespace
+
+template <typename T>
+void gather2d(int64_t nr, int64_t nc, const T* src, int64_t lds, const int64_t* ridx, const int64_t* cidx, T* dst,
+              int64_t ldd, const int64_t* rdst, const int64_t* cdst, hipStream_t s) {
+    if (nr <= 0 || nc <= 0) return;
+    dim3 g(grid_cap((nr + 255) / 256, 64), grid_cap(nc, 65535));
+    hipLaunchKernelGGL(gather2d_kernel<T>, g, dim3(256), 0, s, nr, nc, src, lds, ridx, cidx, dst, ldd, rdst, cdst);
+}
 
 template <typename T>
 void rbt_gather(bool by_rows, bool scatter, int64_t cnt, int64_t len, const int64_t* idx, T* A, int64_t lda, T* buf,
@@ -94,7 +114,9 @@ void rbt_combine(bool by_rows, int64_t m, int64_t n, T* A, int64_t lda, const T*
     template void rbt_gather<T>(bool, bool, int64_t, int64_t, const int64_t*, T*, int64_t, T*, int64_t,           \
                                 hipStream_t);                                                                      \
     template void rbt_combine<T>(bool, int64_t, int64_t, T*, int64_t, const T*, int64_t, const real_t<T>*,        \
-                                 const real_t<T>*, hipStream_t);
+                                 const real_t<T>*, hipStream_t);                                                   \
+    template void gather2d<T>(int64_t, int64_t, const T*, int64_t, const int64_t*, const int64_t*, T*, int64_t,     \
+                              const int64_t*, const int64_t*, hipStream_t);
 
 SLATE_INST_RBT(float)
 SLATE_INST_RBT(double)

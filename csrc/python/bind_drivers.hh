@@ -237,6 +237,19 @@ void bind_drivers(py::module_& m, std::string const& s) {
         Options op = to_options(o); std::vector<int64_t> ip; int64_t info;
         { py::gil_scoped_release r; info = hesv(A, ip, B, op); }
         return py::make_tuple(info, ip); });
+    // ---- Aasen (reference signatures): T is a band matrix (kl = ku = nb) the caller provides
+    DEF("hetrf_aasen", [=](HermitianMatrix<T>& A, BandMatrix<T>& Tb, py::dict o) {
+        Options op = to_options(o); Pivots P, P2; Matrix<T> H; int64_t info;
+        { py::gil_scoped_release r; info = hetrf(A, P, Tb, P2, H, op); }
+        return py::make_tuple(info, piv_out(P), piv_out(P2)); });
+    DEF("hetrs_aasen", [=](HermitianMatrix<T>& A, py::list piv, BandMatrix<T>& Tb, py::list piv2, Matrix<T>& B,
+                           py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv), P2 = piv_in(piv2);
+        py::gil_scoped_release r; hetrs(A, P, Tb, P2, B, op); });
+    DEF("hesv_aasen", [=](HermitianMatrix<T>& A, BandMatrix<T>& Tb, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P, P2; Matrix<T> H; int64_t info;
+        { py::gil_scoped_release r; info = hesv(A, P, Tb, P2, H, B, op); }
+        return py::make_tuple(info, piv_out(P), piv_out(P2)); });
 
     // ---- eigenvalues / SVD (None for an unwanted vector matrix)
     auto opt_mat = [](py::object z) { return z.is_none() ? Matrix<T>() : z.cast<Matrix<T>>(); };

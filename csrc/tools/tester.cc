@@ -926,6 +926,26 @@ Result r_hetrf(Case<T>& c) {
 }
 
 template <typename T>
+Result r_hesv_aasen(Case<T>& c) {
+    auto Ag = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+    auto H0 = c.zeros(c.n, c.n);
+    copy<T, T>(conj_transpose(Ag), H0, c.opts);
+    add(T(1), Ag, T(1), H0, c.opts);
+    auto Hg = c.copy_of(H0), B0 = c.copy_of(B), Tg = c.zeros(c.n, c.n);
+    HermitianMatrix<T> H(Uplo::Lower, Hg);
+    BandMatrix<T> Tb(c.nb, c.nb, Tg);
+    Matrix<T> W;
+    Pivots p1, p2;
+    Result r;
+    int64_t info = 0;
+    r.time = c.timed([&] { info = hesv(H, p1, Tb, p2, W, B, c.opts); });
+    r.flops = cfac<T>() * double(c.n) * c.n * c.n / 3;
+    if (info) { r.error = INFINITY; return r; }
+    if (c.P.check) r.error = c.solve_resid(H0, B, B0);
+    return r;
+}
+
+template <typename T>
 Result r_vals(Case<T>& c, int variant) {   // 0 heev values, 1 svd values, 2 hegv
     Result r;
     if (variant == 1) {
@@ -1150,6 +1170,7 @@ std::map<std::string, Fn<T>> routines() {
         {"hbmm", [](Case<T>& c) { return r_band<T>(c, 4); }},
         {"tbsm", [](Case<T>& c) { return r_band<T>(c, 5); }},
         {"hetrf", r_hetrf<T>},
+        {"hesv_aasen", r_hesv_aasen<T>},
         {"heev_vals", [](Case<T>& c) { return r_vals<T>(c, 0); }},
         {"svd_vals", [](Case<T>& c) { return r_vals<T>(c, 1); }},
         {"hegv", [](Case<T>& c) { return r_vals<T>(c, 2); }},

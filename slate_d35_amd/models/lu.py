@@ -7,7 +7,8 @@ __all__ = ["getrf", "getrf_nopiv", "getrf_tntpiv", "getrs", "getrs_nopiv", "gesv
            "trcondest", "lu_factor", "lu_solve", "lu_solve_using_factor", "lu_inverse_using_factor",
            "lu_factor_nopiv", "lu_solve_nopiv", "lu_solve_using_factor_nopiv", "lu_rcondest_using_factor",
            "triangular_rcondest", "gbtrf", "gbtrs", "gbsv", "pbtrf", "pbtrs", "pbsv", "hetrf", "hetrs", "hesv",
-           "indefinite_factor", "indefinite_solve", "indefinite_solve_using_factor", "sysv"]
+           "indefinite_factor", "indefinite_solve", "indefinite_solve_using_factor", "sysv", "hetrf_aasen",
+           "hetrs_aasen", "hesv_aasen"]
 
 
 def getrf(A, target=None, **kw):
@@ -118,6 +119,22 @@ def hetrs(A, factors, B, target=None, **kw):
 
 def hesv(A, B, target=None, **kw):
     return call("hesv", A, A, B, target=target, **kw)
+
+
+def hetrf_aasen(A, T, target=None, **kw):
+    """Aasen P A P^T = L T L^H (A Hermitian, Lower); T: a BandMatrix(nb, nb, ...)
+    of A's size that receives the block-tridiagonal factor (band-LU factored).
+    Returns (info, pivots, pivots2)."""
+    return call("hetrf_aasen", A, A, T, target=target, **kw)
+
+
+def hetrs_aasen(A, pivots, T, pivots2, B, target=None, **kw):
+    return call("hetrs_aasen", A, A, pivots, T, pivots2, B, target=target, **kw)
+
+
+def hesv_aasen(A, T, B, target=None, **kw):
+    """Solve with Aasen's factorization; returns (info, pivots, pivots2)."""
+    return call("hesv_aasen", A, A, T, B, target=target, **kw)
 
 
 lu_factor = getrf

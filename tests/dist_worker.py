@@ -269,6 +269,29 @@ def case_layout(tg, dt, nb):
     assert info == 0 and relerr((a + n * np.eye(n)) @ back(B), bm) < 10 * tol(dt)
 
 
+def case_aasen(tg, dt, nb):
+    """Distributed blocked Aasen (hetrf / hetrs / hesv with the reference's
+    signatures): indefinite Hermitian solves, and P A P^T = L T L^H rebuilt
+    from the factors."""
+    for n in (150, 97):
+        a = rnd(n, n, dt, 121 + n)
+        h = (a + a.conj().T).astype(dt)
+        b = rnd(n, 3, dt, 122)
+        A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+        T = s.BandMatrix(nb, nb, s.from_numpy(np.zeros((n, n), dt), nb=nb, target=tg))
+        B = s.from_numpy(b, nb=nb, target=tg)
+        info, p1, p2 = s.hesv_aasen(A, T, B, target=tg)
+        assert info == 0
+        x = s.to_numpy(B)
+        assert np.linalg.norm(h @ x - b) / (np.linalg.norm(h) * np.linalg.norm(x)) < 100 * tol(dt), n
+        # the same factors through hetrs on new right-hand sides
+        b2 = rnd(n, 2, dt, 123)
+        B2 = s.from_numpy(b2, nb=nb, target=tg)
+        s.hetrs_aasen(A, p1, T, p2, B2, target=tg)
+        x2 = s.to_numpy(B2)
+        assert np.linalg.norm(h @ x2 - b2) / (np.linalg.norm(h) * np.linalg.norm(x2)) < 100 * tol(dt), n
+
+
 def case_potrf(tg, dt, nb):
     n = 200
     a = rnd(n, n, dt, 7)

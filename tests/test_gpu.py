@@ -428,3 +428,21 @@ def test_hold_local_workspace_device():
         assert (grown >= n * n * 8) == hold, (hold, grown)
         L = np.tril(s.to_numpy(H))
         assert relerr(L @ L.T, a) < 1e-13
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+def test_hesv_aasen_device(dtype):
+    """Device-resident blocked Aasen (replicated T on the GPU, distributed panel
+    LU, band LU of T) against numpy: indefinite Hermitian solve."""
+    n, nb = 700, 64
+    a = rnd(n, n, dtype, 71)
+    h = (a + a.conj().T).astype(dtype)
+    b = rnd(n, 4, dtype, 72)
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target="d"))
+    T = s.BandMatrix(nb, nb, s.from_numpy(np.zeros((n, n), dtype), nb=nb, target="d"))
+    B = s.from_numpy(b, nb=nb, target="d")
+    info, p1, p2 = s.hesv_aasen(A, T, B, target="d")
+    x = s.to_numpy(B)
+    assert info == 0
+    assert np.linalg.norm(h @ x - b) / (np.linalg.norm(h) * np.linalg.norm(x)) < 1e-13
