@@ -6,6 +6,7 @@ import ctypes as C
 import os
 import shutil
 import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -83,6 +84,15 @@ def test_fortran_example(tmp_path):
                     "-lslate_amd", f"-Wl,-rpath,{PKG}", "-o", str(exe)], check=True)
     r = subprocess.run([str(exe)], capture_output=True, text=True, env=ENV, timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
+
+
+def test_fortran_module_generated(tmp_path):
+    """The checked-in Fortran module matches the generator's output for c_api.h
+    (every C API function has an interface, all four precisions)."""
+    out = tmp_path / "gen.f90"
+    subprocess.run([sys.executable, f"{ROOT}/csrc/api/gen_fortran.py", str(out)], check=True, capture_output=True)
+    assert out.read_text() == open(f"{ROOT}/csrc/api/slate_c_api.f90").read()
+    assert out.read_text().count("bind(c, name=") >= 200
 
 
 def test_lapack_gesv_gemm_potrf(lapack):
