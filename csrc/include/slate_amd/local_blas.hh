@@ -51,6 +51,16 @@ template <typename T>
 void gemm(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
           T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc);
 
+/// Right-hand-side counts up to which gemm (n columns, op(B) = B) and Left
+/// trsm take the memory-bound gemv path on the device.
+constexpr int64_t kSkinnyRhs = 16;
+
+/// Y(m x nr) = alpha op(A) X + beta Y, op(A) m x k, X k x nr (device: gemv
+/// kernels, K-chunked with an in-order partial reduction).
+template <typename T>
+void gemv(Ctx const& c, Op opA, int64_t m, int64_t k, int64_t nr, T alpha, T const* A, int64_t lda, T const* X,
+          int64_t ldx, T beta, T* Y, int64_t ldy);
+
 /// Triangle-only gemm: C(uplo) = alpha op(A) op(B) + beta C(uplo), C n x n.
 template <typename T>
 void gemm_tri(Ctx const& c, Uplo uplo, Op opA, Op opB, int64_t n, int64_t k, T alpha,

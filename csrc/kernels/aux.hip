@@ -163,7 +163,7 @@ __global__ void transpose_kernel(bool conjugate, int64_t m, int64_t n, const T* 
 template <typename T>
 __global__ __launch_bounds__(64)
 void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
-                       const T* A, int64_t lda, T* W, int64_t ldw) {
+                       const T* A, int64_t lda, T* W, int64_t ldw, int64_t wrap) {
     __shared__ T L[64][64];
     __shared__ T rd[64];
     const int b = blockIdx.x;
@@ -171,7 +171,9 @@ void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
     const int nb = (int)min<int64_t>(nbs, n - off);
     const int lane = threadIdx.x;
     const T* Ab = A + off + off * lda;
-    T* Wb = W + off + off * ldw;
+    // wrap > 0: W is a stack of wrap x wrap blocks (block t at W + t wrap^2,
+    // ld = wrap), each holding the inverse of A's t-th diagonal wrap-block
+    T* Wb = wrap > 0 ? W + (off / wrap) * wrap * wrap + (off % wrap) * (1 + ldw) : W + off + off * ldw;
     const bool unit = (diag == 'U');
     const bool lower = (uplo == 'L');
     for (int j = 0; j < 64; ++j)
@@ -351,7 +353,14 @@ template <typename T>
 void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t ldw, hipStream_t s) {
     if (n <= 0) return;
     int nblk = (int)((n + nbs - 1) / nbs);
-    hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, ldw);
+    hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, ldw, int64_t(0));
+}
+
+template <typename T>
+void trtri_diag_stack(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t bs, hipStream_t s) {
+    if (n <= 0) return;
+    int nblk = (int)((n + nbs - 1) / nbs);
+    hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, bs, bs);
 }
 
 template <typename T>
@@ -386,6 +395,7 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void gescale<T>(char, int64_t, int64_t, real_t<T>, T*, int64_t, hipStream_t);                \
     template void gescale_row_col<T>(int64_t, int64_t, const real_t<T>*, const real_t<T>*, T*, int64_t, hipStream_t); \
     template void trtri_diag<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t);   \
+    template void trtri_diag_stack<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t); \
     template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \
     template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
     template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);  \

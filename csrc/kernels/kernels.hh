@@ -144,6 +144,19 @@ void gemm_cplx(char uplo, char transA, char transB, int64_t m, int64_t n, int64_
                T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
                T beta, T* C, int64_t ldc, hipStream_t stream);
 
+// ---- skinny products and batched diagonal-block inverse (skinny.hip)
+/// y(m x nr) = alpha op(A) x + beta y; trans 'N' (A m x k) or 'T' / 'C' (A k x m).
+/// P: partial buffer of chunks * m * min(nr, 16) scalars when chunks > 1.
+int gemv_chunks(char trans, int64_t m, int64_t k);
+template <typename T>
+void gemv(char trans, int64_t m, int64_t k, int nr, T alpha, const T* A, int64_t lda, const T* X, int64_t ldx,
+          T beta, T* Y, int64_t ldy, T* P, int chunks, hipStream_t s);
+/// inverses of the nblk full BS x BS diagonal blocks of A's uplo triangle
+/// into W (block t at W + t BS^2, ld BS); work: nblk * BS^2 / 2 scalars
+template <typename T>
+void trtri_blocks(char uplo, char diag, int64_t BS, int64_t nblk, const T* A, int64_t lda, T* W, T* work,
+                  hipStream_t s);
+
 // ---- aux (aux.hip)
 template <typename T>
 void geset(char uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda, hipStream_t s);
@@ -157,6 +170,9 @@ template <typename T>
 void gescale_row_col(int64_t m, int64_t n, const rt<T>* R, const rt<T>* C, T* A, int64_t lda, hipStream_t s);
 template <typename T>
 void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t ldw, hipStream_t s);
+/// trtri_diag into a stack of bs x bs blocks (block t at W + t bs^2, ld bs); bs % nbs == 0
+template <typename T>
+void trtri_diag_stack(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t bs, hipStream_t s);
 template <typename T>
 void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s);
 template <typename T>

@@ -165,7 +165,26 @@ void gemm(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha
         if (opA == Op::ConjTrans) opA = Op::Trans;
         if (opB == Op::ConjTrans) opB = Op::Trans;
     }
+    if (n <= kSkinnyRhs && opB == Op::NoTrans) {
+        // a few right-hand sides (residuals, refinement): memory-bound gemv
+        // instead of 128-wide MFMA tiles with n live columns
+        gemv(c, opA, m, k, n, alpha, A, lda, B, ldb, beta, C, ldc);
+        return;
+    }
     dgemm(c.stream, 'G', opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}
+
+template <typename T>
+void gemv(Ctx const& c, Op opA, int64_t m, int64_t k, int64_t nr, T alpha, T const* A, int64_t lda, T const* X,
+          int64_t ldx, T beta, T* Y, int64_t ldy) {
+    if (m <= 0 || nr <= 0) return;
+    if (!c.dev()) { host::gemm(opA, Op::NoTrans, m, nr, k, alpha, A, lda, X, ldx, beta, Y, ldy); return; }
+    const char tr = opA == Op::NoTrans ? 'N' : (opA == Op::Trans || is_real_v<T>) ? 'T' : 'C';
+    const int chunks = kd::gemv_chunks(tr, m, k);
+    Scratch sc(c);
+    T* P = chunks > 1 ? sc.alloc<T>(size_t(chunks) * m * std::min<int64_t>(nr, kSkinnyRhs)) : nullptr;
+    kd::gemv(tr, m, k, int(nr), dval(alpha), dptr(A), lda, dptr(X), ldx, dval(beta), dptr(Y), ldy, dptr(P), chunks,
+             c.stream);
 }
 
 template <typename T>
@@ -299,6 +318,50 @@ void trtri(Ctx const& c, Uplo uplo, Diag diag, int64_t n, T* A, int64_t lda) {
     kd::gecopy(upc(uplo), 'N', n, n, dptr(W), n, dptr(A), lda, c.stream);
 }
 
+/// Left triangular solve with a few right-hand sides (n <= kSkinnyRhs):
+/// every full BS x BS diagonal block inverted at once (batched doubling
+/// GEMMs), then per block one gemv with the inverse and one gemv update of
+/// the remaining rows -- about 5 launches per block instead of ~20 to
+/// re-invert each block, and no 128-wide MFMA tiles carrying n live columns.
+/// Returns false (caller falls back) for triangles shorter than two blocks.
+template <typename T>
+bool trsm_skinny(Ctx const& c, Uplo uplo, Op op, Diag diag, int64_t m, int64_t n, T const* A, int64_t lda, T* B,
+                 int64_t ldb) {
+    const int64_t BS = m >= 16384 ? 1024 : 512;
+    const int64_t nfull = m / BS, rem = m - nfull * BS;
+    if (nfull < 2) return false;
+    hipStream_t s = c.stream;
+    Scratch sc(c);
+    T* Dinv = sc.alloc<T>(size_t(nfull) * BS * BS + size_t(rem) * rem);
+    {
+        Scratch sw(c);
+        T* work = sw.alloc<T>(size_t(nfull) * BS * BS / 2);
+        kd::trtri_blocks<T>(upc(uplo), char(diag), BS, nfull, A, lda, Dinv, work, s);
+    }
+    T* Drem = Dinv + size_t(nfull) * BS * BS;
+    if (rem > 0) trtri_to(c, uplo, diag, rem, A + nfull * BS * (1 + lda), lda, Drem, rem);
+    T* X = sc.alloc<T>(size_t(BS) * n);
+    const bool lower_eff = (uplo == Uplo::Lower) == (op == Op::NoTrans);
+    const int64_t nblk = nfull + (rem > 0);
+    for (int64_t t = 0; t < nblk; ++t) {
+        const int64_t bi = lower_eff ? t : nblk - 1 - t;
+        const int64_t i0 = bi * BS, b = std::min(BS, m - i0);
+        T const* D = bi < nfull ? Dinv + size_t(bi) * BS * BS : Drem;
+        // x_t = op(A_tt)^{-1} b_t = op(A_tt^{-1}) b_t
+        dcopy(s, b, n, B + i0, ldb, X, b);
+        gemv(c, op, b, b, n, T(1), D, b, X, b, T(0), B + i0, ldb);
+        // b_rest -= op(A)(rest, t) x_t
+        const int64_t r0 = lower_eff ? i0 + b : 0, r1 = lower_eff ? m : i0;
+        if (r1 > r0) {
+            if (op == Op::NoTrans)
+                gemv(c, op, r1 - r0, b, n, T(-1), A + r0 + i0 * lda, lda, B + i0, ldb, T(1), B + r0, ldb);
+            else
+                gemv(c, op, r1 - r0, b, n, T(-1), A + i0 + r0 * lda, lda, B + i0, ldb, T(1), B + r0, ldb);
+        }
+    }
+    return true;
+}
+
 template <typename T>
 void trsm(Ctx const& c, Side side, Uplo uplo, Op op, Diag diag, int64_t m, int64_t n, T alpha,
           T const* A, int64_t lda, T* B, int64_t ldb) {
@@ -307,6 +370,9 @@ void trsm(Ctx const& c, Side side, Uplo uplo, Op op, Diag diag, int64_t m, int64
     if constexpr (is_real_v<T>) { if (op == Op::ConjTrans) op = Op::Trans; }
     hipStream_t s = c.stream;
     if (alpha != T(1)) kd::geadd('G', m, n, dval(alpha), dptr(B), ldb, dval(T(0)), dptr(B), ldb, s);
+    if constexpr (is_real_v<T>) {
+        if (side == Side::Left && n <= kSkinnyRhs && trsm_skinny(c, uplo, op, diag, m, n, A, lda, B, ldb)) return;
+    }
     const int64_t na = side == Side::Left ? m : n;
     const int64_t BS = 512;
     const bool lower_eff = (uplo == Uplo::Lower) == (op == Op::NoTrans);
@@ -889,6 +955,7 @@ void copy2d(Ctx const& c, int64_t m, int64_t n, T const* src, int64_t lds, T* ds
 #define SLATE_LB_INST(T)                                                                                   \
     template void gemm<T>(Ctx const&, Op, Op, int64_t, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
     template void gemm_tri<T>(Ctx const&, Uplo, Op, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
+    template void gemv<T>(Ctx const&, Op, int64_t, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
     template void herk<T>(Ctx const&, Uplo, Op, int64_t, int64_t, real_type<T>, T const*, int64_t, real_type<T>, T*, int64_t); \
     template void syrk<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T, T*, int64_t);  \
     template void her2k<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, real_type<T>, T*, int64_t); \

@@ -9,6 +9,7 @@
 #include <cmath>
 #include <chrono>
 #include <algorithm>
+#include <string>
 
 using namespace slate_amd::dev;
 
@@ -107,8 +108,41 @@ void timeit(char ta, char tb, int64_t n, int64_t k, int reps, int64_t pad = 0) {
     hipFree(A); hipFree(B); hipFree(C); hipFree(tmp);
 }
 
+// trailing-update shapes: general NT / NN and lower-triangle NT (syrk) at n x n x k
+void tri_sweep(int64_t n, int64_t k, int reps) {
+    double *A, *C;
+    CHECK(hipMalloc(&A, n * k * 8)); CHECK(hipMalloc(&C, n * n * 8));
+    fill<<<(n * k + 255) / 256, 256>>>(A, n * k, 7);
+    CHECK(hipMemset(C, 0, n * n * 8));
+    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    auto run = [&](const char* name, double flops, auto&& f) {
+        f(); CHECK(hipDeviceSynchronize());
+        hipEventRecord(e0);
+        for (int r = 0; r < reps; ++r) f();
+        hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        printf("%-10s n=%ld k=%ld : %.3f ms/call %.2f TFLOP/s\n", name, n, k, ms / reps, flops * reps / (ms * 1e-3) / 1e12);
+    };
+    const double full = 2.0 * n * n * k, half = double(n) * (n + 1) * k;
+    run("gemm_NT", full, [&] { gemm_real<double>('N', 'T', n, n, k, -1.0, A, n, 0, A, n, 0, 1.0, C, n, 0, 1, 0); });
+    run("tri_L_NT", half, [&] { gemm_tri_real<double>('L', 'N', 'T', n, k, -1.0, A, n, A, n, 1.0, C, n, 0); });
+    // B stored K-contiguous (the transposed panel copy): NN form
+    double* At; CHECK(hipMalloc(&At, n * k * 8));
+    fill<<<(n * k + 255) / 256, 256>>>(At, n * k, 8);
+    run("gemm_NN", full, [&] { gemm_real<double>('N', 'N', n, n, k, -1.0, A, n, 0, At, k, 0, 1.0, C, n, 0, 1, 0); });
+    run("tri_L_NN", half, [&] { gemm_tri_real<double>('L', 'N', 'N', n, k, -1.0, A, n, At, k, 1.0, C, n, 0); });
+    run("gemm_TN", full, [&] { gemm_real<double>('T', 'N', n, n, k, -1.0, At, k, 0, At, k, 0, 1.0, C, n, 0, 1, 0); });
+    run("tri_L_TN", half, [&] { gemm_tri_real<double>('L', 'T', 'N', n, k, -1.0, At, k, At, k, 1.0, C, n, 0); });
+    hipFree(A); hipFree(At); hipFree(C);
+}
+
 int main(int argc, char** argv) {
     const char ops[2] = {'N', 'T'};
+    if (argc > 1 && std::string(argv[1]) == "tri") {   // gemm_bench tri N K [reps]
+        int64_t N = atoll(argv[2]), K = atoll(argv[3]);
+        tri_sweep(N, K, argc > 4 ? atoi(argv[4]) : 3);
+        return 0;
+    }
     if (argc > 2) {   // gemm_bench N K pad [reps]: leading-dimension padding study only
         int64_t N = atoll(argv[1]), K = atoll(argv[2]), pad = argc > 3 ? atoll(argv[3]) : 0;
         int reps = argc > 4 ? atoi(argv[4]) : 1;

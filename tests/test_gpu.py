@@ -87,6 +87,53 @@ def test_trsm_kernel(dtype, side, uplo, op, diag):
     assert relerr(lhs, b) < 1e-10
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32, np.complex128])
+@pytest.mark.parametrize("ta", ["N", "T", "C"])
+@pytest.mark.parametrize("nr", [1, 3, 16])
+@pytest.mark.parametrize("mk", [(5000, 4099), (37, 20000)])
+def test_gemv_kernel(dtype, ta, nr, mk):
+    """Few-column gemm (n <= 16) takes the gemv kernels: row-per-lane NoTrans
+    and wave-per-row (conj-)transposed, K-chunked for short outputs."""
+    torch = _torch()
+    if ta == "C" and not np.iscomplexobj(np.zeros(1, dtype)):
+        ta = "T"
+    m, k = mk
+    a = rnd(m, k, dtype, 11) if ta == "N" else rnd(k, m, dtype, 11)
+    b = rnd(k, nr, dtype, 12)
+    c = rnd(m, nr, dtype, 13)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
+    alpha, beta = dtype(-1.0), dtype(0.75)
+    s.ops.gemm(ta, "N", alpha, tA, tB, beta, tC)
+    opa = a if ta == "N" else (a.T if ta == "T" else a.conj().T)
+    wide = np.complex128 if np.iscomplexobj(a) else np.float64
+    ref = alpha * opa.astype(wide) @ b.astype(wide) + beta * c
+    assert relerr(tC.cpu().numpy().T, ref) < tol(dtype)
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("uplo,op,diag", [("L", "N", "U"), ("U", "N", "N"), ("L", "T", "U"), ("U", "T", "N")])
+@pytest.mark.parametrize("m", [2500, 17000])
+def test_trsm_skinny_kernel(dtype, uplo, op, diag, m):
+    """Left trsm with few right-hand sides: batched inverse of the BS x BS
+    diagonal blocks (BS = 512 / 1024, remainder block separately) + gemv sweep."""
+    torch = _torch()
+    nr = 2
+    t = (rnd(m, m, dtype, 14) / np.sqrt(m) * 0.5 + 2 * np.eye(m)).astype(dtype)
+    t = np.tril(t) if uplo == "L" else np.triu(t)
+    te = t.astype(np.float64)
+    if diag == "U":
+        np.fill_diagonal(te, 1)
+    b = rnd(m, nr, dtype, 15)
+    tT = torch.from_numpy(np.ascontiguousarray(t.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    s.ops.trsm("L", uplo, op, diag, dtype(1), tT, tB)
+    x = tB.cpu().numpy().T.astype(np.float64)
+    ope = te if op == "N" else te.T
+    assert relerr(ope @ x, b) < (1e-12 if dtype == np.float64 else 2e-5)
+
+
 @pytest.mark.parametrize("n", [64, 200, 512, 1000])
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_potrf_kernel(n, uplo):
@@ -283,10 +330,11 @@ def test_getrf_driver_device(dtype, mn):
     assert info == 0 and relerr(L @ U, pa) < 10 * tol(dtype)
 
 
-def test_gesv_mixed_device():
-    n, nb = 1000, 128
+@pytest.mark.parametrize("n,nrhs", [(1000, 4), (5000, 1)])
+def test_gesv_mixed_device(n, nrhs):
+    nb = 128
     a = rnd(n, n, np.float64, 31)
-    b = rnd(n, 4, np.float64, 32)
+    b = rnd(n, nrhs, np.float64, 32)
     A, B = s.from_numpy(a, nb=nb, target="d"), s.from_numpy(b, nb=nb, target="d")
     X = s.from_numpy(np.zeros_like(b), nb=nb, target="d")
     info, piv, it = s.gesv_mixed(A, B, X, target="d")
