@@ -18,6 +18,10 @@ tester reports them.
 """
 from __future__ import annotations
 
+import time as _time
+
+_T_START = _time.time()   # wall clock of the whole run (the driver's limit counts from launch)
+
 import argparse
 import json
 import os
@@ -61,6 +65,11 @@ def parse():
     ap.add_argument("--extras", default="all", help="BASELINE configs to add after the suite: all, none, or names")
     ap.add_argument("--check", default="yes", choices=["yes", "no"],
                     help="backward-error check of each routine after its timed steps (outside the timed region)")
+    ap.add_argument("--extras-steps", type=int, default=2, help="timed steps per BASELINE extra config")
+    ap.add_argument("--extras-warmup", type=int, default=1, help="warmup steps per BASELINE extra config")
+    ap.add_argument("--time-budget", type=float, default=555.0,
+                    help="seconds since launch after which no further extra config is started (the driver "
+                         "allows 600 s per run; the headline suite itself always runs its K + W steps)")
     return ap.parse_args()
 
 
@@ -156,8 +165,12 @@ def main():
         del A0
         return err
 
-    def run(rname, n_, nb, tg, label):
-        """W untimed + K timed steps of one routine; returns its result dict."""
+    def run(rname, n_, nb, tg, label, warmup=None, steps=None, deadline=None):
+        """W untimed + K timed steps of one routine; returns its result dict.
+        With a deadline (extras only) the timed steps are cut to what fits
+        after the first step's duration is known (at least one)."""
+        warmup = a.warmup if warmup is None else warmup
+        steps = a.steps if steps is None else steps
         mats = {}
         tgt = s.target_of(tg)
         o = dict(target=tg, lookahead=a.lookahead)
@@ -187,12 +200,13 @@ def main():
         kind = "spd" if rname == "dpotrf" else "rands"
         times, extra = [], {}
         seed = 0
-        for step in range(a.warmup + a.steps):
+        step, total = 0, warmup + steps
+        while step < total:
             seed = 100 + step
             if rname != "dgemm":
                 s._slate.generate_matrix_d(kind, mats["A"], seed, -1.0, s.opts(tg))
             barrier_sync()
-            if a.trace and step == a.warmup:
+            if a.trace and step == warmup:
                 s.trace.on()
             t0 = time.perf_counter()
             if rname == "dgemm":
@@ -222,17 +236,24 @@ def main():
                     print(f"# dgesv_mixed iters={iters} phase ms: {tm}", file=sys.stderr, flush=True)
             barrier_sync()
             dt = time.perf_counter() - t0
-            if a.trace and step == a.warmup:
+            if a.trace and step == warmup:
                 s.trace.finish(grid.world, f"{a.trace}_{label}")
                 s.trace.off()
                 s.trace.clear()
-            if step >= a.warmup:
+            if step >= warmup:
                 times.append(dt)
             if rank == 0:
-                print(f"# {label} step {step} {'warm' if step < a.warmup else 'timed'}: {dt*1e3:.1f} ms "
+                print(f"# {label} step {step} {'warm' if step < warmup else 'timed'}: {dt*1e3:.1f} ms "
                       f"{flops/dt/1e12:.2f} TFLOP/s", file=sys.stderr, flush=True)
+            step += 1
+            if deadline is not None and step == 1:
+                # steps that still fit (same decision on every rank)
+                left = -max_over_ranks(-(deadline - (time.time() - _T_START)))
+                fit = int(left // (max_over_ranks(dt) * 1.15))
+                total = min(total, max(warmup + 1, step + fit))
         t = max_over_ranks(float(np.mean(times)))
-        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_}
+        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_,
+               "steps": len(times), "warmup": warmup}
         if a.check == "yes":
             err = residual(rname, mats, kind, seed, nb, n_, tg)
             res["backward_error"] = float(f"{err:.3e}")
@@ -251,6 +272,8 @@ def main():
         results[rname] = run(rname, n, nb_per.get(rname, a.nb), target, rname)
     configs = {}
     extras = list(EXTRAS) if a.extras == "all" else ([] if a.extras == "none" else a.extras.split(","))
+    # per-flop time of the slowest suite routine: first-step estimate for an extra
+    rate = max((r["ms"] / 1e3 / r["flops"] for r in results.values()), default=0.0)
     for name in extras:
         rname, n_, nb_, tg_ = EXTRAS[name]
         tg_ = tg_ or target
@@ -258,7 +281,19 @@ def main():
             continue   # config 1 is a one-process host-target plumbing check
         nb_ = nb_ or nb_per.get(rname, a.nb)
         n_ = n if n_ is None else (n // 2 if n_ == -2 else n_)
-        configs[name] = run(rname, n_, nb_, tg_, name)
+        fl = {"dgemm": F.gemm_flops(n_, n_, n_), "dpotrf": F.potrf_flops(n_), "dgeqrf": F.geqrf_flops(n_)}.get(
+            rname, F.getrf_flops(n_))
+        # the first step, its residual check and the matrix generation must fit
+        need = 2.5 * fl * rate + 5.0 if tg_ != "h" else 5.0
+        elapsed = max_over_ranks(time.time() - _T_START)
+        if elapsed + need > a.time_budget:
+            configs[name] = {"skipped": f"time budget: {elapsed:.0f} s elapsed, ~{need:.0f} s needed, "
+                                        f"budget {a.time_budget:.0f} s"}
+            if rank == 0:
+                print(f"# {name} skipped ({configs[name]['skipped']})", file=sys.stderr, flush=True)
+            continue
+        configs[name] = run(rname, n_, nb_, tg_, name, warmup=a.extras_warmup, steps=a.extras_steps,
+                            deadline=a.time_budget)
 
     tot_flops = sum(r["flops"] for r in results.values())
     tot_t = sum(r["ms"] for r in results.values()) / 1e3
@@ -288,6 +323,7 @@ def main():
                          for kk, vv in v.items() if kk != "flops"} for k, v in results.items()},
         "configs": {k: {kk: (round(vv, 4) if isinstance(vv, float) and kk != "backward_error" else vv)
                         for kk, vv in v.items() if kk != "flops"} for k, v in configs.items()},
+        "wall_s": round(time.time() - _T_START, 1),
     }
     if rank == 0:
         print(json.dumps(line), flush=True)
