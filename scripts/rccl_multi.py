@@ -16,16 +16,22 @@ with socket.socket() as s:
     port = s.getsockname()[1]
 env0 = {k: v for k, v in os.environ.items() if k != "SLATE_COMM"}
 procs = []
+# every rank writes straight to its own file (progress stays visible during long runs)
+logdir = os.environ.get("RANK_LOGDIR", os.path.join(ROOT, "gpurun_out", "ranks"))
+os.makedirs(logdir, exist_ok=True)
+files = [open(os.path.join(logdir, f"rank{r}.log"), "w+") for r in range(n)]
 for r in range(n):
     env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(port), SLATE_MASTER_PORT=str(port), NCCL_HOSTID=f"slate-fake-host-{r}",
                NCCL_SOCKET_IFNAME="lo", NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"), OMP_NUM_THREADS="2")
-    procs.append(subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=subprocess.STDOUT, text=True, env=env))
+    procs.append(subprocess.Popen(cmd, stdout=files[r], stderr=subprocess.STDOUT, text=True, env=env))
 outs, codes = [], []
 try:
-    for p in procs:
-        outs.append(p.communicate(timeout=int(os.environ.get("RANK_TIMEOUT", "300")))[0])
+    for r, p in enumerate(procs):
+        p.wait(timeout=int(os.environ.get("RANK_TIMEOUT", "300")))
         codes.append(p.returncode)
+        files[r].seek(0)
+        outs.append(files[r].read())
 finally:
     for p in procs:
         if p.poll() is None:
