@@ -51,6 +51,14 @@ template <typename T>
 void gemm(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
           T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc);
 
+/// gemm as `splits` K-slices in one batched launch + in-order reduction of the
+/// partials (real device types; otherwise plain gemm).  For short-wide
+/// outputs with a long K (QR's W = V^H C): every workgroup stays short and the
+/// slices fill the waves a handful of output tiles would leave idle.
+template <typename T>
+void gemm_splitk(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, int64_t splits, T alpha,
+                 T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc);
+
 /// Right-hand-side counts up to which gemm (n columns, op(B) = B) and Left
 /// trsm take the memory-bound gemv path on the device.
 constexpr int64_t kSkinnyRhs = 16;

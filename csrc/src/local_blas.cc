@@ -94,6 +94,28 @@ inline char upc(Uplo u) { return char(u); }
 
 template <typename T> constexpr bool is_real_v = !is_complex_v<T>;
 
+// C = alpha op(A) op(B) + beta C as `splits` K-slices of one batched MFMA
+// launch into partials P, then one in-order reduction (deterministic)
+template <typename T>
+void dgemm_splitk(hipStream_t s, char ta, char tb, int64_t m, int64_t n, int64_t k, int64_t splits, T alpha,
+                  T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    int64_t kc = roundup(ceildiv(k, splits), 16);
+    splits = ceildiv(k, kc);
+    int64_t full = k / kc;                 // chunks of exactly kc
+    Scratch sc(Ctx{Target::Devices, s});
+    T* P = sc.alloc<T>(size_t(splits) * m * n);
+    int64_t sA = (ta == 'N') ? kc * lda : kc;
+    int64_t sB = (tb == 'N') ? kc : kc * ldb;
+    if (full > 0)
+        kd::gemm_real<T>(ta, tb, m, n, kc, T(1), A, lda, sA, B, ldb, sB, T(0), P, m, m * n, full, s);
+    if (full < splits) {
+        int64_t krem = k - full * kc;
+        kd::gemm_real<T>(ta, tb, m, n, krem, T(1), A + full * sA, lda, 0, B + full * sB, ldb, 0,
+                         T(0), P + full * m * n, m, 0, 1, s);
+    }
+    kd::splitk_reduce<T>(m, n, int(splits), P, alpha, beta, C, ldc, s);
+}
+
 // device gemm dispatch (real -> MFMA, complex -> complex kernel)
 template <typename T>
 void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
@@ -111,27 +133,26 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
             // about 2 workgroups per CU in total and at most 64 partial
             // products, so the reduction stays a short streaming pass
             int64_t splits = std::min<int64_t>({ceildiv(k, 256), std::max<int64_t>(2, 512 / tiles), int64_t(64)});
-            int64_t kc = roundup(ceildiv(k, splits), 16);
-            splits = ceildiv(k, kc);
-            int64_t full = k / kc;                 // chunks of exactly kc
-            Scratch sc(Ctx{Target::Devices, s});
-            T* P = sc.alloc<T>(size_t(splits) * m * n);
-            int64_t sA = (ta == 'N') ? kc * lda : kc;
-            int64_t sB = (tb == 'N') ? kc : kc * ldb;
-            if (full > 0)
-                kd::gemm_real<T>(ta, tb, m, n, kc, T(1), A, lda, sA, B, ldb, sB, T(0), P, m, m * n, full, s);
-            if (full < splits) {
-                int64_t krem = k - full * kc;
-                kd::gemm_real<T>(ta, tb, m, n, krem, T(1), A + full * sA, lda, 0, B + full * sB, ldb, 0,
-                                 T(0), P + full * m * n, m, 0, 1, s);
-            }
-            kd::splitk_reduce<T>(m, n, int(splits), P, alpha, beta, C, ldc, s);
+            dgemm_splitk(s, ta, tb, m, n, k, splits, alpha, A, lda, B, ldb, beta, C, ldc);
             return;
         }
-        if (uplo == 'G') kd::gemm_real<T>(ta, tb, m, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1, s);
-        else {
-            slate_assert(m == n);
-            kd::gemm_tri_real<T>(uplo, ta, tb, n, k, alpha, A, lda, B, ldb, beta, C, ldc, s);
+        // K-chunked launches for large updates (SLATE_GEMM_KCHUNK): shorter
+        // workgroups free CU slots for the high-priority panel queue sooner
+        static const int64_t kchunk = [] {
+            const char* e = std::getenv("SLATE_GEMM_KCHUNK");
+            return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
+        }();
+        const bool chunk = kchunk > 0 && k > kchunk && m * n >= int64_t(4096) * 4096;
+        for (int64_t k0 = 0; k0 < k; k0 += chunk ? kchunk : k) {
+            const int64_t kk = chunk ? std::min(kchunk, k - k0) : k;
+            T const* Ak = A + (ta == 'N' ? k0 * lda : k0);
+            T const* Bk = B + (tb == 'N' ? k0 : k0 * ldb);
+            const T bk = k0 == 0 ? beta : T(1);
+            if (uplo == 'G') kd::gemm_real<T>(ta, tb, m, n, kk, alpha, Ak, lda, 0, Bk, ldb, 0, bk, C, ldc, 0, 1, s);
+            else {
+                slate_assert(m == n);
+                kd::gemm_tri_real<T>(uplo, ta, tb, n, kk, alpha, Ak, lda, Bk, ldb, bk, C, ldc, s);
+            }
         }
     } else {
         kd::gemm_cplx(uplo, opc(opA), opc(opB), m, n, k, dval(alpha), dptr(A), lda, dptr(B), ldb,
@@ -172,6 +193,20 @@ void gemm(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha
         return;
     }
     dgemm(c.stream, 'G', opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
+}
+
+template <typename T>
+void gemm_splitk(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, int64_t splits, T alpha,
+                 T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc) {
+    if (m <= 0 || n <= 0) return;
+    if constexpr (is_real_v<T>) {
+        if (c.dev() && splits > 1 && k >= 2 * splits) {
+            dgemm_splitk(c.stream, opA == Op::NoTrans ? 'N' : 'T', opB == Op::NoTrans ? 'N' : 'T', m, n, k, splits,
+                         alpha, A, lda, B, ldb, beta, C, ldc);
+            return;
+        }
+    }
+    gemm(c, opA, opB, m, n, k, alpha, A, lda, B, ldb, beta, C, ldc);
 }
 
 template <typename T>
@@ -956,6 +991,7 @@ void copy2d(Ctx const& c, int64_t m, int64_t n, T const* src, int64_t lds, T* ds
     template void gemm<T>(Ctx const&, Op, Op, int64_t, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
     template void gemm_tri<T>(Ctx const&, Uplo, Op, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
     template void gemv<T>(Ctx const&, Op, int64_t, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
+    template void gemm_splitk<T>(Ctx const&, Op, Op, int64_t, int64_t, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, T, T*, int64_t); \
     template void herk<T>(Ctx const&, Uplo, Op, int64_t, int64_t, real_type<T>, T const*, int64_t, real_type<T>, T*, int64_t); \
     template void syrk<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T, T*, int64_t);  \
     template void her2k<T>(Ctx const&, Uplo, Op, int64_t, int64_t, T, T const*, int64_t, T const*, int64_t, real_type<T>, T*, int64_t); \

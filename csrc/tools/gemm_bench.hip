@@ -136,8 +136,50 @@ void tri_sweep(int64_t n, int64_t k, int reps) {
     hipFree(A); hipFree(At); hipFree(C);
 }
 
+// QR trailing-update product W = V^T C (nb x n, K = m): one launch, K-chunked
+// launches with beta accumulation, and batched split-K + in-order reduce
+void vhc_sweep(int64_t nb, int64_t n, int64_t m, int reps) {
+    double *V, *C, *W, *P;
+    CHECK(hipMalloc(&V, m * nb * 8)); CHECK(hipMalloc(&C, m * n * 8)); CHECK(hipMalloc(&W, nb * n * 8));
+    CHECK(hipMalloc(&P, 16 * nb * n * 8));
+    fill<<<(m * nb + 255) / 256, 256>>>(V, m * nb, 3);
+    fill<<<(m * n + 255) / 256, 256>>>(C, m * n, 4);
+    hipEvent_t e0, e1; hipEventCreate(&e0); hipEventCreate(&e1);
+    auto run = [&](const char* name, auto&& f) {
+        f(); CHECK(hipDeviceSynchronize());
+        hipEventRecord(e0);
+        for (int r = 0; r < reps; ++r) f();
+        hipEventRecord(e1); hipEventSynchronize(e1);
+        float ms; hipEventElapsedTime(&ms, e0, e1);
+        printf("%-14s nb=%ld n=%ld m=%ld : %.3f ms/call %.2f TFLOP/s\n", name, nb, n, m, ms / reps,
+               2.0 * nb * n * m * reps / (ms * 1e-3) / 1e12);
+    };
+    run("one_launch", [&] { gemm_real<double>('T', 'N', nb, n, m, 1.0, V, m, 0, C, m, 0, 0.0, W, nb, 0, 1, 0); });
+    for (int64_t kch : {int64_t(8192), int64_t(4096)}) {
+        char name[32]; snprintf(name, sizeof name, "kchunk_%ld", kch);
+        run(name, [&] {
+            for (int64_t r0 = 0; r0 < m; r0 += kch)
+                gemm_real<double>('T', 'N', nb, n, std::min(kch, m - r0), 1.0, V + r0, m, 0, C + r0, m, 0,
+                                  r0 ? 1.0 : 0.0, W, nb, 0, 1, 0);
+        });
+    }
+    for (int S : {2, 4, 8, 16}) {
+        int64_t kc = (m + S - 1) / S;
+        char name[32]; snprintf(name, sizeof name, "splitk_%d", S);
+        run(name, [&] {
+            gemm_real<double>('T', 'N', nb, n, kc, 1.0, V, m, kc, C, m, kc, 0.0, P, nb, nb * n, S, 0);
+            splitk_reduce<double>(nb, n, S, P, 1.0, 0.0, W, nb, 0);
+        });
+    }
+    hipFree(V); hipFree(C); hipFree(W); hipFree(P);
+}
+
 int main(int argc, char** argv) {
     const char ops[2] = {'N', 'T'};
+    if (argc > 1 && std::string(argv[1]) == "vhc") {   // gemm_bench vhc NB N M [reps]
+        vhc_sweep(atoll(argv[2]), atoll(argv[3]), atoll(argv[4]), argc > 5 ? atoi(argv[5]) : 3);
+        return 0;
+    }
     if (argc > 1 && std::string(argv[1]) == "tri") {   // gemm_bench tri N K [reps]
         int64_t N = atoll(argv[2]), K = atoll(argv[3]);
         tri_sweep(N, K, argc > 4 ? atoi(argv[4]) : 3);
