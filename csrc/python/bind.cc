@@ -298,9 +298,13 @@ void bind_type(py::module_& m, const char* sfx) {
         .def(py::init<Uplo, BaseMatrix<T> const&>())
         .def("conj_transpose", [](HermitianMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<BandMatrix<T>, BaseMatrix<T>>(m, ("BandMatrix_" + s).c_str())
-        .def(py::init<int64_t, int64_t, BaseMatrix<T> const&>());
+        .def(py::init<int64_t, int64_t, BaseMatrix<T> const&>())
+        .def("transpose", [](BandMatrix<T> const& A) { return transpose(A); })
+        .def("conj_transpose", [](BandMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<TriangularBandMatrix<T>, BaseMatrix<T>>(m, ("TriangularBandMatrix_" + s).c_str())
-        .def(py::init<Uplo, Diag, int64_t, BaseMatrix<T> const&>());
+        .def(py::init<Uplo, Diag, int64_t, BaseMatrix<T> const&>())
+        .def("transpose", [](TriangularBandMatrix<T> const& A) { return transpose(A); })
+        .def("conj_transpose", [](TriangularBandMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<HermitianBandMatrix<T>, BaseMatrix<T>>(m, ("HermitianBandMatrix_" + s).c_str())
         .def(py::init<Uplo, int64_t, BaseMatrix<T> const&>());
 

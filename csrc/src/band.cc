@@ -166,26 +166,6 @@ int64_t pbtf2(int64_t n, int64_t kd, T* ab, int64_t ldab) {
     return 0;
 }
 
-template <typename T>
-void pbtrs_host(int64_t n, int64_t kd, int64_t nrhs, T const* ab, int64_t ldab, T* b, int64_t ldb) {
-    auto L = [&](int64_t i, int64_t j) { return ab[(i - j) + j * ldab]; };
-    #pragma omp parallel for schedule(static) if (nrhs > 1)
-    for (int64_t c = 0; c < nrhs; ++c) {
-        T* x = b + c * ldb;
-        for (int64_t j = 0; j < n; ++j) {
-            x[j] /= L(j, j);
-            int64_t kn = std::min(kd, n - 1 - j);
-            for (int64_t i = 1; i <= kn; ++i) x[j + i] -= L(j + i, j) * x[j];
-        }
-        for (int64_t j = n - 1; j >= 0; --j) {
-            int64_t kn = std::min(kd, n - 1 - j);
-            T s = x[j];
-            for (int64_t i = 1; i <= kn; ++i) s -= slate::conj(L(j + i, j)) * x[j + i];
-            x[j] = s / slate::conj(L(j, j));
-        }
-    }
-}
-
 /// Dense block-column slabs of a band matrix distributed 1-D over the world
 /// (block column J on rank J % P): rows [J nb - top, J nb + nb + bot) of the
 /// block column, H = top + nb + bot rows, zero outside the band.
@@ -425,44 +405,6 @@ std::vector<int64_t> ipiv_from_pivots(BaseMatrix<T> const& A, Pivots const& pivo
     return ipiv;
 }
 
-/// General copy of a band matrix with out-of-band entries zeroed.
-template <typename T>
-Matrix<T> band_dense(BaseMatrix<T> const& A, int64_t kl, int64_t ku, Options const& opts, bool herm = false,
-                     Uplo uplo = Uplo::General) {
-    Target target = resolve_target(opts);
-    Matrix<T> G(A);
-    G.set_uplo(Uplo::General);
-    Matrix<T> D = G.emptyLike();
-    D.insertLocalTiles(Target::Host);
-    Options oh = {{Option::Target, Target::Host}};
-    slate::copy<T, T>(G, D, oh);
-    if (herm) {
-        // Hermitian band stored in one triangle: mirror it
-        Matrix<T> Dh = D.emptyLike();
-        Dh.insertLocalTiles(Target::Host);
-        slate::copy<T, T>(conj_transpose(D), Dh, oh);
-        D.storage()->get(Loc::Host, true);
-        // combine: D(i,j) = stored-triangle value, other triangle from Dh
-        LocalBlock<T> ld = D.local_raw(Loc::Host), lh = Dh.local_raw(Loc::Host);
-        auto& s = *D.storage();
-        for (int64_t jl = 0; jl < ld.n; ++jl) {
-            int64_t gc = l2g(D.lcol_begin() + jl, s.nb, s.crel(), s.grid->q()) - D.col0();
-            for (int64_t il = 0; il < ld.m; ++il) {
-                int64_t gr = l2g(D.lrow_begin() + il, s.mb, s.rrel(), s.grid->p()) - D.row0();
-                bool stored = (uplo == Uplo::Lower) ? gr >= gc : gr <= gc;
-                T v = stored ? ld.ptr[il + jl * ld.ld] : lh.ptr[il + jl * lh.ld];
-                if (gr == gc) v = T(std::real(v));
-                ld.ptr[il + jl * ld.ld] = v;
-            }
-        }
-    }
-    for_each_local(D, true, [&](int64_t i, int64_t j, T& v) {
-        if (i - j > kl || j - i > ku) v = T(0);
-    });
-    if (target == Target::Devices) D.insertLocalTiles(Target::Devices);
-    return D;
-}
-
 }  // namespace
 
 //------------------------------------------------------------------------------
@@ -540,13 +482,17 @@ template <typename T>
 void pbtrs(HermitianBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("pbtrs");
     internal::DriverScope ds_;
-    const int64_t n = A.n(), kd = A.bandwidth();
-    const bool upper = A.uplo() == Uplo::Upper;
-    std::vector<T> ab = upper ? gather_band<T>(A, 0, kd, 0, kd + 1, true) : gather_band<T>(A, kd, 0, 0, kd + 1);
-    std::vector<T> b = gather_dense(B, opts);
-    pbtrs_host<T>(n, kd, B.n(), ab.data(), kd + 1, b.data(), n);
-    scatter_dense(B, b, n);
-    if (resolve_target(opts) == Target::Devices) B.storage()->get(Loc::Device, false);
+    // two distributed band triangular solves with the factor (reference
+    // src/pbtrs.cc): A = L L^H (Lower) or U^H U (Upper)
+    const Uplo u = A.uplo();
+    TriangularBandMatrix<T> F(u, Diag::NonUnit, A.bandwidth(), BaseMatrix<T>(A));
+    if (u == Uplo::Lower) {
+        tbsm(Side::Left, T(1), F, B, opts);
+        tbsm(Side::Left, T(1), conj_transpose(F), B, opts);
+    } else {
+        tbsm(Side::Left, T(1), conj_transpose(F), B, opts);
+        tbsm(Side::Left, T(1), F, B, opts);
+    }
 }
 
 template <typename T>
@@ -559,12 +505,172 @@ int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, Options const& opts) {
 }
 
 //------------------------------------------------------------------------------
+// Band BLAS (reference src/gbmm.cc, hbmm.cc, tbsm.cc, work on the tiles inside
+// the band only).  Here the band is walked in chunks of block columns: each
+// chunk's band part -- at most (chunk + bandwidth) x chunk elements, entries
+// outside the band zeroed -- is copied out of the storage and applied with one
+// distributed GEMM / TRSM on the sub-views of B and C it touches.  Flops are
+// O(n * bandwidth * nrhs) and the temporaries O(nb * bandwidth) per chunk, not
+// the dense product's O(n^2 * nrhs) / O(n^2).
+namespace {
+
+template <typename T>
+int64_t row_off(BaseMatrix<T> const& A, int64_t i) {
+    int64_t o = 0;
+    for (int64_t t = 0; t < i; ++t) o += A.tileMb(t);
+    return o;
+}
+
+template <typename T>
+int64_t col_off(BaseMatrix<T> const& A, int64_t j) {
+    int64_t o = 0;
+    for (int64_t t = 0; t < j; ++t) o += A.tileNb(t);
+    return o;
+}
+
+/// logical tile row holding element row r (0 <= r < m)
+template <typename T>
+int64_t tile_row_of(BaseMatrix<T> const& A, int64_t r) {
+    int64_t o = 0;
+    for (int64_t t = 0; t < A.mt(); ++t) {
+        o += A.tileMb(t);
+        if (r < o) return t;
+    }
+    return A.mt() - 1;
+}
+
+template <typename T>
+int64_t tile_col_of(BaseMatrix<T> const& A, int64_t c) {
+    int64_t o = 0;
+    for (int64_t t = 0; t < A.nt(); ++t) {
+        o += A.tileNb(t);
+        if (c < o) return t;
+    }
+    return A.nt() - 1;
+}
+
+/// Copy of the tiles [i0..i1] x [k0..k1] of the physical (NoTrans) band
+/// storage Ap keeping only dmin <= i - j <= dmax (global element indices of
+/// Ap); real_diag drops the imaginary part on the diagonal (Hermitian band).
+/// Same distribution as the sub-view, O(chunk) storage.
+template <typename T>
+Matrix<T> band_chunk(BaseMatrix<T> const& Ap, int64_t i0, int64_t i1, int64_t k0, int64_t k1, int64_t dmin,
+                     int64_t dmax, bool real_diag, Target target) {
+    Matrix<T> S(Ap.sub(i0, i1, k0, k1));
+    S.set_uplo(Uplo::General);
+    Matrix<T> D = S.emptyLike();
+    D.insertLocalTiles(Target::Host);
+    Options oh = {{Option::Target, Target::Host}};
+    slate::copy<T, T>(S, D, oh);
+    const int64_t ro = row_off(Ap, i0), co = col_off(Ap, k0);
+    for_each_local(D, true, [&](int64_t i, int64_t j, T& v) {
+        const int64_t d = (ro + i) - (co + j);
+        if (d < dmin || d > dmax) v = T(0);
+        else if (real_diag && d == 0) v = T(std::real(v));
+    });
+    if (target == Target::Devices) D.insertLocalTiles(Target::Devices);
+    return D;
+}
+
+template <typename T>
+Matrix<T> op_view(Op op, Matrix<T> const& D) {
+    if (op == Op::NoTrans) return D;
+    return op == Op::Trans ? transpose(D) : conj_transpose(D);
+}
+
+/// Physical (NoTrans) view of a possibly transposed band operand.
+template <typename T>
+BaseMatrix<T> physical(BaseMatrix<T> const& A) {
+    return A.op() == Op::NoTrans ? A : A.transpose_view(A.op() == Op::ConjTrans);
+}
+
+/// C = beta C (beta = 0 writes zeros, so NaNs in C do not propagate)
+template <typename T>
+void scale_by(T beta, Matrix<T>& C, Options const& opts) {
+    if (beta == T(1)) return;
+    if (beta == T(0)) slate::set(T(0), T(0), C, opts);
+    else slate::add(beta, C, T(0), C, opts);
+}
+
+/// C += alpha op(A) B (Left) or alpha B op(A) (Right), A the band part
+/// dmin <= i - j <= dmax of the physical storage Ap, applied block-column
+/// chunk by chunk of Ap.
+template <typename T>
+void band_apply(Side side, Op op, T alpha, BaseMatrix<T> const& Ap, int64_t dmin, int64_t dmax, bool real_diag,
+                Matrix<T> const& B, Matrix<T>& C, Options const& opts) {
+    const Target target = resolve_target(opts);
+    const int64_t m = Ap.m(), nt = Ap.nt(), nb = std::max<int64_t>(1, Ap.nb());
+    const int64_t kc = std::max<int64_t>(1, ceildiv(std::max<int64_t>(-dmin, 0) + std::max<int64_t>(dmax, 0), nb));
+    for (int64_t k0 = 0; k0 < nt; k0 += kc) {
+        const int64_t k1 = std::min(nt - 1, k0 + kc - 1);
+        const int64_t c0 = col_off(Ap, k0), c1 = col_off(Ap, k1) + Ap.tileNb(k1) - 1;
+        const int64_t r_lo = std::max<int64_t>(0, c0 + dmin), r_hi = std::min(m - 1, c1 + dmax);
+        if (r_lo > r_hi) continue;
+        const int64_t i0 = tile_row_of(Ap, r_lo), i1 = tile_row_of(Ap, r_hi);
+        Matrix<T> D = op_view(op, band_chunk(Ap, i0, i1, k0, k1, dmin, dmax, real_diag, target));
+        // tile ranges of op(A)'s chunk: rows [a0..a1] x cols [b0..b1]
+        const int64_t a0 = op == Op::NoTrans ? i0 : k0, a1 = op == Op::NoTrans ? i1 : k1;
+        const int64_t b0 = op == Op::NoTrans ? k0 : i0, b1 = op == Op::NoTrans ? k1 : i1;
+        if (side == Side::Left) {
+            Matrix<T> Cs = C.sub(a0, a1, 0, C.nt() - 1);
+            gemm(alpha, D, B.sub(b0, b1, 0, B.nt() - 1), T(1), Cs, opts);
+        } else {
+            Matrix<T> Cs = C.sub(0, C.mt() - 1, b0, b1);
+            gemm(alpha, B.sub(0, B.mt() - 1, a0, a1), D, T(1), Cs, opts);
+        }
+    }
+}
+
+/// op(A) X = B (B overwritten) for a triangular band A, by a blocked
+/// substitution over chunks of ~kd columns: a TRSM with the chunk's diagonal
+/// triangle, then one GEMM with the band block that couples it to the next
+/// rows (reference src/tbsm.cc / work_trsm's band form).
+template <typename T>
+void tbsm_left(Op op, BaseMatrix<T> const& Ap, Uplo u, Diag diag, int64_t kd, Matrix<T>& B, Options const& opts) {
+    const Target target = resolve_target(opts);
+    const int64_t nt = Ap.nt(), n = Ap.n(), nb = std::max<int64_t>(1, Ap.nb());
+    const int64_t kc = std::max<int64_t>(1, ceildiv(kd, nb));
+    const int64_t dmin = u == Uplo::Lower ? 0 : -kd, dmax = u == Uplo::Lower ? kd : 0;
+    const bool forward = (u == Uplo::Lower) == (op == Op::NoTrans);
+    // op(A)'s band block rows [r0..r1] x cols [c0..c1] (tiles)
+    auto block = [&](int64_t r0, int64_t r1, int64_t c0, int64_t c1) {
+        return op == Op::NoTrans ? band_chunk(Ap, r0, r1, c0, c1, dmin, dmax, false, target)
+                                 : op_view(op, band_chunk(Ap, c0, c1, r0, r1, dmin, dmax, false, target));
+    };
+    const int64_t nchunks = ceildiv(nt, kc);
+    for (int64_t s = 0; s < nchunks; ++s) {
+        const int64_t cidx = forward ? s : nchunks - 1 - s;
+        const int64_t k0 = cidx * kc, k1 = std::min(nt - 1, k0 + kc - 1);
+        Matrix<T> Bk = B.sub(k0, k1, 0, B.nt() - 1);
+        {
+            Matrix<T> D = band_chunk(Ap, k0, k1, k0, k1, dmin, dmax, false, target);
+            TriangularMatrix<T> Tk(u, diag, D);
+            if (op == Op::NoTrans) trsm(Side::Left, T(1), Tk, Bk, opts);
+            else if (op == Op::Trans) trsm(Side::Left, T(1), transpose(Tk), Bk, opts);
+            else trsm(Side::Left, T(1), conj_transpose(Tk), Bk, opts);
+        }
+        const int64_t e0 = col_off(Ap, k0), e1 = col_off(Ap, k1) + Ap.tileNb(k1) - 1;
+        if (forward && k1 + 1 < nt && kd > 0) {
+            const int64_t r1 = tile_col_of(Ap, std::min(n - 1, e1 + kd));
+            Matrix<T> Bs = B.sub(k1 + 1, r1, 0, B.nt() - 1);
+            gemm(T(-1), block(k1 + 1, r1, k0, k1), Bk, T(1), Bs, opts);
+        } else if (!forward && k0 > 0 && kd > 0) {
+            const int64_t r0 = tile_col_of(Ap, std::max<int64_t>(0, e0 - kd));
+            Matrix<T> Bs = B.sub(r0, k0 - 1, 0, B.nt() - 1);
+            gemm(T(-1), block(r0, k0 - 1, k0, k1), Bk, T(1), Bs, opts);
+        }
+    }
+}
+
+}  // namespace
+
 template <typename T>
 void gbmm(T alpha, BandMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts) {
     trace::Block tb("gbmm");
     internal::DriverScope ds_;
-    Matrix<T> D = band_dense<T>(A, A.lowerBandwidth(), A.upperBandwidth(), opts);
-    gemm(alpha, D, B, beta, C, opts);
+    BaseMatrix<T> Ap = physical<T>(A);
+    scale_by(beta, C, opts);
+    if (alpha != T(0)) band_apply(Side::Left, A.op(), alpha, Ap, -Ap.ku(), Ap.kl(), false, B, C, opts);
 }
 
 template <typename T>
@@ -573,18 +679,44 @@ void hbmm(Side side, T alpha, HermitianBandMatrix<T> const& A, Matrix<T> const& 
     trace::Block tb("hbmm");
     internal::DriverScope ds_;
     const int64_t kd = A.bandwidth();
-    Matrix<T> D = band_dense<T>(A, kd, kd, opts, true, A.uplo());
-    if (side == Side::Left) gemm(alpha, D, B, beta, C, opts);
-    else gemm(alpha, B, D, beta, C, opts);
+    BaseMatrix<T> Ap = physical<T>(A);
+    scale_by(beta, C, opts);
+    if (alpha == T(0)) return;
+    // A = S + E^H: S the stored triangle with a real diagonal, E its strict part
+    const bool lower = A.uplo_physical() == Uplo::Lower;
+    const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+    if (lower) {
+        band_apply(side, Op::NoTrans, alpha, Ap, 0, kd, true, B, C, opts);
+        if (kd > 0) band_apply(side, cT, alpha, Ap, 1, kd, false, B, C, opts);
+    } else {
+        band_apply(side, Op::NoTrans, alpha, Ap, -kd, 0, true, B, C, opts);
+        if (kd > 0) band_apply(side, cT, alpha, Ap, -kd, -1, false, B, C, opts);
+    }
 }
 
 template <typename T>
 void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
     trace::Block tb("tbsm");
     internal::DriverScope ds_;
-    Matrix<T> D = band_dense<T>(A, A.kl(), A.ku(), opts);
-    TriangularMatrix<T> Tm(A.uplo(), A.diag(), D);
-    trsm(side, alpha, Tm, B, opts);
+    BaseMatrix<T> Ap = physical<T>(A);
+    const Uplo u = A.uplo_physical();
+    const int64_t kd = A.bandwidth();
+    if (side == Side::Left) {
+        scale_by(alpha, B, opts);
+        tbsm_left(A.op(), Ap, u, A.diag(), kd, B, opts);
+        return;
+    }
+    // X op(A) = alpha B  <=>  t(op(A)) t(X) = alpha' t(B), t = conj-transpose
+    // (transpose for a Trans view of complex data), solved on a transposed copy
+    const Op t = (is_complex_v<T> && A.op() == Op::Trans) ? Op::Trans : (is_complex_v<T> ? Op::ConjTrans : Op::Trans);
+    const Op op2 = (A.op() == Op::NoTrans) ? t : Op::NoTrans;
+    const T alpha2 = t == Op::ConjTrans ? slate::conj(alpha) : alpha;
+    Matrix<T> Bt = B.emptyLike(0, 0, Op::Trans);
+    Bt.insertLocalTiles(resolve_target(opts));
+    slate::copy<T, T>(op_view(t, B), Bt, opts);
+    scale_by(alpha2, Bt, opts);
+    tbsm_left(op2, Ap, u, A.diag(), kd, Bt, opts);
+    slate::copy<T, T>(op_view(t, Bt), B, opts);
 }
 
 #define SLATE_BAND_INST(T)                                                                                 \

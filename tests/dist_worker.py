@@ -230,6 +230,35 @@ def case_band(tg, dt, nb):
             assert relerr(h @ x, b) < 100 * tol(dt), (kd, uplo)
 
 
+def case_band_blas(tg, dt, nb):
+    """gbmm / hbmm / tbsm / pbtrs over band chunks (distributed GEMM / TRSM on
+    the sub-views the band touches), bandwidths below and above the tile."""
+    n, nr = 150, 7
+    for kl, ku in ((3, 5), (40, 9)):
+        a = rnd(n, n, dt, 111 + kl)
+        b, c = rnd(n, nr, dt, 112), rnd(n, nr, dt, 113)
+        A = s.BandMatrix(kl, ku, s.from_numpy(a, nb=nb, target=tg))
+        B, C = s.from_numpy(b, nb=nb, target=tg), s.from_numpy(c, nb=nb, target=tg)
+        s.gbmm(2.0, A, B, 0.5, C, target=tg)
+        assert relerr(s.to_numpy(C), 2.0 * band_of(a, kl, ku) @ b + 0.5 * c) < tol(dt), (kl, ku)
+        h = (a + a.conj().T) / 2
+        for uplo in (s.Uplo.Lower, s.Uplo.Upper):
+            st = np.tril(h) if uplo == s.Uplo.Lower else np.triu(h)
+            H = s.HermitianBandMatrix(uplo, kl, s.from_numpy(st, nb=nb, target=tg))
+            bt = rnd(nr, n, dt, 114)
+            Bt, Ct = s.from_numpy(bt, nb=nb, target=tg), s.from_numpy(np.zeros((nr, n), dt), nb=nb, target=tg)
+            s.hbmm(s.Side.Right, 1.0, H, Bt, 0.0, Ct, target=tg)
+            assert relerr(s.to_numpy(Ct), bt @ band_of(h, kl, kl)) < tol(dt), (kl, uplo)
+            t = band_of(st, kl, kl) + 4 * np.eye(n, dtype=dt) * (1 + kl)
+            Tb = s.TriangularBandMatrix(uplo, s.Diag.NonUnit, kl, s.from_numpy(t, nb=nb, target=tg))
+            X = s.from_numpy(b, nb=nb, target=tg)
+            s.tbsm(s.Side.Left, 1.0, s.conj_transpose(Tb), X, target=tg)
+            assert relerr(t.conj().T @ s.to_numpy(X), b) < 100 * tol(dt), (kl, uplo)
+            Y = s.from_numpy(bt, nb=nb, target=tg)
+            s.tbsm(s.Side.Right, 2.0, Tb, Y, target=tg)
+            assert relerr(s.to_numpy(Y) @ t, 2.0 * bt) < 100 * tol(dt), (kl, uplo)
+
+
 def case_layout(tg, dt, nb):
     """Arbitrary distribution + non-uniform tiles (reference lambda
     constructor): drivers on lambda-layout operands (block-cyclic working
