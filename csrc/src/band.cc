@@ -9,8 +9,9 @@
 // broadcast ships the panel (and pivots) to the owners of the few block
 // columns it reaches, which apply the swaps, the triangular solve and the
 // GEMM update to their slabs -- the reference's tile-band algorithm with
-// whole-panel collectives instead of per-tile messages.  The solves and band
-// multiplies keep the band form on the host / a band-masked operand.
+// whole-panel collectives instead of per-tile messages.  gbmm / hbmm / tbsm,
+// pbtrs and gbtrs work chunk by chunk on the band's sub-views with the
+// distributed GEMM / TRSM (no dense operand, no replicated right-hand side).
 #include "internal.hh"
 #include "../kernels/kernels.hh"
 
@@ -77,19 +78,6 @@ void scatter_band(BaseMatrix<T>& A, std::vector<T> const& ab, int64_t kl, int64_
     });
 }
 
-/// Dense (replicated, column-major) copy of a distributed matrix.
-template <typename T>
-std::vector<T> gather_dense(BaseMatrix<T> const& B, Options const& opts) {
-    std::vector<T> b;
-    gather(B, b, opts);
-    return b;
-}
-
-template <typename T>
-void scatter_dense(Matrix<T>& B, std::vector<T> const& b, int64_t ldb) {
-    for_each_local(B, true, [&](int64_t i, int64_t j, T& v) { v = b[i + j * ldb]; });
-}
-
 //------------------------------------------------------------------------------
 // host band kernels (LAPACK gbtf2 / gbtrs / pbtf2 / pbtrs semantics)
 template <typename T>
@@ -124,27 +112,6 @@ int64_t gbtf2(int64_t n, int64_t kl, int64_t ku, T* ab, int64_t ldab, int64_t* i
         }
     }
     return info;
-}
-
-template <typename T>
-void gbtrs_host(int64_t n, int64_t kl, int64_t ku, int64_t nrhs, T const* ab, int64_t ldab, int64_t const* ipiv,
-                T* b, int64_t ldb) {
-    const int64_t kv = ku + kl;
-    auto A = [&](int64_t i, int64_t j) { return ab[(kv + i - j) + j * ldab]; };
-    #pragma omp parallel for schedule(static) if (nrhs > 1)
-    for (int64_t c = 0; c < nrhs; ++c) {
-        T* x = b + c * ldb;
-        for (int64_t j = 0; j < n; ++j) {
-            if (ipiv[j] != j) std::swap(x[j], x[ipiv[j]]);
-            int64_t km = std::min(kl, n - 1 - j);
-            for (int64_t i = 1; i <= km; ++i) x[j + i] -= A(j + i, j) * x[j];
-        }
-        for (int64_t j = n - 1; j >= 0; --j) {
-            x[j] /= A(j, j);
-            int64_t lo = std::max<int64_t>(0, j - kv);
-            for (int64_t i = lo; i < j; ++i) x[i] -= A(i, j) * x[j];
-        }
-    }
 }
 
 /// Lower band Cholesky: ab(i - j, j) = A(i, j), ldab >= kd + 1.
@@ -408,103 +375,6 @@ std::vector<int64_t> ipiv_from_pivots(BaseMatrix<T> const& A, Pivots const& pivo
 }  // namespace
 
 //------------------------------------------------------------------------------
-template <typename T>
-int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts) {
-    trace::Block tb("gbtrf");
-    internal::DriverScope ds_;
-    const int64_t n = A.n(), kl = A.lowerBandwidth(), ku = A.upperBandwidth();
-    slate_error_if_msg(A.m() != n, "gbtrf: square band matrix required");
-    const int64_t ldab = 2 * kl + ku + 1, kv = kl + ku;
-    // AB(kv + i - j, j) = A(i, j); rows [0, kl) receive the fill
-    std::vector<T> ab = gather_band<T>(A, kl, ku, kv, ldab);
-    Target target = resolve_target(opts);
-    Comm& w = A.grid()->world();
-    const int64_t nb = std::max<int64_t>(1, A.nb());
-    BandSlabs<T> sl(n, nb, nb * ceildiv(kl + ku + nb - 1, nb), kl, w, target);
-    sl.load(ab, kv, ldab, kl, ku);
-    std::vector<int64_t> ipiv;
-    int64_t info = gbtrf_slabs<T>(sl, kl, ku, w, ipiv);
-    sl.store(ab, kv, ldab, kl, kv, w);
-    // factors: L (kl below) and U (kl + ku above); the matrix's storage holds the fill
-    scatter_band<T>(A, ab, kl, kv, kv, ldab);
-    A.set_band(kl, kl + ku);
-    pivots_from_ipiv(A, ipiv, pivots);
-    if (target == Target::Devices) A.storage()->get(Loc::Device, false);
-    return info;
-}
-
-template <typename T>
-void gbtrs(BandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
-    trace::Block tb("gbtrs");
-    internal::DriverScope ds_;
-    const int64_t n = A.n(), kl = A.lowerBandwidth(), ku_f = A.upperBandwidth();
-    // after gbtrf the stored upper bandwidth is kl + ku (fill)
-    const int64_t ku = std::max<int64_t>(ku_f - kl, 0);
-    const int64_t ldab = 2 * kl + ku + 1;
-    std::vector<T> ab = gather_band<T>(A, kl, kl + ku, kl + ku, ldab);
-    std::vector<int64_t> ipiv = ipiv_from_pivots(A, pivots);
-    std::vector<T> b = gather_dense(B, opts);
-    gbtrs_host<T>(n, kl, ku, B.n(), ab.data(), ldab, ipiv.data(), b.data(), n);
-    scatter_dense(B, b, n);
-    if (resolve_target(opts) == Target::Devices) B.storage()->get(Loc::Device, false);
-}
-
-template <typename T>
-int64_t gbsv(BandMatrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
-    trace::Block tb("gbsv");
-    internal::DriverScope ds_;
-    int64_t info = gbtrf(A, pivots, opts);
-    if (info == 0) gbtrs(A, pivots, B, opts);
-    return info;
-}
-
-template <typename T>
-int64_t pbtrf(HermitianBandMatrix<T>& A, Options const& opts) {
-    trace::Block tb("pbtrf");
-    internal::DriverScope ds_;
-    const int64_t n = A.n(), kd = A.bandwidth();
-    const bool upper = A.uplo() == Uplo::Upper;
-    // lower band storage ab(i - j, j) = L(i, j); an Upper matrix is read as U^H
-    std::vector<T> ab = upper ? gather_band<T>(A, 0, kd, 0, kd + 1, true) : gather_band<T>(A, kd, 0, 0, kd + 1);
-    Target target = resolve_target(opts);
-    Comm& w = A.grid()->world();
-    BandSlabs<T> sl(n, std::max<int64_t>(1, A.nb()), 0, kd, w, target);
-    sl.load(ab, 0, kd + 1, kd, 0);
-    int64_t info = pbtrf_slabs<T>(sl, kd, w);
-    sl.store(ab, 0, kd + 1, kd, 0, w);
-    if (upper) scatter_band<T>(A, ab, 0, kd, 0, kd + 1, true);
-    else scatter_band<T>(A, ab, kd, 0, 0, kd + 1);
-    if (resolve_target(opts) == Target::Devices) A.storage()->get(Loc::Device, false);
-    return info;
-}
-
-template <typename T>
-void pbtrs(HermitianBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
-    trace::Block tb("pbtrs");
-    internal::DriverScope ds_;
-    // two distributed band triangular solves with the factor (reference
-    // src/pbtrs.cc): A = L L^H (Lower) or U^H U (Upper)
-    const Uplo u = A.uplo();
-    TriangularBandMatrix<T> F(u, Diag::NonUnit, A.bandwidth(), BaseMatrix<T>(A));
-    if (u == Uplo::Lower) {
-        tbsm(Side::Left, T(1), F, B, opts);
-        tbsm(Side::Left, T(1), conj_transpose(F), B, opts);
-    } else {
-        tbsm(Side::Left, T(1), conj_transpose(F), B, opts);
-        tbsm(Side::Left, T(1), F, B, opts);
-    }
-}
-
-template <typename T>
-int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, Options const& opts) {
-    trace::Block tb("pbsv");
-    internal::DriverScope ds_;
-    int64_t info = pbtrf(A, opts);
-    if (info == 0) pbtrs(A, B, opts);
-    return info;
-}
-
-//------------------------------------------------------------------------------
 // Band BLAS (reference src/gbmm.cc, hbmm.cc, tbsm.cc, work on the tiles inside
 // the band only).  Here the band is walked in chunks of block columns: each
 // chunk's band part -- at most (chunk + bandwidth) x chunk elements, entries
@@ -663,6 +533,138 @@ void tbsm_left(Op op, BaseMatrix<T> const& Ap, Uplo u, Diag diag, int64_t kd, Ma
 }
 
 }  // namespace
+
+//------------------------------------------------------------------------------
+template <typename T>
+int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts) {
+    trace::Block tb("gbtrf");
+    internal::DriverScope ds_;
+    const int64_t n = A.n(), kl = A.lowerBandwidth(), ku = A.upperBandwidth();
+    slate_error_if_msg(A.m() != n, "gbtrf: square band matrix required");
+    const int64_t ldab = 2 * kl + ku + 1, kv = kl + ku;
+    // AB(kv + i - j, j) = A(i, j); rows [0, kl) receive the fill
+    std::vector<T> ab = gather_band<T>(A, kl, ku, kv, ldab);
+    Target target = resolve_target(opts);
+    Comm& w = A.grid()->world();
+    const int64_t nb = std::max<int64_t>(1, A.nb());
+    BandSlabs<T> sl(n, nb, nb * ceildiv(kl + ku + nb - 1, nb), kl, w, target);
+    sl.load(ab, kv, ldab, kl, ku);
+    std::vector<int64_t> ipiv;
+    int64_t info = gbtrf_slabs<T>(sl, kl, ku, w, ipiv);
+    sl.store(ab, kv, ldab, kl, kv, w);
+    // factors: L (kl below) and U (kl + ku above); the matrix's storage holds the fill
+    scatter_band<T>(A, ab, kl, kv, kv, ldab);
+    A.set_band(kl, kl + ku);
+    pivots_from_ipiv(A, ipiv, pivots);
+    if (target == Target::Devices) A.storage()->get(Loc::Device, false);
+    return info;
+}
+
+template <typename T>
+void gbtrs(BandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("gbtrs");
+    internal::DriverScope ds_;
+    // after gbtrf the stored upper bandwidth is kl + ku (the fill)
+    const int64_t n = A.n(), kl = A.lowerBandwidth(), kuf = A.upperBandwidth();
+    const Target target = resolve_target(opts);
+    if (kl > 0 && n > 0) {
+        // L with the interleaved row swaps (LAPACK gbtrs convention): the
+        // swaps and eliminations of block column [j0, j1) only touch rows
+        // [j0, j1 + kl).  Their product M (tile-padded, identity outside) is
+        // formed on the host from the O(n * kl) L band and applied to those
+        // rows of B by one distributed GEMM per block column (reference
+        // src/gbtrs.cc: tbsm with pivots).
+        std::vector<T> abl = gather_band<T>(A, kl, 0, 0, kl + 1);   // abl(i - j, j) = L(i, j)
+        std::vector<int64_t> ipiv = ipiv_from_pivots(A, pivots);
+        const int64_t nt = A.nt();
+        for (int64_t k = 0; k < nt; ++k) {
+            const int64_t j0 = col_off<T>(A, k), j1 = j0 + A.tileNb(k);
+            const int64_t kr = tile_row_of<T>(A, std::min(n, j1 + kl) - 1);
+            const int64_t R0 = row_off<T>(A, k), Rn = row_off<T>(A, kr) + A.tileMb(kr) - R0;
+            std::vector<T> M(size_t(Rn) * Rn, T(0));
+            for (int64_t i = 0; i < Rn; ++i) M[i + i * Rn] = T(1);
+            for (int64_t j = j0; j < j1; ++j) {
+                const int64_t lj = j - R0, lp = ipiv[j] - R0;
+                if (lp != lj)
+                    for (int64_t c = 0; c < Rn; ++c) std::swap(M[lj + c * Rn], M[lp + c * Rn]);
+                const int64_t km = std::min(kl, n - 1 - j);
+                for (int64_t i = 1; i <= km; ++i) {
+                    const T l = abl[i + j * (kl + 1)];
+                    if (l == T(0)) continue;
+                    for (int64_t c = 0; c < Rn; ++c) M[lj + i + c * Rn] -= l * M[lj + c * Rn];
+                }
+            }
+            Matrix<T> Ms(BaseMatrix<T>(A).sub(k, kr, k, kr));
+            Matrix<T> Mm = Ms.emptyLike();
+            Mm.insertLocalTiles(Target::Host);
+            for_each_local(Mm, true, [&](int64_t i, int64_t j, T& v) { v = M[i + j * Rn]; });
+            if (target == Target::Devices) Mm.insertLocalTiles(Target::Devices);
+            Matrix<T> Bs = B.sub(k, kr, 0, B.nt() - 1);
+            Matrix<T> Bt = Bs.emptyLike();
+            Bt.insertLocalTiles(target);
+            slate::copy<T, T>(Bs, Bt, opts);
+            gemm(T(1), Mm, Bt, T(0), Bs, opts);
+        }
+    }
+    TriangularBandMatrix<T> U(Uplo::Upper, Diag::NonUnit, kuf, BaseMatrix<T>(A));
+    tbsm(Side::Left, T(1), U, B, opts);
+}
+
+template <typename T>
+int64_t gbsv(BandMatrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("gbsv");
+    internal::DriverScope ds_;
+    int64_t info = gbtrf(A, pivots, opts);
+    if (info == 0) gbtrs(A, pivots, B, opts);
+    return info;
+}
+
+template <typename T>
+int64_t pbtrf(HermitianBandMatrix<T>& A, Options const& opts) {
+    trace::Block tb("pbtrf");
+    internal::DriverScope ds_;
+    const int64_t n = A.n(), kd = A.bandwidth();
+    const bool upper = A.uplo() == Uplo::Upper;
+    // lower band storage ab(i - j, j) = L(i, j); an Upper matrix is read as U^H
+    std::vector<T> ab = upper ? gather_band<T>(A, 0, kd, 0, kd + 1, true) : gather_band<T>(A, kd, 0, 0, kd + 1);
+    Target target = resolve_target(opts);
+    Comm& w = A.grid()->world();
+    BandSlabs<T> sl(n, std::max<int64_t>(1, A.nb()), 0, kd, w, target);
+    sl.load(ab, 0, kd + 1, kd, 0);
+    int64_t info = pbtrf_slabs<T>(sl, kd, w);
+    sl.store(ab, 0, kd + 1, kd, 0, w);
+    if (upper) scatter_band<T>(A, ab, 0, kd, 0, kd + 1, true);
+    else scatter_band<T>(A, ab, kd, 0, 0, kd + 1);
+    if (resolve_target(opts) == Target::Devices) A.storage()->get(Loc::Device, false);
+    return info;
+}
+
+template <typename T>
+void pbtrs(HermitianBandMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("pbtrs");
+    internal::DriverScope ds_;
+    // two distributed band triangular solves with the factor (reference
+    // src/pbtrs.cc): A = L L^H (Lower) or U^H U (Upper)
+    const Uplo u = A.uplo();
+    TriangularBandMatrix<T> F(u, Diag::NonUnit, A.bandwidth(), BaseMatrix<T>(A));
+    if (u == Uplo::Lower) {
+        tbsm(Side::Left, T(1), F, B, opts);
+        tbsm(Side::Left, T(1), conj_transpose(F), B, opts);
+    } else {
+        tbsm(Side::Left, T(1), conj_transpose(F), B, opts);
+        tbsm(Side::Left, T(1), F, B, opts);
+    }
+}
+
+template <typename T>
+int64_t pbsv(HermitianBandMatrix<T>& A, Matrix<T>& B, Options const& opts) {
+    trace::Block tb("pbsv");
+    internal::DriverScope ds_;
+    int64_t info = pbtrf(A, opts);
+    if (info == 0) pbtrs(A, B, opts);
+    return info;
+}
+
 
 template <typename T>
 void gbmm(T alpha, BandMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts) {
