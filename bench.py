@@ -59,7 +59,7 @@ def parse():
     ap.add_argument("--routines", default=",".join(ALL))
     ap.add_argument("--p", type=int, default=0)
     ap.add_argument("--q", type=int, default=0)
-    ap.add_argument("--lookahead", type=int, default=1)
+    ap.add_argument("--lookahead", type=int, default=0, help="0: per-routine default (see la_per)")
     ap.add_argument("--method-lu", default="tntpiv", choices=["ppiv", "tntpiv"])
     ap.add_argument("--trace", default="")
     ap.add_argument("--extras", default="all", help="BASELINE configs to add after the suite: all, none, or names")
@@ -97,7 +97,13 @@ def main():
     a.nb = a.nb or 512
     nb_per = dict(default_nb)
     nb_per.update({k: int(v) for k, v in (kv.split("=") for kv in a.nb_per.split(",") if kv)})
-    opts = dict(target=target, lookahead=a.lookahead)
+    # Lookahead: 1 (the reference default), except on one GPU where dpotrf and
+    # dgeqrf measured faster at 2 (profiles/r2_sweep2_la_nb_ppiv.txt: potrf
+    # 59.4 -> 60.1, geqrf 55.7 -> 56.2 TFLOP/s at n=65536).
+    la_per = {"dpotrf": 2, "dgeqrf": 2} if world == 1 else {}
+
+    def la_of(rname):
+        return a.lookahead or la_per.get(rname, 1)
 
     def barrier_sync():
         s.sync()
@@ -173,7 +179,7 @@ def main():
         steps = a.steps if steps is None else steps
         mats = {}
         tgt = s.target_of(tg)
-        o = dict(target=tg, lookahead=a.lookahead)
+        o = dict(target=tg, lookahead=la_of(rname))
         if rname == "dgemm":
             for key, seed in (("A", 1), ("B", 2), ("C", 3)):
                 M = s.Matrix(n_, n_, nb, np.float64, grid)
@@ -252,7 +258,7 @@ def main():
                 fit = int(left // (max_over_ranks(dt) * 1.15))
                 total = min(total, max(warmup + 1, step + fit))
         t = max_over_ranks(float(np.mean(times)))
-        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_,
+        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_, "lookahead": la_of(rname),
                "steps": len(times), "warmup": warmup}
         if a.check == "yes":
             err = residual(rname, mats, kind, seed, nb, n_, tg)
@@ -316,7 +322,7 @@ def main():
             "global_batch": 1,
             "seq_len": n,
             "parallelism": f"2d-block-cyclic {p}x{q} (one process per GPU, RCCL)" if world > 1 else "1x1",
-            "lookahead": a.lookahead,
+            "lookahead": {k: la_of(k) for k in results} if not a.lookahead else a.lookahead,
             "lu_method": a.method_lu,
         },
         "routines": {k: {kk: (round(vv, 4) if isinstance(vv, float) and kk != "backward_error" else vv)

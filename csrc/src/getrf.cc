@@ -687,16 +687,24 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, c1 - c0, T(1),
                      Wk, std::max<int64_t>(mrows_k, 1), a + lr_k + c0 * lda, lda);
         };
-        auto update = [&, kb, lr_k1, lr_k, Wk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        auto update = [&, kb, kd, lr_k1, lr_k, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
             auto cc = lcols(j0, j1);
             int64_t c0 = cc.first, nc = cc.second - cc.first, nr = mloc - lr_k1;
             if (nc <= 0 || nr <= 0) return;
             trace::Block t2("getrf_update");
             // U rows of these columns live in A itself (process row 0 owns them)
+            if (!is_complex_v<T> && c.dev() && update_nt()) {
+                // NT product against U^T (nc x kd, ld nc) in this range's own
+                // slice of the slot's WU buffer
+                T* Ut = WUk + c0 * kd;
+                lb::copy<T, T>(c, Uplo::General, Op::Trans, nc, kd, a + lr_k + c0 * lda, lda, Ut, nc);
+                lb::gemm(c, Op::NoTrans, Op::Trans, nr, nc, kd, T(-1), Wk + (lr_k1 - lr_k),
+                         std::max<int64_t>(mrows_k, 1), Ut, nc, T(1), a + lr_k1 + c0 * lda, lda);
+                return;
+            }
             lb::gemm(c, Op::NoTrans, Op::NoTrans, nr, nc, kb, T(-1), Wk + (lr_k1 - lr_k), std::max<int64_t>(mrows_k, 1),
                      a + lr_k + c0 * lda, lda, T(1), a + lr_k1 + c0 * lda, lda);
         };
-        (void)WUk;
 
         auto range_tasks = [&](int queue, int64_t j0, int64_t j1) {
             std::vector<int64_t> cols;

@@ -9,6 +9,7 @@
 #include "slate_amd/runtime.hh"
 #include "slate_amd/trace.hh"
 
+#include <cstdlib>
 #include <vector>
 
 namespace slate {
@@ -20,6 +21,17 @@ template <> struct lower_prec<std::complex<double>> { using type = std::complex<
 }  // namespace internal
 
 namespace internal {
+
+/// Real trailing updates C -= X Y as NT products against a transposed copy of
+/// Y (the 4-wave rotated MFMA tile, measured faster than the NN 8-wave tile
+/// on large shapes); SLATE_UPDATE_NT=0 keeps the NN form.
+inline bool update_nt() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_UPDATE_NT");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
 
 /// Local row offset within `A`'s local block for view row-tile index i (first
 /// local row whose global index is >= start of tile i).

@@ -297,6 +297,14 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         // C -= V (T^H W)
         auto apply = [&, kb, lr_k, mr, Tk, Vk, ldv, Wk, W2k](lb::Ctx const& c, int64_t c0, int64_t nc) {
             T* Cc = a + lr_k + c0 * lda;
+            if (!is_complex_v<T> && c.dev() && update_nt()) {
+                // (T^H W)^H = W^H T (nc x kb, ld nc): C -= V (W^H T)^H runs as
+                // an NT product
+                T* W2h = W2k + c0 * kb;
+                lb::gemm(c, cT, Op::NoTrans, nc, kb, kb, T(1), Wk + c0 * kb, kb, Tk, kb, T(0), W2h, nc);
+                if (mr > 0) lb::gemm(c, Op::NoTrans, cT, mr, nc, kb, T(-1), Vk, ldv, W2h, nc, T(1), Cc, lda);
+                return;
+            }
             lb::gemm(c, cT, Op::NoTrans, kb, nc, kb, T(1), Tk, kb, Wk + c0 * kb, kb, T(0), W2k + c0 * kb, kb);
             if (mr > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, nc, kb, T(-1), Vk, ldv, W2k + c0 * kb, kb, T(1), Cc, lda);
         };
