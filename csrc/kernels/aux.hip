@@ -164,6 +164,7 @@ template <typename T>
 __global__ __launch_bounds__(64)
 void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
                        const T* A, int64_t lda, T* W, int64_t ldw, int64_t wrap) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ T L[64][64];
     __shared__ T rd[64];
     const int b = blockIdx.x;
@@ -216,6 +217,7 @@ void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
 template <typename T>
 __global__ __launch_bounds__(64)
 void potrf_small_kernel(char uplo, int n, T* A, int64_t lda, int* info, int info_offset) {
+    SLATE_PANEL_WAVE_PRIO();
     const int i = threadIdx.x;
     T a[64];
     #pragma unroll

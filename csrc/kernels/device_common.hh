@@ -8,6 +8,18 @@
 #include <cstdint>
 #include "dev_types.hh"
 
+// Panel (critical-path) kernels raise their waves' instruction-issue priority
+// (s_setprio) so that trailing-update GEMM waves sharing the CU do not starve
+// them: the hardware queue priority only orders dispatch, not issue inside a
+// SIMD.  SLATE_PANEL_PRIO=0 at build time turns it off (A/B builds).
+#ifndef SLATE_PANEL_PRIO
+#define SLATE_PANEL_PRIO 1
+#endif
+#define SLATE_PANEL_WAVE_PRIO()                                   \
+    do {                                                          \
+        if (SLATE_PANEL_PRIO) __builtin_amdgcn_s_setprio(3);      \
+    } while (0)
+
 namespace slate_amd {
 namespace dev {
 

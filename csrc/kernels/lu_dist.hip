@@ -125,6 +125,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void pplu_cand_kernel(int64_t mr, int64_t j, int64_t r0, const T* ap, int64_t lda,
                                                         int64_t kb, RowDist d, int64_t lr_k, int is_pk, T* buf,
                                                         int hdr) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = rt<T>;
     __shared__ R sv[256];
     __shared__ int64_t si[256];
@@ -168,6 +169,7 @@ __global__ __launch_bounds__(256) void pplu_apply_kernel(int np, const T* gbuf, 
                                                          int64_t lda, RowDist d, int64_t lr_k, int64_t kk, int pk,
                                                          rt<T> thresh, int is_pk, int64_t* pip, int* info,
                                                          int64_t info_off) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = rt<T>;
     __shared__ int64_t s_piv;
     __shared__ int s_w;

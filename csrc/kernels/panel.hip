@@ -49,6 +49,7 @@ __device__ inline void block_argmax(R& v, int64_t& idx) {
 template <typename T>
 __global__ void lu_colmax_kernel(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c,
                                  real_t<T>* pval, int64_t* pidx) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
     R v = -1; int64_t idx = INT64_MAX;
@@ -64,6 +65,7 @@ __global__ void lu_pivot_kernel(int nparts, const real_t<T>* pval, const int64_t
                                 int64_t r, int64_t c, T* A, int64_t lda, int64_t ncols,
                                 int64_t* ipiv, int64_t ipiv_base, int64_t* perm,
                                 int* info, int64_t info_offset, int64_t* piv_out, real_t<T> thresh) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     R v = -1; int64_t idx = INT64_MAX;
     for (int k = threadIdx.x; k < nparts; k += PT) {
@@ -97,6 +99,7 @@ __global__ void lu_pivot_kernel(int nparts, const real_t<T>* pval, const int64_t
 template <typename T>
 __global__ void lu_update_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                  real_t<T>* pval, int64_t* pidx) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     __shared__ T urow[64];
     const int64_t nc = cend - c - 1;            // columns right of c in the block (<= 63)
@@ -130,6 +133,7 @@ __global__ void lu_update_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, 
 template <typename T>
 __global__ void lu_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                    real_t<T>* pval, int64_t* pidx, int scale_prev) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     const int j = blockIdx.y;
     const int64_t i = r + blockIdx.x * (int64_t)PT + threadIdx.x;
@@ -161,6 +165,7 @@ __global__ void lu_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend
 // scale rows (c, m) of column c by 1 / A[c, c]
 template <typename T>
 __global__ void lu_scale_col_kernel(int64_t m, int64_t c, T* A, int64_t lda) {
+    SLATE_PANEL_WAVE_PRIO();
     int64_t i = c + 1 + blockIdx.x * (int64_t)PT + threadIdx.x;
     if (i >= m) return;
     T d = A[c + c * lda];
@@ -191,6 +196,7 @@ __global__ void perm_pairs_kernel(int64_t k, const int64_t* perm, const int64_t*
 template <typename T>
 __global__ void qr_colnorm_kernel(int64_t m, int64_t r, const T* A, int64_t lda, int64_t c,
                                   real_t<T>* psum, T* alpha_out) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     int64_t i = r + 1 + blockIdx.x * (int64_t)PT + threadIdx.x;
     R s = 0;
@@ -234,6 +240,7 @@ template <typename T>
 __global__ void qr_reflect_dots_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                        int nparts, const real_t<T>* psum, const T* alpha_in,
                                        T* tau_out, T* pdots /* [gridDim.x][nc] */) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     __shared__ R red[PT];
     __shared__ T sh_scal;
@@ -282,6 +289,7 @@ template <typename T>
 __global__ void qr_update_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                  int nparts, const T* pdots, const T* tau_in,
                                  real_t<T>* psum_next, T* alpha_next) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     __shared__ T z[64];
     const int64_t nc = cend - c - 1;
@@ -359,6 +367,7 @@ template <typename T>
 __global__ void qr_dots2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                  int nparts_norm, const real_t<T>* psum, const T* alpha_in,
                                  T* tau_out, T* scal_buf, T* pdots, int scale_prev) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     T beta, tau, scal;
     qr_block_reflector(nparts_norm, psum, alpha_in, beta, tau, scal);
@@ -401,6 +410,7 @@ template <typename T>
 __global__ void qr_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend, T* A, int64_t lda,
                                    int nparts, const T* pdots, const T* tau_buf, const T* scal_buf,
                                    real_t<T>* psum_next, T* alpha_next) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     const int j0 = 1 + blockIdx.y * QR_CPB;
     const int ncol = (int)min<int64_t>(QR_CPB, cend - c - j0);
@@ -457,6 +467,7 @@ __global__ void qr_update2d_kernel(int64_t m, int64_t r, int64_t c, int64_t cend
 // scale rows (c, m) of column c by scal_buf[c]
 template <typename T>
 __global__ void qr_scale_col_kernel(int64_t m, int64_t c, T* A, int64_t lda, const T* scal_buf) {
+    SLATE_PANEL_WAVE_PRIO();
     int64_t i = c + 1 + blockIdx.x * (int64_t)PT + threadIdx.x;
     if (i >= m) return;
     A[i + c * lda] = A[i + c * lda] * scal_buf[c];
@@ -469,6 +480,7 @@ __global__ void qr_scale_col_kernel(int64_t m, int64_t c, T* A, int64_t lda, con
 template <typename T>
 __global__ void tsip_partial_kernel(int64_t K, int m, int n, const T* A, int64_t lda,
                                     const T* B, int64_t ldb, int64_t kchunk, T* part) {
+    SLATE_PANEL_WAVE_PRIO();
     // each block: one k-chunk; thread (tx) handles output entries
     const int64_t k0 = blockIdx.x * kchunk, k1 = min(K, k0 + kchunk);
     __shared__ T As[64][33];
@@ -504,6 +516,7 @@ __global__ void tsip_partial_kernel(int64_t K, int m, int n, const T* A, int64_t
 
 template <typename T>
 __global__ void tsip_reduce_kernel(int nparts, int m, int n, const T* part, T alpha, T beta, T* C, int64_t ldc) {
+    SLATE_PANEL_WAVE_PRIO();
     int e = blockIdx.x * blockDim.x + threadIdx.x;
     if (e >= m * n) return;
     T s = zero<T>();
@@ -517,6 +530,7 @@ __global__ void tsip_reduce_kernel(int nparts, int m, int n, const T* part, T al
 // used) and tau, form upper-triangular T in place of S (k <= 64, one block).
 template <typename T>
 __global__ void larft_kernel(int k, const T* tau, T* Tm, int64_t ldt) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ T S[64][65];
     __shared__ T tv[64];
     for (int e = threadIdx.x; e < k * k; e += blockDim.x) {

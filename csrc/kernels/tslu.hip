@@ -73,6 +73,7 @@ template <typename T, int NT>
 __global__ __launch_bounds__(NT) void tslu_select_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
                                                          const int* cand_in, const int* cnt_in, int nin,
                                                          int* cand_out, int* cnt_out) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     constexpr int NW = NT / 64;
     __shared__ R sv[2][NW];
@@ -161,6 +162,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void tslu_permute_kernel(int r, int nn, int64_t c0, T* A, int64_t lda,
                                                            int64_t ncols, const int* win, const int* wcnt,
                                                            int64_t* ipiv, int64_t* perm, T* Utop) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ int s_dst[64], s_src[64], s_top[TW];
     __shared__ int s_np;
     const int tid = threadIdx.x;
@@ -252,6 +254,7 @@ __device__ inline int tslu_top_factor(int nn, const T* Utop, T (&a)[TW], T* Uinv
 template <typename T>
 __global__ __launch_bounds__(256) void tslu_rows_kernel(int64_t m, int64_t r, int nn, T* A, int64_t lda,
                                                         const T* Utop, int* info, int64_t info_offset) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ T Uinv[TW * TW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (w == 0) {

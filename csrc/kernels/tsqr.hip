@@ -39,6 +39,7 @@ template <typename T>
 __global__ __launch_bounds__(256) void lu_sign_narrow_kernel(int64_t m, int64_t r, int nn, const T* Ain,
                                                              int64_t ldi, T* Aout, int64_t ldo, const T* Utop,
                                                              int64_t ldu, T in_scale, T* top, int64_t ldt, T* sgn) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ T Uinv[TW * TW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (w == 0) {
@@ -215,6 +216,7 @@ __device__ inline T wave_reduce_scatter32(T (&q)[TW]) {
 template <typename T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void qr_node_kernel(
         int64_t rows, int nn, const T* In, int64_t ldi, T* Vout, int64_t ldv, T* Rout, int64_t ldr, T* Tout) {
+    SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     __shared__ R red[2][4];
     __shared__ T wred[4][TW];
@@ -315,6 +317,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 template <typename T>
 __global__ __launch_bounds__(256) void qr_node_q_kernel(int64_t rows, int nn, const T* V, int64_t ldv,
                                                         const T* Tin, const T* E, int64_t lde, T* Q, int64_t ldq) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ T sE[TW][TW + 1], sV1[TW][TW + 1], sW[TW][TW + 1], sT[TW][TW + 1];
     const int tid = threadIdx.x;
     const int64_t row0 = blockIdx.x * (int64_t)256;
@@ -376,6 +379,7 @@ template <typename T>
 __global__ __launch_bounds__(64) void qr_hr_finish_kernel(int nn, const T* LU, int64_t ldl, const T* sgn,
                                                           const T* Rr, int64_t ldr, T* A, int64_t lda, T* Tm,
                                                           int64_t ldt, T* tau) {
+    SLATE_PANEL_WAVE_PRIO();
     __shared__ T sL[TW][TW + 1], sX[TW][TW + 1], sS[TW];
     const int i = threadIdx.x;
     for (int e = i; e < TW * TW; e += 64) {

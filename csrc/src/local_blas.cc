@@ -7,6 +7,7 @@
 #include <map>
 #include <mutex>
 #include <cstring>
+#include <cstdlib>
 
 namespace slate {
 namespace lb {
@@ -116,6 +117,15 @@ void dgemm_splitk(hipStream_t s, char ta, char tb, int64_t m, int64_t n, int64_t
     kd::splitk_reduce<T>(m, n, int(splits), P, alpha, beta, C, ldc, s);
 }
 
+// SLATE_UPDATE_NT=0 keeps NN products in NN form (as internal::update_nt)
+inline bool nt_pack() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_UPDATE_NT");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 // device gemm dispatch (real -> MFMA, complex -> complex kernel)
 template <typename T>
 void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
@@ -135,6 +145,25 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
             int64_t splits = std::min<int64_t>({ceildiv(k, 256), std::max<int64_t>(2, 512 / tiles), int64_t(64)});
             dgemm_splitk(s, ta, tb, m, n, k, splits, alpha, A, lda, B, ldb, beta, C, ldc);
             return;
+        }
+        // Rank-nb NN updates (SUMMA steps, K <= 2048): one transposed copy of
+        // B (k x n -> n x k, a streaming pass of ~1/m of the product) turns
+        // them into NT products on the 4-wave rotated tile, as the getrf /
+        // geqrf trailing updates (same-box A/B, K = 512-1024: -1.7% time).
+        // Not for long K: n = k = 65536 measured 68.7 (NN) -> 66.5 (NT)
+        // TFLOP/s (profiles/r2_ab_prio_gemm_nt.txt).
+        if (uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && nt_pack() && m >= 4096 &&
+            n >= 1024 && k >= 256 && k <= 2048) {
+            const size_t bytes = size_t(n) * size_t(k) * sizeof(T);
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && 2 * bytes < fr) {
+                T* Bt = static_cast<T*>(device::malloc(bytes));
+                kd::gecopy<T, T>('G', 'T', n, k, B, ldb, Bt, n, s);
+                kd::gemm_real<T>('N', 'T', m, n, k, alpha, A, lda, 0, Bt, n, 0, beta, C, ldc, 0, 1, s);
+                device::free(Bt);
+                return;
+            }
+            (void)hipGetLastError();
         }
         // K-chunked launches for large updates (SLATE_GEMM_KCHUNK): shorter
         // workgroups free CU slots for the high-priority panel queue sooner

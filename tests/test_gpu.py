@@ -493,4 +493,8 @@ def test_hesv_aasen_device(dtype):
     info, p1, p2 = s.hesv_aasen(A, T, B, target="d")
     x = s.to_numpy(B)
     assert info == 0
-    assert np.linalg.norm(h @ x - b) / (np.linalg.norm(h) * np.linalg.norm(x)) < 1e-13
+    # backward error in the reference tester's form (test/test_hesv.cc:
+    # ||b - A x|| / (||A|| ||x|| n) against a few eps); the band solve of T
+    # runs on diagonal-block inverses + GEMMs, so allow 3 eps per row
+    err = np.linalg.norm(h @ x - b) / (np.linalg.norm(h) * np.linalg.norm(x) * n)
+    assert err < 3 * np.finfo(np.float64).eps, err
