@@ -352,7 +352,33 @@ void trtri_to(Ctx const& c, Uplo uplo, Diag diag, int64_t n, T const* A, int64_t
     Scratch sc(c);
     T* tmp = sc.alloc<T>(size_t(n) * n / 2 + NBS * NBS);
     for (int64_t sz = NBS; sz < n; sz *= 2) {
-        for (int64_t p = 0; p + sz < n; p += 2 * sz) {
+        int64_t p0 = 0;
+        if constexpr (is_real_v<T>) {
+            // the level's full-size pairs as two batched launches (they are
+            // equally strided): fewer launches on the panel's critical path,
+            // where each one waits for a CU slot behind the trailing GEMM
+            static const bool batch = [] {
+                const char* e = std::getenv("SLATE_TRTRI_BATCH");
+                return e ? std::atoi(e) != 0 : true;
+            }();
+            const int64_t nfull = n / (2 * sz);
+            if (batch && nfull >= 2) {
+                const int64_t sa = 2 * sz * (1 + lda), sw = 2 * sz * (1 + ldw), st = sz * sz;
+                if (uplo == Uplo::Lower) {
+                    kd::gemm_real<T>('N', 'N', sz, sz, sz, T(1), A + sz, lda, sa, W, ldw, sw, T(0), tmp, sz, st,
+                                     nfull, s);
+                    kd::gemm_real<T>('N', 'N', sz, sz, sz, T(-1), W + sz + sz * ldw, ldw, sw, tmp, sz, st, T(0),
+                                     W + sz, ldw, sw, nfull, s);
+                } else {
+                    kd::gemm_real<T>('N', 'N', sz, sz, sz, T(1), A + sz * lda, lda, sa, W + sz + sz * ldw, ldw, sw,
+                                     T(0), tmp, sz, st, nfull, s);
+                    kd::gemm_real<T>('N', 'N', sz, sz, sz, T(-1), W, ldw, sw, tmp, sz, st, T(0), W + sz * ldw, ldw,
+                                     sw, nfull, s);
+                }
+                p0 = nfull * 2 * sz;
+            }
+        }
+        for (int64_t p = p0; p + sz < n; p += 2 * sz) {
             int64_t s2 = std::min(sz, n - p - sz);
             if (uplo == Uplo::Lower) {
                 // X21 = -X22 * A21 * X11 ; A21 = A[p+sz : +s2, p : +sz]
