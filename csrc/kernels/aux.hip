@@ -254,6 +254,62 @@ void potrf_small_kernel(char uplo, int n, T* A, int64_t lda, int* info, int info
 }
 
 //------------------------------------------------------------------------------
+// Lower Cholesky of a small (n <= 64) diagonal block AND the inverse of its
+// factor in one launch: the factorization as potrf_small (lane i owns row i),
+// then the factor goes through LDS and lane j computes column j of L^{-1} by
+// substitution as trtri_diag does.  A receives L (lower triangle only), W
+// (ld ldw) the full 64 x 64 inverse (zero above the diagonal; identity
+// padding beyond n).  One launch instead of potrf_small + set + trtri_diag
+// on the blocked device potrf's critical path.
+template <typename T>
+__global__ __launch_bounds__(64)
+void potrf_inv_small_kernel(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int info_offset) {
+    SLATE_PANEL_WAVE_PRIO();
+    __shared__ T L[64][65];
+    __shared__ T rd[64];
+    const int i = threadIdx.x;
+    T a[64];
+    #pragma unroll
+    for (int l = 0; l < 64; ++l)
+        a[l] = (i < n && l < n && i >= l) ? A[i + (int64_t)l * lda] : zero<T>();
+    int fail = 0;
+    #pragma unroll
+    for (int j = 0; j < 64; ++j) {
+        if (j < n) {
+            T s = a[j];
+            #pragma unroll
+            for (int l = 0; l < j; ++l) s -= a[l] * conj(bcast_lane(a[l], j));
+            real_t<T> d = real(bcast_lane(s, j));
+            if (!(d > real_t<T>(0)) && fail == 0) fail = j + 1;
+            real_t<T> sd = sqrt(d);
+            if (i == j) a[j] = make_val<T>((double)sd);
+            else if (i > j) a[j] = s * (real_t<T>(1) / sd);
+        }
+    }
+    if (fail && info && i == 0 && *info == 0) *info = info_offset + fail;
+    #pragma unroll
+    for (int l = 0; l < 64; ++l) {
+        // identity padding keeps the substitution below well defined
+        L[i][l] = (i < n && l < n) ? a[l] : ((i == l) ? one<T>() : zero<T>());
+        if (i < n && l < n && l <= i) A[i + (int64_t)l * lda] = a[l];
+    }
+    __syncthreads();
+    rd[i] = one<T>() / L[i][i];
+    __syncthreads();
+    const int j = i;
+    T x[64];
+    #pragma unroll
+    for (int r = 0; r < 64; ++r) {
+        T s = zero<T>();
+        #pragma unroll
+        for (int l = 0; l < r; ++l) s += L[r][l] * x[l];
+        x[r] = (r < j) ? zero<T>() : ((r == j) ? rd[r] : -(s * rd[r]));
+    }
+    #pragma unroll
+    for (int r = 0; r < 64; ++r) W[r + (int64_t)j * ldw] = x[r];
+}
+
+//------------------------------------------------------------------------------
 // Row permutation: for each pair p, row dst[p] of every column receives the
 // value of row src[p] (all reads happen before any write within a column).
 // One 256-thread workgroup per column strip of COLS columns.
@@ -372,6 +428,12 @@ void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset
 }
 
 template <typename T>
+void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int info_offset, hipStream_t s) {
+    if (n <= 0) return;
+    hipLaunchKernelGGL(potrf_inv_small_kernel<T>, dim3(1), dim3(64), 0, s, n, A, lda, W, ldw, info, info_offset);
+}
+
+template <typename T>
 void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
                   const int* npairs, int max_pairs, hipStream_t s) {
     if (n <= 0 || max_pairs <= 0) return;
@@ -399,6 +461,7 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void trtri_diag<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t);   \
     template void trtri_diag_stack<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t); \
     template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \
+    template void potrf_inv_small<T>(int, T*, int64_t, T*, int64_t, int*, int, hipStream_t);                 \
     template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
     template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);  \
     template void rows_pack<T>(int64_t, T*, int64_t, const int64_t*, int, T*, bool, hipStream_t);

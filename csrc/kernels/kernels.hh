@@ -175,6 +175,9 @@ template <typename T>
 void trtri_diag_stack(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t bs, hipStream_t s);
 template <typename T>
 void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s);
+/// Lower Cholesky of an n <= 64 block (in place) plus the 64 x 64 inverse of its factor in W
+template <typename T>
+void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int info_offset, hipStream_t s);
 template <typename T>
 void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
                   const int* npairs, int max_pairs, hipStream_t s);

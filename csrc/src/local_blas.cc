@@ -538,6 +538,34 @@ void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int
     }
     constexpr int64_t NB0 = 64;
     if (n <= NB0) { kd::potrf_small(upc(uplo), int(n), dptr(A), lda, info, int(info_offset), c.stream); return; }
+    static const bool blocked = [] {
+        const char* e = std::getenv("SLATE_POTRF_BLOCKED");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (uplo == Uplo::Lower && blocked) {
+        // Right-looking over 64-column leaves, four launches per leaf: the
+        // leaf's factor and its inverse in one kernel, the rows below as one
+        // GEMM with the inverse (into Y), the trailing triangle as one
+        // triangular GEMM from Y, Y copied back.  The recursive form below
+        // re-inverts every off-diagonal level's triangle (~50 launches for
+        // n = 512 against ~29 here); on the factorization's critical path
+        // each launch waits for a CU slot behind the trailing update.
+        hipStream_t s = c.stream;
+        Scratch sc(c);
+        T* Winv = sc.alloc<T>(size_t(NB0) * NB0);
+        T* Y = sc.alloc<T>(size_t(n) * NB0);
+        for (int64_t j0 = 0; j0 < n; j0 += NB0) {
+            const int64_t b = std::min(NB0, n - j0), r = n - j0 - b;
+            T* Ajj = A + j0 + j0 * lda;
+            kd::potrf_inv_small(int(b), dptr(Ajj), lda, dptr(Winv), NB0, info, int(info_offset + j0), s);
+            if (r == 0) break;
+            T* Ab = Ajj + b;
+            dgemm(s, 'G', Op::NoTrans, Op::ConjTrans, r, b, b, T(1), Ab, lda, Winv, NB0, T(0), Y, r);
+            dgemm(s, 'L', Op::NoTrans, Op::ConjTrans, r, r, b, T(-1), Y, r, Y, r, T(1), Ab + b * lda, lda);
+            dcopy(s, r, b, Y, r, Ab, lda);
+        }
+        return;
+    }
     int64_t n1 = roundup(ceildiv(n, 2), NB0), n2 = n - n1;
     potrf(c, uplo, n1, A, lda, info, info_offset);
     if (uplo == Uplo::Lower) {
