@@ -310,6 +310,54 @@ void potrf_inv_small_kernel(int n, T* A, int64_t lda, T* W, int64_t ldw, int* in
 }
 
 //------------------------------------------------------------------------------
+// Left triangular solve A X = B (NoTrans) with a small triangle (m <= 64):
+// the triangle (identity-padded) and its diagonal reciprocals in LDS, one lane
+// per right-hand-side column holding that column in registers (forward or
+// backward substitution, fully unrolled, wave-uniform LDS broadcasts).  One
+// launch instead of set + trtri_diag + copy + GEMM on the LU panel's
+// recursion, where the narrow blocks' U12 solves are on the critical path.
+template <typename T>
+__global__ __launch_bounds__(64)
+void trsm_small_kernel(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb) {
+    SLATE_PANEL_WAVE_PRIO();
+    __shared__ T L[64][65];
+    __shared__ T rd[64];
+    const int lane = threadIdx.x;
+    for (int j = 0; j < 64; ++j)
+        L[lane][j] = (lane < m && j < m) ? A[lane + (int64_t)j * lda] : (lane == j ? one<T>() : zero<T>());
+    __syncthreads();
+    rd[lane] = (diag == 'U') ? one<T>() : one<T>() / L[lane][lane];
+    __syncthreads();
+    const int64_t col = (int64_t)blockIdx.x * 64 + lane;
+    const bool live = col < n;
+    T x[64];
+    #pragma unroll
+    for (int i = 0; i < 64; ++i) x[i] = (live && i < m) ? B[i + col * ldb] : zero<T>();
+    if (uplo == 'L') {
+        #pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            T s = x[i];
+            #pragma unroll
+            for (int l = 0; l < i; ++l) s -= L[i][l] * x[l];
+            x[i] = s * rd[i];
+        }
+    } else {
+        #pragma unroll
+        for (int i = 63; i >= 0; --i) {
+            T s = x[i];
+            #pragma unroll
+            for (int l = i + 1; l < 64; ++l) s -= L[i][l] * x[l];
+            x[i] = s * rd[i];
+        }
+    }
+    if (live) {
+        #pragma unroll
+        for (int i = 0; i < 64; ++i)
+            if (i < m) B[i + col * ldb] = x[i];
+    }
+}
+
+//------------------------------------------------------------------------------
 // Row permutation: for each pair p, row dst[p] of every column receives the
 // value of row src[p] (all reads happen before any write within a column).
 // One 256-thread workgroup per column strip of COLS columns.
@@ -434,6 +482,13 @@ void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int
 }
 
 template <typename T>
+void trsm_small(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb, hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(trsm_small_kernel<T>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, uplo, diag, m, n, A,
+                       lda, B, ldb);
+}
+
+template <typename T>
 void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
                   const int* npairs, int max_pairs, hipStream_t s) {
     if (n <= 0 || max_pairs <= 0) return;
@@ -462,6 +517,7 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void trtri_diag_stack<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t); \
     template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \
     template void potrf_inv_small<T>(int, T*, int64_t, T*, int64_t, int*, int, hipStream_t);                 \
+    template void trsm_small<T>(char, char, int, int64_t, const T*, int64_t, T*, int64_t, hipStream_t);     \
     template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
     template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);  \
     template void rows_pack<T>(int64_t, T*, int64_t, const int64_t*, int, T*, bool, hipStream_t);

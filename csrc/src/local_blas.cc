@@ -408,6 +408,16 @@ void trtri(Ctx const& c, Uplo uplo, Diag diag, int64_t n, T* A, int64_t lda) {
     kd::gecopy(upc(uplo), 'N', n, n, dptr(W), n, dptr(A), lda, c.stream);
 }
 
+/// small-triangle Left solves in one launch (SLATE_SMALL_TRSM=0: the
+/// inverse + GEMM path)
+inline bool small_trsm() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_SMALL_TRSM");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
+
 /// Left triangular solve with a few right-hand sides (n <= kSkinnyRhs):
 /// every full BS x BS diagonal block inverted at once (batched doubling
 /// GEMMs), then per block one gemv with the inverse and one gemv update of
@@ -460,6 +470,10 @@ void trsm(Ctx const& c, Side side, Uplo uplo, Op op, Diag diag, int64_t m, int64
     if constexpr (is_real_v<T>) { if (op == Op::ConjTrans) op = Op::Trans; }
     hipStream_t s = c.stream;
     if (alpha != T(1)) kd::geadd('G', m, n, dval(alpha), dptr(B), ldb, dval(T(0)), dptr(B), ldb, s);
+    if (side == Side::Left && op == Op::NoTrans && m <= 64 && small_trsm()) {
+        kd::trsm_small(upc(uplo), char(diag), int(m), n, dptr(A), lda, dptr(B), ldb, s);
+        return;
+    }
     if constexpr (is_real_v<T>) {
         if (side == Side::Left && n <= kSkinnyRhs && trsm_skinny(c, uplo, op, diag, m, n, A, lda, B, ldb)) return;
     }

@@ -134,6 +134,26 @@ def test_trsm_skinny_kernel(dtype, uplo, op, diag, m):
     assert relerr(ope @ x, b) < (1e-12 if dtype == np.float64 else 2e-5)
 
 
+@pytest.mark.parametrize("dtype", [np.float64, np.float32])
+@pytest.mark.parametrize("uplo,diag", [("L", "U"), ("L", "N"), ("U", "N"), ("U", "U")])
+@pytest.mark.parametrize("m,nr", [(17, 5), (32, 300), (64, 129)])
+def test_trsm_small_kernel(dtype, uplo, diag, m, nr):
+    """Left NoTrans trsm with a small triangle (m <= 64): one-launch
+    substitution kernel (lane per right-hand-side column) against numpy."""
+    torch = _torch()
+    t = (rnd(m, m, dtype, 16) * 0.3 + 2 * np.eye(m)).astype(dtype)
+    t = np.tril(t) if uplo == "L" else np.triu(t)
+    te = t.astype(np.float64)
+    if diag == "U":
+        np.fill_diagonal(te, 1)
+    b = rnd(m, nr, dtype, 17)
+    tT = torch.from_numpy(np.ascontiguousarray(t.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    s.ops.trsm("L", uplo, "N", diag, dtype(1), tT, tB)
+    x = tB.cpu().numpy().T.astype(np.float64)
+    assert relerr(te @ x, b) < (1e-13 if dtype == np.float64 else 1e-5)
+
+
 @pytest.mark.parametrize("n", [64, 200, 512, 1000])
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_potrf_kernel(n, uplo):
