@@ -447,6 +447,29 @@ def case_norm(tg, dt, nb):
         assert abs(v - ref) <= 1e-4 * ref, (kind, v, ref)
 
 
+def case_norm_masked(tg, dt, nb):
+    """Hermitian and unit-triangular norms (stored triangle only) on the full
+    matrix, a tile-aligned sub-view and an unaligned diagonal slice."""
+    n = 200
+    a = rnd(n, n, dt, 19)
+    a[np.diag_indices(n)] = np.real(np.diag(a))   # Hermitian input: real diagonal
+    A = s.from_numpy(a, nb=nb, target=tg)
+    views = [(A, a), (A.sub(1, 3, 1, 3), a[nb:4 * nb, nb:4 * nb]), (A.slice(10, 149, 10, 149), a[10:150, 10:150])]
+    for V, v in views:
+        for uplo in (s.Uplo.Lower, s.Uplo.Upper):
+            st = np.tril(v) if uplo == s.Uplo.Lower else np.triu(v)
+            h = st + (np.tril(v, -1) if uplo == s.Uplo.Lower else np.triu(v, 1)).conj().T
+            h[np.diag_indices_from(h)] = np.real(np.diag(v))
+            t = (np.tril(v, -1) if uplo == s.Uplo.Lower else np.triu(v, 1)) + np.eye(len(v), dtype=v.dtype)
+            H = s.HermitianMatrix(uplo, V)
+            T = s.TriangularMatrix(uplo, s.Diag.Unit, V)
+            for kind, f in [(s.Norm.One, lambda x: np.linalg.norm(x, 1)), (s.Norm.Inf, lambda x: np.linalg.norm(x, np.inf)),
+                            (s.Norm.Fro, np.linalg.norm), (s.Norm.Max, lambda x: np.abs(x).max())]:
+                for M, ref in ((H, f(h)), (T, f(t))):
+                    val = s.norm(kind, M, target=tg)
+                    assert abs(val - ref) <= 1e-4 * ref, (kind, uplo, val, ref, v.shape)
+
+
 def case_mixed(tg, dt, nb):
     n = 160
     a = rnd(n, n, np.float64, 14) + n * np.eye(n)
