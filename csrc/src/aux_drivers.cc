@@ -659,9 +659,10 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
         Comm& w = As.grid()->world();
         allreduce_host(w, Pc.colsum.data(), Pc.colsum.size(), ReduceOp::Sum);
         allreduce_host(w, Pr.rowsum.data(), Pr.rowsum.size(), ReduceOp::Sum);
-        // diagonal magnitudes (counted in both)
-        std::vector<T> full;
-        std::vector<R> d(As.srows(), 0);
+        // diagonal magnitudes (counted in both); a Hermitian diagonal counts
+        // with its real part only, as LAPACK lanhe does
+        const bool herm = is_complex_v<T> && k != MatrixKind::Symmetric;
+        std::vector<R> d(As.srows(), 0), dre(As.srows(), 0);
         {
             // diagonal: gather via per-tile host reads
             Loc loc = loc_of(target);
@@ -675,12 +676,17 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
                     device::memcpy2d_async(h.data(), sizeof(T), t.data, (t.stride + 1) * sizeof(T), sizeof(T), nd, c.stream);
                     slate_hip_call(hipStreamSynchronize(c.stream));
                 } else for (int64_t ii = 0; ii < nd; ++ii) h[ii] = t.data[ii * (t.stride + 1)];
-                for (int64_t ii = 0; ii < nd; ++ii) d[grow_of(As, i) + ii] = std::abs(h[ii]);
+                for (int64_t ii = 0; ii < nd; ++ii) {
+                    d[grow_of(As, i) + ii] = std::abs(h[ii]);
+                    dre[grow_of(As, i) + ii] = std::abs(std::real(h[ii]));
+                }
             }
             allreduce_host(w, d.data(), d.size(), ReduceOp::Sum);
+            allreduce_host(w, dre.data(), dre.size(), ReduceOp::Sum);
         }
         R v = 0;
-        for (size_t j = 0; j < d.size(); ++j) v = max_nan(v, Pc.colsum[j] + Pr.rowsum[j] - d[j]);
+        for (size_t j = 0; j < d.size(); ++j)
+            v = max_nan(v, herm ? Pc.colsum[j] + Pr.rowsum[j] - 2 * d[j] + dre[j] : Pc.colsum[j] + Pr.rowsum[j] - d[j]);
         return v;
     }
     // Frobenius: 2 * |triangle|^2 - |diag|^2
@@ -688,7 +694,8 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
     local_parts(As, target, 'F', mask, diag, kl, ku, Pt);
     R tri = finish_norm(As, 'F', Pt);
     // diagonal Frobenius
-    NormParts<T> Pd;
+    NormParts<T> Pd, Pdr;
+    const bool herm_f = is_complex_v<T> && k != MatrixKind::Symmetric;
     {
         Loc loc = loc_of(target);
         lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -701,11 +708,16 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
                 device::memcpy2d_async(h.data(), sizeof(T), t.data, (t.stride + 1) * sizeof(T), sizeof(T), nd, c.stream);
                 slate_hip_call(hipStreamSynchronize(c.stream));
             } else for (int64_t ii = 0; ii < nd; ++ii) h[ii] = t.data[ii * (t.stride + 1)];
-            for (int64_t ii = 0; ii < nd; ++ii) add_sumsq(Pd.scale, Pd.sumsq, R(std::abs(h[ii])));
+            for (int64_t ii = 0; ii < nd; ++ii) {
+                add_sumsq(Pd.scale, Pd.sumsq, R(std::abs(h[ii])));
+                add_sumsq(Pdr.scale, Pdr.sumsq, R(std::abs(std::real(h[ii]))));
+            }
         }
     }
     R dg = finish_norm(As, 'F', Pd);
-    R v2 = 2 * tri * tri - dg * dg;
+    // Hermitian: the diagonal counts with its real part only (LAPACK lanhe)
+    R dr = herm_f ? finish_norm(As, 'F', Pdr) : R(0);
+    R v2 = herm_f ? 2 * tri * tri - 2 * dg * dg + dr * dr : 2 * tri * tri - dg * dg;
     return std::sqrt(std::max<R>(v2, 0));
 }
 

@@ -582,11 +582,22 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
     Sched S(target);
     const int R = int(std::max<int64_t>(2, la + 2));
-    std::vector<Work<T>> W(R), WU(R);
+    // SLATE_GETRF_LINV=1: L(k,k)^{-1} once per step, shared by the range
+    // tasks' U solves.  Off by default: neutral for fp64 (same-box A/B, 3450 vs
+    // 3454 ms at n=65536) and, applied to the fp32 factor of dgesv_mixed, the
+    // inverse-based U rows cost accuracy: 24-29 instead of 9 refinement
+    // iterations (profiles/r2_ab_linv.txt)
+    static const bool linv_env = [] {
+        const char* e = std::getenv("SLATE_GETRF_LINV");
+        return e ? std::atoi(e) != 0 : false;
+    }();
+    const bool use_linv = linv_env && target == Target::Devices;
+    std::vector<Work<T>> W(R), WU(R), WI(R);
     std::vector<Work<int64_t>> PV(R);      // [ipiv(kb) | dst(2kb) | src(2kb) | count]
     for (int r = 0; r < R; ++r) {
         W[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
         WU[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
+        WI[r].resize(target, size_t(nb) * nb);
         PV[r].resize(target, size_t(5 * nb + 8));
     }
     Work<int64_t> perm(target, size_t(std::max<int64_t>(m, 1)));
@@ -654,6 +665,16 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             if (q > 1) bcast(g.row(), Wk, size_t(mrows_k * kb), qk, c);
         });
         const int64_t tL = Sched::tok(7, slot);
+        // L(k,k)^{-1} once per step (device): every column range's U solve is
+        // then one GEMM instead of re-inverting the triangle (~10 launches)
+        // in each of the lookahead and trailing tasks
+        T* Lik = WI[slot].data();
+        const int64_t tLi = Sched::tok(12, slot);
+        if (use_linv)
+            S.task(1, {tL}, {tLi}, [&, kd, Wk, Lik, mrows_k](lb::Ctx const& c) {
+                trace::Block t2("getrf_linv");
+                lb::trtri_to(c, Uplo::Lower, Diag::Unit, kd, Wk, std::max<int64_t>(mrows_k, 1), Lik, kd);
+            });
 
         // -------------------------------------- column ranges: permute, U, update
         // apply the step's row permutation to local columns [c0, c1)
@@ -679,10 +700,19 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         T* WUk = WU[slot].data();
         // U row height is kd = tileMb(k) (< kb only for the last block row of a
         // wide matrix; rows beyond it are not part of the matrix)
-        auto urow = [&, kd, lr_k, Wk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        auto urow = [&, kd, lr_k, Wk, Lik, WUk, use_linv](lb::Ctx const& c, int64_t j0, int64_t j1) {
             auto cc = lcols(j0, j1);
             int64_t c0 = cc.first, c1 = cc.second;
             if (c1 <= c0) return;
+            if (use_linv) {
+                // U = L^{-1} A(k, cols) through a copy in this range's slice of WU
+                const int64_t nc = c1 - c0;
+                T* Ac = a + lr_k + c0 * lda;
+                T* tmp = WUk + c0 * kd;
+                lb::copy2d(c, kd, nc, Ac, lda, tmp, kd);
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, kd, nc, kd, T(1), Lik, kd, tmp, kd, T(0), Ac, lda);
+                return;
+            }
             // U(k, j0:j1) = L(k,k)^{-1} A(k, j0:j1); L(k,k) = top kd rows of W_k
             lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, c1 - c0, T(1),
                      Wk, std::max<int64_t>(mrows_k, 1), a + lr_k + c0 * lda, lda);
@@ -710,6 +740,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             std::vector<int64_t> cols;
             for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
             std::vector<int64_t> in = {tBc, tL};
+            if (use_linv) in.push_back(tLi);
             S.task(queue, in, cols, [&, j0, j1](lb::Ctx const& c) {
                 auto cc = lcols(j0, j1);
                 permute(c, cc.first, cc.second);
