@@ -1104,6 +1104,12 @@ Result r_aux(Case<T>& c, int variant) {   // 0 add, 1 copy, 2 scale, 3 set, 4 tr
             if (c.P.check) {
                 BaseTrapezoidMatrix<T> Hs(Uplo::Lower, A, MatrixKind::Trapezoid);
                 auto F = full_of(c, Hs, true);
+                // the Hermitian matrix the stored triangle stands for has a
+                // real diagonal (LAPACK lanhe reads only its real part):
+                // F = (F + F^H) / 2 keeps the off-diagonal, drops Im(diag)
+                auto Ft = c.zeros(c.n, c.n);
+                copy<T, T>(conj_transpose(F), Ft, c.opts);
+                add(T(0.5), Ft, T(0.5), F, c.opts);
                 r.error = std::abs(double(v1) - c.nrm(F)) / c.nrm(F);
             }
             break;
