@@ -21,6 +21,12 @@
 #include "device_common.hh"
 #include "kernels.hh"
 
+// the many-workgroup tree kernels (qr_node / qr_node_q) may opt out of the
+// panel wave priority (A/B builds: SLATE_QR_NODE_PRIO=0)
+#ifndef SLATE_QR_NODE_PRIO
+#define SLATE_QR_NODE_PRIO 1
+#endif
+
 namespace slate_amd {
 namespace dev {
 
@@ -216,7 +222,7 @@ __device__ inline T wave_reduce_scatter32(T (&q)[TW]) {
 template <typename T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) void qr_node_kernel(
         int64_t rows, int nn, const T* In, int64_t ldi, T* Vout, int64_t ldv, T* Rout, int64_t ldr, T* Tout) {
-    SLATE_PANEL_WAVE_PRIO();
+    if (SLATE_QR_NODE_PRIO) SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
     __shared__ R red[2][4];
     __shared__ T wred[4][TW];
@@ -317,7 +323,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1, 1))) voi
 template <typename T>
 __global__ __launch_bounds__(256) void qr_node_q_kernel(int64_t rows, int nn, const T* V, int64_t ldv,
                                                         const T* Tin, const T* E, int64_t lde, T* Q, int64_t ldq) {
-    SLATE_PANEL_WAVE_PRIO();
+    if (SLATE_QR_NODE_PRIO) SLATE_PANEL_WAVE_PRIO();
     __shared__ T sE[TW][TW + 1], sV1[TW][TW + 1], sW[TW][TW + 1], sT[TW][TW + 1];
     const int tid = threadIdx.x;
     const int64_t row0 = blockIdx.x * (int64_t)256;

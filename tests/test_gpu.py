@@ -47,6 +47,20 @@ def test_gemm_kernel(dtype, ta, tb):
     assert relerr(tC.cpu().numpy().T, ref) < tol(dtype)
 
 
+@pytest.mark.parametrize("k", [256, 512, 2048])
+def test_gemm_nn_rank_nb_packed(k):
+    """Rank-nb NN products (m >= 4096, n >= 1024, 256 <= K <= 2048) run as NT
+    products on a transposed copy of B (local_blas.cc dgemm); against numpy."""
+    torch = _torch()
+    m, n = 4160, 1100
+    a, b, c = rnd(m, k, np.float64, 21), rnd(k, n, np.float64, 22), rnd(m, n, np.float64, 23)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
+    s.ops.gemm("N", "N", 1.5, tA, tB, -0.5, tC)
+    assert relerr(tC.cpu().numpy().T, 1.5 * a @ b - 0.5 * c) < 1e-13
+
+
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_herk_kernel(dtype, uplo):
