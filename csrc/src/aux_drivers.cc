@@ -648,6 +648,38 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
     }
     // symmetric/Hermitian from one triangle
     if (kind == 'M') {
+        const int64_t n = std::min(As.srows(), As.scols());
+        if (is_complex_v<T> && k == MatrixKind::Hermitian && kl < 0 && n > 1) {
+            // Hermitian: the diagonal counts with its real part only (LAPACK
+            // lanhe): max over the strict triangle (a shifted slice of the
+            // stored one) and the |Re| of the diagonal
+            BaseMatrix<T> St = mask == Uplo::Lower ? As.slice(1, n - 1, 0, n - 2) : As.slice(0, n - 2, 1, n - 1);
+            NormParts<T> P;
+            local_parts(St, target, 'M', mask, diag, kl, ku, P);
+            R v = finish_norm(St, 'M', P);
+            Loc loc = loc_of(target);
+            lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+            R dmax = 0;
+            for (int64_t i = 0; i < std::min(As.mt(), As.nt()); ++i) {
+                if (!As.tileIsLocal(i, i)) continue;
+                Tile<T> t = As.tile(i, i, loc);
+                int64_t nd = std::min(t.mb, t.nb);
+                std::vector<T> h(nd);
+                if (c.dev()) {
+                    device::memcpy2d_async(h.data(), sizeof(T), t.data, (t.stride + 1) * sizeof(T), sizeof(T), nd, c.stream);
+                    slate_hip_call(hipStreamSynchronize(c.stream));
+                } else for (int64_t ii = 0; ii < nd; ++ii) h[ii] = t.data[ii * (t.stride + 1)];
+                for (int64_t ii = 0; ii < nd; ++ii) dmax = max_nan(dmax, R(std::abs(std::real(h[ii]))));
+            }
+            Comm& w = As.grid()->world();
+            if (w.size() > 1) {
+                R nanflag = std::isnan(dmax) ? R(1) : R(0);
+                nanflag = w.allreduce_scalar<R>(nanflag, ReduceOp::Max);
+                dmax = w.allreduce_scalar<R>(std::isnan(dmax) ? R(0) : dmax, ReduceOp::Max);
+                if (nanflag > 0) dmax = std::numeric_limits<R>::quiet_NaN();
+            }
+            return max_nan(v, dmax);
+        }
         NormParts<T> P;
         local_parts(As, target, 'M', mask, diag, kl, ku, P);
         return finish_norm(As, 'M', P);
