@@ -3,7 +3,7 @@
 # priority; tree build = priority on, alt/ = SLATE_QR_NODE_PRIO=0; interleaved.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out/abqrn
-timeout -k 10 300 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 -k "gemm or geqrf or gels" > gpurun_out/abqrn/tests.log 2>&1 || { tail -30 gpurun_out/abqrn/tests.log; exit 1; }
+timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 280 -k "gemm or geqrf or gels or norm" > gpurun_out/abqrn/tests.log 2>&1 || { tail -30 gpurun_out/abqrn/tests.log; exit 1; }
 tail -1 gpurun_out/abqrn/tests.log
 for v in on off on2 off2; do
   B=bench.py; case $v in off*) B=alt/bench.py;; esac
