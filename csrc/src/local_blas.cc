@@ -165,6 +165,27 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
             }
             (void)hipGetLastError();
         }
+        // Long-K NN products as TN on a transposed copy of A (one streaming
+        // pass): both operands K-contiguous, on the rotated 8-wave tile.
+        // Same-box A/B at n = m = k = 65536 including the copy: 8172 -> 7900
+        // ms, 68.9 -> 71.3 TFLOP/s (profiles/r2_ab_gemm_pack_a.txt); the NT
+        // form (copy of B) measured slower there.  SLATE_GEMM_PACK_A=0: NN.
+        static const bool pack_a = [] {
+            const char* e = std::getenv("SLATE_GEMM_PACK_A");
+            return e ? std::atoi(e) != 0 : true;
+        }();
+        if (pack_a && uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && k > 2048 && m >= 4096 && n >= 4096) {
+            const size_t bytes = size_t(m) * size_t(k) * sizeof(T);
+            size_t fr = 0, tot = 0;
+            if (hipMemGetInfo(&fr, &tot) == hipSuccess && 2 * bytes < fr) {
+                T* At = static_cast<T*>(device::malloc(bytes));
+                kd::gecopy<T, T>('G', 'T', k, m, A, lda, At, k, s);
+                kd::gemm_real<T>('T', 'N', m, n, k, alpha, At, k, 0, B, ldb, 0, beta, C, ldc, 0, 1, s);
+                device::free(At);
+                return;
+            }
+            (void)hipGetLastError();
+        }
         // K-chunked launches for large updates (SLATE_GEMM_KCHUNK): shorter
         // workgroups free CU slots for the high-priority panel queue sooner
         static const int64_t kchunk = [] {
