@@ -592,12 +592,21 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         return e ? std::atoi(e) != 0 : false;
     }();
     const bool use_linv = linv_env && target == Target::Devices;
-    std::vector<Work<T>> W(R), WU(R), WI(R);
+    // SLATE_UPDATE_TN=1: trailing update as a TN product against a once-per-
+    // step transposed copy of L21 (both operands K-contiguous, rotated 8-wave
+    // MFMA tile) instead of the NT form
+    static const bool tn_env = [] {
+        const char* e = std::getenv("SLATE_UPDATE_TN");
+        return e && std::atoi(e) != 0;
+    }();
+    const bool use_tn = tn_env && !is_complex_v<T> && target == Target::Devices;
+    std::vector<Work<T>> W(R), WU(R), WI(R), WLT(R);
     std::vector<Work<int64_t>> PV(R);      // [ipiv(kb) | dst(2kb) | src(2kb) | count]
     for (int r = 0; r < R; ++r) {
         W[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
         WU[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         WI[r].resize(target, size_t(nb) * nb);
+        if (use_tn) WLT[r].resize(target, size_t(nb) * std::max<int64_t>(mloc, 1));
         PV[r].resize(target, size_t(5 * nb + 8));
     }
     Work<int64_t> perm(target, size_t(std::max<int64_t>(m, 1)));
@@ -668,6 +677,14 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         // L(k,k)^{-1} once per step (device): every column range's U solve is
         // then one GEMM instead of re-inverting the triangle (~10 launches)
         // in each of the lookahead and trailing tasks
+        T* Ltk = use_tn ? WLT[slot].data() : nullptr;
+        const int64_t tLt = Sched::tok(13, slot);
+        if (use_tn && mloc > lr_k1)
+            S.task(1, {tL}, {tLt}, [&, kd, Wk, Ltk, mrows_k, lr_k, lr_k1](lb::Ctx const& c) {
+                trace::Block t2("getrf_lt");
+                lb::copy<T, T>(c, Uplo::General, Op::Trans, kd, mloc - lr_k1, Wk + (lr_k1 - lr_k),
+                               std::max<int64_t>(mrows_k, 1), Ltk, kd);
+            });
         T* Lik = WI[slot].data();
         const int64_t tLi = Sched::tok(12, slot);
         if (use_linv)
@@ -717,12 +734,17 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, kd, c1 - c0, T(1),
                      Wk, std::max<int64_t>(mrows_k, 1), a + lr_k + c0 * lda, lda);
         };
-        auto update = [&, kb, kd, lr_k1, lr_k, Wk, WUk](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        auto update = [&, kb, kd, lr_k1, lr_k, Wk, WUk, Ltk, use_tn](lb::Ctx const& c, int64_t j0, int64_t j1) {
             auto cc = lcols(j0, j1);
             int64_t c0 = cc.first, nc = cc.second - cc.first, nr = mloc - lr_k1;
             if (nc <= 0 || nr <= 0) return;
             trace::Block t2("getrf_update");
             // U rows of these columns live in A itself (process row 0 owns them)
+            if (use_tn) {
+                lb::gemm(c, Op::Trans, Op::NoTrans, nr, nc, kd, T(-1), Ltk, kd, a + lr_k + c0 * lda, lda, T(1),
+                         a + lr_k1 + c0 * lda, lda);
+                return;
+            }
             if (!is_complex_v<T> && c.dev() && update_nt()) {
                 // NT product against U^T (nc x kd, ld nc) in this range's own
                 // slice of the slot's WU buffer
@@ -741,6 +763,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
             std::vector<int64_t> in = {tBc, tL};
             if (use_linv) in.push_back(tLi);
+            if (use_tn && mloc > lr_k1) in.push_back(tLt);
             S.task(queue, in, cols, [&, j0, j1](lb::Ctx const& c) {
                 auto cc = lcols(j0, j1);
                 permute(c, cc.first, cc.second);
