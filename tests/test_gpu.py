@@ -47,6 +47,19 @@ def test_gemm_kernel(dtype, ta, tb):
     assert relerr(tC.cpu().numpy().T, ref) < tol(dtype)
 
 
+def test_gemm_nn_long_k_packed_a():
+    """Long-K NN products (K > 2048, m, n >= 4096) run as TN on a transposed
+    copy of A (local_blas.cc dgemm); against numpy."""
+    torch = _torch()
+    m, n, k = 4200, 4100, 2300
+    a, b, c = rnd(m, k, np.float64, 24), rnd(k, n, np.float64, 25), rnd(m, n, np.float64, 26)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
+    s.ops.gemm("N", "N", 0.75, tA, tB, 2.0, tC)
+    assert relerr(tC.cpu().numpy().T, 0.75 * a @ b + 2.0 * c) < 1e-13
+
+
 @pytest.mark.parametrize("k", [256, 512, 2048])
 def test_gemm_nn_rank_nb_packed(k):
     """Rank-nb NN products (m >= 4096, n >= 1024, 256 <= K <= 2048) run as NT
