@@ -63,6 +63,14 @@ void event_put(hipEvent_t e);
 /// kernels.
 void* malloc(size_t bytes);
 void  free(void* ptr);
+/// Stream-ordered scratch: a block freed with free_async(p, s) is only
+/// handed out again by malloc_async(.., s) on the same stream (stream order
+/// makes immediate reuse safe), so per-call scratch of a kernel sequence on
+/// one stream never reaches hipMalloc after the first call.  The block must
+/// not be used by any other stream.
+void* malloc_async(size_t bytes, hipStream_t s);
+void  free_async(void* ptr, hipStream_t s);
+size_t bytes_stream_cached();
 void* malloc_host(size_t bytes);   // pinned host memory
 void  free_host(void* ptr);
 /// Release all cached (unused) blocks back to HIP.

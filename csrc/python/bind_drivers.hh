@@ -140,6 +140,8 @@ void bind_drivers(py::module_& m, std::string const& s) {
         Options op = to_options(o); py::gil_scoped_release r; return getrf_nopiv(A, op); });
     DEF("getrs", [=](Matrix<T> const& A, py::list piv, Matrix<T>& B, py::dict o) {
         Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; getrs(A, P, B, op); });
+    DEF("getrs_op", [=](Op trans, Matrix<T> const& A, py::list piv, Matrix<T>& B, py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; getrs(trans, A, P, B, op); });
     DEF("getrs_nopiv", [](Matrix<T> const& A, Matrix<T>& B, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; getrs_nopiv(A, B, op); });
     DEF("gesv", [=](Matrix<T>& A, Matrix<T>& B, py::dict o) {

@@ -649,14 +649,18 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
     // symmetric/Hermitian from one triangle
     if (kind == 'M') {
         const int64_t n = std::min(As.srows(), As.scols());
-        if (is_complex_v<T> && k == MatrixKind::Hermitian && kl < 0 && n > 1) {
+        if (is_complex_v<T> && k == MatrixKind::Hermitian && kl < 0 && n >= 1) {
             // Hermitian: the diagonal counts with its real part only (LAPACK
             // lanhe): max over the strict triangle (a shifted slice of the
             // stored one) and the |Re| of the diagonal
-            BaseMatrix<T> St = mask == Uplo::Lower ? As.slice(1, n - 1, 0, n - 2) : As.slice(0, n - 2, 1, n - 1);
-            NormParts<T> P;
-            local_parts(St, target, 'M', mask, diag, kl, ku, P);
-            R v = finish_norm(St, 'M', P);
+            // (n == 1: the strict triangle is empty)
+            R v = 0;
+            if (n > 1) {
+                BaseMatrix<T> St = mask == Uplo::Lower ? As.slice(1, n - 1, 0, n - 2) : As.slice(0, n - 2, 1, n - 1);
+                NormParts<T> P;
+                local_parts(St, target, 'M', mask, diag, kl, ku, P);
+                v = finish_norm(St, 'M', P);
+            }
             Loc loc = loc_of(target);
             lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
             R dmax = 0;

@@ -26,6 +26,12 @@ struct State {
     // before the free on every queue (and the null stream) has drained
     struct Pending { void* p; size_t b; std::vector<hipEvent_t> ev; };
     std::deque<Pending> pending;
+    // stream-private free lists (free_async): a block freed on stream s is
+    // reused at once by the next malloc_async on s -- stream order makes that
+    // safe without waiting for an event
+    std::map<hipStream_t, std::multimap<size_t, void*>> stream_free;
+    std::map<void*, hipStream_t> live_stream;      // blocks from malloc_async
+    size_t stream_cached = 0;
     std::map<void*, size_t> host_live;   // pinned host blocks
     size_t host_in_use = 0;
 };
@@ -190,12 +196,21 @@ void event_put(hipEvent_t e) {
     s.events.push_back(e);
 }
 
-void* malloc(size_t bytes) {
-    auto& s = st();
-    std::lock_guard<std::mutex> g(s.mtx);
-    ensure_device_locked(s);
+namespace {
+/// stream-private blocks back to the shared cache (every queue drained first)
+void flush_stream_free_locked(State& s) {
+    if (s.stream_free.empty()) return;
+    if (s.streams_ready)
+        for (int i = 0; i < kNumQueues; ++i) slate_hip_call(hipStreamSynchronize(s.streams[i]));
+    slate_hip_call(hipStreamSynchronize(nullptr));
+    for (auto& kv : s.stream_free)
+        for (auto& b : kv.second) { s.free_blocks.emplace(b.first, b.second); s.cached += b.first; }
+    s.stream_free.clear();
+    s.stream_cached = 0;
+}
+
+void* malloc_locked(State& s, size_t b) {
     if (!s.pending.empty()) reclaim_locked(s, false);
-    size_t b = bucket(bytes);
     auto it = s.free_blocks.find(b);
     void* p = nullptr;
     if (it != s.free_blocks.end()) {
@@ -205,9 +220,10 @@ void* malloc(size_t bytes) {
     } else {
         hipError_t e = hipMalloc(&p, b);
         if (e != hipSuccess) {
-            // release the cache and retry once
+            // release every cache and retry once
             (void)hipGetLastError();
             reclaim_locked(s, true);
+            flush_stream_free_locked(s);
             for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
             s.free_blocks.clear();
             s.cached = 0;
@@ -218,6 +234,52 @@ void* malloc(size_t bytes) {
     s.in_use += b;
     return p;
 }
+}  // namespace
+
+void* malloc(size_t bytes) {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_device_locked(s);
+    return malloc_locked(s, bucket(bytes));
+}
+
+void* malloc_async(size_t bytes, hipStream_t stream) {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_device_locked(s);
+    const size_t b = bucket(bytes);
+    void* p = nullptr;
+    auto sf = s.stream_free.find(stream);
+    if (sf != s.stream_free.end()) {
+        auto it = sf->second.find(b);
+        if (it != sf->second.end()) {
+            p = it->second;
+            sf->second.erase(it);
+            s.stream_cached -= b;
+            s.live[p] = b;
+            s.in_use += b;
+        }
+    }
+    if (!p) p = malloc_locked(s, b);
+    s.live_stream[p] = stream;
+    return p;
+}
+
+void free_async(void* ptr, hipStream_t stream) {
+    if (!ptr) return;
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    auto it = s.live.find(ptr);
+    slate_assert(it != s.live.end());
+    const size_t b = it->second;
+    s.live.erase(it);
+    s.live_stream.erase(ptr);
+    s.in_use -= b;
+    s.stream_free[stream].emplace(b, ptr);
+    s.stream_cached += b;
+}
+
+size_t bytes_stream_cached() { return st().stream_cached; }
 
 void free(void* ptr) {
     if (!ptr) return;
@@ -227,6 +289,7 @@ void free(void* ptr) {
     slate_assert(it != s.live.end());
     size_t b = it->second;
     s.live.erase(it);
+    s.live_stream.erase(ptr);
     s.in_use -= b;
     if (!s.streams_ready) {
         // no queue ever ran: only synchronous (null-stream) use is possible
@@ -250,6 +313,7 @@ void release_cache() {
     auto& s = st();
     std::lock_guard<std::mutex> g(s.mtx);
     reclaim_locked(s, true);
+    flush_stream_free_locked(s);
     for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
     s.free_blocks.clear();
     s.cached = 0;

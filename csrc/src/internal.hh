@@ -149,6 +149,23 @@ template <typename T>
 Matrix<T> bc_operand(BaseMatrix<T> const& A, Options const& opts) {
     return A.arbitrary_layout() ? block_cyclic(A, opts) : Matrix<T>(A);
 }
+/// Block-cyclic copy of B whose row tiles are those of the (block-cyclic)
+/// factor F, on F's grid: the right-hand side of a solve with F's factors.
+template <typename T>
+Matrix<T> block_cyclic_rows_of(BaseMatrix<T> const& F, BaseMatrix<T> const& B, Options const& opts) {
+    Matrix<T> Bb(B.m(), B.n(), F.mb(), F.mb(), F.grid());
+    Bb.insertLocalTiles(resolve_target(opts));
+    slate::copy<T, T>(B, Bb, opts);
+    return Bb;
+}
+/// Pivots / T factors of an arbitrary-layout matrix are expressed in the
+/// tiling of its block-cyclic working copy (block_cyclic(), tile size = the
+/// largest tile of A), which is deterministic; the solve-side drivers (getrs,
+/// getri, unmqr, unmlq) re-create that copy, so factor and solve agree.
+template <typename T>
+bool needs_bc(BaseMatrix<T> const& A, BaseMatrix<T> const& B) {
+    return A.arbitrary_layout() || B.arbitrary_layout();
+}
 
 /// Broadcast a contiguous buffer over `comm` from `root` (stream-ordered).
 template <typename T>

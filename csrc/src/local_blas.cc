@@ -152,39 +152,42 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
         // geqrf trailing updates (same-box A/B, K = 512-1024: -1.7% time).
         // Not for long K: n = k = 65536 measured 68.7 (NN) -> 66.5 (NT)
         // TFLOP/s (profiles/r2_ab_prio_gemm_nt.txt).
+        // (the copy is n x k <= n x 2048: bounded scratch, stream-ordered
+        // reuse, so steady-state calls never reach hipMalloc)
         if (uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && nt_pack() && m >= 4096 &&
             n >= 1024 && k >= 256 && k <= 2048) {
             const size_t bytes = size_t(n) * size_t(k) * sizeof(T);
-            size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess && 2 * bytes < fr) {
-                T* Bt = static_cast<T*>(device::malloc(bytes));
-                kd::gecopy<T, T>('G', 'T', n, k, B, ldb, Bt, n, s);
-                kd::gemm_real<T>('N', 'T', m, n, k, alpha, A, lda, 0, Bt, n, 0, beta, C, ldc, 0, 1, s);
-                device::free(Bt);
-                return;
-            }
-            (void)hipGetLastError();
+            T* Bt = static_cast<T*>(device::malloc_async(bytes, s));
+            kd::gecopy<T, T>('G', 'T', n, k, B, ldb, Bt, n, s);
+            kd::gemm_real<T>('N', 'T', m, n, k, alpha, A, lda, 0, Bt, n, 0, beta, C, ldc, 0, 1, s);
+            device::free_async(Bt, s);
+            return;
         }
         // Long-K NN products as TN on a transposed copy of A (one streaming
         // pass): both operands K-contiguous, on the rotated 8-wave tile.
         // Same-box A/B at n = m = k = 65536 including the copy: 8172 -> 7900
         // ms, 68.9 -> 71.3 TFLOP/s (profiles/r2_ab_gemm_pack_a.txt); the NT
         // form (copy of B) measured slower there.  SLATE_GEMM_PACK_A=0: NN.
+        // The copy is made in K slices of at most pack_bytes() (default
+        // 8 GiB; later slices accumulate with beta = 1), so the scratch is
+        // bounded independently of k and of the free HBM.
         static const bool pack_a = [] {
             const char* e = std::getenv("SLATE_GEMM_PACK_A");
             return e ? std::atoi(e) != 0 : true;
         }();
         if (pack_a && uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && k > 2048 && m >= 4096 && n >= 4096) {
-            const size_t bytes = size_t(m) * size_t(k) * sizeof(T);
-            size_t fr = 0, tot = 0;
-            if (hipMemGetInfo(&fr, &tot) == hipSuccess && 2 * bytes < fr) {
-                T* At = static_cast<T*>(device::malloc(bytes));
-                kd::gecopy<T, T>('G', 'T', k, m, A, lda, At, k, s);
-                kd::gemm_real<T>('T', 'N', m, n, k, alpha, At, k, 0, B, ldb, 0, beta, C, ldc, 0, 1, s);
-                device::free(At);
-                return;
+            const char* be = std::getenv("SLATE_GEMM_PACK_BYTES");
+            const size_t budget = be ? size_t(std::atoll(be)) : (size_t(8) << 30);
+            const int64_t kc = std::min<int64_t>(k, std::max<int64_t>(2048, int64_t(budget / (size_t(m) * sizeof(T))) / 256 * 256));
+            T* At = static_cast<T*>(device::malloc_async(size_t(m) * size_t(kc) * sizeof(T), s));
+            for (int64_t k0 = 0; k0 < k; k0 += kc) {
+                const int64_t kk = std::min(kc, k - k0);
+                kd::gecopy<T, T>('G', 'T', kk, m, A + k0 * lda, lda, At, kk, s);
+                kd::gemm_real<T>('T', 'N', m, n, kk, alpha, At, kk, 0, B + k0, ldb, 0, k0 == 0 ? beta : T(1), C, ldc, 0,
+                                 1, s);
             }
-            (void)hipGetLastError();
+            device::free_async(At, s);
+            return;
         }
         // K-chunked launches for large updates (SLATE_GEMM_KCHUNK): shorter
         // workgroups free CU slots for the high-priority panel queue sooner
@@ -193,7 +196,8 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
             return e ? std::max<int64_t>(0, std::atoll(e)) : int64_t(0);
         }();
         const bool chunk = kchunk > 0 && k > kchunk && m * n >= int64_t(4096) * 4096;
-        for (int64_t k0 = 0; k0 < k; k0 += chunk ? kchunk : k) {
+        // k == 0 still runs once: C = beta C (BLAS semantics)
+        for (int64_t k0 = 0; k0 < std::max<int64_t>(k, 1); k0 += chunk ? kchunk : std::max<int64_t>(k, 1)) {
             const int64_t kk = chunk ? std::min(kchunk, k - k0) : k;
             T const* Ak = A + (ta == 'N' ? k0 * lda : k0);
             T const* Bk = B + (tb == 'N' ? k0 : k0 * ldb);

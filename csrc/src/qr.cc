@@ -414,6 +414,12 @@ void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
 
 template <typename T>
 void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        // T is expressed in the tiling of A's block-cyclic working copy
+        Matrix<T> Ab = internal::block_cyclic(A, opts);
+        unmqr(side, op, Ab, T_, C, opts);
+        return;
+    }
     trace::Block tb("unmqr");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);

@@ -29,6 +29,14 @@ TriangularMatrix<T> tri(Uplo u, Diag d, BaseMatrix<T> const& A) {
 //------------------------------------------------------------------------------
 template <typename T>
 void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
+    if (needs_bc(A, B)) {
+        // factors of an arbitrary-layout A live in its block-cyclic tiling
+        Matrix<T> Ab = bc_operand(A, opts);
+        Matrix<T> Bb = block_cyclic_rows_of(Ab, B, opts);
+        getrs(Ab, pivots, Bb, opts);
+        slate::copy<T, T>(Bb, B, opts);
+        return;
+    }
     trace::Block tb("getrs");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -42,6 +50,13 @@ void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const
 template <typename T>
 void getrs(Op trans, Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
     if (trans == Op::NoTrans) { getrs(A, pivots, B, opts); return; }
+    if (needs_bc(A, B)) {
+        Matrix<T> Ab = bc_operand(A, opts);
+        Matrix<T> Bb = block_cyclic_rows_of(Ab, B, opts);
+        getrs(trans, Ab, pivots, Bb, opts);
+        slate::copy<T, T>(Bb, B, opts);
+        return;
+    }
     trace::Block tb("getrs_trans");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -192,6 +207,12 @@ int64_t potri(HermitianMatrix<T>& A, Options const& opts) {
 
 template <typename T>
 int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> Ab = internal::block_cyclic(A, opts);
+        int64_t info = getri(Ab, pivots, opts);
+        slate::copy<T, T>(Ab, A, opts);
+        return info;
+    }
     trace::Block tb("getri");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);

@@ -25,6 +25,7 @@
 #include <netinet/in.h>
 #include <netinet/tcp.h>
 #include <sys/socket.h>
+#include <sys/time.h>
 #include <unistd.h>
 
 #include <algorithm>
@@ -65,6 +66,15 @@ bool read_all(int fd, void* p, size_t n) {
         c += r; n -= size_t(r);
     }
     return true;
+}
+
+/// receive timeout on a socket (0 = none): a stray connection that sends
+/// nothing cannot block a rendezvous / mesh accept forever
+void set_rcv_timeout(int fd, double seconds) {
+    timeval tv{};
+    tv.tv_sec = time_t(seconds);
+    tv.tv_usec = suseconds_t((seconds - double(tv.tv_sec)) * 1e6);
+    ::setsockopt(fd, SOL_SOCKET, SO_RCVTIMEO, &tv, sizeof(tv));
 }
 
 int env_int(const char* name, int dflt) {
@@ -179,6 +189,7 @@ public:
                 socklen_t len = sizeof(a);
                 int fd = ::accept(rfd, reinterpret_cast<sockaddr*>(&a), &len);
                 if (fd < 0) sys_fail("accept (rendezvous)");
+                set_rcv_timeout(fd, std::min(timeout_s, 10.0));
                 Hello h{};
                 // wrong token, bad or duplicate rank: drop the connection
                 if (!read_all(fd, &h, sizeof(h)) || h.token != token || h.rank <= 0 || h.rank >= size_ ||
@@ -186,6 +197,7 @@ public:
                     ::close(fd);
                     continue;
                 }
+                set_rcv_timeout(fd, 0);
                 seen[h.rank] = 1;
                 ips[h.rank] = a.sin_addr.s_addr;
                 ports[h.rank] = h.port;
@@ -225,12 +237,14 @@ public:
             if (fd < 0) sys_fail("accept (mesh)");
             int one = 1;
             ::setsockopt(fd, IPPROTO_TCP, TCP_NODELAY, &one, sizeof(one));
+            set_rcv_timeout(fd, std::min(timeout_s, 10.0));
             Hello h{};
             if (!read_all(fd, &h, sizeof(h)) || h.token != token || h.rank <= rank_ || h.rank >= size_ ||
                 peers_[h.rank].fd >= 0) {
                 ::close(fd);   // not a peer of this job (or a duplicate rank)
                 continue;
             }
+            set_rcv_timeout(fd, 0);   // the receiver thread blocks for the job's lifetime
             peers_[h.rank].fd = fd;
             ++n;
         }

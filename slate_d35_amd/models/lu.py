@@ -1,5 +1,6 @@
 """LU family (reference src/getrf*.cc, getrs*.cc, gesv*.cc, getri*.cc,
 gecondest.cc, trtri.cc, trtrm.cc, trcondest.cc)."""
+from .. import _slate
 from ._wrap import call
 
 __all__ = ["getrf", "getrf_nopiv", "getrf_tntpiv", "getrs", "getrs_nopiv", "gesv", "gesv_nopiv",
@@ -26,7 +27,11 @@ def getrf_tntpiv(A, target=None, **kw):
     return call("getrf_tntpiv", A, A, target=target, **kw)
 
 
-def getrs(A, pivots, B, target=None, **kw):
+def getrs(A, pivots, B, target=None, trans=None, **kw):
+    """op(A) X = B with the getrf factors (trans: Op.NoTrans / Trans / ConjTrans)."""
+    if trans is not None and int(trans) != int(_slate.Op.NoTrans):
+        call("getrs_op", A, trans, A, pivots, B, target=target, **kw)
+        return
     call("getrs", A, A, pivots, B, target=target, **kw)
 
 

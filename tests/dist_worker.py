@@ -296,6 +296,30 @@ def case_layout(tg, dt, nb):
     B = lay(bm, cs, [20, 20])
     info, _ = s.gesv(G, B, target=tg)
     assert info == 0 and relerr((a + n * np.eye(n)) @ back(B), bm) < 10 * tol(dt)
+    # getrf then getrs / getri as separate calls, max tileNb (50) > max
+    # tileMb (40), arbitrary-layout right-hand side with its own row tiling
+    ad = a + 0.1 * np.eye(n, dtype=dt)
+    G = lay(ad, rs, cs)
+    info, piv = s.getrf(G, target=tg)
+    assert info == 0
+    B = lay(bm, [60, 45, 45], [40])
+    s.getrs(G, piv, B, target=tg)
+    assert relerr(ad @ back(B), bm) < 1e3 * tol(dt)
+    B = lay(bm, cs, [40])
+    s.getrs(G, piv, B, target=tg, trans=s.Op.Trans)
+    assert relerr(ad.T @ back(B), bm) < 1e3 * tol(dt)
+    s.getri(G, piv, target=tg)
+    assert relerr(back(G) @ ad, np.eye(n)) < 1e3 * tol(dt)
+    # geqrf then unmqr on an arbitrary-layout A and C
+    Q = lay(a, rs, cs)
+    T = s.geqrf(Q, target=tg)
+    C = lay(bm, cs, [40])
+    s.unmqr(s.Side.Left, s.Op.ConjTrans, Q, T, C, target=tg)
+    r = np.triu(back(Q))
+    qhb = back(C)
+    # Q^H b has the norm of b column by column, and R^{-1} (Q^H b) solves a x = b
+    x = np.linalg.solve(r, qhb)
+    assert relerr(a @ x, bm) < 1e4 * tol(dt)
 
 
 def case_aasen(tg, dt, nb):

@@ -66,3 +66,15 @@ def test_masked_norms_whole_block(tg):
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "masked_norm_check.py"), tg],
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "masked norms ok" in r.stdout, r.stdout + r.stderr
+
+
+@pytest.mark.parametrize("n", [1, 2, 5])
+def test_hermitian_max_norm_real_diagonal(n):
+    """lanhe semantics: the Hermitian Max norm reads only Re of the diagonal,
+    also for n == 1 (empty strict triangle)."""
+    a = np.zeros((n, n), np.complex128)
+    a[np.tril_indices(n, -1)] = 0.5 + 0.25j
+    np.fill_diagonal(a, 0.75 + 3.0j)      # imaginary part must be ignored
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=2, grid=grid()))
+    v = s.norm(s.Norm.Max, H, target="h")
+    assert abs(v - 0.75) < 1e-15

@@ -47,6 +47,27 @@ def test_gemm_kernel(dtype, ta, tb):
     assert relerr(tC.cpu().numpy().T, ref) < tol(dtype)
 
 
+@pytest.mark.parametrize("n", [40, 300])
+def test_gemm_herk_k0_scales_by_beta(n):
+    """k == 0: C = beta C (BLAS semantics) for gemm and herk on the device."""
+    torch = _torch()
+    m = 257
+    c = rnd(m, n, np.float64, 30)
+    tA = torch.zeros((0, m), dtype=torch.float64).cuda()
+    tB = torch.zeros((n, 0), dtype=torch.float64).cuda()
+    tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
+    s.ops.gemm("N", "N", 1.0, tA, tB, -0.5, tC)
+    assert relerr(tC.cpu().numpy().T, -0.5 * c) < 1e-15
+    h = rnd(n, n, np.float64, 31)
+    tH = torch.from_numpy(np.ascontiguousarray(h.T)).cuda()
+    tK = torch.zeros((0, n), dtype=torch.float64).cuda()
+    s.ops.herk("L", "N", 1.0, tK, 3.0, tH)
+    got = tH.cpu().numpy().T
+    low = np.tril(np.ones((n, n), bool))
+    assert relerr(got[low], 3.0 * h[low]) < 1e-15
+    np.testing.assert_array_equal(got[~low], h[~low])
+
+
 def test_gemm_nn_long_k_packed_a():
     """Long-K NN products (K > 2048, m, n >= 4096) run as TN on a transposed
     copy of A (local_blas.cc dgemm); against numpy."""
@@ -58,6 +79,20 @@ def test_gemm_nn_long_k_packed_a():
     tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
     s.ops.gemm("N", "N", 0.75, tA, tB, 2.0, tC)
     assert relerr(tC.cpu().numpy().T, 0.75 * a @ b + 2.0 * c) < 1e-13
+
+
+def test_gemm_nn_long_k_packed_a_sliced(monkeypatch):
+    """The transposed copy of A is made in K slices bounded by
+    SLATE_GEMM_PACK_BYTES (later slices accumulate with beta = 1)."""
+    torch = _torch()
+    m, n, k = 4200, 4100, 6000
+    monkeypatch.setenv("SLATE_GEMM_PACK_BYTES", str(4200 * 2304 * 8))   # 2304-row slices
+    a, b, c = rnd(m, k, np.float64, 27), rnd(k, n, np.float64, 28), rnd(m, n, np.float64, 29)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+    tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
+    s.ops.gemm("N", "N", -1.25, tA, tB, 0.5, tC)
+    assert relerr(tC.cpu().numpy().T, -1.25 * a @ b + 0.5 * c) < 1e-13
 
 
 @pytest.mark.parametrize("k", [256, 512, 2048])
