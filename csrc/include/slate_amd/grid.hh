@@ -40,6 +40,22 @@ public:
     CommPtr row_ptr() const { return row_; }
     CommPtr col_ptr() const { return col_; }
 
+    /// Critical-path ("fast lane") row / column communicators: duplicates of
+    /// row() / col() over the same processes (a second ncclCommSplit for RCCL).
+    /// Panel, tournament, TSQR and lookahead messages travel on these, issued
+    /// on the high-priority panel queue, so they never wait behind the bulk
+    /// trailing-update traffic that the plain comms carry on the comm queue
+    /// (the reference gives panel / lookahead tasks priority 1 and the
+    /// trailing update priority 0, src/getrf.cc:92,124,175-186).  Without
+    /// duplicates (host transports, which are synchronous anyway) they alias
+    /// row() / col().
+    Comm& row_fast() const { return *(row_fast_ ? row_fast_ : row_); }
+    Comm& col_fast() const { return *(col_fast_ ? col_fast_ : col_); }
+    CommPtr row_fast_ptr() const { return row_fast_ ? row_fast_ : row_; }
+    CommPtr col_fast_ptr() const { return col_fast_ ? col_fast_ : col_; }
+    bool has_fast_lane() const { return row_fast_ != nullptr || col_fast_ != nullptr; }
+    void set_fast(CommPtr row_fast, CommPtr col_fast) { row_fast_ = row_fast; col_fast_ = col_fast; }
+
     /// The same processes viewed as a q x p grid (tile (i,j) of a matrix on
     /// the transposed grid lives where tile (j,i) lives on this grid);
     /// reference func::transpose_grid (func.hh:230).
@@ -52,6 +68,7 @@ private:
     GridOrder order_;
     int myrow_, mycol_;
     CommPtr world_, row_, col_;
+    CommPtr row_fast_, col_fast_;
 };
 
 using GridPtr = std::shared_ptr<Grid>;

@@ -55,6 +55,11 @@ struct LocalBlock {
     T* at(int64_t i, int64_t j) const { return ptr + i + j * ld; }
 };
 
+/// Largest single local-array allocation (bytes) of any matrix since the last
+/// reset -- lets tests assert that a driver made no n x n temporary.
+size_t storage_alloc_max();
+void storage_alloc_reset();
+
 //------------------------------------------------------------------------------
 /// Per-process storage of a distributed matrix.
 template <typename T>

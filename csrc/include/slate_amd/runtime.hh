@@ -18,6 +18,8 @@
 #include <functional>
 #include <initializer_list>
 #include <map>
+#include <string>
+#include <utility>
 #include <vector>
 
 namespace slate {
@@ -40,6 +42,13 @@ public:
     lb::Ctx ctx(int queue) const;
     Target target() const { return target_; }
     bool device() const { return target_ == Target::Devices; }
+
+    /// Lane log (tests / diagnostics): when enabled, every task appends
+    /// (label of its first trace::Block, queue index) in enqueue order, on
+    /// host targets too -- pins which queue (and so which communication
+    /// lane) each critical-path and bulk task is issued on.
+    static void lane_log_enable(bool on);
+    static std::vector<std::pair<std::string, int>> lane_log_take();
 
     /// Token helpers for common dependency names.
     static int64_t col(int64_t k)  { return 1000000 + k; }

@@ -37,6 +37,14 @@ SLATE_HD inline int64_t rd_l2g(RowDist const& d, int64_t li) {
     return ((L / d.mb) * d.p + d.rrel) * d.mb + L % d.mb - d.row0;
 }
 
+/// storage-local index of every process row's first panel row (p <= 16)
+struct PanelBases { int64_t base[16]; };
+/// mode 0: P(i, :) = row kk+i gathered from G (process r's panel rows at
+/// G + r maxr kb, ld maxr); mode 1: my rows of P back into ap (ld lda)
+template <typename T>
+void panel_xfer(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb, int64_t maxr, T* G, T* P, int64_t ldp,
+                T* ap, int64_t lda, int mode, hipStream_t s);
+
 // ---- distributed LU row permutations (lu_dist.hip)
 /// out(i, :) = A(sel[i], :) for i < cnt (ncols columns); id_out[i] = id_in[sel[i]]
 /// when id_in is given, else the global row of local row li_base + sel[i].

@@ -226,6 +226,30 @@ __global__ __launch_bounds__(256) void pplu_apply_kernel(int np, const T* gbuf, 
     }
 }
 
+
+// ---- exact partial pivoting on p > 1 with one collective per panel: every
+// process of the panel column packs its panel rows (local order, ld maxr) into
+// its block of an all-gather buffer G; the same M x kb panel (rows kk..m-1 in
+// global order) is then assembled on every process (mode 0), factored
+// redundantly by the device panel, and each process copies its own rows back
+// (mode 1).  base[r] = storage-local index of process r's first panel row.
+template <typename T>
+__global__ __launch_bounds__(64) void panel_xfer_kernel(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb,
+                                                        int64_t maxr, T* G, T* P, int64_t ldp, T* ap, int64_t lda,
+                                                        int mode) {
+    const int64_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= M) return;
+    const int64_t R = d.row0 + kk + i;
+    const int r = int((R / d.mb + d.rsrc) % d.p);
+    const int64_t t = (R / d.mb / d.p) * d.mb + R % d.mb - pb.base[r];
+    if (mode == 0) {
+        const T* g = G + (int64_t)r * maxr * kb + t;
+        for (int64_t j = blockIdx.y; j < kb; j += gridDim.y) P[i + j * ldp] = g[j * maxr];
+    } else if (r == d.myrow) {
+        for (int64_t j = blockIdx.y; j < kb; j += gridDim.y) ap[t + j * lda] = P[i + j * ldp];
+    }
+}
+
 }  // namespace
 
 template <typename T>
@@ -309,6 +333,14 @@ void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int6
                        info_off);
 }
 
+template <typename T>
+void panel_xfer(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb, int64_t maxr, T* G, T* P, int64_t ldp,
+                T* ap, int64_t lda, int mode, hipStream_t s) {
+    if (M <= 0 || kb <= 0) return;
+    dim3 g((unsigned)((M + 63) / 64), (unsigned)std::min<int64_t>(kb, 64));
+    hipLaunchKernelGGL(panel_xfer_kernel<T>, g, dim3(64), 0, s, M, kb, kk, d, pb, maxr, G, P, ldp, ap, lda, mode);
+}
+
 #define SLATE_INST_LUDIST(T)                                                                                       \
     template void gather_rows_ids<T>(int64_t, int64_t, const int64_t*, const T*, int64_t, T*, int64_t,            \
                                      const int64_t*, int64_t*, RowDist, int64_t, hipStream_t);                    \
@@ -321,7 +353,9 @@ void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int6
     template void pplu_cand<T>(int64_t, int64_t, int64_t, const T*, int64_t, int64_t, RowDist, int64_t, bool, T*,  \
                                hipStream_t);                                                                       \
     template void pplu_apply<T>(int, const T*, int64_t, int64_t, int64_t, int64_t, int64_t, T*, int64_t, RowDist, \
-                                int64_t, int64_t, int, double, bool, int64_t*, int*, int64_t, hipStream_t);
+                                int64_t, int64_t, int, double, bool, int64_t*, int*, int64_t, hipStream_t);       \
+    template void panel_xfer<T>(int64_t, int64_t, int64_t, RowDist, PanelBases, int64_t, T*, T*, int64_t, T*,     \
+                                int64_t, int, hipStream_t);
 
 SLATE_INST_LUDIST(float)
 SLATE_INST_LUDIST(double)

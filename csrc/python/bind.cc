@@ -369,7 +369,9 @@ PYBIND11_MODULE(_slate, m) {
         .def("transposed", &Grid::transposed)
         .def_property_readonly("world", &Grid::world_ptr)
         .def_property_readonly("row_comm", &Grid::row_ptr)
-        .def_property_readonly("col_comm", &Grid::col_ptr);
+        .def_property_readonly("col_comm", &Grid::col_ptr)
+        .def("set_fast", &Grid::set_fast)
+        .def_property_readonly("has_fast_lane", &Grid::has_fast_lane);
     m.def("generate_matrix_usage", &slate::generate_matrix_usage);
     m.def("default_grid", &default_grid);
     m.def("set_default_grid", &set_default_grid);
@@ -381,6 +383,10 @@ PYBIND11_MODULE(_slate, m) {
     m.def("get_device", &device::get_device);
     m.def("sync", &slate::sync, py::call_guard<py::gil_scoped_release>());
     m.def("release_cache", &device::release_cache);
+    m.def("lane_log_enable", &Sched::lane_log_enable);
+    m.def("storage_alloc_max", &storage_alloc_max);
+    m.def("storage_alloc_reset", &storage_alloc_reset);
+    m.def("lane_log_take", &Sched::lane_log_take);
     m.def("bytes_in_use", &device::bytes_in_use);
     m.def("debug_on", &Debug::on);
     m.def("debug_off", &Debug::off);

@@ -284,16 +284,41 @@ void gemm(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
 }
 
 //------------------------------------------------------------------------------
-// trsm: block sweeps over B's block rows (Left).  Right-side and transposed
-// solves are reduced to Left / NoTrans by explicit distributed transposes on
-// grids larger than 1x1.
+// trsm: block sweeps over B's block rows (Left), reference
+// src/work/work_trsm.cc:101-185 (forward) / :186+ (backward) and
+// src/work/work_trsmA.cc.  op(A) = A^T / A^H is NOT materialized: the sweep
+// runs on the transposed process grid, where A^T is A's own local array read
+// with a transposed operand (zero copy) and B's rows follow A's COLUMN
+// distribution; only B (m x nrhs) is redistributed when it does not conform.
+// Right-side solves are reduced to Left by transposing B.
 namespace {
 
+/// Process column of B's grid holding op(A)'s panel k (and the diagonal
+/// tile): A's column owner for NoTrans, its row owner for (conj-)transposes
+/// (B's grid is then A's transposed grid).
 template <typename T>
-void trsm_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target,
-                       int64_t la) {
+inline int panel_col(BaseMatrix<T> const& A, Op op, int64_t k) {
+    return op == Op::NoTrans ? A.scol_owner(k) : A.srow_owner(k);
+}
+/// op(A)'s panel k for my local rows of B (mloc x kb, ld mloc): A(:, k) or
+/// op(A(k, :)) packed from the local array
+template <typename T>
+inline void pack_op_panel(lb::Ctx const& c, BaseMatrix<T> const& A, LocalBlock<T> const& lA, Op op, int64_t k,
+                          int64_t mloc, int64_t kb, T* W) {
+    if (op == Op::NoTrans) pack(c, mloc, kb, lA.ptr + lcol_of(A, k) * lA.ld, lA.ld, W);
+    else lb::copy<T, T>(c, Uplo::General, op, mloc, kb, lA.ptr + lrow_of(A, k), lA.ld, W, std::max<int64_t>(mloc, 1));
+}
+
+/// op(A) X = alpha B, A the PHYSICAL triangle (NoTrans storage view, uplo_phys),
+/// B's rows conforming to op(A)'s rows (NoTrans: A's grid and row tiles;
+/// otherwise A's transposed grid and column tiles).  trsmB sweep: per step
+/// the diagonal tile along B's process row, op(A)'s panel along process rows,
+/// the solved block row down process columns, one local GEMM per process.
+template <typename T>
+void trsm_left_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target,
+                     int64_t la) {
     auto& g = *B.grid();
-    const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    const int myrow = g.myrow(), mycol = g.mycol();
     const Loc loc = loc_of(target);
     LocalBlock<T> lbk = B.local(loc, true);
     LocalBlock<T> lA = A.local(loc, false);
@@ -312,38 +337,39 @@ void trsm_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Ma
         WB[r].resize(target, size_t(nbmax) * std::max<int64_t>(lbk.n, 1));
         WD[r].resize(target, size_t(nbmax) * nbmax);
     }
-    const bool lower = (uplo == Uplo::Lower);
+    // op(A) lower <=> forward sweep
+    const bool lower = (op == Op::NoTrans) == (uplo_phys == Uplo::Lower);
     for (int64_t t = 0; t < mt; ++t) {
         const int64_t k = lower ? t : mt - 1 - t;
         const int slot = int(t % R);
         const int64_t kb = B.tileMb(k);
-        const int pk = B.srow_owner(k), qk = A.scol_owner(k);
+        const int pk = B.srow_owner(k), qk = panel_col(A, op, k);
         const int64_t lrk = lrow_of(B, k);
         T* D = WD[slot].data();
         T* WAk = WA[slot].data();
         T* WBk = WB[slot].data();
-        // A(k,k) to every process of row pk; A(:,k) local rows along rows
+        // A(k,k) to every process of row pk; op(A)'s panel k (my rows) along rows
         S.task(device::kCommQueue, {}, {Sched::bcast(slot)}, [&, k, kb, pk, qk, D, WAk](lb::Ctx const& c) {
-            // diagonal tile: owner (pk, qk) -> process row pk
+            trace::Block t2("trsm_bcast_panel");
             if (myrow == pk) {
                 if (mycol == qk) pack(c, kb, kb, lA.ptr + lrow_of(A, k) + lcol_of(A, k) * lA.ld, lA.ld, D);
                 bcast(g.row(), D, size_t(kb * kb), qk, c);
             }
-            // column panel A(:, k) rows local to me (all my rows) along process rows
-            if (mycol == qk) pack(c, lbk.m, kb, lA.ptr + lcol_of(A, k) * lA.ld, lA.ld, WAk);
+            if (mycol == qk) pack_op_panel(c, A, lA, op, k, lbk.m, kb, WAk);
             bcast(g.row(), WAk, size_t(lbk.m * kb), qk, c);
         });
         // solve the block row on process row pk, then broadcast it down columns
         S.task(0, {Sched::bcast(slot)}, {Sched::tok(9, 0)}, [&, k, kb, pk, D, WBk, lrk](lb::Ctx const& c) {
             if (myrow == pk) {
-                lb::trsm(c, Side::Left, uplo, Op::NoTrans, diag, kb, lbk.n, T(1), D, kb, lbk.ptr + lrk, lbk.ld);
+                lb::trsm(c, Side::Left, uplo_phys, op, diag, kb, lbk.n, T(1), D, kb, lbk.ptr + lrk, lbk.ld);
                 lb::copy2d(c, kb, lbk.n, lbk.ptr + lrk, lbk.ld, WBk, kb);
             }
         });
         S.task(device::kCommQueue, {Sched::tok(9, 0)}, {Sched::tok(8, slot)}, [&, kb, pk, WBk](lb::Ctx const& c) {
+            trace::Block t2("trsm_bcast_x");
             bcast(g.col(), WBk, size_t(kb * lbk.n), pk, c);
         });
-        // update the remaining block rows: B(i) -= A(i,k) X(k)
+        // update the remaining block rows: B(i) -= op(A)(i,k) X(k)
         S.task(0, {Sched::tok(8, slot), Sched::bcast(slot)}, {Sched::tok(9, 0)}, [&, k, kb, WAk, WBk](lb::Ctx const& c) {
             int64_t r0 = lower ? lrow_of(B, k + 1) : 0;
             int64_t r1 = lower ? lbk.m : lrow_of(B, k);
@@ -359,10 +385,13 @@ void trsm_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Ma
 /// A never moves.  Each process keeps a partial-sum block W (its local rows x
 /// all columns of B); step k sums block row k of W across process row pk,
 /// the owner of A(k,k) solves it, broadcasts X(k) down its process column, and
-/// that column updates W(i) -= A(i,k) X(k) for its local rows.  Traffic per
-/// step is kb x n, instead of trsmB's A panel of (local rows) x kb.
+/// that column updates W(i) -= op(A)(i,k) X(k) for its local rows.  Traffic per
+/// step is kb x n, instead of trsmB's A panel of (local rows) x kb.  For
+/// op(A) = A^T / A^H the same algorithm runs on the transposed grid (B's
+/// rows follow A's columns) and the update reads op(A(k, i)) straight from
+/// the local array.
 template <typename T>
-void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target) {
+void trsmA_left(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target) {
     auto& g = *B.grid();
     const int myrow = g.myrow(), mycol = g.mycol();
     const Loc loc = loc_of(target);
@@ -382,11 +411,11 @@ void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, M
                 lb::add(c, Uplo::General, mloc, B.tileNb(j), alpha, lbk.ptr + lcol_of(B, j) * lbk.ld, lbk.ld, T(1),
                         W.data() + gcol_of(B, j) * ldw, ldw);
     });
-    const bool lower = (uplo == Uplo::Lower);
+    const bool lower = (op == Op::NoTrans) == (uplo_phys == Uplo::Lower);
     for (int64_t t = 0; t < mt; ++t) {
         const int64_t k = lower ? t : mt - 1 - t;
         const int64_t kb = B.tileMb(k);
-        const int pk = B.srow_owner(k), qk = A.scol_owner(k);
+        const int pk = B.srow_owner(k), qk = panel_col(A, op, k);
         const int64_t lrk = lrow_of(B, k);
         S.task(device::kCommQueue, {tW}, {tW}, [&, kb, pk, lrk](lb::Ctx const& c) {
             trace::Block t2("trsmA_reduce");
@@ -396,7 +425,7 @@ void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, M
         });
         S.task(0, {tW}, {tX}, [&, k, kb, pk, qk, lrk](lb::Ctx const& c) {
             if (myrow != pk || mycol != qk) return;
-            lb::trsm(c, Side::Left, uplo, Op::NoTrans, diag, kb, n, T(1),
+            lb::trsm(c, Side::Left, uplo_phys, op, diag, kb, n, T(1),
                      lA.ptr + lrow_of(A, k) + lcol_of(A, k) * lA.ld, lA.ld, WX.data(), kb);
             lb::copy2d(c, kb, n, WX.data(), kb, X.data() + lrk, ldw);
         });
@@ -407,9 +436,13 @@ void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, M
         S.task(0, {tX}, {tW}, [&, k, kb, qk, lrk](lb::Ctx const& c) {
             if (mycol != qk) return;
             const int64_t r0 = lower ? lrow_of(B, k + 1) : 0, r1 = lower ? mloc : lrk;
-            if (r1 > r0)
+            if (r1 <= r0) return;
+            if (op == Op::NoTrans)
                 lb::gemm(c, Op::NoTrans, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + r0 + lcol_of(A, k) * lA.ld,
                          lA.ld, WX.data(), kb, T(1), W.data() + r0, ldw);
+            else   // op(A(k, cols r0..r1)): my local columns of A = my local rows of B
+                lb::gemm(c, op, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + lrow_of(A, k) + r0 * lA.ld, lA.ld,
+                         WX.data(), kb, T(1), W.data() + r0, ldw);
         });
     }
     // X(k) sits on process column qk of block row k: sum across the process
@@ -424,6 +457,29 @@ void trsmA_left_notrans(Uplo uplo, Diag diag, T alpha, BaseMatrix<T> const& A, M
                            lbk.ptr + lcol_of(B, j) * lbk.ld, lbk.ld);
     });
     S.wait_all();
+}
+
+/// Do B's row tiles follow op(A)'s rows (NoTrans: A's rows on A's grid;
+/// otherwise A's columns on A's transposed grid)?
+template <typename T>
+bool b_conforms(BaseMatrix<T> const& Ap, Op op, BaseMatrix<T> const& B) {
+    if (B.op() != Op::NoTrans || !B.aligned()) return false;
+    auto& ga = *Ap.grid();
+    auto& gb = *B.grid();
+    if (!ga.same_processes(gb)) return false;
+    if (op == Op::NoTrans) {
+        if (!rows_conform(Ap, B)) return false;
+        for (int64_t j = 0; j < Ap.nt(); ++j) if (Ap.tileNb(j) != B.tileMb(j)) return false;
+        return true;
+    }
+    // B on the transposed grid: B's process (r, c) is A's process (c, r)
+    // (swapped dimensions + opposite order: rank_of_B(r, c) == rank_of_A(c, r))
+    if (gb.p() != ga.q() || gb.q() != ga.p() || (gb.size() > 1 && gb.order() == ga.order())) return false;
+    if (B.mt() != Ap.nt()) return false;
+    for (int64_t i = 0; i < Ap.nt(); ++i)
+        if (Ap.tileNb(i) != B.tileMb(i) || Ap.scol_owner(i) != B.srow_owner(i) || Ap.tileMb(i) != Ap.tileNb(i))
+            return false;
+    return true;
 }
 
 }  // namespace
@@ -457,7 +513,7 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
     Method method = get_option<int64_t>(opts, Option::MethodTrsm, MethodTrsm::Auto);
     if (method == MethodTrsm::Auto) method = B.nt() < 2 ? MethodTrsm::TrsmA : MethodTrsm::TrsmB;
     slate_error_if_msg(method != MethodTrsm::TrsmA && method != MethodTrsm::TrsmB, "trsm: unknown MethodTrsm");
-    // distributed: reduce to Left, NoTrans, A conforming to B's rows
+    // distributed: reduce to Left
     if (side == Side::Right) {
         // X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T (use conj for ConjTrans pairs)
         bool conj = is_complex_v<T>;
@@ -471,22 +527,32 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         slate::copy<T, T>(conj ? conj_transpose(Bt) : transpose(Bt), B, opts);
         return;
     }
-    // materialize op(A) as a NoTrans triangle conforming to B (rows and cols)
-    Uplo u = A.uplo();
-    BaseMatrix<T> Ause = A;
+    // A's physical triangle (no copy); op(A) is handled by the sweeps
+    const Op op = A.op();
+    BaseMatrix<T> Ap = op == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(op == Op::ConjTrans);
+    const Uplo up = A.uplo_physical();
     Matrix<T> Ac;
-    bool conform = A.op() == Op::NoTrans && rows_conform(BaseMatrix<T>(A), BaseMatrix<T>(B)) &&
-                   A.grid()->same_processes(*gB);
-    if (conform) {
-        for (int64_t j = 0; j < A.nt(); ++j) if (A.tileNb(j) != B.tileMb(j)) conform = false;
+    if (!Ap.aligned() || Ap.mb() != Ap.nb()) {
+        // unaligned sub-view of A: square-tile aligned copy (the only case
+        // that still copies A)
+        Ac = materialize<T>(Ap, target, Ap.grid(), B.mb(), B.mb(), 0, 0);
+        Ap = Ac;
     }
-    if (!conform) {
-        Ac = materialize<T>(A, target, gB, B.mb(), B.mb(), row0_owner(B), 0);
-        Ause = Ac;
+    auto run = [&](Matrix<T>& Bx) {
+        if (method == MethodTrsm::TrsmA) trsmA_left(up, op, A.diag(), alpha, Ap, Bx, target);
+        else trsm_left_sweep(up, op, A.diag(), alpha, Ap, Bx, target, option_la(opts));
+    };
+    if (b_conforms(Ap, op, B)) {
+        run(B);
+        internal::finish_origin(B, opts);
+        return;
     }
-    if (method == MethodTrsm::TrsmA) trsmA_left_notrans(u, A.diag(), alpha, Ause, B, target);
-    else trsm_left_notrans(u, A.diag(), alpha, Ause, B, target, option_la(opts));
-    internal::finish_origin(B, opts);
+    // redistribute B (m x nrhs) to follow op(A)'s rows, never A
+    GridPtr gx = op == Op::NoTrans ? Ap.grid() : Ap.grid()->transposed();
+    const int rsrc = op == Op::NoTrans ? row0_owner(Ap) : col0_owner(Ap);
+    Matrix<T> Bx = materialize<T>(B, target, gx, Ap.nb(), B.nb(), rsrc, 0);
+    run(Bx);
+    slate::copy<T, T>(Bx, B, opts);
 }
 
 //------------------------------------------------------------------------------

@@ -5,9 +5,11 @@
 //   panel (queue 1): the whole m x nb panel is factored ON THE DEVICE by the
 //     recursive LU kernel (device pivot search, in-kernel row swaps across the
 //     panel, trsm/gemm recursion) -- no host round trip per column.  With
-//     p = 1 the panel is local to its process column.  With p > 1 the panel
-//     rows are gathered to the diagonal process over the column communicator,
-//     factored there and scattered back (exact partial pivoting).
+//     p = 1 the panel is local to its process column.  With p > 1 (see
+//     getrf_dist) partial pivoting all-gathers the panel rows over the column
+//     (ONE collective per panel) and factors the assembled panel redundantly on
+//     every process of the column; tournament pivoting (CALU) runs a
+//     cross-process tree.
 //   The panel's row permutation is turned into (dst, src) row pairs on the
 //   device; they travel with the pivots in one broadcast, and every process
 //   permutes its local columns with ONE gather/scatter kernel per column
@@ -16,10 +18,9 @@
 //   U row: trsm on process row pk, broadcast down columns; trailing update
 //   A22 -= L21 U12 as one MFMA GEMM per process; lookahead columns on their
 //   own queues.
-// getrf_tntpiv (CALU) shares this driver: its panel (gathered to the diagonal
-// process when p > 1) selects the pivots of every 32-column narrow block by a
-// tournament over 256-row leaves on the device (kernels/tslu.hip), then
-// factors that block without further pivoting.
+// getrf_tntpiv (CALU) shares this driver: its panel selects the pivots of
+// every 32-column narrow block by a tournament over 256-row leaves on the
+// device (kernels/tslu.hip), then factors that block without further pivoting.
 #include "internal.hh"
 #include "lu_dist.hh"
 #include "../kernels/kernels.hh"
@@ -181,18 +182,29 @@ enum class PanelMode { Partial, Tournament, NoPiv };
 ///     the root's final LU gives the winners and [L11\U11].  Winners and LU11
 ///     go down the column; the panel rows are permuted (slot all-reduce) and
 ///     L21 = A21 U11^{-1} is a local trsm on every process.
-///   Partial (PPLU): exact partial pivoting.  The panel's rows are gathered to
-///     pk over the column communicator (sizes known from the distribution),
-///     factored there by the device panel and scattered back; the LAPACK ipiv
-///     becomes the same device slots.
+///   Partial (PPLU, reference Tile_getrf.hh:162-450 does one MPI_Allreduce
+///     MAXLOC per column): ONE all-gather of the panel rows over the column
+///     communicator; every process of the column assembles the M x kb panel in
+///     global row order, factors it with the device partial-pivoting panel
+///     (identical, deterministic result on every process: exact partial
+///     pivoting, the same pivots as on one GPU) and keeps its own rows.
+///     1 collective per panel instead of nb.
 ///   NoPiv: pk factors the diagonal block, the column solves L21 locally.
 /// Row permutation of every other column range: lu_dist.hip slots (pack ->
 /// all-reduce over the column communicator -> unpack), which also delivers
 /// the (unsolved) U block row to every process of the column, so U12 =
-/// L11^{-1} (...) is computed redundantly instead of broadcast.  Trailing
-/// columns are processed in chunks so the all-reduce of chunk c+1 overlaps the
-/// GEMM of chunk c.  The interchanges of the left columns [0, k) are applied
-/// one step late, behind the next panel's messages on the comm queue.
+/// L11^{-1} (...) is computed redundantly instead of broadcast.
+/// Two communication lanes (Grid::row_fast / col_fast): every message on the
+/// critical path -- tournament / panel gather, LU11 + pivots + L panel
+/// broadcasts, and the row exchange of the lookahead columns -- is issued on
+/// the high-priority panel queue over duplicate communicators; the trailing
+/// chunks' row exchanges and the left-column swaps stay on the comm queue
+/// over the plain communicators.  So step k+1's panel never waits behind
+/// step k's bulk traffic (reference priorities: src/getrf.cc:92,124,175-186).
+/// Every communicator sees its operations in the same order on every rank
+/// (one program order, and a task only waits on earlier tasks), so the lanes
+/// cannot deadlock.  Trailing columns are processed in chunks so the
+/// all-reduce of chunk c+1 overlaps the GEMM of chunk c.
 /// Option::PivotThreshold in (0, 1] (reference src/getrf.cc:39): partial
 /// pivoting keeps the diagonal while |a_jj| >= threshold * column max
 inline double pivot_threshold(Options const& opts) {
@@ -220,6 +232,10 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
     const bool pivot = mode != PanelMode::NoPiv;
     const RowDist rd = row_dist(A);
     const int qC = device::kCommQueue, qP = 1;
+    // critical-path lane (panel queue, duplicate comms) / bulk lane (comm queue)
+    Comm& colF = g.col_fast();
+    Comm& rowF = g.row_fast();
+    auto& st = *A.storage();
 
     Sched S(target);
     const int R = int(std::max<int64_t>(3, la + 2));
@@ -237,12 +253,15 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
     Work<T> Cb(target, size_t(nb) * nb), Cr(target, size_t(nb) * nb), Sb(target, size_t(2 * nb) * nb),
         Fb(target, size_t(2 * nb) * nb);
     Work<int64_t> ids(target, nb), idr(target, nb), idS(target, 2 * nb),
-        perm(target, size_t(std::max<int64_t>(mloc, 2 * nb))), pip(target, nb);
-    Work<T> PPe, PPg, U12;     // partial pivoting: all-gather entry / gathered entries / U12 rows
+        perm(target, size_t(std::max<int64_t>(mode == PanelMode::Partial ? m : mloc, 2 * nb))), pip(target, nb);
+    // partial pivoting: my packed panel rows / all-gathered rows / assembled panel
+    Work<T> PS, PG, PP;
+    const int64_t maxloc_rows = ceildiv(std::max<int64_t>(m, 1), st.mb * p) * st.mb;
     if (mode == PanelMode::Partial) {
-        PPe.resize(target, size_t(pplu_entry<T>(nb)));
-        PPg.resize(target, size_t(p) * pplu_entry<T>(nb));
-        U12.resize(target, size_t(32) * nb);
+        slate_error_if_msg(p > 16, "getrf partial pivoting: more than 16 process rows");
+        PS.resize(target, size_t(maxloc_rows) * nb);
+        PG.resize(target, size_t(p) * maxloc_rows * nb);
+        PP.resize(target, size_t(std::max<int64_t>(m, 1)) * nb);
     }
     Work<int64_t> ipiv_all(target, size_t(std::max<int64_t>(kt, 1)) * nb);
     Work<int> dinfo(target, 2);               // [info, dummy]
@@ -334,21 +353,21 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
                 int64_t ldF = mr;
                 for (auto const& rd_ : rounds) {
                     if (!rd_.recv) {
-                        S.task(qC, {tSel}, {tSel}, [&, rd_, kb](lb::Ctx const& c) {
+                        S.task(qP, {tSel}, {tSel}, [&, rd_, kb](lb::Ctx const& c) {
                             trace::Block t2("getrf_tnt_send");
                             std::vector<Comm::P2P> ops{{Cb.data(), size_t(rd_.mine * kb), rd_.peer, true}};
-                            g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                            colF.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
                             std::vector<Comm::P2P> ops2{{ids.data(), size_t(rd_.mine), rd_.peer, true}};
-                            g.col().exchange(ops2, scalar_type<int64_t>(), c.loc(), c.stream);
+                            colF.exchange(ops2, scalar_type<int64_t>(), c.loc(), c.stream);
                         });
                         break;
                     }
-                    S.task(qC, {}, {tSel}, [&, rd_, kb](lb::Ctx const& c) {
+                    S.task(qP, {}, {tSel}, [&, rd_, kb](lb::Ctx const& c) {
                         trace::Block t2("getrf_tnt_recv");
                         std::vector<Comm::P2P> ops{{Cr.data(), size_t(rd_.theirs * kb), rd_.peer, false}};
-                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                        colF.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
                         std::vector<Comm::P2P> ops2{{idr.data(), size_t(rd_.theirs), rd_.peer, false}};
-                        g.col().exchange(ops2, scalar_type<int64_t>(), c.loc(), c.stream);
+                        colF.exchange(ops2, scalar_type<int64_t>(), c.loc(), c.stream);
                     });
                     const int64_t ms = rd_.mine + rd_.theirs, c2 = std::min(ms, kd);
                     S.task(qP, {}, {tSel}, [&, rd_, kb, kk, ms, c2](lb::Ctx const& c) {
@@ -379,70 +398,39 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
                 (void)cur;
             }
             // winners and [L11\U11] down the panel column
-            S.task(qC, {}, {tPV}, [&, kd, kb, pk, LUk, win](lb::Ctx const& c) {
+            S.task(qP, {}, {tPV}, [&, kd, kb, pk, LUk, win](lb::Ctx const& c) {
                 trace::Block t2("getrf_bcast_winners");
-                bcast(g.col(), win, size_t(kd), pk, c);
-                bcast(g.col(), LUk, size_t(kd * kb), pk, c);
+                bcast(colF, win, size_t(kd), pk, c);
+                bcast(colF, LUk, size_t(kd * kb), pk, c);
             });
             S.task(qP, {}, {tPV}, [&, k, kk, kd, win, ipv, ssrc, sdst](lb::Ctx const& c) {
                 perm_slots(c, 0, kk, int(kd), win, 0, ipv, ssrc, sdst);
             });
             // panel rows: displaced rows to the vacated winner positions
-            S.task(qC, {tPV}, {Sched::col(k), tPB}, [&, kd, kb, apc, ssrc, sdst](lb::Ctx const& c) {
+            S.task(qP, {tPV}, {Sched::col(k), tPB}, [&, kd, kb, apc, ssrc, sdst](lb::Ctx const& c) {
                 trace::Block t2("getrf_panel_perm");
                 slots_pack(c, int(kd), int(2 * kd), kb, ssrc, apc, lda, rd, PB.data(), kd);
-                g.col().allreduce(PB.data(), size_t(kd * kb), ReduceOp::Sum, c.loc(), c.stream);
+                colF.allreduce(PB.data(), size_t(kd * kb), ReduceOp::Sum, c.loc(), c.stream);
                 slots_unpack(c, int(kd), int(2 * kd), kb, sdst, PB.data(), kd, apc, lda, rd);
             });
         } else if (in_col && mode == PanelMode::Partial) {
-            // distributed partial pivoting (reference Tile_getrf.hh:270): column
-            // by column, ONE all-gather over the panel column of every process's
-            // {max |a|, row id, candidate row, row kk+j}; each process then picks
-            // the same pivot and swaps / scales / updates the rows it owns.
-            // Narrow blocks of 32 columns; the rest of the panel is updated by
-            // U12 = L11^{-1} A12 (pk, broadcast down the column) and a GEMM.
-            const int64_t E = pplu_entry<T>(kb);
-            for (int64_t c0 = 0; c0 < kd; c0 += 32) {
-                const int64_t cend = std::min<int64_t>(c0 + 32, kd), nn = cend - c0;
-                for (int64_t j = c0; j < cend; ++j) {
-                    S.task(qC, {Sched::col(k)}, {Sched::col(k)}, [&, j, cend, kb, kk, E, mr, diag, pk, ap, lr_k](lb::Ctx const& c) {
-                        trace::Block t2("getrf_pp_column");
-                        pplu_cand(c, mr, j, diag ? j : 0, ap, lda, kb, rd, lr_k, diag, PPe.data());
-                        g.col().allgather(PPe.data(), PPg.data(), size_t(E), scalar_type<T>(), c.loc(), c.stream);
-                        pplu_apply(c, p, PPg.data(), kb, j, cend, mr, diag ? j + 1 : 0, ap, lda, rd, lr_k, kk, pk, thresh,
-                                   diag, pip.data(), diag ? info_real : info_dummy, kk);
-                    });
-                }
-                if (cend < kb) {
-                    const int64_t rest = kb - cend;
-                    S.task(qC, {Sched::col(k)}, {Sched::col(k)}, [&, c0, nn, cend, rest, diag, pk, ap](lb::Ctx const& c) {
-                        trace::Block t2("getrf_pp_u12");
-                        if (diag) {
-                            lb::trsm(c, Side::Left, Uplo::Lower, Op::NoTrans, Diag::Unit, nn, rest, T(1),
-                                     ap + c0 + c0 * lda, lda, ap + c0 + cend * lda, lda);
-                            lb::copy2d(c, nn, rest, ap + c0 + cend * lda, lda, U12.data(), nn);
-                        }
-                        bcast(g.col(), U12.data(), size_t(nn * rest), pk, c);
-                    });
-                    S.task(qP, {Sched::col(k)}, {Sched::col(k)}, [&, c0, nn, cend, rest, diag, mr, ap](lb::Ctx const& c) {
-                        trace::Block t2("getrf_pp_a22");
-                        const int64_t r0 = diag ? cend : 0;
-                        if (mr > r0)
-                            lb::gemm(c, Op::NoTrans, Op::NoTrans, mr - r0, rest, nn, T(-1), ap + r0 + c0 * lda, lda,
-                                     U12.data(), nn, T(1), ap + r0 + cend * lda, lda);
-                    });
-                }
-            }
-            if (diag)
-                S.task(qP, {Sched::col(k)}, {tPV}, [&, kd, kb, ap, LUk](lb::Ctx const& c) {
-                    lb::copy2d(c, kd, kb, ap, lda, LUk, kd);
-                });
-            S.task(qC, {}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) {
-                trace::Block t2("getrf_bcast_lu11");
-                bcast(g.col(), LUk, size_t(kd * kb), pk, c);
-            });
-            // pip is replicated by the per-column all-gathers
-            S.task(qP, {Sched::col(k)}, {tPV}, [&, k, kk, kd, ipv, ssrc, sdst](lb::Ctx const& c) {
+            // exact partial pivoting with ONE all-gather per panel (see above):
+            // pack my panel rows, all-gather over the column, assemble the
+            // M x kb panel in global row order, factor it on the device (the
+            // same deterministic result on every process of the column), keep
+            // my rows, LU11 and the pivot slots
+            const int64_t maxr = *std::max_element(rows_r.begin(), rows_r.end());
+            PanelBases pb{};
+            for (int r = 0; r < p; ++r) pb.base[r] = g2l_ceil(A.row0() + kk, st.mb, (r - st.rsrc + p) % p, p);
+            S.task(qP, {Sched::col(k)}, {Sched::col(k), tPV}, [&, k, kk, kd, kb, M, mr, maxr, pb, diag, ap, LUk, ipv, ssrc, sdst](lb::Ctx const& c) {
+                trace::Block t2("getrf_pp_panel");
+                lb::copy2d(c, mr, kb, ap, lda, PS.data(), maxr);
+                colF.allgather(PS.data(), PG.data(), size_t(maxr * kb), scalar_type<T>(), c.loc(), c.stream);
+                panel_xfer<T>(c, M, kb, kk, rd, pb, maxr, PG.data(), PP.data(), M, nullptr, 1, 0);
+                lb::getrf_panel(c, M, kb, PP.data(), M, pip.data(), perm.data(), diag ? info_real : info_dummy, kk,
+                                true, false, thresh);
+                panel_xfer<T>(c, M, kb, kk, rd, pb, maxr, nullptr, PP.data(), M, ap, lda, 1);
+                lb::copy2d(c, kd, kb, PP.data(), M, LUk, kd);
                 perm_slots(c, 1, kk, int(kd), pip.data(), kk, ipv, ssrc, sdst);
             });
         } else if (in_col) {
@@ -453,7 +441,7 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
                     lb::copy2d(c, kd, kb, ap, lda, LUk, kd);
                 });
             }
-            S.task(qC, {}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) { bcast(g.col(), LUk, size_t(kd * kb), pk, c); });
+            S.task(qP, {}, {tPV}, [&, kd, kb, pk, LUk](lb::Ctx const& c) { bcast(colF, LUk, size_t(kd * kb), pk, c); });
         }
         // L21 = A21 U11^{-1} (tournament / no pivoting: the panel rows are still
         // original; partial: already factored by pk) and the L panel for the row
@@ -470,17 +458,17 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
             });
         }
         // pivots + LU11 and the L panel along the process rows
-        S.task(qC, {}, {tPV}, [&, k, kd, kb, qk, pv, ipv, LUk](lb::Ctx const& c) {
+        S.task(qP, {}, {tPV}, [&, k, kd, kb, qk, pv, ipv, LUk](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_row");
             if (pivot) {
-                bcast(g.row(), pv, size_t(6 * nb), qk, c);
+                bcast(rowF, pv, size_t(6 * nb), qk, c);
                 lb::copy2d(c, kd, int64_t(1), ipv, kd, ipiv_all.data() + k * nb, kd);
             }
-            bcast(g.row(), LUk, size_t(kd * kb), qk, c);
+            bcast(rowF, LUk, size_t(kd * kb), qk, c);
         });
-        S.task(qC, {}, {tW}, [&, kb, qk, mr, Wk](lb::Ctx const& c) {
+        S.task(qP, {}, {tW}, [&, kb, qk, mr, Wk](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_L");
-            bcast(g.row(), Wk, size_t(mr * kb), qk, c);
+            bcast(rowF, Wk, size_t(mr * kb), qk, c);
         });
 
         // ============================================== column ranges: U + update
@@ -493,16 +481,19 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
             std::vector<int64_t> cols;
             for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
             T* buf = UB.data() + c0 * ldu;
-            // permuted block row k of these columns -> buf (every process of the column)
-            S.task(qC, {tPV}, cols, [&, c0, nc, buf](lb::Ctx const& c) {
+            // permuted block row k of these columns -> buf (every process of
+            // the column); lookahead columns on the critical-path lane
+            const bool crit = (queue == device::kLookaheadQueue);
+            Comm& cc_ = crit ? colF : g.col();
+            S.task(crit ? qP : qC, {tPV}, cols, [&, c0, nc, buf](lb::Ctx const& c) {
                 trace::Block t2("getrf_rows_exchange");
                 if (pivot) {
                     slots_pack(c, 0, int(2 * kd), nc, ssrc, a + c0 * lda, lda, rd, buf, ldu);
-                    g.col().allreduce(buf, size_t(ldu * nc), ReduceOp::Sum, c.loc(), c.stream);
+                    cc_.allreduce(buf, size_t(ldu * nc), ReduceOp::Sum, c.loc(), c.stream);
                     slots_unpack(c, int(kd), int(2 * kd), nc, sdst, buf + kd, ldu, a + c0 * lda, lda, rd);
                 } else {
                     if (diag) lb::copy2d(c, kd, nc, a + lr_k + c0 * lda, lda, buf, ldu);
-                    bcast(g.col(), buf, size_t(ldu * nc), pk, c);
+                    bcast(cc_, buf, size_t(ldu * nc), pk, c);
                 }
             });
             std::vector<int64_t> in{tPV, tW};
@@ -659,19 +650,20 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         }
 
         // ------------------------------- (ipiv, pairs) along the process row
-        S.task(device::kCommQueue, {tPanel}, {tBc}, [&, k, kd, slot, pv_ipiv](lb::Ctx const& c) {
+        // (critical path: on the panel queue over the fast-lane row comm)
+        S.task(1, {tPanel}, {tBc}, [&, k, kd, slot, pv_ipiv](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_piv");
-            bcast(g.row(), PV[slot].data(), size_t(5 * nb + 8), qk, c);
+            bcast(g.row_fast(), PV[slot].data(), size_t(5 * nb + 8), qk, c);
             if (pivot) lb::copy2d(c, kd, int64_t(1), pv_ipiv, kd, ipiv_all.data() + k * nb, kd);
         });
 
         // ----------------------------------------- L panel along process rows
         T* Wk = W[slot].data();
         const int64_t mrows_k = mloc - lr_k;     // my rows >= kk
-        S.task(device::kCommQueue, {Sched::col(k), tBc}, {Sched::tok(7, slot)}, [&, lr_k, lc_k, kb, qk, Wk, mrows_k](lb::Ctx const& c) {
+        S.task(1, {Sched::col(k), tBc}, {Sched::tok(7, slot)}, [&, lr_k, lc_k, kb, qk, Wk, mrows_k](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_L");
             if (mycol == qk) pack(c, mrows_k, kb, a + lr_k + lc_k * lda, lda, Wk);
-            if (q > 1) bcast(g.row(), Wk, size_t(mrows_k * kb), qk, c);
+            if (q > 1) bcast(g.row_fast(), Wk, size_t(mrows_k * kb), qk, c);
         });
         const int64_t tL = Sched::tok(7, slot);
         // L(k,k)^{-1} once per step (device): every column range's U solve is

@@ -28,7 +28,9 @@ std::shared_ptr<Grid> Grid::self() {
 std::shared_ptr<Grid> Grid::transposed() const {
     // (r, c) on this grid  ->  (c, r) on a q x p grid with the opposite order
     GridOrder o = order_ == GridOrder::Col ? GridOrder::Row : GridOrder::Col;
-    return std::make_shared<Grid>(q_, p_, o, world_, col_, row_);
+    auto t = std::make_shared<Grid>(q_, p_, o, world_, col_, row_);
+    if (has_fast_lane()) t->set_fast(col_fast_ptr(), row_fast_ptr());
+    return t;
 }
 
 namespace {

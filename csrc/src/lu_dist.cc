@@ -211,6 +211,26 @@ void pplu_apply(lb::Ctx const& c, int np, T const* gbuf, int64_t kb, int64_t j, 
     }
 }
 
+template <typename T>
+void panel_xfer(lb::Ctx const& c, int64_t M, int64_t kb, int64_t kk, RowDist const& d, PanelBases const& pb,
+                int64_t maxr, T* G, T* P, int64_t ldp, T* ap, int64_t lda, int mode) {
+    if (M <= 0 || kb <= 0) return;
+    if (c.dev()) {
+        kd::panel_xfer(M, kb, kk, d, pb, maxr, dptr(G), dptr(P), ldp, dptr(ap), lda, mode, c.stream);
+        return;
+    }
+    for (int64_t i = 0; i < M; ++i) {
+        const int64_t R = d.row0 + kk + i;
+        const int r = int((R / d.mb + d.rsrc) % d.p);
+        const int64_t t = (R / d.mb / d.p) * d.mb + R % d.mb - pb.base[r];
+        if (mode == 0) {
+            for (int64_t j = 0; j < kb; ++j) P[i + j * ldp] = G[r * maxr * kb + t + j * maxr];
+        } else if (r == d.myrow) {
+            for (int64_t j = 0; j < kb; ++j) ap[t + j * lda] = P[i + j * ldp];
+        }
+    }
+}
+
 #define SLATE_LUDIST_INST(T)                                                                                    \
     template int64_t pplu_entry<T>(int64_t);                                                                   \
     template void pplu_cand<T>(lb::Ctx const&, int64_t, int64_t, int64_t, T const*, int64_t, int64_t,        \
@@ -224,7 +244,9 @@ void pplu_apply(lb::Ctx const& c, int np, T const* gbuf, int64_t kb, int64_t j, 
                                 RowDist const&, T*, int64_t);                                                  \
     template void slots_unpack<T>(lb::Ctx const&, int, int, int64_t, int64_t const*, T const*, int64_t, T*,    \
                                   int64_t, RowDist const&);                                                    \
-    template void lu_sign<T>(lb::Ctx const&, int64_t, T*, int64_t, T*);
+    template void lu_sign<T>(lb::Ctx const&, int64_t, T*, int64_t, T*);                                         \
+    template void panel_xfer<T>(lb::Ctx const&, int64_t, int64_t, int64_t, RowDist const&, PanelBases const&,    \
+                                int64_t, T*, T*, int64_t, T*, int64_t, int);
 
 SLATE_LUDIST_INST(float)
 SLATE_LUDIST_INST(double)

@@ -10,6 +10,14 @@ namespace internal {
 namespace ludist {
 
 using RowDist = slate_amd::dev::RowDist;
+using PanelBases = slate_amd::dev::PanelBases;
+
+/// Panel rows kk.. of the view: assemble the all-gathered per-process blocks
+/// into one M x kb panel in global row order (mode 0), or copy my rows of the
+/// assembled panel back to my local panel rows ap (mode 1).
+template <typename T>
+void panel_xfer(lb::Ctx const& c, int64_t M, int64_t kb, int64_t kk, RowDist const& d, PanelBases const& pb,
+                int64_t maxr, T* G, T* P, int64_t ldp, T* ap, int64_t lda, int mode);
 
 /// Row distribution of view A as seen by this process.
 template <typename T>

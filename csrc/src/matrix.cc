@@ -1,4 +1,5 @@
 // MatrixStorage / BaseMatrix implementation and explicit instantiations.
+#include <atomic>
 #include "slate_amd/matrix.hh"
 
 #include <complex>
@@ -100,9 +101,19 @@ void MatrixStorage<T>::attach(T* ptr, int64_t ld_, Loc loc) {
     kind_ = TileKind::UserOwned;
 }
 
+namespace {
+std::atomic<size_t> g_storage_max{0};
+}
+size_t storage_alloc_max() { return g_storage_max.load(); }
+void storage_alloc_reset() { g_storage_max.store(0); }
+
 template <typename T>
 void MatrixStorage<T>::allocate(Loc loc) {
     size_t bytes = size_t(lld) * size_t(std::max<int64_t>(nloc, 1)) * sizeof(T);
+    if ((loc == Loc::Host ? host_ : dev_) == nullptr) {
+        size_t cur = g_storage_max.load();
+        while (bytes > cur && !g_storage_max.compare_exchange_weak(cur, bytes)) {}
+    }
     if (loc == Loc::Host) {
         if (host_) return;
         void* p = nullptr;

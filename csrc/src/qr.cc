@@ -6,13 +6,21 @@
 //     Householder kernel (column norms, reflector, rank-1 updates and the
 //     T factor all on the GPU; T from V^H V + the larft recurrence, as the
 //     reference's larft-by-gemm trick internal_geqrf.cc:286-330).  p > 1:
-//     gathered to the diagonal process, factored, scattered back.
+//     TSQR over the process column (local QR of every process's panel rows,
+//     binary tree of stacked-R QRs rooted at the diagonal process, reference
+//     ttqrt internal_ttqrt.cc:35-130), then Householder reconstruction of
+//     the panel's (V, T) from the tree's explicit Q (sign-modified LU), so
+//     the trailing update below stays one 2-D larfb.
 //   update: the explicit V (unit lower) and T_k are broadcast along process
 //     rows; every process computes W = V_loc^H C_loc for its trailing
 //     columns, the partial W is all-reduced over the column communicator
 //     (p > 1), then W = T^H W and C_loc -= V_loc W -- two MFMA GEMMs and a
-//     small one per process (ScaLAPACK-style 2D larfb).  The reference uses
-//     a TSQR tree (ttqrt/ttmqr) for the p > 1 panel instead.
+//     small one per process (ScaLAPACK-style 2D larfb) -- instead of the
+//     reference's tree application ttmqr (internal_ttmqr.cc:99-290).
+//   lanes: TSQR / (V, T) / lookahead-W messages on the panel queue over the
+//     duplicate comms (Grid::col_fast / row_fast), trailing W all-reduces on
+//     the comm queue, so step k+1's tree never queues behind step k's bulk
+//     all-reduces.
 // T factors: T[0] is an nb x n matrix replicated on every rank (tile k holds
 // the panel's nb x nb upper-triangular T).
 #include "internal.hh"
@@ -35,6 +43,195 @@ inline int64_t qr_kchunk() {
     return v;
 }
 
+/// TSQR of one distributed panel over a communicator (tree rooted at `root`)
+/// followed by Householder reconstruction of the panel's (V, T): every
+/// participant's local panel rows (ap, mr x kb) are overwritten with V (and,
+/// at the root, R + Y1 in the top kd rows); the root gets T in Tk.  The tree
+/// (reference ttqrt, internal_ttqrt.cc:35-130) runs on the panel queue over
+/// the given (fast-lane) communicator; the reconstruction makes the trailing
+/// update one 2-D larfb instead of the reference's tree application (ttmqr).
+/// Used by geqrf (process-column tree) and gelqf (process-row tree on the
+/// conjugate-transposed row panel).
+template <typename T>
+struct TsqrPanel {
+    static constexpr int maxr = 8;   // tree levels (comm size <= 256)
+    int64_t nb;
+    Work<T> Tloc, Rcur, Rrecv, Ecur, Etmp, Qloc, LUb, Ytmp, Dg, Tw, sgn, taul;
+    std::vector<Work<T>> Sst, Ttt;
+    const int64_t tSel = Sched::tok(30, 0);
+
+    TsqrPanel(Target target, int np, int64_t nb_, int64_t max_rows) : nb(nb_) {
+        if (np <= 1) return;
+        const size_t nn = size_t(nb) * nb;
+        Tloc.resize(target, nn); Rcur.resize(target, nn); Rrecv.resize(target, nn);
+        Ecur.resize(target, 2 * nn); Etmp.resize(target, 2 * nn); LUb.resize(target, nn); Ytmp.resize(target, nn);
+        Dg.resize(target, nn); Tw.resize(target, nn); sgn.resize(target, nb); taul.resize(target, 2 * nb);
+        Qloc.resize(target, size_t(std::max<int64_t>(max_rows, 1)) * nb);
+        Sst.resize(maxr); Ttt.resize(maxr);
+        for (int r = 0; r < maxr; ++r) { Sst[r].resize(target, 2 * nn); Ttt[r].resize(target, nn); }
+    }
+
+    /// rows_r[r]: panel rows of comm rank r; me: my comm rank; tPan: the
+    /// panel's data token; tP: output token of (V, T).
+    void enqueue(Sched& S, int qP, Comm& cm, int root, int me, std::vector<int64_t> const& rows_r, T* ap,
+                 int64_t lda, int64_t mr, int64_t kb, int64_t kd, T* Tk, int64_t tPan, int64_t tP) {
+        const int p = int(rows_r.size());
+        const int pk = root;
+        const bool diag = (me == root);
+        const int myrow = me;
+        Comm& colF = cm;
+        std::vector<int> part;
+        for (int d = 0; d < p; ++d) { int r = (pk + d) % p; if (rows_r[r] > 0) part.push_back(r); }
+        const int np = int(part.size());
+        std::vector<int64_t> cnt(np);
+        for (int i = 0; i < np; ++i) cnt[i] = std::min(rows_r[part[i]], kb);
+        int ix = -1;
+        for (int i = 0; i < np; ++i) if (part[i] == myrow) ix = i;
+        struct Round { bool recv; int peer; int64_t mine, theirs; int level; };
+        std::vector<Round> rounds;
+        int lev = 0;
+        for (int l = 1; l < np; l *= 2, ++lev) {
+            for (int i = 0; i + l < np; i += 2 * l) {
+                if (i == ix) rounds.push_back({true, part[i + l], cnt[i], cnt[i + l], lev});
+                if (i + l == ix) rounds.push_back({false, part[i], cnt[i + l], 0, lev});
+                cnt[i] = std::min(cnt[i] + cnt[i + l], kb);
+            }
+        }
+        slate_error_if_msg(lev > maxr, "TSQR: process grid too tall for the tree");
+        const int64_t rr = std::min(mr, kb);     // rows of my local R
+        if (ix >= 0) {
+            // (a) local QR of my panel rows; R -> Rcur (rr x kb, ld rr, zeros below)
+            S.task(qP, {tPan}, {tPan, tSel}, [&, ap, mr, kb, rr](lb::Ctx const& c) {
+                trace::Block t2("geqrf_tsqr_local");
+                lb::geqrf_panel(c, mr, kb, ap, lda, taul.data(), Tloc.data(), nb);
+                lb::set(c, Uplo::General, rr, kb, T(0), T(0), Rcur.data(), rr);
+                lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, rr, kb, ap, lda, Rcur.data(), rr);
+            });
+            // (b) reduction tree: QR of the stacked [R_a; R_b], factors kept per level
+            int64_t cur = rr;
+            int nrecv = 0;
+            for (auto const& r_ : rounds) {
+                if (!r_.recv) {
+                    S.task(qP, {tSel}, {tSel}, [&, r_, kb](lb::Ctx const& c) {
+                        trace::Block t2("geqrf_tsqr_sendR");
+                        std::vector<Comm::P2P> ops{{Rcur.data(), size_t(r_.mine * kb), r_.peer, true}};
+                        colF.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                    });
+                    break;
+                }
+                const int64_t ms = r_.mine + r_.theirs, c2 = std::min(ms, kb);
+                S.task(qP, {}, {tSel}, [&, r_, kb](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_recvR");
+                    std::vector<Comm::P2P> ops{{Rrecv.data(), size_t(r_.theirs * kb), r_.peer, false}};
+                    colF.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                });
+                T* Sb = Sst[r_.level].data();
+                T* Tt = Ttt[r_.level].data();
+                S.task(qP, {}, {tSel}, [&, r_, kb, ms, c2, Sb, Tt](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_merge");
+                    lb::copy2d(c, r_.mine, kb, Rcur.data(), r_.mine, Sb, ms);
+                    lb::copy2d(c, r_.theirs, kb, Rrecv.data(), r_.theirs, Sb + r_.mine, ms);
+                    lb::geqrf_panel(c, ms, kb, Sb, ms, taul.data(), Tt, nb);
+                    lb::set(c, Uplo::General, c2, kb, T(0), T(0), Rcur.data(), c2);
+                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, c2, kb, Sb, ms, Rcur.data(), c2);
+                });
+                cur = c2;
+                ++nrecv;
+            }
+            // (c) explicit Q (first kd columns), top-down: E = [I; 0] at the root
+            const bool sender = !rounds.empty() && !rounds.back().recv;
+            int64_t ecnt = 0;                  // rows of my current E block (ld ecnt)
+            if (diag) {
+                S.task(qP, {}, {tSel}, [&, cur, kd](lb::Ctx const& c) {
+                    lb::set(c, Uplo::General, cur, kd, T(0), T(1), Ecur.data(), cur);
+                });
+                ecnt = cur;
+            } else if (sender) {
+                auto const r_ = rounds.back();
+                S.task(qP, {}, {tSel}, [&, r_, kd](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_recvE");
+                    std::vector<Comm::P2P> ops{{Ecur.data(), size_t(r_.mine * kd), r_.peer, false}};
+                    colF.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                });
+                ecnt = r_.mine;
+            }
+            for (int t = nrecv - 1; t >= 0; --t) {
+                auto const r_ = rounds[t];
+                const int64_t ms = r_.mine + r_.theirs, c2 = std::min(ms, kb);
+                T* Sb = Sst[r_.level].data();
+                T* Tt = Ttt[r_.level].data();
+                // E (c2 x kd) -> [E; 0] (ms x kd) -> Q_level [E; 0]
+                S.task(qP, {}, {tSel}, [&, ms, c2, kd, Sb, Tt](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_qtree");
+                    lb::set(c, Uplo::General, ms, kd, T(0), T(0), Etmp.data(), ms);
+                    lb::copy2d(c, c2, kd, Ecur.data(), c2, Etmp.data(), ms);
+                    lb::larfb(c, Side::Left, Op::NoTrans, ms, kd, c2, Sb, ms, Tt, nb, Etmp.data(), ms);
+                });
+                // partner's rows go down the tree, mine stay (compacted to ld = mine)
+                S.task(qP, {}, {tSel}, [&, r_, ms, kd](lb::Ctx const& c) {
+                    trace::Block t2("geqrf_tsqr_sendE");
+                    lb::copy2d(c, r_.theirs, kd, Etmp.data() + r_.mine, ms, Rrecv.data(), r_.theirs);
+                    std::vector<Comm::P2P> ops{{Rrecv.data(), size_t(r_.theirs * kd), r_.peer, true}};
+                    colF.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+                });
+                S.task(qP, {}, {tSel}, [&, r_, ms, kd](lb::Ctx const& c) {
+                    lb::copy2d(c, r_.mine, kd, Etmp.data(), ms, Ecur.data(), r_.mine);
+                });
+                ecnt = r_.mine;
+            }
+            // (d) local rows of Q: Qloc = Q_local [E; 0]  (mr x kd)
+            S.task(qP, {tSel}, {tSel}, [&, ap, mr, rr, kd, ecnt](lb::Ctx const& c) {
+                trace::Block t2("geqrf_tsqr_qlocal");
+                lb::set(c, Uplo::General, mr, kd, T(0), T(0), Qloc.data(), mr);
+                lb::copy2d(c, ecnt, kd, Ecur.data(), ecnt, Qloc.data(), mr);
+                lb::larfb(c, Side::Left, Op::NoTrans, mr, kd, rr, ap, lda, Tloc.data(), nb, Qloc.data(), mr);
+            });
+        }
+        // (e) pk: sign-modified LU of [S - Q11]  ->  Y1, U', S
+        if (diag) {
+            S.task(qP, {tSel}, {tSel}, [&, mr, kd](lb::Ctx const& c) {
+                trace::Block t2("geqrf_tsqr_hr_lu");
+                lb::add(c, Uplo::General, kd, kd, T(-1), Qloc.data(), mr, T(0), LUb.data(), kd);
+                internal::ludist::lu_sign(c, kd, LUb.data(), kd, sgn.data());
+            });
+        }
+        S.task(qP, {}, {tSel}, [&, kd, pk](lb::Ctx const& c) {
+            trace::Block t2("geqrf_tsqr_bcast_lu");
+            bcast(colF, LUb.data(), size_t(kd * kd), pk, c);
+            bcast(colF, sgn.data(), size_t(kd), pk, c);
+        });
+        // (f) V below T: Y2 = -Q21 U'^{-1}, written into the panel rows
+        const int64_t off = diag ? kd : 0, nbelow = std::max<int64_t>(mr - off, 0);
+        S.task(qP, {tSel}, {tPan, tSel}, [&, ap, mr, kd, off, nbelow](lb::Ctx const& c) {
+            trace::Block t2("geqrf_tsqr_hr_v");
+            lb::trsm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, nbelow, kd, T(-1), LUb.data(), kd,
+                     Qloc.data() + off, std::max<int64_t>(mr, 1));
+            lb::copy2d(c, nbelow, kd, Qloc.data() + off, std::max<int64_t>(mr, 1), ap + off, lda);
+        });
+        // (g) pk: R = S R_tsqr and Y1 into the diagonal block; T = U' S^H Y1^{-H}
+        if (diag) {
+            S.task(qP, {tSel}, {tPan, tSel, tP}, [&, ap, kb, kd, Tk](lb::Ctx const& c) {
+                trace::Block t2("geqrf_tsqr_hr_t");
+                // Dg = diag(s)
+                lb::set(c, Uplo::General, kd, kd, T(0), T(0), Dg.data(), kd);
+                lb::copy2d(c, int64_t(1), kd, sgn.data(), int64_t(1), Dg.data(), kd + 1);
+                // A(T rows) = S R_tsqr (upper trapezoid) + strictly-lower Y1
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, kd, kb, kd, T(1), Dg.data(), kd, Rcur.data(), kd, T(0), ap,
+                         lda);
+                lb::copy2d(c, kd, kd, LUb.data(), kd, Ytmp.data(), kd);
+                lb::set(c, Uplo::Upper, kd, kd, T(0), T(0), Ytmp.data(), kd);
+                lb::add(c, Uplo::Lower, kd, kd, T(1), Ytmp.data(), kd, T(1), ap, lda);
+                // T = triu(U') S^H Y1^{-H}, padded to kb x kb
+                lb::set(c, Uplo::General, kd, kd, T(0), T(0), Tw.data(), kd);
+                lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, kd, kd, LUb.data(), kd, Tw.data(), kd);
+                lb::set(c, Uplo::General, kb, kb, T(0), T(0), Tk, kb);
+                lb::gemm(c, Op::NoTrans, Op::ConjTrans, kd, kd, kd, T(1), Tw.data(), kd, Dg.data(), kd, T(0), Tk, kb);
+                lb::trsm(c, Side::Right, Uplo::Lower, Op::ConjTrans, Diag::Unit, kd, kd, T(1), LUb.data(), kd, Tk, kb);
+            });
+        }
+    }
+};
+
 template <typename T>
 void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
     auto& g = *A.grid();
@@ -50,6 +247,11 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
     T* tm = LT.ptr;
     const int64_t ldt = LT.ld;
     const int qC = device::kCommQueue, qP = 1;
+    // critical-path lane: TSQR tree, (V, T) broadcasts and the lookahead
+    // columns' W all-reduce on the panel queue over the duplicate comms;
+    // the trailing chunks' W all-reduces stay on the comm queue (bulk lane)
+    Comm& colF = g.col_fast();
+    Comm& rowF = g.row_fast();
 
     Sched S(target);
     const int R = int(std::max<int64_t>(2, la + 2));
@@ -61,20 +263,7 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         WW2[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         Wtau[r].resize(target, size_t(nb));
     }
-    // TSQR scratch (p > 1): local T, current / received R, E blocks of the
-    // explicit Q, per-level stacked factors, local Q rows, the sign-modified LU
-    const int maxr = 8;   // tree levels (p <= 256)
-    Work<T> Tloc, Rcur, Rrecv, Ecur, Etmp, Qloc, LUb, Ytmp, Dg, Tw, sgn, taul;
-    std::vector<Work<T>> Sst(p > 1 ? maxr : 0), Ttt(p > 1 ? maxr : 0);
-    if (p > 1) {
-        const size_t nn = size_t(nb) * nb;
-        Tloc.resize(target, nn); Rcur.resize(target, nn); Rrecv.resize(target, nn);
-        Ecur.resize(target, 2 * nn); Etmp.resize(target, 2 * nn); LUb.resize(target, nn); Ytmp.resize(target, nn);
-        Dg.resize(target, nn); Tw.resize(target, nn); sgn.resize(target, nb); taul.resize(target, 2 * nb);
-        Qloc.resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
-        for (int r = 0; r < maxr; ++r) { Sst[r].resize(target, 2 * nn); Ttt[r].resize(target, nn); }
-    }
-    const int64_t tSel = Sched::tok(30, 0);
+    TsqrPanel<T> tsqr(target, p > 1 ? p : 1, nb, mloc);
     const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
 
     for (int64_t k = 0; k < kt; ++k) {
@@ -104,171 +293,23 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
             //      reconstruction of (V, T) (kernels/tsqr.hip)
             std::vector<int64_t> rows_r(p, 0);
             for (int64_t i = k; i < mt; ++i) rows_r[A.srow_owner(i)] += A.tileMb(i);
-            std::vector<int> part;
-            for (int d = 0; d < p; ++d) { int r = (pk + d) % p; if (rows_r[r] > 0) part.push_back(r); }
-            const int np = int(part.size());
-            std::vector<int64_t> cnt(np);
-            for (int i = 0; i < np; ++i) cnt[i] = std::min(rows_r[part[i]], kb);
-            int ix = -1;
-            for (int i = 0; i < np; ++i) if (part[i] == myrow) ix = i;
-            struct Round { bool recv; int peer; int64_t mine, theirs; int level; };
-            std::vector<Round> rounds;
-            int lev = 0;
-            for (int l = 1; l < np; l *= 2, ++lev) {
-                for (int i = 0; i + l < np; i += 2 * l) {
-                    if (i == ix) rounds.push_back({true, part[i + l], cnt[i], cnt[i + l], lev});
-                    if (i + l == ix) rounds.push_back({false, part[i], cnt[i + l], 0, lev});
-                    cnt[i] = std::min(cnt[i] + cnt[i + l], kb);
-                }
-            }
-            slate_error_if_msg(lev > maxr, "geqrf: process grid too tall for the TSQR tree");
-            const int64_t rr = std::min(mr, kb);     // rows of my local R
-            if (ix >= 0) {
-                // (a) local QR of my panel rows; R -> Rcur (rr x kb, ld rr, zeros below)
-                S.task(qP, {Sched::col(k)}, {Sched::col(k), tSel}, [&, ap, mr, kb, rr](lb::Ctx const& c) {
-                    trace::Block t2("geqrf_tsqr_local");
-                    lb::geqrf_panel(c, mr, kb, ap, lda, taul.data(), Tloc.data(), nb);
-                    lb::set(c, Uplo::General, rr, kb, T(0), T(0), Rcur.data(), rr);
-                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, rr, kb, ap, lda, Rcur.data(), rr);
-                });
-                // (b) reduction tree: QR of the stacked [R_a; R_b], factors kept per level
-                int64_t cur = rr;
-                int nrecv = 0;
-                for (auto const& r_ : rounds) {
-                    if (!r_.recv) {
-                        S.task(qC, {tSel}, {tSel}, [&, r_, kb](lb::Ctx const& c) {
-                            trace::Block t2("geqrf_tsqr_sendR");
-                            std::vector<Comm::P2P> ops{{Rcur.data(), size_t(r_.mine * kb), r_.peer, true}};
-                            g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                        });
-                        break;
-                    }
-                    const int64_t ms = r_.mine + r_.theirs, c2 = std::min(ms, kb);
-                    S.task(qC, {}, {tSel}, [&, r_, kb](lb::Ctx const& c) {
-                        trace::Block t2("geqrf_tsqr_recvR");
-                        std::vector<Comm::P2P> ops{{Rrecv.data(), size_t(r_.theirs * kb), r_.peer, false}};
-                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                    });
-                    T* Sb = Sst[r_.level].data();
-                    T* Tt = Ttt[r_.level].data();
-                    S.task(qP, {}, {tSel}, [&, r_, kb, ms, c2, Sb, Tt](lb::Ctx const& c) {
-                        trace::Block t2("geqrf_tsqr_merge");
-                        lb::copy2d(c, r_.mine, kb, Rcur.data(), r_.mine, Sb, ms);
-                        lb::copy2d(c, r_.theirs, kb, Rrecv.data(), r_.theirs, Sb + r_.mine, ms);
-                        lb::geqrf_panel(c, ms, kb, Sb, ms, taul.data(), Tt, nb);
-                        lb::set(c, Uplo::General, c2, kb, T(0), T(0), Rcur.data(), c2);
-                        lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, c2, kb, Sb, ms, Rcur.data(), c2);
-                    });
-                    cur = c2;
-                    ++nrecv;
-                }
-                // (c) explicit Q (first kd columns), top-down: E = [I; 0] at the root
-                const bool sender = !rounds.empty() && !rounds.back().recv;
-                int64_t ecnt = 0;                  // rows of my current E block (ld ecnt)
-                if (diag) {
-                    S.task(qP, {}, {tSel}, [&, cur, kd](lb::Ctx const& c) {
-                        lb::set(c, Uplo::General, cur, kd, T(0), T(1), Ecur.data(), cur);
-                    });
-                    ecnt = cur;
-                } else if (sender) {
-                    auto const r_ = rounds.back();
-                    S.task(qC, {}, {tSel}, [&, r_, kd](lb::Ctx const& c) {
-                        trace::Block t2("geqrf_tsqr_recvE");
-                        std::vector<Comm::P2P> ops{{Ecur.data(), size_t(r_.mine * kd), r_.peer, false}};
-                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                    });
-                    ecnt = r_.mine;
-                }
-                for (int t = nrecv - 1; t >= 0; --t) {
-                    auto const r_ = rounds[t];
-                    const int64_t ms = r_.mine + r_.theirs, c2 = std::min(ms, kb);
-                    T* Sb = Sst[r_.level].data();
-                    T* Tt = Ttt[r_.level].data();
-                    // E (c2 x kd) -> [E; 0] (ms x kd) -> Q_level [E; 0]
-                    S.task(qP, {}, {tSel}, [&, ms, c2, kd, Sb, Tt](lb::Ctx const& c) {
-                        trace::Block t2("geqrf_tsqr_qtree");
-                        lb::set(c, Uplo::General, ms, kd, T(0), T(0), Etmp.data(), ms);
-                        lb::copy2d(c, c2, kd, Ecur.data(), c2, Etmp.data(), ms);
-                        lb::larfb(c, Side::Left, Op::NoTrans, ms, kd, c2, Sb, ms, Tt, nb, Etmp.data(), ms);
-                    });
-                    // partner's rows go down the tree, mine stay (compacted to ld = mine)
-                    S.task(qC, {}, {tSel}, [&, r_, ms, kd](lb::Ctx const& c) {
-                        trace::Block t2("geqrf_tsqr_sendE");
-                        lb::copy2d(c, r_.theirs, kd, Etmp.data() + r_.mine, ms, Rrecv.data(), r_.theirs);
-                        std::vector<Comm::P2P> ops{{Rrecv.data(), size_t(r_.theirs * kd), r_.peer, true}};
-                        g.col().exchange(ops, scalar_type<T>(), c.loc(), c.stream);
-                    });
-                    S.task(qP, {}, {tSel}, [&, r_, ms, kd](lb::Ctx const& c) {
-                        lb::copy2d(c, r_.mine, kd, Etmp.data(), ms, Ecur.data(), r_.mine);
-                    });
-                    ecnt = r_.mine;
-                }
-                // (d) local rows of Q: Qloc = Q_local [E; 0]  (mr x kd)
-                S.task(qP, {tSel}, {tSel}, [&, ap, mr, rr, kd, ecnt](lb::Ctx const& c) {
-                    trace::Block t2("geqrf_tsqr_qlocal");
-                    lb::set(c, Uplo::General, mr, kd, T(0), T(0), Qloc.data(), mr);
-                    lb::copy2d(c, ecnt, kd, Ecur.data(), ecnt, Qloc.data(), mr);
-                    lb::larfb(c, Side::Left, Op::NoTrans, mr, kd, rr, ap, lda, Tloc.data(), nb, Qloc.data(), mr);
-                });
-            }
-            // (e) pk: sign-modified LU of [S - Q11]  ->  Y1, U', S
-            if (diag) {
-                S.task(qP, {tSel}, {tSel}, [&, mr, kd](lb::Ctx const& c) {
-                    trace::Block t2("geqrf_tsqr_hr_lu");
-                    lb::add(c, Uplo::General, kd, kd, T(-1), Qloc.data(), mr, T(0), LUb.data(), kd);
-                    internal::ludist::lu_sign(c, kd, LUb.data(), kd, sgn.data());
-                });
-            }
-            S.task(qC, {}, {tSel}, [&, kd, pk](lb::Ctx const& c) {
-                trace::Block t2("geqrf_tsqr_bcast_lu");
-                bcast(g.col(), LUb.data(), size_t(kd * kd), pk, c);
-                bcast(g.col(), sgn.data(), size_t(kd), pk, c);
-            });
-            // (f) V below T: Y2 = -Q21 U'^{-1}, written into the panel rows
-            const int64_t off = diag ? kd : 0, nbelow = std::max<int64_t>(mr - off, 0);
-            S.task(qP, {tSel}, {Sched::col(k), tSel}, [&, ap, mr, kd, off, nbelow](lb::Ctx const& c) {
-                trace::Block t2("geqrf_tsqr_hr_v");
-                lb::trsm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, nbelow, kd, T(-1), LUb.data(), kd,
-                         Qloc.data() + off, std::max<int64_t>(mr, 1));
-                lb::copy2d(c, nbelow, kd, Qloc.data() + off, std::max<int64_t>(mr, 1), ap + off, lda);
-            });
-            // (g) pk: R = S R_tsqr and Y1 into the diagonal block; T = U' S^H Y1^{-H}
-            if (diag) {
-                S.task(qP, {tSel}, {Sched::col(k), tSel, tP}, [&, ap, kb, kd, Tk](lb::Ctx const& c) {
-                    trace::Block t2("geqrf_tsqr_hr_t");
-                    // Dg = diag(s)
-                    lb::set(c, Uplo::General, kd, kd, T(0), T(0), Dg.data(), kd);
-                    lb::copy2d(c, int64_t(1), kd, sgn.data(), int64_t(1), Dg.data(), kd + 1);
-                    // A(T rows) = S R_tsqr (upper trapezoid) + strictly-lower Y1
-                    lb::gemm(c, Op::NoTrans, Op::NoTrans, kd, kb, kd, T(1), Dg.data(), kd, Rcur.data(), kd, T(0), ap,
-                             lda);
-                    lb::copy2d(c, kd, kd, LUb.data(), kd, Ytmp.data(), kd);
-                    lb::set(c, Uplo::Upper, kd, kd, T(0), T(0), Ytmp.data(), kd);
-                    lb::add(c, Uplo::Lower, kd, kd, T(1), Ytmp.data(), kd, T(1), ap, lda);
-                    // T = triu(U') S^H Y1^{-H}, padded to kb x kb
-                    lb::set(c, Uplo::General, kd, kd, T(0), T(0), Tw.data(), kd);
-                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, kd, kd, LUb.data(), kd, Tw.data(), kd);
-                    lb::set(c, Uplo::General, kb, kb, T(0), T(0), Tk, kb);
-                    lb::gemm(c, Op::NoTrans, Op::ConjTrans, kd, kd, kd, T(1), Tw.data(), kd, Dg.data(), kd, T(0), Tk, kb);
-                    lb::trsm(c, Side::Right, Uplo::Lower, Op::ConjTrans, Diag::Unit, kd, kd, T(1), LUb.data(), kd, Tk, kb);
-                });
-            }
+            tsqr.enqueue(S, qP, colF, pk, myrow, rows_r, ap, lda, mr, kb, kd, Tk, Sched::col(k), tP);
         }
 
         // ======================= T_k down the panel column, then (V, T_k) along rows
         T* Vk = WV[slot].data();
         const int64_t ldv = std::max<int64_t>(mr, 1);
-        S.task(qC, {tP, Sched::col(k)}, {tB}, [&, kb, kk, lr_k, lc_k, mr, pk, qk, Tk, Vk, ldv, in_col, diag](lb::Ctx const& c) {
+        S.task(qP, {tP, Sched::col(k)}, {tB}, [&, kb, kk, lr_k, lc_k, mr, pk, qk, Tk, Vk, ldv, in_col, diag](lb::Ctx const& c) {
             trace::Block t2("geqrf_bcast");
             if (in_col) {
-                if (p > 1) bcast(g.col(), Tk, size_t(kb * kb), pk, c);
+                if (p > 1) bcast(colF, Tk, size_t(kb * kb), pk, c);
                 // explicit V: my rows >= kk; the diagonal process row has the unit upper part
                 pack(c, mr, kb, a + lr_k + lc_k * lda, lda, Vk);
                 if (diag) lb::set(c, Uplo::Upper, std::min<int64_t>(kb, mr), kb, T(0), T(1), Vk, ldv);
             }
             if (q > 1) {
-                bcast(g.row(), Tk, size_t(kb * kb), qk, c);
-                bcast(g.row(), Vk, size_t(mr * kb), qk, c);
+                bcast(rowF, Tk, size_t(kb * kb), qk, c);
+                bcast(rowF, Vk, size_t(mr * kb), qk, c);
             }
             // keep T_k in the replicated factor matrix
             lb::copy2d(c, kb, kb, Tk, kb, tm + kk * ldt, ldt);
@@ -324,9 +365,11 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
             // p > 1: the column all-reduce of W runs on the comm queue between
             // the two halves, which stay on the compute queue
             S.task(queue, {tB}, cols, [&, c0, nc](lb::Ctx const& c) { trace::Block t2("geqrf_update_w"); vhc(c, c0, nc); });
-            S.task(qC, {}, cols, [&, c0, nc, kb, Wk](lb::Ctx const& c) {
+            const bool crit = (queue == device::kLookaheadQueue);
+            Comm& cw = crit ? colF : g.col();
+            S.task(crit ? qP : qC, {}, cols, [&, c0, nc, kb, Wk](lb::Ctx const& c) {
                 trace::Block t2("geqrf_update_allreduce");
-                g.col().allreduce(Wk + c0 * kb, size_t(kb * nc), ReduceOp::Sum, c.loc(), c.stream);
+                cw.allreduce(Wk + c0 * kb, size_t(kb * nc), ReduceOp::Sum, c.loc(), c.stream);
             });
             S.task(queue, {tB}, cols, [&, c0, nc](lb::Ctx const& c) { trace::Block t2("geqrf_update_c"); apply(c, c0, nc); });
         };
@@ -458,30 +501,262 @@ void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
     slate::copy<T, T>(conj_transpose(Cx), C, opts);
 }
 
-// LQ via the QR of A^H: A^H = Q' R'  =>  A = R'^H Q'^H = L Q.
+//------------------------------------------------------------------------------
+// LQ (reference src/gelqf.cc:207-298 with ttlqt/ttmlq, src/unmlq.cc).
+namespace {
+
+/// A = L Q on row panels, in place, no transposed copy of A.  Per block row
+/// k the row panel A(k, k:) (process row pk, spread over the process
+/// columns) is conjugate-transposed into a column buffer P (my local columns
+/// x kb), QR-factored there -- the device panel kernel when q == 1, else the
+/// TSQR tree over the PROCESS ROW (fast-lane row comm) -- and written back:
+/// L(k,k) on/below the diagonal, the reflectors Y^H stored row-wise to its
+/// right (LAPACK gelqf layout).  With H_k = I - Y T Y^H, the rows below are
+/// updated from the right, C := C H_k = C - (C Y) T Y^H: W = C Y per
+/// process, all-reduced across the process row, then two GEMMs.  Y goes down
+/// the process columns, T along the row; the block row k+1 is updated first
+/// (lookahead queue, fast lane), the rest on the trailing queue.
+template <typename T>
+void gelqf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target) {
+    auto& g = *A.grid();
+    const int q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    const int64_t mt = A.mt(), nt = A.nt(), n = A.n();
+    const int64_t kt = std::min(mt, nt);
+    const int64_t nb = A.nb();
+    LocalBlock<T> L = A.local(loc, true);
+    T* a = L.ptr;
+    const int64_t lda = L.ld, mloc = L.m, nloc = L.n;
+    LocalBlock<T> LT = Tf.local(loc, true);
+    T* tm = LT.ptr;
+    const int64_t ldt = LT.ld;
+    const int qC = device::kCommQueue, qP = 1;
+    Comm& colF = g.col_fast();
+    Comm& rowF = g.row_fast();
+    Sched S(target);
+    const int R = 3;
+    std::vector<Work<T>> WY(R), WT(R), WW(R), WW2(R), Wtau(R);
+    for (int r = 0; r < R; ++r) {
+        WY[r].resize(target, size_t(std::max<int64_t>(nloc, 1)) * nb);
+        WT[r].resize(target, size_t(nb) * nb);
+        WW[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+        WW2[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
+        Wtau[r].resize(target, size_t(nb));
+    }
+    TsqrPanel<T> tsqr(target, q, nb, nloc);
+    for (int64_t k = 0; k < kt; ++k) {
+        const int64_t kb = A.tileMb(k);               // panel rows
+        const int64_t kk = gcol_of(A, k);             // first panel column
+        const int64_t N = n - kk, kd = std::min(kb, N);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const bool in_row = (myrow == pk), diag = (mycol == qk);
+        const int64_t lc_k = lcol_of(A, k), nc = nloc - lc_k, ldy = std::max<int64_t>(nc, 1);
+        const int64_t lr_k = in_row ? lrow_of(A, k) : 0;
+        T* rp = a + lr_k + lc_k * lda;
+        const int slot = int(k % R);
+        T* Yk = WY[slot].data();
+        T* Tk = WT[slot].data();
+        const int64_t tP = Sched::tok(6, slot), tB = Sched::bcast(slot), tPan = Sched::row(k);
+        // ---- panel: P = rp^H, QR(P), rp = P^H, explicit Y
+        if (in_row) {
+            // (tB as an output: Y_k / T_k of this ring slot are free once the
+            // previous step using the slot has finished its updates)
+            S.task(qP, {Sched::row(k)}, {tPan, tB}, [&, kb, nc, rp, Yk, ldy](lb::Ctx const& c) {
+                trace::Block t2("gelqf_panel_pack");
+                lb::copy<T, T>(c, Uplo::General, Op::ConjTrans, nc, kb, rp, lda, Yk, ldy);
+            });
+            if (q == 1) {
+                S.task(qP, {tPan}, {tPan, tP}, [&, nc, kb, Yk, ldy, Tk, slot](lb::Ctx const& c) {
+                    trace::Block t2("gelqf_panel");
+                    lb::geqrf_panel(c, nc, kb, Yk, ldy, Wtau[slot].data(), Tk, kb);
+                });
+            } else {
+                std::vector<int64_t> cols_c(q, 0);
+                for (int64_t j = k; j < nt; ++j) cols_c[A.scol_owner(j)] += A.tileNb(j);
+                tsqr.enqueue(S, qP, rowF, qk, mycol, cols_c, Yk, ldy, nc, kb, kd, Tk, tPan, tP);
+            }
+            S.task(qP, {tPan}, {tPan, Sched::row(k)}, [&, kb, kd, nc, rp, Yk, ldy, diag](lb::Ctx const& c) {
+                trace::Block t2("gelqf_panel_unpack");
+                lb::copy<T, T>(c, Uplo::General, Op::ConjTrans, kb, nc, Yk, ldy, rp, lda);
+                if (diag) lb::set(c, Uplo::Upper, std::min<int64_t>(kd, nc), kb, T(0), T(1), Yk, ldy);
+            });
+        }
+        // ---- T_k along the panel's process row, then Y and T_k down the columns
+        S.task(qP, {tP, tPan}, {tB}, [&, kb, kk, nc, pk, qk, Tk, Yk, in_row](lb::Ctx const& c) {
+            trace::Block t2("gelqf_bcast");
+            if (in_row && q > 1) bcast(rowF, Tk, size_t(kb * kb), qk, c);
+            bcast(colF, Tk, size_t(kb * kb), pk, c);
+            bcast(colF, Yk, size_t(nc * kb), pk, c);
+            lb::copy2d(c, kb, kb, Tk, kb, tm + kk * ldt, ldt);
+        });
+        // ---- rows below: C := C - (C Y) T Y^H
+        auto upd = [&, k, kb, nc, lc_k, Yk, Tk, ldy, slot](int queue, int64_t i0, int64_t i1, bool crit) {
+            const int64_t r0 = lrow_of(A, i0), r1 = lrow_of(A, i1), mr = r1 - r0;
+            std::vector<int64_t> rows;
+            for (int64_t i = i0; i < i1; ++i) rows.push_back(Sched::row(i));
+            // row chunk [r0, r1) of W / W2, contiguous (ld = mr) for the all-reduce
+            T* W = WW[slot].data() + r0 * kb;
+            T* W2 = WW2[slot].data() + r0 * kb;
+            const int64_t ldw = std::max<int64_t>(mr, 1);
+            T* C = a + r0 + lc_k * lda;
+            S.task(queue, {tB}, rows, [&, mr, W, C](lb::Ctx const& c) {
+                trace::Block t2("gelqf_update_w");
+                if (mr <= 0) return;
+                if (nc > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, kb, nc, T(1), C, lda, Yk, ldy, T(0), W, ldw);
+                else lb::set(c, Uplo::General, mr, kb, T(0), T(0), W, ldw);
+            });
+            if (q > 1) {
+                Comm& cw = crit ? rowF : g.row();
+                S.task(crit ? qP : qC, {}, rows, [&, mr, W](lb::Ctx const& c) {
+                    trace::Block t2("gelqf_update_allreduce");
+                    if (mr > 0) cw.allreduce(W, W, size_t(mr * kb), scalar_type<T>(), ReduceOp::Sum, c.loc(), c.stream);
+                });
+            }
+            S.task(queue, {tB}, rows, [&, mr, W, W2, C](lb::Ctx const& c) {
+                trace::Block t2("gelqf_update_c");
+                if (mr <= 0) return;
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, kb, kb, T(1), W, ldw, Tk, kb, T(0), W2, ldw);
+                if (nc > 0) lb::gemm(c, Op::NoTrans, Op::ConjTrans, mr, nc, kb, T(-1), W2, ldw, Yk, ldy, T(1), C, lda);
+            });
+        };
+        if (k + 1 < mt) {
+            upd(device::kLookaheadQueue, k + 1, k + 2, true);
+            if (k + 2 < mt) upd(device::kTrailQueue, k + 2, mt, false);
+        }
+    }
+    S.wait_all();
+    A.storage()->update_origin();
+    Tf.storage()->update_origin();
+}
+
+/// C = op(Q) C with the gelqf factors, C's rows following A's COLUMNS (C on
+/// A's transposed grid): Q = H_{kt-1}^H ... H_0^H, H_k = I - Y T Y^H.
+/// NoTrans: k ascending with T^H; ConjTrans: k descending with T.  Per step
+/// Y_k (the conj-transposed row panel, my local columns) goes down the
+/// process columns of A, W = Y^H C is all-reduced across A's process row,
+/// C -= Y (op(T) W).
+template <typename T>
+void unmlq_left(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Target target) {
+    auto& g = *A.grid();
+    const int mycol = g.mycol(), myrow = g.myrow();
+    const Loc loc = loc_of(target);
+    const int64_t kt = std::min(A.mt(), A.nt());
+    LocalBlock<T> L = A.local(loc, false);
+    LocalBlock<T> LC = C.local(loc, true);
+    LocalBlock<T> LT = Tf.local(loc, false);
+    const int64_t nb = A.nb(), nloc = L.n;
+    Sched S(target);
+    Work<T> Y(target, size_t(std::max<int64_t>(nloc, 1)) * nb), W(target, size_t(nb) * std::max<int64_t>(LC.n, 1)),
+        W2(target, size_t(nb) * std::max<int64_t>(LC.n, 1));
+    const int64_t tY = Sched::tok(40, 0), tC = Sched::tok(41, 0);
+    for (int64_t t = 0; t < kt; ++t) {
+        const int64_t k = (op == Op::NoTrans) ? t : kt - 1 - t;
+        const int64_t kb = A.tileMb(k), kk = gcol_of(A, k), kd = std::min(kb, A.n() - kk);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int64_t lc_k = lcol_of(A, k), nc = nloc - lc_k, ldy = std::max<int64_t>(nc, 1);
+        const int64_t lcr = lrow_of(C, k);     // C's local rows >= kk (rows follow A's columns)
+        S.task(1, {tC}, {tY}, [&, kb, kd, nc, lc_k, ldy, pk, qk](lb::Ctx const& c) {
+            trace::Block t2("unmlq_bcast_y");
+            if (myrow == pk) {
+                lb::copy<T, T>(c, Uplo::General, Op::ConjTrans, nc, kb, L.ptr + lrow_of(A, k) + lc_k * L.ld, L.ld,
+                               Y.data(), ldy);
+                if (mycol == qk) lb::set(c, Uplo::Upper, std::min<int64_t>(kd, nc), kb, T(0), T(1), Y.data(), ldy);
+            }
+            bcast(g.col_fast(), Y.data(), size_t(nc * kb), pk, c);
+        });
+        S.task(0, {tY}, {tC}, [&, kb, kk, nc, ldy, lcr](lb::Ctx const& c) {
+            trace::Block t2("unmlq_update");
+            const int64_t ncC = LC.n;
+            T* Cc = LC.ptr + lcr;
+            if (nc > 0) lb::gemm(c, Op::ConjTrans, Op::NoTrans, kb, ncC, nc, T(1), Y.data(), ldy, Cc, LC.ld, T(0),
+                                 W.data(), kb);
+            else lb::set(c, Uplo::General, kb, ncC, T(0), T(0), W.data(), kb);
+            if (g.q() > 1) g.row().allreduce(W.data(), W.data(), size_t(kb * ncC), scalar_type<T>(), ReduceOp::Sum,
+                                             c.loc(), c.stream);
+            lb::gemm(c, op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans, Op::NoTrans, kb, ncC, kb, T(1),
+                     LT.ptr + kk * LT.ld, LT.ld, W.data(), kb, T(0), W2.data(), kb);
+            if (nc > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, nc, ncC, kb, T(-1), Y.data(), ldy, W2.data(), kb, T(1),
+                                 Cc, LC.ld);
+        });
+    }
+    S.wait_all();
+    C.storage()->update_origin();
+}
+
+/// Does C's row distribution follow A's columns (C on A's transposed grid)?
+template <typename T>
+bool rows_follow_cols(BaseMatrix<T> const& A, BaseMatrix<T> const& C) {
+    auto& ga = *A.grid();
+    auto& gc = *C.grid();
+    if (C.op() != Op::NoTrans || !C.aligned() || !ga.same_processes(gc)) return false;
+    if (gc.p() != ga.q() || gc.q() != ga.p() || (gc.size() > 1 && gc.order() == ga.order())) return false;
+    if (C.mt() != A.nt()) return false;
+    for (int64_t j = 0; j < A.nt(); ++j)
+        if (A.tileNb(j) != C.tileMb(j) || A.scol_owner(j) != C.srow_owner(j)) return false;
+    return true;
+}
+
+}  // namespace
+
 template <typename T>
 void gelqf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> Ab = internal::block_cyclic(A, opts);
+        gelqf(Ab, T_, opts);
+        slate::copy<T, T>(Ab, A, opts);
+        return;
+    }
     trace::Block tb("gelqf");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
-    Matrix<T> Ah = A.emptyLike(0, 0, Op::ConjTrans);
-    Ah.insertLocalTiles(target);
-    slate::copy<T, T>(conj_transpose(A), Ah, opts);
-    geqrf(Ah, T_, opts);
-    slate::copy<T, T>(conj_transpose(Ah), A, opts);
+    slate_error_if_msg(A.op() != Op::NoTrans || !A.aligned() || A.mb() != A.nb(),
+                       "gelqf: NoTrans, tile-aligned, square-tile matrix required");
+    // T_k is tileMb(k) x tileMb(k) at column gcol(k): room for a full last tile
+    Matrix<T> Tf(A.nb(), std::max<int64_t>(A.n(), 1) + A.nb(), A.nb(), A.nb(), Grid::self());
+    Tf.insertLocalTiles(target);
+    set(T(0), T(0), Tf, opts);
+    gelqf_impl<T>(A, Tf, target);
+    if (target == Target::Devices) lb::check_panel_errors();
+    internal::finish_origin(A, opts);
+    T_.clear();
+    T_.push_back(Tf);
 }
 
 template <typename T>
 void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C, Options const& opts) {
+    if (A.arbitrary_layout()) {
+        Matrix<T> Ab = internal::block_cyclic(A, opts);
+        unmlq(side, op, Ab, T_, C, opts);
+        return;
+    }
     trace::Block tb("unmlq");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
-    // Q = Q'^H where Q' is the QR factor of A^H
-    Matrix<T> Ah = A.emptyLike(0, 0, Op::ConjTrans);
-    Ah.insertLocalTiles(target);
-    slate::copy<T, T>(conj_transpose(A), Ah, opts);
-    Op o2 = (op == Op::NoTrans) ? Op::ConjTrans : Op::NoTrans;
-    unmqr(side, o2, Ah, T_, C, opts);
+    slate_error_if_msg(T_.empty(), "unmlq: missing T factors");
+    if (!is_complex_v<T> && op == Op::Trans) op = Op::ConjTrans;
+    const Op opl = (op == Op::NoTrans) ? Op::NoTrans : Op::ConjTrans;
+    GridPtr gt = A.grid()->transposed();
+    const int rsrc = A.nt() ? A.scol_owner(0) : 0;
+    if (side == Side::Left) {
+        if (rows_follow_cols(A, C)) {
+            unmlq_left<T>(opl, A, T_[0], C, target);
+            internal::finish_origin(C, opts);
+            return;
+        }
+        // C (n x nrhs) redistributed to follow A's columns -- never A
+        Matrix<T> Cx(C.m(), C.n(), A.nb(), C.nb(), gt, rsrc, 0);
+        Cx.insertLocalTiles(target);
+        slate::copy<T, T>(C, Cx, opts);
+        unmlq_left<T>(opl, A, T_[0], Cx, target);
+        slate::copy<T, T>(Cx, C, opts);
+        return;
+    }
+    // C op(Q) = (op(Q)^H C^H)^H
+    Matrix<T> Cx(C.n(), C.m(), A.nb(), C.mb(), gt, rsrc, 0);
+    Cx.insertLocalTiles(target);
+    slate::copy<T, T>(conj_transpose(C), Cx, opts);
+    unmlq_left<T>(opl == Op::NoTrans ? Op::ConjTrans : Op::NoTrans, A, T_[0], Cx, target);
+    slate::copy<T, T>(conj_transpose(Cx), C, opts);
 }
 
 template <typename T>

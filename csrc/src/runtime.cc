@@ -1,7 +1,28 @@
 #include "slate_amd/runtime.hh"
 #include "slate_amd/trace.hh"
 
+#include <mutex>
+
 namespace slate {
+
+namespace {
+std::mutex g_lane_mtx;
+bool g_lane_on = false;
+std::vector<std::pair<std::string, int>> g_lane_log;
+}  // namespace
+
+void Sched::lane_log_enable(bool on) {
+    std::lock_guard<std::mutex> l(g_lane_mtx);
+    g_lane_on = on;
+    g_lane_log.clear();
+}
+
+std::vector<std::pair<std::string, int>> Sched::lane_log_take() {
+    std::lock_guard<std::mutex> l(g_lane_mtx);
+    auto v = std::move(g_lane_log);
+    g_lane_log.clear();
+    return v;
+}
 
 Sched::Sched(Target target) : target_(target) {}
 
@@ -20,8 +41,15 @@ void Sched::task(int queue, std::initializer_list<int64_t> in, std::initializer_
 }
 
 void Sched::task(int queue, std::vector<int64_t> const& in, std::vector<int64_t> const& out, Fn fn) {
+    const bool lane = g_lane_on;
     if (target_ != Target::Devices) {
+        if (lane) trace::task_label_begin();
         fn(ctx(queue));
+        if (lane) {
+            const char* l = trace::task_label_end();
+            std::lock_guard<std::mutex> g(g_lane_mtx);
+            g_lane_log.emplace_back(l ? l : "task", queue);
+        }
         return;
     }
     hipStream_t s = device::queue(queue);
@@ -41,10 +69,21 @@ void Sched::task(int queue, std::vector<int64_t> const& in, std::vector<int64_t>
     if (trace::Trace::is_on() && hipEventCreate(&ta) == hipSuccess) {
         (void)hipEventRecord(ta, s);
         trace::task_label_begin();
+    } else if (lane) {
+        trace::task_label_begin();
     }
     fn(ctx(queue));
+    if (!ta && lane) {
+        const char* l = trace::task_label_end();
+        std::lock_guard<std::mutex> g(g_lane_mtx);
+        g_lane_log.emplace_back(l ? l : "task", queue);
+    }
     if (ta) {
         const char* label = trace::task_label_end();
+        if (lane) {
+            std::lock_guard<std::mutex> g(g_lane_mtx);
+            g_lane_log.emplace_back(label ? label : "task", queue);
+        }
         hipEvent_t tb = nullptr;
         if (hipEventCreate(&tb) == hipSuccess) {
             (void)hipEventRecord(tb, s);

@@ -229,6 +229,7 @@ int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts) {
 // mixed precision iterative refinement
 namespace {
 
+template <typename T> using R_of = real_type<T>;
 
 template <typename T>
 bool iter_ref_converged(std::vector<real_type<T>> const& rnorm, std::vector<real_type<T>> const& xnorm,
@@ -238,9 +239,13 @@ bool iter_ref_converged(std::vector<real_type<T>> const& rnorm, std::vector<real
     return true;
 }
 
-template <typename T, typename Fac, typename Slv, typename FullSolve>
+/// Mixed-precision iterative refinement.  A is the working-precision matrix
+/// as a general view of its storage (for posv_mixed only its stored triangle
+/// is valid); residual(Rm, X) computes Rm = Rm - A X.
+template <typename T, typename Fac, typename Slv, typename FullSolve, typename Resid>
 int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts,
-                     Fac&& factor_lo, Slv&& solve_lo, FullSolve&& full_solve, char const* name) {
+                     Fac&& factor_lo, Slv&& solve_lo, FullSolve&& full_solve, Resid&& residual, R_of<T> Anorm,
+                     char const* name) {
     using Lo = typename lower_prec<T>::type;
     using R = real_type<T>;
     Target target = resolve_target(opts);
@@ -250,9 +255,8 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
     Timer timer;
     iter = 0;
     const int64_t n = A.n(), nrhs = B.n();
-    R Anorm = norm(Norm::Inf, A, opts);
     const R cte = Anorm * eps * std::sqrt(R(n));
-    // low-precision copies
+    // low-precision copies (A_lo is the one n x n temporary, in fp32)
     Matrix<Lo> A_lo(A.m(), A.n(), A.mb(), A.nb(), A.grid());
     A_lo.insertLocalTiles(target);
     Matrix<Lo> X_lo(B.m(), B.n(), B.mb(), B.nb(), B.grid());
@@ -269,12 +273,14 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
         slate::copy<Lo, T>(X_lo, X, opts);
         Matrix<T> Rm = B.emptyLike();
         Rm.insertLocalTiles(target);
+        Matrix<T> D = X.emptyLike();      // correction, allocated once
+        D.insertLocalTiles(target);
         std::vector<R> rnorm(nrhs), xnorm(nrhs);
         timer.reset();
         for (int it = 0; it <= itermax; ++it) {
             // R = B - A X
             slate::copy<T, T>(B, Rm, opts);
-            gemm(T(-1), A, X, T(1), Rm, opts);
+            residual(Rm, X);
             colNorms(Norm::Max, X, xnorm.data(), opts);
             colNorms(Norm::Max, Rm, rnorm.data(), opts);
             if (iter_ref_converged<T>(rnorm, xnorm, cte)) {
@@ -286,8 +292,6 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
             // correction in low precision: X += A_lo^{-1} R
             slate::copy<T, Lo>(Rm, X_lo, opts);
             solve_lo(A_lo, X_lo);
-            Matrix<T> D = X.emptyLike();
-            D.insertLocalTiles(target);
             slate::copy<Lo, T>(X_lo, D, opts);
             add(T(1), D, T(1), X, opts);
         }
@@ -317,7 +321,9 @@ int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int
         return mixed_refine<T>(A, B, X, iter, opts,
             [&](Matrix<Lo>& A_lo) { return getrf(A_lo, piv_lo, opts); },
             [&](Matrix<Lo>& A_lo, Matrix<Lo>& X_lo) { getrs(A_lo, piv_lo, X_lo, opts); },
-            [&](Matrix<T>& Af, Matrix<T>& Xf) { return gesv(Af, pivots, Xf, opts); }, "gesv_mixed");
+            [&](Matrix<T>& Af, Matrix<T>& Xf) { return gesv(Af, pivots, Xf, opts); },
+            [&](Matrix<T>& Rm, Matrix<T>& Xc) { gemm(T(-1), A, Xc, T(1), Rm, opts); },
+            norm(Norm::Inf, A, opts), "gesv_mixed");
     }
     return 0;
 }
@@ -330,22 +336,17 @@ int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter,
     if constexpr (std::is_same_v<Lo, T>) {
         slate_error("posv_mixed requires a double-precision type");
     } else {
+        // the stored triangle only: the residual is a distributed hemm and
+        // the fp32 copy takes the triangle (no dense fp64 n x n temporary)
         Matrix<T> Ag(A);
         Ag.set_uplo(Uplo::General);
-        // the residual needs the full Hermitian matrix: use hemm via a dense copy
         Uplo u = A.uplo();
-        Matrix<T> Afull = Ag.emptyLike();
-        Afull.insertLocalTiles(resolve_target(opts));
-        {
-            // Afull = herm(A)
-            slate::copy<T, T>(conj_transpose(Ag), Afull, opts);
-            BaseTrapezoidMatrix<T> At(u, Ag, MatrixKind::Trapezoid), Ft(u, Afull, MatrixKind::Trapezoid);
-            slate::copy<T, T>(At, Ft, opts);
-        }
-        return mixed_refine<T>(Afull, B, X, iter, opts,
+        return mixed_refine<T>(Ag, B, X, iter, opts,
             [&](Matrix<Lo>& A_lo) { HermitianMatrix<Lo> H(u, A_lo); return potrf(H, opts); },
             [&](Matrix<Lo>& A_lo, Matrix<Lo>& X_lo) { HermitianMatrix<Lo> H(u, A_lo); potrs(H, X_lo, opts); },
-            [&](Matrix<T>&, Matrix<T>& Xf) { return posv(A, Xf, opts); }, "posv_mixed");
+            [&](Matrix<T>&, Matrix<T>& Xf) { return posv(A, Xf, opts); },
+            [&](Matrix<T>& Rm, Matrix<T>& Xc) { hemm(Side::Left, T(-1), A, Xc, T(1), Rm, opts); },
+            norm(Norm::Inf, A, opts), "posv_mixed");
     }
     return 0;
 }

@@ -486,7 +486,7 @@ GridPtr init_grid(int p, int q, GridOrder order, std::string transport) {
     CommPtr tcp = make_tcp_world();
     int myrow = order == GridOrder::Col ? rank % p : rank / q;
     int mycol = order == GridOrder::Col ? rank / p : rank % q;
-    CommPtr world, row, col;
+    CommPtr world, row, col, rowf, colf;
     if (transport == "rccl") {
         std::string uid(128, '\0');
         if (rank == 0) uid = rccl_unique_id();
@@ -495,6 +495,9 @@ GridPtr init_grid(int p, int q, GridOrder order, std::string transport) {
         world = make_rccl_comm(uid, n, rank);
         row = rccl_split(world, myrow, mycol);
         col = rccl_split(world, p + mycol, myrow);
+        // critical-path duplicates (Grid::row_fast / col_fast)
+        rowf = rccl_split(world, myrow, mycol);
+        colf = rccl_split(world, p + mycol, myrow);
     } else {
         slate_error_if_msg(transport != "tcp", "init_grid: transport must be auto, rccl or tcp");
         world = tcp;
@@ -502,6 +505,8 @@ GridPtr init_grid(int p, int q, GridOrder order, std::string transport) {
         col = tcp_split(tcp, p + mycol, myrow);
     }
     auto g = std::make_shared<Grid>(p, q, order, world, row, col);
+    if (rowf && std::getenv("SLATE_FAST_LANE") == nullptr) g->set_fast(rowf, colf);
+    else if (rowf && std::atoi(std::getenv("SLATE_FAST_LANE")) != 0) g->set_fast(rowf, colf);
     set_default_grid(g);
     return g;
 }

@@ -186,6 +186,9 @@ def init_grid(p: int | None = None, q: int | None = None, order=GridOrder.Col, t
         world = _slate.make_rccl_comm(uid[0], n, rank)
         rowc = _slate.rccl_split(world, myrow, mycol)
         colc = _slate.rccl_split(world, p + mycol, myrow)
+        # critical-path duplicates (Grid.set_fast): panel / lookahead messages
+        # on the panel queue, bulk trailing traffic on the comm queue
+        fast = (_slate.rccl_split(world, myrow, mycol), _slate.rccl_split(world, p + mycol, myrow))
     else:
         world = TorchHostComm(list(range(n)), None)
         rowc = colc = None
@@ -202,6 +205,9 @@ def init_grid(p: int | None = None, q: int | None = None, order=GridOrder.Col, t
                 colc = TorchHostComm(ranks, g)
     _KEEP.extend([world, rowc, colc])
     _GRID = _slate.Grid(p, q, order, world, rowc, colc)
+    if transport == "rccl" and os.environ.get("SLATE_FAST_LANE", "1") != "0":
+        _KEEP.extend(fast)
+        _GRID.set_fast(*fast)
     _slate.set_default_grid(_GRID)
     return _GRID
 

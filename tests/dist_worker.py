@@ -390,6 +390,148 @@ def case_getrf_thresh(tg, dt, nb):
         assert np.abs(Lf).max() <= bound * (1 + 1e-5), (thresh, np.abs(Lf).max())
 
 
+def case_pplu_exact(tg, dt, nb):
+    """Partial pivoting on p > 1 is EXACT partial pivoting (one all-gather
+    per panel, the assembled panel factored redundantly): the same pivots as
+    LAPACK getrf (scipy.linalg.lu_factor, |re| + |im| pivot choice)."""
+    import scipy.linalg as sla
+    for (m, n) in ((190, 190), (230, 140)):
+        a = rnd(m, n, dt, 97)
+        A = s.from_numpy(a, nb=nb, target=tg)
+        info, piv = s.getrf(A, target=tg)
+        assert info == 0
+        _, ref = sla.lu_factor(a.astype(np.complex128 if np.iscomplexobj(a) else np.float64))
+        got = ipiv_of(piv, nb)
+        assert list(got) == list(ref[:len(got)]), (m, n)
+
+
+def case_lanes(tg, dt, nb):
+    """Communication lanes (Grid.row_fast / col_fast): critical-path tasks --
+    tournament / panel gather, pivot + LU11 + L broadcasts, lookahead row
+    exchanges, TSQR, (V, T) broadcasts -- are enqueued on the panel queue (1);
+    the trailing chunks' row exchanges / W all-reduces and the left swaps on
+    the comm queue (3).  Also: PPLU issues one collective task per panel."""
+    n = 6 * nb + 7
+    a = rnd(n, n, dt, 131)
+    crit_getrf = {"getrf_tnt_send", "getrf_tnt_recv", "getrf_bcast_winners", "getrf_panel_perm", "getrf_bcast_row",
+                  "getrf_bcast_L", "getrf_pp_panel"}
+    for fn, kw in ((s.getrf_tntpiv, {}), (s.getrf, {})):
+        A = s.from_numpy(a, nb=nb, target=tg)
+        s._slate.lane_log_enable(True)
+        fn(A, target=tg, **kw)
+        log = s._slate.lane_log_take()
+        s._slate.lane_log_enable(False)
+        for label, qu in log:
+            if label in crit_getrf:
+                assert qu == 1, (label, qu)
+            if label == "getrf_left_swap":
+                assert qu == 3, (label, qu)
+        qs = {qu for label, qu in log if label == "getrf_rows_exchange"}
+        assert qs <= {1, 3} and (1 in qs or parallel.current_grid().p == 1), qs
+        if fn is s.getrf and parallel.current_grid().p > 1:
+            # the process column of each panel runs exactly one panel task (one collective)
+            g = parallel.current_grid()
+            mine = sum(1 for k in range((n + nb - 1) // nb) if k % g.q == g.mycol)
+            assert sum(1 for label, _ in log if label == "getrf_pp_panel") == mine
+            assert not any(label == "getrf_pp_column" for label, _ in log)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    s._slate.lane_log_enable(True)
+    s.geqrf(A, target=tg)
+    log = s._slate.lane_log_take()
+    s._slate.lane_log_enable(False)
+    for label, qu in log:
+        if label.startswith("geqrf_tsqr") or label == "geqrf_bcast":
+            assert qu == 1, (label, qu)
+    qs = {qu for label, qu in log if label == "geqrf_update_allreduce"}
+    assert qs <= {1, 3}, qs
+
+
+def case_solve_notemp(tg, dt, nb):
+    """Transposed / few-RHS distributed solves make no n x n temporary:
+    potrs (L then L^H), getrs with Trans / ConjTrans and posv_mixed (whose
+    only n x n temporary is the fp32 factor) -- the transposed sweeps read
+    op(A) from A's own local array on the transposed process grid and only
+    B is redistributed.  Checked with the matrix-storage allocation peak."""
+    n, nrhs = 5 * nb + 3, 3
+    a = rnd(n, n, dt, 141)
+    h = (a @ a.conj().T + n * np.eye(n)).astype(dt)
+    b = rnd(n, nrhs, dt, 142)
+    g = parallel.current_grid()
+    p, q = g.p, g.q
+    s._slate.storage_alloc_reset()
+    s.from_numpy(np.zeros((n, n), dt), nb=nb, target=tg)
+    full = s._slate.storage_alloc_max()          # this rank's local n x n array (padded ld)
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+    assert s.potrf(H, target=tg) == 0
+    B = s.from_numpy(b, nb=nb, target=tg)
+    s._slate.storage_alloc_reset()
+    s.potrs(H, B, target=tg)
+    assert s._slate.storage_alloc_max() < full / 4, (s._slate.storage_alloc_max(), full)
+    assert relerr(h @ s.to_numpy(B), b) < 100 * tol(dt)
+    A = s.from_numpy(a + 0.2 * np.eye(n, dtype=dt), nb=nb, target=tg)
+    info, piv = s.getrf(A, target=tg)
+    assert info == 0
+    ad = a + 0.2 * np.eye(n, dtype=dt)
+    for op, ref in ((s.Op.Trans, ad.T), (s.Op.ConjTrans, ad.conj().T)):
+        B = s.from_numpy(b, nb=nb, target=tg)
+        s._slate.storage_alloc_reset()
+        s.getrs(A, piv, B, target=tg, trans=op)
+        assert s._slate.storage_alloc_max() < full / 4, (op, s._slate.storage_alloc_max(), full)
+        assert relerr(ref @ s.to_numpy(B), b) < 1e3 * tol(dt), op
+    for meth in ("trsmA", "trsmB"):
+        # op(A) = L^T with B already on the transposed grid (no redistribution)
+        L = s.TriangularMatrix(s.Uplo.Lower, s.Diag.NonUnit, s.from_numpy(np.tril(h), nb=nb, target=tg))
+        Bt = s.from_numpy(b, nb=nb, target=tg, grid=g.transposed())
+        s._slate.storage_alloc_reset()
+        s.trsm(s.Side.Left, 1.0, s.transpose(L), Bt, target=tg, method_trsm=meth)
+        assert s._slate.storage_alloc_max() < full / 4, meth
+        assert relerr(np.tril(h).T @ s.to_numpy(Bt), b) < 100 * tol(dt), meth
+    if dt in (np.float64, np.complex128):
+        H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+        B = s.from_numpy(b, nb=nb, target=tg)
+        X = s.from_numpy(np.zeros_like(b), nb=nb, target=tg)
+        s._slate.storage_alloc_reset()
+        s.from_numpy(np.zeros((n, n), np.float32 if dt == np.float64 else np.complex64), nb=nb, target=tg)
+        lo = s._slate.storage_alloc_max()          # the fp32 factor's local array
+        s._slate.storage_alloc_reset()
+        info, it = s.posv_mixed(H, B, X, target=tg)
+        assert info == 0 and it >= 0
+        assert s._slate.storage_alloc_max() <= lo < full, (s._slate.storage_alloc_max(), lo, full)
+        assert relerr(h @ s.to_numpy(X), b) < 100 * tol(dt)
+
+
+def case_gelqf(tg, dt, nb):
+    """Native LQ on row panels (TSQR over the process row when q > 1): L Q = A
+    rebuilt through unmlq (Right), Q^H Q = I through unmlq (Left, both ops),
+    and the minimum-norm gels (m < n).  No transposed copy of A."""
+    for (m, n) in ((120, 230), (150, 150), (170, 100)):
+        a = rnd(m, n, dt, 151 + m)
+        A = s.from_numpy(a, nb=nb, target=tg)
+        T = s.gelqf(A, target=tg)
+        f = s.to_numpy(A)
+        k = min(m, n)
+        Lf = np.zeros((m, n), dt)
+        Lf[:, :k] = np.tril(f[:, :k])
+        C = s.from_numpy(Lf, nb=nb, target=tg)
+        s.unmlq(s.Side.Right, s.Op.NoTrans, A, T, C, target=tg)
+        assert relerr(s.to_numpy(C), a) < 100 * tol(dt), (m, n)
+        c = rnd(n, 4, dt, 152)
+        C = s.from_numpy(c, nb=nb, target=tg)
+        s.unmlq(s.Side.Left, s.Op.ConjTrans, A, T, C, target=tg)
+        assert abs(np.linalg.norm(s.to_numpy(C)) - np.linalg.norm(c)) < 100 * tol(dt) * np.linalg.norm(c)
+        s.unmlq(s.Side.Left, s.Op.NoTrans, A, T, C, target=tg)
+        assert relerr(s.to_numpy(C), c) < 100 * tol(dt), (m, n)
+    m, n = 90, 200
+    a = rnd(m, n, dt, 161)
+    b = rnd(m, 3, dt, 162)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    BX = s.from_numpy(np.vstack([b, np.zeros((n - m, 3), dt)]), nb=nb, target=tg)
+    s.gels(A, BX, target=tg)
+    x = s.to_numpy(BX)
+    ref = np.linalg.lstsq(a, b, rcond=None)[0]
+    assert relerr(x, ref) < 1e3 * tol(dt)
+
+
 def ipiv_of(piv, nb):
     """Reference Pivots (per block column k: (tile index rel. to k, offset)) ->
     LAPACK-style 0-based sequential interchanges."""

@@ -12,7 +12,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 WORKER = os.path.join(HERE, "dist_worker.py")
-CASES = "gemm,herk,rank2k,trsm,trmm,hemm,stationary,rbt,heev,band,band_blas,layout,aasen,potrf,getrf,getrf_shapes,getrf_thresh,geqrf,geqrf_shapes,norm,norm_masked,mixed"
+CASES = "lanes,pplu_exact,solve_notemp,gelqf,gemm,herk,rank2k,trsm,trmm,hemm,stationary,rbt,heev,band,band_blas,layout,aasen,potrf,getrf,getrf_shapes,getrf_thresh,geqrf,geqrf_shapes,norm,norm_masked,mixed"
 
 
 def _free_port():
@@ -78,7 +78,7 @@ def test_dist_lu_qr_deep_trees(p, q):
     """Tournament / TSQR trees with 2 levels and uneven process rows (p = 3, 4):
     distributed CALU / PPLU / no-pivoting LU reconstructed as P A = L U, and
     TSQR + Householder-reconstruction QR checked through unmqr."""
-    run_workers(p, q, "h", cases="getrf_shapes,getrf,getrf_thresh,geqrf_shapes,geqrf", dtypes="float64,complex128")
+    run_workers(p, q, "h", cases="getrf_shapes,getrf,getrf_thresh,pplu_exact,lanes,geqrf_shapes,geqrf", dtypes="float64,complex128")
 
 
 @pytest.mark.gpu
