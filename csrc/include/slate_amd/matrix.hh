@@ -84,6 +84,30 @@ public:
                   std::function<int(int64_t, int64_t)> const& tile_rank, GridPtr grid);
     std::shared_ptr<Layout> layout;
     bool general() const { return layout != nullptr; }
+
+    /// Band-only storage (reference BaseBandMatrix.hh:219-258: only the tiles
+    /// that intersect the band exist).  Tile (i, j) is stored iff
+    /// j - band_ut <= i <= j + band_lt (tile bandwidths).  Within each local
+    /// tile column the stored tiles are a contiguous range of local rows
+    /// [boff, bend); the allocation is lld (= the largest range, padded) x
+    /// nloc, element (lr, lc) at (lr - boff[lc / nb]) + lc * lld.  O(n x
+    /// bandwidth) memory instead of the dense local array.
+    struct BandTag {};
+    MatrixStorage(int64_t m, int64_t n, int64_t nb, GridPtr grid, int64_t kl, int64_t ku, BandTag);
+    bool banded = false;
+    int64_t band_lt = 0, band_ut = 0;
+    std::vector<int64_t> boff, bend;   // per local tile column
+    /// host/device pointer of local element (lr, lc), or null when the tile
+    /// is outside the stored band (banded storage) -- dense storage: always
+    T* local_ptr(Loc loc, int64_t lr, int64_t lc) const {
+        T* base = raw(loc);
+        if (!base) return nullptr;
+        const int64_t ld = this->ld(loc);
+        if (!banded) return base + lr + lc * ld;
+        const int64_t lj = lc / nb;
+        if (lr < boff[lj] || lr >= bend[lj]) return nullptr;
+        return base + (lr - boff[lj]) + lc * ld;
+    }
     ~MatrixStorage();
     MatrixStorage(MatrixStorage const&) = delete;
     MatrixStorage& operator=(MatrixStorage const&) = delete;
@@ -311,6 +335,12 @@ public:
     Matrix(int64_t m, int64_t n, int64_t mb, int64_t nb, GridPtr grid, int rsrc = 0, int csrc = 0)
         : BaseMatrix<T>(std::make_shared<MatrixStorage<T>>(m, n, mb, nb, grid ? grid : default_grid(), rsrc, csrc)) {}
     explicit Matrix(BaseMatrix<T> const& b) : BaseMatrix<T>(b) { this->set_kind(MatrixKind::General); }
+    /// Band-only storage for an m x n matrix of bandwidths kl / ku (see
+    /// MatrixStorage::BandTag); used by the sized band-matrix constructors.
+    static Matrix banded(int64_t m, int64_t n, int64_t kl, int64_t ku, int64_t nb, GridPtr grid) {
+        return Matrix(BaseMatrix<T>(std::make_shared<MatrixStorage<T>>(
+            m, n, nb, grid ? grid : default_grid(), kl, ku, typename MatrixStorage<T>::BandTag{})));
+    }
     /// Arbitrary distribution with non-uniform tiles (reference Matrix.hh:
     /// 207-212): tileMb(i), tileNb(j), tileRank({i, j}) (world rank),
     /// tileDevice (one GPU per process here, accepted for API parity).  The
@@ -412,8 +442,9 @@ public:
         : HermitianMatrix(uplo, Matrix<T>(n, n, nb, g)) {}
 };
 
-/// General band matrix with lower/upper bandwidths kl/ku.  Storage is the
-/// full local array; only tiles intersecting the band are touched by drivers.
+/// General band matrix with lower/upper bandwidths kl/ku.  The sized
+/// constructor allocates band-only storage (tiles intersecting the band); a
+/// band view of an existing dense matrix keeps that matrix's storage.
 template <typename T>
 class BandMatrix : public BaseMatrix<T> {
 public:
@@ -421,8 +452,10 @@ public:
     BandMatrix(int64_t kl, int64_t ku, BaseMatrix<T> const& b) : BaseMatrix<T>(b) {
         this->set_kind(MatrixKind::Band); this->set_band(kl, ku);
     }
+    /// (the upper storage bandwidth is ku + kl: room for gbtrf's fill, as
+    /// LAPACK's 2 kl + ku + 1 band rows)
     BandMatrix(int64_t m, int64_t n, int64_t kl, int64_t ku, int64_t nb, GridPtr g = nullptr)
-        : BandMatrix(kl, ku, Matrix<T>(m, n, nb, g)) {}
+        : BandMatrix(kl, ku, Matrix<T>::banded(m, n, kl, ku + kl, nb, g)) {}
     int64_t lowerBandwidth() const { return this->kl(); }
     int64_t upperBandwidth() const { return this->ku(); }
 };
@@ -435,6 +468,9 @@ public:
         this->set_kind(MatrixKind::TriangularBand); this->set_uplo(uplo); this->set_diag(diag);
         this->set_band(uplo == Uplo::Lower ? kd : 0, uplo == Uplo::Upper ? kd : 0);
     }
+    TriangularBandMatrix(Uplo uplo, Diag diag, int64_t n, int64_t kd, int64_t nb, GridPtr g = nullptr)
+        : TriangularBandMatrix(uplo, diag, kd, Matrix<T>::banded(n, n, uplo == Uplo::Lower ? kd : 0,
+                                                                 uplo == Uplo::Upper ? kd : 0, nb, g)) {}
     int64_t bandwidth() const { return std::max(this->kl(), this->ku()); }
 };
 
@@ -447,7 +483,8 @@ public:
         this->set_band(uplo == Uplo::Lower ? kd : 0, uplo == Uplo::Upper ? kd : 0);
     }
     HermitianBandMatrix(Uplo uplo, int64_t n, int64_t kd, int64_t nb, GridPtr g = nullptr)
-        : HermitianBandMatrix(uplo, kd, Matrix<T>(n, n, nb, g)) {}
+        : HermitianBandMatrix(uplo, kd, Matrix<T>::banded(n, n, uplo == Uplo::Lower ? kd : 0,
+                                                          uplo == Uplo::Upper ? kd : 0, nb, g)) {}
     int64_t bandwidth() const { return std::max(this->kl(), this->ku()); }
 };
 

@@ -299,14 +299,29 @@ void bind_type(py::module_& m, const char* sfx) {
         .def("conj_transpose", [](HermitianMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<BandMatrix<T>, BaseMatrix<T>>(m, ("BandMatrix_" + s).c_str())
         .def(py::init<int64_t, int64_t, BaseMatrix<T> const&>())
+        // band-only storage (reference BandMatrix(m, n, kl, ku, nb, ...) ctor)
+        .def_static("banded", [](int64_t mm, int64_t n, int64_t kl, int64_t ku, int64_t nb, GridPtr g) {
+            return BandMatrix<T>(mm, n, kl, ku, nb, g ? g : default_grid());
+        }, py::arg("m"), py::arg("n"), py::arg("kl"), py::arg("ku"), py::arg("nb"), py::arg("grid") = nullptr)
+        .def_property_readonly("is_band_storage", [](BandMatrix<T> const& A) { return A.storage()->banded; })
+        .def_property_readonly("storage_bytes", [](BandMatrix<T> const& A) {
+            auto& st = *A.storage();
+            return size_t(st.lld) * size_t(std::max<int64_t>(st.nloc, 1)) * sizeof(T);
+        })
         .def("transpose", [](BandMatrix<T> const& A) { return transpose(A); })
         .def("conj_transpose", [](BandMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<TriangularBandMatrix<T>, BaseMatrix<T>>(m, ("TriangularBandMatrix_" + s).c_str())
         .def(py::init<Uplo, Diag, int64_t, BaseMatrix<T> const&>())
+        .def_static("banded", [](Uplo u, Diag d, int64_t n, int64_t kd, int64_t nb, GridPtr g) {
+            return TriangularBandMatrix<T>(u, d, n, kd, nb, g ? g : default_grid());
+        }, py::arg("uplo"), py::arg("diag"), py::arg("n"), py::arg("kd"), py::arg("nb"), py::arg("grid") = nullptr)
         .def("transpose", [](TriangularBandMatrix<T> const& A) { return transpose(A); })
         .def("conj_transpose", [](TriangularBandMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<HermitianBandMatrix<T>, BaseMatrix<T>>(m, ("HermitianBandMatrix_" + s).c_str())
-        .def(py::init<Uplo, int64_t, BaseMatrix<T> const&>());
+        .def(py::init<Uplo, int64_t, BaseMatrix<T> const&>())
+        .def_static("banded", [](Uplo u, int64_t n, int64_t kd, int64_t nb, GridPtr g) {
+            return HermitianBandMatrix<T>(u, n, kd, nb, g ? g : default_grid());
+        }, py::arg("uplo"), py::arg("n"), py::arg("kd"), py::arg("nb"), py::arg("grid") = nullptr);
 
     bind_drivers<T>(m, s);
 }

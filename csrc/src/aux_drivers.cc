@@ -209,10 +209,38 @@ template void redistribute_op<std::complex<double>>(BaseMatrix<std::complex<doub
 using namespace internal;
 
 //------------------------------------------------------------------------------
+/// same process grid, tile sizes and first-tile owner (local elements match)
+template <typename Ts, typename Td>
+bool co_located(BaseMatrix<Ts> const& A, BaseMatrix<Td> const& B) {
+    auto &sa = *A.storage(), &sb = *B.storage();
+    return A.op() == Op::NoTrans && B.op() == Op::NoTrans && A.grid().get() == B.grid().get() && sa.mb == sb.mb &&
+           sa.nb == sb.nb && sa.rsrc == sb.rsrc && sa.csrc == sb.csrc && A.row0() == B.row0() &&
+           A.col0() == B.col0() && A.m() == B.m() && A.n() == B.n();
+}
+
 template <typename Ts, typename Td>
 void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
     trace::Block tb("copy");
     internal::DriverScope ds_;
+    if (A.storage()->banded || B.storage()->banded) {
+        // band-only storage on either side: element copy on the host between
+        // co-located matrices (entries outside a source band are zero,
+        // entries outside a destination band are not stored)
+        slate_error_if_msg(!co_located(A, B), "copy: band-only storage needs co-located operands");
+        auto& sa = *A.storage();
+        auto& g = *sa.grid;
+        sa.get(Loc::Host, false);
+        Uplo mask = is_trapezoid_kind(B.matrix_kind()) ? B.uplo() : Uplo::General;
+        for_each_stored(B, true, [&](int64_t i, int64_t j, Td& v) {
+            if (mask == Uplo::Lower ? i < j : (mask == Uplo::Upper ? i > j : false)) return;
+            const int64_t gr = A.row0() + i, gc = A.col0() + j;
+            Ts const* e = sa.local_ptr(Loc::Host, g2l(gr, sa.mb, g.p()), g2l(gc, sa.nb, g.q()));
+            v = e ? Td(*e) : Td(0);
+        });
+        if (resolve_target(opts) == Target::Devices) B.storage()->get(Loc::Device, false);
+        internal::finish_origin(B, opts);
+        return;
+    }
     Target target = resolve_target(opts);
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
@@ -388,6 +416,14 @@ void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
     trace::Block tb("set");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
+    if (A.storage()->banded) {
+        // band-only storage: the stored band elements (host), then the device
+        slate_error_if_msg(A.op() != Op::NoTrans, "set: band-only storage needs a NoTrans view");
+        for_each_stored(A, true, [&](int64_t i, int64_t j, T& v) { v = (i == j) ? diag : offdiag; });
+        if (target == Target::Devices) A.storage()->get(Loc::Device, false);
+        internal::finish_origin(A, opts);
+        return;
+    }
     Loc loc = loc_of(target);
     lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
     bool trap = is_trapezoid_kind(A.matrix_kind());
@@ -450,6 +486,23 @@ void gather(BaseMatrix<T> const& A, std::vector<T>& full, Options const& opts) {
     int64_t m = A.m(), n = A.n();
     full.assign(size_t(m) * n, T(0));
     auto& s = *A.storage();
+    if (s.banded) {
+        // band-only storage: scatter the stored elements, sum over ranks
+        // (every element has one owner; zeros elsewhere)
+        BaseMatrix<T> As = A.op() == Op::NoTrans ? A : A.transpose_view(A.op() == Op::ConjTrans);
+        const bool tr = A.op() != Op::NoTrans, cj = A.op() == Op::ConjTrans;
+        for_each_stored(As, false, [&](int64_t i, int64_t j, T& v) {
+            if (tr) full[j + i * m] = cj ? slate::conj(v) : v;
+            else full[i + j * m] = v;
+        });
+        Comm& w = A.grid()->world();
+        if (w.size() > 1) {
+            using R = real_type<T>;
+            allreduce_host<R>(w, reinterpret_cast<R*>(full.data()), full.size() * (is_complex_v<T> ? 2 : 1),
+                              ReduceOp::Sum);
+        }
+        return;
+    }
     // host instance of the local data
     T* base = s.get(Loc::Host, false);
     (void)base;
@@ -606,6 +659,67 @@ real_type<T> finish_norm(BaseMatrix<T> const& A, char kind, NormParts<T>& P) {
     return P.scale * std::sqrt(P.sumsq);
 }
 
+/// Norm of a matrix with band-only storage: host pass over the stored
+/// band elements, masked to the logical band / triangle (General, Band,
+/// TriangularBand, HermitianBand kinds), then one world reduction.
+template <typename T>
+real_type<T> norm_band_stored(Norm in_norm, BaseMatrix<T> const& A) {
+    using R = real_type<T>;
+    Norm nrm = in_norm;
+    if (A.op() != Op::NoTrans) nrm = nrm == Norm::One ? Norm::Inf : (nrm == Norm::Inf ? Norm::One : nrm);
+    BaseMatrix<T> As = A.op() == Op::NoTrans ? A : A.transpose_view(A.op() == Op::ConjTrans);
+    const MatrixKind k = A.matrix_kind();
+    const bool herm = (k == MatrixKind::HermitianBand);
+    const bool unit = (k == MatrixKind::TriangularBand && As.diag() == Diag::Unit);
+    int64_t kl = As.kl(), ku = As.ku();
+    if (k == MatrixKind::General) { kl = As.m(); ku = As.n(); }
+    const int64_t m = As.m(), n = As.n();
+    R mx = 0, scale = 0, sumsq = 1;
+    std::vector<R> colsum(nrm == Norm::One || herm ? n : 0, R(0)), rowsum(nrm == Norm::Inf || herm ? m : 0, R(0));
+    bool nan = false;
+    auto add = [&](int64_t i, int64_t j, R a, bool twice) {
+        if (std::isnan(a)) nan = true;
+        mx = std::max(mx, a);
+        if (!colsum.empty()) { colsum[j] += a; if (twice) colsum[i] += a; }
+        if (!rowsum.empty()) { rowsum[i] += a; if (twice) rowsum[j] += a; }
+        if (nrm == Norm::Fro && a != R(0)) {
+            for (int t = 0; t < (twice ? 2 : 1); ++t) {
+                if (scale < a) { sumsq = 1 + sumsq * (scale / a) * (scale / a); scale = a; }
+                else sumsq += (a / scale) * (a / scale);
+            }
+        }
+    };
+    for_each_stored(As, false, [&](int64_t i, int64_t j, T& v) {
+        if (i - j > kl || j - i > ku) return;
+        if (i == j && unit) { add(i, j, R(1), false); return; }
+        R a = (herm && i == j) ? std::abs(std::real(v)) : std::abs(v);
+        add(i, j, a, herm && i != j);
+    });
+    Comm& w = As.grid()->world();
+    if (w.size() > 1) {
+        nan = w.allreduce_scalar<R>(nan ? R(1) : R(0), ReduceOp::Max) > 0;
+        mx = w.allreduce_scalar<R>(mx, ReduceOp::Max);
+        if (!colsum.empty()) allreduce_host(w, colsum.data(), colsum.size(), ReduceOp::Sum);
+        if (!rowsum.empty()) allreduce_host(w, rowsum.data(), rowsum.size(), ReduceOp::Sum);
+        if (nrm == Norm::Fro) {
+            // combine (scale, sumsq) pairs through the world max scale
+            R smax = w.allreduce_scalar<R>(scale, ReduceOp::Max);
+            R part = smax > 0 ? sumsq * (scale / smax) * (scale / smax) : R(0);
+            part = w.allreduce_scalar<R>(part, ReduceOp::Sum);
+            scale = smax; sumsq = part;
+        }
+    }
+    if (nan) return std::numeric_limits<R>::quiet_NaN();
+    switch (nrm) {
+        case Norm::Max: return mx;
+        case Norm::One: return colsum.empty() ? R(0) : *std::max_element(colsum.begin(), colsum.end());
+        case Norm::Inf: return rowsum.empty() ? R(0) : *std::max_element(rowsum.begin(), rowsum.end());
+        case Norm::Fro: return scale * std::sqrt(sumsq);
+        default: slate_not_implemented("two-norm of a band matrix");
+    }
+    return 0;
+}
+
 }  // namespace
 
 template <typename T>
@@ -622,6 +736,7 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
     internal::DriverScope ds_;
     using R = real_type<T>;
     Target target = resolve_target(opts);
+    if (A.storage()->banded) return norm_band_stored(in_norm, A);
     // normalize: work in storage orientation; One<->Inf swap for transposed views
     Norm nrm = in_norm;
     if (A.op() != Op::NoTrans) {

@@ -27,18 +27,7 @@ namespace {
 /// relative to the view; f(i, j, T& value).  Host instance, optionally for write.
 template <typename T, typename F>
 void for_each_local(BaseMatrix<T> const& A, bool write, F&& f) {
-    slate_error_if_msg(A.op() != Op::NoTrans, "band: NoTrans view required");
-    auto& s = *A.storage();
-    s.get(Loc::Host, write);
-    const int64_t ld = s.ld(Loc::Host);
-    LocalBlock<T> la = A.local_raw(Loc::Host);
-    std::vector<int64_t> gr(la.m);
-    for (int64_t il = 0; il < la.m; ++il)
-        gr[il] = l2g(A.lrow_begin() + il, s.mb, s.rrel(), s.grid->p()) - A.row0();
-    for (int64_t jl = 0; jl < la.n; ++jl) {
-        int64_t gc = l2g(A.lcol_begin() + jl, s.nb, s.crel(), s.grid->q()) - A.col0();
-        for (int64_t il = 0; il < la.m; ++il) f(gr[il], gc, la.ptr[il + jl * ld]);
-    }
+    for_each_stored(A, write, std::forward<F>(f));
 }
 
 /// Replicated LAPACK band storage: AB(r0 + i - j, j) = A(i, j) for
@@ -430,9 +419,23 @@ Matrix<T> band_chunk(BaseMatrix<T> const& Ap, int64_t i0, int64_t i1, int64_t k0
     S.set_uplo(Uplo::General);
     Matrix<T> D = S.emptyLike();
     D.insertLocalTiles(Target::Host);
-    Options oh = {{Option::Target, Target::Host}};
-    slate::copy<T, T>(S, D, oh);
     const int64_t ro = row_off(Ap, i0), co = col_off(Ap, k0);
+    if (Ap.storage()->banded) {
+        // band-only storage: D is co-located with the sub-view, so every
+        // local element of D is a local element of Ap (stored or outside)
+        auto& st = *Ap.storage();
+        st.get(Loc::Host, false);
+        auto& g = *st.grid;
+        const int64_t R0 = Ap.row0() + ro, C0 = Ap.col0() + co;
+        for_each_local(D, true, [&](int64_t i, int64_t j, T& v) {
+            const int64_t gr = R0 + i, gc = C0 + j;
+            T* e = st.local_ptr(Loc::Host, g2l(gr, st.mb, g.p()), g2l(gc, st.nb, g.q()));
+            v = e ? *e : T(0);
+        });
+    } else {
+        Options oh = {{Option::Target, Target::Host}};
+        slate::copy<T, T>(S, D, oh);
+    }
     for_each_local(D, true, [&](int64_t i, int64_t j, T& v) {
         const int64_t d = (ro + i) - (co + j);
         if (d < dmin || d > dmax) v = T(0);

@@ -167,6 +167,30 @@ bool needs_bc(BaseMatrix<T> const& A, BaseMatrix<T> const& B) {
     return A.arbitrary_layout() || B.arbitrary_layout();
 }
 
+/// Visit every STORED local element of the NoTrans view A on the host
+/// instance (dense: the whole local block; band-only storage: the stored band
+/// tiles) with its view-relative global (i, j): f(i, j, T& value).
+template <typename T, typename F>
+void for_each_stored(BaseMatrix<T> const& A, bool write, F&& f) {
+    slate_error_if_msg(A.op() != Op::NoTrans, "for_each_stored: NoTrans view required");
+    auto& s = *A.storage();
+    s.get(Loc::Host, write);
+    const int64_t r0 = A.lrow_begin(), r1 = A.lrow_end();
+    const int p = s.grid->p(), q = s.grid->q();
+    for (int64_t lc = A.lcol_begin(); lc < A.lcol_end(); ++lc) {
+        const int64_t gc = l2g(lc, s.nb, s.crel(), q) - A.col0();
+        int64_t a = r0, b = r1;
+        if (s.banded) {
+            const int64_t lj = lc / s.nb;
+            a = std::max(r0, s.boff[lj]);
+            b = std::min(r1, s.bend[lj]);
+        }
+        if (b <= a) continue;
+        T* col = s.local_ptr(Loc::Host, a, lc);
+        for (int64_t lr = a; lr < b; ++lr) f(l2g(lr, s.mb, s.rrel(), p) - A.row0(), gc, col[lr - a]);
+    }
+}
+
 /// Broadcast a contiguous buffer over `comm` from `root` (stream-ordered).
 template <typename T>
 inline void bcast(Comm& comm, T* buf, size_t count, int root, lb::Ctx const& c) {

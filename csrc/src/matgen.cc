@@ -181,6 +181,21 @@ void fill(gen::Spec spec, BaseMatrix<T>& A, Target target, std::vector<double> c
     auto& s = *A.storage();
     auto& g = *s.grid;
     Loc loc = internal::loc_of(target);
+    if (s.banded) {
+        // band-only storage: the stored band elements on the host (the same
+        // grid-independent values as a dense matrix), then the device
+        spec.m = A.m(); spec.n = A.n(); spec.max_mn = std::max(A.m(), A.n());
+        if (sigma) spec.sigma = sigma->data();
+        using R = real_type<T>;
+        internal::for_each_stored(A, true, [&](int64_t gi, int64_t gj, T& v) {
+            double re, im;
+            gen::entry(spec, gi, gj, is_complex_v<T>, re, im);
+            if constexpr (is_complex_v<T>) v = T(R(re), R(im));
+            else v = T(re);
+        });
+        if (target == Target::Devices) s.get(Loc::Device, false);
+        return;
+    }
     LocalBlock<T> lb = A.local(loc, true);
     const int64_t rb = A.lrow_begin(), cb = A.lcol_begin();
     spec.m = A.m(); spec.n = A.n(); spec.max_mn = std::max(A.m(), A.n());

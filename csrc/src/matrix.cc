@@ -78,6 +78,30 @@ MatrixStorage<T>::MatrixStorage(int64_t m_, int64_t n_, std::function<int64_t(in
 }
 
 template <typename T>
+MatrixStorage<T>::MatrixStorage(int64_t m_, int64_t n_, int64_t nb_, GridPtr g, int64_t kl, int64_t ku, BandTag)
+    : MatrixStorage(m_, n_, nb_, nb_, g, 0, 0)
+{
+    slate_error_if_msg(kl < 0 || ku < 0, "band matrix: negative bandwidth");
+    banded = true;
+    band_lt = ceildiv(kl, nb);
+    band_ut = ceildiv(ku, nb);
+    const int64_t mt = ceildiv(m, mb), ntl = ceildiv(nloc, nb);
+    const int p = grid->p(), q = grid->q();
+    boff.assign(ntl, 0);
+    bend.assign(ntl, 0);
+    int64_t h = 0;
+    for (int64_t lj = 0; lj < ntl; ++lj) {
+        const int64_t J = lj * q + crel();
+        const int64_t i_lo = std::max<int64_t>(0, J - band_ut), i_hi = std::min<int64_t>(mt - 1, J + band_lt);
+        if (i_lo > i_hi) { boff[lj] = bend[lj] = 0; continue; }
+        boff[lj] = numroc(i_lo * mb, mb, rrel(), p);
+        bend[lj] = numroc(std::min(m, (i_hi + 1) * mb), mb, rrel(), p);
+        h = std::max(h, bend[lj] - boff[lj]);
+    }
+    lld = pad_ld(h, sizeof(T));
+}
+
+template <typename T>
 MatrixStorage<T>::~MatrixStorage() {
     if (host_owned_ && host_) std::free(host_);
     if (dev_owned_ && dev_) {
@@ -136,8 +160,9 @@ void MatrixStorage<T>::copy_instance(Loc to) {
     int64_t sld = to == Loc::Host ? dev_ld_ : host_ld_;
     int64_t dld = to == Loc::Host ? host_ld_ : dev_ld_;
     if (mloc == 0 || nloc == 0) return;
+    const int64_t rows = banded ? lld : mloc;     // band-only storage: the whole band array
     hipStream_t s = device::queue(0);
-    device::memcpy2d_async(dst, dld * sizeof(T), src, sld * sizeof(T), mloc * sizeof(T), nloc, s);
+    device::memcpy2d_async(dst, dld * sizeof(T), src, sld * sizeof(T), rows * sizeof(T), nloc, s);
     slate_hip_call(hipStreamSynchronize(s));
 }
 
@@ -246,6 +271,8 @@ LocalBlock<T> BaseMatrix<T>::local_raw(Loc loc) const {
     slate_error_if_msg(storage_->general(),
                        "arbitrary-distribution matrix: no block-cyclic local array (copy / redistribute it into a "
                        "block-cyclic Matrix, as the drivers do)");
+    slate_error_if_msg(storage_->banded,
+                       "band-only storage: no dense local array (band drivers read it tile column by tile column)");
     LocalBlock<T> b;
     int64_t rb = lrow_begin(), re = lrow_end(), cb = lcol_begin(), ce = lcol_end();
     b.m = re - rb; b.n = ce - cb;
@@ -283,7 +310,8 @@ Tile<T> BaseMatrix<T>::tile(int64_t i, int64_t j, Loc loc) const {
     int64_t ld = storage_->ld(loc);
     T* base = storage_->raw(loc);
     slate_error_if_msg(!base, "tile: storage not allocated at location");
-    t.data = base + lr + lc * ld;
+    t.data = storage_->banded ? storage_->local_ptr(loc, lr, lc) : base + lr + lc * ld;
+    slate_error_if_msg(!t.data, "tile: outside the stored band");
     t.mb = srow_size(si); t.nb = scol_size(sj); t.stride = ld;
     t.op = op_; t.uplo = uplo_physical();
     t.device = loc == Loc::Host ? HostNum : 0;
@@ -297,8 +325,10 @@ T& BaseMatrix<T>::elem(int64_t i, int64_t j) {
     auto& g = *storage_->grid;
     slate_error_if_msg(storage_->row_owner(gr / storage_->mb) != g.myrow() ||
                        storage_->col_owner(gc / storage_->nb) != g.mycol(), "elem: not local");
-    T* base = storage_->get(Loc::Host, false);
-    return base[g2l(gr, storage_->mb, g.p()) + g2l(gc, storage_->nb, g.q()) * storage_->ld(Loc::Host)];
+    storage_->get(Loc::Host, false);
+    T* e = storage_->local_ptr(Loc::Host, g2l(gr, storage_->mb, g.p()), g2l(gc, storage_->nb, g.q()));
+    slate_error_if_msg(!e, "elem: outside the stored band");
+    return *e;
 }
 
 //------------------------------------------------------------------------------

@@ -386,46 +386,88 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
     Tf.storage()->update_origin();
 }
 
-/// Apply Q (or Q^H) from geqrf to C from the left: C = op(Q) C.
+/// Apply Q (or Q^H) from geqrf to C from the left: C = op(Q) C (reference
+/// src/unmqr.cc, internal_unmqr.cc:161-234), as a stream DAG: per step the
+/// explicit V_k (my panel rows) is packed and broadcast along the process
+/// row on the panel queue (fast lane) one step ahead; C's local columns are
+/// split in up to 4 chunks, each W = V^H C chunk is all-reduced down the
+/// process column on the comm queue while the next chunk's GEMM runs, then
+/// C -= V (op(T) W).  No host synchronization until the end.
 template <typename T>
 void unmqr_left(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Target target) {
     auto& g = *A.grid();
     const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
-    (void)myrow;
     const Loc loc = loc_of(target);
     const int64_t kt = std::min(A.mt(), A.nt());
-    const int64_t m = A.m();
     LocalBlock<T> L = A.local(loc, false);
     LocalBlock<T> LC = C.local(loc, true);
     LocalBlock<T> LT = Tf.local(loc, false);
-    const int64_t nb = A.nb();
-    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
-    Work<T> Vk(target, size_t(std::max<int64_t>(L.m, 1)) * nb), W(target, size_t(nb) * std::max<int64_t>(LC.n, 1)),
-        W2(target, size_t(nb) * std::max<int64_t>(LC.n, 1));
-    Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
-    // Q^H C: k ascending with T^H; Q C: k descending with T
-    for (int64_t t = 0; t < kt; ++t) {
-        int64_t k = (op == Op::NoTrans) ? kt - 1 - t : t;
-        int64_t kb = A.tileNb(k), kk = grow_of(A, k);
-        int pk = A.srow_owner(k), qk = A.scol_owner(k);
-        int64_t lr_k = lrow_of(A, k), mr = L.m - lr_k, ldv = std::max<int64_t>(mr, 1);
-        int64_t lcr = lrow_of(C, k);    // C's local rows >= kk (C conforms to A's rows)
-        if (mycol == qk) {
-            pack(c, mr, kb, L.ptr + lr_k + lcol_of(A, k) * L.ld, L.ld, Vk.data());
-            if (g.myrow() == pk) lb::set(c, Uplo::Upper, std::min<int64_t>(kb, mr), kb, T(0), T(1), Vk.data(), ldv);
-        }
-        if (q > 1) bcast(g.row(), Vk.data(), size_t(mr * kb), qk, c);
-        int64_t nc = LC.n;
-        T* Cc = LC.ptr + lcr;
-        if (mr > 0) lb::gemm(c, cT, Op::NoTrans, kb, nc, mr, T(1), Vk.data(), ldv, Cc, LC.ld, T(0), W.data(), kb);
-        else lb::set(c, Uplo::General, kb, nc, T(0), T(0), W.data(), kb);
-        if (p > 1) g.col().allreduce(W.data(), W.data(), size_t(kb * nc), scalar_type<T>(), ReduceOp::Sum, c.loc(), c.stream);
-        lb::gemm(c, op == Op::NoTrans ? Op::NoTrans : cT, Op::NoTrans, kb, nc, kb, T(1), LT.ptr + kk * LT.ld, LT.ld,
-                 W.data(), kb, T(0), W2.data(), kb);
-        if (mr > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, nc, kb, T(-1), Vk.data(), ldv, W2.data(), kb, T(1), Cc, LC.ld);
-        (void)m;
+    const int64_t nb = A.nb(), ncC = LC.n;
+    const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+    Sched S(target);
+    const int R = 3;
+    std::vector<Work<T>> WV(R), WW(R), WW2(R);
+    for (int r = 0; r < R; ++r) {
+        WV[r].resize(target, size_t(std::max<int64_t>(L.m, 1)) * nb);
+        WW[r].resize(target, size_t(nb) * std::max<int64_t>(ncC, 1));
+        WW2[r].resize(target, size_t(nb) * std::max<int64_t>(ncC, 1));
     }
-    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    // column chunks of C (whole local tiles)
+    std::vector<int64_t> cb{0};
+    {
+        const int64_t nch = std::min<int64_t>(4, std::max<int64_t>(C.nt(), 1));
+        for (int64_t ch = 1; ch <= nch; ++ch) {
+            int64_t j = ch * C.nt() / nch;
+            int64_t lc = j >= C.nt() ? ncC : lcol_of(C, j);
+            if (lc > cb.back()) cb.push_back(lc);
+        }
+        if (cb.back() < ncC) cb.push_back(ncC);
+    }
+    for (int64_t t = 0; t < kt; ++t) {
+        const int64_t k = (op == Op::NoTrans) ? kt - 1 - t : t;   // Q C: k descending with T; Q^H C: ascending, T^H
+        const int64_t kb = A.tileNb(k), kk = grow_of(A, k);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int64_t lr_k = lrow_of(A, k), mr = L.m - lr_k, ldv = std::max<int64_t>(mr, 1);
+        const int64_t lcr = lrow_of(C, k);    // C's local rows >= kk (C conforms to A's rows)
+        const int slot = int(t % R);
+        T* Vk = WV[slot].data();
+        T* W = WW[slot].data();
+        T* W2 = WW2[slot].data();
+        const int64_t tV = Sched::bcast(slot);
+        S.task(1, {}, {tV}, [&, k, kb, mr, ldv, lr_k, pk, qk, Vk](lb::Ctx const& c) {
+            trace::Block t2("unmqr_bcast_v");
+            if (mycol == qk) {
+                pack(c, mr, kb, L.ptr + lr_k + lcol_of(A, k) * L.ld, L.ld, Vk);
+                if (myrow == pk) lb::set(c, Uplo::Upper, std::min<int64_t>(kb, mr), kb, T(0), T(1), Vk, ldv);
+            }
+            if (q > 1) bcast(g.row_fast(), Vk, size_t(mr * kb), qk, c);
+        });
+        T const* Tk = LT.ptr + kk * LT.ld;
+        for (size_t ch = 0; ch + 1 < cb.size(); ++ch) {
+            const int64_t c0 = cb[ch], nc = cb[ch + 1] - c0;
+            T* Cc = LC.ptr + lcr + c0 * LC.ld;
+            const int64_t tc = Sched::col(int64_t(ch));
+            S.task(0, {tV}, {tc}, [&, kb, mr, ldv, nc, Cc, Vk, W, c0](lb::Ctx const& c) {
+                trace::Block t2("unmqr_w");
+                if (mr > 0) lb::gemm(c, cT, Op::NoTrans, kb, nc, mr, T(1), Vk, ldv, Cc, LC.ld, T(0), W + c0 * kb, kb);
+                else lb::set(c, Uplo::General, kb, nc, T(0), T(0), W + c0 * kb, kb);
+            });
+            if (p > 1)
+                S.task(device::kCommQueue, {}, {tc}, [&, kb, nc, W, c0](lb::Ctx const& c) {
+                    trace::Block t2("unmqr_allreduce");
+                    g.col().allreduce(W + c0 * kb, W + c0 * kb, size_t(kb * nc), scalar_type<T>(), ReduceOp::Sum,
+                                      c.loc(), c.stream);
+                });
+            S.task(0, {tV}, {tc}, [&, kb, mr, ldv, nc, Cc, Vk, W, W2, c0, Tk](lb::Ctx const& c) {
+                trace::Block t2("unmqr_c");
+                lb::gemm(c, op == Op::NoTrans ? Op::NoTrans : cT, Op::NoTrans, kb, nc, kb, T(1), Tk, LT.ld,
+                         W + c0 * kb, kb, T(0), W2 + c0 * kb, kb);
+                if (mr > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mr, nc, kb, T(-1), Vk, ldv, W2 + c0 * kb, kb, T(1), Cc,
+                                     LC.ld);
+            });
+        }
+    }
+    S.wait_all();
     C.storage()->update_origin();
 }
 
@@ -683,6 +725,72 @@ void unmlq_left(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Targe
     C.storage()->update_origin();
 }
 
+/// C = C op(Q) with the gelqf factors when C's COLUMNS follow A's columns
+/// (same grid, e.g. the trailing block of ge2tb): C H^(H) = C - (C Y) op(T)^.. Y^H
+/// row-wise, with no transposed copy of C.  Q = H_{kt-1}^H ... H_0^H:
+/// C Q applies k descending with T^H, C Q^H k ascending with T.  Per step:
+/// Y_k down the process columns (fast lane), W = C Y all-reduced across the
+/// process row, C -= (W op(T)) Y^H.
+template <typename T>
+void unmlq_right(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Target target) {
+    auto& g = *A.grid();
+    const int mycol = g.mycol(), myrow = g.myrow();
+    const Loc loc = loc_of(target);
+    const int64_t kt = std::min(A.mt(), A.nt());
+    LocalBlock<T> L = A.local(loc, false);
+    LocalBlock<T> LC = C.local(loc, true);
+    LocalBlock<T> LT = Tf.local(loc, false);
+    const int64_t nb = A.nb(), nloc = L.n, mrC = LC.m, ldw = std::max<int64_t>(mrC, 1);
+    Sched S(target);
+    Work<T> Y(target, size_t(std::max<int64_t>(nloc, 1)) * nb), W(target, size_t(ldw) * nb), W2(target, size_t(ldw) * nb);
+    const int64_t tY = Sched::tok(40, 0), tC = Sched::tok(41, 0);
+    for (int64_t t = 0; t < kt; ++t) {
+        const int64_t k = (op == Op::NoTrans) ? kt - 1 - t : t;
+        const int64_t kb = A.tileMb(k), kk = gcol_of(A, k), kd = std::min(kb, A.n() - kk);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int64_t lc_k = lcol_of(A, k), nc = nloc - lc_k, ldy = std::max<int64_t>(nc, 1);
+        const int64_t lcc = lcol_of(C, k);    // C's local columns >= kk
+        S.task(1, {tC}, {tY}, [&, k, kb, kd, nc, lc_k, ldy, pk, qk](lb::Ctx const& c) {
+            trace::Block t2("unmlq_bcast_y");
+            if (myrow == pk) {
+                lb::copy<T, T>(c, Uplo::General, Op::ConjTrans, nc, kb, L.ptr + lrow_of(A, k) + lc_k * L.ld, L.ld,
+                               Y.data(), ldy);
+                if (mycol == qk) lb::set(c, Uplo::Upper, std::min<int64_t>(kd, nc), kb, T(0), T(1), Y.data(), ldy);
+            }
+            bcast(g.col_fast(), Y.data(), size_t(nc * kb), pk, c);
+        });
+        S.task(0, {tY}, {tC}, [&, kb, kk, nc, ldy, lcc](lb::Ctx const& c) {
+            trace::Block t2("unmlq_update_right");
+            if (mrC <= 0) return;
+            T* Cc = LC.ptr + lcc * LC.ld;
+            if (nc > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mrC, kb, nc, T(1), Cc, LC.ld, Y.data(), ldy, T(0),
+                                 W.data(), ldw);
+            else lb::set(c, Uplo::General, mrC, kb, T(0), T(0), W.data(), ldw);
+            if (g.q() > 1) g.row().allreduce(W.data(), W.data(), size_t(ldw * kb), scalar_type<T>(), ReduceOp::Sum,
+                                             c.loc(), c.stream);
+            lb::gemm(c, Op::NoTrans, op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans, mrC, kb, kb, T(1), W.data(), ldw,
+                     LT.ptr + kk * LT.ld, LT.ld, T(0), W2.data(), ldw);
+            if (nc > 0) lb::gemm(c, Op::NoTrans, Op::ConjTrans, mrC, nc, kb, T(-1), W2.data(), ldw, Y.data(), ldy, T(1),
+                                 Cc, LC.ld);
+        });
+    }
+    S.wait_all();
+    C.storage()->update_origin();
+}
+
+/// Do C's columns follow A's columns (same grid and column tiles)?
+template <typename T>
+bool cols_follow_cols(BaseMatrix<T> const& A, BaseMatrix<T> const& C) {
+    auto& ga = *A.grid();
+    auto& gc = *C.grid();
+    if (C.op() != Op::NoTrans || !C.aligned() || !ga.same_processes(gc)) return false;
+    if (gc.p() != ga.p() || gc.q() != ga.q() || gc.order() != ga.order()) return false;
+    if (C.nt() != A.nt()) return false;
+    for (int64_t j = 0; j < A.nt(); ++j)
+        if (A.tileNb(j) != C.tileNb(j) || A.scol_owner(j) != C.scol_owner(j)) return false;
+    return true;
+}
+
 /// Does C's row distribution follow A's columns (C on A's transposed grid)?
 template <typename T>
 bool rows_follow_cols(BaseMatrix<T> const& A, BaseMatrix<T> const& C) {
@@ -749,6 +857,11 @@ void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
         slate::copy<T, T>(C, Cx, opts);
         unmlq_left<T>(opl, A, T_[0], Cx, target);
         slate::copy<T, T>(Cx, C, opts);
+        return;
+    }
+    if (cols_follow_cols(A, C)) {
+        unmlq_right<T>(opl, A, T_[0], C, target);
+        internal::finish_origin(C, opts);
         return;
     }
     // C op(Q) = (op(Q)^H C^H)^H

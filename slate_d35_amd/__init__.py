@@ -19,7 +19,8 @@ except Exception:  # torch is optional for the native library
 from . import _slate
 from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid, Job,  # noqa: F401
                     Matrix, HermitianMatrix, SymmetricMatrix, TriangularMatrix, TrapezoidMatrix,
-                    BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general,
+                    BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general, band_matrix,
+                    hermitian_band_matrix,
                     from_numpy, to_numpy, matrix_layout, empty_like, local_tensor, transpose, conj_transpose,
                     version, suffix_of, dtype_of, opts, target_of)
 from .parallel import init_grid, choose_grid, TorchHostComm, current_grid, finalize  # noqa: F401

@@ -98,6 +98,21 @@ def BandMatrix(kl, ku, A):
     return _cls("BandMatrix", A)(kl, ku, A)
 
 
+def band_matrix(m, n, kl, ku, nb, dtype=np.float64, grid=None, target=None):
+    """Band matrix with band-only storage (only the tiles that intersect the
+    band plus gbtrf's fill are allocated: O(n * (2 kl + ku)) memory)."""
+    B = getattr(_slate, f"BandMatrix_{_SUFFIX[np.dtype(dtype)]}").banded(m, n, kl, ku, nb, grid)
+    B.insertLocalTiles(target_of(target) if target is not None else Target.Host)
+    return B
+
+
+def hermitian_band_matrix(uplo, n, kd, nb, dtype=np.float64, grid=None, target=None):
+    """Hermitian band matrix with band-only storage."""
+    B = getattr(_slate, f"HermitianBandMatrix_{_SUFFIX[np.dtype(dtype)]}").banded(uplo, n, kd, nb, grid)
+    B.insertLocalTiles(target_of(target) if target is not None else Target.Host)
+    return B
+
+
 def TriangularBandMatrix(uplo, diag, kd, A):
     return _cls("TriangularBandMatrix", A)(uplo, diag, kd, A)
 
