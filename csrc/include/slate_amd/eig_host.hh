@@ -130,5 +130,11 @@ struct RotSink {
 template <typename R>
 int64_t bdsqr_core(int64_t n, R* d, R* e, RotSink<R>* sink);
 
+/// Implicit QL on (d, e) with every rotation sent to `sink` (sweep: the
+/// sweep's rotations in application order, i descending; permute: the final
+/// ascending sort).  Returns the number of unconverged eigenvalues.
+template <typename R>
+int64_t steqr_core(int64_t n, R* d, R* e, RotSink<R>* sink);
+
 }  // namespace host
 }  // namespace slate

@@ -115,6 +115,24 @@ __global__ void scale_kernel(char uplo, int64_t m, int64_t n, real_t<T> mul, T* 
 }
 
 // A = diag(R) A diag(C)  (equilibration); R or C may be null
+// B(i, j) = s[i] * A(i, j) with A real: a real eigenvector matrix into the
+// (complex) working precision with a row phase (heev / svd stage 2)
+template <typename T>
+__global__ void real_rowscale_kernel(int64_t m, int64_t n, const real_t<T>* A, int64_t lda, const T* sc, T* B,
+                                     int64_t ldb) {
+    int64_t i = blockIdx.x * (int64_t)TX + threadIdx.x;
+    if (i >= m) return;
+    const T si = sc ? sc[i] : T(real_t<T>(1));
+    for (int64_t j = blockIdx.y * (int64_t)TY * COLS_PER_THREAD + threadIdx.y; j < n;
+         j += (int64_t)gridDim.y * TY * COLS_PER_THREAD) {
+        #pragma unroll
+        for (int c = 0; c < COLS_PER_THREAD; ++c) {
+            int64_t jj = j + c * TY;
+            if (jj < n) B[i + jj * ldb] = si * T(A[i + jj * lda]);
+        }
+    }
+}
+
 template <typename T>
 __global__ void scale_row_col_kernel(int64_t m, int64_t n, const real_t<T>* R, const real_t<T>* C,
                                      T* A, int64_t lda) {
@@ -450,6 +468,13 @@ void gescale(char uplo, int64_t m, int64_t n, real_t<T> mul, T* A, int64_t lda, 
 }
 
 template <typename T>
+void real_rowscale(int64_t m, int64_t n, const real_t<T>* A, int64_t lda, const T* sc, T* B, int64_t ldb,
+                   hipStream_t s) {
+    if (m <= 0 || n <= 0) return;
+    hipLaunchKernelGGL(real_rowscale_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, m, n, A, lda, sc, B, ldb);
+}
+
+template <typename T>
 void gescale_row_col(int64_t m, int64_t n, const real_t<T>* R, const real_t<T>* C, T* A, int64_t lda, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
     hipLaunchKernelGGL(scale_row_col_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, m, n, R, C, A, lda);
@@ -513,6 +538,7 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void geadd<T>(char, int64_t, int64_t, T, const T*, int64_t, T, T*, int64_t, hipStream_t);   \
     template void gescale<T>(char, int64_t, int64_t, real_t<T>, T*, int64_t, hipStream_t);                \
     template void gescale_row_col<T>(int64_t, int64_t, const real_t<T>*, const real_t<T>*, T*, int64_t, hipStream_t); \
+    template void real_rowscale<T>(int64_t, int64_t, const real_t<T>*, int64_t, const T*, T*, int64_t, hipStream_t); \
     template void trtri_diag<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t);   \
     template void trtri_diag_stack<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t); \
     template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \

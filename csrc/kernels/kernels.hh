@@ -86,6 +86,29 @@ void pplu_apply(int np, const T* gbuf, int64_t kb, int64_t j, int64_t cend, int6
                 int64_t lda, RowDist d, int64_t lr_k, int64_t kk, int pk, double thresh, bool is_pk, int64_t* pip,
                 int* info, int64_t info_off, hipStream_t s);
 
+// ---- distributed divide and conquer (stedc.hip)
+/// secular roots of D + rho z z^T (dd ascending, k of them): lambda_j = dd[org[j]] + tau[j]
+void secular_roots(int64_t k, double rho, const double* dd, const double* zz, double znorm2, int64_t* org,
+                   double* tau, hipStream_t s);
+/// Gu-Eisenstat z from the computed roots
+void gu_eisenstat(int64_t k, double rho, const double* dd, const double* zz, const int64_t* org, const double* tau,
+                  double* zh, hipStream_t s);
+/// one merge's device vectors and the local layout of the n2 x n2 block (see stedc.hip)
+struct StedcMerge {
+    int64_t n2 = 0, k = 0, nrot = 0;
+    const double *dd = nullptr, *zh = nullptr, *tau = nullptr;
+    const int64_t *org = nullptr, *act = nullptr, *defl = nullptr, *ord = nullptr, *inv_perm = nullptr;
+    const int64_t* rot_ab = nullptr;
+    const double* rot_cs = nullptr;
+    int64_t lrows = 0, mb = 1, p = 1, rrel = 0, row_off = 0;
+    int64_t nb = 1, q = 1, crel = 0, col_off = 0;
+    int64_t lr0 = 0, lc0 = 0;
+};
+/// local columns [c_first, c_first + ncols) of the merge matrix into M (ld ldm); scratch: ncols * n2 reals
+template <typename T>
+void merge_matrix(StedcMerge const& m, int64_t c_first, int64_t ncols, T* M, int64_t ldm, double* scratch,
+                  hipStream_t s);
+
 // ---- eigensolver back-transform (eig.hip)
 /// G (k x k Gram V^H V) -> T^{-1} = striu(G) + diag(1 / tau) in place.
 template <typename T>
@@ -176,6 +199,9 @@ template <typename T>
 void gescale(char uplo, int64_t m, int64_t n, rt<T> mul, T* A, int64_t lda, hipStream_t s);
 template <typename T>
 void gescale_row_col(int64_t m, int64_t n, const rt<T>* R, const rt<T>* C, T* A, int64_t lda, hipStream_t s);
+/// B(i, j) = sc[i] * A(i, j), A real (sc null: 1)
+template <typename T>
+void real_rowscale(int64_t m, int64_t n, const rt<T>* A, int64_t lda, const T* sc, T* B, int64_t ldb, hipStream_t s);
 template <typename T>
 void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t ldw, hipStream_t s);
 /// trtri_diag into a stack of bs x bs blocks (block t at W + t bs^2, ld bs); bs % nbs == 0

@@ -1,0 +1,171 @@
+// Device side of the distributed divide-and-conquer tridiagonal eigensolver
+// (eig_dist.cc; reference src/stedc_secular.cc, stedc_merge.cc, and LAPACK
+// laed3 / laed4 semantics).
+//
+// One merge of two halves (n2 = n1 + (n2 - n1) columns of Q) on the rank-one
+// modified system D + rho z z^T after sorting and deflation (host, O(n2)):
+//   * secular_roots: one thread per non-deflated root j, bisection to full
+//     relative precision of tau_j = lambda_j - dd[org_j] (distance to the
+//     nearest pole), which the Gu-Eisenstat vectors need;
+//   * gu_eisenstat_z: z recomputed from the computed roots, one thread per i;
+//   * merge_matrix: every rank builds ONLY its local entries of the n2 x n2
+//     merge matrix M (Q_new = Q_old M): per output column one workgroup forms
+//     the column in the sorted basis (normalized Gu-Eisenstat eigenvector of
+//     the secular system, or a unit vector for a deflated column), applies the
+//     deflation Givens rotations in reverse order, and scatters its local rows
+//     through the sort permutation.  The product itself is the distributed
+//     MFMA GEMM; no n x n matrix exists on any host.
+#include "device_common.hh"
+#include "kernels.hh"
+
+namespace slate_amd {
+namespace dev {
+
+namespace {
+
+__device__ inline double secular_f(int64_t k, double rho, const double* dd, const double* zz, int64_t o2, double t) {
+    double sum = 0;
+    const double d0 = dd[o2];
+    for (int64_t i = 0; i < k; ++i) sum += zz[i] * zz[i] / ((dd[i] - d0) - t);
+    return 1.0 + rho * sum;
+}
+
+__global__ __launch_bounds__(64) void secular_roots_kernel(int64_t k, double rho, const double* dd, const double* zz,
+                                                           double znorm2, int64_t* org, double* tau) {
+    const int64_t j = blockIdx.x * 64 + threadIdx.x;
+    if (j >= k) return;
+    const double eps = 2.220446049250313e-16;
+    const double lo_abs = dd[j];
+    const double hi_abs = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2;
+    const double mid = (hi_abs - lo_abs) / 2;
+    int64_t o2 = j;
+    double a = 0, b = mid;
+    if (j + 1 < k && secular_f(k, rho, dd, zz, j, mid) < 0) { o2 = j + 1; a = -mid; b = 0; }
+    else if (j + 1 >= k) { a = 0; b = hi_abs - lo_abs; }
+    for (int it = 0; it < 400; ++it) {
+        const double t = (a + b) / 2;
+        if (t == a || t == b) break;
+        const double fv = secular_f(k, rho, dd, zz, o2, t);
+        if (fv > 0) b = t; else a = t;
+        if (fabs(b - a) <= 2 * eps * fmin(fabs(a), fabs(b))) break;
+    }
+    org[j] = o2;
+    tau[j] = (a + b) / 2;
+}
+
+__global__ __launch_bounds__(64) void gu_eisenstat_kernel(int64_t k, double rho, const double* dd, const double* zz,
+                                                          const int64_t* org, const double* tau, double* zh) {
+    const int64_t i = blockIdx.x * 64 + threadIdx.x;
+    if (i >= k) return;
+    auto lmd = [&](int64_t j) { return (dd[org[j]] - dd[i]) + tau[j]; };
+    double pr = lmd(k - 1) / rho;
+    for (int64_t j = 0; j < k - 1; ++j) {
+        const double den = (j < i) ? (dd[j] - dd[i]) : (dd[j + 1] - dd[i]);
+        pr *= lmd(j) / den;
+    }
+    zh[i] = copysign(sqrt(fabs(pr)), zz[i]);
+}
+
+// Merge matrix, local part.  Block-cyclic local rows / columns of the n2 x n2
+// block (view-relative global index = l2g(local) - off).  Output column jo
+// holds result column r = ord[jo]: r < k the secular eigenvector, else the
+// deflated sorted column defl[r - k].  Sorted basis -> rows: row src takes
+// vec[inv_perm[src]].  vec is per-workgroup global scratch (n2 reals).
+struct MergeArgs {
+    int64_t n2, k, nrot;
+    const double *dd, *zh, *tau;
+    const int64_t *org, *act, *defl, *ord, *inv_perm;
+    const int64_t* rot_ab;          // nrot pairs (a, b) in application order
+    const double* rot_cs;           // nrot pairs (c, s)
+    // local layout of the block
+    int64_t lrows, mb, p, rrel, row_off;     // row: global = ((l / mb) * p + rrel) * mb + l % mb - row_off
+    int64_t nb, q, crel, col_off;             // col: same for local column index lc0 + blockIdx
+    int64_t lr0, lc0;                         // first local row / col of the block
+};
+
+__device__ inline int64_t bc_l2g(int64_t l, int64_t b, int64_t procs, int64_t rel) {
+    return ((l / b) * procs + rel) * b + l % b;
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void merge_matrix_kernel(MergeArgs a, int64_t c_first, T* M, int64_t ldm,
+                                                           double* scratch) {
+    const int64_t lcb = c_first + blockIdx.x;                     // local column within the block
+    const int64_t jo = bc_l2g(a.lc0 + lcb, a.nb, a.q, a.crel) - a.col_off;
+    double* vec = scratch + blockIdx.x * a.n2;
+    __shared__ double red[256];
+    for (int64_t s = threadIdx.x; s < a.n2; s += 256) vec[s] = 0.0;
+    __syncthreads();
+    const int64_t r = a.ord[jo];
+    if (r < a.k) {
+        const double dr = a.dd[a.org[r]], tr = a.tau[r];
+        double part = 0;
+        for (int64_t i = threadIdx.x; i < a.k; i += 256) {
+            const double u = a.zh[i] / ((a.dd[i] - dr) - tr);
+            vec[a.act[i]] = u;
+            part += u * u;
+        }
+        red[threadIdx.x] = part;
+        __syncthreads();
+        for (int w = 128; w > 0; w >>= 1) {
+            if (threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+            __syncthreads();
+        }
+        const double inv = 1.0 / sqrt(red[0]);
+        for (int64_t i = threadIdx.x; i < a.k; i += 256) vec[a.act[i]] *= inv;
+    } else if (threadIdx.x == 0) {
+        vec[a.defl[r - a.k]] = 1.0;
+    }
+    __syncthreads();
+    // G w with G = G_1 ... G_t: the last rotation acts first
+    if (threadIdx.x == 0) {
+        for (int64_t t = a.nrot - 1; t >= 0; --t) {
+            const int64_t x = a.rot_ab[2 * t], y = a.rot_ab[2 * t + 1];
+            const double c = a.rot_cs[2 * t], sn = a.rot_cs[2 * t + 1];
+            const double vx = vec[x], vy = vec[y];
+            vec[x] = c * vx - sn * vy;
+            vec[y] = sn * vx + c * vy;
+        }
+    }
+    __syncthreads();
+    for (int64_t lr = threadIdx.x; lr < a.lrows; lr += 256) {
+        const int64_t src = bc_l2g(a.lr0 + lr, a.mb, a.p, a.rrel) - a.row_off;
+        M[lr + lcb * ldm] = T(vec[a.inv_perm[src]]);
+    }
+}
+
+}  // namespace
+
+void secular_roots(int64_t k, double rho, const double* dd, const double* zz, double znorm2, int64_t* org, double* tau,
+                   hipStream_t s) {
+    if (k <= 0) return;
+    hipLaunchKernelGGL(secular_roots_kernel, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, k, rho, dd, zz, znorm2,
+                       org, tau);
+}
+
+void gu_eisenstat(int64_t k, double rho, const double* dd, const double* zz, const int64_t* org, const double* tau,
+                  double* zh, hipStream_t s) {
+    if (k <= 0) return;
+    hipLaunchKernelGGL(gu_eisenstat_kernel, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, k, rho, dd, zz, org,
+                       tau, zh);
+}
+
+template <typename T>
+void merge_matrix(StedcMerge const& m, int64_t c_first, int64_t ncols, T* M, int64_t ldm, double* scratch,
+                  hipStream_t s) {
+    if (ncols <= 0) return;
+    MergeArgs a;
+    a.n2 = m.n2; a.k = m.k; a.nrot = m.nrot;
+    a.dd = m.dd; a.zh = m.zh; a.tau = m.tau;
+    a.org = m.org; a.act = m.act; a.defl = m.defl; a.ord = m.ord; a.inv_perm = m.inv_perm;
+    a.rot_ab = m.rot_ab; a.rot_cs = m.rot_cs;
+    a.lrows = m.lrows; a.mb = m.mb; a.p = m.p; a.rrel = m.rrel; a.row_off = m.row_off;
+    a.nb = m.nb; a.q = m.q; a.crel = m.crel; a.col_off = m.col_off;
+    a.lr0 = m.lr0; a.lc0 = m.lc0;
+    hipLaunchKernelGGL(merge_matrix_kernel<T>, dim3((unsigned)ncols), dim3(256), 0, s, a, c_first, M, ldm, scratch);
+}
+template void merge_matrix<double>(StedcMerge const&, int64_t, int64_t, double*, int64_t, double*, hipStream_t);
+template void merge_matrix<float>(StedcMerge const&, int64_t, int64_t, float*, int64_t, double*, hipStream_t);
+
+}  // namespace dev
+}  // namespace slate_amd

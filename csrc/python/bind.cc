@@ -174,6 +174,11 @@ void bind_type(py::module_& m, const char* sfx) {
     using R = real_type<T>;
     std::string s(sfx);
     auto BM = py::class_<BaseMatrix<T>>(m, ("BaseMatrix_" + s).c_str())
+        .def_property_readonly("is_band_storage", [](BaseMatrix<T> const& A) { return A.storage()->banded; })
+        .def_property_readonly("storage_bytes", [](BaseMatrix<T> const& A) {
+            auto& st = *A.storage();
+            return size_t(st.lld) * size_t(std::max<int64_t>(st.nloc, 1)) * sizeof(T);
+        })
         .def_property_readonly("m", &BaseMatrix<T>::m)
         .def_property_readonly("n", &BaseMatrix<T>::n)
         .def_property_readonly("mt", &BaseMatrix<T>::mt)
@@ -303,11 +308,6 @@ void bind_type(py::module_& m, const char* sfx) {
         .def_static("banded", [](int64_t mm, int64_t n, int64_t kl, int64_t ku, int64_t nb, GridPtr g) {
             return BandMatrix<T>(mm, n, kl, ku, nb, g ? g : default_grid());
         }, py::arg("m"), py::arg("n"), py::arg("kl"), py::arg("ku"), py::arg("nb"), py::arg("grid") = nullptr)
-        .def_property_readonly("is_band_storage", [](BandMatrix<T> const& A) { return A.storage()->banded; })
-        .def_property_readonly("storage_bytes", [](BandMatrix<T> const& A) {
-            auto& st = *A.storage();
-            return size_t(st.lld) * size_t(std::max<int64_t>(st.nloc, 1)) * sizeof(T);
-        })
         .def("transpose", [](BandMatrix<T> const& A) { return transpose(A); })
         .def("conj_transpose", [](BandMatrix<T> const& A) { return conj_transpose(A); });
     py::class_<TriangularBandMatrix<T>, BaseMatrix<T>>(m, ("TriangularBandMatrix_" + s).c_str())

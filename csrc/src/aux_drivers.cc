@@ -439,10 +439,9 @@ void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
         if (u == Uplo::General) {
             // whole tile, then the diagonal run r - c == cj - ri (if any) through a sub-block
             const int64_t k = cj - ri, r = std::max<int64_t>(k, 0), cc = std::max<int64_t>(-k, 0);
-            bool has_diag = r < t.mb && cc < t.nb;
-            if (!has_diag || !(diag == offdiag))
-                lb::set(c, Uplo::General, t.mb, t.nb, offdiag, offdiag, t.data, t.stride);
-            if (has_diag)
+            const bool has_diag = r < t.mb && cc < t.nb;
+            lb::set(c, Uplo::General, t.mb, t.nb, offdiag, offdiag, t.data, t.stride);
+            if (has_diag && !(diag == offdiag))
                 lb::set(c, Uplo::General, t.mb - r, t.nb - cc, offdiag, diag, t.data + r + cc * t.stride, t.stride);
             return;
         }

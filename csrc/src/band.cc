@@ -30,43 +30,6 @@ void for_each_local(BaseMatrix<T> const& A, bool write, F&& f) {
     for_each_stored(A, write, std::forward<F>(f));
 }
 
-/// Replicated LAPACK band storage: AB(r0 + i - j, j) = A(i, j) for
-/// -ku <= i - j <= kl; ldab >= r0 + kl + 1.  conj_upper: read A's upper
-/// band (i < j) as the conj-transposed lower band (Hermitian band, Upper).
-template <typename T>
-std::vector<T> gather_band(BaseMatrix<T> const& A, int64_t kl, int64_t ku, int64_t r0, int64_t ldab,
-                           bool upper_as_lower = false) {
-    const int64_t n = A.n();
-    std::vector<T> ab(size_t(ldab) * n, T(0));
-    for_each_local(A, false, [&](int64_t i, int64_t j, T& v) {
-        if (upper_as_lower) {
-            if (j >= i && j - i <= ku) ab[(r0 + j - i) + i * ldab] = slate::conj(v);   // (j, i) of the lower band
-        } else if (i - j <= kl && j - i <= ku) {
-            ab[(r0 + i - j) + j * ldab] = v;
-        }
-    });
-    // every band entry is owned by exactly one rank
-    Comm& w = A.grid()->world();
-    if (w.size() > 1) {
-        using R = real_type<T>;
-        size_t mult = is_complex_v<T> ? 2 : 1;
-        allreduce_host<R>(w, reinterpret_cast<R*>(ab.data()), ab.size() * mult, ReduceOp::Sum);
-    }
-    return ab;
-}
-
-template <typename T>
-void scatter_band(BaseMatrix<T>& A, std::vector<T> const& ab, int64_t kl, int64_t ku, int64_t r0, int64_t ldab,
-                  bool upper_as_lower = false) {
-    for_each_local(A, true, [&](int64_t i, int64_t j, T& v) {
-        if (upper_as_lower) {
-            if (j >= i && j - i <= ku) v = slate::conj(ab[(r0 + j - i) + i * ldab]);
-        } else if (i - j <= kl && j - i <= ku) {
-            v = ab[(r0 + i - j) + j * ldab];
-        }
-    });
-}
-
 //------------------------------------------------------------------------------
 // host band kernels (LAPACK gbtf2 / gbtrs / pbtf2 / pbtrs semantics)
 template <typename T>
@@ -546,7 +509,7 @@ int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts) {
     slate_error_if_msg(A.m() != n, "gbtrf: square band matrix required");
     const int64_t ldab = 2 * kl + ku + 1, kv = kl + ku;
     // AB(kv + i - j, j) = A(i, j); rows [0, kl) receive the fill
-    std::vector<T> ab = gather_band<T>(A, kl, ku, kv, ldab);
+    std::vector<T> ab = band_gather<T>(A, kl, ku, kv, ldab);
     Target target = resolve_target(opts);
     Comm& w = A.grid()->world();
     const int64_t nb = std::max<int64_t>(1, A.nb());
@@ -556,7 +519,7 @@ int64_t gbtrf(BandMatrix<T>& A, Pivots& pivots, Options const& opts) {
     int64_t info = gbtrf_slabs<T>(sl, kl, ku, w, ipiv);
     sl.store(ab, kv, ldab, kl, kv, w);
     // factors: L (kl below) and U (kl + ku above); the matrix's storage holds the fill
-    scatter_band<T>(A, ab, kl, kv, kv, ldab);
+    band_scatter<T>(A, ab, kl, kv, kv, ldab);
     A.set_band(kl, kl + ku);
     pivots_from_ipiv(A, ipiv, pivots);
     if (target == Target::Devices) A.storage()->get(Loc::Device, false);
@@ -577,24 +540,33 @@ void gbtrs(BandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options c
         // formed on the host from the O(n * kl) L band and applied to those
         // rows of B by one distributed GEMM per block column (reference
         // src/gbtrs.cc: tbsm with pivots).
-        std::vector<T> abl = gather_band<T>(A, kl, 0, 0, kl + 1);   // abl(i - j, j) = L(i, j)
+        std::vector<T> abl = band_gather<T>(A, kl, 0, 0, kl + 1);   // abl(i - j, j) = L(i, j)
         std::vector<int64_t> ipiv = ipiv_from_pivots(A, pivots);
         const int64_t nt = A.nt();
         for (int64_t k = 0; k < nt; ++k) {
             const int64_t j0 = col_off<T>(A, k), j1 = j0 + A.tileNb(k);
             const int64_t kr = tile_row_of<T>(A, std::min(n, j1 + kl) - 1);
             const int64_t R0 = row_off<T>(A, k), Rn = row_off<T>(A, kr) + A.tileMb(kr) - R0;
+            // M = (swap, eliminate)_j1-1 ... (swap, eliminate)_j0 applied to
+            // the identity, one column at a time (columns are independent;
+            // contiguous axpys, skipped where the pivot row entry is zero).
+            // Rows at or past Ct are never touched, so those columns stay e_c.
+            const int64_t Ct = std::min(Rn, j1 - R0 + kl);
             std::vector<T> M(size_t(Rn) * Rn, T(0));
-            for (int64_t i = 0; i < Rn; ++i) M[i + i * Rn] = T(1);
-            for (int64_t j = j0; j < j1; ++j) {
-                const int64_t lj = j - R0, lp = ipiv[j] - R0;
-                if (lp != lj)
-                    for (int64_t c = 0; c < Rn; ++c) std::swap(M[lj + c * Rn], M[lp + c * Rn]);
-                const int64_t km = std::min(kl, n - 1 - j);
-                for (int64_t i = 1; i <= km; ++i) {
-                    const T l = abl[i + j * (kl + 1)];
-                    if (l == T(0)) continue;
-                    for (int64_t c = 0; c < Rn; ++c) M[lj + i + c * Rn] -= l * M[lj + c * Rn];
+            #pragma omp parallel for schedule(dynamic, 16)
+            for (int64_t c = 0; c < Rn; ++c) {
+                T* col = M.data() + c * Rn;
+                col[c] = T(1);
+                if (c >= Ct) continue;
+                for (int64_t j = j0; j < j1; ++j) {
+                    const int64_t lj = j - R0, lp = ipiv[j] - R0;
+                    if (lp != lj) std::swap(col[lj], col[lp]);
+                    const T b = col[lj];
+                    if (b == T(0)) continue;
+                    const int64_t km = std::min(kl, n - 1 - j);
+                    T const* l = abl.data() + 1 + j * (kl + 1);
+                    T* y = col + lj + 1;
+                    for (int64_t i = 0; i < km; ++i) y[i] -= l[i] * b;
                 }
             }
             Matrix<T> Ms(BaseMatrix<T>(A).sub(k, kr, k, kr));
@@ -629,15 +601,15 @@ int64_t pbtrf(HermitianBandMatrix<T>& A, Options const& opts) {
     const int64_t n = A.n(), kd = A.bandwidth();
     const bool upper = A.uplo() == Uplo::Upper;
     // lower band storage ab(i - j, j) = L(i, j); an Upper matrix is read as U^H
-    std::vector<T> ab = upper ? gather_band<T>(A, 0, kd, 0, kd + 1, true) : gather_band<T>(A, kd, 0, 0, kd + 1);
+    std::vector<T> ab = upper ? band_gather<T>(A, 0, kd, 0, kd + 1, true) : band_gather<T>(A, kd, 0, 0, kd + 1);
     Target target = resolve_target(opts);
     Comm& w = A.grid()->world();
     BandSlabs<T> sl(n, std::max<int64_t>(1, A.nb()), 0, kd, w, target);
     sl.load(ab, 0, kd + 1, kd, 0);
     int64_t info = pbtrf_slabs<T>(sl, kd, w);
     sl.store(ab, 0, kd + 1, kd, 0, w);
-    if (upper) scatter_band<T>(A, ab, 0, kd, 0, kd + 1, true);
-    else scatter_band<T>(A, ab, kd, 0, 0, kd + 1);
+    if (upper) band_scatter<T>(A, ab, 0, kd, 0, kd + 1, true);
+    else band_scatter<T>(A, ab, kd, 0, 0, kd + 1);
     if (resolve_target(opts) == Target::Devices) A.storage()->get(Loc::Device, false);
     return info;
 }

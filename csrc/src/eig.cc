@@ -6,12 +6,17 @@
 // ge2tb reduce to band form with one geqrf (and gelqf) per block column and
 // two-sided block updates through unmqr / unmlq, so every flop-heavy piece is
 // the same device-resident QR machinery as the geqrf headline.
-// Stage 2 (host, every rank redundantly, deterministic): the band (O(n nb)
-// data) is gathered, chased to tridiagonal / bidiagonal (eig_host.cc), and
-// solved by divide and conquer (stedc), QR iteration (steqr/sterf) or
-// Golub-Reinsch (bdsqr).  The stage-2 reflectors are applied on the host, then
-// the stage-1 back-transform runs distributed (unmqr / unmlq on Z, U, VT).
+// Stage 2: the band (O(n nb) data) is gathered to every rank and chased to
+// tridiagonal / bidiagonal on the host (eig_host.cc, deterministic); the
+// tridiagonal eigenvectors come from the distributed divide and conquer (Q on
+// the 2-D grid, merges as MFMA GEMMs) or the QL iteration with the rotations
+// applied to each rank's rows (eig_dist.cc); bdsqr's rotations likewise act on
+// each rank's rows of U / Vt (eig_sinks.hh).  The stage-2 reflectors are
+// applied blocked to each rank's columns (unmtr_hb2st_blocked), then the
+// stage-1 back-transform runs distributed (unmqr / unmlq on Z, U, VT).  No
+// rank holds an n x n array on the host.
 #include "internal.hh"
+#include "eig_sinks.hh"
 #include "slate_amd/eig_host.hh"
 #include "../kernels/kernels.hh"
 
@@ -206,33 +211,11 @@ void unmtr_hb2st_blocked(host::Reflectors<T> const& Q, int64_t n, int64_t kd, T*
     });
     const int64_t vr = GS + kd, VB = vr * GS;
     const size_t ng = keys.size();
-    std::vector<T> hV(ng * VB, T(0)), ht(ng * GS, T(0));
-    std::vector<int64_t> r0s(ng), ws(ng);
-    #pragma omp parallel for schedule(dynamic)
-    for (size_t gi = 0; gi < ng; ++gi) {
-        const int64_t J = keys[gi].first, t = keys[gi].second, r0 = J * GS + t * kd + 1;
-        r0s[gi] = r0;
-        int64_t w = 0;
-        for (size_t r : groups.at(keys[gi])) {
-            const int64_t i = Q.tag[r] - J * GS;
-            slate_assert(Q.off[r] - r0 == i && i + Q.len[r] <= vr);
-            T const* v = Q.v.data() + Q.voff[r];
-            for (int64_t ii = 0; ii < Q.len[r]; ++ii) hV[gi * VB + (i + ii) + i * vr] = v[ii];
-            ht[gi * GS + i] = Q.tau[r];
-            w = std::max(w, i + 1);
-        }
-        ws[gi] = w;
-    }
+    // blocks are staged in batches of at most kBatch groups (pinned host,
+    // double-buffered device copies): bounded host memory instead of the
+    // whole blocked Q2
+    const size_t kBatch = 64;
     const Target tg = c.dev() ? Target::Devices : Target::HostTask;
-    Work<T> dV, dt;
-    if (c.dev()) {
-        dV.resize(tg, hV.size());
-        dt.resize(tg, ht.size());
-        device::memcpy_async(dV.data(), hV.data(), hV.size() * sizeof(T), c.stream);
-        device::memcpy_async(dt.data(), ht.data(), ht.size() * sizeof(T), c.stream);
-    }
-    T const* Vall = c.dev() ? dV.data() : hV.data();
-    T const* tall = c.dev() ? dt.data() : ht.data();
     Work<T> G(tg, size_t(GS) * GS), W(tg, size_t(GS) * ncols);
     auto tinv = [&](int64_t w, T* Gm, T const* tau) {
         if (c.dev()) { kd_::tinv_from_gram(w, kd_::dptr(Gm), GS, kd_::dptr(tau), c.stream); return; }
@@ -243,218 +226,95 @@ void unmtr_hb2st_blocked(host::Reflectors<T> const& Q, int64_t n, int64_t kd, T*
                 else if (i == j) x = tau[i] == T(0) ? T(1) : T(1) / tau[i];
             }
     };
-    for (size_t gi = 0; gi < ng; ++gi) {
-        const int64_t r0 = r0s[gi], w = ws[gi];                 // w: columns in use
-        const int64_t rows = std::min(w - 1 + kd, n - r0);
-        if (rows <= 0 || w <= 0) continue;
-        T const* V = Vall + gi * VB;
-        T* Zr = Z + r0;
-        lb::gemm(c, Op::ConjTrans, Op::NoTrans, w, w, rows, T(1), V, vr, V, vr, T(0), G.data(), GS);
-        tinv(w, G.data(), tall + gi * GS);
-        lb::gemm(c, Op::ConjTrans, Op::NoTrans, w, ncols, rows, T(1), V, vr, Zr, ldz, T(0), W.data(), GS);
-        lb::trsm(c, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, w, ncols, T(1), G.data(), GS, W.data(), GS);
-        lb::gemm(c, Op::NoTrans, Op::NoTrans, rows, ncols, w, T(-1), V, vr, W.data(), GS, T(1), Zr, ldz);
-    }
-    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-}
-
-/// 1 x P grid over the processes of g (every row local: 1-D column layout)
-inline GridPtr row_grid(GridPtr const& g) {
-    if (g->p() == 1) return g;
-    return std::make_shared<Grid>(1, g->size(), GridOrder::Col, g->world_ptr(), g->world_ptr(),
-                                  std::make_shared<SelfComm>());
-}
-
-/// P x 1 grid over the processes of g (all columns local: 1-D row layout)
-inline GridPtr col_grid(GridPtr const& g) {
-    if (g->q() == 1) return g;
-    return std::make_shared<Grid>(g->size(), 1, GridOrder::Col, g->world_ptr(), std::make_shared<SelfComm>(),
-                                  g->world_ptr());
-}
-
-/// bdsqr transformations on the local rows of U and Vt (row layout: rows are
-/// independent under column rotations, so no communication).  Device: QR
-/// sweeps are batched kRotBatch at a time into step-ordered (c, s) tables
-/// (pinned, double-buffered) and applied by the register-window wavefront
-/// kernel while the host keeps iterating on (d, e); host: loops.
-template <typename T>
-struct RowRotSink : host::RotSink<real_type<T>> {
-    using R = real_type<T>;
-    using Rots = std::vector<host::PlaneRot<R>>;
-    static constexpr int K = slate_amd::dev::kRotBatch;
-    lb::Ctx c;
-    int64_t n = 0;
-    T* U = nullptr; int64_t ldu = 0, urows = 0;
-    T* V = nullptr; int64_t ldv = 0, vrows = 0;
-    size_t tsz = 0;                                // reals per table (one matrix)
-    R* hb[2] = {nullptr, nullptr};
-    Work<R> db[2];
+    std::vector<T> hVb(kBatch * VB), htb(kBatch * GS);
+    Work<T> dV[2], dtv[2];
     hipEvent_t ev[2] = {nullptr, nullptr};
+    if (c.dev())
+        for (int b = 0; b < 2; ++b) {
+            dV[b].resize(tg, hVb.size());
+            dtv[b].resize(tg, htb.size());
+            ev[b] = device::event_get();
+            slate_hip_call(hipEventRecord(ev[b], c.stream));
+        }
+    std::vector<int64_t> r0s(kBatch), ws(kBatch);
     int cur = 0;
-    std::vector<Rots> bu, bv;                      // the batch's sweeps
-
-    RowRotSink(lb::Ctx const& c_, int64_t n_) : c(c_), n(n_) {
+    for (size_t g0 = 0; g0 < ng; g0 += kBatch) {
+        const size_t nbat = std::min(kBatch, ng - g0);
+        // the device buffer about to be refilled must be free (its last use
+        // was two batches ago)
+        if (c.dev()) slate_hip_call(hipEventSynchronize(ev[cur]));
+        std::fill(hVb.begin(), hVb.end(), T(0));
+        std::fill(htb.begin(), htb.end(), T(0));
+        #pragma omp parallel for schedule(dynamic)
+        for (size_t bi = 0; bi < nbat; ++bi) {
+            const size_t gi = g0 + bi;
+            const int64_t J = keys[gi].first, t = keys[gi].second, r0 = J * GS + t * kd + 1;
+            r0s[bi] = r0;
+            int64_t w = 0;
+            for (size_t r : groups.at(keys[gi])) {
+                const int64_t i = Q.tag[r] - J * GS;
+                slate_assert(Q.off[r] - r0 == i && i + Q.len[r] <= vr);
+                T const* v = Q.v.data() + Q.voff[r];
+                for (int64_t ii = 0; ii < Q.len[r]; ++ii) hVb[bi * VB + (i + ii) + i * vr] = v[ii];
+                htb[bi * GS + i] = Q.tau[r];
+                w = std::max(w, i + 1);
+            }
+            ws[bi] = w;
+        }
+        T const* Vall = hVb.data();
+        T const* tall = htb.data();
         if (c.dev()) {
-            tsz = size_t(2 * K) * size_t(n + 2 * K);
-            for (int b = 0; b < 2; ++b) {
-                hb[b] = static_cast<R*>(device::malloc_host(sizeof(R) * 2 * tsz));
-                db[b].resize(Target::Devices, 2 * tsz);
-                ev[b] = device::event_get();
-                slate_hip_call(hipEventRecord(ev[b], c.stream));
-            }
+            device::memcpy_async(dV[cur].data(), hVb.data(), nbat * VB * sizeof(T), c.stream);
+            device::memcpy_async(dtv[cur].data(), htb.data(), nbat * GS * sizeof(T), c.stream);
+            Vall = dV[cur].data();
+            tall = dtv[cur].data();
         }
-    }
-    ~RowRotSink() override {
+        for (size_t bi = 0; bi < nbat; ++bi) {
+            const int64_t r0 = r0s[bi], w = ws[bi];                 // w: columns in use
+            const int64_t rows = std::min(w - 1 + kd, n - r0);
+            if (rows <= 0 || w <= 0) continue;
+            T const* V = Vall + bi * VB;
+            T* Zr = Z + r0;
+            lb::gemm(c, Op::ConjTrans, Op::NoTrans, w, w, rows, T(1), V, vr, V, vr, T(0), G.data(), GS);
+            tinv(w, G.data(), tall + bi * GS);
+            lb::gemm(c, Op::ConjTrans, Op::NoTrans, w, ncols, rows, T(1), V, vr, Zr, ldz, T(0), W.data(), GS);
+            lb::trsm(c, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, w, ncols, T(1), G.data(), GS, W.data(), GS);
+            lb::gemm(c, Op::NoTrans, Op::NoTrans, rows, ncols, w, T(-1), V, vr, W.data(), GS, T(1), Zr, ldz);
+        }
         if (c.dev()) {
-            (void)hipStreamSynchronize(c.stream);
-            for (int b = 0; b < 2; ++b) { device::free_host(hb[b]); device::event_put(ev[b]); }
+            // the host staging buffer is reused next batch: wait for the upload
+            slate_hip_call(hipEventRecord(ev[cur], c.stream));
+            slate_hip_call(hipStreamSynchronize(c.stream));
+            cur ^= 1;
         }
     }
-    /// host twin of the rot_sweeps kernel (same table, same step order), so
-    /// the CPU tests check the batching
-    static void sweeps_host(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, R const* D) {
-        if (p1 - p0 < 2) return;
-        const int64_t tend = p1 - 2 + 2 * (K - 1);
-        #pragma omp parallel for schedule(static) if (rows > 64)
-        for (int64_t r = 0; r < rows; ++r) {
-            T w[2 * K];
-            for (int i = 0; i < 2 * K; ++i) w[i] = T(0);
-            w[2 * K - 2] = M[r + p0 * ld];
-            w[2 * K - 1] = (p0 + 1 < p1) ? M[r + (p0 + 1) * ld] : T(0);
-            for (int64_t tau = p0; tau <= tend; ++tau) {
-                R const* cs = D + 2 * K * (tau - p0);
-                for (int q = 0; q < K; ++q) {
-                    const R cc = cs[2 * q], sn = cs[2 * q + 1];
-                    const T x = w[2 * K - 2 - 2 * q], y = w[2 * K - 1 - 2 * q];
-                    w[2 * K - 2 - 2 * q] = x * cc - y * sn;
-                    w[2 * K - 1 - 2 * q] = x * sn + y * cc;
-                }
-                const int64_t cr = tau - 2 * K + 2;
-                if (cr >= p0) M[r + cr * ld] = w[0];
-                for (int i = 0; i < 2 * K - 1; ++i) w[i] = w[i + 1];
-                w[2 * K - 1] = (tau + 2 < p1) ? M[r + (tau + 2) * ld] : T(0);
-            }
-            M[r + (p1 - 1) * ld] = w[0];
-        }
+    if (c.dev()) {
+        slate_hip_call(hipStreamSynchronize(c.stream));
+        for (int b = 0; b < 2; ++b) device::event_put(ev[b]);
     }
-    static std::pair<int64_t, int64_t> build(std::vector<Rots> const& b, R* D) {
-        int64_t p0 = INT64_MAX, p1 = -1;
-        for (auto const& rs : b)
-            if (!rs.empty()) { p0 = std::min(p0, rs.front().i); p1 = std::max(p1, rs.back().i + 2); }
-        if (p1 < 0) return {0, 0};
-        const int64_t steps = p1 - p0 + 2 * K - 3;
-        for (int64_t t = 0; t < steps; ++t)
-            for (int q = 0; q < K; ++q) { D[2 * (t * K + q)] = R(1); D[2 * (t * K + q) + 1] = R(0); }
-        for (size_t q = 0; q < b.size(); ++q)
-            for (auto const& g : b[q]) {
-                const int64_t t = g.i + 2 * int64_t(q) - p0;
-                D[2 * (t * K + q)] = g.c;
-                D[2 * (t * K + q) + 1] = g.s;
-            }
-        return {p0, p1};
-    }
-    void flush() {
-        if (bu.empty()) return;
-        if (!c.dev()) {
-            std::vector<R> D(size_t(2 * K) * size_t(n + 2 * K));
-            auto ru = build(bu, D.data());
-            if (U) sweeps_host(urows, U, ldu, ru.first, ru.second, D.data());
-            auto rv = build(bv, D.data());
-            if (V) sweeps_host(vrows, V, ldv, rv.first, rv.second, D.data());
-            bu.clear();
-            bv.clear();
-            return;
-        }
-        namespace kd_ = slate_amd::dev;
-        R* Du = hb[cur];
-        R* Dv = hb[cur] + tsz;
-        auto ru = build(bu, Du), rv = build(bv, Dv);
-        const size_t su = size_t(std::max<int64_t>(ru.second - ru.first + 2 * K - 3, 0)) * 2 * K;
-        const size_t sv = size_t(std::max<int64_t>(rv.second - rv.first + 2 * K - 3, 0)) * 2 * K;
-        if (su) device::memcpy_async(db[cur].data(), Du, su * sizeof(R), c.stream);
-        if (sv) device::memcpy_async(db[cur].data() + tsz, Dv, sv * sizeof(R), c.stream);
-        if (U && su) kd_::rot_sweeps(urows, kd_::dptr(U), ldu, ru.first, ru.second, db[cur].data(), c.stream);
-        if (V && sv) kd_::rot_sweeps(vrows, kd_::dptr(V), ldv, rv.first, rv.second, db[cur].data() + tsz, c.stream);
-        slate_hip_call(hipEventRecord(ev[cur], c.stream));
-        cur ^= 1;
-        bu.clear();
-        bv.clear();
-        slate_hip_call(hipEventSynchronize(ev[cur]));   // the other staging buffer is free again
-    }
-    void sweep(Rots const& ru, Rots const& rv) override {
-        bu.push_back(ru);
-        bv.push_back(rv);
-        if (int(bu.size()) == K) flush();
-    }
-    void rot_u(int64_t a, int64_t b, R cc, R sn) override {
-        if (!U) return;
-        flush();
-        if (!c.dev()) {
-            T* x = U + a * ldu;
-            T* y = U + b * ldu;
-            for (int64_t r = 0; r < urows; ++r) {
-                T p = x[r], q = y[r];
-                x[r] = p * cc + q * sn;
-                y[r] = q * cc - p * sn;
-            }
-            return;
-        }
-        flush();
-        slate_amd::dev::rot_cols(urows, slate_amd::dev::dptr(U), ldu, a, b, cc, sn, c.stream);
-    }
-    void negate_v(int64_t k) override {
-        if (!V) return;
-        flush();
-        lb::scale(c, Uplo::General, vrows, int64_t(1), R(-1), R(1), V + k * ldv, ldv);
-    }
-    void permute(std::vector<int64_t> const& perm) override {
-        flush();
-        auto pc = [&](T* M, int64_t ld, int64_t rows) {
-            if (!M || rows <= 0) return;
-            Work<T> tmp(c.dev() ? Target::Devices : Target::HostTask, size_t(rows) * n);
-            if (c.dev()) {
-                Work<int64_t> dp(Target::Devices, perm.size());
-                device::memcpy_async(dp.data(), perm.data(), perm.size() * sizeof(int64_t), c.stream);
-                slate_amd::dev::rbt_gather(false, false, n, rows, dp.data(), slate_amd::dev::dptr(M), ld,
-                                           slate_amd::dev::dptr(tmp.data()), rows, c.stream);
-                lb::copy2d(c, rows, n, tmp.data(), rows, M, ld);
-                slate_hip_call(hipStreamSynchronize(c.stream));
-            } else {
-                for (int64_t i = 0; i < n; ++i)
-                    for (int64_t r = 0; r < rows; ++r) tmp.data()[r + i * rows] = M[r + perm[i] * ld];
-                for (int64_t i = 0; i < n; ++i)
-                    for (int64_t r = 0; r < rows; ++r) M[r + i * ld] = tmp.data()[r + i * rows];
-            }
-        };
-        pc(U, ldu, urows);
-        pc(V, ldv, vrows);
-    }
-    void finish() {
-        flush();
-        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    }
-};
+}
 
-/// Local rows of a P x 1 row-layout n x n matrix set to diag(dg) (host build, one upload).
+/// Local rows of a P x 1 row-layout n x n matrix set to diag(dg): zero fill,
+/// then each local tile's diagonal run written with one strided copy
+/// (O(n) host memory).
 template <typename T>
 void set_diag_rows(Matrix<T>& M, std::vector<T> const& dg, Target target) {
+    Options o = {{Option::Target, target}};
+    set(T(0), T(0), M, o);
     const Loc loc = loc_of(target);
     LocalBlock<T> lm = M.local(loc, true);
-    const int64_t n = M.n();
-    std::vector<T> h(size_t(std::max<int64_t>(lm.m, 1)) * n, T(0));
+    if (lm.m == 0) return;
+    hipStream_t st = target == Target::Devices ? device::queue(0) : nullptr;
     for (int64_t i = 0; i < M.mt(); ++i) {
         if (M.srow_owner(i) != M.grid()->myrow()) continue;
-        const int64_t lr = lrow_of(M, i), gr = grow_of(M, i);
-        for (int64_t ii = 0; ii < M.tileMb(i); ++ii) h[(lr + ii) + (gr + ii) * lm.m] = dg[gr + ii];
+        const int64_t lr = lrow_of(M, i), gr = grow_of(M, i), mb = M.tileMb(i);
+        T* dst = lm.ptr + lr + gr * lm.ld;
+        if (target == Target::Devices)
+            device::memcpy2d_async(dst, (lm.ld + 1) * sizeof(T), dg.data() + gr, sizeof(T), sizeof(T), mb, st);
+        else
+            for (int64_t ii = 0; ii < mb; ++ii) dst[ii * (lm.ld + 1)] = dg[gr + ii];
     }
-    if (lm.m == 0) return;
-    if (target == Target::Devices) {
-        device::memcpy2d_async(lm.ptr, lm.ld * sizeof(T), h.data(), lm.m * sizeof(T), lm.m * sizeof(T), n,
-                               device::queue(0));
-        slate_hip_call(hipStreamSynchronize(device::queue(0)));
-    } else {
-        for (int64_t j = 0; j < n; ++j) std::copy(h.begin() + j * lm.m, h.begin() + (j + 1) * lm.m, lm.ptr + j * lm.ld);
-    }
+    if (st) slate_hip_call(hipStreamSynchronize(st));
 }
 
 template <typename T>
@@ -511,40 +371,46 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     }
     const int64_t me = get_option<int64_t>(opts, Option::MethodEig, int64_t(MethodEig::DC));
     const bool use_qr = (me == int64_t(MethodEig::QR) || me == 'q');
-    std::vector<R> Zr(size_t(n) * n, R(0));
+    // tridiagonal eigenvectors, distributed on A's grid (no n x n host array):
+    // divide and conquer with the merges as distributed GEMMs, or QL with the
+    // rotations applied to each rank's rows (eig_dist.cc)
+    const int64_t nbq = std::max<int64_t>(kd, std::min<int64_t>(A.nb(), 512));
+    Matrix<R> Qt(n, n, nbq, nbq, gA);
+    Qt.insertLocalTiles(target);
     {
         trace::Block t2("tridiag_eig");
         if (use_qr) {
-            for (int64_t i = 0; i < n; ++i) Zr[i + i * n] = R(1);
-            host::steqr<R, R>(n, d.data(), e.data(), Zr.data(), n, n);
+            set(R(0), R(1), Qt, opts);
+            steqr2_dist<R>(d, e, Qt, opts);
         } else {
-            host::stedc<R>(n, d.data(), e.data(), Zr.data(), n);
+            stedc_dist<R>(d, e, Qt, opts);
         }
     }
     Lambda = d;
-    // Z1 (1-D column layout, kd-wide column tiles): my columns of
-    // diag(phase) Zr, then Q2 applied to all rows of them
+    // Z1 (1-D column layout, kd-wide column tiles): diag(phase) Qt, then Q2
+    // applied to all rows of my columns
     Matrix<T> Z1(n, n, n, kd, row_grid(gA));
     Z1.insertLocalTiles(target);
     {
         trace::Block t2("unmtr_hb2st");
+        Matrix<R> Q1(n, n, n, kd, row_grid(gA));
+        Q1.insertLocalTiles(target);
+        slate::copy<R, R>(Qt, Q1, opts);
+        Qt = Matrix<R>();
+        LocalBlock<R> lq = Q1.local(loc, false);
         LocalBlock<T> lz = Z1.local(loc, true);
-        std::vector<T> hz(size_t(n) * std::max<int64_t>(lz.n, 1));
-        for (int64_t j = 0; j < Z1.nt(); ++j) {
-            if (Z1.scol_owner(j) != Z1.grid()->mycol()) continue;
-            const int64_t lc = lcol_of(Z1, j), gc = gcol_of(Z1, j);
-            for (int64_t jj = 0; jj < Z1.tileNb(j); ++jj)
-                for (int64_t i = 0; i < n; ++i) hz[i + (lc + jj) * n] = phase[i] * T(Zr[i + (gc + jj) * n]);
-        }
-        Zr.clear(); Zr.shrink_to_fit();
+        lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
         if (lz.n > 0) {
-            lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
-            if (c.dev())
-                device::memcpy2d_async(lz.ptr, lz.ld * sizeof(T), hz.data(), n * sizeof(T), n * sizeof(T), lz.n,
-                                       c.stream);
-            else
+            if (c.dev()) {
+                Work<T> dph(Target::Devices, size_t(n));
+                device::memcpy_async(dph.data(), phase.data(), n * sizeof(T), c.stream);
+                slate_amd::dev::real_rowscale(n, lz.n, lq.ptr, lq.ld, slate_amd::dev::dptr(dph.data()),
+                                              slate_amd::dev::dptr(lz.ptr), lz.ld, c.stream);
+                slate_hip_call(hipStreamSynchronize(c.stream));
+            } else {
                 for (int64_t j = 0; j < lz.n; ++j)
-                    std::copy(hz.begin() + j * n, hz.begin() + (j + 1) * n, lz.ptr + j * lz.ld);
+                    for (int64_t i = 0; i < n; ++i) lz.ptr[i + j * lz.ld] = phase[i] * T(lq.ptr[i + j * lq.ld]);
+            }
             unmtr_hb2st_blocked(Q2, n, kd, lz.ptr, lz.ld, lz.n, c);
         }
     }

@@ -378,6 +378,72 @@ int64_t steqr(int64_t n, R* d, R* e_in, T* Z, int64_t ldz, int64_t zrows) {
     return unconverged;
 }
 
+/// steqr with every rotation sent to a sink (distributed Z rows): one
+/// sink->sweep per QL sweep, rotations in application order (i DEscending,
+/// [x y] <- [c x - s y, s x + c y] on columns (i, i+1)); the final ascending
+/// sort as one sink->permute.
+template <typename R>
+int64_t steqr_core(int64_t n, R* d, R* e_in, RotSink<R>* sink) {
+    if (n <= 0) return 0;
+    std::vector<R> e(n, R(0));
+    for (int64_t i = 0; i + 1 < n; ++i) e[i] = e_in[i];
+    const R eps = std::numeric_limits<R>::epsilon();
+    R f = 0, tst1 = 0;
+    int64_t unconverged = 0;
+    std::vector<PlaneRot<R>> rots;
+    const std::vector<PlaneRot<R>> none;
+    for (int64_t l = 0; l < n; ++l) {
+        tst1 = std::max(tst1, std::abs(d[l]) + std::abs(e[l]));
+        int64_t m = l;
+        while (m < n - 1 && std::abs(e[m]) > eps * tst1) ++m;
+        if (m > l) {
+            int iter = 0;
+            do {
+                if (++iter > 60) { ++unconverged; break; }
+                R g = d[l];
+                R p = (d[l + 1] - g) / (R(2) * e[l]);
+                R r = std::hypot(p, R(1));
+                if (p < 0) r = -r;
+                d[l] = e[l] / (p + r);
+                d[l + 1] = e[l] * (p + r);
+                R dl1 = d[l + 1];
+                R h = g - d[l];
+                for (int64_t i = l + 2; i < n; ++i) d[i] -= h;
+                f += h;
+                p = d[m];
+                R c = 1, c2 = 1, c3 = 1, el1 = e[l + 1], s = 0, s2 = 0;
+                rots.clear();
+                for (int64_t i = m - 1; i >= l; --i) {
+                    c3 = c2; c2 = c; s2 = s;
+                    g = c * e[i];
+                    h = c * p;
+                    r = std::hypot(p, e[i]);
+                    e[i + 1] = s * r;
+                    s = e[i] / r;
+                    c = p / r;
+                    p = c * d[i] - s * g;
+                    d[i + 1] = h + s * (c * g + s * d[i]);
+                    rots.push_back({i, c, s});
+                }
+                if (sink) sink->sweep(rots, none);
+                p = -s * s2 * c3 * el1 * e[l] / dl1;
+                e[l] = s * p;
+                d[l] = c * p;
+            } while (std::abs(e[l]) > eps * tst1);
+        }
+        d[l] += f;
+        e[l] = 0;
+    }
+    std::vector<int64_t> perm(n);
+    std::iota(perm.begin(), perm.end(), int64_t(0));
+    std::stable_sort(perm.begin(), perm.end(), [&](int64_t a, int64_t b) { return d[a] < d[b]; });
+    std::vector<R> ds(n);
+    for (int64_t i = 0; i < n; ++i) ds[i] = d[perm[i]];
+    std::copy(ds.begin(), ds.end(), d);
+    if (sink) sink->permute(perm);
+    return unconverged;
+}
+
 template <typename R>
 int64_t sterf(int64_t n, R* d, R* e) {
     return steqr<R, R>(n, d, e, nullptr, 1, 0);
@@ -778,6 +844,8 @@ SLATE_EIGH_INST(std::complex<double>)
 template int64_t bdsqr_core<float>(int64_t, float*, float*, RotSink<float>*);
 template int64_t bdsqr_core<double>(int64_t, double*, double*, RotSink<double>*);
 template int64_t sterf<float>(int64_t, float*, float*);
+template int64_t steqr_core<float>(int64_t, float*, float*, RotSink<float>*);
+template int64_t steqr_core<double>(int64_t, double*, double*, RotSink<double>*);
 template int64_t sterf<double>(int64_t, double*, double*);
 template int64_t stedc<float>(int64_t, float*, float*, float*, int64_t);
 template int64_t stedc<double>(int64_t, double*, double*, double*, int64_t);

@@ -4,12 +4,18 @@
 // steqr2, sterf, unmbr_tb2bd; syev/sygv/sygst/sysv/sytrf/sytrs, gesvd,
 // svd_vals, gels_qr, gels_cholqr).
 //
-// The bulge-chasing stages run on the host of every rank (the reference runs
-// hb2st/tb2bd on one node with OpenMP tasks, hb2st.cc / tb2bd.cc); their
-// reflectors are kept as BandReflectors, replicated on every rank, instead of
-// the reference's V matrix.  Vector matrices are updated through replicated
-// host copies and written back to each rank's local part.
+// The bulge-chasing stages run on the host of every rank from the gathered
+// band only (O(n kd) data; the reference runs hb2st/tb2bd on one node with
+// OpenMP tasks, hb2st.cc / tb2bd.cc); their reflectors are kept as
+// BandReflectors, replicated on every rank, instead of the reference's V
+// matrix.  The vector stages keep their matrices distributed: the reflectors /
+// rotations act within columns (rows), so they run on a 1-D copy in which
+// every rank holds whole columns (rows) of its share; stedc is the distributed
+// divide and conquer (eig_dist.cc).  The low-level stedc_* building blocks
+// (z_vector, sort, deflate, secular) keep replicated host copies: they are
+// test hooks for the merge steps, not the solver's path.
 #include "internal.hh"
+#include "eig_sinks.hh"
 
 #include <functional>
 
@@ -52,23 +58,37 @@ void apply_band_reflectors_left(Op op, BandReflectors<T> const& V, int64_t n, T*
     }
 }
 
-/// Left or right application of a reflector sequence to a distributed C.
+/// Left or right application of a reflector sequence to a distributed C:
+/// Left acts within columns, so C is copied to a 1 x P layout (every rank
+/// holds whole columns); Right acts within rows (P x 1 layout).  Each rank
+/// applies the reflectors to its own share: per-rank host memory O(m n / P).
 template <typename T>
-void apply_band_reflectors(Side side, Op op, BandReflectors<T> const& V, Matrix<T>& C, Options const& opts) {
+void apply_band_reflectors(Side side, Op op, BandReflectors<T> const& V, Matrix<T>& C, Options const&) {
     const int64_t m = C.m(), n = C.n();
-    std::vector<T> h = replicate(C, opts);
+    if (m == 0 || n == 0) return;
+    Options oh = {{Option::Target, Target::Host}};
     if (side == Side::Left) {
-        apply_band_reflectors_left(op, V, n, h.data(), m, m);
-        write_back(C, h, m);
+        Matrix<T> C1(m, n, m, std::max<int64_t>(1, C.nb()), row_grid(C.grid()));
+        C1.insertLocalTiles(Target::Host);
+        slate::copy<T, T>(C, C1, oh);
+        LocalBlock<T> l = C1.local(Loc::Host, true);
+        if (l.n > 0) apply_band_reflectors_left(op, V, l.n, l.ptr, l.ld, m);
+        slate::copy<T, T>(C1, C, oh);
     } else {
-        // C M = (M^H C^H)^H
-        std::vector<T> t(size_t(n) * m);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = 0; i < m; ++i) t[j + i * n] = slate::conj(h[i + j * m]);
-        apply_band_reflectors_left(op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans, V, m, t.data(), n, n);
-        for (int64_t j = 0; j < n; ++j)
-            for (int64_t i = 0; i < m; ++i) h[i + j * m] = slate::conj(t[j + i * n]);
-        write_back(C, h, m);
+        // C M = (M^H C^H)^H on my rows
+        Matrix<T> C1(m, n, std::max<int64_t>(1, C.mb()), n, col_grid(C.grid()));
+        C1.insertLocalTiles(Target::Host);
+        slate::copy<T, T>(C, C1, oh);
+        LocalBlock<T> l = C1.local(Loc::Host, true);
+        if (l.m > 0) {
+            std::vector<T> t(size_t(n) * l.m);
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < l.m; ++i) t[j + i * n] = slate::conj(l.ptr[i + j * l.ld]);
+            apply_band_reflectors_left(op == Op::NoTrans ? Op::ConjTrans : Op::NoTrans, V, l.m, t.data(), n, n);
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < l.m; ++i) l.ptr[i + j * l.ld] = slate::conj(t[j + i * n]);
+        }
+        slate::copy<T, T>(C1, C, oh);
     }
 }
 
@@ -80,19 +100,24 @@ void hb2st(HermitianBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector<
            BandReflectors<T>& V, Options const& opts) {
     trace::Block tb("hb2st");
     internal::DriverScope ds_;
+    (void)opts;
     const int64_t n = A.n(), kd = A.bandwidth();
-    std::vector<T> full = replicate(A, opts);
-    const bool lower = A.uplo() == Uplo::Lower;
-    std::vector<T> B(size_t(n) * n, T(0));
-    for (int64_t j = 0; j < n; ++j)
-        for (int64_t i = j; i <= std::min(n - 1, j + kd); ++i) {
-            T v = lower ? full[i + j * n] : slate::conj(full[j + i * n]);
-            B[i + j * n] = v;
-            B[j + i * n] = slate::conj(v);
-        }
-    for (int64_t i = 0; i < n; ++i) B[i + i * n] = T(std::real(B[i + i * n]));
+    // the lower band gathered into general band storage with room for the
+    // bulge (kl = ku = 2 kd), then mirrored: (i, j) at B[M + i - j + j ldb]
+    const int64_t M = 2 * std::max<int64_t>(kd, 1), ldb = 2 * M + 1;
+    BaseMatrix<T> Ap = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(A.op() == Op::ConjTrans);
+    const bool lower = (A.uplo_physical() == Uplo::Lower);
+    std::vector<T> B = lower ? band_gather<T>(Ap, kd, 0, M, ldb) : band_gather<T>(Ap, 0, kd, M, ldb, true);
+    if (A.op() != Op::NoTrans && is_complex_v<T> && A.op() == Op::Trans)
+        for (auto& x : B) x = slate::conj(x);
+    for (int64_t j = 0; j < n; ++j) {
+        for (int64_t i = j + 1; i <= std::min(n - 1, j + kd); ++i)
+            B[size_t(M + j - i + i * ldb)] = slate::conj(B[size_t(M + i - j + j * ldb)]);
+        T& dd = B[size_t(M + j * ldb)];
+        dd = T(std::real(dd));
+    }
     V = BandReflectors<T>{};
-    host::hb2st<T>(n, kd, B.data(), n, D, E, V.Q, V.phase);
+    host::hb2st<T>(n, kd, B.data() + M, ldb - 1, D, E, V.Q, V.phase);
 }
 
 template <typename T>
@@ -131,12 +156,20 @@ void tb2bd(TriangularBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector
     internal::DriverScope ds_;
     slate_error_if_msg(A.uplo() != Uplo::Upper, "tb2bd: A must be upper triangular band");
     const int64_t m = A.m(), n = A.n(), kd = A.bandwidth();
+    U = BandReflectors<T>{};
+    V = BandReflectors<T>{};
+    if (m == n && A.op() == Op::NoTrans) {
+        // band only, in general band storage with room for the bulge
+        // (kl = ku = 3 kd + 2, as the svd driver): (i, j) at B[M + i - j + j ldb]
+        const int64_t M = 3 * std::max<int64_t>(kd, 1) + 2, ldb = 2 * M + 1;
+        std::vector<T> B = band_gather<T>(A, 0, kd, M, ldb);
+        host::tb2bd<T>(m, n, kd, B.data() + M, ldb - 1, D, E, U.Q, V.Q, U.phase, V.phase);
+        return;
+    }
     std::vector<T> full = replicate(A, opts);
     std::vector<T> B(size_t(m) * n, T(0));
     for (int64_t j = 0; j < n; ++j)
         for (int64_t i = std::max<int64_t>(0, j - kd); i <= std::min(j, m - 1); ++i) B[i + j * m] = full[i + j * m];
-    U = BandReflectors<T>{};
-    V = BandReflectors<T>{};
     host::tb2bd<T>(m, n, kd, B.data(), m, D, E, U.Q, V.Q, U.phase, V.phase);
 }
 
@@ -194,36 +227,42 @@ void steqr2(Job jobz, std::vector<real_type<T>>& D, std::vector<real_type<T>>& E
         host::sterf<R>(n, D.data(), E.data());
         return;
     }
-    // Z's rows are independent under the column rotations: update the
-    // replicated rows (reference steqr2 keeps them distributed per rank)
-    const int64_t zm = Z.m();
-    std::vector<T> h = replicate(Z, opts);
-    int64_t info = host::steqr<R, T>(n, D.data(), E.data(), h.data(), zm, zm);
+    // Z's rows are independent under the column rotations: each rank applies
+    // them to its own rows (reference steqr2.cc:60-74)
+    slate_error_if_msg(Z.n() != n, "steqr2: Z must have n columns");
+    int64_t info = internal::steqr2_dist<T>(D, E, Z, opts);
     slate_error_if_msg(info != 0, "steqr2: QL iteration did not converge");
-    write_back(Z, h, zm);
+}
+
+/// Distributed divide and conquer into Q (eig_dist.cc); a Q that is not a
+/// square-tiled block-cyclic n x n matrix gets a block-cyclic working copy.
+template <typename R>
+void stedc_into(std::vector<R>& D, std::vector<R> const& E, Matrix<R>& Q, Options const& opts) {
+    const int64_t n = int64_t(D.size());
+    slate_error_if_msg(Q.m() != n || Q.n() != n, "stedc: Q must be n x n");
+    if (!Q.arbitrary_layout() && Q.op() == Op::NoTrans && Q.mb() == Q.nb() && Q.aligned()) {
+        internal::stedc_dist<R>(D, E, Q, opts);
+        return;
+    }
+    const int64_t b = std::max<int64_t>(1, std::max(Q.mb(), Q.nb()));
+    Matrix<R> Qb(n, n, b, b, Q.grid());
+    Qb.insertLocalTiles(resolve_target(opts));
+    internal::stedc_dist<R>(D, E, Qb, opts);
+    slate::copy<R, R>(Qb, Q, opts);
 }
 
 template <typename R>
-void stedc(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const&) {
+void stedc(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const& opts) {
     trace::Block tb("stedc");
     internal::DriverScope ds_;
-    const int64_t n = int64_t(D.size());
-    std::vector<R> h(size_t(n) * n);
-    host::stedc<R>(n, D.data(), E.data(), h.data(), n);
-    write_back(Q, h, n);
+    stedc_into(D, E, Q, opts);
 }
 
 template <typename R>
 void stedc_solve(std::vector<R>& D, std::vector<R>& E, Matrix<R>& Q, Options const& opts) {
     trace::Block tb("stedc_solve");
     internal::DriverScope ds_;
-    const int64_t n = int64_t(D.size());
-    std::vector<R> ee(E.begin(), E.end());
-    ee.resize(std::max<int64_t>(n, 1), R(0));
-    std::vector<R> h(size_t(n) * n);
-    host::stedc_solve<R>(n, D.data(), ee.data(), h.data(), n);
-    write_back(Q, h, n);
-    (void)opts;
+    stedc_into(D, E, Q, opts);
 }
 
 template <typename R>
@@ -279,15 +318,41 @@ void bdsqr(Job jobu, Job jobvt, std::vector<real_type<T>>& D, std::vector<real_t
     using R = real_type<T>;
     const int64_t n = int64_t(D.size());
     const bool wu = jobu != Job::NoVec && wanted(U), wv = jobvt != Job::NoVec && wanted(VT);
-    std::vector<T> hu, hv;
-    if (wu) hu = replicate(U, opts);
-    if (wv) hv = replicate(VT, opts);
-    const int64_t um = wu ? U.m() : 1, vn = wv ? VT.n() : 1;
-    int64_t info = host::bdsqr<R, T>(n, D.data(), E.data(), wu ? hu.data() : nullptr, um, um,
-                                     wv ? hv.data() : nullptr, std::max<int64_t>(n, 1), vn);
+    if (!wu && !wv) {
+        int64_t info = host::bdsqr_core<R>(n, D.data(), E.data(), nullptr);
+        slate_error_if_msg(info != 0, "bdsqr: QR iteration did not converge");
+        return;
+    }
+    // the rotations act on columns of U and rows of VT: U's rows and VT's
+    // columns (rows of Vt = VT^T) are spread over the ranks (P x 1 layouts);
+    // every rank rotates its own rows, on the device through the batched
+    // wavefront kernel (eig_sinks.hh)
+    const Target target = resolve_target(opts);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    slate_error_if_msg((wu && U.n() != n) || (wv && VT.m() != n), "bdsqr: U must be m x n and VT n x n");
+    Matrix<T> Ur, Vr;
+    if (wu) {
+        Ur = Matrix<T>(U.m(), n, std::max<int64_t>(1, U.mb()), std::max<int64_t>(n, 1), col_grid(U.grid()));
+        Ur.insertLocalTiles(target);
+        slate::copy<T, T>(U, Ur, opts);
+    }
+    if (wv) {
+        Vr = Matrix<T>(VT.n(), n, std::max<int64_t>(1, VT.nb()), std::max<int64_t>(n, 1), col_grid(VT.grid()));
+        Vr.insertLocalTiles(target);
+        slate::copy<T, T>(transpose(VT), Vr, opts);
+    }
+    int64_t info = 0;
+    {
+        RowRotSink<T> sink(c, n);
+        LocalBlock<T> lu, lv;
+        if (wu) { lu = Ur.local(loc_of(target), true); sink.U = lu.m > 0 ? lu.ptr : nullptr; sink.ldu = lu.ld; sink.urows = lu.m; }
+        if (wv) { lv = Vr.local(loc_of(target), true); sink.V = lv.m > 0 ? lv.ptr : nullptr; sink.ldv = lv.ld; sink.vrows = lv.m; }
+        info = host::bdsqr_core<R>(n, D.data(), E.data(), &sink);
+        sink.finish();
+    }
     slate_error_if_msg(info != 0, "bdsqr: QR iteration did not converge");
-    if (wu) write_back(U, hu, um);
-    if (wv) write_back(VT, hv, std::max<int64_t>(n, 1));
+    if (wu) slate::copy<T, T>(Ur, U, opts);
+    if (wv) slate::copy<T, T>(transpose(Vr), VT, opts);
 }
 
 //------------------------------------------------------------------------------

@@ -218,10 +218,55 @@ inline void allreduce_host(Comm& comm, R* v, size_t n, ReduceOp op) {
     comm.allreduce(v, v, n, scalar_type<R>(), op, Loc::Host, nullptr);
 }
 
+/// Replicated LAPACK band storage: AB(r0 + i - j, j) = A(i, j) for
+/// -ku <= i - j <= kl; ldab >= r0 + kl + 1.  conj_upper: read A's upper
+/// band (i < j) as the conj-transposed lower band (Hermitian band, Upper).
+template <typename T>
+std::vector<T> band_gather(BaseMatrix<T> const& A, int64_t kl, int64_t ku, int64_t r0, int64_t ldab,
+                           bool upper_as_lower = false) {
+    const int64_t n = A.n();
+    std::vector<T> ab(size_t(ldab) * n, T(0));
+    for_each_stored(A, false, [&](int64_t i, int64_t j, T& v) {
+        if (upper_as_lower) {
+            if (j >= i && j - i <= ku) ab[(r0 + j - i) + i * ldab] = slate::conj(v);   // (j, i) of the lower band
+        } else if (i - j <= kl && j - i <= ku) {
+            ab[(r0 + i - j) + j * ldab] = v;
+        }
+    });
+    // every band entry is owned by exactly one rank
+    Comm& w = A.grid()->world();
+    if (w.size() > 1) {
+        using R = real_type<T>;
+        size_t mult = is_complex_v<T> ? 2 : 1;
+        allreduce_host<R>(w, reinterpret_cast<R*>(ab.data()), ab.size() * mult, ReduceOp::Sum);
+    }
+    return ab;
+}
+
+template <typename T>
+void band_scatter(BaseMatrix<T>& A, std::vector<T> const& ab, int64_t kl, int64_t ku, int64_t r0, int64_t ldab,
+                  bool upper_as_lower = false) {
+    for_each_stored(A, true, [&](int64_t i, int64_t j, T& v) {
+        if (upper_as_lower) {
+            if (j >= i && j - i <= ku) v = slate::conj(ab[(r0 + j - i) + i * ldab]);
+        } else if (i - j <= kl && j - i <= ku) {
+            v = ab[(r0 + i - j) + j * ldab];
+        }
+    });
+}
+
 /// General redistribution B = op(A) between two matrices over the same world
 /// (any grids / tile sizes with equal element counts), tile by tile over p2p.
 template <typename T>
 void redistribute_op(BaseMatrix<T> const& A, BaseMatrix<T>& B, Target target);
+
+/// Distributed tridiagonal eigensolvers (eig_dist.cc): divide and conquer
+/// with Q on its 2-D grid, and QL with the rotations applied to each rank's
+/// rows of Z.  d, e replicated; eigenvalues ascending in d.
+template <typename R>
+void stedc_dist(std::vector<R>& d, std::vector<R> const& e, Matrix<R>& Q, Options const& opts);
+template <typename T>
+int64_t steqr2_dist(std::vector<real_type<T>>& d, std::vector<real_type<T>>& e, Matrix<T>& Z, Options const& opts);
 
 /// Apply LU pivots to the rows of B (forward: P B; backward: P^T B).
 template <typename T>

@@ -185,6 +185,27 @@ def case_heev(tg, dt, nb):
     assert np.abs(np.sort(lam) - ref).max() <= 100 * tol(dt) * np.abs(ref).max(), "eigenvalues"
     z = s.to_numpy(Z)
     assert np.linalg.norm(h @ z - z * lam) <= 100 * tol(dt) * np.linalg.norm(h) * np.sqrt(n), "vectors"
+    # stage 2 distributed: QL with the rotations on each rank's rows of Z
+    # (method_eig="qr"), and divide and conquer with many merges and heavy
+    # deflation (repeated eigenvalues) -- Q stays on the 2-D grid
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+    Z = s.from_numpy(np.zeros((n, n), dt), nb=nb, target=tg)
+    lam = s.heev(H, Z, target=tg, method_eig="qr")
+    assert np.abs(np.sort(lam) - ref).max() <= 100 * tol(dt) * np.abs(ref).max(), "qr eigenvalues"
+    z = s.to_numpy(Z)
+    assert np.linalg.norm(h @ z - z * lam) <= 100 * tol(dt) * np.linalg.norm(h) * np.sqrt(n), "qr vectors"
+    n3 = 260
+    q3, _ = np.linalg.qr(rnd(n3, n3, dt, 96))
+    ev3 = np.repeat(np.arange(1.0, 14.0), 20)
+    h3 = ((q3 * ev3) @ q3.conj().T).astype(dt)
+    h3 = ((h3 + h3.conj().T) / 2).astype(dt)
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h3, nb=nb, target=tg))
+    Z = s.from_numpy(np.zeros((n3, n3), dt), nb=nb, target=tg)
+    lam = s.heev(H, Z, target=tg)
+    assert np.abs(np.sort(lam) - np.sort(ev3)).max() <= 200 * tol(dt) * 13, "dc deflated eigenvalues"
+    z = s.to_numpy(Z)
+    assert np.linalg.norm(h3 @ z - z * lam) <= 200 * tol(dt) * np.linalg.norm(h3) * np.sqrt(n3), "dc deflated vectors"
+    assert np.abs(z.conj().T @ z - np.eye(n3)).max() < 200 * tol(dt) * n3, "dc orthogonality"
     sv = s.svd_vals(s.from_numpy(a, nb=nb, target=tg), target=tg)
     assert np.abs(np.sort(sv)[::-1] - np.linalg.svd(a, compute_uv=False)).max() <= 100 * tol(dt) * sv.max()
     for (m2, n2) in ((170, 120), (110, 160)):
@@ -197,6 +218,62 @@ def case_heev(tg, dt, nb):
         assert relerr((u * sv) @ vt, b2) < 100 * tol(dt), ("svd", m2, n2)
         assert np.abs(u.conj().T @ u - np.eye(k2)).max() < 100 * tol(dt) * k2
         assert np.abs(vt @ vt.conj().T - np.eye(k2)).max() < 100 * tol(dt) * k2
+
+
+def case_stages(tg, dt, nb):
+    """Stage API on the grid: he2hb -> hb2st (band-only storage input) ->
+    stedc / steqr2 with the vectors distributed -> unmtr_hb2st ->
+    unmtr_he2hb; ge2tb -> tb2bd -> bdsqr on distributed U / VT -> unmbr."""
+    n = 120
+    t = tol(dt)
+    a = rnd(n, n, dt, 71)
+    a = ((a + a.conj().T) / 2).astype(dt)
+    F = s.from_numpy(a, nb=nb, target=tg)
+    Ts = s.he2hb(F, target=tg)
+    f = s.to_numpy(F)
+    band = np.where((np.subtract.outer(np.arange(n), np.arange(n)) >= 0)
+                    & (np.subtract.outer(np.arange(n), np.arange(n)) <= nb), f, 0).astype(dt)
+    Hd = s.HermitianBandMatrix(s.Uplo.Lower, nb, s.from_numpy(band, nb=nb, target=tg))
+    ref = np.linalg.eigvalsh(a)
+    # the same band in band-only storage: hb2st reads the stored band only
+    Hs = s.hermitian_band_matrix(s.Uplo.Lower, n, nb, nb, dtype=dt, target=tg)
+    assert Hs.is_band_storage
+    s.copy(Hd, Hs, target=tg)
+    ds, es, _ = s.hb2st_band(Hs, target=tg)
+    for solver in ("stedc", "steqr2"):
+        d, e, V = s.hb2st_band(Hd, target=tg)
+        assert np.abs(np.asarray(d) - np.asarray(ds)).max() < 100 * t * np.abs(ref).max(), "band-storage hb2st"
+        Zr = s.from_numpy(np.eye(n), nb=nb, target=tg)
+        if solver == "stedc":
+            lam = s.stedc_matrix(d, e, Zr, target=tg)
+        else:
+            lam = s.steqr2(s.Job.Vec, d, e, Zr, target=tg)
+        assert np.abs(np.sort(lam) - ref).max() < 100 * t * np.abs(ref).max(), solver
+        Z = s.from_numpy(s.to_numpy(Zr).astype(dt), nb=nb, target=tg)
+        s.unmtr_hb2st(s.Side.Left, s.Op.NoTrans, V, Z, target=tg)
+        s.unmtr_he2hb(s.Side.Left, s.Op.NoTrans, F, Ts, Z, target=tg)
+        z = s.to_numpy(Z)
+        assert relerr(a @ z, z * lam[None, :]) < 100 * t, solver
+    m2, n2 = 100, 72
+    b = rnd(m2, n2, dt, 72)
+    W = s.from_numpy(b, nb=nb, target=tg)
+    TU, TV = s.ge2tb(W, target=tg)
+    w = s.to_numpy(W)
+    ii, jj = np.meshgrid(np.arange(m2), np.arange(n2), indexing="ij")
+    ub = np.where((jj >= ii) & (jj - ii <= nb), w, 0)[:n2, :].astype(dt)
+    B = s.TriangularBandMatrix(s.Uplo.Upper, s.Diag.NonUnit, nb, s.from_numpy(ub, nb=nb, target=tg))
+    d, e, U2, V2 = s.tb2bd_band(B, target=tg)
+    Ub = s.from_numpy(np.eye(n2, dtype=dt), nb=nb, target=tg)
+    VTb = s.from_numpy(np.eye(n2, dtype=dt), nb=nb, target=tg)
+    sig = s.bdsqr_matrix(s.Job.Vec, s.Job.Vec, d, e, Ub, VTb, target=tg)
+    assert np.abs(np.sort(sig)[::-1] - np.linalg.svd(b, compute_uv=False)).max() < 100 * t * sig.max()
+    s.unmbr_tb2bd(s.Side.Left, s.Op.NoTrans, U2, Ub, target=tg)
+    s.unmbr_tb2bd(s.Side.Right, s.Op.ConjTrans, V2, VTb, target=tg)
+    U = s.from_numpy(np.vstack([s.to_numpy(Ub), np.zeros((m2 - n2, n2), dt)]), nb=nb, target=tg)
+    s.unmbr_ge2tb(s.Side.Left, s.Op.NoTrans, W, TU, U, target=tg)
+    s.unmbr_ge2tb(s.Side.Right, s.Op.NoTrans, W, TV, VTb, target=tg)
+    u, vt = s.to_numpy(U), s.to_numpy(VTb)
+    assert relerr((u * sig[None, :]) @ vt, b) < 100 * t
 
 
 def band_of(a, kl, ku):

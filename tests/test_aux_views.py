@@ -78,3 +78,18 @@ def test_hermitian_max_norm_real_diagonal(n):
     H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=2, grid=grid()))
     v = s.norm(s.Norm.Max, H, target="h")
     assert abs(v - 0.75) < 1e-15
+
+
+def test_set_rectangular_tiles_equal_values():
+    """set(offdiag == diag) on tiles that are not square (mb != nb): every
+    tile is overwritten, including the columns left of the tile's diagonal
+    run (regression: only the diagonal-run sub-block used to be written)."""
+    A = s.Matrix(100, 100, 100, np.float64, mb=32)
+    A.insertLocalTiles(s.Target.Host)
+    A.set_local(np.asfortranarray(np.random.default_rng(0).random((100, 100))))
+    s._slate.set_d(0.0, 0.0, A, s.opts("t"))
+    assert np.abs(s.to_numpy(A)).max() == 0.0
+    s._slate.set_d(2.0, 5.0, A, s.opts("t"))
+    ref = np.full((100, 100), 2.0)
+    np.fill_diagonal(ref, 5.0)
+    assert np.array_equal(s.to_numpy(A), ref)
