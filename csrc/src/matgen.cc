@@ -196,6 +196,31 @@ void fill(gen::Spec spec, BaseMatrix<T>& A, Target target, std::vector<double> c
         if (target == Target::Devices) s.get(Loc::Device, false);
         return;
     }
+    if (s.general()) {
+        // arbitrary distribution (non-uniform tiles, any owner map): my tiles
+        // one by one on the host with the same grid-independent values, then
+        // the device instance
+        spec.m = A.m(); spec.n = A.n(); spec.max_mn = std::max(A.m(), A.n());
+        if (sigma) spec.sigma = sigma->data();
+        using R = real_type<T>;
+        slate_error_if_msg(A.row0() != 0 || A.col0() != 0, "generate_matrix: arbitrary layouts need the whole matrix");
+        s.get(Loc::Host, true);
+        for (int64_t j = 0; j < A.nt(); ++j)
+            for (int64_t i = 0; i < A.mt(); ++i) {
+                if (!A.tileIsLocal(i, j)) continue;
+                Tile<T> t = A.tile(i, j, Loc::Host);
+                const int64_t gi0 = s.layout->rs[i], gj0 = s.layout->cs[j];
+                for (int64_t jj = 0; jj < t.nb; ++jj)
+                    for (int64_t ii = 0; ii < t.mb; ++ii) {
+                        double re, im;
+                        gen::entry(spec, gi0 + ii, gj0 + jj, is_complex_v<T>, re, im);
+                        if constexpr (is_complex_v<T>) t.data[ii + jj * t.stride] = T(R(re), R(im));
+                        else t.data[ii + jj * t.stride] = T(re);
+                    }
+            }
+        if (target == Target::Devices) s.get(Loc::Device, false);
+        return;
+    }
     LocalBlock<T> lb = A.local(loc, true);
     const int64_t rb = A.lrow_begin(), cb = A.lcol_begin();
     spec.m = A.m(); spec.n = A.n(); spec.max_mn = std::max(A.m(), A.n());

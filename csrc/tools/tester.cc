@@ -53,6 +53,17 @@ struct Params {
     int64_t itermax = -1;
     int fallback = -1;
     double pivot_threshold = -1;
+    // operand shape flags of the BLAS-3 / triangular routines (reference
+    // --uplo --trans --side --diag)
+    Uplo uplo = Uplo::Lower;
+    Op trans = Op::NoTrans;
+    Side side = Side::Left;
+    Diag diag = Diag::NonUnit;
+    double cond = std::numeric_limits<double>::quiet_NaN();   // --cond: spectral --matrix kinds
+    int64_t ib = -1;                                          // --ib: inner blocking
+    bool nonuniform = false;                                  // --nonuniform-nb y: varying tile sizes
+    GridOrder order = GridOrder::Col;                         // --go c|r: process grid order
+    char dev_order = 'r';                                     // --do: one GPU per process (accepted)
 };
 
 std::vector<int64_t> parse_list(std::string const& s) {
@@ -111,6 +122,7 @@ struct Case {
         if (P.itermax >= 0) opts[Option::MaxIterations] = P.itermax;
         if (P.fallback >= 0) opts[Option::UseFallbackSolver] = int64_t(P.fallback);
         if (P.pivot_threshold > 0) opts[Option::PivotThreshold] = P.pivot_threshold;
+        if (P.ib > 0) opts[Option::InnerBlocking] = P.ib;
     }
     /// where operands are generated: --origin h puts them on the host (the
     /// drivers then move them to the target and back, reference --origin)
@@ -124,14 +136,41 @@ struct Case {
         BaseMatrix<T>& b = A;
         Options go = opts;
         go[Option::Target] = gt;
+        if (main && P.nonuniform) {
+            // --nonuniform-nb: tiles alternate nb and nb/2 + 1 rows/cols, on a
+            // 2-D cyclic tile map (the drivers' arbitrary-layout path)
+            auto g = default_grid();
+            const int64_t b0 = nb, b1 = std::max<int64_t>(1, nb / 2 + 1);
+            auto tsz = [b0, b1](int64_t i) { return (i % 2 == 0) ? b0 : b1; };
+            const int p = g->p(), q = g->q();
+            const bool colmajor = P.order == GridOrder::Col;
+            Matrix<T> An(rows, cols, tsz, tsz,
+                         [p, q, colmajor](std::tuple<int64_t, int64_t> ij) {
+                             const int64_t i = std::get<0>(ij) % p, j = std::get<1>(ij) % q;
+                             return int(colmajor ? i + j * p : i * q + j);
+                         },
+                         [](std::tuple<int64_t, int64_t>) { return 0; }, g);
+            An.insertLocalTiles(gt);
+            BaseMatrix<T>& bn = An;
+            generate_matrix(P.matrix.empty() ? std::string(kind) : P.matrix, bn, seed++, shift, go);
+            return An;
+        }
         if (main && !P.matrix.empty()) {
-            // --matrix: any matgen kind (element kinds, or spectral ones such as svd / poev / geev)
-            try {
-                generate_matrix(P.matrix, b, seed, shift, go);
-            } catch (std::exception const&) {
+            // --matrix: any matgen kind (element kinds, or spectral ones such as
+            // svd / poev / geev, whose condition number --cond sets)
+            bool done = false;
+            if (std::isnan(P.cond)) {
+                try {
+                    generate_matrix(P.matrix, b, seed, shift, go);
+                    done = true;
+                } catch (std::exception const&) {
+                }
+            }
+            if (!done) {
                 MatgenParams mp;
                 mp.kind = P.matrix;
                 mp.seed = int64_t(seed);
+                mp.cond_request = P.cond;
                 generate_matrix(mp, A, go);
             }
             ++seed;
@@ -242,37 +281,73 @@ Result r_hemm(Case<T>& c) {
     return r;
 }
 
+/// dense diagonal part of a square matrix (a kl = ku = 0 band through gbmm)
+template <typename T>
+Matrix<T> dense_diag(Case<T>& c, Matrix<T> const& D) {
+    auto I = c.zeros(D.n(), D.n()), F = c.zeros(D.m(), D.n());
+    set(T(0), T(1), I, c.opts);
+    gbmm(T(1), BandMatrix<T>(0, 0, D), I, T(0), F, c.opts);
+    return F;
+}
+
+/// op(A) for --trans n|t|c on a triangular view
+template <typename T>
+TriangularMatrix<T> op_tri(Op op, TriangularMatrix<T> const& A) {
+    if (op == Op::Trans) return transpose(A);
+    if (op == Op::ConjTrans) return conj_transpose(A);
+    return A;
+}
+
 template <typename T>
 Result r_trsm(Case<T>& c) {
-    auto Tg = c.mat(c.m, c.m, "rands+n"), B = c.mat(c.m, c.n);
+    // op(A) X = alpha B (--side l) or X op(A) = alpha B (--side r)
+    const bool left = c.P.side == Side::Left;
+    const int64_t an = left ? c.m : c.n;
+    auto Tg = c.mat(an, an, "rands+n"), B = c.mat(c.m, c.n);
     auto B0 = c.copy_of(B);
-    TriangularMatrix<T> L(Uplo::Lower, Diag::NonUnit, Tg);
+    TriangularMatrix<T> A0(c.P.uplo, c.P.diag, Tg);
+    auto A = op_tri(c.P.trans, A0);
     T alpha(2);
     Result r;
-    r.time = c.timed([&] { trsm(Side::Left, alpha, L, B, c.opts); });
-    r.flops = cfac<T>() * double(c.m) * c.m * c.n;
+    r.time = c.timed([&] { trsm(c.P.side, alpha, A, B, c.opts); });
+    r.flops = cfac<T>() * double(an) * an * (left ? c.n : c.m);
     if (c.P.check) {
         auto X = c.copy_of(B);
-        trmm(Side::Left, T(1), L, X, c.opts);          // L X
-        add(-alpha, B0, T(1), X, c.opts);              // L X - alpha B0
-        r.error = c.nrm(X) / (c.nrm(Tg) * c.nrm(B) * double(c.m));
+        trmm(c.P.side, T(1), A, X, c.opts);            // op(A) X  or  X op(A)
+        add(-alpha, B0, T(1), X, c.opts);              //  - alpha B0
+        r.error = c.nrm(X) / (c.nrm(Tg) * c.nrm(B) * double(an));
     }
     return r;
 }
 
 template <typename T>
 Result r_trmm(Case<T>& c) {
-    auto Tg = c.mat(c.m, c.m, "rands+n"), B = c.mat(c.m, c.n);
+    const bool left = c.P.side == Side::Left;
+    const int64_t an = left ? c.m : c.n;
+    auto Tg = c.mat(an, an, "rands+n"), B = c.mat(c.m, c.n);
     auto B0 = c.copy_of(B);
-    TriangularMatrix<T> U(Uplo::Upper, Diag::NonUnit, Tg);
+    TriangularMatrix<T> A0(c.P.uplo, c.P.diag, Tg);
+    auto A = op_tri(c.P.trans, A0);
     Result r;
-    r.time = c.timed([&] { trmm(Side::Left, T(1), U, B, c.opts); });
-    r.flops = cfac<T>() * double(c.m) * c.m * c.n;
+    r.time = c.timed([&] { trmm(c.P.side, T(1), A, B, c.opts); });
+    r.flops = cfac<T>() * double(an) * an * (left ? c.n : c.m);
     if (c.P.check) {
-        auto X = c.copy_of(B);
-        trsm(Side::Left, T(1), U, X, c.opts);           // U^{-1} (U B0) = B0
-        add(T(-1), B0, T(1), X, c.opts);
-        r.error = c.nrm(X) / (c.nrm(B0) * double(c.m));
+        // forward check against a dense copy of the triangle: op(D) B0 or B0 op(D)
+        // (a trsm back-substitution would be ill-conditioned for unit diagonals)
+        auto D = c.zeros(an, an);
+        BaseTrapezoidMatrix<T> Ts(c.P.uplo, Tg, MatrixKind::Trapezoid), Ds(c.P.uplo, D, MatrixKind::Trapezoid);
+        copy<T, T>(Ts, Ds, c.opts);
+        if (c.P.diag == Diag::Unit) {
+            auto Dd = dense_diag(c, D);
+            add(T(-1), Dd, T(1), D, c.opts);
+            auto I = c.zeros(an, an);
+            set(T(0), T(1), I, c.opts);
+            add(T(1), I, T(1), D, c.opts);
+        }
+        Matrix<T> opD = c.P.trans == Op::Trans ? transpose(D) : (c.P.trans == Op::ConjTrans ? conj_transpose(D) : D);
+        if (left) gemm(T(-1), opD, B0, T(1), B, c.opts);
+        else gemm(T(-1), B0, opD, T(1), B, c.opts);
+        r.error = c.nrm(B) / (c.nrm(D) * c.nrm(B0) * double(an));
     }
     return r;
 }
@@ -342,8 +417,8 @@ Result r_gesv_mixed_v(Case<T>& c, int variant) {
     if constexpr (!std::is_same_v<T, double> && !std::is_same_v<T, std::complex<double>>) {
         Result r; r.skipped = true; r.note = "double precisions only"; return r;
     } else {
-        const int64_t nrhs = variant == 1 ? 1 : c.P.nrhs;   // GMRES-IR: one right-hand side
-        auto A = c.mat(c.n, c.n, variant == 2 ? "spd" : "rands+n"), B = c.mat(c.n, nrhs);
+        const int64_t nrhs = (variant == 1 || variant == 3) ? 1 : c.P.nrhs;   // GMRES-IR: one right-hand side
+        auto A = c.mat(c.n, c.n, variant >= 2 ? "spd" : "rands+n"), B = c.mat(c.n, nrhs);
         auto A0 = c.copy_of(A), X = c.zeros(c.n, nrhs);
         Result r;
         int64_t info = 0;
@@ -354,10 +429,10 @@ Result r_gesv_mixed_v(Case<T>& c, int variant) {
             else if (variant == 1) info = gesv_mixed_gmres(A, piv, B, X, iter, c.opts);
             else {
                 HermitianMatrix<T> H(Uplo::Lower, A);
-                info = posv_mixed(H, B, X, iter, c.opts);
+                info = variant == 2 ? posv_mixed(H, B, X, iter, c.opts) : posv_mixed_gmres(H, B, X, iter, c.opts);
             }
         });
-        r.flops = variant == 2 ? potrf_fl<T>(c.n) : getrf_fl<T>(c.n);
+        r.flops = variant >= 2 ? potrf_fl<T>(c.n) : getrf_fl<T>(c.n);
         r.note = "iter=" + std::to_string(iter);
         if (info) { r.error = INFINITY; return r; }
         if (c.P.check) r.error = c.solve_resid(A0, X, B);
@@ -819,7 +894,7 @@ template <typename T>
 Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbtrs, 3 gbmm, 4 hbmm, 5 tbsm
     const int64_t kd = std::max<int64_t>(1, c.nb / 2);
     Result r;
-    if (variant == 1 || variant == 2 || variant == 4) {
+    if (variant == 1 || variant == 2 || variant == 4 || variant == 7) {
         auto Ag = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
         // Hermitian band with a dominant diagonal: H = band(A + A^H) + 4 kd I
         auto F = c.zeros(c.n, c.n);
@@ -850,6 +925,14 @@ Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbt
             return r;
         }
         int64_t info = 0;
+        if (variant == 7) {
+            info = pbtrf(H, c.opts);
+            if (info) { r.error = INFINITY; return r; }
+            r.time = c.timed([&] { pbtrs(H, B, c.opts); });
+            r.flops = cfac<T>() * 4.0 * c.n * kd * c.P.nrhs;
+            if (c.P.check) r.error = c.solve_resid(Fz, B, B0);
+            return r;
+        }
         r.time = c.timed([&] {
             if (variant == 1) info = pbsv(H, B, c.opts);
             else { info = pbtrf(H, c.opts); if (!info) pbtrs(H, B, c.opts); }
@@ -892,8 +975,16 @@ Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbt
         return r;
     }
     int64_t info = 0;
-    r.time = c.timed([&] { Pivots piv; info = gbtrf(A, piv, c.opts); if (!info) gbtrs(A, piv, B, c.opts); });
-    r.flops = cfac<T>() * 2.0 * c.n * kd * (1.5 * kd + 1);
+    if (variant == 6) {
+        Pivots piv;
+        info = gbtrf(A, piv, c.opts);
+        if (info) { r.error = INFINITY; return r; }
+        r.time = c.timed([&] { gbtrs(A, piv, B, c.opts); });
+        r.flops = cfac<T>() * 2.0 * c.n * (2.5 * kd + 1) * c.P.nrhs;
+    } else {
+        r.time = c.timed([&] { Pivots piv; info = gbtrf(A, piv, c.opts); if (!info) gbtrs(A, piv, B, c.opts); });
+    }
+    if (variant != 6) r.flops = cfac<T>() * 2.0 * c.n * kd * (1.5 * kd + 1);
     if (info) { r.error = INFINITY; return r; }
     if (c.P.check) {
         auto Rm = c.copy_of(B0);
@@ -1133,6 +1224,425 @@ Result r_aux(Case<T>& c, int variant) {   // 0 add, 1 copy, 2 scale, 3 set, 4 tr
     return r;
 }
 
+//------------------------------------------------------------------------------
+// Breadth 2: stage-level eigen / SVD routines, the remaining solve variants,
+// band / symmetric / triangular norms, trapezoid aux variants, sy* solvers.
+
+/// dense copy of a Hermitian band (lower, kd) through hbmm with the identity
+template <typename T>
+Matrix<T> dense_hband(Case<T>& c, HermitianBandMatrix<T> const& H) {
+    auto I = c.zeros(H.n(), H.n()), F = c.zeros(H.n(), H.n());
+    set(T(0), T(1), I, c.opts);
+    hbmm(Side::Left, T(1), H, I, T(0), F, c.opts);
+    return F;
+}
+
+/// dense copy of a general band through gbmm with the identity
+template <typename T>
+Matrix<T> dense_band(Case<T>& c, BandMatrix<T> const& B) {
+    auto I = c.zeros(B.n(), B.n()), F = c.zeros(B.m(), B.n());
+    set(T(0), T(1), I, c.opts);
+    gbmm(T(1), B, I, T(0), F, c.opts);
+    return F;
+}
+
+/// Hermitian test matrix (A + A^H) / 2 from the main operand
+template <typename T>
+Matrix<T> herm_of(Case<T>& c, int64_t n) {
+    auto Ag = c.mat(n, n, "rands", -1, true);
+    auto H = c.zeros(n, n);
+    copy<T, T>(conj_transpose(Ag), H, c.opts);
+    add(T(0.5), Ag, T(0.5), H, c.opts);
+    return H;
+}
+
+template <typename T>
+Result r_he2hb(Case<T>& c, int variant) {   // 0 he2hb (A = Q B Q^H), 1 unmtr_he2hb (Q (Q^H C) = C)
+    auto A = herm_of(c, c.n);
+    auto A0 = c.copy_of(A);
+    std::vector<TriangularFactors<T>> Ts;
+    Result r;
+    const double n = double(c.n);
+    if (variant == 0) {
+        r.time = c.timed([&] { he2hb(A, Ts, c.opts); });
+        r.flops = cfac<T>() * 4.0 / 3 * n * n * n;
+        if (c.P.check) {
+            HermitianBandMatrix<T> Hb(Uplo::Lower, c.nb, A);
+            auto F = dense_hband(c, Hb);
+            unmtr_he2hb(Side::Left, Op::NoTrans, A, Ts, F, c.opts);
+            unmtr_he2hb(Side::Right, Op::ConjTrans, A, Ts, F, c.opts);
+            add(T(-1), A0, T(1), F, c.opts);
+            r.error = c.nrm(F) / (n * c.nrm(A0));
+        }
+        return r;
+    }
+    he2hb(A, Ts, c.opts);
+    auto C = c.mat(c.n, c.P.nrhs);
+    auto C0 = c.copy_of(C);
+    r.time = c.timed([&] { unmtr_he2hb(Side::Left, Op::ConjTrans, A, Ts, C, c.opts); });
+    r.flops = cfac<T>() * 2.0 * n * n * c.P.nrhs;
+    if (c.P.check) {
+        unmtr_he2hb(Side::Left, Op::NoTrans, A, Ts, C, c.opts);
+        add(T(-1), C0, T(1), C, c.opts);
+        r.error = c.nrm(C) / (n * c.nrm(C0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_hb2st(Case<T>& c, int variant) {   // 0 hb2st (Frobenius norm preserved), 1 unmtr_hb2st
+    using R = R_<T>;
+    auto A = herm_of(c, c.n);
+    const int64_t kd = std::max<int64_t>(1, c.nb / 2);
+    HermitianBandMatrix<T> Hb(Uplo::Lower, kd, A);
+    std::vector<R> d, e;
+    BandReflectors<T> V;
+    Result r;
+    const double n = double(c.n);
+    if (variant == 0) {
+        r.time = c.timed([&] { hb2st(Hb, d, e, V, c.opts); });
+        r.flops = cfac<T>() * 6.0 * n * n * kd;
+        if (c.P.check) {
+            // orthogonal similarity: ||band||_F^2 = sum d^2 + 2 sum e^2
+            const double f = double(norm(Norm::Fro, dense_hband(c, Hb), c.opts));
+            double t = 0;
+            for (auto v : d) t += double(v) * double(v);
+            for (auto v : e) t += 2.0 * double(v) * double(v);
+            r.error = std::abs(t - f * f) / (f * f * n);
+        }
+        return r;
+    }
+    hb2st(Hb, d, e, V, c.opts);
+    auto C = c.mat(c.n, c.P.nrhs);
+    auto C0 = c.copy_of(C);
+    r.time = c.timed([&] { unmtr_hb2st(Side::Left, Op::NoTrans, V, C, c.opts); });
+    r.flops = cfac<T>() * 2.0 * n * n * c.P.nrhs;
+    if (c.P.check) {
+        unmtr_hb2st(Side::Left, Op::ConjTrans, V, C, c.opts);
+        add(T(-1), C0, T(1), C, c.opts);
+        r.error = c.nrm(C) / (n * c.nrm(C0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_ge2tb(Case<T>& c) {   // A = U B V^H with B upper band of width nb
+    if (c.m < c.n) { Result r; r.skipped = true; r.note = "m >= n"; return r; }
+    auto A = c.mat(c.m, c.n, "rands", -1, true);
+    auto A0 = c.copy_of(A);
+    std::vector<TriangularFactors<T>> TU, TV;
+    Result r;
+    r.time = c.timed([&] { ge2tb(A, TU, TV, c.opts); });
+    r.flops = cfac<T>() * 4.0 * double(c.n) * c.n * (c.m - c.n / 3.0);
+    if (c.P.check) {
+        BandMatrix<T> Bb(0, c.nb, A);
+        auto F = dense_band(c, Bb);
+        unmbr_ge2tb(Side::Left, Op::NoTrans, A, TU, F, c.opts);
+        unmbr_ge2tb(Side::Right, Op::NoTrans, A, TV, F, c.opts);
+        add(T(-1), A0, T(1), F, c.opts);
+        r.error = c.nrm(F) / (double(c.m) * c.nrm(A0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_tb2bd(Case<T>& c, int variant) {   // 0 tb2bd (Frobenius preserved), 1 unmbr_tb2bd
+    using R = R_<T>;
+    auto A = c.mat(c.n, c.n, "rands", -1, true);
+    const int64_t kd = std::max<int64_t>(1, c.nb / 2);
+    TriangularBandMatrix<T> Tb(Uplo::Upper, Diag::NonUnit, kd, A);
+    std::vector<R> d, e;
+    BandReflectors<T> U, V;
+    Result r;
+    const double n = double(c.n);
+    if (variant == 0) {
+        r.time = c.timed([&] { tb2bd(Tb, d, e, U, V, c.opts); });
+        r.flops = cfac<T>() * 8.0 * n * n * kd;
+        if (c.P.check) {
+            BandMatrix<T> Bb(0, kd, A);
+            const double f = double(norm(Norm::Fro, dense_band(c, Bb), c.opts));
+            double t = 0;
+            for (auto v : d) t += double(v) * double(v);
+            for (auto v : e) t += double(v) * double(v);
+            r.error = std::abs(t - f * f) / (f * f * n);
+        }
+        return r;
+    }
+    tb2bd(Tb, d, e, U, V, c.opts);
+    auto C = c.mat(c.n, c.P.nrhs);
+    auto C0 = c.copy_of(C);
+    r.time = c.timed([&] { unmbr_tb2bd(Side::Left, Op::NoTrans, U, C, c.opts); });
+    r.flops = cfac<T>() * 2.0 * n * n * c.P.nrhs;
+    if (c.P.check) {
+        unmbr_tb2bd(Side::Left, Op::ConjTrans, U, C, c.opts);
+        add(T(-1), C0, T(1), C, c.opts);
+        r.error = c.nrm(C) / (n * c.nrm(C0));
+    }
+    return r;
+}
+
+/// the test tridiagonal / bidiagonal of the stage tests
+template <typename R>
+void test_tridiag(int64_t n, std::vector<R>& d, std::vector<R>& e) {
+    d.resize(n);
+    e.assign(std::max<int64_t>(n - 1, 0), R(0));
+    for (int64_t i = 0; i < n; ++i) d[i] = R(2) + R(i % 7) / R(10);
+    for (int64_t i = 0; i + 1 < n; ++i) e[i] = R(-1) + R(i % 5) / R(20);
+}
+
+template <typename T>
+Result r_bdsqr(Case<T>& c) {   // B = U diag(s) VT for an upper bidiagonal B
+    using R = R_<T>;
+    const int64_t n = c.n;
+    std::vector<R> d, e;
+    test_tridiag(n, d, e);
+    auto d0 = d;
+    auto e0 = e;
+    auto U = c.zeros(n, n), VT = c.zeros(n, n);
+    set(T(0), T(1), U, c.opts);
+    set(T(0), T(1), VT, c.opts);
+    Result r;
+    r.time = c.timed([&] { bdsqr(Job::Vec, Job::Vec, d, e, U, VT, c.opts); });
+    r.flops = 12.0 * double(n) * n * n;
+    if (c.P.check) {
+        auto Bm = c.zeros(n, n);
+        std::function<T(int64_t, int64_t)> bv = [&](int64_t i, int64_t j) -> T {
+            if (i == j) return T(d0[i]);
+            if (j == i + 1) return T(e0[i]);
+            return T(0);
+        };
+        set(bv, Bm, c.opts);
+        std::vector<R> ones(n, R(1));
+        auto US = c.copy_of(U);
+        scale_row_col(Equed::Col, ones, d, US, c.opts);
+        gemm(T(1), US, VT, T(-1), Bm, c.opts);
+        r.error = c.nrm(Bm) / (double(n) * 4.0);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_stedc(Case<T>& c) {   // T Q = Q diag(lambda), Q distributed
+    using R = R_<T>;
+    if constexpr (is_complex_v<T>) {
+        Result r; r.skipped = true; r.note = "real types (stedc works on R)"; return r;
+    } else {
+        const int64_t n = c.n;
+        std::vector<R> d, e;
+        test_tridiag(n, d, e);
+        auto d0 = d;
+        auto e0 = e;
+        auto Q = c.zeros(n, n);
+        Result r;
+        r.time = c.timed([&] { stedc(d, e, Q, c.opts); });
+        r.flops = 4.0 / 3 * double(n) * n * n;
+        if (c.P.check) {
+            auto Tm = c.zeros(n, n);
+            std::function<T(int64_t, int64_t)> tv = [&](int64_t i, int64_t j) -> T {
+                if (i == j) return T(d0[i]);
+                if (i == j + 1) return T(e0[j]);
+                if (j == i + 1) return T(e0[i]);
+                return T(0);
+            };
+            set(tv, Tm, c.opts);
+            auto TQ = c.zeros(n, n), QL = c.copy_of(Q);
+            gemm(T(1), Tm, Q, T(0), TQ, c.opts);
+            std::vector<R> ones(n, R(1));
+            scale_row_col(Equed::Col, ones, d, QL, c.opts);
+            add(T(-1), QL, T(1), TQ, c.opts);
+            r.error = c.nrm(TQ) / (double(n) * c.nrm(Tm));
+        }
+        return r;
+    }
+}
+
+template <typename T>
+Result r_hegst(Case<T>& c) {   // itype 1: C = L^{-1} A L^{-H}; check L C L^H = A
+    auto A = herm_of(c, c.n);
+    auto A0 = c.copy_of(A);
+    auto Bg = c.mat(c.n, c.n, "spd");
+    HermitianMatrix<T> Bh(Uplo::Lower, Bg);
+    if (potrf(Bh, c.opts)) { Result r; r.error = INFINITY; return r; }
+    HermitianMatrix<T> Ah(Uplo::Lower, A);
+    Result r;
+    r.time = c.timed([&] { hegst(1, Ah, Bh, c.opts); });
+    r.flops = cfac<T>() * double(c.n) * c.n * c.n;
+    if (c.P.check) {
+        BaseTrapezoidMatrix<T> As(Uplo::Lower, A, MatrixKind::Trapezoid);
+        auto F = full_of(c, As, true);
+        TriangularMatrix<T> L(Uplo::Lower, Diag::NonUnit, Bg);
+        trmm(Side::Left, T(1), L, F, c.opts);
+        trmm(Side::Right, T(1), conj_transpose(L), F, c.opts);
+        add(T(-1), A0, T(1), F, c.opts);
+        r.error = c.nrm(F) / (double(c.n) * c.nrm(A0));
+    }
+    return r;
+}
+
+template <typename T>
+Result r_getrs_v(Case<T>& c, int variant) {   // 0 getrs_nopiv, 1 getrs after tournament pivoting
+    auto A = c.mat(c.n, c.n, variant == 0 ? "rands+n" : "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+    auto A0 = c.copy_of(A), B0 = c.copy_of(B);
+    Result r;
+    Pivots piv;
+    int64_t info = 0;
+    if (variant == 0) info = getrf_nopiv(A, c.opts);
+    else {
+        Options o = c.opts;
+        o[Option::MethodLU] = int64_t(MethodLU::CALU);
+        info = getrf(A, piv, o);
+    }
+    if (info) { r.error = INFINITY; return r; }
+    r.time = c.timed([&] {
+        if (variant == 0) getrs_nopiv(A, B, c.opts);
+        else getrs(A, piv, B, c.opts);
+    });
+    r.flops = cfac<T>() * 2.0 * c.n * c.n * c.P.nrhs;
+    if (c.P.check) r.error = c.solve_resid(A0, B, B0);
+    return r;
+}
+
+template <typename T>
+Result r_scale_row_col(Case<T>& c) {
+    using R = R_<T>;
+    auto A = c.mat(c.m, c.n, "rands", -1, true);
+    auto A0 = c.copy_of(A);
+    std::vector<R> rs(c.m), cs(c.n), ri(c.m), ci(c.n);
+    for (int64_t i = 0; i < c.m; ++i) { rs[i] = R(1) + R(i % 5) / R(4); ri[i] = R(1) / rs[i]; }
+    for (int64_t j = 0; j < c.n; ++j) { cs[j] = R(2) - R(j % 3) / R(4); ci[j] = R(1) / cs[j]; }
+    Result r;
+    r.time = c.timed([&] { scale_row_col(Equed::Both, rs, cs, A, c.opts); });
+    r.flops = 2.0 * double(c.m) * c.n;
+    if (c.P.check) {
+        scale_row_col(Equed::Both, ri, ci, A, c.opts);
+        add(T(-1), A0, T(1), A, c.opts);
+        r.error = c.nrm(A) / c.nrm(A0);
+    }
+    return r;
+}
+
+template <typename T>
+Result r_norm_kind(Case<T>& c, int kind) {   // 0 gbnorm, 1 hbnorm, 2 synorm, 3 trnorm
+    auto Ag = c.mat(c.n, c.n, "rands", -1, true);
+    const int64_t kd = std::max<int64_t>(1, c.nb / 2);
+    Result r;
+    r.flops = double(c.n) * c.n;
+    const Norm nt = Norm::One;
+    R_<T> v = 0;
+    double ref = 0;
+    if (kind == 0) {
+        BandMatrix<T> B(kd, kd / 2 + 1, Ag);
+        r.time = c.timed([&] { v = norm(nt, B, c.opts); });
+        if (c.P.check) ref = c.nrm(dense_band(c, B));
+    } else if (kind == 1) {
+        HermitianBandMatrix<T> H(Uplo::Lower, kd, Ag);
+        r.time = c.timed([&] { v = norm(nt, H, c.opts); });
+        if (c.P.check) {
+            // lanhb reads only the real part of the diagonal
+            auto F = dense_hband(c, H), Ft = c.zeros(c.n, c.n);
+            copy<T, T>(conj_transpose(F), Ft, c.opts);
+            add(T(0.5), Ft, T(0.5), F, c.opts);
+            ref = c.nrm(F);
+        }
+    } else if (kind == 2) {
+        SymmetricMatrix<T> S(c.P.uplo, Ag);
+        r.time = c.timed([&] { v = norm(nt, S, c.opts); });
+        if (c.P.check) {
+            BaseTrapezoidMatrix<T> Ss(c.P.uplo, Ag, MatrixKind::Trapezoid);
+            ref = c.nrm(full_of(c, Ss, false));
+        }
+    } else {
+        TriangularMatrix<T> Tm(c.P.uplo, c.P.diag, Ag);
+        r.time = c.timed([&] { v = norm(nt, Tm, c.opts); });
+        if (c.P.check) {
+            auto D = c.zeros(c.n, c.n);
+            BaseTrapezoidMatrix<T> Ls(c.P.uplo, Ag, MatrixKind::Trapezoid), Ds(c.P.uplo, D, MatrixKind::Trapezoid);
+            copy<T, T>(Ls, Ds, c.opts);
+            if (c.P.diag == Diag::Unit) {
+                // unit diagonal: D - diag(D) + I
+                auto Dd = dense_diag(c, D);
+                add(T(-1), Dd, T(1), D, c.opts);
+                auto I = c.zeros(c.n, c.n);
+                set(T(0), T(1), I, c.opts);
+                add(T(1), I, T(1), D, c.opts);
+            }
+            ref = c.nrm(D);
+        }
+    }
+    if (c.P.check) r.error = std::abs(double(v) - ref) / std::max(ref, 1e-300);
+    return r;
+}
+
+/// trapezoid aux variants on the --uplo triangle: 0 set, 1 copy, 2 scale, 3 add;
+/// kind: the view type name (tz / tr / sy / he) only selects the wrapper.
+template <typename T>
+Result r_tzaux(Case<T>& c, int op) {
+    auto A = c.mat(c.m, c.n, "rands", -1, true), B = c.mat(c.m, c.n);
+    std::vector<T> a0, b0;
+    gather(A, a0, c.opts);
+    gather(B, b0, c.opts);
+    const Uplo u = c.P.uplo;
+    BaseTrapezoidMatrix<T> At(u, A, MatrixKind::Trapezoid), Bt(u, B, MatrixKind::Trapezoid);
+    Result r;
+    r.flops = double(c.m) * c.n / 2;
+    const T off(0.25), dg(3), al(2), be(-1);
+    r.time = c.timed([&] {
+        if (op == 0) set(off, dg, Bt, c.opts);
+        else if (op == 1) copy<T, T>(At, Bt, c.opts);
+        else if (op == 2) scale(R_<T>(3), R_<T>(2), Bt, c.opts);
+        else add(al, At, be, Bt, c.opts);
+    });
+    if (c.P.check) {
+        std::vector<T> b1;
+        gather(B, b1, c.opts);
+        double err = 0, mx = 1e-300;
+        for (int64_t j = 0; j < c.n; ++j)
+            for (int64_t i = 0; i < c.m; ++i) {
+                const size_t x = size_t(i) + size_t(j) * c.m;
+                const bool in = u == Uplo::Lower ? i >= j : i <= j;
+                T want = b0[x];
+                if (in) {
+                    if (op == 0) want = i == j ? dg : off;
+                    else if (op == 1) want = a0[x];
+                    else if (op == 2) want = b0[x] * T(1.5);
+                    else want = al * a0[x] + be * b0[x];
+                }
+                err = std::max(err, double(std::abs(b1[x] - want)));
+                mx = std::max(mx, double(std::abs(want)));
+            }
+        r.error = err / mx;
+    }
+    return r;
+}
+
+template <typename T>
+Result r_sy(Case<T>& c, int variant) {   // 0 sysv, 1 sytrf (+ sytrs for the check), 2 sytrs
+    if constexpr (is_complex_v<T>) {
+        Result r; r.skipped = true; r.note = "real types (use hesv/hetrf)"; return r;
+    } else {
+        auto S0 = herm_of(c, c.n);
+        auto Sg = c.copy_of(S0), B = c.mat(c.n, c.P.nrhs);
+        auto B0 = c.copy_of(B);
+        SymmetricMatrix<T> S(Uplo::Lower, Sg);
+        std::vector<int64_t> ipiv;
+        Result r;
+        int64_t info = 0;
+        r.flops = double(c.n) * c.n * c.n / 3;
+        if (variant == 0) r.time = c.timed([&] { info = sysv(S, ipiv, B, c.opts); });
+        else if (variant == 1) {
+            r.time = c.timed([&] { info = sytrf(S, ipiv, c.opts); });
+            if (!info) sytrs(S, ipiv, B, c.opts);
+        } else {
+            info = sytrf(S, ipiv, c.opts);
+            if (!info) r.time = c.timed([&] { sytrs(S, ipiv, B, c.opts); });
+            r.flops = 2.0 * double(c.n) * c.n * c.P.nrhs;
+        }
+        if (info) { r.error = INFINITY; return r; }
+        if (c.P.check) r.error = c.solve_resid(S0, B, B0);
+        return r;
+    }
+}
+
 template <typename T>
 using Fn = std::function<Result(Case<T>&)>;
 
@@ -1190,6 +1700,45 @@ std::map<std::string, Fn<T>> routines() {
         {"colnorms", [](Case<T>& c) { return r_aux<T>(c, 5); }},
         {"henorm", [](Case<T>& c) { return r_aux<T>(c, 6); }},
         {"redistribute", [](Case<T>& c) { return r_aux<T>(c, 7); }},
+        {"he2hb", [](Case<T>& c) { return r_he2hb<T>(c, 0); }},
+        {"unmtr_he2hb", [](Case<T>& c) { return r_he2hb<T>(c, 1); }},
+        {"hb2st", [](Case<T>& c) { return r_hb2st<T>(c, 0); }},
+        {"unmtr_hb2st", [](Case<T>& c) { return r_hb2st<T>(c, 1); }},
+        {"ge2tb", r_ge2tb<T>},
+        {"tb2bd", [](Case<T>& c) { return r_tb2bd<T>(c, 0); }},
+        {"unmbr_tb2bd", [](Case<T>& c) { return r_tb2bd<T>(c, 1); }},
+        {"bdsqr", r_bdsqr<T>},
+        {"stedc", r_stedc<T>},
+        {"hegst", r_hegst<T>},
+        {"getrs_nopiv", [](Case<T>& c) { return r_getrs_v<T>(c, 0); }},
+        {"getrs_tntpiv", [](Case<T>& c) { return r_getrs_v<T>(c, 1); }},
+        {"posv_mixed_gmres", [](Case<T>& c) { return r_gesv_mixed_v<T>(c, 3); }},
+        {"gbtrs", [](Case<T>& c) { return r_band<T>(c, 6); }},
+        {"pbtrs", [](Case<T>& c) { return r_band<T>(c, 7); }},
+        {"scale_row_col", r_scale_row_col<T>},
+        {"gbnorm", [](Case<T>& c) { return r_norm_kind<T>(c, 0); }},
+        {"hbnorm", [](Case<T>& c) { return r_norm_kind<T>(c, 1); }},
+        {"synorm", [](Case<T>& c) { return r_norm_kind<T>(c, 2); }},
+        {"trnorm", [](Case<T>& c) { return r_norm_kind<T>(c, 3); }},
+        {"tzset", [](Case<T>& c) { return r_tzaux<T>(c, 0); }},
+        {"tzcopy", [](Case<T>& c) { return r_tzaux<T>(c, 1); }},
+        {"tzscale", [](Case<T>& c) { return r_tzaux<T>(c, 2); }},
+        {"tzadd", [](Case<T>& c) { return r_tzaux<T>(c, 3); }},
+        {"trset", [](Case<T>& c) { return r_tzaux<T>(c, 0); }},
+        {"trcopy", [](Case<T>& c) { return r_tzaux<T>(c, 1); }},
+        {"trscale", [](Case<T>& c) { return r_tzaux<T>(c, 2); }},
+        {"tradd", [](Case<T>& c) { return r_tzaux<T>(c, 3); }},
+        {"syset", [](Case<T>& c) { return r_tzaux<T>(c, 0); }},
+        {"sycopy", [](Case<T>& c) { return r_tzaux<T>(c, 1); }},
+        {"syscale", [](Case<T>& c) { return r_tzaux<T>(c, 2); }},
+        {"syadd", [](Case<T>& c) { return r_tzaux<T>(c, 3); }},
+        {"heset", [](Case<T>& c) { return r_tzaux<T>(c, 0); }},
+        {"hecopy", [](Case<T>& c) { return r_tzaux<T>(c, 1); }},
+        {"hescale", [](Case<T>& c) { return r_tzaux<T>(c, 2); }},
+        {"headd", [](Case<T>& c) { return r_tzaux<T>(c, 3); }},
+        {"sysv", [](Case<T>& c) { return r_sy<T>(c, 0); }},
+        {"sytrf", [](Case<T>& c) { return r_sy<T>(c, 1); }},
+        {"sytrs", [](Case<T>& c) { return r_sy<T>(c, 2); }},
     };
 }
 
@@ -1231,7 +1780,8 @@ int run_type(Params const& P, char tc, std::string const& name) {
                     double gf = (r.time > 0 && r.flops > 0) ? r.flops / r.time / 1e9 : NAN;
                     std::printf("%-16s %-4c %7lld %7lld %7lld %5lld %2d %2d %s %10.4f %11.2f  %s%s%s\n", name.c_str(), tc,
                                 (long long)c.m, (long long)c.n, (long long)c.k, (long long)nb, g->p(), g->q(), es,
-                                r.time, gf, status.c_str(), r.note.empty() ? "" : "  ", r.note.c_str());
+                                r.time, gf, status.c_str(), (r.note.empty() || r.skipped) ? "" : "  ",
+                                r.skipped ? "" : r.note.c_str());
                     std::fflush(stdout);
                 }
                 if (P.timer_level >= 2) {
@@ -1255,6 +1805,8 @@ void usage() {
         "       [--matrix KIND] [--method-lu ppiv|calu|nopiv] [--method-trsm auto|A|B]\n"
         "       [--method-gemm auto|A|C] [--method-hemm auto|A|C] [--origin h|d]\n"
         "       [--timer-level 1|2] [--itermax N] [--fallback y|n] [--pivot-threshold X]\n"
+        "       [--uplo l|u] [--trans n|t|c] [--side l|r] [--diag n|u] [--cond C] [--ib IB]\n"
+        "       [--nonuniform-nb y|n] [--go c|r] [--do r|c]\n"
         "routines:");
     for (auto const& kv : routines<double>()) std::printf(" %s", kv.first.c_str());
     std::printf("\n");
@@ -1297,11 +1849,23 @@ int main(int argc, char** argv) {
         else if (a == "--itermax") P.itermax = std::stoll(val());
         else if (a == "--fallback") P.fallback = val()[0] == 'y' ? 1 : 0;
         else if (a == "--pivot-threshold") P.pivot_threshold = std::stod(val());
+        else if (a == "--uplo") { char v = char(std::tolower(val()[0])); P.uplo = v == 'u' ? Uplo::Upper : Uplo::Lower; }
+        else if (a == "--trans") {
+            char v = char(std::tolower(val()[0]));
+            P.trans = v == 't' ? Op::Trans : (v == 'c' ? Op::ConjTrans : Op::NoTrans);
+        }
+        else if (a == "--side") P.side = char(std::tolower(val()[0])) == 'r' ? Side::Right : Side::Left;
+        else if (a == "--diag") P.diag = char(std::tolower(val()[0])) == 'u' ? Diag::Unit : Diag::NonUnit;
+        else if (a == "--cond") P.cond = std::stod(val());
+        else if (a == "--ib") P.ib = std::stoll(val());
+        else if (a == "--nonuniform-nb") P.nonuniform = val()[0] == 'y';
+        else if (a == "--go") P.order = char(std::tolower(val()[0])) == 'r' ? GridOrder::Row : GridOrder::Col;
+        else if (a == "--do") P.dev_order = char(std::tolower(val()[0]));
         else if (!a.empty() && a[0] != '-') rlist = rlist.empty() ? a : rlist + "," + a;
         else { usage(); return 2; }
     }
     if (rlist.empty()) { usage(); return 2; }
-    init_grid(P.p, P.q);
+    init_grid(P.p, P.q, P.order);
     if (rlist == "all") {
         rlist.clear();
         for (auto const& kv : routines<double>()) rlist += (rlist.empty() ? "" : ",") + kv.first;

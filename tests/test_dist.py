@@ -98,3 +98,17 @@ def test_rccl_lu_qr_p_gt_1(nprocs, grid, la, routines):
                         "--nb", "128", "--grid", grid, "--target", "d", "--lookahead", la],
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("la,routines", [("1", "getrf,getrf_tntpiv,gesv,geqrf,gels,potrf"), ("2", "getrf_tntpiv,geqrf")])
+def test_rccl_2x4_n4096(la, routines):
+    """Eight ranks on a 2 x 4 grid over real RCCL (all sharing one GPU, so the
+    rig exercises the schedule and the fast/bulk communication lanes, not
+    speed): n = 4096 with nb = 256 (16 panels, every grid row and column owns
+    several), lookahead 1 and 2, residual checks of the tester."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), "8",
+                        routines, "--type", "d", "--dim", "4096", "--nb", "256", "--grid", "2x4",
+                        "--target", "d", "--lookahead", la],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]

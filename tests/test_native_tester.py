@@ -41,7 +41,7 @@ def launch(args, nprocs=1, timeout=600, target="h"):
 def test_all_routines_single_process():
     codes, outs = launch(["all", "--type", "d,z", "--dim", "200", "--nb", "48"])
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
-    assert outs[0].count("pass") >= 110       # ~62 routines x 2 types
+    assert outs[0].count("pass") >= 180       # ~100 routines x 2 types (real-only ones skip for z)
 
 
 @pytest.mark.parametrize("nprocs,grid", [(2, "1x2"), (4, "2x2")])
@@ -74,6 +74,37 @@ def test_tester_flags():
                           "--timer-level", "2", "--pivot-threshold", "0.5"])
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
     assert "#   getrf" in outs[0]
+
+
+def test_breadth2_distributed_2x2():
+    """Stage-level eigen/SVD routines, the remaining solve variants, band /
+    symmetric / triangular norms, trapezoid aux variants and sy* solvers on a
+    2x2 grid (reference test/test.cc routine list)."""
+    codes, outs = launch(["he2hb,unmtr_he2hb,hb2st,unmtr_hb2st,ge2tb,tb2bd,unmbr_tb2bd,bdsqr,stedc,hegst,"
+                          "getrs_nopiv,getrs_tntpiv,posv_mixed_gmres,gbtrs,pbtrs,scale_row_col,gbnorm,hbnorm,synorm,"
+                          "trnorm,tzset,tzcopy,tzscale,tzadd,sysv,sytrf,sytrs",
+                          "--type", "d,z", "--dim", "150,140x110x110", "--nb", "32", "--grid", "2x2"], 4)
+    assert codes == [0] * 4 and "all tests passed" in outs[0], "\n".join(o[-2500:] for o in outs)
+
+
+@pytest.mark.parametrize("flags", [["--side", "r", "--trans", "c", "--uplo", "u", "--diag", "u"],
+                                   ["--side", "l", "--trans", "t", "--uplo", "u"]])
+def test_shape_flags(flags):
+    """--side / --trans / --uplo / --diag on the triangular routines and norms."""
+    codes, outs = launch(["trsm,trmm,trnorm,synorm,tzset,tzadd", "--type", "d,z", "--dim", "130x90x90", "--nb", "32"]
+                         + flags)
+    assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
+
+
+def test_nonuniform_and_grid_order():
+    """--nonuniform-nb y (alternating nb, nb/2+1 tiles on a 2-D cyclic map:
+    the drivers' arbitrary-layout path), --go r (row-major process grid),
+    --cond with a spectral --matrix, --ib."""
+    codes, outs = launch(["getrf,gesv,geqrf,gels,heev", "--type", "d", "--dim", "170x130x130,160", "--nb", "32",
+                          "--grid", "1x2", "--nonuniform-nb", "y", "--go", "r", "--ib", "16"], 2)
+    assert codes == [0, 0] and "all tests passed" in outs[0], "\n".join(o[-2500:] for o in outs)
+    codes, outs = launch(["gesv,getrf", "--type", "d", "--dim", "200", "--nb", "32", "--matrix", "svd", "--cond", "1e6"])
+    assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
 
 
 @pytest.mark.gpu
