@@ -12,6 +12,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <limits>
 #include <complex>
 #include <cstring>
 #include <vector>
@@ -323,11 +324,35 @@ void larfg(int64_t n, T& alpha, T* x, int64_t incx, T& tau) {
     R alphr = real(alpha), alphi = imag(alpha);
     if (xnorm == 0 && alphi == 0) { tau = T(0); return; }
     R beta = -std::copysign(std::hypot(std::hypot(alphr, alphi), xnorm), alphr);
+    // |beta| below the safe minimum (bulge chasing drives entries toward
+    // denormals): rescale x and alpha by 1/safmin until it is not, as LAPACK
+    // larfg does, so 1 / (alpha - beta) cannot overflow
+    const R safmin = std::numeric_limits<R>::min() / std::numeric_limits<R>::epsilon();
+    int knt = 0;
+    if (std::abs(beta) < safmin) {
+        const R rsafmn = R(1) / safmin;
+        do {
+            ++knt;
+            for (int64_t i = 0; i < n - 1; ++i) x[i * incx] *= rsafmn;
+            beta *= rsafmn;
+            alpha *= rsafmn;
+        } while (std::abs(beta) < safmin && knt < 20);
+        scale = 0; ssq = 1;
+        for (int64_t i = 0; i < n - 1; ++i) {
+            R a = std::abs(x[i * incx]);
+            if (a != 0) add_sumsq(scale, ssq, a);
+        }
+        xnorm = scale * std::sqrt(ssq);
+        alphr = real(alpha);
+        alphi = imag(alpha);
+        beta = -std::copysign(std::hypot(std::hypot(alphr, alphi), xnorm), alphr);
+    }
     T t;
     if constexpr (is_complex_v<T>) t = T((beta - alphr) / beta, -alphi / beta);
     else t = T((beta - alphr) / beta);
     T scal = T(1) / (alpha - T(beta));
     for (int64_t i = 0; i < n - 1; ++i) x[i * incx] *= scal;
+    for (int k = 0; k < knt; ++k) beta *= safmin;
     tau = t;
     alpha = T(beta);
 }

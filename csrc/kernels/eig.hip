@@ -27,56 +27,83 @@ __global__ __launch_bounds__(256) void tinv_from_gram_kernel(int64_t k, T* G, in
     }
 }
 
-// ---- bdsqr rotations on the device.  Every row of M is independent; one
-// thread owns one row and walks the columns once per batch of K QR sweeps
-// with a register window of 2K columns: at step tau, sweep s applies its
-// rotation at column pair (j, j + 1), j = tau - 2 s.  Sweep s at j only needs
-// sweep s - 1 to be done with column j + 1, which happened at step tau - 1,
-// so the K rotations of one step touch disjoint pairs and are independent
-// (ILP instead of a K-long dependency chain).  Each column is read and
-// written once per batch instead of once per sweep.  D holds the rotations in
-// step order: D[2 (tau - p0) K + 2 s + {0, 1}] = (c, s) of sweep s at step
-// tau (identity where sweep s has no rotation), so a step reads 2K
-// consecutive reals (prefetched one step ahead).  [x y] <- [c x - s y,
-// s x + c y] on columns [p0, p1).
-template <typename T, typename R, int K>
-__global__ __launch_bounds__(64) void rot_sweeps_kernel(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1,
-                                                        const R* D) {
-    const int64_t r = blockIdx.x * 64 + threadIdx.x;
-    if (r >= rows) return;
-    T* row = M + r;
+// ---- bdsqr / steqr rotations on the device.  Every row of M is
+// independent; one thread owns one row and walks the columns once per batch
+// of K QR sweeps with a register window of 2K columns: at step tau, sweep s
+// applies its rotation at column pair (j, j + 1), j = tau - 2 s.  Sweep s at j
+// only needs sweep s - 1 to be done with column j + 1, which happened at step
+// tau - 1, so the K rotations of one step touch disjoint pairs and are
+// independent (ILP instead of a K-long dependency chain).  Each column is read
+// and written once per batch instead of once per sweep.  With only n rows
+// (n / 64 waves for the whole chip) a step cannot hide an HBM round trip
+// behind other waves, so the column a step needs is loaded PF steps ahead into
+// a register ring.  D holds the rotations in step order: D[2 (tau - p0) K +
+// 2 s + {0, 1}] = (c, s) of sweep s at step tau (identity where sweep s has no
+// rotation); the step's 2K reals are wave-uniform loads.
+// [x y] <- [c x - s y, s x + c y] on columns [p0, p1).
+template <typename T, typename R>
+struct RotJob {
+    int64_t rows;
+    T* M;
+    int64_t ld, p0, p1;
+    const R* D;
+};
+
+template <typename T, typename R, int K, int PF>
+__device__ inline void rot_sweeps_row(RotJob<T, R> const& J, int64_t r) {
+    T* row = J.M + r;
+    const int64_t ld = J.ld, p0 = J.p0, p1 = J.p1;
+    const R* D = J.D;
     T w[2 * K];
     #pragma unroll
     for (int i = 0; i < 2 * K; ++i) w[i] = T();
     w[2 * K - 2] = row[p0 * ld];
     w[2 * K - 1] = (p0 + 1 < p1) ? row[(p0 + 1) * ld] : T();
-    const int64_t tend = p1 - 2 + 2 * (K - 1);
-    R cs[2 * K], nx[2 * K];
+    T pf[PF];
     #pragma unroll
-    for (int i = 0; i < 2 * K; ++i) cs[i] = D[i];
-    for (int64_t tau = p0; tau <= tend; ++tau) {
-        const R* Dn = D + 2 * K * (tau + 1 - p0);
-        if (tau < tend) {
+    for (int i = 0; i < PF; ++i) {
+        const int64_t cpf = p0 + 2 + i;
+        pf[i] = cpf < p1 ? row[cpf * ld] : T();
+    }
+    const int64_t tend = p1 - 2 + 2 * (K - 1);
+    for (int64_t t0 = p0; t0 <= tend; t0 += PF) {
+        #pragma unroll
+        for (int u = 0; u < PF; ++u) {
+            const int64_t tau = t0 + u;
+            if (tau > tend) break;
+            const R* cs = D + 2 * K * (tau - p0);
             #pragma unroll
-            for (int i = 0; i < 2 * K; ++i) nx[i] = Dn[i];
+            for (int s = 0; s < K; ++s) {
+                const R c = cs[2 * s], sn = cs[2 * s + 1];
+                const T x = w[2 * K - 2 - 2 * s], y = w[2 * K - 1 - 2 * s];
+                w[2 * K - 2 - 2 * s] = x * c - y * sn;
+                w[2 * K - 1 - 2 * s] = x * sn + y * c;
+            }
+            const int64_t cr = tau - 2 * K + 2;
+            if (cr >= p0) row[cr * ld] = w[0];
+            #pragma unroll
+            for (int i = 0; i < 2 * K - 1; ++i) w[i] = w[i + 1];
+            w[2 * K - 1] = pf[u];                         // column tau + 2
+            const int64_t cn = tau + 2 + PF;
+            pf[u] = cn < p1 ? row[cn * ld] : T();
         }
-        #pragma unroll
-        for (int s = 0; s < K; ++s) {
-            const R c = cs[2 * s], sn = cs[2 * s + 1];
-            const T x = w[2 * K - 2 - 2 * s], y = w[2 * K - 1 - 2 * s];
-            w[2 * K - 2 - 2 * s] = x * c - y * sn;
-            w[2 * K - 1 - 2 * s] = x * sn + y * c;
-        }
-        const int64_t cr = tau - 2 * K + 2;
-        if (cr >= p0) row[cr * ld] = w[0];
-        #pragma unroll
-        for (int i = 0; i < 2 * K - 1; ++i) w[i] = w[i + 1];
-        const int64_t cn = tau + 2;
-        w[2 * K - 1] = (cn < p1) ? row[cn * ld] : T();
-        #pragma unroll
-        for (int i = 0; i < 2 * K; ++i) cs[i] = nx[i];
     }
     if (p1 - 1 >= p0) row[(p1 - 1) * ld] = w[0];
+}
+
+constexpr int kRotPrefetch = 16;
+
+// two independent jobs (U and Vt of bdsqr) in one launch: blocks [0, nblk_a)
+// take job a, the rest job b
+template <typename T, typename R, int K>
+__global__ __launch_bounds__(64) void rot_sweeps_kernel(RotJob<T, R> a, RotJob<T, R> b, int64_t nblk_a) {
+    const bool first = int64_t(blockIdx.x) < nblk_a;
+    const int64_t r = (first ? int64_t(blockIdx.x) : int64_t(blockIdx.x) - nblk_a) * 64 + threadIdx.x;
+    if (first) {
+        if (r < a.rows) rot_sweeps_row<T, R, K, kRotPrefetch>(a, r);
+    } else {
+        if (r < b.rows) rot_sweeps_row<T, R, K, kRotPrefetch>(b, r);
+    }
 }
 
 // one rotation on columns (a, b): [x y] <- [x c + y s, y c - x s]
@@ -94,9 +121,19 @@ __global__ __launch_bounds__(256) void rot_cols_kernel(int64_t rows, T* M, int64
 
 template <typename T>
 void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, const rt<T>* D, hipStream_t s) {
-    if (rows <= 0 || p1 - p0 < 2) return;
-    hipLaunchKernelGGL((rot_sweeps_kernel<T, rt<T>, kRotBatch>), dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s,
-                       rows, M, ld, p0, p1, D);
+    rot_sweeps2(rows, M, ld, p0, p1, D, int64_t(0), static_cast<T*>(nullptr), int64_t(1), int64_t(0), int64_t(0),
+                static_cast<const rt<T>*>(nullptr), s);
+}
+
+template <typename T>
+void rot_sweeps2(int64_t rows_a, T* A, int64_t lda, int64_t pa0, int64_t pa1, const rt<T>* Da, int64_t rows_b, T* B,
+                 int64_t ldb, int64_t pb0, int64_t pb1, const rt<T>* Db, hipStream_t s) {
+    const bool ua = rows_a > 0 && A && pa1 - pa0 >= 2, ub = rows_b > 0 && B && pb1 - pb0 >= 2;
+    if (!ua && !ub) return;
+    RotJob<T, rt<T>> ja{ua ? rows_a : 0, A, lda, pa0, pa1, Da}, jb{ub ? rows_b : 0, B, ldb, pb0, pb1, Db};
+    const int64_t na = (ja.rows + 63) / 64, nbk = (jb.rows + 63) / 64;
+    hipLaunchKernelGGL((rot_sweeps_kernel<T, rt<T>, kRotBatch>), dim3((unsigned)(na + nbk)), dim3(64), 0, s, ja, jb,
+                       na);
 }
 
 template <typename T>
@@ -116,6 +153,8 @@ void tinv_from_gram(int64_t k, T* G, int64_t ldg, const T* tau, hipStream_t s) {
 #define SLATE_INST_EIG(T)                                                                                          \
     template void tinv_from_gram<T>(int64_t, T*, int64_t, const T*, hipStream_t);                                 \
     template void rot_sweeps<T>(int64_t, T*, int64_t, int64_t, int64_t, const rt<T>*, hipStream_t);             \
+    template void rot_sweeps2<T>(int64_t, T*, int64_t, int64_t, int64_t, const rt<T>*, int64_t, T*, int64_t,     \
+                                 int64_t, int64_t, const rt<T>*, hipStream_t);                                  \
     template void rot_cols<T>(int64_t, T*, int64_t, int64_t, int64_t, rt<T>, rt<T>, hipStream_t);
 
 SLATE_INST_EIG(float)

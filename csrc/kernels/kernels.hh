@@ -122,6 +122,10 @@ constexpr int kRotBatch = 16;
 /// p0 .. p1 - 2 + 2 (kRotBatch - 1)).
 template <typename T>
 void rot_sweeps(int64_t rows, T* M, int64_t ld, int64_t p0, int64_t p1, const rt<T>* D, hipStream_t s);
+/// Two independent rot_sweeps jobs (bdsqr's U and Vt) in one launch.
+template <typename T>
+void rot_sweeps2(int64_t rows_a, T* A, int64_t lda, int64_t pa0, int64_t pa1, const rt<T>* Da, int64_t rows_b, T* B,
+                 int64_t ldb, int64_t pb0, int64_t pb1, const rt<T>* Db, hipStream_t s);
 /// One rotation on columns (a, b): [x y] <- [x c + y s, y c - x s].
 template <typename T>
 void rot_cols(int64_t rows, T* M, int64_t ld, int64_t a, int64_t b, rt<T> c, rt<T> sn, hipStream_t s);

@@ -390,6 +390,12 @@ void trsm_left_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> co
 /// op(A) = A^T / A^H the same algorithm runs on the transposed grid (B's
 /// rows follow A's columns) and the update reads op(A(k, i)) straight from
 /// the local array.
+///
+/// Lookahead 1: step k's update is split into the NEXT block row (k +- 1,
+/// panel queue, right after the broadcast) and the REST (trailing queue), so
+/// the reduce / solve / broadcast of step k+1 -- the latency chain -- runs
+/// while the rest of step k's update is still computing; the REST of step k
+/// only has to finish before step k+2's reduce.
 template <typename T>
 void trsmA_left(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B, Target target) {
     auto& g = *B.grid();
@@ -400,10 +406,16 @@ void trsmA_left(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& 
     const int64_t mt = B.mt(), n = B.n(), mloc = lbk.m, ldw = std::max<int64_t>(mloc, 1);
     Sched S(target);
     Work<T> W(target, size_t(ldw) * std::max<int64_t>(n, 1)), X(target, size_t(ldw) * std::max<int64_t>(n, 1));
-    Work<T> WX(target, size_t(B.mb()) * std::max<int64_t>(n, 1));
-    const int64_t tW = Sched::tok(9, 0), tX = Sched::tok(8, 0);
+    Work<T> WX[2];
+    for (auto& w : WX) w.resize(target, size_t(B.mb()) * std::max<int64_t>(n, 1));
+    constexpr int qP = 1, qT = 0;
+    // tokens: tI init; tS(k%2) step k's solved X(k) in WX; tN next-row update
+    // done; tR(k%2) step k's rest update done
+    const int64_t tI = Sched::tok(9, 0), tN = Sched::tok(9, 1);
+    auto tS = [](int64_t k) { return Sched::tok(8, k & 1); };
+    auto tR = [](int64_t k) { return Sched::tok(7, k & 1); };
     // W = alpha B at B's global columns (zero elsewhere), X = 0
-    S.task(0, {}, {tW, tX}, [&](lb::Ctx const& c) {
+    S.task(qT, {}, {tI, tN, tR(-1), tR(-2)}, [&](lb::Ctx const& c) {
         lb::set(c, Uplo::General, mloc, n, T(0), T(0), W.data(), ldw);
         lb::set(c, Uplo::General, mloc, n, T(0), T(0), X.data(), ldw);
         for (int64_t j = 0; j < B.nt(); ++j)
@@ -412,45 +424,68 @@ void trsmA_left(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& 
                         W.data() + gcol_of(B, j) * ldw, ldw);
     });
     const bool lower = (op == Op::NoTrans) == (uplo_phys == Uplo::Lower);
+    // W(rows [r0, r1)) -= op(A)(rows, k) X(k)
+    auto update = [&, op, lower](lb::Ctx const& c, int64_t k, int64_t kb, T const* Xk, int64_t r0, int64_t r1) {
+        if (r1 <= r0) return;
+        if (op == Op::NoTrans)
+            lb::gemm(c, Op::NoTrans, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + r0 + lcol_of(A, k) * lA.ld, lA.ld,
+                     Xk, kb, T(1), W.data() + r0, ldw);
+        else   // op(A(k, cols r0..r1)): my local columns of A = my local rows of B
+            lb::gemm(c, op, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + lrow_of(A, k) + r0 * lA.ld, lA.ld, Xk, kb,
+                     T(1), W.data() + r0, ldw);
+    };
     for (int64_t t = 0; t < mt; ++t) {
         const int64_t k = lower ? t : mt - 1 - t;
         const int64_t kb = B.tileMb(k);
         const int pk = B.srow_owner(k), qk = panel_col(A, op, k);
         const int64_t lrk = lrow_of(B, k);
-        S.task(device::kCommQueue, {tW}, {tW}, [&, kb, pk, lrk](lb::Ctx const& c) {
+        T* WXk = WX[t & 1].data();
+        // reduce: block row k of W is final after step t-1's next-row update
+        // and step t-2's rest (earlier rests are ordered before it)
+        S.task(device::kCommQueue, {tI, tN, tR(t - 2)}, {tS(t)}, [&, kb, pk, lrk, WXk](lb::Ctx const& c) {
             trace::Block t2("trsmA_reduce");
             if (myrow != pk) return;
-            pack(c, kb, n, W.data() + lrk, ldw, WX.data());
-            allreduce_sum(g.row(), WX.data(), size_t(kb) * n, c);
+            pack(c, kb, n, W.data() + lrk, ldw, WXk);
+            allreduce_sum(g.row(), WXk, size_t(kb) * n, c);
         });
-        S.task(0, {tW}, {tX}, [&, k, kb, pk, qk, lrk](lb::Ctx const& c) {
+        S.task(qP, {tS(t)}, {tS(t)}, [&, k, kb, pk, qk, lrk, WXk](lb::Ctx const& c) {
             if (myrow != pk || mycol != qk) return;
             lb::trsm(c, Side::Left, uplo_phys, op, diag, kb, n, T(1),
-                     lA.ptr + lrow_of(A, k) + lcol_of(A, k) * lA.ld, lA.ld, WX.data(), kb);
-            lb::copy2d(c, kb, n, WX.data(), kb, X.data() + lrk, ldw);
+                     lA.ptr + lrow_of(A, k) + lcol_of(A, k) * lA.ld, lA.ld, WXk, kb);
+            lb::copy2d(c, kb, n, WXk, kb, X.data() + lrk, ldw);
         });
-        S.task(device::kCommQueue, {tX}, {tX}, [&, kb, pk, qk](lb::Ctx const& c) {
+        S.task(device::kCommQueue, {tS(t)}, {tS(t)}, [&, kb, pk, qk, WXk](lb::Ctx const& c) {
             trace::Block t2("trsmA_bcast");
-            if (mycol == qk) bcast(g.col(), WX.data(), size_t(kb) * n, pk, c);
+            if (mycol == qk) bcast(g.col(), WXk, size_t(kb) * n, pk, c);
         });
-        S.task(0, {tX}, {tW}, [&, k, kb, qk, lrk](lb::Ctx const& c) {
+        // my local rows of the next block row to solve, and the rest
+        int64_t n0 = 0, n1 = 0;
+        if (t + 1 < mt) {
+            const int64_t kn = lower ? k + 1 : k - 1;
+            if (B.srow_owner(kn) == myrow) { n0 = lrow_of(B, kn); n1 = n0 + B.tileMb(kn); }
+        }
+        const int64_t r0 = lower ? lrow_of(B, k + 1) : 0, r1 = lower ? mloc : lrk;
+        // next row: needs X(k) and step t-1's rest (it also writes these rows)
+        S.task(qP, {tS(t), tR(t - 1)}, {tN}, [&, k, kb, qk, WXk, n0, n1](lb::Ctx const& c) {
             if (mycol != qk) return;
-            const int64_t r0 = lower ? lrow_of(B, k + 1) : 0, r1 = lower ? mloc : lrk;
-            if (r1 <= r0) return;
-            if (op == Op::NoTrans)
-                lb::gemm(c, Op::NoTrans, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + r0 + lcol_of(A, k) * lA.ld,
-                         lA.ld, WX.data(), kb, T(1), W.data() + r0, ldw);
-            else   // op(A(k, cols r0..r1)): my local columns of A = my local rows of B
-                lb::gemm(c, op, Op::NoTrans, r1 - r0, n, kb, T(-1), lA.ptr + lrow_of(A, k) + r0 * lA.ld, lA.ld,
-                         WX.data(), kb, T(1), W.data() + r0, ldw);
+            update(c, k, kb, WXk, n0, n1);
+        });
+        S.task(qT, {tS(t), tR(t - 1)}, {tR(t)}, [&, k, kb, qk, WXk, n0, n1, r0, r1](lb::Ctx const& c) {
+            if (mycol != qk) return;
+            if (n1 > n0) {
+                update(c, k, kb, WXk, r0, std::min(r1, n0));
+                update(c, k, kb, WXk, std::max(r0, n1), r1);
+            } else {
+                update(c, k, kb, WXk, r0, r1);
+            }
         });
     }
     // X(k) sits on process column qk of block row k: sum across the process
     // row, then each process keeps its own columns of B
-    S.task(device::kCommQueue, {tW}, {tX}, [&](lb::Ctx const& c) {
+    S.task(device::kCommQueue, {tN, tR(mt - 1), tR(mt - 2), tS(mt - 1)}, {tI}, [&](lb::Ctx const& c) {
         allreduce_sum(g.row(), X.data(), size_t(ldw) * n, c);
     });
-    S.task(0, {tX}, {tW}, [&](lb::Ctx const& c) {
+    S.task(qT, {tI}, {tI}, [&](lb::Ctx const& c) {
         for (int64_t j = 0; j < B.nt(); ++j)
             if (B.scol_owner(j) == mycol)
                 lb::copy2d(c, mloc, B.tileNb(j), X.data() + gcol_of(B, j) * ldw, ldw,

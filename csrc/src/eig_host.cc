@@ -200,7 +200,10 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
     auto right = [&](int64_t r, int64_t c0, int64_t L, T tau, const T* v, T* w) {
         // rows in window (skip r): A[row, J] = A[row, J] H, column-oriented
         // (contiguous inner loops; the row-wise form strides by lda)
-        int64_t w0 = std::max<int64_t>(0, c0 - 2 * b - 1), w1 = std::min<int64_t>(m - 1, c0 + L - 1 + 2 * b);
+        // rows with nonzeros in columns [c0, c0 + L): the band rows
+        // [c0 - b, c0 + L) (earlier rows are bidiagonal already, and the
+        // previous sweep's bulge is kLag steps further down)
+        int64_t w0 = std::max<int64_t>(0, c0 - b), w1 = std::min<int64_t>(m - 1, c0 + L - 1);
         const int64_t nr = w1 - w0 + 1;
         if (nr <= 0) return;
         std::fill(w, w + nr, T(0));
@@ -219,7 +222,10 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         }
     };
     auto left = [&](int64_t c, int64_t r0, int64_t L, T tau, const T* v) {
-        int64_t w0 = std::max<int64_t>(0, r0 - 2 * b - 1), w1 = std::min<int64_t>(n - 1, r0 + L - 1 + 2 * b);
+        // columns with nonzeros in rows [r0, r0 + L): the band columns up to
+        // r0 + L - 1 + b; left of r0 these rows are zero (below the diagonal
+        // and outside this step's bulge)
+        int64_t w0 = r0, w1 = std::min<int64_t>(n - 1, r0 + L - 1 + b);
         for (int64_t jj = w0; jj <= w1; ++jj) {
             if (jj == c) continue;
             T s = T(0);
@@ -229,9 +235,10 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         }
     };
     // Sweeps pipelined over threads as in hb2st: step t of sweep j touches
-    // rows/columns [c0 - 2b - 1, c0 + 3b) with c0 = j + 1 + t b, so it may run
-    // once sweep j-1 has finished its steps 0..t+5; reflectors are kept per
-    // sweep and concatenated in sweep order (out-of-order ones commute).
+    // rows/columns [c0 - b, c0 + 2b) with c0 = j + 1 + t b, so it may run once
+    // sweep j-1 has finished its steps 0..t+5 (a conservative lag); reflectors
+    // are kept per sweep and concatenated in sweep order (out-of-order ones
+    // commute).
     const int64_t nsw = n > 1 ? n - 1 : 0;
     constexpr int64_t kLag = 6;
     constexpr int64_t kDone = std::numeric_limits<int64_t>::max();

@@ -128,8 +128,8 @@ struct RowRotSink : host::RotSink<real_type<T>> {
         const size_t sv = size_t(std::max<int64_t>(rv.second - rv.first + 2 * K - 3, 0)) * 2 * K;
         if (su) device::memcpy_async(db[cur].data(), Du, su * sizeof(R), c.stream);
         if (sv) device::memcpy_async(db[cur].data() + tsz, Dv, sv * sizeof(R), c.stream);
-        if (U && su) kd_::rot_sweeps(urows, kd_::dptr(U), ldu, ru.first, ru.second, db[cur].data(), c.stream);
-        if (V && sv) kd_::rot_sweeps(vrows, kd_::dptr(V), ldv, rv.first, rv.second, db[cur].data() + tsz, c.stream);
+        kd_::rot_sweeps2(U && su ? urows : 0, kd_::dptr(U), ldu, ru.first, ru.second, db[cur].data(),
+                         V && sv ? vrows : 0, kd_::dptr(V), ldv, rv.first, rv.second, db[cur].data() + tsz, c.stream);
         slate_hip_call(hipEventRecord(ev[cur], c.stream));
         cur ^= 1;
         bu.clear();

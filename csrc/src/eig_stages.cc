@@ -158,7 +158,7 @@ void tb2bd(TriangularBandMatrix<T>& A, std::vector<real_type<T>>& D, std::vector
     const int64_t m = A.m(), n = A.n(), kd = A.bandwidth();
     U = BandReflectors<T>{};
     V = BandReflectors<T>{};
-    if (m == n && A.op() == Op::NoTrans) {
+    if (m == n && A.op() == Op::NoTrans && !std::getenv("SLATE_TB2BD_FULL")) {
         // band only, in general band storage with room for the bulge
         // (kl = ku = 3 kd + 2, as the svd driver): (i, j) at B[M + i - j + j ldb]
         const int64_t M = 3 * std::max<int64_t>(kd, 1) + 2, ldb = 2 * M + 1;
