@@ -52,9 +52,30 @@ inline Method str2method(std::string s) {
 }
 }  // namespace MethodHemm
 
+/// How cholqr forms A^H A (reference method.hh:181-232): HerkC (triangle
+/// only, default on devices), GemmA / GemmC (full product by the stationary-A
+/// or SUMMA gemm; GemmA is the host default).
 namespace MethodCholQR {
-const Method Error = baseMethodError, Auto = baseMethodAuto, GemmA = 1, GemmC = 2, HerkA = 3, HerkC = 4;
+const Method Error = baseMethodError, Auto = baseMethodAuto, HerkC = 1, GemmA = 2, GemmC = 3;
+inline Method select_algo(Target target) { return target == Target::Devices ? HerkC : GemmA; }
+inline Method str2method(std::string s) {
+    std::transform(s.begin(), s.end(), s.begin(), ::tolower);
+    if (s == "auto") return Auto;
+    if (s == "herkc" || s == "herk") return HerkC;
+    if (s == "gemma") return GemmA;
+    if (s == "gemmc" || s == "gemm") return GemmC;
+    throw Exception("unknown cholQR method");
 }
+inline const char* method2str(Method m) {
+    switch (m) {
+        case Auto: return "auto";
+        case HerkC: return "herkC";
+        case GemmA: return "gemmA";
+        case GemmC: return "gemmC";
+        default: return "error";
+    }
+}
+}  // namespace MethodCholQR
 
 namespace MethodGels {
 const Method Error = baseMethodError, Auto = baseMethodAuto, Geqrf = 1, Cholqr = 2;

@@ -156,7 +156,7 @@ Options to_options(py::dict d) {
         else if (k == "method_lu") o[Option::MethodLU] = meth(v, MethodLU::str2method);
         else if (k == "method_trsm") o[Option::MethodTrsm] = meth(v, MethodTrsm::str2method);
         else if (k == "method_gels") o[Option::MethodGels] = meth(v, MethodGels::str2method);
-        else if (k == "method_cholqr") o[Option::MethodCholQR] = v.cast<int64_t>();
+        else if (k == "method_cholqr") o[Option::MethodCholQR] = meth(v, MethodCholQR::str2method);
         else if (k == "method_hemm") o[Option::MethodHemm] = meth(v, MethodHemm::str2method);
         else if (k == "method_eig") o[Option::MethodEig] = OptionValue(int64_t(v.cast<std::string>()[0]));
         else if (k == "print_verbose") o[Option::PrintVerbose] = v.cast<int64_t>();

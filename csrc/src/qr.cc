@@ -919,11 +919,31 @@ template <typename T>
 int64_t cholqr(Matrix<T>& A, Matrix<T>& R, Options const& opts) {
     trace::Block tb("cholqr");
     internal::DriverScope ds_;
-    // R^H R = A^H A ; Q = A R^{-1} (reference src/cholqr.cc)
+    // R^H R = A^H A ; Q = A R^{-1} (reference src/cholqr.cc:24-130).
+    // Option::MethodCholQR picks how A^H A is formed: HerkC computes the upper
+    // triangle only (half the flops; device default), GemmA / GemmC the full
+    // product with the stationary-A or SUMMA gemm (host default GemmA).
     Target target = resolve_target(opts);
-    (void)target;
+    Method method = get_option<int64_t>(opts, Option::MethodCholQR, MethodCholQR::Auto);
+    if (method == MethodCholQR::Auto) method = MethodCholQR::select_algo(target);
+    switch (method) {
+        case MethodCholQR::HerkC: {
+            HermitianMatrix<T> H(Uplo::Upper, R);
+            herk(real_type<T>(1), conj_transpose(A), real_type<T>(0), H, opts);
+            break;
+        }
+        case MethodCholQR::GemmA:
+        case MethodCholQR::GemmC: {
+            Options o2 = opts;
+            o2[Option::MethodGemm] = int64_t(method == MethodCholQR::GemmA ? MethodGemm::GemmA : MethodGemm::GemmC);
+            Matrix<T> Rg(R); Rg.set_uplo(Uplo::General);
+            gemm(T(1), conj_transpose(A), A, T(0), Rg, o2);
+            break;
+        }
+        default:
+            slate_error("cholqr: unknown MethodCholQR");
+    }
     HermitianMatrix<T> H(Uplo::Upper, R);
-    herk(real_type<T>(1), conj_transpose(A), real_type<T>(0), H, opts);
     int64_t info = potrf(H, opts);
     if (info) return info;
     Matrix<T> Rg(R); Rg.set_uplo(Uplo::General);

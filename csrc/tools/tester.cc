@@ -47,7 +47,7 @@ struct Params {
     int repeat = 1;
     bool trace = false;
     std::string matrix;          // --matrix: matgen kind of the main operand (default per routine)
-    int64_t method_lu = -1, method_trsm = -1, method_gemm = -1, method_hemm = -1;
+    int64_t method_lu = -1, method_trsm = -1, method_gemm = -1, method_hemm = -1, method_cholqr = -1;
     char origin = 'x';           // --origin h|d: where the operands are generated (x: the target)
     int timer_level = 1;         // --timer-level 2: per-driver trace timers after each case
     int64_t itermax = -1;
@@ -116,6 +116,7 @@ struct Case {
         : P(p), m(d[0]), n(d[1]), k(d[2]), nb(nb_) {
         opts = {{Option::Target, P.target}, {Option::Lookahead, P.lookahead}};
         if (P.method_lu >= 0) opts[Option::MethodLU] = P.method_lu;
+        if (P.method_cholqr >= 0) opts[Option::MethodCholQR] = P.method_cholqr;
         if (P.method_trsm >= 0) opts[Option::MethodTrsm] = P.method_trsm;
         if (P.method_gemm >= 0) opts[Option::MethodGemm] = P.method_gemm;
         if (P.method_hemm >= 0) opts[Option::MethodHemm] = P.method_hemm;
@@ -1803,7 +1804,8 @@ void usage() {
         "       [--nb NB,...] [--grid PxQ] [--target d|h] [--lookahead LA] [--nrhs K]\n"
         "       [--check y|n] [--tol T] [--repeat R] [--trace y|n]\n"
         "       [--matrix KIND] [--method-lu ppiv|calu|nopiv] [--method-trsm auto|A|B]\n"
-        "       [--method-gemm auto|A|C] [--method-hemm auto|A|C] [--origin h|d]\n"
+        "       [--method-gemm auto|A|C] [--method-hemm auto|A|C] [--method-cholqr auto|herkC|gemmA|gemmC]\n"
+        "       [--origin h|d]\n"
         "       [--timer-level 1|2] [--itermax N] [--fallback y|n] [--pivot-threshold X]\n"
         "       [--uplo l|u] [--trans n|t|c] [--side l|r] [--diag n|u] [--cond C] [--ib IB]\n"
         "       [--nonuniform-nb y|n] [--go c|r] [--do r|c]\n"
@@ -1844,6 +1846,7 @@ int main(int argc, char** argv) {
         else if (a == "--method-trsm") P.method_trsm = MethodTrsm::str2method(val());
         else if (a == "--method-gemm") P.method_gemm = MethodGemm::str2method(val());
         else if (a == "--method-hemm") P.method_hemm = MethodHemm::str2method(val());
+        else if (a == "--method-cholqr") P.method_cholqr = MethodCholQR::str2method(val());
         else if (a == "--origin") P.origin = char(std::tolower(val()[0]));
         else if (a == "--timer-level") P.timer_level = std::stoi(val());
         else if (a == "--itermax") P.itermax = std::stoll(val());

@@ -114,3 +114,12 @@ def test_device_routines():
                           "svd_vals,hegv,steqr2,redistribute",
                           "--type", "d,z", "--dim", "1000", "--nb", "128"], target="d")
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
+
+
+@pytest.mark.parametrize("method", ["herkC", "gemmA", "gemmC"])
+def test_cholqr_methods(method):
+    """--method-cholqr: A^H A by herk (triangle), stationary-A gemm or SUMMA
+    gemm (reference method.hh MethodCholQR), on a 2x2 grid."""
+    codes, outs = launch(["cholqr", "--type", "d,z", "--dim", "170x90x90", "--nb", "32", "--grid", "2x2",
+                          "--method-cholqr", method], 4)
+    assert codes == [0] * 4 and "all tests passed" in outs[0], "\n".join(o[-2500:] for o in outs)
