@@ -184,9 +184,19 @@ struct TileLoader {
 // Epilogue shared by the MFMA GEMM kernels: lane&15 runs along M (contiguous
 // in column-major C).  For beta != 0 the C values of two accumulator columns
 // are loaded together before any store so the loads overlap.
+// First valid row (relative to C's row 0) of C's column gn under a StairMap.
+__device__ inline int64_t stair_row0(StairMap const& sm, int64_t gn) {
+    const int64_t lc = sm.c0 + gn;
+    const int64_t lt = lc / sm.nb, o = lc - lt * sm.nb;
+    const int64_t J = lt * sm.q + sm.pcol;                       // global tile of the column
+    const int64_t li = J > sm.prow ? (J - sm.prow + sm.p - 1) / sm.p : 0;   // first local row tile >= J
+    return li * sm.nb + (li * sm.p + sm.prow == J ? o : 0) - sm.r0;
+}
+
 template <typename T, int TM, int TN, char TRI>
 __device__ inline void gemm_epilogue(typename Mfma<T>::acc_t (&acc)[TM][TN], int64_t m, int64_t n, T alpha,
-                                     T beta, T* __restrict__ C, int64_t ldc, int64_t wm0, int64_t wn0, int lane) {
+                                     T beta, T* __restrict__ C, int64_t ldc, int64_t wm0, int64_t wn0, int lane,
+                                     StairMap const& sm) {
     using M = Mfma<T>;
     const bool beta_zero = (beta == T(0));
     constexpr int JB = GEMM_JB;
@@ -194,6 +204,7 @@ __device__ inline void gemm_epilogue(typename Mfma<T>::acc_t (&acc)[TM][TN], int
         bool in = gm < m && gn < n;
         if constexpr (TRI == 'L') in = in && gm >= gn;
         if constexpr (TRI == 'U') in = in && gm <= gn;
+        if constexpr (TRI == 'S') in = in && gm >= stair_row0(sm, gn);
         return in;
     };
     #pragma unroll
@@ -253,7 +264,7 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
                       const T* __restrict__ A, int64_t lda, int64_t sA,
                       const T* __restrict__ B, int64_t ldb, int64_t sB,
                       T beta, T* __restrict__ C, int64_t ldc, int64_t sC,
-                      bool aligned)
+                      bool aligned, StairMap sm)
 {
     using M = Mfma<T>;
     using acc_t = typename M::acc_t;
@@ -276,7 +287,7 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     // tile coordinates: XCD remap, then grouped order (GROUP tile-rows)
     const int mt = (int)((m + BM - 1) / BM), nt = (int)((n + BN - 1) / BN);
     int tm, tn;
-    if constexpr (TRI == 0) {
+    if constexpr (TRI == 0 || TRI == 'S') {
         const int nblk = mt * nt;
         int bid = xcd_remap(blockIdx.x, nblk);
         constexpr int GROUP = 8;
@@ -297,6 +308,14 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
         if constexpr (TRI == 'L') { tm = r; tn = c; } else { tm = c; tn = r; }
     }
     const int64_t m0 = (int64_t)tm * BM, n0 = (int64_t)tn * BN;
+    if constexpr (TRI == 'S') {
+        // tiles wholly above the staircase do nothing (the row start is
+        // nondecreasing along the local columns, so column n0 has the lowest)
+        if (stair_row0(sm, n0) >= m0 + BM) return;
+        // this tile's B^T rows: its local column tile's slab in the operand
+        const int64_t lc = sm.c0 + n0;
+        B += sm.btab[lc / sm.nb - sm.c0 / sm.nb] + (lc % sm.nb) - n0;
+    }
 
     const int lane = threadIdx.x & 63;
     const int wid  = threadIdx.x >> 6;
@@ -424,7 +443,7 @@ void gemm_mfma_kernel(int64_t m, int64_t n, int64_t k, T alpha,
     else if (GEMM_SPLIT && aligned && mfull && nfull && k % BK == 0) kloop(std::true_type{});
     else kloop(std::false_type{});
 
-    gemm_epilogue<T, TM, TN, TRI>(acc, m, n, alpha, beta, C, ldc, m0 + wm * WTM, n0 + wn * WTN, lane);
+    gemm_epilogue<T, TM, TN, TRI>(acc, m, n, alpha, beta, C, ldc, m0 + wm * WTM, n0 + wn * WTN, lane, sm);
 }
 
 template <typename T, bool A_KC, bool B_KC, char TRI, int BM, int BN, int BK = 16, int WTN = 64, int WTM = 64,
@@ -433,21 +452,21 @@ static void launch_tile(int64_t m, int64_t n, int64_t k, T alpha,
                         const T* A, int64_t lda, int64_t sA,
                         const T* B, int64_t ldb, int64_t sB,
                         T beta, T* C, int64_t ldc, int64_t sC,
-                        int64_t batch, bool aligned, hipStream_t stream)
+                        int64_t batch, bool aligned, hipStream_t stream, StairMap const& sm = StairMap{})
 {
     constexpr int NTHR = 64 * (BM / WTM) * (BN / WTN);
     int64_t mt = (m + BM - 1) / BM, nt = (n + BN - 1) / BN;
-    int64_t nblk = TRI ? mt * (mt + 1) / 2 : mt * nt;
+    int64_t nblk = (TRI == 'L' || TRI == 'U') ? mt * (mt + 1) / 2 : mt * nt;
     dim3 grid((unsigned)nblk, (unsigned)batch);
     // every tile interior (the common case for nb-multiple trailing updates):
     // a kernel without the bounds-checked path, whose registers then go to
     // the hot loop alone
     if (aligned && m % BM == 0 && n % BN == 0 && k % BK == 0 && k > 0)
         hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, ROT, true>), grid, dim3(NTHR),
-                           0, stream, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+                           0, stream, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned, sm);
     else
         hipLaunchKernelGGL((gemm_mfma_kernel<T, BM, BN, BK, A_KC, B_KC, TRI, WTN, WTM, ROT, false>), grid, dim3(NTHR),
-                           0, stream, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned);
+                           0, stream, m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC, aligned, sm);
 }
 
 // fp32 only: 256 x 128 tiles (8 waves, 1 workgroup per CU) cut operand
@@ -531,6 +550,26 @@ void gemm_tri_real(char uplo, char transA, char transB, int64_t n, int64_t k,
     else { SLATE_TRI_LAUNCH('U') }
 #undef SLATE_TRI_LAUNCH
 }
+
+// Staircase trailing update of a block-cyclic lower-triangular matrix (p x q
+// potrf / herk): one launch over the whole local trailing block instead of one
+// GEMM per local tile column; B^T tiles come from wherever the gathered panel
+// keeps them (btab).  NT operand form on the 4-wave rotated 128 x 128 tile.
+template <typename T>
+void gemm_stair_real(int64_t m, int64_t n, int64_t k, T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
+                     StairMap const& sm, T beta, T* C, int64_t ldc, hipStream_t stream)
+{
+    if (m <= 0 || n <= 0) return;
+    constexpr int VEC = 16 / sizeof(T);
+    auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };
+    bool aligned = al(A) && al(B) && (lda % VEC == 0) && (ldb % VEC == 0) && sm.nb % VEC == 0;
+    launch_tile<T, false, false, 'S', 128, 128>(m, n, k, alpha, A, lda, 0, B, ldb, 0, beta, C, ldc, 0, 1,
+                                                aligned, stream, sm);
+}
+template void gemm_stair_real<double>(int64_t, int64_t, int64_t, double, const double*, int64_t, const double*, int64_t,
+                                      StairMap const&, double, double*, int64_t, hipStream_t);
+template void gemm_stair_real<float>(int64_t, int64_t, int64_t, float, const float*, int64_t, const float*, int64_t,
+                                     StairMap const&, float, float*, int64_t, hipStream_t);
 
 // split-K reduction: C = alpha * sum_s P[s] + beta * C (P: splits x m x n, ld m)
 template <typename T>

@@ -174,6 +174,21 @@ void gemm_tri_real(char uplo, char transA, char transB, int64_t n, int64_t k,
                    T beta, T* C, int64_t ldc, hipStream_t stream);
 template <typename T>
 void splitk_reduce(int64_t m, int64_t n, int splits, const T* P, T alpha, T beta, T* C, int64_t ldc, hipStream_t s);
+/// Staircase (block-cyclic lower-triangular) output map for one launch of a
+/// p x q trailing update: local column c0 + j of C belongs to global tile
+/// (c0 + j) / nb * q + pcol; its valid local rows are those whose global index
+/// is >= the column's (lower triangle of the global matrix), and its rows of
+/// the B^T operand (n x k) start at btab[(c0 + j) / nb - c0 / nb] + (c0 + j) % nb.
+struct StairMap {
+    const int64_t* btab = nullptr;  // device: element offset of each local column tile's B rows
+    int64_t c0 = 0, r0 = 0;         // local column / row index of C(0, 0)
+    int nb = 0, p = 1, q = 1, prow = 0, pcol = 0;   // tile size, grid, my row / column (relative to the source)
+};
+/// C(staircase) = alpha A B^T + beta C over the StairMap's lower staircase;
+/// tiles entirely above it are never computed.  Requires nb % 128 == 0.
+template <typename T>
+void gemm_stair_real(int64_t m, int64_t n, int64_t k, T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,
+                     StairMap const& sm, T beta, T* C, int64_t ldc, hipStream_t stream);
 template <typename T>
 void gemm_cplx(char uplo, char transA, char transB, int64_t m, int64_t n, int64_t k,
                T alpha, const T* A, int64_t lda, const T* B, int64_t ldb,

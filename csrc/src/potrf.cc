@@ -14,9 +14,16 @@
 //                      On a 1x1 grid the trailing update is a single
 //                      triangular-output MFMA GEMM (herk) over the whole
 //                      trailing matrix.
+//                      On a p x q grid (device, real types, nb % 128 == 0)
+//                      every range is ONE staircase MFMA launch over the
+//                      local lower-trapezoidal block (gemm_stair_real): the
+//                      valid rows of each local column follow from the
+//                      block-cyclic map, and each local tile column's B^T
+//                      rows are read where the gathered panel keeps them.
 // The reference instead issues one batched herk/gemm per tile group per
 // step and syncs its queues after each op (internal_herk.cc:491-530).
 #include "internal.hh"
+#include "../kernels/kernels.hh"
 
 #include <algorithm>
 #include <numeric>
@@ -55,6 +62,47 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
             Dk[r].resize(target, size_t(nb) * nb);
         }
     }
+    // ---- staircase single-launch updates on p x q > 1 (see header)
+    // local row / column tile t of the view is view tile prow + t p / pcol + t q
+    // on a block-cyclic layout; verified here, else the per-tile-column path
+    const int64_t nloc = L.n;
+    std::vector<int64_t> rtiles, ctiles;     // view tile of each local row / column tile
+    for (int64_t i = 0; i < A.mt(); ++i) if (A.srow_owner(i) == myrow) rtiles.push_back(i);
+    for (int64_t j = 0; j < nt; ++j) if (A.scol_owner(j) == mycol) ctiles.push_back(j);
+    bool stair = (p * q > 1) && target == Target::Devices && !is_complex_v<T> && nb % 128 == 0;
+    if (stair) {
+        for (size_t t = 0; t < rtiles.size() && stair; ++t)
+            stair = rtiles[t] == rtiles[0] + int64_t(t) * p && lrow_of(A, rtiles[t]) == int64_t(t) * nb &&
+                    (rtiles[t] == A.mt() - 1 || A.tileMb(rtiles[t]) == nb);
+        for (size_t t = 0; t < ctiles.size() && stair; ++t)
+            stair = ctiles[t] == ctiles[0] + int64_t(t) * q && lcol_of(A, ctiles[t]) == int64_t(t) * nb &&
+                    (ctiles[t] == nt - 1 || A.tileNb(ctiles[t]) == nb);
+        stair = stair && (rtiles.empty() || rtiles[0] < p) && (ctiles.empty() || ctiles[0] < q);
+    }
+    const int prow0 = rtiles.empty() ? myrow : int(rtiles[0]), pcol0 = ctiles.empty() ? mycol : int(ctiles[0]);
+    const int64_t nlt = int64_t(ctiles.size());
+    // btab[k][t]: offset of local column tile t's B^T rows in step k's operand
+    // (p == 1: rows of W_k, ld ldW; p > 1: tiles of the gathered Wt, ld nb)
+    Work<int64_t> btab;
+    if (stair && nlt > 0) {
+        std::vector<int64_t> tab(size_t(nt) * nlt, 0);
+        for (int64_t k = 0; k + 1 < nt; ++k) {
+            const int64_t lr_k1 = lrow_of(A, k + 1);
+            std::vector<int64_t> seen(p, 0);
+            for (int64_t J = k + 1; J < nt; ++J) {
+                if (A.scol_owner(J) != mycol) continue;
+                const int64_t t = (lcol_of(A, J)) / nb;
+                const int r = A.srow_owner(J);
+                tab[size_t(k) * nlt + t] = (p == 1) ? lrow_of(A, J) - lr_k1 : (int64_t(r) * maxcnt + seen[r]) * nb * nb;
+                ++seen[r];
+            }
+        }
+        btab.resize(target, tab.size());
+        device::memcpy_async(btab.data(), tab.data(), tab.size() * sizeof(int64_t), S.ctx(1).stream);
+        slate_hip_call(hipStreamSynchronize(S.ctx(1).stream));
+    }
+    (void)nloc;
+
     Work<int> dinfo(target, 1);
     {
         lb::Ctx c0 = S.ctx(1);
@@ -133,8 +181,22 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         });
 
         // ---- trailing updates
-        auto update = [&, Wk, ldW, kb, slot, lists, lr_k1](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        auto update = [&, Wk, ldW, kb, slot, lists, lr_k1, k](lb::Ctx const& c, int64_t j0, int64_t j1) {
             trace::Block tb("potrf_update");
+            if (stair && c.dev()) {
+                if constexpr (!is_complex_v<T>) {
+                    const int64_t c0 = lcol_of(A, j0), nc = lcol_of(A, j1) - c0;
+                    const int64_t r0 = lrow_of(A, j0), nrows = mloc - r0;
+                    if (nc <= 0 || nrows <= 0) return;
+                    slate_amd::dev::StairMap sm;
+                    sm.btab = btab.data() + k * nlt + c0 / nb;
+                    sm.c0 = c0; sm.r0 = r0; sm.nb = int(nb); sm.p = p; sm.q = q; sm.prow = prow0; sm.pcol = pcol0;
+                    const T* Bb = (p == 1) ? Wk : Wt[slot].data();
+                    slate_amd::dev::gemm_stair_real<T>(nrows, nc, kb, T(-1), Wk + (r0 - lr_k1), ldW, Bb,
+                                                       p == 1 ? ldW : nb, sm, T(1), a + r0 + c0 * lda, lda, c.stream);
+                }
+                return;
+            }
             // fast path: 1x1 grid, contiguous range -> one herk over [j0, j1) x [j0, ...)
             if (p == 1 && q == 1) {
                 int64_t r0 = lrow_of(A, j0), c0 = lcol_of(A, j0), c1 = lcol_of(A, j1);

@@ -112,3 +112,17 @@ def test_rccl_2x4_n4096(la, routines):
                         "--target", "d", "--lookahead", la],
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("nprocs,grid,la", [(4, "2x2", "1"), (2, "1x2", "2"), (2, "2x1", "1"), (8, "2x4", "2")])
+def test_rccl_potrf_staircase(nprocs, grid, la):
+    """p x q device Cholesky with nb = 128: every trailing range is one
+    staircase MFMA launch (gemm_stair_real) reading the gathered panel tiles
+    in place; uneven n leaves a partial last tile.  Residual checks of the
+    tester (potrf, posv, potri) in fp32 and fp64 over real RCCL."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), str(nprocs),
+                        "potrf,posv,potri", "--type", "s,d", "--dim", "1000,1536", "--nb", "128", "--grid", grid,
+                        "--target", "d", "--lookahead", la],
+                       capture_output=True, text=True, timeout=900)
+    assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
