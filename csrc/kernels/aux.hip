@@ -334,26 +334,35 @@ void potrf_inv_small_kernel(int n, T* A, int64_t lda, T* W, int64_t ldw, int* in
 // backward substitution, fully unrolled, wave-uniform LDS broadcasts).  One
 // launch instead of set + trtri_diag + copy + GEMM on the LU panel's
 // recursion, where the narrow blocks' U12 solves are on the critical path.
-template <typename T>
+template <typename T, int MM>
 __global__ __launch_bounds__(64)
 void trsm_small_kernel(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb) {
     SLATE_PANEL_WAVE_PRIO();
-    __shared__ T L[64][65];
-    __shared__ T rd[64];
+    // MM = 32 or 64 (m <= MM): the padded triangle, and the workgroup's 64
+    // right-hand-side columns staged through LDS so that global loads and
+    // stores run along the columns (a lane-per-column access would touch a
+    // different cache line in every lane)
+    __shared__ T L[MM][MM + 1];
+    __shared__ T X[64][MM + 1];
+    __shared__ T rd[MM];
     const int lane = threadIdx.x;
-    for (int j = 0; j < 64; ++j)
-        L[lane][j] = (lane < m && j < m) ? A[lane + (int64_t)j * lda] : (lane == j ? one<T>() : zero<T>());
+    const int64_t col0 = (int64_t)blockIdx.x * 64;
+    const int ncol = (int)min<int64_t>(64, n - col0);
+    for (int j = 0; j < MM; ++j)
+        if (lane < MM)
+            L[lane][j] = (lane < m && j < m) ? A[lane + (int64_t)j * lda] : (lane == j ? one<T>() : zero<T>());
+    for (int c = 0; c < ncol; ++c)
+        if (lane < m) X[c][lane] = B[lane + (col0 + c) * ldb];
     __syncthreads();
-    rd[lane] = (diag == 'U') ? one<T>() : one<T>() / L[lane][lane];
+    if (lane < MM) rd[lane] = (diag == 'U') ? one<T>() : one<T>() / L[lane][lane];
     __syncthreads();
-    const int64_t col = (int64_t)blockIdx.x * 64 + lane;
-    const bool live = col < n;
-    T x[64];
+    const bool live = lane < ncol;
+    T x[MM];
     #pragma unroll
-    for (int i = 0; i < 64; ++i) x[i] = (live && i < m) ? B[i + col * ldb] : zero<T>();
+    for (int i = 0; i < MM; ++i) x[i] = (live && i < m) ? X[lane][i] : zero<T>();
     if (uplo == 'L') {
         #pragma unroll
-        for (int i = 0; i < 64; ++i) {
+        for (int i = 0; i < MM; ++i) {
             T s = x[i];
             #pragma unroll
             for (int l = 0; l < i; ++l) s -= L[i][l] * x[l];
@@ -361,18 +370,20 @@ void trsm_small_kernel(char uplo, char diag, int m, int64_t n, const T* A, int64
         }
     } else {
         #pragma unroll
-        for (int i = 63; i >= 0; --i) {
+        for (int i = MM - 1; i >= 0; --i) {
             T s = x[i];
             #pragma unroll
-            for (int l = i + 1; l < 64; ++l) s -= L[i][l] * x[l];
+            for (int l = i + 1; l < MM; ++l) s -= L[i][l] * x[l];
             x[i] = s * rd[i];
         }
     }
     if (live) {
         #pragma unroll
-        for (int i = 0; i < 64; ++i)
-            if (i < m) B[i + col * ldb] = x[i];
+        for (int i = 0; i < MM; ++i) X[lane][i] = x[i];
     }
+    __syncthreads();
+    for (int c = 0; c < ncol; ++c)
+        if (lane < m) B[lane + (col0 + c) * ldb] = X[c][lane];
 }
 
 //------------------------------------------------------------------------------
@@ -402,6 +413,17 @@ __global__ void permute_rows_kernel(int64_t n, T* A, int64_t lda, const int64_t*
         }
         __syncthreads();
     }
+}
+
+// V = unit-lower part of A (one launch instead of a copy plus a triangle set)
+// (diagonal of column j at row j + off)
+template <typename T>
+__global__ void form_v_kernel(int64_t m, int64_t k, int64_t off, const T* A, int64_t lda, T* V, int64_t ldv) {
+    const int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x;
+    const int64_t j = blockIdx.y;
+    if (i >= m) return;
+    const int64_t d = j + off;
+    V[i + j * ldv] = i < d ? zero<T>() : (i == d ? one<T>() : A[i + j * lda]);
 }
 
 // Row gather / scatter between a column strip of A and a packed buffer
@@ -509,8 +531,19 @@ void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int
 template <typename T>
 void trsm_small(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
-    hipLaunchKernelGGL(trsm_small_kernel<T>, dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, uplo, diag, m, n, A,
-                       lda, B, ldb);
+    if (m <= 32)
+        hipLaunchKernelGGL((trsm_small_kernel<T, 32>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, uplo, diag, m,
+                           n, A, lda, B, ldb);
+    else
+        hipLaunchKernelGGL((trsm_small_kernel<T, 64>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, uplo, diag, m,
+                           n, A, lda, B, ldb);
+}
+
+template <typename T>
+void form_v(int64_t m, int64_t k, int64_t off, const T* A, int64_t lda, T* V, int64_t ldv, hipStream_t s) {
+    if (m <= 0 || k <= 0) return;
+    hipLaunchKernelGGL(form_v_kernel<T>, dim3((unsigned)((m + 255) / 256), (unsigned)k), dim3(256), 0, s, m, k, off,
+                       A, lda, V, ldv);
 }
 
 template <typename T>
@@ -545,6 +578,7 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void potrf_inv_small<T>(int, T*, int64_t, T*, int64_t, int*, int, hipStream_t);                 \
     template void trsm_small<T>(char, char, int, int64_t, const T*, int64_t, T*, int64_t, hipStream_t);     \
     template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
+    template void form_v<T>(int64_t, int64_t, int64_t, const T*, int64_t, T*, int64_t, hipStream_t);                     \
     template void laswp<T>(int64_t, T*, int64_t, int64_t, int64_t, const int64_t*, int64_t, hipStream_t);  \
     template void rows_pack<T>(int64_t, T*, int64_t, const int64_t*, int, T*, bool, hipStream_t);
 

@@ -210,6 +210,9 @@ void trtri_blocks(char uplo, char diag, int64_t BS, int64_t nblk, const T* A, in
 // ---- aux (aux.hip)
 template <typename T>
 void geset(char uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda, hipStream_t s);
+/// Explicit unit-lower reflector block: V(i, j) = 0 (i < j + off), 1 (i == j + off), A(i, j) below; m x k.
+template <typename T>
+void form_v(int64_t m, int64_t k, int64_t off, const T* A, int64_t lda, T* V, int64_t ldv, hipStream_t s);
 template <typename Ts, typename Td>
 void gecopy(char uplo, char trans, int64_t m, int64_t n, const Ts* A, int64_t lda, Td* B, int64_t ldb, hipStream_t s);
 template <typename T>

@@ -9,10 +9,14 @@
 // MI355X design: the tournament is played on a 32-column narrow block inside
 // the recursive device panel (local_blas.cc LuPanelDev), so a 32768-row panel
 // costs four or five launches instead of two launches per column:
-//   select  leaves: 256 rows per workgroup, one row per lane held in VGPRs;
+//   select  one WAVE per leaf / tree node, RPT = 16 / sizeof(T) rows per lane
+//           held in VGPRs (fp64: 128-row leaves, nodes of 4 x 32 candidates):
 //           GEPP with a DPP (quad_perm/row_ror) + v_readlane wave argmax and
-//           an LDS broadcast of the pivot row.
-//   select  tree nodes: 512-lane workgroups, fan-in 16 (16 x 32 candidates).
+//           a wave-local LDS broadcast of the pivot row -- no workgroup
+//           barrier in the 32-step loop (measured ~46-59 us per launch for the
+//           earlier 256/512-thread workgroup form with two barriers per step,
+//           which made the panel latency-bound at small M).  SLATE_TSLU_WG=1
+//           selects the workgroup form (A/B).
 //   permute each workgroup owns panel columns; it re-derives the interchanges
 //           from the winners in one wave (ballot/readlane, all scalar), applies
 //           the net row permutation to its columns and copies the permuted
@@ -24,6 +28,7 @@
 #include "kernels.hh"
 
 #include <climits>
+#include <cstdlib>
 #include <type_traits>
 
 namespace slate_amd {
@@ -32,6 +37,15 @@ namespace dev {
 namespace {
 
 constexpr int TW = 32;        // tournament / narrow-block width
+
+// for (k = B; k < E; ++k) f(integral_constant<k>) -- compile-time indices
+template <int B, int E, typename F>
+__device__ __forceinline__ void static_for(F&& f) {
+    if constexpr (B < E) {
+        f(std::integral_constant<int, B>{});
+        static_for<B + 1, E>(f);
+    }
+}
 constexpr int TR = 256;       // leaf rows per workgroup
 constexpr int NODE_NT = 512;  // node workgroup size
 constexpr int FANIN = NODE_NT / TW;
@@ -130,6 +144,137 @@ __global__ __launch_bounds__(NT) void tslu_select_kernel(int64_t m, int64_t r, i
     if (tid == 0) cnt_out[blockIdx.x] = cnt;
 }
 
+// 32-bit pivot-search key of a candidate: 1 + the fp32 bit pattern of its
+// magnitude (monotonic for non-negative floats; NaN sorts above +inf, so it
+// wins as LAPACK's i*amax would report it), 0 for "no candidate".  A wave max
+// of the key is one DPP v_max_u32 per stage instead of a (double, index) pair
+// through compare / select chains; magnitudes within one fp32 ulp tie and the
+// lowest lane wins, which is as good a tournament pivot.
+template <typename T>
+__device__ inline uint32_t pivot_key(T v) {
+    return 1u + __float_as_uint(float(abs1(v)));
+}
+
+__device__ inline uint32_t wave_max_u32(uint32_t k) {
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x124, 0xF, 0xF, false));  // row_ror:4
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x128, 0xF, 0xF, false));  // row_ror:8
+    uint32_t a = __builtin_amdgcn_readlane(k, 0), b = __builtin_amdgcn_readlane(k, 16);
+    uint32_t c = __builtin_amdgcn_readlane(k, 32), d = __builtin_amdgcn_readlane(k, 48);
+    return max(max(a, b), max(c, d));
+}
+
+// Reciprocal for the elimination multipliers: v_rcp + two Newton steps for
+// fp64 (the correctly rounded division sequence is ~10 dependent fp64 ops on
+// the critical path of every step).
+__device__ inline double fast_rcp(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ inline float fast_rcp(float d) { return 1.0f / d; }
+template <typename R>
+__device__ inline cplx<R> fast_rcp(cplx<R> d) { return one<cplx<R>>() / d; }
+
+// Wave-per-leaf / wave-per-node tournament round (see header).  Leaves
+// (cand_in == nullptr) take rows [r + 64 RPT b, ...); nodes take the candidate
+// lists of 2 RPT children.  Rows are read from the unmodified panel.
+template <typename T, int RPT>
+__global__ __launch_bounds__(64) void tslu_select_wave_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
+                                                              const int* cand_in, const int* cnt_in, int nin,
+                                                              int* cand_out, int* cnt_out, T* lu_out) {
+    SLATE_PANEL_WAVE_PRIO();
+    __shared__ T prow[TW];
+    const int lane = threadIdx.x;
+    int idx[RPT];
+    bool act[RPT];
+    T a[RPT][TW];
+    #pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+        idx[i] = INT_MAX;
+        act[i] = false;
+        if (cand_in == nullptr) {
+            int64_t g = r + (int64_t)blockIdx.x * (64 * RPT) + i * 64 + lane;
+            if (g < m) { idx[i] = (int)g; act[i] = true; }
+        } else {
+            int e = i * 64 + lane;
+            int child = blockIdx.x * (64 * RPT / TW) + e / TW, k = e % TW;
+            if (child < nin && k < cnt_in[child]) { idx[i] = cand_in[child * TW + k]; act[i] = true; }
+        }
+    }
+    #pragma unroll
+    for (int j = 0; j < TW; ++j)
+        #pragma unroll
+        for (int i = 0; i < RPT; ++i) a[i][j] = (act[i] && j < nn) ? A[idx[i] + j * lda] : zero<T>();
+
+    int cnt = 0;
+    bool done = false;
+    // compile-time step index: every a[i][j] access is static (a runtime k
+    // would push a[][] to scratch)
+    static_for<0, TW>([&](auto kc) {
+        constexpr int k = decltype(kc)::value;
+        if (k < nn && !done) {
+            // my best row: first of the largest keys
+            uint32_t key = 0;
+            int bi = 0;
+            #pragma unroll
+            for (int i = 0; i < RPT; ++i) {
+                const uint32_t ki = act[i] ? pivot_key(a[i][k]) : 0u;
+                if (ki > key) { key = ki; bi = i; }
+            }
+            const uint32_t kmax = wave_max_u32(key);
+            if (kmax == 0) {
+                done = true;                       // uniform: no candidates left
+            } else {
+                const unsigned long long win = __ballot(key == kmax);
+                const int wl = __ffsll((long long)win) - 1;
+                const bool mine = (lane == wl);
+                int myid = INT_MAX;
+                #pragma unroll
+                for (int i = 0; i < RPT; ++i) {
+                    if (mine && bi == i) {
+                        myid = idx[i];
+                        #pragma unroll
+                        for (int j = k; j < TW; ++j) prow[j] = a[i][j];
+                        act[i] = false;
+                        // final round: the winners in pivot order ARE the
+                        // permuted top block, and this GEPP its LU: row k =
+                        // multipliers (j < k) and the U row (j >= k)
+                        if (lu_out) {
+                            #pragma unroll
+                            for (int j = 0; j < TW; ++j) if (j < nn) lu_out[k + j * TW] = a[i][j];
+                        }
+                    }
+                }
+                const int id = __builtin_amdgcn_readlane(myid, wl);
+                // one wave: its LDS operations complete in order; the fence
+                // keeps the compiler from moving the reads above the writes
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                const T d = prow[k];
+                const T rd = is_zero(d) ? zero<T>() : fast_rcp(d);
+                #pragma unroll
+                for (int i = 0; i < RPT; ++i) {
+                    if (act[i]) {
+                        const T l = a[i][k] * rd;
+                        #pragma unroll
+                        for (int j = k + 1; j < TW; ++j) a[i][j] -= l * prow[j];
+                        a[i][k] = l;
+                    }
+                }
+                if (lane == 0) cand_out[blockIdx.x * TW + k] = id;
+                cnt = k + 1;
+                __builtin_amdgcn_wave_barrier();   // prow is rewritten next step
+            }
+        }
+    });
+    if (lane == 0) cnt_out[blockIdx.x] = cnt;
+}
+
 // Winners -> LAPACK ipiv (sequential interchanges with row r+k) and the net
 // row permutation as (pos <- orig).  One wave: lanes 0..31 track positions
 // r..r+31, lanes 32..63 the winners that lie below; an interchange swaps the
@@ -204,42 +349,67 @@ __device__ inline void mfma16(double a, double b, double (&c)[4]) {
 }
 
 // Top block LU without pivoting (one wave; lane i = row i, readlane
-// broadcasts) and column-oriented inverse of U11 (lane j = column j of
-// U11^{-1}, back substitution).  Writes Uinv[i*TW + j] (zero outside the nn x
-// nn triangle); returns the first zero pivot (or -1).
+// broadcasts) -- or, with lu_in, the LU the final tournament round already
+// produced -- and the inverse of U11 with lane j holding column j: per step k
+// (backward) one scaling and k independent FMAs against U's column k read
+// from LDS (axpy form: no serial dot-product chain and no divide per step).
+// Writes Uinv[i*TW + j] (zero outside the nn x nn triangle); returns the first
+// zero pivot (or -1).
 template <typename T>
-__device__ inline int tslu_top_factor(int nn, const T* Utop, T (&a)[TW], T* Uinv) {
+__device__ inline int tslu_top_factor(int nn, const T* Utop, const T* lu_in, T (&a)[TW], T* Uinv, T (*Us)[TW + 1],
+                                      T* Rd) {
     const int tid = threadIdx.x & 63;
     const bool live = tid < nn;
-    #pragma unroll
-    for (int j = 0; j < TW; ++j) a[j] = (live && j < nn) ? Utop[j * TW + tid] : zero<T>();
     int bad = -1;
-    #pragma unroll
-    for (int k = 0; k < TW; ++k) {
-        if (k < nn) {
-            T d = bcast_lane(a[k], k);
-            if (is_zero(d) && bad < 0) bad = k;
-            T rd = is_zero(d) ? zero<T>() : one<T>() / d;
-            T lk = a[k] * rd;
-            #pragma unroll
-            for (int j = k + 1; j < TW; ++j) {
-                T ukj = bcast_lane(a[j], k);
-                if (tid > k) a[j] -= lk * ukj;
+    if (lu_in) {
+        #pragma unroll
+        for (int j = 0; j < TW; ++j) a[j] = (live && j < nn) ? lu_in[tid + j * TW] : zero<T>();
+        T dg = zero<T>();
+        #pragma unroll
+        for (int j = 0; j < TW; ++j) if (j == tid) dg = a[j];
+        const unsigned long long z = __ballot(live && is_zero(dg));
+        bad = z ? __ffsll((long long)z) - 1 : -1;
+    } else {
+        #pragma unroll
+        for (int j = 0; j < TW; ++j) a[j] = (live && j < nn) ? Utop[j * TW + tid] : zero<T>();
+        #pragma unroll
+        for (int k = 0; k < TW; ++k) {
+            if (k < nn) {
+                T d = bcast_lane(a[k], k);
+                if (is_zero(d) && bad < 0) bad = k;
+                T rd = is_zero(d) ? zero<T>() : one<T>() / d;
+                T lk = a[k] * rd;
+                #pragma unroll
+                for (int j = k + 1; j < TW; ++j) {
+                    T ukj = bcast_lane(a[j], k);
+                    if (tid > k) a[j] -= lk * ukj;
+                }
+                if (tid > k) a[k] = lk;
             }
-            if (tid > k) a[k] = lk;
         }
     }
+    if (tid < TW) {
+        T dg = zero<T>();
+        #pragma unroll
+        for (int j = 0; j < TW; ++j) {
+            Us[tid][j] = a[j];
+            if (j == tid) dg = a[j];
+        }
+        Rd[tid] = (live && !is_zero(dg)) ? fast_rcp(dg) : zero<T>();
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     T x[TW];
     #pragma unroll
-    for (int i = TW - 1; i >= 0; --i) {
-        x[i] = zero<T>();
-        if (i < nn) {
-            T s = (i == tid) ? one<T>() : zero<T>();
+    for (int i = 0; i < TW; ++i) x[i] = (i == tid && live) ? one<T>() : zero<T>();
+    #pragma unroll
+    for (int k = TW - 1; k >= 0; --k) {
+        if (k < nn) {
+            const T xk = x[k] * Rd[k];
+            x[k] = xk;
             #pragma unroll
-            for (int k = i + 1; k < TW; ++k)
-                if (k < nn) s -= bcast_lane(a[k], i) * x[k];
-            T d = bcast_lane(a[i], i);
-            x[i] = is_zero(d) ? zero<T>() : s / d;
+            for (int i = 0; i < k; ++i) x[i] -= Us[i][k] * xk;
         }
     }
     if (tid < TW) {
@@ -253,13 +423,16 @@ __device__ inline int tslu_top_factor(int nn, const T* Utop, T (&a)[TW], T* Uinv
 // top block and the info flag.  256 threads = 4 waves x 4 slabs of 16 rows.
 template <typename T>
 __global__ __launch_bounds__(256) void tslu_rows_kernel(int64_t m, int64_t r, int nn, T* A, int64_t lda,
-                                                        const T* Utop, int* info, int64_t info_offset) {
+                                                        const T* Utop, const T* lu_in, int* info,
+                                                        int64_t info_offset) {
     SLATE_PANEL_WAVE_PRIO();
     __shared__ T Uinv[TW * TW];
+    __shared__ T Us[TW][TW + 1];
+    __shared__ T Rd[TW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (w == 0) {
         T a[TW];
-        int bad = tslu_top_factor<T>(nn, Utop, a, Uinv);
+        int bad = tslu_top_factor<T>(nn, Utop, lu_in, a, Uinv, Us, Rd);
         if (blockIdx.x == 0) {
             if (lane < nn) {
                 #pragma unroll
@@ -329,8 +502,8 @@ __global__ __launch_bounds__(256) void tslu_rows_kernel(int64_t m, int64_t r, in
 constexpr int64_t kUtopI64 = 2 * TW * TW;
 
 int64_t tslu_workspace(int64_t rows) {
-    int64_t nleaf = (rows + TR - 1) / TR;
-    return kUtopI64 + nleaf * TW + nleaf + 64;
+    int64_t nleaf = (rows + 63) / 64;      // smallest leaf: one wave, one row per lane
+    return 2 * kUtopI64 + nleaf * TW + nleaf + 64;
 }
 
 template <typename T>
@@ -338,30 +511,52 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
                  int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
-    int nleaf = (int)((rows + TR - 1) / TR);
+    static const bool wg_form = [] { const char* e = std::getenv("SLATE_TSLU_WG"); return e && std::atoi(e) != 0; }();
+    const int64_t nleaf_max = (rows + 63) / 64;
     T* Utop = reinterpret_cast<T*>(work);
-    int* candA = reinterpret_cast<int*>(work + kUtopI64);
-    int* candB = candA + (int64_t)nleaf * TW;
-    int* cntA = candB + (int64_t)nleaf * TW;
-    int* cntB = cntA + nleaf + 1;
-    hipLaunchKernelGGL((tslu_select_kernel<T, TR>), dim3(nleaf), dim3(TR), 0, s, m, r, nn, Ablk, lda,
-                       (const int*)nullptr, (const int*)nullptr, 0, candA, cntA);
-    int n = nleaf;
-    while (n > 1) {
-        int n2 = (n + FANIN - 1) / FANIN;
-        hipLaunchKernelGGL((tslu_select_kernel<T, NODE_NT>), dim3(n2), dim3(NODE_NT), 0, s, m, r, nn, Ablk, lda,
-                           (const int*)candA, (const int*)cntA, n, candB, cntB);
-        std::swap(candA, candB);
-        std::swap(cntA, cntB);
-        n = n2;
+    T* LU11 = reinterpret_cast<T*>(work + kUtopI64);      // final round's LU of the winners
+    T* lu_final = nullptr;
+    int* candA = reinterpret_cast<int*>(work + 2 * kUtopI64);
+    int* candB = candA + nleaf_max * TW;
+    int* cntA = candB + nleaf_max * TW;
+    int* cntB = cntA + nleaf_max + 1;
+    if (wg_form) {
+        int nleaf = (int)((rows + TR - 1) / TR);
+        hipLaunchKernelGGL((tslu_select_kernel<T, TR>), dim3(nleaf), dim3(TR), 0, s, m, r, nn, Ablk, lda,
+                           (const int*)nullptr, (const int*)nullptr, 0, candA, cntA);
+        int n = nleaf;
+        while (n > 1) {
+            int n2 = (n + FANIN - 1) / FANIN;
+            hipLaunchKernelGGL((tslu_select_kernel<T, NODE_NT>), dim3(n2), dim3(NODE_NT), 0, s, m, r, nn, Ablk, lda,
+                               (const int*)candA, (const int*)cntA, n, candB, cntB);
+            std::swap(candA, candB);
+            std::swap(cntA, cntB);
+            n = n2;
+        }
+    } else {
+        constexpr int RPT = (sizeof(T) >= 16) ? 1 : int(16 / sizeof(T));
+        constexpr int LEAF = 64 * RPT, FAN = LEAF / TW;
+        int nleaf = (int)((rows + LEAF - 1) / LEAF);
+        lu_final = LU11;
+        hipLaunchKernelGGL((tslu_select_wave_kernel<T, RPT>), dim3(nleaf), dim3(64), 0, s, m, r, nn, Ablk, lda,
+                           (const int*)nullptr, (const int*)nullptr, 0, candA, cntA, nleaf == 1 ? LU11 : nullptr);
+        int n = nleaf;
+        while (n > 1) {
+            int n2 = (n + FAN - 1) / FAN;
+            hipLaunchKernelGGL((tslu_select_wave_kernel<T, RPT>), dim3(n2), dim3(64), 0, s, m, r, nn, Ablk, lda,
+                               (const int*)candA, (const int*)cntA, n, candB, cntB, n2 == 1 ? LU11 : nullptr);
+            std::swap(candA, candB);
+            std::swap(cntA, cntB);
+            n = n2;
+        }
     }
     const int64_t c0 = (Ablk - Apanel) / lda;
     const int pgrid = (int)std::min<int64_t>((ncols + 3) / 4, 1024);
     hipLaunchKernelGGL(tslu_permute_kernel<T>, dim3(pgrid), dim3(256), 0, s, (int)r, nn, c0, Apanel, lda, ncols,
                        (const int*)candA, (const int*)cntA, ipiv, perm, Utop);
     const int rgrid = (int)std::max<int64_t>(1, (rows - nn + 255) / 256);
-    hipLaunchKernelGGL(tslu_rows_kernel<T>, dim3(rgrid), dim3(256), 0, s, m, r, nn, Ablk, lda, (const T*)Utop, info,
-                       info_offset);
+    hipLaunchKernelGGL(tslu_rows_kernel<T>, dim3(rgrid), dim3(256), 0, s, m, r, nn, Ablk, lda, (const T*)Utop,
+                       (const T*)lu_final, info, info_offset);
 }
 
 #define SLATE_INST_TSLU(T) \

@@ -768,9 +768,16 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             range_tasks(device::kLookaheadQueue, j, j + 1);
         if (jla_end < nt) range_tasks(device::kTrailQueue, jla_end, nt);
 
-        // left columns [0, k): apply the step's interchanges (deferred queue)
+        // left columns [0, k): apply the step's interchanges.  Off the
+        // trailing queue (the comm queue is idle on a p == 1 grid): nothing
+        // on the critical path reads these columns again, so the memory-bound
+        // swaps overlap the trailing GEMM instead of serializing before it
+        static const int left_q = [] {
+            const char* e = std::getenv("SLATE_LU_LEFT_TRAIL");   // A/B: 1 = back on the trailing queue
+            return (e && std::atoi(e)) ? device::kTrailQueue : device::kCommQueue;
+        }();
         if (k > 0 && pivot) {
-            S.task(device::kTrailQueue, {tBc}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
+            S.task(left_q, {tBc}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
                 auto cc = lcols(0, k);
                 permute(c, cc.first, cc.second);
             });

@@ -754,8 +754,7 @@ void form_v(Ctx const& c, int64_t m, int64_t k, T const* A, int64_t lda, T* W, i
                 W[i + j * ldw] = i < j ? T(0) : (i == j ? T(1) : A[i + j * lda]);
         return;
     }
-    dcopy(c.stream, m, k, A, lda, W, ldw);
-    dset(c.stream, 'U', std::min(m, k), k, T(0), T(1), W, ldw);
+    kd::form_v(m, k, int64_t(0), dptr(A), lda, dptr(W), ldw, c.stream);
 }
 
 template <typename T>
@@ -815,6 +814,16 @@ struct QrPanelDev {
     Ctx ctx;
     real_type<T>* psum; T* alpha; T* pdots; T* work; int64_t work_elems; T* scal;
     T* tsqr_work = nullptr;
+    // explicit unit-lower V of the whole panel (ld m), filled once per narrow
+    // block: the recursion's larfb / merge GEMMs read it directly instead of
+    // forming V again (copy + triangle set) at every level
+    T* Vp = nullptr; int64_t ldvp = 0;
+
+    // (all m rows of the block's columns: the zeros above its diagonal are
+    // read by the outer levels' products, whose V spans several blocks)
+    void keep_v(int64_t c0, int64_t kmax) {
+        kd::form_v(m, kmax, c0, dptr(A0 + c0 * lda), lda, dptr(Vp + c0 * ldvp), ldvp, s);
+    }
 
     // narrow block [c0, c0+nn): Householder columns + T block (nn x nn at Tm[c0, c0])
     void narrow(int64_t c0, int64_t nn) {
@@ -827,6 +836,7 @@ struct QrPanelDev {
             // 2 log8(rows/256) + 4 launches per narrow block instead of two per column
             kd::qr_tsqr_narrow<DT>(m - c0, int(nn), A + c0 + c0 * lda, lda, dptr(Tm + c0 + c0 * ldt), ldt,
                                    dptr(tau + c0), dptr(tsqr_work), s);
+            keep_v(c0, kmax);
             return;
         }
         if (use_persistent(c0)) {
@@ -890,14 +900,35 @@ struct QrPanelDev {
 
     // T block of the narrow block: S = V^H V then the larft recurrence
     void t_block(int64_t c0, int64_t kmax) {
-        Scratch sc(ctx);
         int64_t mv = m - c0;
-        T* Vx = sc.alloc<T>(size_t(mv) * kmax);
-        form_v(ctx, mv, kmax, A0 + c0 + c0 * lda, lda, Vx, mv);
+        keep_v(c0, kmax);
+        T* Vx = Vp + c0 + c0 * ldvp;
         T* Tb = Tm + c0 + c0 * ldt;
-        kd::tsip(mv, int(kmax), int(kmax), dval(T(1)), dptr(Vx), mv, dptr(Vx), mv, dval(T(0)), dptr(Tb), ldt,
+        kd::tsip(mv, int(kmax), int(kmax), dval(T(1)), dptr(Vx), ldvp, dptr(Vx), ldvp, dval(T(0)), dptr(Tb), ldt,
                  dptr(work), work_elems, s);
         kd::larft_small(int(kmax), dptr(tau + c0), dptr(Tb), ldt, s);
+    }
+
+    // C -= V T^H V^H C for the panel's block [c0, c0 + k) applied to
+    // columns [cc, cc + n) (V explicit in Vp)
+    void apply_left(int64_t c0, int64_t k, int64_t cc, int64_t n) {
+        const int64_t mv = m - c0;
+        if (mv <= 0 || n <= 0 || k <= 0) return;
+        Scratch sc(ctx);
+        const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+        T const* V = Vp + c0 + c0 * ldvp;
+        T* C = A0 + c0 + cc * lda;
+        T* W = sc.alloc<T>(size_t(k) * n);
+        T* W2 = sc.alloc<T>(size_t(k) * n);
+        if (n <= 32 && k <= 32) {   // tsip handles m, n <= 32
+            T* wk = sc.alloc<T>(size_t(1) << 20);
+            kd::tsip(mv, int(k), int(n), dval(T(1)), dptr(V), ldvp, dptr(C), lda, dval(T(0)), dptr(W), k, dptr(wk),
+                     int64_t(1) << 20, s);
+        } else {
+            dgemm(s, 'G', cT, Op::NoTrans, k, n, mv, T(1), V, ldvp, C, lda, T(0), W, k);
+        }
+        dgemm(s, 'G', cT, Op::NoTrans, k, n, k, T(1), Tm + c0 + c0 * ldt, ldt, W, k, T(0), W2, k);
+        dgemm(s, 'G', Op::NoTrans, Op::NoTrans, mv, n, k, T(-1), V, ldvp, W2, k, T(1), C, lda);
     }
 
     void rec(int64_t c0, int64_t nn) {
@@ -907,27 +938,26 @@ struct QrPanelDev {
         int64_t n1 = roundup(ceildiv(nn, 2), W), n2 = nn - n1;
         rec(c0, n1);
         // apply H1^H to the right columns
-        larfb(ctx, Side::Left, Op::ConjTrans, m - c0, n2, std::min(n1, m - c0), A0 + c0 + c0 * lda, lda,
-              Tm + c0 + c0 * ldt, ldt, A0 + c0 + (c0 + n1) * lda, lda);
+        apply_left(c0, std::min(n1, m - c0), c0 + n1, n2);
         rec(c0 + n1, n2);
         if (c0 + n1 >= m) return;
         // merge: T12 = -T11 (V1^H V2) T22, V1 rows from c0+n1, V2 rows from c0+n1
         int64_t k2 = std::min(n2, m - c0 - n1);
         Scratch sc(ctx);
         int64_t mv = m - c0 - n1;
-        T* V2 = sc.alloc<T>(size_t(mv) * k2);
-        form_v(ctx, mv, k2, A0 + (c0 + n1) + (c0 + n1) * lda, lda, V2, mv);
+        T const* V2 = Vp + (c0 + n1) + (c0 + n1) * ldvp;
         T* S = sc.alloc<T>(size_t(n1) * k2);
         Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
         // V1 rows [c0+n1, m) are plain stored (below V1's diagonal block)
-        dgemm(s, 'G', cT, Op::NoTrans, n1, k2, mv, T(1), A0 + (c0 + n1) + c0 * lda, lda, V2, mv, T(0), S, n1);
+        dgemm(s, 'G', cT, Op::NoTrans, n1, k2, mv, T(1), A0 + (c0 + n1) + c0 * lda, lda, V2, ldvp, T(0), S, n1);
         T* S2 = sc.alloc<T>(size_t(n1) * k2);
         dgemm(s, 'G', Op::NoTrans, Op::NoTrans, n1, k2, k2, T(1), S, n1, Tm + (c0 + n1) + (c0 + n1) * ldt, ldt,
               T(0), S2, n1);
-        // T11 is upper triangular: zero its strict lower part in the product via trmm
-        trmm(ctx, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, n1, k2, T(-1),
-             Tm + c0 + c0 * ldt, ldt, S2, n1);
-        dcopy(s, n1, k2, S2, n1, Tm + c0 + (c0 + n1) * ldt, ldt);
+        // T11 is stored upper triangular with explicit zeros below (narrow
+        // blocks and merges write it so, and T starts zeroed): the trmm is a
+        // plain GEMM straight into T12
+        dgemm(s, 'G', Op::NoTrans, Op::NoTrans, n1, k2, n1, T(-1), Tm + c0 + c0 * ldt, ldt, S2, n1, T(0),
+              Tm + c0 + (c0 + n1) * ldt, ldt);
     }
 };
 
@@ -953,6 +983,8 @@ void geqrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, T* tau, 
     P.work_elems = int64_t(1) << 20;
     P.work = sc.alloc<T>(P.work_elems);
     P.tsqr_work = sc.alloc<T>(size_t(kd::qr_tsqr_workspace(m)));
+    P.ldvp = m;
+    P.Vp = sc.alloc<T>(size_t(m) * k);
     // zero all of T (n x n when the panel is wider than tall: the driver's
     // block update multiplies by the full nb x nb T)
     int64_t nt_ = std::min(n, ldt);

@@ -12,9 +12,12 @@ nb = int(sys.argv[2]) if len(sys.argv) > 2 else 512
 reps = 5
 torch.manual_seed(0)
 A0 = torch.rand(nb, m, dtype=torch.float64, device="cuda") * 2 - 1   # column-major m x nb
+ONLY = os.environ.get("PANELS", "")
 for name, fn in [("getrf_partial", lambda A: s.ops.getrf_panel(A, tournament=False)),
                  ("getrf_tournament", lambda A: s.ops.getrf_panel(A, tournament=True)),
                  ("geqrf", lambda A: s.ops.geqrf_panel(A))]:
+    if ONLY and not any(o in name for o in ONLY.split(",")):
+        continue
     ts = []
     for r in range(reps + 1):
         A = A0.clone()

@@ -1,0 +1,20 @@
+#!/bin/bash
+# tournament v2 (32-bit keys, LU11 from the final round, axpy U11 inverse):
+# tests, isolated panel A/B, dgetrf bench A/B of the left-swap queue, trace
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+O=gpurun_out/tslu2; mkdir -p $O
+timeout -k 10 400 python -u -m pytest tests/test_gpu.py -x -q --timeout 120 --timeout-method thread -k "getrf or permute or trsm or gesv or lu" > $O/pytest.log 2>&1 || { tail -30 $O/pytest.log; exit 1; }
+tail -2 $O/pytest.log
+for mode in 0 1; do
+  for m in 2048 32768; do
+    SLATE_TSLU_WG=$mode PANELS=tournament timeout -k 10 120 python3 scripts/bench_panel.py $m 1024 2>&1 | grep -v "^W2026\|amdgpu.ids" | sed "s/^/wg=$mode /" >> $O/panel.txt || exit 1
+  done
+done
+cat $O/panel.txt
+for v in "" "SLATE_LU_LEFT_TRAIL=1" "SLATE_TSLU_WG=1"; do
+  env $v timeout -k 10 300 python3 bench.py --routines dgetrf --steps 1 --warmup 1 --extras none > $O/bench.log 2>&1 || { tail -20 $O/bench.log; exit 1; }
+  echo "== $v"; grep -E "timed|error" $O/bench.log
+done
+ROUTINES=dgetrf bash scripts/r3_tail.sh > /dev/null 2>&1 || exit 1
+head -14 gpurun_out/tail/dgetrf_summary.txt; grep -A12 "gemm-covered" gpurun_out/tail/dgetrf_summary.txt | head -14; tail -1 gpurun_out/tail/dgetrf_steps.txt

@@ -10,7 +10,7 @@ rows = sqlite3.connect(a.db).execute("select name, start, end, stream_id from ke
 t1 = max(r[2] for r in rows)
 w0 = t1 - a.from_end_ms * 1e6; w1 = w0 + a.ms * 1e6
 win = [r for r in rows if r[1] >= w0 and r[1] < w1]
-short = lambda n: n.split("(")[0].replace("void ", "").replace("slate_amd::dev::", "").replace("(anonymous namespace)::", "")[:60]
+short = lambda n: n.replace("(anonymous namespace)::", "").split("(")[0].replace("void ", "").replace("slate_amd::dev::", "")[:60]
 by = collections.defaultdict(list)
 for r in win: by[r[3]].append(r)
 for sid, rs in by.items():
