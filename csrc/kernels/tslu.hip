@@ -9,14 +9,14 @@
 // MI355X design: the tournament is played on a 32-column narrow block inside
 // the recursive device panel (local_blas.cc LuPanelDev), so a 32768-row panel
 // costs four or five launches instead of two launches per column:
-//   select  one WAVE per leaf / tree node, RPT = 16 / sizeof(T) rows per lane
-//           held in VGPRs (fp64: 128-row leaves, nodes of 4 x 32 candidates):
-//           GEPP with a DPP (quad_perm/row_ror) + v_readlane wave argmax and
-//           a wave-local LDS broadcast of the pivot row -- no workgroup
-//           barrier in the 32-step loop (measured ~46-59 us per launch for the
-//           earlier 256/512-thread workgroup form with two barriers per step,
-//           which made the panel latency-bound at small M).  SLATE_TSLU_WG=1
-//           selects the workgroup form (A/B).
+//   select  leaves: 256 rows per workgroup, one row per thread held in VGPRs;
+//           tree nodes: 512-thread workgroups, fan-in 16 (16 x 32 candidates).
+//           GEPP per step: a 32-bit key DPP max inside each wave, the wave's
+//           best row published to LDS, ONE workgroup barrier, then every
+//           thread picks the best slot (measured 46-59 us per launch for the
+//           earlier two-barrier (value, index) form at small M, which made the
+//           panel latency-bound).  The final round also emits the LU of the
+//           winners, so the rows kernel does not refactor the top block.
 //   permute each workgroup owns panel columns; it re-derives the interchanges
 //           from the winners in one wave (ballot/readlane, all scalar), applies
 //           the net row permutation to its columns and copies the permuted
@@ -78,72 +78,6 @@ __device__ inline void wave_argmax(R& v, int& id) {
     v = bv; id = bi;
 }
 
-// One tournament round: each workgroup factors up to NT rows x nn columns with
-// partial pivoting and emits its (up to nn) pivot rows, in pivot order.
-// Leaves (cand_in == nullptr) take rows [r + NT*b, ...); nodes take the
-// candidate lists of NT/TW children.  Rows are read from the unmodified panel
-// (CALU plays every round on original rows).
-template <typename T, int NT>
-__global__ __launch_bounds__(NT) void tslu_select_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
-                                                         const int* cand_in, const int* cnt_in, int nin,
-                                                         int* cand_out, int* cnt_out) {
-    SLATE_PANEL_WAVE_PRIO();
-    using R = real_t<T>;
-    constexpr int NW = NT / 64;
-    __shared__ R sv[2][NW];
-    __shared__ int si[2][NW];
-    __shared__ T prow[2][TW];
-    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-    int idx = INT_MAX;
-    bool act = false;
-    if (cand_in == nullptr) {
-        int64_t i = r + blockIdx.x * (int64_t)NT + tid;
-        if (i < m) { idx = (int)i; act = true; }
-    } else {
-        int child = blockIdx.x * (NT / TW) + tid / TW, k = tid % TW;
-        if (child < nin && k < cnt_in[child]) { idx = cand_in[child * TW + k]; act = true; }
-    }
-    T a[TW];
-    #pragma unroll
-    for (int j = 0; j < TW; ++j) a[j] = (act && j < nn) ? A[idx + j * lda] : zero<T>();
-
-    // (guarded, not `break`: the loop must fully unroll so a[] stays in VGPRs)
-    int cnt = 0;
-    bool done = false;
-    #pragma unroll
-    for (int k = 0; k < TW; ++k) {
-        if (k < nn && !done) {
-            R v = act ? abs1(a[k]) : R(-1);
-            int id = act ? idx : INT_MAX;
-            wave_argmax(v, id);
-            if (lane == 0) { sv[k & 1][w] = v; si[k & 1][w] = id; }
-            __syncthreads();
-            v = sv[k & 1][0]; id = si[k & 1][0];
-            #pragma unroll
-            for (int q = 1; q < NW; ++q) argmax_pick(v, id, sv[k & 1][q], si[k & 1][q]);
-            if (id == INT_MAX) {
-                done = true;                       // uniform: no candidates left
-            } else {
-                if (act && idx == id) {
-                    #pragma unroll
-                    for (int j = k; j < TW; ++j) prow[k & 1][j] = a[j];
-                    act = false;
-                }
-                __syncthreads();
-                if (act) {
-                    T d = prow[k & 1][k];
-                    T l = a[k] * (is_zero(d) ? zero<T>() : one<T>() / d);
-                    #pragma unroll
-                    for (int j = k + 1; j < TW; ++j) a[j] -= l * prow[k & 1][j];
-                }
-                if (tid == 0) cand_out[blockIdx.x * TW + k] = id;
-                cnt = k + 1;
-            }
-        }
-    }
-    if (tid == 0) cnt_out[blockIdx.x] = cnt;
-}
-
 // 32-bit pivot-search key of a candidate: 1 + the fp32 bit pattern of its
 // magnitude (monotonic for non-negative floats; NaN sorts above +inf, so it
 // wins as LAPACK's i*amax would report it), 0 for "no candidate".  A wave max
@@ -179,100 +113,85 @@ __device__ inline float fast_rcp(float d) { return 1.0f / d; }
 template <typename R>
 __device__ inline cplx<R> fast_rcp(cplx<R> d) { return one<cplx<R>>() / d; }
 
-// Wave-per-leaf / wave-per-node tournament round (see header).  Leaves
-// (cand_in == nullptr) take rows [r + 64 RPT b, ...); nodes take the candidate
-// lists of 2 RPT children.  Rows are read from the unmodified panel.
-template <typename T, int RPT>
-__global__ __launch_bounds__(64) void tslu_select_wave_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
-                                                              const int* cand_in, const int* cnt_in, int nin,
-                                                              int* cand_out, int* cnt_out, T* lu_out) {
+// One tournament round: each workgroup factors up to NT rows x nn columns with
+// partial pivoting and emits its (up to nn) pivot rows, in pivot order.
+// Leaves (cand_in == nullptr) take rows [r + NT*b, ...); nodes take the
+// candidate lists of NT/TW children.  Rows are read from the unmodified panel
+// (CALU plays every round on original rows).  One row per thread in VGPRs.
+// Per step ONE workgroup barrier: every wave finds its best row (32-bit key,
+// DPP max), and that row's lane publishes key, index and the whole row to the
+// wave's LDS slot; after the barrier every thread picks the best slot and
+// eliminates against its row.  Slots are double-buffered by step parity, so
+// the next step's writes never meet this step's reads.  With lu_out (the
+// final round, one workgroup) the winners' GEPP -- the LU of the permuted top
+// block -- is written out as well (multipliers below the diagonal).
+template <typename T, int NT>
+__global__ __launch_bounds__(NT) void tslu_select_kernel(int64_t m, int64_t r, int nn, const T* A, int64_t lda,
+                                                         const int* cand_in, const int* cnt_in, int nin,
+                                                         int* cand_out, int* cnt_out, T* lu_out) {
     SLATE_PANEL_WAVE_PRIO();
-    __shared__ T prow[TW];
-    const int lane = threadIdx.x;
-    int idx[RPT];
-    bool act[RPT];
-    T a[RPT][TW];
-    #pragma unroll
-    for (int i = 0; i < RPT; ++i) {
-        idx[i] = INT_MAX;
-        act[i] = false;
-        if (cand_in == nullptr) {
-            int64_t g = r + (int64_t)blockIdx.x * (64 * RPT) + i * 64 + lane;
-            if (g < m) { idx[i] = (int)g; act[i] = true; }
-        } else {
-            int e = i * 64 + lane;
-            int child = blockIdx.x * (64 * RPT / TW) + e / TW, k = e % TW;
-            if (child < nin && k < cnt_in[child]) { idx[i] = cand_in[child * TW + k]; act[i] = true; }
-        }
+    constexpr int NW = NT / 64;
+    __shared__ uint32_t skey[2][NW];
+    __shared__ int sidx[2][NW];
+    __shared__ T srow[2][NW][TW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    int idx = INT_MAX;
+    bool act = false;
+    if (cand_in == nullptr) {
+        int64_t i = r + blockIdx.x * (int64_t)NT + tid;
+        if (i < m) { idx = (int)i; act = true; }
+    } else {
+        int child = blockIdx.x * (NT / TW) + tid / TW, k = tid % TW;
+        if (child < nin && k < cnt_in[child]) { idx = cand_in[child * TW + k]; act = true; }
     }
+    T a[TW];
     #pragma unroll
-    for (int j = 0; j < TW; ++j)
-        #pragma unroll
-        for (int i = 0; i < RPT; ++i) a[i][j] = (act[i] && j < nn) ? A[idx[i] + j * lda] : zero<T>();
+    for (int j = 0; j < TW; ++j) a[j] = (act && j < nn) ? A[idx + j * lda] : zero<T>();
 
     int cnt = 0;
     bool done = false;
-    // compile-time step index: every a[i][j] access is static (a runtime k
-    // would push a[][] to scratch)
     static_for<0, TW>([&](auto kc) {
         constexpr int k = decltype(kc)::value;
+        constexpr int bf = k & 1;
         if (k < nn && !done) {
-            // my best row: first of the largest keys
-            uint32_t key = 0;
-            int bi = 0;
-            #pragma unroll
-            for (int i = 0; i < RPT; ++i) {
-                const uint32_t ki = act[i] ? pivot_key(a[i][k]) : 0u;
-                if (ki > key) { key = ki; bi = i; }
+            const uint32_t key = act ? pivot_key(a[k]) : 0u;
+            const uint32_t kw = wave_max_u32(key);
+            const unsigned long long win = __ballot(key == kw && kw != 0u);
+            const int wl = win ? __ffsll((long long)win) - 1 : 0;
+            if (lane == wl) {
+                skey[bf][w] = kw;
+                sidx[bf][w] = idx;
+                #pragma unroll
+                for (int j = 0; j < TW; ++j) srow[bf][w][j] = a[j];
             }
-            const uint32_t kmax = wave_max_u32(key);
-            if (kmax == 0) {
+            __syncthreads();
+            uint32_t kb = skey[bf][0];
+            int wb = 0;
+            #pragma unroll
+            for (int q = 1; q < NW; ++q) {
+                const uint32_t kq = skey[bf][q];
+                if (kq > kb) { kb = kq; wb = q; }
+            }
+            if (kb == 0u) {
                 done = true;                       // uniform: no candidates left
             } else {
-                const unsigned long long win = __ballot(key == kmax);
-                const int wl = __ffsll((long long)win) - 1;
-                const bool mine = (lane == wl);
-                int myid = INT_MAX;
-                #pragma unroll
-                for (int i = 0; i < RPT; ++i) {
-                    if (mine && bi == i) {
-                        myid = idx[i];
-                        #pragma unroll
-                        for (int j = k; j < TW; ++j) prow[j] = a[i][j];
-                        act[i] = false;
-                        // final round: the winners in pivot order ARE the
-                        // permuted top block, and this GEPP its LU: row k =
-                        // multipliers (j < k) and the U row (j >= k)
-                        if (lu_out) {
-                            #pragma unroll
-                            for (int j = 0; j < TW; ++j) if (j < nn) lu_out[k + j * TW] = a[i][j];
-                        }
-                    }
-                }
-                const int id = __builtin_amdgcn_readlane(myid, wl);
-                // one wave: its LDS operations complete in order; the fence
-                // keeps the compiler from moving the reads above the writes
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                const T d = prow[k];
+                const int id = sidx[bf][wb];
+                if (act && idx == id) act = false;
+                const T d = srow[bf][wb][k];
                 const T rd = is_zero(d) ? zero<T>() : fast_rcp(d);
-                #pragma unroll
-                for (int i = 0; i < RPT; ++i) {
-                    if (act[i]) {
-                        const T l = a[i][k] * rd;
-                        #pragma unroll
-                        for (int j = k + 1; j < TW; ++j) a[i][j] -= l * prow[j];
-                        a[i][k] = l;
-                    }
+                if (act) {
+                    const T l = a[k] * rd;
+                    #pragma unroll
+                    for (int j = k + 1; j < TW; ++j) a[j] -= l * srow[bf][wb][j];
+                    a[k] = l;
                 }
-                if (lane == 0) cand_out[blockIdx.x * TW + k] = id;
+                if (tid == 0) cand_out[blockIdx.x * TW + k] = id;
+                if (lu_out && tid < TW && tid < nn) lu_out[k + tid * TW] = srow[bf][wb][tid];
                 cnt = k + 1;
-                __builtin_amdgcn_wave_barrier();   // prow is rewritten next step
             }
         }
     });
-    if (lane == 0) cnt_out[blockIdx.x] = cnt;
+    if (tid == 0) cnt_out[blockIdx.x] = cnt;
 }
 
 // Winners -> LAPACK ipiv (sequential interchanges with row r+k) and the net
@@ -502,7 +421,7 @@ __global__ __launch_bounds__(256) void tslu_rows_kernel(int64_t m, int64_t r, in
 constexpr int64_t kUtopI64 = 2 * TW * TW;
 
 int64_t tslu_workspace(int64_t rows) {
-    int64_t nleaf = (rows + 63) / 64;      // smallest leaf: one wave, one row per lane
+    int64_t nleaf = (rows + TR - 1) / TR;
     return 2 * kUtopI64 + nleaf * TW + nleaf + 64;
 }
 
@@ -511,52 +430,33 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
                  int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
-    static const bool wg_form = [] { const char* e = std::getenv("SLATE_TSLU_WG"); return e && std::atoi(e) != 0; }();
-    const int64_t nleaf_max = (rows + 63) / 64;
+    const int64_t nleaf_max = (rows + TR - 1) / TR;
     T* Utop = reinterpret_cast<T*>(work);
     T* LU11 = reinterpret_cast<T*>(work + kUtopI64);      // final round's LU of the winners
-    T* lu_final = nullptr;
     int* candA = reinterpret_cast<int*>(work + 2 * kUtopI64);
     int* candB = candA + nleaf_max * TW;
     int* cntA = candB + nleaf_max * TW;
     int* cntB = cntA + nleaf_max + 1;
-    if (wg_form) {
-        int nleaf = (int)((rows + TR - 1) / TR);
-        hipLaunchKernelGGL((tslu_select_kernel<T, TR>), dim3(nleaf), dim3(TR), 0, s, m, r, nn, Ablk, lda,
-                           (const int*)nullptr, (const int*)nullptr, 0, candA, cntA);
-        int n = nleaf;
-        while (n > 1) {
-            int n2 = (n + FANIN - 1) / FANIN;
-            hipLaunchKernelGGL((tslu_select_kernel<T, NODE_NT>), dim3(n2), dim3(NODE_NT), 0, s, m, r, nn, Ablk, lda,
-                               (const int*)candA, (const int*)cntA, n, candB, cntB);
-            std::swap(candA, candB);
-            std::swap(cntA, cntB);
-            n = n2;
-        }
-    } else {
-        constexpr int RPT = (sizeof(T) >= 16) ? 1 : int(16 / sizeof(T));
-        constexpr int LEAF = 64 * RPT, FAN = LEAF / TW;
-        int nleaf = (int)((rows + LEAF - 1) / LEAF);
-        lu_final = LU11;
-        hipLaunchKernelGGL((tslu_select_wave_kernel<T, RPT>), dim3(nleaf), dim3(64), 0, s, m, r, nn, Ablk, lda,
-                           (const int*)nullptr, (const int*)nullptr, 0, candA, cntA, nleaf == 1 ? LU11 : nullptr);
-        int n = nleaf;
-        while (n > 1) {
-            int n2 = (n + FAN - 1) / FAN;
-            hipLaunchKernelGGL((tslu_select_wave_kernel<T, RPT>), dim3(n2), dim3(64), 0, s, m, r, nn, Ablk, lda,
-                               (const int*)candA, (const int*)cntA, n, candB, cntB, n2 == 1 ? LU11 : nullptr);
-            std::swap(candA, candB);
-            std::swap(cntA, cntB);
-            n = n2;
-        }
+    const int nleaf = (int)nleaf_max;
+    hipLaunchKernelGGL((tslu_select_kernel<T, TR>), dim3(nleaf), dim3(TR), 0, s, m, r, nn, Ablk, lda,
+                       (const int*)nullptr, (const int*)nullptr, 0, candA, cntA, nleaf == 1 ? LU11 : nullptr);
+    int n = nleaf;
+    while (n > 1) {
+        int n2 = (n + FANIN - 1) / FANIN;
+        hipLaunchKernelGGL((tslu_select_kernel<T, NODE_NT>), dim3(n2), dim3(NODE_NT), 0, s, m, r, nn, Ablk, lda,
+                           (const int*)candA, (const int*)cntA, n, candB, cntB, n2 == 1 ? LU11 : nullptr);
+        std::swap(candA, candB);
+        std::swap(cntA, cntB);
+        n = n2;
     }
+    const T* lu_final = LU11;
     const int64_t c0 = (Ablk - Apanel) / lda;
     const int pgrid = (int)std::min<int64_t>((ncols + 3) / 4, 1024);
     hipLaunchKernelGGL(tslu_permute_kernel<T>, dim3(pgrid), dim3(256), 0, s, (int)r, nn, c0, Apanel, lda, ncols,
                        (const int*)candA, (const int*)cntA, ipiv, perm, Utop);
     const int rgrid = (int)std::max<int64_t>(1, (rows - nn + 255) / 256);
     hipLaunchKernelGGL(tslu_rows_kernel<T>, dim3(rgrid), dim3(256), 0, s, m, r, nn, Ablk, lda, (const T*)Utop,
-                       (const T*)lu_final, info, info_offset);
+                       lu_final, info, info_offset);
 }
 
 #define SLATE_INST_TSLU(T) \

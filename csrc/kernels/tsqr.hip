@@ -41,12 +41,25 @@ __device__ inline double unit_phase(double b) { return b < 0.0 ? -1.0 : 1.0; }
 template <typename R>
 __device__ inline cplx<R> unit_phase(cplx<R> b) { return cplx<R>(b.re < R(0) ? R(-1) : R(1), R(0)); }
 
+__device__ inline double rcp_nr(double d) {
+    double r = __builtin_amdgcn_rcp(d);
+    double e = fma(-d, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-d, r, 1.0);
+    return fma(r, e, r);
+}
+__device__ inline float rcp_nr(float d) { return 1.0f / d; }
+template <typename R>
+__device__ inline cplx<R> rcp_nr(cplx<R> d) { return one<cplx<R>>() / d; }
+
 template <typename T>
 __global__ __launch_bounds__(256) void lu_sign_narrow_kernel(int64_t m, int64_t r, int nn, const T* Ain,
                                                              int64_t ldi, T* Aout, int64_t ldo, const T* Utop,
                                                              int64_t ldu, T in_scale, T* top, int64_t ldt, T* sgn) {
     SLATE_PANEL_WAVE_PRIO();
     __shared__ T Uinv[TW * TW];
+    __shared__ T Us[TW][TW + 1];
+    __shared__ T Rd[TW];
     const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
     if (w == 0) {
         const bool live = lane < nn;
@@ -62,7 +75,7 @@ __global__ __launch_bounds__(256) void lu_sign_narrow_kernel(int64_t m, int64_t 
                 T s = unit_phase(b);
                 T d = b + s;
                 if (lane == k) { a[k] = d; s_mine = s; }
-                T rd = one<T>() / d;
+                T rd = rcp_nr(d);
                 T lk = a[k] * rd;
                 #pragma unroll
                 for (int j = k + 1; j < TW; ++j) {
@@ -72,17 +85,30 @@ __global__ __launch_bounds__(256) void lu_sign_narrow_kernel(int64_t m, int64_t 
                 if (lane > k) a[k] = lk;
             }
         }
-        // U11^{-1}: lane j = column j (back substitution)
+        // U11^{-1}, lane j = column j, axpy-form back substitution against
+        // U's columns in LDS (independent FMAs per step)
+        if (lane < TW) {
+            T dg = zero<T>();
+            #pragma unroll
+            for (int j = 0; j < TW; ++j) {
+                Us[lane][j] = a[j];
+                if (j == lane) dg = a[j];
+            }
+            Rd[lane] = live ? rcp_nr(dg) : zero<T>();
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         T x[TW];
         #pragma unroll
-        for (int i = TW - 1; i >= 0; --i) {
-            x[i] = zero<T>();
-            if (i < nn) {
-                T sum = (i == lane) ? one<T>() : zero<T>();
+        for (int i = 0; i < TW; ++i) x[i] = (i == lane && live) ? one<T>() : zero<T>();
+        #pragma unroll
+        for (int k = TW - 1; k >= 0; --k) {
+            if (k < nn) {
+                const T xk = x[k] * Rd[k];
+                x[k] = xk;
                 #pragma unroll
-                for (int k = i + 1; k < TW; ++k)
-                    if (k < nn) sum -= bcast_lane(a[k], i) * x[k];
-                x[i] = sum / bcast_lane(a[i], i);
+                for (int i = 0; i < k; ++i) x[i] -= Us[i][k] * xk;
             }
         }
         if (lane < TW) {
@@ -98,16 +124,22 @@ __global__ __launch_bounds__(256) void lu_sign_narrow_kernel(int64_t m, int64_t 
     __syncthreads();
     const int64_t row = r + nn + blockIdx.x * (int64_t)256 + tid;
     if (row < m) {
-        T av[TW];
+        // row of L21 = A21 U11^{-1}: 32 independent accumulators (one serial
+        // dot product per output would chain 32 dependent FMAs 32 times)
+        T acc[TW];
         #pragma unroll
-        for (int k = 0; k < TW; ++k) av[k] = k < nn ? in_scale * Ain[row + (r + k) * ldi] : zero<T>();
-        #pragma unroll 1
-        for (int j = 0; j < nn; ++j) {
-            T sum = zero<T>();
-            #pragma unroll
-            for (int k = 0; k < TW; ++k) sum += av[k] * Uinv[k * TW + j];
-            Aout[row + (r + j) * ldo] = sum;
+        for (int j = 0; j < TW; ++j) acc[j] = zero<T>();
+        #pragma unroll
+        for (int k = 0; k < TW; ++k) {
+            if (k < nn) {
+                const T av = in_scale * Ain[row + (r + k) * ldi];
+                #pragma unroll
+                for (int j = 0; j < TW; ++j) acc[j] += av * Uinv[k * TW + j];
+            }
         }
+        #pragma unroll
+        for (int j = 0; j < TW; ++j)
+            if (j < nn) Aout[row + (r + j) * ldo] = acc[j];
     }
 }
 
@@ -398,14 +430,22 @@ __global__ __launch_bounds__(64) void qr_hr_finish_kernel(int nn, const T* LU, i
     const T si = sS[i];
     // row i of the top block: S R above/on the diagonal, Y1 strictly below
     for (int j = 0; j < nn; ++j) A[i + j * lda] = (i <= j) ? si * Rr[i + j * ldr] : sL[i][j];
-    // X Y1^H = Tw with Tw(i, j) = U'(i, j) conj(s_j) (i <= j): forward substitution over j
-    for (int j = 0; j < nn; ++j) {
-        T tw = (i <= j) ? sL[i][j] * conj(sS[j]) : zero<T>();
-        for (int l = 0; l < j; ++l) tw -= sX[i][l] * conj(sL[j][l]);
-        sX[i][j] = tw;
-        Tm[i + j * ldt] = tw;
+    // X Y1^H = Tw with Tw(i, j) = U'(i, j) conj(s_j) (i <= j): forward
+    // substitution along row i in axpy form (x_l final at step l, then one
+    // independent FMA per later entry; no serial dot-product chain)
+    T acc[TW];
+    #pragma unroll
+    for (int j = 0; j < TW; ++j) acc[j] = (i <= j && j < nn) ? sL[i][j] * conj(sS[j]) : zero<T>();
+    #pragma unroll
+    for (int l = 0; l < TW; ++l) {
+        if (l < nn) {
+            const T xl = acc[l];
+            Tm[i + l * ldt] = xl;
+            if (l == i) tau[i] = xl;
+            #pragma unroll
+            for (int j = l + 1; j < TW; ++j) acc[j] -= xl * conj(sL[j][l]);
+        }
     }
-    tau[i] = sX[i][i];
 }
 
 }  // namespace

@@ -592,14 +592,19 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     }();
     const bool use_tn = tn_env && !is_complex_v<T> && target == Target::Devices;
     std::vector<Work<T>> W(R), WU(R), WI(R), WLT(R);
-    std::vector<Work<int64_t>> PV(R);      // [ipiv(kb) | dst(2kb) | src(2kb) | count]
+    // pivot slots live in a deeper ring than the panel buffers: the left
+    // swaps of step k (comm queue, off the critical path) read PV up to RP
+    // steps later before panel k + RP may rewrite it (token tPV, WAR)
+    const int RP = R + 8;
+    std::vector<Work<int64_t>> PV(RP);     // [ipiv(kb) | dst(2kb) | src(2kb) | count]
     for (int r = 0; r < R; ++r) {
         W[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
         WU[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         WI[r].resize(target, size_t(nb) * nb);
         if (use_tn) WLT[r].resize(target, size_t(nb) * std::max<int64_t>(mloc, 1));
-        PV[r].resize(target, size_t(5 * nb + 8));
+        (void)0;
     }
+    for (int r = 0; r < RP; ++r) PV[r].resize(target, size_t(5 * nb + 8));
     Work<int64_t> perm(target, size_t(std::max<int64_t>(m, 1)));
     Work<int> dinfo(target, 1);
     // every step's panel-relative pivots, copied to the host once at the end
@@ -620,7 +625,9 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         const int64_t lr_k = lrow_of(A, k), lr_k1 = lrow_of(A, k + 1);
         const int64_t lc_k = in_col ? lcol_of(A, k) : 0;
         const int slot = int(k % R);
-        int64_t* pv = PV[slot].data();
+        const int pvs = int(k % RP);
+        int64_t* pv = PV[pvs].data();
+        const int64_t tPV = Sched::tok(14, pvs);
         int64_t* pv_ipiv = pv;
         int64_t* pv_dst = pv + nb;
         int64_t* pv_src = pv + 3 * nb;
@@ -628,7 +635,8 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
         // ------------------------------------------------------------ panel
         if (in_col) {
-            S.task(1, {}, {Sched::col(k), tPanel}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pv_dst, pv_src](lb::Ctx const& c) {
+            // (writes PV[pvs]: tPV orders it after that slot's last readers)
+            S.task(1, {}, {Sched::col(k), tPanel, tPV}, [&, k, kb, kk, M, kd, lr_k, lc_k, pv_ipiv, pv_dst, pv_src](lb::Ctx const& c) {
                 trace::Block t2("getrf_panel");
                 T* ap = a + lr_k + lc_k * lda;
                 lb::getrf_panel(c, M, kb, ap, lda, pv_ipiv, perm.data(), dinfo.data(), kk, pivot, tnt, thresh);
@@ -651,9 +659,9 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
         // ------------------------------- (ipiv, pairs) along the process row
         // (critical path: on the panel queue over the fast-lane row comm)
-        S.task(1, {tPanel}, {tBc}, [&, k, kd, slot, pv_ipiv](lb::Ctx const& c) {
+        S.task(1, {tPanel}, {tBc, tPV}, [&, k, kd, pvs, pv_ipiv](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_piv");
-            bcast(g.row_fast(), PV[slot].data(), size_t(5 * nb + 8), qk, c);
+            bcast(g.row_fast(), PV[pvs].data(), size_t(5 * nb + 8), qk, c);
             if (pivot) lb::copy2d(c, kd, int64_t(1), pv_ipiv, kd, ipiv_all.data() + k * nb, kd);
         });
 
@@ -687,10 +695,10 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
         // -------------------------------------- column ranges: permute, U, update
         // apply the step's row permutation to local columns [c0, c1)
-        auto permute = [&, kk, kd, slot](lb::Ctx const& c, int64_t c0, int64_t c1) {
+        auto permute = [&, kk, kd, pvs](lb::Ctx const& c, int64_t c0, int64_t c1) {
             if (c1 <= c0 || !pivot) return;
             // rows: local == global; pairs relative to kk
-            int64_t* pvv = PV[slot].data();
+            int64_t* pvv = PV[pvs].data();
             if (c.dev()) {
                 slate_amd::dev::permute_rows(c1 - c0, slate_amd::dev::dptr(a + kk + c0 * lda), lda,
                                              pvv + nb, pvv + 3 * nb, nullptr, int(2 * kd), c.stream);
@@ -753,7 +761,7 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         auto range_tasks = [&](int queue, int64_t j0, int64_t j1) {
             std::vector<int64_t> cols;
             for (int64_t j = j0; j < j1; ++j) cols.push_back(Sched::col(j));
-            std::vector<int64_t> in = {tBc, tL};
+            std::vector<int64_t> in = {tBc, tL, tPV};
             if (use_linv) in.push_back(tLi);
             if (use_tn && mloc > lr_k1) in.push_back(tLt);
             S.task(queue, in, cols, [&, j0, j1](lb::Ctx const& c) {
@@ -777,7 +785,9 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             return (e && std::atoi(e)) ? device::kTrailQueue : device::kCommQueue;
         }();
         if (k > 0 && pivot) {
-            S.task(left_q, {tBc}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
+            // reads PV[pvs] (tPV): the panel that next rewrites the slot, RP
+            // steps later, waits for it (write-after-read across queues)
+            S.task(left_q, {tPV}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
                 auto cc = lcols(0, k);
                 permute(c, cc.first, cc.second);
             });
