@@ -10,6 +10,8 @@
 #include "device_common.hh"
 #include "kernels.hh"
 
+#include <stdexcept>
+
 namespace slate_amd {
 namespace dev {
 
@@ -426,6 +428,23 @@ __global__ void form_v_kernel(int64_t m, int64_t k, int64_t off, const T* A, int
     V[i + j * ldv] = i < d ? zero<T>() : (i == d ? one<T>() : A[i + j * lda]);
 }
 
+// More pairs than one register pass holds (2 * nb > 2048, i.e. nb > 1024):
+// every source value of the column is staged in LDS before any write (the
+// register kernel's second pass would read rows its first pass overwrote).
+template <typename T>
+__global__ void permute_rows_lds_kernel(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
+                                        const int* npairs_ptr, int max_pairs) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char perm_smem[];
+    T* v = reinterpret_cast<T*>(perm_smem);
+    const int npairs = npairs_ptr ? min(*npairs_ptr, max_pairs) : max_pairs;
+    const int64_t j = blockIdx.x;
+    if (j >= n) return;
+    T* col = A + j * lda;
+    for (int p = threadIdx.x; p < npairs; p += blockDim.x) v[p] = col[src[p]];
+    __syncthreads();
+    for (int p = threadIdx.x; p < npairs; p += blockDim.x) col[dst[p]] = v[p];
+}
+
 // Row gather / scatter between a column strip of A and a packed buffer
 // (buf is count x n, column-major, ld = count): gather buf(t, :) = A(idx[t], :),
 // scatter A(idx[t], :) = buf(t, :).  Used by the distributed row exchange.
@@ -550,7 +569,15 @@ template <typename T>
 void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
                   const int* npairs, int max_pairs, hipStream_t s) {
     if (n <= 0 || max_pairs <= 0) return;
-    hipLaunchKernelGGL(permute_rows_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src, npairs, max_pairs);
+    if (max_pairs <= 256 * 8) {
+        hipLaunchKernelGGL(permute_rows_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src, npairs,
+                           max_pairs);
+        return;
+    }
+    const size_t shm = size_t(max_pairs) * sizeof(T);
+    if (shm > 65536) throw std::runtime_error("permute_rows: more row pairs than one LDS pass holds");
+    hipLaunchKernelGGL(permute_rows_lds_kernel<T>, dim3((unsigned)n), dim3(256), shm, s, n, A, lda, dst, src, npairs,
+                       max_pairs);
 }
 
 template <typename T>

@@ -412,6 +412,26 @@ def test_getrf_driver_device(dtype, mn):
     assert info == 0 and relerr(L @ U, pa) < 10 * tol(dtype)
 
 
+@pytest.mark.parametrize("method", ["ppiv", "tntpiv"])
+@pytest.mark.parametrize("nb", [1280, 2048])
+def test_getrf_device_wide_tiles(method, nb):
+    """Tiles wider than 1024: the per-step row permutation then has more than
+    2048 (dst, src) pairs and takes the LDS-staged permute kernel (a second
+    register pass used to read rows the first pass had overwritten)."""
+    n = 3000
+    a = rnd(n, n, np.float64, 27)
+    A = s.from_numpy(a, nb=nb, target="d")
+    info, piv = s.getrf(A, target="d", method_lu=method)
+    f = s.to_numpy(A)
+    L = np.tril(f, -1) + np.eye(n)
+    U = np.triu(f)
+    ip = [kk * nb + ti * nb + off for kk, pv in enumerate(piv) for (ti, off) in pv]
+    pa = a.copy()
+    for j, p_ in enumerate(ip):
+        pa[[j, p_]] = pa[[p_, j]]
+    assert info == 0 and relerr(L @ U, pa) < 1e-12
+
+
 @pytest.mark.parametrize("n,nrhs", [(1000, 4), (5000, 1)])
 def test_gesv_mixed_device(n, nrhs):
     nb = 128
