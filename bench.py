@@ -91,7 +91,11 @@ def main():
     # (384: 50.5, 512: 51.9).  Multi-GPU grids keep 512 so the 2-D cyclic
     # distribution has enough block columns per process.
     # dgesv_mixed likewise (fp32 LU: 2.49 -> 2.42 s, profiles/r1_gesv_mixed_n64k_norm_fix.txt).
-    default_nb = {"dgetrf": 1024, "dpotrf": 1024, "dgesv_mixed": 1024} if world == 1 else {}
+    # Round 3: dgetrf at nb = 2048 once tiles wider than 1024 factor correctly
+    # (LDS-staged row permutation): 3370 -> 3283-3299 ms at n = 65536
+    # (profiles/r3_nb_sweep.txt); dgeqrf 512 vs 1024 and dpotrf 1024 vs 2048
+    # measured equal on one box.
+    default_nb = {"dgetrf": 2048, "dpotrf": 1024, "dgesv_mixed": 1024} if world == 1 else {}
     if a.nb:
         default_nb = {}
     a.nb = a.nb or 512
