@@ -496,6 +496,23 @@ void trsm(Ctx const& c, Side side, Uplo uplo, Op op, Diag diag, int64_t m, int64
     hipStream_t s = c.stream;
     if (alpha != T(1)) kd::geadd('G', m, n, dval(alpha), dptr(B), ldb, dval(T(0)), dptr(B), ldb, s);
     if (side == Side::Left && op == Op::NoTrans && m <= 64 && small_trsm()) {
+        if (sizeof(T) == 4 && m > 32) {
+            // fp32 64-row triangles as two 32-row solves and one GEMM: the
+            // single 64-row fp32 launch measured ~2.5 ms per call beside the
+            // fp32 trailing GEMM (profiles/r3_fp32_lu_trace.txt), the 32-row
+            // one ~20 us
+            const int64_t m1 = 32, m2 = m - 32;
+            if (uplo == Uplo::Lower) {
+                kd::trsm_small(upc(uplo), char(diag), int(m1), n, dptr(A), lda, dptr(B), ldb, s);
+                dgemm(s, 'G', Op::NoTrans, Op::NoTrans, m2, n, m1, T(-1), A + m1, lda, B, ldb, T(1), B + m1, ldb);
+                kd::trsm_small(upc(uplo), char(diag), int(m2), n, dptr(A + m1 + m1 * lda), lda, dptr(B + m1), ldb, s);
+            } else {
+                kd::trsm_small(upc(uplo), char(diag), int(m2), n, dptr(A + m1 + m1 * lda), lda, dptr(B + m1), ldb, s);
+                dgemm(s, 'G', Op::NoTrans, Op::NoTrans, m1, n, m2, T(-1), A + m1 * lda, lda, B + m1, ldb, T(1), B, ldb);
+                kd::trsm_small(upc(uplo), char(diag), int(m1), n, dptr(A), lda, dptr(B), ldb, s);
+            }
+            return;
+        }
         kd::trsm_small(upc(uplo), char(diag), int(m), n, dptr(A), lda, dptr(B), ldb, s);
         return;
     }
