@@ -10,6 +10,7 @@
 #include "device_common.hh"
 #include "kernels.hh"
 
+#include <cstdlib>
 #include <stdexcept>
 
 namespace slate_amd {
@@ -392,10 +393,9 @@ void trsm_small_kernel(char uplo, char diag, int m, int64_t n, const T* A, int64
 // Row permutation: for each pair p, row dst[p] of every column receives the
 // value of row src[p] (all reads happen before any write within a column).
 // One 256-thread workgroup per column strip of COLS columns.
-template <typename T>
+template <typename T, int PER>
 __global__ void permute_rows_kernel(int64_t n, T* A, int64_t lda, const int64_t* dst,
                                     const int64_t* src, const int* npairs_ptr, int max_pairs) {
-    constexpr int PER = 8;
     const int npairs = npairs_ptr ? min(*npairs_ptr, max_pairs) : max_pairs;
     const int64_t j = blockIdx.x;
     if (j >= n) return;
@@ -569,9 +569,17 @@ template <typename T>
 void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_t* src,
                   const int* npairs, int max_pairs, hipStream_t s) {
     if (n <= 0 || max_pairs <= 0) return;
+    // one register pass: every gather of the column in flight before the
+    // barrier (a second pass would read rows the first had overwritten)
     if (max_pairs <= 256 * 8) {
-        hipLaunchKernelGGL(permute_rows_kernel<T>, dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src, npairs,
-                           max_pairs);
+        hipLaunchKernelGGL((permute_rows_kernel<T, 8>), dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src,
+                           npairs, max_pairs);
+        return;
+    }
+    static const bool force_lds = [] { const char* e = std::getenv("SLATE_PERM_LDS"); return e && std::atoi(e); }();
+    if (max_pairs <= 256 * 16 && sizeof(T) <= 8 && !force_lds) {
+        hipLaunchKernelGGL((permute_rows_kernel<T, 16>), dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src,
+                           npairs, max_pairs);
         return;
     }
     const size_t shm = size_t(max_pairs) * sizeof(T);

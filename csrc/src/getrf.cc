@@ -283,11 +283,21 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
         const int s2 = int(k2 % R);
         const int64_t kd2 = std::min(A.tileNb(k2), m - grow_of(A, k2));
         int64_t* pv2 = PV[s2].data();
-        S.task(qC, {Sched::tok(31, s2), Sched::col(k2 - 1)}, {tLeft}, [&, nc, kd2, pv2](lb::Ctx const& c) {
-            trace::Block t2("getrf_left_swap");
-            const int ns = int(2 * kd2);
+        // pack / unpack on a compute queue, only the all-reduce on the comm
+        // queue (tLeft chains the three and the next step's use of LB)
+        const int ns = int(2 * kd2);
+        const int qL = device::kTrailQueue;
+        S.task(qL, {Sched::tok(31, s2), Sched::col(k2 - 1)}, {tLeft}, [&, nc, ns, pv2](lb::Ctx const& c) {
+            trace::Block t2("getrf_left_pack");
             slots_pack(c, 0, ns, nc, pv2 + 2 * nb, a, lda, rd, LB.data(), ns);
+        });
+        S.task(qC, {}, {tLeft}, [&, nc, ns](lb::Ctx const& c) {
+            trace::Block t2("getrf_left_swap");
             g.col().allreduce(LB.data(), size_t(ns) * nc, ReduceOp::Sum, c.loc(), c.stream);
+        });
+        // (reads PV[s2] too: the token makes its next writer wait for it)
+        S.task(qL, {Sched::tok(31, s2)}, {tLeft, Sched::col(k2 - 1)}, [&, nc, ns, pv2](lb::Ctx const& c) {
+            trace::Block t2("getrf_left_unpack");
             slots_unpack(c, 0, ns, nc, pv2 + 4 * nb, LB.data(), ns, a, lda, rd);
         });
     };
@@ -485,6 +495,23 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
             // the column); lookahead columns on the critical-path lane
             const bool crit = (queue == device::kLookaheadQueue);
             Comm& cc_ = crit ? colF : g.col();
+            if (!crit && pivot) {
+                // bulk lane: slot pack / unpack on the range's compute queue,
+                // only the all-reduce on the comm queue (the cols tokens
+                // order the three)
+                S.task(queue, {tPV}, cols, [&, c0, nc, buf](lb::Ctx const& c) {
+                    trace::Block t2("getrf_rows_pack");
+                    slots_pack(c, 0, int(2 * kd), nc, ssrc, a + c0 * lda, lda, rd, buf, ldu);
+                });
+                S.task(qC, {}, cols, [&, nc, buf](lb::Ctx const& c) {
+                    trace::Block t2("getrf_rows_exchange");
+                    cc_.allreduce(buf, size_t(ldu * nc), ReduceOp::Sum, c.loc(), c.stream);
+                });
+                S.task(queue, {tPV}, cols, [&, c0, nc, buf](lb::Ctx const& c) {
+                    trace::Block t2("getrf_rows_unpack");
+                    slots_unpack(c, int(kd), int(2 * kd), nc, sdst, buf + kd, ldu, a + c0 * lda, lda, rd);
+                });
+            } else
             S.task(crit ? qP : qC, {tPV}, cols, [&, c0, nc, buf](lb::Ctx const& c) {
                 trace::Block t2("getrf_rows_exchange");
                 if (pivot) {
