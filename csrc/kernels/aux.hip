@@ -576,7 +576,10 @@ void permute_rows(int64_t n, T* A, int64_t lda, const int64_t* dst, const int64_
                            npairs, max_pairs);
         return;
     }
-    static const bool force_lds = [] { const char* e = std::getenv("SLATE_PERM_LDS"); return e && std::atoi(e); }();
+    // (> 2048 pairs: the LDS-staged kernel measured equal-or-faster than a
+    // 16-per-thread register pass, 3306-3334 vs 3344-3352 ms for dgetrf at
+    // nb = 2048; SLATE_PERM_LDS=0 selects the register pass)
+    static const bool force_lds = [] { const char* e = std::getenv("SLATE_PERM_LDS"); return !e || std::atoi(e); }();
     if (max_pairs <= 256 * 16 && sizeof(T) <= 8 && !force_lds) {
         hipLaunchKernelGGL((permute_rows_kernel<T, 16>), dim3((unsigned)n), dim3(256), 0, s, n, A, lda, dst, src,
                            npairs, max_pairs);
