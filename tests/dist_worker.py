@@ -533,7 +533,8 @@ def case_lanes(tg, dt, nb):
     tournament / panel gather, pivot + LU11 + L broadcasts, lookahead row
     exchanges, TSQR, (V, T) broadcasts -- are enqueued on the panel queue (1);
     the trailing chunks' row exchanges / W all-reduces and the left swaps on
-    the comm queue (3).  Also: PPLU issues one collective task per panel."""
+    the comm queue (3), with their slot pack / unpack kernels on a compute
+    queue.  Also: PPLU issues one collective task per panel."""
     n = 6 * nb + 7
     a = rnd(n, n, dt, 131)
     crit_getrf = {"getrf_tnt_send", "getrf_tnt_recv", "getrf_bcast_winners", "getrf_panel_perm", "getrf_bcast_row",
@@ -549,6 +550,12 @@ def case_lanes(tg, dt, nb):
                 assert qu == 1, (label, qu)
             if label == "getrf_left_swap":
                 assert qu == 3, (label, qu)
+            # slot pack / unpack are compute: never on the comm queue
+            if label in ("getrf_rows_pack", "getrf_rows_unpack", "getrf_left_pack", "getrf_left_unpack"):
+                assert qu != 3, (label, qu)
+        if parallel.current_grid().p > 1:
+            labels = {label for label, _ in log}
+            assert {"getrf_left_pack", "getrf_left_unpack"} <= labels, labels
         qs = {qu for label, qu in log if label == "getrf_rows_exchange"}
         assert qs <= {1, 3} and (1 in qs or parallel.current_grid().p == 1), qs
         if fn is s.getrf and parallel.current_grid().p > 1:
