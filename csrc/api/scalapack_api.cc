@@ -216,6 +216,27 @@ void pgesv(int const* n, int const* nrhs, T* A, int const* iA, int const* jA, in
     to_ipiv(Am, P, ipiv);
 }
 
+/// Mixed-precision solve, ScaLAPACK p?gesv_mixed naming of the reference
+/// (scalapack_api/scalapack_gesv_mixed.cc): pdsgesv / pzcgesv.  A is factored
+/// in the lower precision (A's tiles keep the original fp64 values; the
+/// factors live in a separate low-precision copy), X gets the refined solution,
+/// iter the refinement count (negative: fell back to the full-precision LU).
+template <typename T>
+void pgesv_mixed(int const* n, int const* nrhs, T* A, int const* iA, int const* jA, int const* descA, int* ipiv,
+                 T* B, int const* iB, int const* jB, int const* descB, T* X, int const* iX, int const* jX,
+                 int const* descX, int* iter, int* info) {
+    auto Am = SUB(A, *n, *n);
+    auto Bm = SUB(B, *n, *nrhs);
+    auto Xm = SUB(X, *n, *nrhs);
+    Pivots P;
+    int it = 0;
+    *info = int(gesv_mixed(Am, P, Bm, Xm, it, sl_opts()));
+    *iter = it;
+    done(Am);
+    done(Xm);
+    to_ipiv(Am, P, ipiv);
+}
+
 template <typename T>
 void pgetri(int const* n, T* A, int const* iA, int const* jA, int const* descA, int const* ipiv, int* info) {
     auto Am = SUB(A, *n, *n);
@@ -439,6 +460,11 @@ SL3(void, p##gesvd, P##GESVD, (char const* ju, char const* jv, int const* m, int
     real_type<T>* S, DESC(U), DESC(VT), T*, int const*, int* info),                                         \
     pgesvd<T>(ju, jv, m, n, DARGS(A), S, DARGS(U), DARGS(VT), info))
 
+// p?gesv_mixed: only the fp64 -> fp32 pairs exist (pdsgesv, pzcgesv)
+#define SLATE_SCALAPACK_API_MIXED(name, NAME, T)                                                             \
+SL3(void, name, NAME, (int const* n, int const* nrhs, DESC(A), int* ipiv, DESC(B), DESC(X), int* iter,       \
+    int* info), pgesv_mixed<T>(n, nrhs, DARGS(A), ipiv, DARGS(B), DARGS(X), iter, info))
+
 #define SLATE_SCALAPACK_API_REAL(p, P, T)                                                                    \
 SL3(void, p##syev, P##SYEV, (char const* jz, char const* ul, int const* n, DESC(A), T* W, DESC(Z), T*,      \
     int const*, int* info), pheev<T>(jz, ul, n, DARGS(A), W, DARGS(Z), info))                               \
@@ -478,6 +504,7 @@ SLATE_SCALAPACK_API_REAL(ps, PS, T)
 #define T d_t
 SLATE_SCALAPACK_API(pd, PD, T)
 SLATE_SCALAPACK_API_REAL(pd, PD, T)
+SLATE_SCALAPACK_API_MIXED(pdsgesv, PDSGESV, T)
 #undef T
 #define T c_t
 SLATE_SCALAPACK_API(pc, PC, T)
@@ -486,4 +513,5 @@ SLATE_SCALAPACK_API_CPLX(pc, PC, T)
 #define T z_t
 SLATE_SCALAPACK_API(pz, PZ, T)
 SLATE_SCALAPACK_API_CPLX(pz, PZ, T)
+SLATE_SCALAPACK_API_MIXED(pzcgesv, PZCGESV, T)
 #undef T

@@ -192,3 +192,22 @@ def test_scalapack_pdgemm_pdgesv_pdposv(scalapack):
     scalapack.pdposv_(ch("U"), I(n), I(2), ptr(spd), I(1), I(1), ptr(da), ptr(bb), I(1), I(1), ptr(db),
                       C.byref(info))
     assert info.value == 0 and relerr(s0 @ bb, b0) < 1e-10
+
+
+def test_scalapack_pdsgesv_pzcgesv(scalapack):
+    """p?gesv_mixed (reference scalapack_api/scalapack_gesv_mixed.cc): fp32
+    factor, fp64 refinement; A keeps its fp64 values, X the refined solution."""
+    n, nb = 96, 32
+    for dt, fn in ((np.float64, scalapack.pdsgesv_), (np.complex128, scalapack.pzcgesv_)):
+        a = np.asfortranarray(rnd(n, n, dt, 21)) + n * np.eye(n, order="F")
+        b = np.asfortranarray(rnd(n, 3, dt, 22))
+        x = np.zeros((n, 3), dtype=dt, order="F")
+        a0, b0 = a.copy(), b.copy()
+        da, db = desc(n, n, nb, nb, n), desc(n, 3, nb, nb, n)
+        ipiv = np.zeros(n + nb, np.int32)
+        it, info = C.c_int(0), C.c_int(0)
+        fn(I(n), I(3), ptr(a), I(1), I(1), ptr(da), ptr(ipiv), ptr(b), I(1), I(1), ptr(db),
+           ptr(x), I(1), I(1), ptr(db), C.byref(it), C.byref(info))
+        assert info.value == 0 and it.value >= 0
+        assert relerr(a0 @ x, b0) < 1e-12
+        assert np.array_equal(b, b0)
