@@ -1644,6 +1644,158 @@ Result r_sy(Case<T>& c, int variant) {   // 0 sysv, 1 sytrf (+ sytrs for the che
     }
 }
 
+
+template <typename T>
+Result r_hetrs(Case<T>& c) {   // Bunch-Kaufman solve with an untimed hetrf (reference test_hesv.cc, hetrs)
+    auto Ag = c.mat(c.n, c.n, "rands", -1, true), B = c.mat(c.n, c.P.nrhs);
+    auto H0 = c.zeros(c.n, c.n);
+    copy<T, T>(conj_transpose(Ag), H0, c.opts);
+    add(T(1), Ag, T(1), H0, c.opts);
+    auto Hg = c.copy_of(H0), B0 = c.copy_of(B);
+    HermitianMatrix<T> H(Uplo::Lower, Hg);
+    std::vector<int64_t> ipiv;
+    Result r;
+    if (hetrf(H, ipiv, c.opts)) { r.error = INFINITY; return r; }
+    r.time = c.timed([&] { hetrs(H, ipiv, B, c.opts); });
+    r.flops = cfac<T>() * 2.0 * double(c.n) * c.n * c.P.nrhs;
+    if (c.P.check) r.error = c.solve_resid(H0, B, B0);
+    return r;
+}
+
+/// D&C stages on their own (reference test_stedc_{z_vector,sort,deflate,
+/// secular}.cc).  Each checks its defining property on the host:
+///   0 z_vector: z = [Q(n1-1, 0:n1); sgn Q(n1, n1:n)] / sqrt 2
+///   1 sort:     D ascending, (D, z, Q columns) permuted consistently
+///   2 deflate:  Q (diag(D) + rho z z^T) Q^T invariant, deflated z ~ 0
+///   3 secular:  (diag(D) + rho z z^T) U = U diag(Lambda), U orthogonal
+template <typename T>
+Result r_stedc_stage(Case<T>& c, int stage) {
+    using R = R_<T>;
+    Result r;
+    if constexpr (is_complex_v<T>) {
+        r.skipped = true; r.note = "real types (stedc works on R)"; return r;
+    } else {
+        const int64_t n = c.n, n1 = n / 2;
+        const R eps = std::numeric_limits<R>::epsilon();
+        auto hv = [](int64_t i, uint64_t salt) {   // deterministic values in [-1, 1)
+            uint64_t x = (uint64_t(i) + 1) * 0x9E3779B97F4A7C15ull ^ (salt * 0xBF58476D1CE4E5B9ull);
+            x ^= x >> 31; x *= 0x94D049BB133111EBull; x ^= x >> 29;
+            return R(double(x >> 11) / double(1ull << 53) * 2.0 - 1.0);
+        };
+        auto Q = c.zeros(n, n);
+        std::vector<T> q0, q1;
+        if (stage == 0) {
+            std::function<T(int64_t, int64_t)> qv = [&](int64_t i, int64_t j) -> T { return T(hv(i * n + j, 1)); };
+            set(qv, Q, c.opts);
+            std::vector<R> z;
+            r.time = c.timed([&] { stedc_z_vector(Q, n1, R(-1), z, c.opts); });
+            double err = 0;
+            for (int64_t j = 0; j < n; ++j) {
+                R want = (j < n1 ? hv((n1 - 1) * n + j, 1) : -hv(n1 * n + j, 1)) / std::sqrt(R(2));
+                err = std::max(err, double(std::abs(z[j] - want)));
+            }
+            r.error = err;
+            r.flops = double(n);
+            return r;
+        }
+        if (stage == 1) {
+            std::function<T(int64_t, int64_t)> qv = [&](int64_t i, int64_t j) -> T { return T(hv(i * n + j, 2)); };
+            set(qv, Q, c.opts);
+            std::vector<R> D(n), z(n);
+            for (int64_t j = 0; j < n; ++j) { D[j] = hv(j, 3); z[j] = hv(j, 4); }
+            auto D0 = D; auto z0 = z;
+            auto Qo = c.zeros(n, n);
+            std::vector<int64_t> perm;
+            gather(Q, q0, c.opts);
+            r.time = c.timed([&] { stedc_sort(D, z, Q, Qo, perm, c.opts); });
+            gather(Qo, q1, c.opts);
+            double err = 0;
+            for (int64_t j = 0; j < n; ++j) {
+                if (j > 0 && D[j] < D[j - 1]) err = INFINITY;
+                err = std::max(err, double(std::abs(D[j] - D0[perm[j]]) + std::abs(z[j] - z0[perm[j]])));
+                for (int64_t i = 0; i < n; ++i)
+                    err = std::max(err, double(std::abs(q1[i + j * n] - q0[i + perm[j] * n])));
+            }
+            r.error = err;
+            r.flops = double(n) * n;
+            return r;
+        }
+        // rank-one modified diagonal: sorted D with clusters (pairs within
+        // ~eps) and a few tiny z entries, so the deflation paths all run
+        std::vector<R> D(n), z(n);
+        for (int64_t j = 0; j < n; ++j) D[j] = R(j / 2) + ((j % 2) ? R(4) * eps : R(0)) + R(0.25) * R(j % 3 == 0);
+        std::sort(D.begin(), D.end());
+        R zn = 0;
+        for (int64_t j = 0; j < n; ++j) { z[j] = (j % 11 == 5) ? R(1e-20) : R(0.5) + R(0.5) * std::abs(hv(j, 5)); zn += z[j] * z[j]; }
+        for (auto& x : z) x /= std::sqrt(zn);
+        const R rho = R(1.5);
+        auto M = [&](std::vector<R> const& d, std::vector<R> const& zz) {
+            std::vector<R> m(size_t(n) * n, R(0));
+            for (int64_t j = 0; j < n; ++j) {
+                for (int64_t i = 0; i < n; ++i) m[i + j * n] = rho * zz[i] * zz[j];
+                m[j + j * n] += d[j];
+            }
+            return m;
+        };
+        const auto M0 = M(D, z);
+        double m0 = 0;
+        for (auto v : M0) m0 = std::max(m0, double(std::abs(v)));
+        if (stage == 2) {
+            set(T(0), T(1), Q, c.opts);
+            std::vector<char> defl;
+            int64_t k = 0;
+            r.time = c.timed([&] { k = stedc_deflate(rho, D, z, Q, defl, c.opts); });
+            gather(Q, q1, c.opts);
+            const auto M1 = M(D, z);
+            // Q M1 Q^T - M0
+            double err = 0;
+            std::vector<R> QM(size_t(n) * n, R(0));
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t l = 0; l < n; ++l) {
+                    R b = M1[l + j * n];
+                    if (b == R(0)) continue;
+                    for (int64_t i = 0; i < n; ++i) QM[i + j * n] += R(q1[i + l * n]) * b;
+                }
+            for (int64_t j = 0; j < n; ++j)
+                for (int64_t i = 0; i < n; ++i) {
+                    R v = 0;
+                    for (int64_t l = 0; l < n; ++l) v += QM[i + l * n] * R(q1[j + l * n]);
+                    err = std::max(err, double(std::abs(v - M0[i + j * n])));
+                }
+            int64_t nd = 0;
+            for (int64_t j = 0; j < n; ++j) if (defl[j]) { ++nd; err = std::max(err, double(rho * std::abs(z[j])) / 64); }
+            if (nd + k != n || nd == 0) err = INFINITY;   // the test matrix must deflate something
+            r.error = err / (m0 * double(n));
+            r.flops = double(n) * n;
+            return r;
+        }
+        // secular: strictly separated D, no deflation
+        for (int64_t j = 0; j < n; ++j) D[j] = R(j) + R(0.1) * hv(j, 6);
+        for (int64_t j = 0; j < n; ++j) z[j] = R(0.2) + std::abs(hv(j, 7));
+        const auto Ms = M(D, z);
+        double ms = 0;
+        for (auto v : Ms) ms = std::max(ms, double(std::abs(v)));
+        std::vector<R> lam;
+        auto U = c.zeros(n, n);
+        r.time = c.timed([&] { stedc_secular(rho, D, z, lam, U, c.opts); });
+        gather(U, q1, c.opts);
+        double err = 0, orth = 0;
+        for (int64_t j = 0; j < n; ++j)
+            for (int64_t i = 0; i < n; ++i) {
+                R v = 0, o = 0;
+                for (int64_t l = 0; l < n; ++l) {
+                    v += Ms[i + l * n] * R(q1[l + j * n]);
+                    o += R(q1[l + i * n]) * R(q1[l + j * n]);
+                }
+                err = std::max(err, double(std::abs(v - lam[j] * R(q1[i + j * n]))));
+                orth = std::max(orth, double(std::abs(o - (i == j ? R(1) : R(0)))));
+            }
+        r.error = std::max(err / ms, orth) / double(n);
+        r.flops = 4.0 * double(n) * n;
+        return r;
+    }
+}
+
 template <typename T>
 using Fn = std::function<Result(Case<T>&)>;
 
@@ -1740,6 +1892,11 @@ std::map<std::string, Fn<T>> routines() {
         {"sysv", [](Case<T>& c) { return r_sy<T>(c, 0); }},
         {"sytrf", [](Case<T>& c) { return r_sy<T>(c, 1); }},
         {"sytrs", [](Case<T>& c) { return r_sy<T>(c, 2); }},
+        {"hetrs", r_hetrs<T>},
+        {"stedc_z_vector", [](Case<T>& c) { return r_stedc_stage<T>(c, 0); }},
+        {"stedc_sort", [](Case<T>& c) { return r_stedc_stage<T>(c, 1); }},
+        {"stedc_deflate", [](Case<T>& c) { return r_stedc_stage<T>(c, 2); }},
+        {"stedc_secular", [](Case<T>& c) { return r_stedc_stage<T>(c, 3); }},
     };
 }
 

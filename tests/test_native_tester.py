@@ -82,7 +82,8 @@ def test_breadth2_distributed_2x2():
     2x2 grid (reference test/test.cc routine list)."""
     codes, outs = launch(["he2hb,unmtr_he2hb,hb2st,unmtr_hb2st,ge2tb,tb2bd,unmbr_tb2bd,bdsqr,stedc,hegst,"
                           "getrs_nopiv,getrs_tntpiv,posv_mixed_gmres,gbtrs,pbtrs,scale_row_col,gbnorm,hbnorm,synorm,"
-                          "trnorm,tzset,tzcopy,tzscale,tzadd,sysv,sytrf,sytrs",
+                          "trnorm,tzset,tzcopy,tzscale,tzadd,sysv,sytrf,sytrs,hetrs,stedc_z_vector,stedc_sort,"
+                          "stedc_deflate,stedc_secular",
                           "--type", "d,z", "--dim", "150,140x110x110", "--nb", "32", "--grid", "2x2"], 4)
     assert codes == [0] * 4 and "all tests passed" in outs[0], "\n".join(o[-2500:] for o in outs)
 
