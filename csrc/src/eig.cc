@@ -317,6 +317,33 @@ void set_diag_rows(Matrix<T>& M, std::vector<T> const& dg, Target target) {
     if (st) slate_hip_call(hipStreamSynchronize(st));
 }
 
+namespace {
+
+/// Range guard shared by heev and svd (reference heev.cc:73-102, svd.cc:85-125):
+/// returns the factor alpha the matrix was scaled to (1 if untouched) and sets
+/// `bad` when ||A||_max is NaN or Inf.  A matrix with ||A||_max below
+/// sqrt(safe_min / eps) or above its reciprocal is scaled by alpha / ||A||_max,
+/// so the reductions neither underflow nor overflow; the caller rescales the
+/// eigen / singular values by ||A||_max / alpha afterwards.
+template <typename R>
+R range_alpha(R anorm, bool& bad) {
+    const R sml = std::numeric_limits<R>::min() / std::numeric_limits<R>::epsilon();
+    const R sqrt_sml = std::sqrt(sml), sqrt_big = R(1) / sqrt_sml;
+    bad = std::isnan(anorm) || std::isinf(anorm);
+    if (bad) return R(1);
+    if (anorm > R(0) && anorm < sqrt_sml) return sqrt_sml;
+    if (anorm > sqrt_big) return sqrt_big;
+    return R(1);
+}
+
+template <typename R>
+void rescale_values(std::vector<R>& v, R anorm, R alpha) {
+    if (alpha == R(1)) return;
+    for (auto& x : v) x = x / alpha * anorm;   // divide first: x / alpha stays in range
+}
+
+}  // namespace
+
 template <typename T>
 void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts) {
     if (A.arbitrary_layout() || Z.arbitrary_layout()) {
@@ -334,6 +361,12 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     const int64_t n = A.n();
     Lambda.assign(n, R(0));
     if (n == 0) return;
+    // range guard (reference heev.cc:73-102): the scaled copy F is reduced,
+    // Lambda is rescaled at the end; eigenvectors are scale-invariant
+    const R anorm = slate::norm(Norm::Max, A, opts);
+    bool bad = false;
+    const R alpha = range_alpha(anorm, bad);
+    if (bad) { Lambda.assign(n, anorm); return; }
     // band width of the two-stage reduction: the bulge chase costs O(n^2 kd)
     // on the host, the first stage is memory-bound either way, so large tiles
     // are re-tiled to kd <= 64 (reference uses the tile size)
@@ -349,6 +382,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         if (A.uplo() == Uplo::Lower) slate::copy<T, T>(At, Fl, opts);
         else slate::copy<T, T>(conj_transpose(Ag), F, opts);   // upper: mirror into the lower triangle
     }
+    if (alpha != R(1)) scale(alpha, anorm, F, opts);
     const int64_t nt = F.nt();
     std::vector<TriangularFactors<T>> Ts;
     he2hb(F, Ts, opts);
@@ -367,6 +401,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         trace::Block t2("sterf");
         host::sterf<R>(n, d.data(), e.data());
         Lambda = d;
+        rescale_values(Lambda, anorm, alpha);
         return;
     }
     const int64_t me = get_option<int64_t>(opts, Option::MethodEig, int64_t(MethodEig::DC));
@@ -387,6 +422,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         }
     }
     Lambda = d;
+    rescale_values(Lambda, anorm, alpha);
     // Z1 (1-D column layout, kd-wide column tiles): diag(phase) Qt, then Q2
     // applied to all rows of my columns
     Matrix<T> Z1(n, n, n, kd, row_grid(gA));
@@ -509,6 +545,17 @@ void ge2tb(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<Tria
     }
 }
 
+
+template <typename T>
+void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts);
+
+/// SVD A = U diag(Sigma) VT (thin: U m x k, VT k x n, k = min(m, n)).
+/// Reference src/svd.cc: range scaling with a NaN / Inf guard, then
+///   m > 5/3 n: QR pre-reduction, A = Q R, SVD of the n x n R, U = Q [U_R; 0];
+///   n > m:     LQ pre-reduction, A = L Q, SVD of the m x m L, VT = [VT_L 0] Q;
+///   otherwise  the three-stage ge2tb -> tb2bd -> bdsqr path on A itself.
+/// The pre-reductions factor A in place (A is destroyed, as in the reference)
+/// and never form a transposed copy of A.
 template <typename T>
 void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts) {
     if (A.arbitrary_layout() || U.arbitrary_layout() || VT.arbitrary_layout()) {
@@ -523,20 +570,77 @@ void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>
     internal::DriverScope ds_;
     using R = real_type<T>;
     Target target = resolve_target(opts);
-    const int64_t m = A.m(), n = A.n();
-    if (m < n) {
-        // A^H = U' S V'^H  =>  A = V' S U'^H
-        Matrix<T> Ah = A.emptyLike(0, 0, Op::ConjTrans);
+    const int64_t m = A.m(), n = A.n(), k = std::min(m, n);
+    if (k == 0) { Sigma.clear(); return; }
+    const R anorm = slate::norm(Norm::Max, A, opts);
+    bool bad = false;
+    const R alpha = range_alpha(anorm, bad);
+    if (bad) { Sigma.assign(k, anorm); return; }
+    if (alpha != R(1)) scale(alpha, anorm, A, opts);
+    const bool wu = wanted(U), wv = wanted(VT);
+    auto gA = A.grid();
+    if (3 * m > 5 * n || n > m) {
+        const bool qr = (3 * m > 5 * n);
+        TriangularFactors<T> TQ;
+        if (qr) geqrf(A, TQ, opts);
+        else gelqf(A, TQ, opts);
+        // the k x k triangle (R upper / L lower), zero elsewhere
+        Matrix<T> Ak = A.slice(0, k - 1, 0, k - 1);
+        Matrix<T> Ah(k, k, A.mb(), A.nb(), gA);
         Ah.insertLocalTiles(target);
-        slate::copy<T, T>(conj_transpose(A), Ah, opts);
-        Matrix<T> Uh, VTh;
-        if (wanted(VT)) { Uh = Matrix<T>(n, m, Ah.mb(), Ah.nb(), Ah.grid()); Uh.insertLocalTiles(target); }
-        if (wanted(U)) { VTh = Matrix<T>(m, m, Ah.nb(), Ah.nb(), Ah.grid()); VTh.insertLocalTiles(target); }
-        svd(Ah, Sigma, Uh, VTh, opts);
-        if (wanted(U)) slate::copy<T, T>(conj_transpose(VTh), U, opts);
-        if (wanted(VT)) slate::copy<T, T>(conj_transpose(Uh), VT, opts);
-        return;
+        set(T(0), T(0), Ah, opts);
+        {
+            const Uplo ul = qr ? Uplo::Upper : Uplo::Lower;
+            BaseTrapezoidMatrix<T> St(ul, Ak, MatrixKind::Trapezoid), Dt(ul, Ah, MatrixKind::Trapezoid);
+            slate::copy<T, T>(St, Dt, opts);
+        }
+        // the side that the pre-reduction's Q multiplies gets a k x k
+        // factor first; the other side is the caller's matrix directly
+        Matrix<T> Uk, Vk;
+        if (wu) { if (qr) { Uk = Matrix<T>(k, k, A.nb(), A.nb(), gA); Uk.insertLocalTiles(target); } else Uk = U; }
+        if (wv) { if (!qr) { Vk = Matrix<T>(k, k, A.mb(), A.mb(), gA); Vk.insertLocalTiles(target); } else Vk = VT; }
+        svd_square(Ah, Sigma, Uk, Vk, opts);
+        // the caller's U / VT is used in place when it shares A's tiling of
+        // the dimension Q acts on (the usual case), else a work copy
+        auto fits = [&](Matrix<T> const& X, bool rows) {
+            return X.grid().get() == gA.get() && X.aligned() && X.op() == Op::NoTrans &&
+                   (rows ? X.mb() == A.mb() : X.nb() == A.nb());
+        };
+        if (qr && wu) {
+            // U = Q [U_R; 0]
+            const bool direct = fits(U, true);
+            Matrix<T> Uw = U;
+            if (!direct) { Uw = Matrix<T>(m, k, A.mb(), A.nb(), gA); Uw.insertLocalTiles(target); }
+            set(T(0), T(0), Uw, opts);
+            Matrix<T> Ut = Uw.slice(0, k - 1, 0, k - 1);
+            slate::copy<T, T>(Uk, Ut, opts);
+            unmqr(Side::Left, Op::NoTrans, A, TQ, Uw, opts);
+            if (!direct) slate::copy<T, T>(Uw, U, opts);
+        }
+        if (!qr && wv) {
+            // VT = [VT_L 0] Q
+            const bool direct = fits(VT, false);
+            Matrix<T> Vw = VT;
+            if (!direct) { Vw = Matrix<T>(k, n, A.mb(), A.nb(), gA); Vw.insertLocalTiles(target); }
+            set(T(0), T(0), Vw, opts);
+            Matrix<T> Vt = Vw.slice(0, k - 1, 0, k - 1);
+            slate::copy<T, T>(Vk, Vt, opts);
+            unmlq(Side::Right, Op::NoTrans, A, TQ, Vw, opts);
+            if (!direct) slate::copy<T, T>(Vw, VT, opts);
+        }
+    } else {
+        svd_square(A, Sigma, U, VT, opts);
     }
+    rescale_values(Sigma, anorm, alpha);
+}
+
+/// Three-stage SVD of an m x n matrix with n <= m <= 5/3 n (no pre-reduction).
+template <typename T>
+void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts) {
+    using R = real_type<T>;
+    Target target = resolve_target(opts);
+    const int64_t m = A.m(), n = A.n();
+    slate_assert(m >= n);
     // stage 1 on kd-wide tiles (see heev)
     const int64_t kd = std::min<int64_t>(A.nb(), 64);
     auto gA = A.grid();

@@ -139,3 +139,67 @@ def test_svd(dt, mn):
     assert np.linalg.norm(vt @ vt.conj().T - np.eye(k)) / k < tol(dt)
     A2 = s.from_numpy(a, nb=nb)
     assert np.allclose(s.svd_vals(A2), ref, atol=tol(dt) * ref.max())
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.complex128])
+@pytest.mark.parametrize("shape", ["tall4", "wide3"])
+def test_svd_pre_reduction(dt, shape):
+    """m = 4n runs the QR pre-reduction, n = 3m the LQ one (reference
+    svd.cc:130-216): no full-size work matrix (neither a transposed copy of A
+    nor a work U / VT) -- the largest storage allocation stays below half of
+    A's local array -- and the factors are exact."""
+    nb = 16
+    m, n = (192, 48) if shape == "tall4" else (96, 288)
+    k = min(m, n)
+    a = rnd(m, n, dt, 31)
+    s._slate.storage_alloc_reset()
+    A = s.from_numpy(a, nb=nb)
+    U = s.from_numpy(np.zeros((m, k), dt), nb=nb)
+    VT = s.from_numpy(np.zeros((k, n), dt), nb=nb)
+    full = s._slate.storage_alloc_max()
+    s._slate.storage_alloc_reset()
+    sv = s.svd(A, U, VT)
+    assert s._slate.storage_alloc_max() <= full // 2, (s._slate.storage_alloc_max(), full)
+    ref = np.linalg.svd(a, compute_uv=False)
+    assert np.allclose(sv, ref, atol=1e-12 * ref.max())
+    u, vt = s.to_numpy(U), s.to_numpy(VT)
+    assert np.linalg.norm(u @ np.diag(sv) @ vt - a) / (np.linalg.norm(a) * k) < 1e-12
+    assert np.linalg.norm(u.conj().T @ u - np.eye(k)) / k < 1e-12
+    assert np.linalg.norm(vt @ vt.conj().T - np.eye(k)) / k < 1e-12
+    # values only
+    assert np.allclose(s.svd_vals(s.from_numpy(a, nb=nb)), ref, atol=1e-12 * ref.max())
+
+
+@pytest.mark.parametrize("scale", [1e-300, 1e300])
+def test_heev_svd_range_scaling(scale):
+    """Matrices near under/overflow are scaled into range and the values
+    scaled back (reference heev.cc:73-102, svd.cc:85-125): without it the
+    reflector norms square to 0 or inf."""
+    n, nb = 60, 16
+    a = herm(n, np.float64, 41)
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a * scale, nb=nb))
+    Z = s.from_numpy(np.zeros((n, n)), nb=nb)
+    w = s.heev(A, Z)
+    ref = np.linalg.eigvalsh(a)
+    assert np.all(np.isfinite(w))
+    assert np.allclose(w / scale, ref, atol=1e-10 * abs(ref).max())
+    z = s.to_numpy(Z)
+    assert np.linalg.norm(a @ z - z * (w / scale)) / (np.linalg.norm(a) * n) < 1e-10
+    for m_, n_ in ((90, 60), (60, 60), (40, 70)):
+        g = rnd(m_, n_, np.float64, 42)
+        sv = s.svd_vals(s.from_numpy(g * scale, nb=nb))
+        sref = np.linalg.svd(g, compute_uv=False)
+        assert np.all(np.isfinite(sv)) and np.allclose(sv / scale, sref, atol=1e-10 * sref.max()), (m_, n_)
+
+
+def test_heev_svd_nan_inf_guard():
+    """NaN / Inf input: every value is ||A||_max (NaN or Inf), no exception,
+    no hang in the bulge chase (reference heev.cc:86-90, svd.cc:109-112)."""
+    n, nb = 40, 16
+    for bad in (np.nan, np.inf):
+        a = herm(n, np.float64, 43)
+        a[3, 5] = a[5, 3] = bad
+        w = s.heev(s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb)))
+        assert len(w) == n and (np.all(np.isnan(w)) if np.isnan(bad) else np.all(np.isinf(w)))
+        sv = s.svd_vals(s.from_numpy(a[:, :30], nb=nb))
+        assert len(sv) == 30 and (np.all(np.isnan(sv)) if np.isnan(bad) else np.all(np.isinf(sv)))
