@@ -48,6 +48,51 @@ EXTRAS = {
 }
 
 
+class Watchdog:
+    """Fail fast on a hung step (a peer that never joins a collective): after
+    the armed deadline, abort every RCCL communicator of this process (the
+    stuck kernels return) and exit 124, so torchrun tears the job down and
+    the run reports an error instead of holding the node until the driver's
+    limit.  SLATE_BENCH_STEP_TIMEOUT (s) bounds a routine's first step and
+    every generation / check phase; later steps get max(60 s, 4x the first)."""
+
+    def __init__(self, rank):
+        import threading
+        self.rank, self.deadline, self.what = rank, None, ""
+        self.base = float(os.environ.get("SLATE_BENCH_STEP_TIMEOUT", "300"))
+        self.lock = threading.Lock()
+        threading.Thread(target=self._loop, daemon=True).start()
+
+    def arm(self, what, secs=None):
+        with self.lock:
+            self.what, self.deadline = what, time.time() + (secs or self.base)
+
+    def disarm(self):
+        with self.lock:
+            self.deadline = None
+
+    def _loop(self):
+        import threading
+        while True:
+            time.sleep(1.0)
+            with self.lock:
+                late = self.deadline is not None and time.time() > self.deadline
+                what = self.what
+            if not late:
+                continue
+            errs = ""
+            try:
+                errs = s._slate.comm_async_errors()
+            except Exception:
+                pass
+            print(f"# WATCHDOG rank {self.rank}: '{what}' exceeded its time limit; RCCL async errors: "
+                  f"{errs or 'none'}; aborting communicators", file=sys.stderr, flush=True)
+            t = threading.Thread(target=lambda: s._slate.comm_abort_all(), daemon=True)
+            t.start()
+            t.join(30)
+            os._exit(124)
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -83,7 +128,10 @@ def main():
         s._slate.set_device(int(os.environ.get("LOCAL_RANK", "0")) % max(1, s._slate.device_count()))
     target = "d" if s.device_available() else "h"
     p, q = (a.p, a.q) if a.p and a.q else s.choose_grid(world)
+    wd = Watchdog(rank)
+    wd.arm("init_grid")
     grid = s.init_grid(p, q)
+    wd.disarm()
     n = a.n
     # Default tiles: 512 everywhere, except on one GPU where dgetrf / dpotrf
     # run 2-4% faster at nb = 1024 (profiles/nb_sweep_r1_n65536_1gpu.txt:
@@ -211,11 +259,14 @@ def main():
         times, extra = [], {}
         seed = 0
         step, total = 0, warmup + steps
+        first_dt = None
         while step < total:
             seed = 100 + step
+            wd.arm(f"{label} generate {step}")
             if rname != "dgemm":
                 s._slate.generate_matrix_d(kind, mats["A"], seed, -1.0, s.opts(tg))
             barrier_sync()
+            wd.arm(f"{label} step {step}", None if first_dt is None else max(60.0, 4 * first_dt))
             if a.trace and step == warmup:
                 s.trace.on()
             t0 = time.perf_counter()
@@ -246,6 +297,9 @@ def main():
                     print(f"# dgesv_mixed iters={iters} phase ms: {tm}", file=sys.stderr, flush=True)
             barrier_sync()
             dt = time.perf_counter() - t0
+            wd.disarm()
+            if first_dt is None:
+                first_dt = dt
             if a.trace and step == warmup:
                 s.trace.finish(grid.world, f"{a.trace}_{label}")
                 s.trace.off()
@@ -265,7 +319,9 @@ def main():
         res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_, "lookahead": la_of(rname),
                "steps": len(times), "warmup": warmup}
         if a.check == "yes":
+            wd.arm(f"{label} residual check")
             err = residual(rname, mats, kind, seed, nb, n_, tg)
+            wd.disarm()
             res["backward_error"] = float(f"{err:.3e}")
             res["check"] = "pass" if err < 50 else "FAIL"
             if rank == 0:

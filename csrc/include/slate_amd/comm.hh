@@ -124,5 +124,11 @@ CommPtr make_rccl_comm(std::string const& unique_id, int nranks, int rank);
 std::string rccl_unique_id();
 /// Split an RCCL communicator (ncclCommSplit); collective over `parent`.
 CommPtr rccl_split(CommPtr const& parent, int color, int key);
+/// Abort every live RCCL communicator of this process (ncclCommAbort; safe
+/// from a watchdog thread while another thread waits on a stuck collective).
+/// Returns how many were aborted; the communicators are unusable afterwards.
+int comm_abort_all();
+/// Asynchronous errors reported by the live RCCL communicators ("" if none).
+std::string comm_async_errors();
 
 }  // namespace slate

@@ -350,6 +350,8 @@ PYBIND11_MODULE(_slate, m) {
         .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>());
     py::class_<SelfComm, Comm, std::shared_ptr<SelfComm>>(m, "SelfComm").def(py::init<>());
     py::class_<HostComm, PyHostComm, Comm, std::shared_ptr<HostComm>>(m, "HostComm").def(py::init<>());
+    m.def("comm_abort_all", &comm_abort_all, py::call_guard<py::gil_scoped_release>());
+    m.def("comm_async_errors", &comm_async_errors);
     m.def("rccl_unique_id", []() { return py::bytes(rccl_unique_id()); });
     m.def("make_rccl_comm", [](py::bytes uid, int nranks, int rank) {
         std::string s = uid;

@@ -4,7 +4,10 @@
 #include "slate_amd/comm.hh"
 
 #include <rccl/rccl.h>
+#include <algorithm>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #define slate_nccl_call(call) do {                                            \
     ncclResult_t _r = (call);                                                 \
@@ -40,16 +43,35 @@ ncclRedOp_t nccl_op(ReduceOp op) {
     return ncclSum;
 }
 
+/// Every live communicator, so a watchdog can abort them all (comm_abort_all):
+/// ncclCommAbort makes RCCL kernels stuck on a peer that never arrives return,
+/// so a hung multi-GPU run ends with an error instead of holding its GPUs.
+std::mutex g_reg_mtx;
+std::vector<ncclComm_t>& registry() {
+    static auto* v = new std::vector<ncclComm_t>();   // leaked: outlives static dtors
+    return *v;
+}
+bool g_aborted = false;
+
 class RcclComm : public Comm {
 public:
     RcclComm(ncclComm_t c) : comm_(c) {
         slate_nccl_call(ncclCommCount(comm_, &size_));
         slate_nccl_call(ncclCommUserRank(comm_, &rank_));
+        std::lock_guard<std::mutex> l(g_reg_mtx);
+        registry().push_back(comm_);
     }
     ~RcclComm() override {
+        bool aborted;
+        {
+            std::lock_guard<std::mutex> l(g_reg_mtx);
+            auto& r = registry();
+            r.erase(std::remove(r.begin(), r.end(), comm_), r.end());
+            aborted = g_aborted;
+        }
         // Destroy only if the process is still healthy; at interpreter exit the
-        // HIP runtime may already be torn down.
-        if (comm_) (void)ncclCommDestroy(comm_);
+        // HIP runtime may already be torn down.  An aborted comm is gone.
+        if (comm_ && !aborted) (void)ncclCommDestroy(comm_);
     }
     int rank() const override { return rank_; }
     int size() const override { return size_; }
@@ -101,6 +123,34 @@ private:
 };
 
 }  // namespace
+
+int comm_abort_all() {
+    std::vector<ncclComm_t> v;
+    {
+        std::lock_guard<std::mutex> l(g_reg_mtx);
+        v = registry();
+        g_aborted = true;
+    }
+    for (ncclComm_t c : v) (void)ncclCommAbort(c);
+    return int(v.size());
+}
+
+std::string comm_async_errors() {
+    std::vector<ncclComm_t> v;
+    {
+        std::lock_guard<std::mutex> l(g_reg_mtx);
+        v = registry();
+    }
+    std::string out;
+    for (ncclComm_t c : v) {
+        ncclResult_t r = ncclSuccess;
+        if (ncclCommGetAsyncError(c, &r) == ncclSuccess && r != ncclSuccess && r != ncclInProgress) {
+            if (!out.empty()) out += "; ";
+            out += ncclGetErrorString(r);
+        }
+    }
+    return out;
+}
 
 std::string rccl_unique_id() {
     ncclUniqueId id;
