@@ -103,6 +103,20 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
     }
     (void)nloc;
 
+    // Panel messages (diagonal tile down the column, L panel along the row,
+    // transposed tiles over the column) are all on the critical path: they go
+    // on the panel queue over the fast-lane (duplicate) communicators
+    // (as getrf / geqrf), so step k+1's panel chain is one stream with no
+    // cross-queue hops; SLATE_POTRF_COMM_QUEUE=1 keeps them on the comm queue.
+    static const bool comm_q_env = [] {
+        const char* e = std::getenv("SLATE_POTRF_COMM_QUEUE");
+        return e && std::atoi(e) != 0;
+    }();
+    const bool fast = !comm_q_env;   // (the fast comms alias row() / col() without a duplicate)
+    const int qM = fast ? 1 : device::kCommQueue;
+    Comm& rowM = fast ? g.row_fast() : g.row();
+    Comm& colM = fast ? g.col_fast() : g.col();
+
     Work<int> dinfo(target, 1);
     {
         lb::Ctx c0 = S.ctx(1);
@@ -136,10 +150,10 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         int64_t ldL = lda;
         if (in_col && p > 1) {
             T* D = Dk[slot].data();
-            S.task(device::kCommQueue, {Sched::col(k)}, {tDiag}, [&, D, akk, kb, pk](lb::Ctx const& c) {
+            S.task(qM, {Sched::col(k)}, {tDiag}, [&, D, akk, kb, pk](lb::Ctx const& c) {
                 trace::Block tb("bcast_diag");
                 if (myrow == pk) pack(c, kb, kb, akk, lda, D);
-                bcast(g.col(), D, size_t(kb * kb), pk, c);
+                bcast(colM, D, size_t(kb * kb), pk, c);
             });
             Lkk = D; ldL = kb;
         }
@@ -160,11 +174,11 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         std::vector<std::vector<int64_t>> lists(p);
         for (int64_t J = k + 1; J < nt; ++J)
             if (A.scol_owner(J) == mycol) lists[A.srow_owner(J)].push_back(J);
-        S.task(device::kCommQueue, {Sched::col(k)}, {tBc}, [&, Wk, apan, mrows, kb, qk, slot, lists, lr_k1, ldW](lb::Ctx const& c) {
+        S.task(qM, {Sched::col(k)}, {tBc}, [&, Wk, apan, mrows, kb, qk, slot, lists, lr_k1, ldW](lb::Ctx const& c) {
             trace::Block tb("bcast_panel");
             if (q > 1) {
                 if (mycol == qk) pack(c, mrows, kb, apan, lda, Wk);
-                bcast(g.row(), Wk, size_t(mrows * kb), qk, c);
+                bcast(rowM, Wk, size_t(mrows * kb), qk, c);
             }
             if (p > 1) {
                 // pack my tiles (rows of Wk) for the column all-gather
@@ -176,7 +190,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
                     lb::copy2d(c, jb, kb, Wk + off, ldW, Sb + cnt * nb * nb, nb);
                     ++cnt;
                 }
-                g.col().allgather(Sb, Wt[slot].data(), size_t(maxcnt * nb * nb), scalar_type<T>(), c.loc(), c.stream);
+                colM.allgather(Sb, Wt[slot].data(), size_t(maxcnt * nb * nb), scalar_type<T>(), c.loc(), c.stream);
             }
         });
 

@@ -574,6 +574,19 @@ def case_lanes(tg, dt, nb):
             assert qu == 1, (label, qu)
     qs = {qu for label, qu in log if label == "geqrf_update_allreduce"}
     assert qs <= {1, 3}, qs
+    # potrf: every panel message is critical-path -> panel queue (fast lane)
+    h = (a @ a.conj().T + n * np.eye(n)).astype(dt)
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+    s._slate.lane_log_enable(True)
+    assert s.potrf(H, target=tg) == 0
+    log = s._slate.lane_log_take()
+    s._slate.lane_log_enable(False)
+    labels = {label for label, _ in log}
+    g = parallel.current_grid()
+    assert g.p * g.q == 1 or "bcast_panel" in labels, labels
+    for label, qu in log:
+        if label in ("bcast_diag", "bcast_panel"):
+            assert qu == 1, (label, qu)
 
 
 def case_solve_notemp(tg, dt, nb):

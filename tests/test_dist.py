@@ -126,3 +126,16 @@ def test_rccl_potrf_staircase(nprocs, grid, la):
                         "--target", "d", "--lookahead", la],
                        capture_output=True, text=True, timeout=900)
     assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+def test_rccl_2x2_no_fast_lane():
+    """SLATE_FAST_LANE=0: no duplicate communicators, every critical-path
+    message shares the plain row / column comms with the bulk traffic (the
+    lanes alias); LU / QR / Cholesky must still be deadlock-free and correct."""
+    env = dict(os.environ, SLATE_FAST_LANE="0")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), "4",
+                        "getrf,getrf_tntpiv,geqrf,potrf", "--type", "d", "--dim", "1000", "--nb", "128",
+                        "--grid", "2x2", "--target", "d", "--lookahead", "2"],
+                       capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
