@@ -107,6 +107,8 @@ def parse():
     ap.add_argument("--lookahead", type=int, default=0, help="0: per-routine default (see la_per)")
     ap.add_argument("--method-lu", default="tntpiv", choices=["ppiv", "tntpiv"])
     ap.add_argument("--trace", default="")
+    ap.add_argument("--mixed-escalate", default="yes", choices=["yes", "no"],
+                    help="dgesv_mixed: GMRES-IR escalation before the fp64 fallback (no = reference semantics)")
     ap.add_argument("--extras", default="all", help="BASELINE configs to add after the suite: all, none, or names")
     ap.add_argument("--check", default="yes", choices=["yes", "no"],
                     help="backward-error check of each routine after its timed steps (outside the timed region)")
@@ -287,13 +289,22 @@ def main():
             elif rname == "dgesv_mixed":
                 s._slate.clear_timers()
                 lu = {"tntpiv": 2, "ppiv": 1}[a.method_lu]  # MethodLU::CALU / PartialPiv
-                info, piv, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], method_lu=lu, **o)
+                # GMRES-IR escalation on the same fp32 factors when classical
+                # refinement stalls (Option::EscalateGmres; the fp64 fallback
+                # stays behind it): a random n = 65536 matrix is sometimes too
+                # ill-conditioned for classical fp32 refinement within 30 steps
+                info, piv, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], method_lu=lu,
+                                                escalate_gmres=a.mixed_escalate == "yes", **o)
                 mats["piv"] = piv
                 assert info == 0, f"dgesv_mixed info={info} iters={iters}"
-                extra["iterations"] = int(iters)
-                extra["fallback"] = bool(iters < 0)
+                if step >= warmup:
+                    extra.setdefault("iterations_per_step", []).append(int(iters))
+                    extra["iterations"] = int(iters)
+                    extra["fallback"] = bool(extra.get("fallback", False) or iters < 0)
+                    extra["escalate_gmres"] = a.mixed_escalate == "yes"
                 if rank == 0:
-                    tm = {k: round(v * 1e3, 1) for k, v in s._slate.timers().items() if "gesv_mixed" in k}
+                    tm = {k: round(v * 1e3, 1) for k, v in s._slate.timers().items()
+                          if "gesv_mixed" in k or "gmres" in k}
                     print(f"# dgesv_mixed iters={iters} phase ms: {tm}", file=sys.stderr, flush=True)
             barrier_sync()
             dt = time.perf_counter() - t0

@@ -57,6 +57,12 @@ enum class Option : char {
     MaxIterations,
     UseFallbackSolver,
     PivotThreshold,
+    /// Mixed-precision solvers (gesv_mixed / posv_mixed): when classical
+    /// refinement stalls or is projected to miss MaxIterations, continue with
+    /// GMRES-IR preconditioned by the same low-precision factors before the
+    /// full-precision fallback.  Not in the reference (default off: the
+    /// reference semantics, classical refinement then fallback).
+    EscalateGmres,
 
     PrintVerbose = 50,
     PrintEdgeItems,

@@ -148,6 +148,7 @@ Options to_options(py::dict d) {
         else if (k == "tolerance") o[Option::Tolerance] = v.cast<double>();
         else if (k == "max_iterations") o[Option::MaxIterations] = v.cast<int64_t>();
         else if (k == "use_fallback_solver") o[Option::UseFallbackSolver] = v.cast<bool>();
+        else if (k == "escalate_gmres") o[Option::EscalateGmres] = int64_t(v.cast<bool>());
         else if (k == "pivot_threshold") o[Option::PivotThreshold] = v.cast<double>();
         else if (k == "hold_local_workspace") o[Option::HoldLocalWorkspace] = v.cast<bool>();
         else if (k == "depth") o[Option::Depth] = v.cast<int64_t>();

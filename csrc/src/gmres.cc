@@ -148,6 +148,57 @@ bool gmres_ir(int64_t n, std::vector<T> const& b, std::vector<T>& x, real_type<T
 
 }  // namespace
 
+namespace internal {
+
+template <typename T>
+bool gmres_refine(Matrix<T>& B, Matrix<T>& X, real_type<T> Anorm, int itermax, int& iters,
+                  std::function<void(Matrix<T>&, Matrix<T>&)> const& residual,
+                  std::function<void(Matrix<typename lower_prec<T>::type>&)> const& solve_lo, Options const& opts) {
+    trace::Block tb("gmres_refine");
+    using Lo = typename lower_prec<T>::type;
+    Target target = resolve_target(opts);
+    const int64_t n = B.m(), nrhs = B.n();
+    const int restart = std::max(1, std::min(30, itermax));
+    Vec<T> io{n, B.mb(), B.grid(), target, B.srow_owner(0)};
+    std::vector<T> bh, xh;
+    gather<T>(B, bh, opts);
+    gather<T>(X, xh, opts);
+    auto precond = [&](std::vector<T> const& v, std::vector<T>& z) {
+        Matrix<Lo> Vm = io.template make<Lo>(v);
+        solve_lo(Vm);
+        io.read(Vm, z);
+    };
+    auto matvec = [&](std::vector<T> const& v, std::vector<T>& y) {
+        Matrix<T> Vm = io.template make<T>(v);
+        Matrix<T> Y = io.template make<T>(std::vector<T>(n, T(0)));
+        residual(Y, Vm);                          // Y = -A v
+        io.read(Y, y);
+        for (auto& e : y) e = -e;
+    };
+    bool ok = true;
+    iters = 0;
+    for (int64_t j = 0; j < nrhs; ++j) {
+        std::vector<T> b(bh.begin() + j * n, bh.begin() + (j + 1) * n), x(xh.begin() + j * n, xh.begin() + (j + 1) * n);
+        int it = 0;
+        ok = gmres_ir<T>(n, b, x, Anorm, itermax, restart, matvec, precond, it) && ok;
+        iters = std::max(iters, it);
+        std::copy(x.begin(), x.end(), xh.begin() + j * n);
+    }
+    Options oh = {{Option::Target, Target::Host}};
+    set<T>(std::function<T(int64_t, int64_t)>([&](int64_t i, int64_t j) { return xh[i + j * n]; }), X, oh);
+    return ok;
+}
+
+template bool gmres_refine<double>(Matrix<double>&, Matrix<double>&, double, int, int&,
+                                   std::function<void(Matrix<double>&, Matrix<double>&)> const&,
+                                   std::function<void(Matrix<float>&)> const&, Options const&);
+template bool gmres_refine<std::complex<double>>(
+    Matrix<std::complex<double>>&, Matrix<std::complex<double>>&, double, int, int&,
+    std::function<void(Matrix<std::complex<double>>&, Matrix<std::complex<double>>&)> const&,
+    std::function<void(Matrix<std::complex<float>>&)> const&, Options const&);
+
+}  // namespace internal
+
 template <typename T>
 int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
     trace::Block tb("gesv_mixed_gmres");

@@ -10,6 +10,7 @@
 #include "slate_amd/trace.hh"
 
 #include <cstdlib>
+#include <functional>
 #include <vector>
 
 namespace slate {
@@ -18,6 +19,17 @@ namespace internal {
 template <typename T> struct lower_prec { using type = T; };
 template <> struct lower_prec<double> { using type = float; };
 template <> struct lower_prec<std::complex<double>> { using type = std::complex<float>; };
+
+/// GMRES-IR continuation of a mixed-precision solve (gmres.cc): each column
+/// of X (the current estimate) is refined by restarted GMRES on A x = b with
+/// the low-precision factors as right preconditioner (solve_lo, in place on a
+/// low-precision vector); residual(R, V) computes R -= A V.  Returns true when
+/// every column met the classical stopping test; iters = the largest GMRES
+/// iteration count over the columns.
+template <typename T>
+bool gmres_refine(Matrix<T>& B, Matrix<T>& X, real_type<T> Anorm, int itermax, int& iters,
+                  std::function<void(Matrix<T>&, Matrix<T>&)> const& residual,
+                  std::function<void(Matrix<typename lower_prec<T>::type>&)> const& solve_lo, Options const& opts);
 }  // namespace internal
 
 namespace internal {

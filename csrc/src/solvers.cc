@@ -231,6 +231,15 @@ namespace {
 
 template <typename T> using R_of = real_type<T>;
 
+/// SLATE_MIXED_VERBOSE=1: per-iteration refinement distance / contraction on rank 0
+bool mixed_verbose() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_MIXED_VERBOSE");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
 template <typename T>
 bool iter_ref_converged(std::vector<real_type<T>> const& rnorm, std::vector<real_type<T>> const& xnorm,
                         real_type<T> cte) {
@@ -251,6 +260,7 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
     Target target = resolve_target(opts);
     const int itermax = int(get_option<int64_t>(opts, Option::MaxIterations, 30));
     const bool fallback = get_option<int64_t>(opts, Option::UseFallbackSolver, 1) != 0;
+    const bool escalate = get_option<int64_t>(opts, Option::EscalateGmres, 0) != 0;
     const R eps = std::numeric_limits<R>::epsilon();
     Timer timer;
     iter = 0;
@@ -277,25 +287,64 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
         D.insertLocalTiles(target);
         std::vector<R> rnorm(nrhs), xnorm(nrhs);
         timer.reset();
+        // distance to convergence max_j rnorm_j / (xnorm_j cte) per iteration:
+        // its ratio is the refinement's contraction factor
+        std::vector<double> dist;
+        bool stalled = false;
         for (int it = 0; it <= itermax; ++it) {
             // R = B - A X
             slate::copy<T, T>(B, Rm, opts);
             residual(Rm, X);
             colNorms(Norm::Max, X, xnorm.data(), opts);
             colNorms(Norm::Max, Rm, rnorm.data(), opts);
+            double dmax = 0;
+            for (int64_t j = 0; j < nrhs; ++j)
+                dmax = std::max(dmax, double(rnorm[j]) / std::max(double(xnorm[j]) * double(cte), 1e-300));
+            dist.push_back(dmax);
+            if (mixed_verbose() && A.grid()->rank() == 0)
+                std::fprintf(stderr, "# %s it %d: max_j |r_j|/(|x_j| n^1/2 eps |A|) = %.3e%s\n", name, it, dmax,
+                             it > 0 ? (" contraction " + std::to_string(dmax / dist[it - 1])).c_str() : "");
             if (iter_ref_converged<T>(rnorm, xnorm, cte)) {
                 iter = it;
                 timers()[std::string(name) + "::iter_ref"] = timer.elapsed();
                 return 0;
             }
             if (it == itermax) break;
+            // stagnation / projected miss (escalation only): with contraction
+            // rho the remaining log(d) / -log(rho) iterations exceed the budget
+            if (escalate && it >= 3) {
+                const double rho = dist[it] / dist[it - 1], rho2 = dist[it - 1] / dist[it - 2];
+                const double r = std::max(rho, rho2);
+                if (r >= 0.9 || (r < 1 && it + std::log(dmax) / -std::log(r) > 1.2 * itermax)) {
+                    stalled = true;
+                    break;
+                }
+            }
             // correction in low precision: X += A_lo^{-1} R
             slate::copy<T, Lo>(Rm, X_lo, opts);
             solve_lo(A_lo, X_lo);
             slate::copy<Lo, T>(X_lo, D, opts);
             add(T(1), D, T(1), X, opts);
         }
+        timers()[std::string(name) + "::iter_ref"] = timer.elapsed();
+        const int it_ir = int(dist.size()) - 1;
         iter = -itermax - 1;
+        if (escalate) {
+            // GMRES-IR from the current X with the same low-precision factors
+            timer.reset();
+            int it_g = 0;
+            const bool ok = internal::gmres_refine<T>(B, X, Anorm, itermax, it_g, residual,
+                                                      [&](Matrix<Lo>& V) { solve_lo(A_lo, V); }, opts);
+            timers()[std::string(name) + "::gmres"] = timer.elapsed();
+            if (mixed_verbose() && A.grid()->rank() == 0)
+                std::fprintf(stderr, "# %s: classical IR %s after %d iterations, GMRES-IR %s in %d\n", name,
+                             stalled ? "stalled" : "did not converge", it_ir, ok ? "converged" : "failed", it_g);
+            if (ok) {
+                iter = it_ir + it_g;
+                return 0;
+            }
+            iter = -(it_ir + it_g) - 1;
+        }
     }
     if (!fallback) return info;
     // fall back to a full precision solve

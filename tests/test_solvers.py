@@ -171,3 +171,38 @@ def test_gerbt_matches_dense_butterflies(depth):
     s.gerbt(A, depth, 1, 2)
     U, V = _butterfly(m, depth, 1), _butterfly(n, depth, 2)
     assert relerr(s.to_numpy(A), U.T @ a @ V) < 1e-14
+
+
+@pytest.mark.parametrize("dtype", [np.float64, np.complex128])
+@pytest.mark.parametrize("nrhs", [1, 3])
+def test_mixed_escalate_gmres(dtype, nrhs):
+    """Option::EscalateGmres: on a matrix too ill-conditioned for classical
+    fp32 refinement (kappa ~ 1e8: kappa eps_32 > 1, refinement
+    stalls or diverges), gesv_mixed / posv_mixed switch to GMRES-IR with the SAME fp32
+    factors instead of the fp64 refactorization.  Default (reference
+    semantics): classical refinement, then the fallback (iter < 0)."""
+    n = 192
+    a = _ill(n, dtype, 51, 1e8).astype(dtype)
+    b = rnd(n, nrhs, dtype, 52)
+    res = {}
+    for esc in (False, True):
+        A, B = s.from_numpy(a, nb=32), s.from_numpy(b, nb=32)
+        X = s.from_numpy(np.zeros_like(b), nb=32)
+        info, _, it = s.gesv_mixed(A, B, X, escalate_gmres=esc, max_iterations=20)
+        x = s.to_numpy(X)
+        assert info == 0
+        assert np.linalg.norm(a @ x - b) / (np.linalg.norm(a) * np.linalg.norm(x)) < 1e-14
+        res[esc] = it
+    assert res[False] < 0, res          # classical refinement gave up -> fp64 fallback
+    assert res[True] > 0, res           # escalation converged on the fp32 factors
+    # Hermitian positive definite: posv_mixed
+    c = _ill(n, dtype, 53, 1e4)
+    h = (c @ c.conj().T).astype(dtype)
+    for esc in (False, True):
+        H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=32))
+        B, X = s.from_numpy(b, nb=32), s.from_numpy(np.zeros_like(b), nb=32)
+        info, it = s.posv_mixed(H, B, X, escalate_gmres=esc, max_iterations=20)
+        x = s.to_numpy(X)
+        assert info == 0
+        assert np.linalg.norm(h @ x - b) / (np.linalg.norm(h) * np.linalg.norm(x)) < 1e-14
+        assert (it > 0) if esc else (it < 0), (esc, it)
