@@ -6,8 +6,16 @@
 // GPU (SLATE_LAPACK_TARGET=d, the default when a GPU is visible) or on the
 // host (=h), with tile size SLATE_LAPACK_NB (default 512 on the GPU, 256 on
 // the host).  Results are copied back to the user's arrays before returning.
+//
+// Intra-process multi-GPU (reference lapack_api/lapack_slate.hh: the shim
+// goes to the device target whenever GPUs exist, and its rank spreads tiles
+// over all of them): when inproc_ranks() > 1 -- every visible GPU by default,
+// or $SLATE_INPROC_RANKS -- the factorizations / solves / gemm below run on a
+// p x q grid of in-process ranks, one per GPU (inproc.hh), each copying its
+// own tiles in from and back out to the caller's array.
 #include "slate_amd/slate.hh"
 #include "slate_amd/device.hh"
+#include "slate_amd/inproc.hh"
 
 #include <cctype>
 #include <complex>
@@ -55,6 +63,37 @@ Matrix<T> wrap(int64_t m, int64_t n, T* A, int64_t lda, Target t) {
 template <typename T>
 void done(BaseMatrix<T>& A) { A.tileUpdateAllOrigin(); }
 
+/// One caller array of an in-process multi-rank call.
+struct HostArg { void* A; int64_t m, n, ld; bool out; };
+
+/// Run body(mats, rank) on the in-process grid with each array distributed
+/// (2-D block cyclic, tile size lapack_nb) when more than one rank is
+/// configured and the problem has at least as many tile rows as ranks;
+/// returns false (caller takes the one-rank path) otherwise.
+template <typename T>
+bool run_multi(std::vector<HostArg> const& args, std::function<void(std::vector<Matrix<T>>&, int)> const& body) {
+    const int nr = inproc_ranks();
+    if (nr <= 1 || args.empty()) return false;
+    const Target t = lapack_target();
+    const int64_t nb = lapack_nb(t);
+    if ((args[0].m + nb - 1) / nb < 2) return false;   // too small to split
+    int p, q;
+    inproc_grid_shape(nr, p, q);
+    run_in_process(p, q, [&](int rank, GridPtr const& g) {
+        std::vector<Matrix<T>> M;
+        for (auto const& a : args) {
+            Matrix<T> X(a.m, a.n, nb, g);
+            X.insertLocalTiles(t);
+            scatter_from_host(static_cast<T const*>(a.A), a.ld, X, t);
+            M.push_back(X);
+        }
+        body(M, rank);
+        for (size_t i = 0; i < args.size(); ++i)
+            if (args[i].out) gather_to_host(M[i], static_cast<T*>(args[i].A), args[i].ld);
+    });
+    return true;
+}
+
 // LAPACK ipiv (1-based global rows) <-> Pivots (tile offset, element offset)
 template <typename T>
 void to_ipiv(Matrix<T> const& A, Pivots const& P, int* ipiv) {
@@ -81,6 +120,15 @@ void gemm_(char const* ta, char const* tb, int const* m, int const* n, int const
            int const* lda, T* B, int const* ldb, T const* beta, T* C, int const* ldc) {
     Target t = lapack_target();
     Op oa = op_of(ta), ob = op_of(tb);
+    const int64_t am = oa == Op::NoTrans ? *m : *k, an = oa == Op::NoTrans ? *k : *m;
+    const int64_t bm = ob == Op::NoTrans ? *k : *n, bn = ob == Op::NoTrans ? *n : *k;
+    if (run_multi<T>({{C, *m, *n, *ldc, true}, {A, am, an, *lda, false}, {B, bm, bn, *ldb, false}},
+                     [&](std::vector<Matrix<T>>& M, int) {
+                         Matrix<T> Ao = oa == Op::NoTrans ? M[1] : oa == Op::Trans ? transpose(M[1]) : conj_transpose(M[1]);
+                         Matrix<T> Bo = ob == Op::NoTrans ? M[2] : ob == Op::Trans ? transpose(M[2]) : conj_transpose(M[2]);
+                         gemm(*alpha, Ao, Bo, *beta, M[0], lapack_opts());
+                     }))
+        return;
     auto Am = wrap(oa == Op::NoTrans ? *m : *k, oa == Op::NoTrans ? *k : *m, A, *lda, t);
     auto Bm = wrap(ob == Op::NoTrans ? *k : *n, ob == Op::NoTrans ? *n : *k, B, *ldb, t);
     auto Cm = wrap<T>(*m, *n, C, *ldc, t);
@@ -159,6 +207,12 @@ void trmm_(bool solve, char const* side, char const* uplo, char const* transa, c
 
 template <typename T>
 void getrf_(int const* m, int const* n, T* A, int const* lda, int* ipiv, int* info) {
+    if (run_multi<T>({{A, *m, *n, *lda, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+            Pivots P;
+            int inf = int(getrf(M[0], P, lapack_opts()));
+            if (rank == 0) { *info = inf; to_ipiv(M[0], P, ipiv); }
+        }))
+        return;
     Target t = lapack_target();
     auto Am = wrap<T>(*m, *n, A, *lda, t);
     Pivots P;
@@ -170,6 +224,12 @@ void getrf_(int const* m, int const* n, T* A, int const* lda, int* ipiv, int* in
 template <typename T>
 void getrs_(char const* trans, int const* n, int const* nrhs, T* A, int const* lda, int const* ipiv, T* B,
             int const* ldb, int* info) {
+    *info = 0;
+    if (run_multi<T>({{A, *n, *n, *lda, false}, {B, *n, *nrhs, *ldb, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            Pivots P = from_ipiv(M[0], *n, ipiv);
+            getrs(op_of(trans), M[0], P, M[1], lapack_opts());
+        }))
+        return;
     Target t = lapack_target();
     auto Am = wrap<T>(*n, *n, A, *lda, t);
     auto Bm = wrap<T>(*n, *nrhs, B, *ldb, t);
@@ -181,6 +241,12 @@ void getrs_(char const* trans, int const* n, int const* nrhs, T* A, int const* l
 
 template <typename T>
 void gesv_(int const* n, int const* nrhs, T* A, int const* lda, int* ipiv, T* B, int const* ldb, int* info) {
+    if (run_multi<T>({{A, *n, *n, *lda, true}, {B, *n, *nrhs, *ldb, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+            Pivots P;
+            int inf = int(gesv(M[0], P, M[1], lapack_opts()));
+            if (rank == 0) { *info = inf; to_ipiv(M[0], P, ipiv); }
+        }))
+        return;
     Target t = lapack_target();
     auto Am = wrap<T>(*n, *n, A, *lda, t);
     auto Bm = wrap<T>(*n, *nrhs, B, *ldb, t);
@@ -218,6 +284,12 @@ void getri_(int const* n, T* A, int const* lda, int const* ipiv, int* info) {
 
 template <typename T>
 void potrf_(char const* uplo, int const* n, T* A, int const* lda, int* info) {
+    if (run_multi<T>({{A, *n, *n, *lda, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+            HermitianMatrix<T> H(uplo_of(uplo), M[0]);
+            int inf = int(potrf(H, lapack_opts()));
+            if (rank == 0) *info = inf;
+        }))
+        return;
     Target t = lapack_target();
     auto Am = wrap<T>(*n, *n, A, *lda, t);
     HermitianMatrix<T> H(uplo_of(uplo), Am);
@@ -227,6 +299,12 @@ void potrf_(char const* uplo, int const* n, T* A, int const* lda, int* info) {
 
 template <typename T>
 void posv_(char const* uplo, int const* n, int const* nrhs, T* A, int const* lda, T* B, int const* ldb, int* info) {
+    if (run_multi<T>({{A, *n, *n, *lda, true}, {B, *n, *nrhs, *ldb, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+            HermitianMatrix<T> H(uplo_of(uplo), M[0]);
+            int inf = int(posv(H, M[1], lapack_opts()));
+            if (rank == 0) *info = inf;
+        }))
+        return;
     Target t = lapack_target();
     auto Am = wrap<T>(*n, *n, A, *lda, t);
     auto Bm = wrap<T>(*n, *nrhs, B, *ldb, t);

@@ -124,6 +124,15 @@ CommPtr make_rccl_comm(std::string const& unique_id, int nranks, int rank);
 std::string rccl_unique_id();
 /// Split an RCCL communicator (ncclCommSplit); collective over `parent`.
 CommPtr rccl_split(CommPtr const& parent, int color, int key);
+/// In-process communicators (thread_comm.cc): `n` ranks that are threads of
+/// one process; element r is rank r's endpoint, to be used by one thread.
+/// device_mode: buffers are device memory of the ranks' contexts and data
+/// moves by peer copies ordered with events; else host memory (memcpy).
+std::vector<CommPtr> make_thread_comms(int n, bool device_mode);
+/// Wake every rank blocked on this in-process communicator with an exception
+/// (a rank failed); no-op for other transports.
+void thread_comm_abort(Comm& c);
+
 /// Abort every live RCCL communicator of this process (ncclCommAbort; safe
 /// from a watchdog thread while another thread waits on a stuck collective).
 /// Returns how many were aborted; the communicators are unusable afterwards.

@@ -1,4 +1,5 @@
-// Device runtime: one GPU per process, HIP streams/events, caching memory pool.
+// Device runtime: one GPU per rank (per process, or per in-process rank
+// context), HIP streams/events, caching memory pool.
 //
 // Reference counterparts: BLAS++ Queue per device (MatrixStorage.hh:574-591:
 // one comm queue + compute queues), Memory block pool (src/core/Memory.cc).
@@ -46,7 +47,25 @@ int  count();
 void set_device(int dev);
 int  get_device();
 
-/// Per-process stream set.  Queue 1 (panel) is created with high priority.
+/// Device contexts (intra-process multi-GPU).  A context is one rank's view
+/// of a device: its own stream set, event pool and allocator cache.  Every
+/// thread uses the process context (device set_device / $LOCAL_RANK) unless
+/// it has bound another one; in-process ranks (inproc.hh) bind one context
+/// per rank thread, so N ranks on N GPUs -- or several ranks on one GPU --
+/// each schedule onto their own queues.  Memory is returned to the context
+/// that allocated it, whichever thread frees it.
+struct Context;
+/// New context on device `dev` (streams are created on first use).
+Context* context_create(int dev);
+/// Make `ctx` current for the calling thread (nullptr: the process context);
+/// also makes its device current (hipSetDevice).
+void context_bind(Context* ctx);
+Context* context_current();
+/// Synchronize the context's queues, release its cached memory and streams.
+void context_destroy(Context* ctx);
+int context_device(Context* ctx);
+
+/// Stream set of the current context.  Queue 1 (panel) is created with high priority.
 hipStream_t queue(int index);
 void sync_all();
 /// CUs reserved for the panel/comm queues (0 = no partitioning).

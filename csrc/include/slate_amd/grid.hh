@@ -74,8 +74,17 @@ private:
 using GridPtr = std::shared_ptr<Grid>;
 
 /// Default grid for new matrices when none is given (1 x 1 self unless the
-/// embedding runtime installed one).
+/// embedding runtime installed one).  A thread may override it for itself
+/// (in-process ranks: each rank thread sees its own grid).
 GridPtr default_grid();
 void set_default_grid(GridPtr g);
+void set_thread_default_grid(GridPtr g);   // nullptr: back to the process default
+
+/// p x q grid of in-process ranks (thread_comm.cc): one Grid per rank, world
+/// rank r = element r.  `devices` (one entry per rank, may repeat) selects
+/// device mode and enables peer access between them; empty = host mode.
+std::vector<GridPtr> make_thread_grids(int p, int q, GridOrder order, std::vector<int> const& devices);
+/// Abort every in-process communicator of g (see thread_comm_abort).
+void thread_grid_abort(Grid const& g);
 
 }  // namespace slate

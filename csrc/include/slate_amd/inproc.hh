@@ -1,0 +1,48 @@
+// Intra-process multi-GPU: one process drives every GPU of the node.
+//
+// Reference: an MPI rank spreads its tiles over all of its GPUs
+// (tileDevice = func::device_1d_grid, include/slate/internal/
+// MatrixStorage.hh:503-511) and its LAPACK shim switches to the device
+// target when GPUs exist (lapack_api/lapack_slate.hh).  Here every GPU is a
+// rank of the ordinary p x q machinery: run_in_process starts one thread per
+// rank, binds it to its own device context (streams, events, allocator) and
+// an in-process communicator (thread_comm.cc: peer copies over xGMI ordered
+// by events), and runs the same driver code as a one-process-per-GPU job.
+#pragma once
+
+#include "matrix.hh"
+#include "grid.hh"
+
+#include <functional>
+#include <vector>
+
+namespace slate {
+
+/// Run fn(rank, grid) on p*q in-process ranks (threads; rank r on device
+/// devices[r], default r % device count; host mode when no GPU is visible).
+/// Each thread sees `grid` as its default grid.  The first exception of any
+/// rank is rethrown after every thread has stopped (the others are woken by
+/// aborting their communicators).  Calls are serialized.
+void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const& fn,
+                    std::vector<int> devices = {}, GridOrder order = GridOrder::Col);
+
+/// Number of run_in_process calls so far (tests: did a call take the
+/// in-process multi-rank path?) and the grid shape of the last one.
+int64_t inproc_run_count();
+void inproc_last_shape(int& p, int& q);
+
+/// Ranks the single-process APIs (LAPACK-compatible shim) spread work over:
+/// $SLATE_INPROC_RANKS if set, else the number of visible GPUs (1 without).
+int inproc_ranks();
+/// Near-square p x q with p <= q for n ranks (1x1, 1x2, 2x2, 2x4, ...).
+void inproc_grid_shape(int n, int& p, int& q);
+
+/// Copy this rank's tiles of M from / to a global column-major array A (lda)
+/// that every in-process rank can read (scatter) or write (gather, disjoint
+/// tiles): the data path of the single-process APIs.
+template <typename T>
+void scatter_from_host(T const* A, int64_t lda, Matrix<T>& M, Target target);
+template <typename T>
+void gather_to_host(Matrix<T>& M, T* A, int64_t lda);
+
+}  // namespace slate

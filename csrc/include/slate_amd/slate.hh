@@ -14,6 +14,7 @@
 #include "comm.hh"
 #include "grid.hh"
 #include "matrix.hh"
+#include "inproc.hh"
 #include "func.hh"
 #include "method.hh"
 #include "matgen.hh"

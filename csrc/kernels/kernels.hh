@@ -45,6 +45,12 @@ template <typename T>
 void panel_xfer(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb, int64_t maxr, T* G, T* P, int64_t ldp,
                 T* ap, int64_t lda, int mode, hipStream_t s);
 
+// ---- in-process communicator (comm.hip)
+/// out[i] = op_b in[i + b stride], b < nbuf; type 'f' 'd' 'i' (int32) 'l'
+/// (int64) 'b' (int8); op 0 sum, 1 max, 2 min.
+void reduce_slabs(char type, int op, void* out, const void* in, int nbuf, int64_t count, int64_t stride,
+                  hipStream_t s);
+
 // ---- distributed LU row permutations (lu_dist.hip)
 /// out(i, :) = A(sel[i], :) for i < cnt (ncols columns); id_out[i] = id_in[sel[i]]
 /// when id_in is given, else the global row of local row li_base + sel[i].

@@ -36,8 +36,40 @@ struct State {
     size_t host_in_use = 0;
 };
 
-State& st() {
+void flush_stream_free_locked(State& s);
+
+State& process_state() {
     static State* s = new State();  // intentionally leaked: outlives static dtors
+    return *s;
+}
+
+// the calling thread's bound context (nullptr: the process context)
+thread_local State* t_ctx = nullptr;
+
+State& st() { return t_ctx ? *t_ctx : process_state(); }
+
+// owner of every device block, so a block freed by another thread (e.g. a
+// matrix made by a rank thread and dropped by the main thread) returns to the
+// context that allocated it
+std::mutex g_owner_mtx;
+std::map<void*, State*>& owners() {
+    static auto* m = new std::map<void*, State*>();
+    return *m;
+}
+bool g_multi_ctx = false;   // any context besides the process one ever made
+
+void own(void* p, State* s) {
+    if (!g_multi_ctx) return;
+    std::lock_guard<std::mutex> l(g_owner_mtx);
+    owners()[p] = s;
+}
+State& owner_of(void* p) {
+    if (!g_multi_ctx) return st();
+    std::lock_guard<std::mutex> l(g_owner_mtx);
+    auto it = owners().find(p);
+    if (it == owners().end()) return st();
+    State* s = it->second;
+    owners().erase(it);
     return *s;
 }
 
@@ -139,6 +171,54 @@ void reclaim_locked(State& s, bool wait) {
 
 }  // namespace
 
+struct Context : State {};
+
+Context* context_create(int dev) {
+    int n = count();
+    slate_error_if_msg(n <= 0, "context_create: no HIP device");
+    slate_error_if_msg(dev < 0 || dev >= n, "context_create: device out of range");
+    g_multi_ctx = true;
+    auto* c = new Context();
+    c->device = dev;
+    return c;
+}
+
+void context_bind(Context* ctx) {
+    t_ctx = ctx;
+    if (ctx) slate_hip_call(hipSetDevice(ctx->device));
+    else if (process_state().device >= 0) slate_hip_call(hipSetDevice(process_state().device));
+}
+
+Context* context_current() { return static_cast<Context*>(t_ctx); }
+
+int context_device(Context* ctx) { return ctx ? ctx->device : get_device(); }
+
+void context_destroy(Context* ctx) {
+    if (!ctx) return;
+    State* prev = t_ctx;
+    t_ctx = ctx;
+    (void)hipSetDevice(ctx->device);
+    {
+        std::lock_guard<std::mutex> g(ctx->mtx);
+        if (ctx->streams_ready)
+            for (int i = 0; i < kNumQueues; ++i) (void)hipStreamSynchronize(ctx->streams[i]);
+        reclaim_locked(*ctx, true);
+        flush_stream_free_locked(*ctx);
+        for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
+        ctx->free_blocks.clear();
+        ctx->cached = 0;
+        for (auto e : ctx->events) (void)hipEventDestroy(e);
+        ctx->events.clear();
+        if (ctx->streams_ready)
+            for (int i = 0; i < kNumQueues; ++i) (void)hipStreamDestroy(ctx->streams[i]);
+        ctx->streams_ready = false;
+    }
+    t_ctx = prev;
+    context_bind(static_cast<Context*>(prev));
+    // blocks still live (handed out, not yet freed) keep the context alive
+    if (ctx->live.empty()) delete ctx;
+}
+
 int reserved_cus() { return st().reserved_cus; }
 
 bool available() {
@@ -238,14 +318,19 @@ void* malloc_locked(State& s, size_t b) {
 
 void* malloc(size_t bytes) {
     auto& s = st();
-    std::lock_guard<std::mutex> g(s.mtx);
-    ensure_device_locked(s);
-    return malloc_locked(s, bucket(bytes));
+    void* p;
+    {
+        std::lock_guard<std::mutex> g(s.mtx);
+        ensure_device_locked(s);
+        p = malloc_locked(s, bucket(bytes));
+    }
+    own(p, &s);
+    return p;
 }
 
 void* malloc_async(size_t bytes, hipStream_t stream) {
     auto& s = st();
-    std::lock_guard<std::mutex> g(s.mtx);
+    std::unique_lock<std::mutex> g(s.mtx);
     ensure_device_locked(s);
     const size_t b = bucket(bytes);
     void* p = nullptr;
@@ -262,12 +347,13 @@ void* malloc_async(size_t bytes, hipStream_t stream) {
     }
     if (!p) p = malloc_locked(s, b);
     s.live_stream[p] = stream;
+    own(p, &s);
     return p;
 }
 
 void free_async(void* ptr, hipStream_t stream) {
     if (!ptr) return;
-    auto& s = st();
+    auto& s = owner_of(ptr);
     std::lock_guard<std::mutex> g(s.mtx);
     auto it = s.live.find(ptr);
     slate_assert(it != s.live.end());
@@ -283,7 +369,7 @@ size_t bytes_stream_cached() { return st().stream_cached; }
 
 void free(void* ptr) {
     if (!ptr) return;
-    auto& s = st();
+    auto& s = owner_of(ptr);
     std::lock_guard<std::mutex> g(s.mtx);
     auto it = s.live.find(ptr);
     slate_assert(it != s.live.end());

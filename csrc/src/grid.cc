@@ -38,10 +38,15 @@ std::mutex g_mtx;
 GridPtr g_default;
 }
 
+thread_local GridPtr t_default;
+
 GridPtr default_grid() {
+    if (t_default) return t_default;
     std::lock_guard<std::mutex> l(g_mtx);
     return g_default ? g_default : Grid::self();
 }
+
+void set_thread_default_grid(GridPtr g) { t_default = std::move(g); }
 
 void set_default_grid(GridPtr g) {
     std::lock_guard<std::mutex> l(g_mtx);

@@ -1,0 +1,150 @@
+// In-process ranks (see inproc.hh).
+#include "slate_amd/inproc.hh"
+#include "internal.hh"
+
+#include <atomic>
+#include <cmath>
+#include <cstring>
+#include <exception>
+#include <mutex>
+#include <thread>
+
+namespace slate {
+
+namespace {
+std::mutex g_run_mtx;
+// device contexts of the rank threads, reused across runs (stream creation
+// and the allocator's cache survive from one LAPACK call to the next)
+std::vector<device::Context*> g_ctx;
+std::vector<int> g_ctx_dev;
+std::atomic<int64_t> g_runs{0};
+int g_last_p = 0, g_last_q = 0;
+}  // namespace
+
+int64_t inproc_run_count() { return g_runs.load(); }
+void inproc_last_shape(int& p, int& q) { p = g_last_p; q = g_last_q; }
+
+int inproc_ranks() {
+    if (const char* e = std::getenv("SLATE_INPROC_RANKS")) return std::max(1, std::atoi(e));
+    return device::available() ? std::max(1, device::count()) : 1;
+}
+
+void inproc_grid_shape(int n, int& p, int& q) {
+    p = int(std::sqrt(double(n)));
+    while (p > 1 && n % p) --p;
+    q = n / p;
+}
+
+void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const& fn, std::vector<int> devices,
+                    GridOrder order) {
+    std::lock_guard<std::mutex> run_lock(g_run_mtx);
+    const int n = p * q;
+    ++g_runs;
+    g_last_p = p;
+    g_last_q = q;
+    const bool dev = device::available();
+    if (dev && devices.empty())
+        for (int r = 0; r < n; ++r) devices.push_back(r % device::count());
+    if (!dev) devices.clear();
+    slate_error_if_msg(dev && int(devices.size()) != n, "run_in_process: one device per rank");
+    auto grids = make_thread_grids(p, q, order, devices);
+    if (dev) {
+        if (int(g_ctx.size()) < n) { g_ctx.resize(n, nullptr); g_ctx_dev.resize(n, -1); }
+        for (int r = 0; r < n; ++r)
+            if (!g_ctx[r] || g_ctx_dev[r] != devices[r]) {
+                if (g_ctx[r]) device::context_destroy(g_ctx[r]);
+                g_ctx[r] = device::context_create(devices[r]);
+                g_ctx_dev[r] = devices[r];
+            }
+    }
+    std::vector<std::exception_ptr> err(n);
+    std::vector<std::thread> th;
+    for (int r = 0; r < n; ++r) {
+        th.emplace_back([&, r] {
+            try {
+                if (dev) device::context_bind(g_ctx[r]);
+                set_thread_default_grid(grids[r]);
+                fn(r, grids[r]);
+                if (dev) device::sync_all();
+            } catch (...) {
+                err[r] = std::current_exception();
+                thread_grid_abort(*grids[r]);   // wake the ranks waiting on me
+            }
+            set_thread_default_grid(nullptr);
+            if (dev) {
+                try { device::sync_all(); } catch (...) {}
+                device::context_bind(nullptr);
+            }
+        });
+    }
+    for (auto& t : th) t.join();
+    // report the root cause: a rank that failed on its own, not one woken by an abort
+    std::exception_ptr first;
+    for (auto& e : err) {
+        if (!e) continue;
+        try { std::rethrow_exception(e); }
+        catch (CommException const&) { if (!first) first = e; continue; }
+        catch (...) { first = e; break; }
+    }
+    if (first) std::rethrow_exception(first);
+}
+
+template <typename T>
+void scatter_from_host(T const* A, int64_t lda, Matrix<T>& M, Target target) {
+    using namespace internal;
+    const Loc loc = loc_of(target);
+    LocalBlock<T> L = M.local(loc, true);
+    if (L.empty()) return;
+    auto& g = *M.grid();
+    hipStream_t s = target == Target::Devices ? device::queue(device::kCommQueue) : nullptr;
+    for (int64_t j = 0; j < M.nt(); ++j) {
+        if (M.scol_owner(j) != g.mycol()) continue;
+        const int64_t lc = lcol_of(M, j), gc = gcol_of(M, j), nbj = M.tileNb(j);
+        for (int64_t i = 0; i < M.mt(); ++i) {
+            if (M.srow_owner(i) != g.myrow()) continue;
+            const int64_t lr = lrow_of(M, i), gr = grow_of(M, i), mbi = M.tileMb(i);
+            T const* src = A + gr + gc * lda;
+            T* dst = L.ptr + lr + lc * L.ld;
+            if (s) device::memcpy2d_async(dst, L.ld * sizeof(T), src, lda * sizeof(T), mbi * sizeof(T), nbj, s);
+            else for (int64_t c = 0; c < nbj; ++c) std::memcpy(dst + c * L.ld, src + c * lda, mbi * sizeof(T));
+        }
+    }
+    if (s) slate_hip_call(hipStreamSynchronize(s));
+}
+
+template <typename T>
+void gather_to_host(Matrix<T>& M, T* A, int64_t lda) {
+    using namespace internal;
+    auto& st = *M.storage();
+    const bool on_dev = st.has(Loc::Device) && st.state(Loc::Device) != Invalid;
+    const Loc loc = on_dev ? Loc::Device : Loc::Host;
+    LocalBlock<T> L = M.local(loc, false);
+    if (L.empty()) return;
+    auto& g = *M.grid();
+    hipStream_t s = loc == Loc::Device ? device::queue(device::kCommQueue) : nullptr;
+    if (s) device::sync_all();
+    for (int64_t j = 0; j < M.nt(); ++j) {
+        if (M.scol_owner(j) != g.mycol()) continue;
+        const int64_t lc = lcol_of(M, j), gc = gcol_of(M, j), nbj = M.tileNb(j);
+        for (int64_t i = 0; i < M.mt(); ++i) {
+            if (M.srow_owner(i) != g.myrow()) continue;
+            const int64_t lr = lrow_of(M, i), gr = grow_of(M, i), mbi = M.tileMb(i);
+            T const* src = L.ptr + lr + lc * L.ld;
+            T* dst = A + gr + gc * lda;
+            if (s) device::memcpy2d_async(dst, lda * sizeof(T), src, L.ld * sizeof(T), mbi * sizeof(T), nbj, s);
+            else for (int64_t c = 0; c < nbj; ++c) std::memcpy(dst + c * lda, src + c * L.ld, mbi * sizeof(T));
+        }
+    }
+    if (s) slate_hip_call(hipStreamSynchronize(s));
+}
+
+#define SLATE_INPROC_INST(T)                                                          \
+    template void scatter_from_host<T>(T const*, int64_t, Matrix<T>&, Target);      \
+    template void gather_to_host<T>(Matrix<T>&, T*, int64_t);
+
+SLATE_INPROC_INST(float)
+SLATE_INPROC_INST(double)
+SLATE_INPROC_INST(std::complex<float>)
+SLATE_INPROC_INST(std::complex<double>)
+
+}  // namespace slate

@@ -211,3 +211,64 @@ def test_scalapack_pdsgesv_pzcgesv(scalapack):
         assert info.value == 0 and it.value >= 0
         assert relerr(a0 @ x, b0) < 1e-12
         assert np.array_equal(b, b0)
+
+
+def _inproc_lapack_case(lapack, dt, pre):
+    """slate_?gesv_ / ?getrf_ + ?getrs_ / ?potrf_ / ?posv_ / ?gemm_ of ONE
+    process on a grid of in-process ranks (inproc.hh; host mode here, one
+    rank per GPU on a GPU box)."""
+    n, nb = 200, 32
+    f = lambda name: getattr(lapack, f"slate_{pre}{name}_")
+    a = np.asfortranarray(rnd(n, n, dt, 61)) + n * np.eye(n, order="F")
+    b = np.asfortranarray(rnd(n, 3, dt, 62))
+    a0, b0 = a.copy(), b.copy()
+    ipiv = np.zeros(n, np.int32)
+    info = C.c_int(-7)
+    f("gesv")(I(n), I(3), ptr(a), I(n), ptr(ipiv), ptr(b), I(n), C.byref(info))
+    assert info.value == 0 and relerr(a0 @ b, b0) < 1e-12
+    # getrf + getrs, ipiv in LAPACK convention
+    a = a0.copy(order="F")
+    f("getrf")(I(n), I(n), ptr(a), I(n), ptr(ipiv), C.byref(info))
+    assert info.value == 0
+    L = np.tril(a, -1) + np.eye(n)
+    U = np.triu(a)
+    pa = a0.copy()
+    for i, pv in enumerate(ipiv):
+        pa[[i, pv - 1]] = pa[[pv - 1, i]]
+    assert relerr(L @ U, pa) < 1e-12
+    bb = b0.copy(order="F")
+    f("getrs")(ch("N"), I(n), I(3), ptr(a), I(n), ptr(ipiv), ptr(bb), I(n), C.byref(info))
+    assert relerr(a0 @ bb, b0) < 1e-12
+    # Cholesky
+    h = np.asfortranarray(a0 @ a0.conj().T)
+    h0 = h.copy()
+    f("potrf")(ch("L"), I(n), ptr(h), I(n), C.byref(info))
+    Lc = np.tril(h)
+    assert info.value == 0 and relerr(Lc @ Lc.conj().T, h0) < 1e-12
+    h = h0.copy(order="F")
+    bb = b0.copy(order="F")
+    f("posv")(ch("U"), I(n), I(3), ptr(h), I(n), ptr(bb), I(n), C.byref(info))
+    assert info.value == 0 and relerr(h0 @ bb, b0) < 1e-10
+    # gemm with transposes
+    g1 = np.asfortranarray(rnd(150, n, dt, 63))
+    g2 = np.asfortranarray(rnd(n, 90, dt, 64))
+    c = np.asfortranarray(rnd(n, 90, dt, 65))
+    c0 = c.copy()
+    one = (C.c_double * 2)(1.0, 0.0) if dt == np.complex128 else C.c_double(1.0)
+    half = (C.c_double * 2)(0.5, 0.0) if dt == np.complex128 else C.c_double(0.5)
+    f("gemm")(ch("T"), ch("N"), I(n), I(90), I(150), C.byref(one), ptr(g1), I(150), ptr(g2[:150].copy(order="F")),
+              I(150), C.byref(half), ptr(c), I(n), )
+    assert relerr(c, g1.T @ g2[:150] + 0.5 * c0) < 1e-13
+
+
+@pytest.mark.parametrize("ranks", ["2", "4", "8"])
+def test_lapack_inproc_ranks(lapack, ranks, monkeypatch):
+    monkeypatch.setenv("SLATE_INPROC_RANKS", ranks)
+    monkeypatch.setenv("SLATE_LAPACK_NB", "32")
+    c0 = s._slate.inproc_run_count()
+    for dt, pre in ((np.float64, "d"), (np.complex128, "z")):
+        _inproc_lapack_case(lapack, dt, pre)
+    # every call above took the multi-rank path: 6 per type
+    assert s._slate.inproc_run_count() - c0 == 12
+    p, q = s._slate.inproc_last_shape()
+    assert p * q == int(ranks) and p <= q

@@ -622,3 +622,19 @@ def test_band_storage_200k_fits_one_gpu():
     s.gbmm(-1.0, A0, s.from_numpy(x, nb=nb, target="d"), 1.0, R, target="d")
     r = s.to_numpy(R)
     assert np.abs(r).max() / (s.norm(s.Norm.Inf, A0, target="d") * np.abs(x).max()) < 1e-13
+
+
+@pytest.mark.parametrize("ranks", ["2", "4"])
+def test_inproc_multirank_lapack_device(ranks):
+    """Intra-process multi-GPU: ONE process runs the LAPACK shim's dgesv /
+    dgetrf+dgetrs / dpotrf / dposv / dgemm on a grid of in-process ranks, each
+    with its own device context (streams, allocator) and the peer-copy
+    in-process communicator -- on this 1-GPU box all ranks share device 0."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SLATE_INPROC_RANKS=ranks, SLATE_LAPACK_TARGET="d", SLATE_LAPACK_NB="128")
+    r = subprocess.run([sys.executable, os.path.join(root, "scripts", "inproc_check.py"), "1536"], env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "INPROC_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
