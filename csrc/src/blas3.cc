@@ -381,6 +381,150 @@ void trsm_left_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> co
     S.wait_all();
 }
 
+/// X op(A) = alpha B (Side::Right), the column sweep mirroring
+/// trsm_left_sweep, so a right-side solve never transposes B (the reference
+/// turns Right into Left with shallow transpose views, work_trsm.cc:74-82;
+/// here B's local array is used in place).  A is the PHYSICAL triangle whose
+/// op(A) columns conform to B's columns: NoTrans -- A on B's grid, A's column
+/// tiles = B's; otherwise A on B's transposed grid, A's ROW tiles = B's
+/// column tiles (op(A)(k, j) = op(A(j, k)) then lives in A's local column k).
+/// Per step: the diagonal tile down B's process column qk, the solve of B's
+/// block column k there, X(:, k) along the process rows, op(A)'s block row k
+/// (my local columns) down the process columns, one local GEMM.
+///
+/// same_grid (op(A) = A^T / A^H with A on B's OWN grid, A's row tiles = B's
+/// column tiles): op(A)(k, j) = op(A(j, k)) for my columns j sits in other
+/// process rows, so A's block column k (a panel, n x kb) goes along the
+/// process rows from its owner and is all-gathered over the process column;
+/// every process then packs op() of the tiles of its own columns.
+template <typename T>
+void trsm_right_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B,
+                      Target target, int64_t la, bool same_grid = false) {
+    auto& g = *B.grid();
+    const int myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    LocalBlock<T> lbk = B.local(loc, true);
+    LocalBlock<T> lA = A.local(loc, false);
+    const int64_t nt = B.nt(), mloc = lbk.m, nloc = lbk.n, ldx = std::max<int64_t>(mloc, 1);
+    const int p = g.p();
+    // same_grid: offset of tile i within its owner's local rows, and the
+    // largest local row count (all-gather slab)
+    std::vector<int64_t> rowoff(size_t(A.mt()), 0);
+    int64_t maxr = 1;
+    if (same_grid) {
+        std::vector<int64_t> cnt(p, 0);
+        for (int64_t i = 0; i < A.mt(); ++i) {
+            rowoff[i] = cnt[A.srow_owner(i)];
+            cnt[A.srow_owner(i)] += A.tileMb(i);
+        }
+        maxr = std::max<int64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
+    }
+    Sched S(target);
+    if (alpha != T(1))
+        S.task(0, {}, {Sched::tok(9, 0)}, [&](lb::Ctx const& c) {
+            lb::add(c, Uplo::General, mloc, nloc, T(0), lbk.ptr, lbk.ld, alpha, lbk.ptr, lbk.ld);
+        });
+    const int R = int(std::max<int64_t>(2, la + 2));
+    const int64_t nbmax = B.nb();
+    std::vector<Work<T>> WA(R), WX(R), WD(R), WG(R);
+    Work<T> Gs;
+    for (int r = 0; r < R; ++r) {
+        WA[r].resize(target, size_t(nbmax) * std::max<int64_t>(nloc, 1));
+        WX[r].resize(target, size_t(ldx) * nbmax);
+        WD[r].resize(target, size_t(nbmax) * nbmax);
+        if (same_grid) WG[r].resize(target, size_t(p) * maxr * nbmax);
+    }
+    if (same_grid) Gs.resize(target, size_t(maxr) * nbmax);
+    // op(A) upper <=> forward over B's block columns
+    const bool upper = (op == Op::NoTrans) == (uplo_phys == Uplo::Upper);
+    for (int64_t t = 0; t < nt; ++t) {
+        const int64_t k = upper ? t : nt - 1 - t;
+        const int slot = int(t % R);
+        const int64_t kb = B.tileNb(k);
+        const int qk = B.scol_owner(k);
+        const int pr = op == Op::NoTrans ? A.srow_owner(k) : A.scol_owner(k);   // B's process row holding op(A)(k, :)
+        const int64_t lck = lcol_of(B, k);
+        T* D = WD[slot].data();
+        T* WAk = WA[slot].data();
+        T* WXk = WX[slot].data();
+        // op(A)(k, k) down process column qk; op(A)'s block row k (my local
+        // columns, kb x nloc) down every process column from row pr
+        if (same_grid) {
+            T* G = WG[slot].data();
+            const int qa = A.scol_owner(k);
+            S.task(device::kCommQueue, {}, {Sched::bcast(slot)}, [&, k, kb, qa, D, WAk, G](lb::Ctx const& c) {
+                trace::Block t2("trsm_bcast_panel");
+                if (mycol == qa) lb::copy2d(c, lA.m, kb, lA.ptr + lcol_of(A, k) * lA.ld, lA.ld, Gs.data(), maxr);
+                bcast(g.row(), Gs.data(), size_t(maxr * kb), qa, c);
+                g.col().allgather(Gs.data(), G, size_t(maxr * kb), scalar_type<T>(), c.loc(), c.stream);
+                // op() of the tiles of my columns -> W (kb x nloc), and op(A)(k, k)
+                for (int64_t j = 0; j < nt; ++j) {
+                    if (B.scol_owner(j) != mycol) continue;
+                    const T* src = G + size_t(A.srow_owner(j)) * maxr * kb + rowoff[j];
+                    lb::copy<T, T>(c, Uplo::General, op, kb, B.tileNb(j), src, maxr, WAk + lcol_of(B, j) * kb, kb);
+                }
+                lb::copy<T, T>(c, Uplo::General, op, kb, kb, G + size_t(A.srow_owner(k)) * maxr * kb + rowoff[k], maxr,
+                               D, kb);
+            });
+        } else
+        S.task(device::kCommQueue, {}, {Sched::bcast(slot)}, [&, k, kb, qk, pr, D, WAk](lb::Ctx const& c) {
+            trace::Block t2("trsm_bcast_panel");
+            const int64_t lrA = op == Op::NoTrans ? lrow_of(A, k) : 0, lcA = op == Op::NoTrans ? 0 : lcol_of(A, k);
+            if (myrow == pr) {
+                if (op == Op::NoTrans) lb::copy2d(c, kb, nloc, lA.ptr + lrA, lA.ld, WAk, kb);
+                else lb::copy<T, T>(c, Uplo::General, op, kb, nloc, lA.ptr + lcA * lA.ld, lA.ld, WAk, kb);
+                if (mycol == qk) lb::copy2d(c, kb, kb, WAk + lck * kb, kb, D, kb);   // op(A)(k, k)
+            }
+            bcast(g.col(), WAk, size_t(kb * nloc), pr, c);
+            if (mycol == qk) bcast(g.col(), D, size_t(kb * kb), pr, c);
+        });
+        // solve B(:, k) on process column qk, then X(:, k) along the rows
+        S.task(0, {Sched::bcast(slot)}, {Sched::tok(9, 0)}, [&, kb, qk, D, WXk, lck](lb::Ctx const& c) {
+            if (mycol == qk && mloc > 0) {
+                // D holds op(A)(k, k) explicitly: solve against it as NoTrans
+                // with op(A)'s triangle (upper iff forward)
+                lb::trsm(c, Side::Right, upper ? Uplo::Upper : Uplo::Lower, Op::NoTrans, diag, mloc, kb, T(1), D, kb,
+                         lbk.ptr + lck * lbk.ld, lbk.ld);
+                lb::copy2d(c, mloc, kb, lbk.ptr + lck * lbk.ld, lbk.ld, WXk, ldx);
+            }
+        });
+        S.task(device::kCommQueue, {Sched::tok(9, 0)}, {Sched::tok(8, slot)}, [&, kb, qk, WXk](lb::Ctx const& c) {
+            trace::Block t2("trsm_bcast_x");
+            bcast(g.row(), WXk, size_t(ldx * kb), qk, c);
+        });
+        // B(:, j) -= X(:, k) op(A)(k, j) for the block columns still to solve
+        S.task(0, {Sched::tok(8, slot), Sched::bcast(slot)}, {Sched::tok(9, 0)}, [&, k, kb, WAk, WXk](lb::Ctx const& c) {
+            const int64_t c0 = upper ? lcol_of(B, k + 1) : 0;
+            const int64_t c1 = upper ? nloc : lcol_of(B, k);
+            if (c1 > c0 && mloc > 0)
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, mloc, c1 - c0, kb, T(-1), WXk, ldx, WAk + c0 * kb, kb, T(1),
+                         lbk.ptr + c0 * lbk.ld, lbk.ld);
+        });
+    }
+    S.wait_all();
+}
+
+/// Do op(A)'s columns line up with B's columns (trsm_right_sweep's layout)?
+template <typename T>
+bool b_conforms_right(BaseMatrix<T> const& Ap, Op op, BaseMatrix<T> const& B) {
+    if (B.op() != Op::NoTrans || !B.aligned()) return false;
+    auto& ga = *Ap.grid();
+    auto& gb = *B.grid();
+    if (!ga.same_processes(gb) || Ap.mb() != Ap.nb()) return false;
+    if (op == Op::NoTrans) {
+        if (!cols_conform(Ap, B)) return false;
+        for (int64_t j = 0; j < Ap.nt(); ++j) if (Ap.tileMb(j) != B.tileNb(j)) return false;
+        return true;
+    }
+    // A on B's transposed grid: A's process (r, c) is B's process (c, r)
+    if (gb.p() != ga.q() || gb.q() != ga.p() || (gb.size() > 1 && gb.order() == ga.order())) return false;
+    if (B.nt() != Ap.mt()) return false;
+    for (int64_t j = 0; j < Ap.mt(); ++j)
+        if (Ap.tileMb(j) != B.tileNb(j) || Ap.srow_owner(j) != B.scol_owner(j) || Ap.tileMb(j) != Ap.tileNb(j))
+            return false;
+    return true;
+}
+
 /// Stationary-A triangular solve for narrow B (reference src/work/work_trsmA.cc):
 /// A never moves.  Each process keeps a partial-sum block W (its local rows x
 /// all columns of B); step k sums block row k of W across process row pk,
@@ -546,8 +690,29 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
     // MethodTrsm (reference include/slate/method.hh:35-45): stationary A for a
     // single block column of right-hand sides, else the trsmB sweep
     Method method = get_option<int64_t>(opts, Option::MethodTrsm, MethodTrsm::Auto);
-    if (method == MethodTrsm::Auto) method = B.nt() < 2 ? MethodTrsm::TrsmA : MethodTrsm::TrsmB;
+    // (narrow = one block column of right-hand sides: B's columns for Left,
+    // its rows for Right)
+    if (method == MethodTrsm::Auto)
+        method = (side == Side::Left ? B.nt() : B.mt()) < 2 ? MethodTrsm::TrsmA : MethodTrsm::TrsmB;
     slate_error_if_msg(method != MethodTrsm::TrsmA && method != MethodTrsm::TrsmB, "trsm: unknown MethodTrsm");
+    // Right side: the column sweep on B in place when op(A)'s columns conform
+    // to B's (the usual case: same tiles, A on B's grid or, for op(A) =
+    // A^T / A^H, on its transposed grid); else reduced to Left below
+    if (side == Side::Right && method == MethodTrsm::TrsmB) {
+        const Op op = A.op();
+        BaseMatrix<T> Ap = op == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(op == Op::ConjTrans);
+        if (Ap.aligned() && b_conforms_right(Ap, op, B)) {
+            trsm_right_sweep(A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts));
+            internal::finish_origin(B, opts);
+            return;
+        }
+        if (op != Op::NoTrans && Ap.aligned() && b_conforms_right(Ap, Op::NoTrans, B)) {
+            // op(A) = A^T / A^H with A on B's own grid: column panels gathered
+            trsm_right_sweep(A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts), true);
+            internal::finish_origin(B, opts);
+            return;
+        }
+    }
     // distributed: reduce to Left
     if (side == Side::Right) {
         // X op(A) = alpha B  <=>  op(A)^T X^T = alpha B^T (use conj for ConjTrans pairs)

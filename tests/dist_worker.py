@@ -72,6 +72,25 @@ def case_trsm(tg, dt, nb):
     B = s.from_numpy(b, nb=nb, target=tg)
     s.trsm(s.Side.Left, 1.0, T, B, target=tg)
     assert relerr(t @ s.to_numpy(B), b) < tol(dt)
+    # Right side (native column sweep, B in place): every uplo / op / diag
+    m = 90
+    a0 = rnd(n, n, dt, 7) / n + 2 * np.eye(n, dtype=dt)
+    for uplo, tri in ((s.Uplo.Lower, np.tril), (s.Uplo.Upper, np.triu)):
+        for diag in (s.Diag.NonUnit, s.Diag.Unit):
+            teff = tri(a0).copy()
+            if diag == s.Diag.Unit:
+                np.fill_diagonal(teff, 1)
+            for op in ("n", "t", "c"):
+                b = rnd(m, n, dt, 8)
+                T = s.TriangularMatrix(uplo, diag, s.from_numpy(a0, nb=nb, target=tg))
+                opt = teff
+                if op == "t":
+                    T, opt = s.transpose(T), teff.T
+                elif op == "c":
+                    T, opt = s.conj_transpose(T), teff.conj().T
+                B = s.from_numpy(b, nb=nb, target=tg)
+                s.trsm(s.Side.Right, dt(2), T, B, target=tg, method_trsm="trsmB")
+                assert relerr(s.to_numpy(B) @ opt, 2 * b) < 10 * tol(dt), (uplo, diag, op)
 
 
 def case_trmm(tg, dt, nb):
@@ -633,6 +652,18 @@ def case_solve_notemp(tg, dt, nb):
         s.trsm(s.Side.Left, 1.0, s.transpose(L), Bt, target=tg, method_trsm=meth)
         assert not chk or s._slate.storage_alloc_max() < full / 4, meth
         assert relerr(np.tril(h).T @ s.to_numpy(Bt), b) < 100 * tol(dt), meth
+    # Right-side solve on an n x n B: the column sweep works on B in place
+    # (no transposed copy of B), op(A) = A^H with A on B's grid included
+    L = s.TriangularMatrix(s.Uplo.Lower, s.Diag.NonUnit, s.from_numpy(np.tril(h), nb=nb, target=tg))
+    for opname in ("n", "c"):
+        bb = rnd(n, n, dt, 143)
+        Bn = s.from_numpy(bb, nb=nb, target=tg)
+        Lop = L if opname == "n" else s.conj_transpose(L)
+        ref = np.tril(h) if opname == "n" else np.tril(h).conj().T
+        s._slate.storage_alloc_reset()
+        s.trsm(s.Side.Right, 1.0, Lop, Bn, target=tg)
+        assert not chk or s._slate.storage_alloc_max() < full / 4, ("trsm right", opname, s._slate.storage_alloc_max(), full)
+        assert relerr(s.to_numpy(Bn) @ ref, bb) < 100 * tol(dt), ("trsm right", opname)
     if dt in (np.float64, np.complex128):
         H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
         B = s.from_numpy(b, nb=nb, target=tg)
