@@ -397,9 +397,15 @@ void trsm_left_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> co
 /// process rows, so A's block column k (a panel, n x kb) goes along the
 /// process rows from its owner and is all-gathered over the process column;
 /// every process then packs op() of the tiles of its own columns.
+///
+/// solve = false runs trmm's B := alpha B op(A) with the same panels, in
+/// place: op(A) upper -> block columns in descending order (B(:, k) is still
+/// the original when its turn comes), lower -> ascending; per step the old
+/// B(:, k) goes along the rows, the other columns accumulate B(:, k) op(A)(k, j)
+/// and B(:, k) is multiplied by the diagonal triangle last.
 template <typename T>
-void trsm_right_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B,
-                      Target target, int64_t la, bool same_grid = false) {
+void tr_right_sweep(bool solve, Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> const& A, Matrix<T>& B,
+                    Target target, int64_t la, bool same_grid = false) {
     auto& g = *B.grid();
     const int myrow = g.myrow(), mycol = g.mycol();
     const Loc loc = loc_of(target);
@@ -420,7 +426,7 @@ void trsm_right_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> c
         maxr = std::max<int64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
     }
     Sched S(target);
-    if (alpha != T(1))
+    if (solve && alpha != T(1))
         S.task(0, {}, {Sched::tok(9, 0)}, [&](lb::Ctx const& c) {
             lb::add(c, Uplo::General, mloc, nloc, T(0), lbk.ptr, lbk.ld, alpha, lbk.ptr, lbk.ld);
         });
@@ -435,10 +441,11 @@ void trsm_right_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> c
         if (same_grid) WG[r].resize(target, size_t(p) * maxr * nbmax);
     }
     if (same_grid) Gs.resize(target, size_t(maxr) * nbmax);
-    // op(A) upper <=> forward over B's block columns
+    // op(A) upper <=> forward over B's block columns (solve), backward (multiply)
     const bool upper = (op == Op::NoTrans) == (uplo_phys == Uplo::Upper);
+    const bool forward = solve ? upper : !upper;
     for (int64_t t = 0; t < nt; ++t) {
-        const int64_t k = upper ? t : nt - 1 - t;
+        const int64_t k = forward ? t : nt - 1 - t;
         const int slot = int(t % R);
         const int64_t kb = B.tileNb(k);
         const int qk = B.scol_owner(k);
@@ -478,6 +485,28 @@ void trsm_right_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> c
             bcast(g.col(), WAk, size_t(kb * nloc), pr, c);
             if (mycol == qk) bcast(g.col(), D, size_t(kb * kb), pr, c);
         });
+        if (!solve) {
+            // multiply: the ORIGINAL B(:, k) along the rows, the other columns
+            // accumulate it, B(:, k) times the diagonal triangle last
+            S.task(device::kCommQueue, {Sched::tok(9, 0)}, {Sched::tok(8, slot)}, [&, kb, qk, WXk, lck](lb::Ctx const& c) {
+                trace::Block t2("trmm_bcast_b");
+                if (mycol == qk) lb::copy2d(c, mloc, kb, lbk.ptr + lck * lbk.ld, lbk.ld, WXk, ldx);
+                bcast(g.row(), WXk, size_t(ldx * kb), qk, c);
+            });
+            S.task(0, {Sched::tok(8, slot), Sched::bcast(slot)}, {Sched::tok(9, 0)},
+                   [&, k, kb, qk, D, WAk, WXk, lck](lb::Ctx const& c) {
+                trace::Block t2("trmm_update");
+                const int64_t c0 = upper ? lcol_of(B, k + 1) : 0;
+                const int64_t c1 = upper ? nloc : lcol_of(B, k);
+                if (c1 > c0 && mloc > 0)
+                    lb::gemm(c, Op::NoTrans, Op::NoTrans, mloc, c1 - c0, kb, T(1), WXk, ldx, WAk + c0 * kb, kb, T(1),
+                             lbk.ptr + c0 * lbk.ld, lbk.ld);
+                if (mycol == qk && mloc > 0)
+                    lb::trmm(c, Side::Right, upper ? Uplo::Upper : Uplo::Lower, Op::NoTrans, diag, mloc, kb, T(1), D, kb,
+                             lbk.ptr + lck * lbk.ld, lbk.ld);
+            });
+            continue;
+        }
         // solve B(:, k) on process column qk, then X(:, k) along the rows
         S.task(0, {Sched::bcast(slot)}, {Sched::tok(9, 0)}, [&, kb, qk, D, WXk, lck](lb::Ctx const& c) {
             if (mycol == qk && mloc > 0) {
@@ -501,10 +530,14 @@ void trsm_right_sweep(Uplo uplo_phys, Op op, Diag diag, T alpha, BaseMatrix<T> c
                          lbk.ptr + c0 * lbk.ld, lbk.ld);
         });
     }
+    if (!solve && alpha != T(1))
+        S.task(0, {}, {Sched::tok(9, 0)}, [&](lb::Ctx const& c) {
+            lb::add(c, Uplo::General, mloc, nloc, T(0), lbk.ptr, lbk.ld, alpha, lbk.ptr, lbk.ld);
+        });
     S.wait_all();
 }
 
-/// Do op(A)'s columns line up with B's columns (trsm_right_sweep's layout)?
+/// Do op(A)'s columns line up with B's columns (tr_right_sweep's layout)?
 template <typename T>
 bool b_conforms_right(BaseMatrix<T> const& Ap, Op op, BaseMatrix<T> const& B) {
     if (B.op() != Op::NoTrans || !B.aligned()) return false;
@@ -702,13 +735,13 @@ void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
         const Op op = A.op();
         BaseMatrix<T> Ap = op == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(op == Op::ConjTrans);
         if (Ap.aligned() && b_conforms_right(Ap, op, B)) {
-            trsm_right_sweep(A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts));
+            tr_right_sweep(true, A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts));
             internal::finish_origin(B, opts);
             return;
         }
         if (op != Op::NoTrans && Ap.aligned() && b_conforms_right(Ap, Op::NoTrans, B)) {
             // op(A) = A^T / A^H with A on B's own grid: column panels gathered
-            trsm_right_sweep(A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts), true);
+            tr_right_sweep(true, A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts), true);
             internal::finish_origin(B, opts);
             return;
         }
@@ -1310,6 +1343,17 @@ void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
     // distributed: reduce to Left with a NoTrans triangle conforming to B's
     // rows (as trsm does), then a SUMMA that skips the zero part of A
     auto gB = B.grid();
+    if (side == Side::Right) {
+        // in place on B when op(A)'s columns conform to B's (see tr_right_sweep)
+        const Op op = A.op();
+        BaseMatrix<T> Ap = op == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(op == Op::ConjTrans);
+        if (Ap.aligned() && (b_conforms_right(Ap, op, B) || (op != Op::NoTrans && b_conforms_right(Ap, Op::NoTrans, B)))) {
+            tr_right_sweep(false, A.uplo_physical(), op, A.diag(), alpha, Ap, B, target, option_la(opts),
+                           !b_conforms_right(Ap, op, B));
+            internal::finish_origin(B, opts);
+            return;
+        }
+    }
     if (side == Side::Right) {
         // B op(A) = (op(A)^H B^H)^H
         bool conj = is_complex_v<T>;

@@ -104,13 +104,16 @@ def case_trmm(tg, dt, nb):
                 teff = tri(t).copy()
                 if diag == s.Diag.Unit:
                     np.fill_diagonal(teff, 1)
-                for op in ("n", "c"):
+                for op in ("n", "t", "c"):
                     b = rnd(m, n, dt, 52)
                     T = s.TriangularMatrix(uplo, diag, s.from_numpy(t, nb=nb, target=tg))
                     opt = teff
                     if op == "c":
                         T = s.conj_transpose(T)
                         opt = teff.conj().T
+                    elif op == "t":
+                        T = s.transpose(T)
+                        opt = teff.T
                     B = s.from_numpy(b, nb=nb, target=tg)
                     s.trmm(side, dt(1.5), T, B, target=tg)
                     ref = 1.5 * (opt @ b if side == s.Side.Left else b @ opt)
@@ -664,6 +667,15 @@ def case_solve_notemp(tg, dt, nb):
         s.trsm(s.Side.Right, 1.0, Lop, Bn, target=tg)
         assert not chk or s._slate.storage_alloc_max() < full / 4, ("trsm right", opname, s._slate.storage_alloc_max(), full)
         assert relerr(s.to_numpy(Bn) @ ref, bb) < 100 * tol(dt), ("trsm right", opname)
+    for opname in ("n", "t"):
+        bb = rnd(n, n, dt, 144)
+        Bn = s.from_numpy(bb, nb=nb, target=tg)
+        Lop = L if opname == "n" else s.transpose(L)
+        ref = np.tril(h) if opname == "n" else np.tril(h).T
+        s._slate.storage_alloc_reset()
+        s.trmm(s.Side.Right, dt(0.5), Lop, Bn, target=tg)
+        assert not chk or s._slate.storage_alloc_max() < full / 4, ("trmm right", opname, s._slate.storage_alloc_max(), full)
+        assert relerr(s.to_numpy(Bn), 0.5 * bb @ ref) < 100 * tol(dt), ("trmm right", opname)
     if dt in (np.float64, np.complex128):
         H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
         B = s.from_numpy(b, nb=nb, target=tg)
