@@ -1181,6 +1181,93 @@ void hemmC_left(Uplo uplo, bool herm, T alpha, BaseMatrix<T> const& A, BaseMatri
     S.wait_all();
 }
 
+/// hemm / symm, Right, in place on C (no transposed copies of B and C):
+/// C = alpha B A + beta C as a SUMMA over A's block rows.  Row k of the
+/// Hermitian A is assembled from what is stored: the stored part of block row
+/// k (process row pk, down the process columns) and, mirrored, the stored
+/// part of block column k (gathered: along the rows from its owner, then
+/// all-gathered over the column), op = ^H (herm) or ^T (symm); the diagonal
+/// tile is expanded from its stored triangle.  B(:, k) goes along the rows and
+/// every process adds B(:, k) A(k, my columns) to its C in one GEMM.
+/// Needs A on C's grid with A's tiles = C's column tiles, B's rows = C's rows
+/// and B's column tiles = A's tiles.
+template <typename T>
+void hemmC_right(Uplo uplo, bool herm, T alpha, BaseMatrix<T> const& A, BaseMatrix<T> const& B, T beta,
+                 Matrix<T>& C, Target target, int64_t la) {
+    auto& g = *C.grid();
+    const int p = g.p(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    LocalBlock<T> lc = C.local(loc, true), lB = B.local(loc, false), lA = A.local(loc, false);
+    const int64_t kt = A.nt(), nloc = lc.n, mloc = lc.m, nb = A.nb(), ldx = std::max<int64_t>(mloc, 1);
+    const bool lower = (uplo == Uplo::Lower);
+    const Op opH = herm ? Op::ConjTrans : Op::Trans;
+    std::vector<int64_t> rowoff(size_t(A.mt()), 0);
+    std::vector<int64_t> cnt(p, 0);
+    for (int64_t i = 0; i < A.mt(); ++i) {
+        rowoff[i] = cnt[A.srow_owner(i)];
+        cnt[A.srow_owner(i)] += A.tileMb(i);
+    }
+    const int64_t maxr = std::max<int64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
+    Sched S(target);
+    const int64_t tC = Sched::tok(9, 0);
+    S.task(0, {}, {tC}, [&](lb::Ctx const& c) { scale_c(c, beta, mloc, nloc, lc.ptr, lc.ld); });
+    const int R = int(std::max<int64_t>(2, la + 2));
+    std::vector<Work<T>> WA(R), WX(R), WR(R), WG(R);
+    Work<T> Gs(target, size_t(maxr) * nb);
+    for (int r = 0; r < R; ++r) {
+        WA[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
+        WR[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
+        WX[r].resize(target, size_t(ldx) * nb);
+        WG[r].resize(target, size_t(p) * maxr * nb);
+    }
+    for (int64_t k = 0; k < kt; ++k) {
+        const int slot = int(k % R);
+        const int64_t kb = A.tileNb(k);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k), qb = B.scol_owner(k);
+        T* WAk = WA[slot].data();
+        T* WXk = WX[slot].data();
+        T* WRk = WR[slot].data();
+        T* G = WG[slot].data();
+        S.task(device::kCommQueue, {}, {Sched::bcast(slot)}, [&, k, kb, pk, qk, qb, WAk, WXk, WRk, G](lb::Ctx const& c) {
+            trace::Block t2("hemm_bcast");
+            // block column k (all rows) everywhere, block row k down the columns
+            if (mycol == qk) lb::copy2d(c, lA.m, kb, lA.ptr + lcol_of(A, k) * lA.ld, lA.ld, Gs.data(), maxr);
+            bcast(g.row(), Gs.data(), size_t(maxr * kb), qk, c);
+            g.col().allgather(Gs.data(), G, size_t(maxr * kb), scalar_type<T>(), c.loc(), c.stream);
+            if (nloc > 0) {
+                if (myrow == pk) lb::copy2d(c, kb, nloc, lA.ptr + lrow_of(A, k), lA.ld, WRk, kb);
+                bcast(g.col(), WRk, size_t(kb * nloc), pk, c);
+            }
+            if (mloc > 0) {
+                if (mycol == qb) lb::copy2d(c, mloc, kb, lB.ptr + lcol_of(B, k) * lB.ld, lB.ld, WXk, ldx);
+                bcast(g.row(), WXk, size_t(ldx * kb), qb, c);
+            }
+            // A(k, j) for my column tiles j: stored in row k (j on the stored
+            // side), mirrored from column k (other side), expanded diagonal
+            for (int64_t j = 0; j < C.nt(); ++j) {
+                if (C.scol_owner(j) != mycol) continue;
+                const int64_t nbj = C.tileNb(j), cj = lcol_of(C, j);
+                T const* Gj = G + size_t(A.srow_owner(j)) * maxr * kb + rowoff[j];
+                T* Wj = WAk + cj * kb;
+                if (j == k) {
+                    lb::copy<T, T>(c, uplo, Op::NoTrans, kb, kb, Gj, maxr, Wj, kb);
+                    lb::copy<T, T>(c, lower ? Uplo::Upper : Uplo::Lower, opH, kb, kb, Gj, maxr, Wj, kb);
+                } else if (lower ? j < k : j > k) {
+                    lb::copy2d(c, kb, nbj, WRk + cj * kb, kb, Wj, kb);
+                } else {
+                    lb::copy<T, T>(c, Uplo::General, opH, kb, nbj, Gj, maxr, Wj, kb);
+                }
+            }
+        });
+        S.task(0, {Sched::bcast(slot)}, {tC}, [&, kb, WAk, WXk](lb::Ctx const& c) {
+            trace::Block t2("hemm_update");
+            if (mloc > 0 && nloc > 0)
+                lb::gemm(c, Op::NoTrans, Op::NoTrans, mloc, nloc, kb, alpha, WXk, ldx, WAk, kb, T(1), lc.ptr, lc.ld);
+        });
+    }
+    S.wait_all();
+}
+
 /// hemmA / symmA, Left (reference src/hemmA.cc): A stays where it is.  B
 /// (narrow) is replicated on the device; every process multiplies its stored
 /// tiles by the matching rows of B, both as A(i,j) B(j,:) into row i and as
@@ -1244,9 +1331,21 @@ void hemm_dist(Side side, bool herm, T alpha, BaseTrapezoidMatrix<T> const& A, M
                Matrix<T>& C, Options const& opts) {
     Target target = resolve_target(opts);
     Method method = get_option<int64_t>(opts, Option::MethodHemm, MethodHemm::Auto);
-    if (method == MethodHemm::Auto) method = B.nt() < 2 ? MethodHemm::HemmA : MethodHemm::HemmC;
+    if (method == MethodHemm::Auto)   // narrow B: one block of right-hand sides (columns Left, rows Right)
+        method = (side == Side::Left ? B.nt() : B.mt()) < 2 ? MethodHemm::HemmA : MethodHemm::HemmC;
     slate_error_if_msg(method != MethodHemm::HemmA && method != MethodHemm::HemmC, "hemm: unknown MethodHemm");
     auto gC = C.grid();
+    if (side == Side::Right && method == MethodHemm::HemmC && C.op() == Op::NoTrans && C.aligned() &&
+        A.op() == Op::NoTrans && A.aligned() && A.mb() == A.nb() && B.op() == Op::NoTrans && B.aligned() &&
+        cols_conform(BaseMatrix<T>(A), BaseMatrix<T>(C)) && rows_conform(BaseMatrix<T>(B), BaseMatrix<T>(C)) &&
+        B.nt() == A.nt()) {
+        bool ok = true;
+        for (int64_t j = 0; j < A.nt(); ++j) ok = ok && B.tileNb(j) == A.tileNb(j) && A.tileMb(j) == A.tileNb(j);
+        if (ok) {
+            hemmC_right(A.uplo(), herm, alpha, A, B, beta, C, target, option_la(opts));
+            return;
+        }
+    }
     if (side == Side::Right) {
         // C = a B A + b C  <=>  C^H = conj(a) A B^H + conj(b) C^H (A = A^H), C^T = a A B^T + b C^T (A = A^T)
         Matrix<T> Ct = materialize<T>(herm ? conj_transpose(C) : transpose(C), target, gC, C.nb(), C.mb(), 0, 0);

@@ -124,9 +124,30 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         else dinfo.data()[0] = 0;
     }
 
+    // 1x1 device grid: once the remaining matrix is at most `tail` wide, factor
+    // it with ONE recursive device potrf (local_blas.cc: 64-column leaves,
+    // four launches each) instead of nb-wide steps, whose per-step panel,
+    // trsm and lookahead hops dominate when the trailing update has shrunk to
+    // a few hundred microseconds.  SLATE_POTRF_TAIL = width (0: off).
+    static const int64_t tail_env = [] {
+        const char* e = std::getenv("SLATE_POTRF_TAIL");
+        return e ? std::atoll(e) : int64_t(4096);
+    }();
+    const bool tail_ok = p * q == 1 && target == Target::Devices && tail_env > 0;
     for (int64_t k = 0; k < nt; ++k) {
         const int64_t kb = A.tileNb(k);
         const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        if (tail_ok && k > 0 && A.n() - grow_of(A, k) <= std::max(tail_env, nb)) {
+            const int64_t kk0 = grow_of(A, k), rest = A.n() - kk0;
+            std::vector<int64_t> cols;
+            for (int64_t j = k; j < nt; ++j) cols.push_back(Sched::col(j));
+            T* akk0 = a + lrow_of(A, k) + lcol_of(A, k) * lda;
+            S.task(1, cols, cols, [&, akk0, rest, kk0](lb::Ctx const& c) {
+                trace::Block tb("potrf_tail");
+                lb::potrf(c, Uplo::Lower, rest, akk0, lda, dinfo.data(), kk0);
+            });
+            break;
+        }
         const int64_t lr_k = lrow_of(A, k), lr_k1 = lrow_of(A, k + 1);
         const int64_t mrows = mloc - lr_k1;
         const int slot = int(k % R);

@@ -667,6 +667,14 @@ def case_solve_notemp(tg, dt, nb):
         s.trsm(s.Side.Right, 1.0, Lop, Bn, target=tg)
         assert not chk or s._slate.storage_alloc_max() < full / 4, ("trsm right", opname, s._slate.storage_alloc_max(), full)
         assert relerr(s.to_numpy(Bn) @ ref, bb) < 100 * tol(dt), ("trsm right", opname)
+    # hemm Right on n x n B, C: in place, no (conj-)transposed copies
+    H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
+    bb, cc = rnd(n, n, dt, 145), rnd(n, n, dt, 146)
+    Bn, Cn = s.from_numpy(bb, nb=nb, target=tg), s.from_numpy(cc, nb=nb, target=tg)
+    s._slate.storage_alloc_reset()
+    s.hemm(s.Side.Right, dt(1.5), H, Bn, dt(0.5), Cn, target=tg)
+    assert not chk or s._slate.storage_alloc_max() < full / 4, ("hemm right", s._slate.storage_alloc_max(), full)
+    assert relerr(s.to_numpy(Cn), 1.5 * bb @ h + 0.5 * cc) < 100 * tol(dt), "hemm right"
     for opname in ("n", "t"):
         bb = rnd(n, n, dt, 144)
         Bn = s.from_numpy(bb, nb=nb, target=tg)
