@@ -289,6 +289,167 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
     return reduce_info(info, g.world());
 }
 
+/// Upper storage A = U^H U, in place (the reference factors the conjugate
+/// transpose as a shallow view, potrf.cc:45-47; here the mirror of
+/// potrf_lower with block ROWS): per step the diagonal tile along process
+/// row pk, the row panel U(k, k+1:) = U(k,k)^{-H} A(k, k+1:) solved there
+/// and broadcast down the process columns, the tiles U(k, I) each process
+/// needs for its local ROWS all-gathered over the process row, and the upper
+/// trapezoid of every local column range updated by C -= U(k, rows)^H
+/// U(k, cols) (on a 1 x 1 grid one herk + one gemm per range).
+template <typename T>
+int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
+    using namespace internal;
+    auto& g = *A.grid();
+    const int p = g.p(), q = g.q(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    const int64_t nt = A.nt();
+    if (nt == 0) return 0;
+    slate_error_if_msg(A.mb() != A.nb(), "potrf requires square tiles");
+    slate_error_if_msg(!A.aligned(), "potrf requires a tile-aligned matrix");
+    const int64_t nb = A.nb();
+    LocalBlock<T> L = A.local(loc, true);
+    T* a = L.ptr;
+    const int64_t lda = L.ld, nloc = L.n;
+    Sched S(target);
+    const int R = int(std::max<int64_t>(2, la + 2));
+    std::vector<Work<T>> W(R), Wt(R), Dk(R), Ws(R), X(R);
+    const int64_t lcm = std::lcm(int64_t(p), int64_t(q));
+    const int64_t maxcnt = ceildiv(nt, lcm) + 1;
+    const int64_t mloc = L.m;
+    for (int r = 0; r < R; ++r) {
+        if (p > 1) W[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
+        if (q > 1) {
+            Wt[r].resize(target, size_t(q) * maxcnt * nb * nb);
+            Ws[r].resize(target, size_t(maxcnt) * nb * nb);
+            Dk[r].resize(target, size_t(nb) * nb);
+        }
+        if (p * q > 1) X[r].resize(target, size_t(nb) * std::max<int64_t>(mloc, 1));
+    }
+    Work<int> dinfo(target, 1);
+    {
+        lb::Ctx c0 = S.ctx(1);
+        if (c0.dev()) device::memset_async(dinfo.data(), 0, sizeof(int), c0.stream);
+        else dinfo.data()[0] = 0;
+    }
+    for (int64_t k = 0; k < nt; ++k) {
+        const int64_t kb = A.tileNb(k);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int64_t lr_k = lrow_of(A, k), lr_k1 = lrow_of(A, k + 1);
+        const int64_t lc_k1 = lcol_of(A, k + 1), ncols = nloc - lc_k1;
+        const int slot = int(k % R);
+        const int64_t kk = grow_of(A, k);
+        const bool in_row = (myrow == pk);
+        const int64_t lc_k = (mycol == qk) ? lcol_of(A, k) : 0;
+        T* akk = a + lr_k + lc_k * lda;
+        T* apan = a + lr_k + lc_k1 * lda;     // my columns right of the diagonal, row k
+        const int64_t tDiag = Sched::tok(5, slot), tBc = Sched::bcast(slot);
+        if (in_row && mycol == qk)
+            S.task(1, {}, {Sched::col(k)}, [&, akk, kb, kk](lb::Ctx const& c) {
+                trace::Block tb("potrf_diag");
+                lb::potrf(c, Uplo::Upper, kb, akk, lda, dinfo.data(), kk);
+            });
+        T* Ukk = akk;
+        int64_t ldU = lda;
+        if (in_row && q > 1) {
+            T* D = Dk[slot].data();
+            S.task(1, {Sched::col(k)}, {tDiag}, [&, D, akk, kb, qk](lb::Ctx const& c) {
+                trace::Block tb("bcast_diag");
+                if (mycol == qk) pack(c, kb, kb, akk, lda, D);
+                bcast(g.row_fast(), D, size_t(kb * kb), qk, c);
+            });
+            Ukk = D; ldU = kb;
+        }
+        if (in_row && ncols > 0)
+            S.task(1, {tDiag}, {Sched::col(k)}, [&, Ukk, ldU, apan, ncols, kb](lb::Ctx const& c) {
+                trace::Block tb("potrf_trsm");
+                lb::trsm(c, Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, kb, ncols, T(1), Ukk, ldU, apan, lda);
+            });
+        if (k == nt - 1) break;
+        // row panel down the process columns; the tiles of my local rows over the row
+        T* Wk = (p > 1) ? W[slot].data() : apan;
+        const int64_t ldW = (p > 1) ? kb : lda;
+        std::vector<std::vector<int64_t>> lists(q);     // tiles I > k of my process ROW, by column owner
+        for (int64_t I = k + 1; I < nt; ++I)
+            if (A.srow_owner(I) == myrow) lists[A.scol_owner(I)].push_back(I);
+        T* Xk = (p * q > 1) ? X[slot].data() : nullptr;   // U(k, my rows > k) as kb x rows
+        S.task(1, {Sched::col(k)}, {tBc}, [&, Wk, ldW, apan, ncols, kb, pk, slot, lists, Xk, lr_k1](lb::Ctx const& c) {
+            trace::Block tb("bcast_panel");
+            if (p > 1) {
+                if (in_row) lb::copy2d(c, kb, ncols, apan, lda, Wk, ldW);
+                bcast(g.col_fast(), Wk, size_t(kb * ncols), pk, c);
+            }
+            if (Xk) {
+                if (q > 1) {
+                    // my column tiles J that row owner r needs: pack, all-gather over the row
+                    T* Sb = Ws[slot].data();
+                    int64_t cnt = 0;
+                    for (int64_t J = k + 1; J < nt; ++J) {
+                        if (A.scol_owner(J) != mycol || A.srow_owner(J) != myrow) continue;
+                        lb::copy2d(c, kb, A.tileNb(J), Wk + (lcol_of(A, J) - lc_k1) * ldW, ldW, Sb + cnt * nb * nb, kb);
+                        ++cnt;
+                    }
+                    g.row_fast().allgather(Sb, Wt[slot].data(), size_t(maxcnt * nb * nb), scalar_type<T>(), c.loc(),
+                                           c.stream);
+                    for (int cc = 0; cc < q; ++cc)
+                        for (size_t t = 0; t < lists[cc].size(); ++t) {
+                            const int64_t I = lists[cc][t];
+                            lb::copy2d(c, kb, A.tileMb(I), Wt[slot].data() + (int64_t(cc) * maxcnt + int64_t(t)) * nb * nb,
+                                       kb, Xk + (lrow_of(A, I) - lr_k1) * kb, kb);
+                        }
+                } else {
+                    // q == 1: my columns are every column; my rows' tiles sit in Wk
+                    for (int64_t I = k + 1; I < nt; ++I)
+                        if (A.srow_owner(I) == myrow)
+                            lb::copy2d(c, kb, A.tileMb(I), Wk + (lcol_of(A, I) - lc_k1) * ldW, ldW,
+                                       Xk + (lrow_of(A, I) - lr_k1) * kb, kb);
+                }
+            }
+        });
+        // trailing update of local column tiles [j0, j1): rows k+1 .. J (upper part)
+        auto update = [&, Wk, ldW, Xk, kb, lr_k1, lc_k1](lb::Ctx const& c, int64_t j0, int64_t j1) {
+            trace::Block tb("potrf_update");
+            if (p * q == 1) {
+                const int64_t c0 = lcol_of(A, j0), c1 = lcol_of(A, j1), r0 = lrow_of(A, j0);
+                const int64_t nc = c1 - c0, nabove = r0 - lr_k1;
+                T const* Wc = Wk + (c0 - lc_k1) * ldW;
+                lb::herk(c, Uplo::Upper, Op::ConjTrans, nc, kb, real_type<T>(-1), Wc, ldW, real_type<T>(1),
+                         a + r0 + c0 * lda, lda);
+                if (nabove > 0)
+                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, nabove, nc, kb, T(-1), Wk, ldW, Wc, ldW, T(1),
+                             a + lr_k1 + c0 * lda, lda);
+                return;
+            }
+            for (int64_t J = j0; J < j1; ++J) {
+                if (A.scol_owner(J) != mycol) continue;
+                const int64_t jb = A.tileNb(J), cJ = lcol_of(A, J);
+                T const* WJ = Wk + (cJ - lc_k1) * ldW;
+                // my rows in (k, J): above-diagonal; tile J itself if mine: upper triangle
+                const int64_t rJ = lrow_of(A, J), rJ1 = lrow_of(A, J + 1);
+                const bool diag_mine = A.srow_owner(J) == myrow;
+                const int64_t nabove = rJ - lr_k1;
+                if (nabove > 0)
+                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, nabove, jb, kb, T(-1), Xk, kb, WJ, ldW, T(1),
+                             a + lr_k1 + cJ * lda, lda);
+                if (diag_mine && rJ1 > rJ)
+                    lb::gemm_tri(c, Uplo::Upper, Op::ConjTrans, Op::NoTrans, jb, kb, T(-1), Xk + (rJ - lr_k1) * kb, kb,
+                                 WJ, ldW, T(1), a + rJ + cJ * lda, lda);
+            }
+        };
+        const int64_t jla_end = std::min(nt, k + 1 + la);
+        for (int64_t j = k + 1; j < jla_end; ++j)
+            S.task(device::kLookaheadQueue, {tBc}, {Sched::col(j)}, [&, update, j](lb::Ctx const& c) { update(c, j, j + 1); });
+        if (jla_end < nt) {
+            std::vector<int64_t> outs;
+            for (int64_t j = jla_end; j < nt; ++j) outs.push_back(Sched::col(j));
+            S.task(device::kTrailQueue, {tBc}, outs, [&, update, jla_end](lb::Ctx const& c) { update(c, jla_end, nt); });
+        }
+    }
+    S.wait_all();
+    int64_t info = fetch_info(target, dinfo.data());
+    return reduce_info(info, g.world());
+}
+
 }  // namespace
 
 template <typename T>
@@ -309,14 +470,7 @@ int64_t potrf(HermitianMatrix<T>& A_in, Options const& opts) {
     if (A_in.uplo_physical() == Uplo::Lower) {
         info = potrf_lower(A, target, la);
     } else {
-        // Upper: factor the conjugate transpose on the transposed grid
-        // (local transposes only), then transpose back.
-        Matrix<T> Ah = Matrix<T>(A).emptyLike(0, 0, Op::ConjTrans);
-        Ah.insertLocalTiles(target);
-        slate::copy<T, T>(conj_transpose(Matrix<T>(A)), Ah, opts);
-        info = potrf_lower(BaseMatrix<T>(Ah), target, la);
-        Matrix<T> Ad(A);
-        slate::copy<T, T>(conj_transpose(Ah), Ad, opts);
+        info = potrf_upper(A, target, la);   // in place, no transposed copy
     }
     internal::finish_origin(A, opts);
     return info;

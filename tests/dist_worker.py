@@ -500,6 +500,15 @@ def case_potrf(tg, dt, nb):
     info = s.posv(A, B, target=tg)
     assert info == 0
     assert relerr(a @ s.to_numpy(B), b) < 10 * tol(dt)
+    # Upper storage (in place, potrf_upper): U^H U = A, lookahead 1 and 2
+    for la in (1, 2):
+        A = s.HermitianMatrix(s.Uplo.Upper, s.from_numpy(a, nb=nb, target=tg))
+        assert s.potrf(A, target=tg, lookahead=la) == 0
+        U = np.triu(s.to_numpy(A))
+        assert relerr(U.conj().T @ U, a) < 10 * tol(dt), la
+        B = s.from_numpy(b, nb=nb, target=tg)
+        s.potrs(A, B, target=tg)
+        assert relerr(a @ s.to_numpy(B), b) < 10 * tol(dt), la
 
 
 def case_getrf(tg, dt, nb):
@@ -667,6 +676,13 @@ def case_solve_notemp(tg, dt, nb):
         s.trsm(s.Side.Right, 1.0, Lop, Bn, target=tg)
         assert not chk or s._slate.storage_alloc_max() < full / 4, ("trsm right", opname, s._slate.storage_alloc_max(), full)
         assert relerr(s.to_numpy(Bn) @ ref, bb) < 100 * tol(dt), ("trsm right", opname)
+    # potrf on Upper storage: in place (no conj-transposed n x n copies)
+    Hu = s.HermitianMatrix(s.Uplo.Upper, s.from_numpy(h, nb=nb, target=tg))
+    s._slate.storage_alloc_reset()
+    assert s.potrf(Hu, target=tg) == 0
+    assert not chk or s._slate.storage_alloc_max() < full / 4, ("potrf upper", s._slate.storage_alloc_max(), full)
+    Uu = np.triu(s.to_numpy(Hu))
+    assert relerr(Uu.conj().T @ Uu, h) < 100 * tol(dt), "potrf upper"
     # hemm Right on n x n B, C: in place, no (conj-)transposed copies
     H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(h, nb=nb, target=tg))
     bb, cc = rnd(n, n, dt, 145), rnd(n, n, dt, 146)
