@@ -1,0 +1,103 @@
+// Helpers of the CholeskyQR panel (qr.cc TsqrPanel, shifted CholeskyQR3 +
+// Householder reconstruction): the Gram-matrix shift of the first pass and
+// the orthogonality check of the last one.  One 256-thread workgroup: the
+// Gram matrix is nb x nb (<= 1024), the work is a trace and a max.
+#include "device_common.hh"
+#include "kernels.hh"
+
+namespace slate_amd {
+namespace dev {
+
+namespace {
+
+template <typename R>
+__device__ inline R block_sum(R v, R* sh) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (tid < s) sh[tid] += sh[tid + s];
+        __syncthreads();
+    }
+    R r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+template <typename R>
+__device__ inline R block_max(R v, R* sh) {
+    const int tid = threadIdx.x;
+    sh[tid] = v;
+    __syncthreads();
+    for (int s = blockDim.x / 2; s > 0; s >>= 1) {
+        if (tid < s) { R o = sh[tid + s]; sh[tid] = (o > sh[tid] || isnan(o)) ? o : sh[tid]; }
+        __syncthreads();
+    }
+    R r = sh[0];
+    __syncthreads();
+    return r;
+}
+
+template <typename T>
+__device__ inline real_t<T> re_of(T x) {
+    if constexpr (is_cplx<T>::value) return x.re; else return x;
+}
+
+/// G(i, i) += c * trace(G)   (real shift on the diagonal)
+template <typename T>
+__global__ __launch_bounds__(256) void cholqr_shift_kernel(T* G, int64_t ldg, int n, double c) {
+    using R = real_t<T>;
+    __shared__ R sh[256];
+    R t = 0;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) t += re_of(G[i + i * ldg]);
+    const R tr = block_sum(t, sh);
+    const R add = R(c) * tr;
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if constexpr (is_cplx<T>::value) G[i + i * ldg].re += add; else G[i + i * ldg] += add;
+    }
+}
+
+/// flag = 1 if the upper triangle of G is not within tol of I (or not finite)
+template <typename T>
+__global__ __launch_bounds__(256) void cholqr_check_kernel(const T* G, int64_t ldg, int n, double tol, int* flag) {
+    using R = real_t<T>;
+    __shared__ R sh[256];
+    R m = 0;
+    for (int64_t e = threadIdx.x; e < int64_t(n) * n; e += blockDim.x) {
+        const int i = int(e % n), j = int(e / n);
+        if (i > j) continue;
+        T g = G[i + j * ldg];
+        R d;
+        if constexpr (is_cplx<T>::value) d = fabs(g.re - (i == j ? R(1) : R(0))) + fabs(g.im);
+        else d = fabs(g - (i == j ? R(1) : R(0)));
+        if (!(d <= R(1e300))) d = R(INFINITY);   // NaN / Inf
+        m = d > m ? d : m;
+    }
+    const R mx = block_max(m, sh);
+    if (threadIdx.x == 0) *flag = (mx <= R(tol)) ? 0 : 1;
+}
+
+}  // namespace
+
+template <typename T>
+void cholqr_shift(T* G, int64_t ldg, int n, double c, hipStream_t s) {
+    if (n <= 0) return;
+    cholqr_shift_kernel<T><<<1, 256, 0, s>>>(G, ldg, n, c);
+}
+
+template <typename T>
+void cholqr_check(const T* G, int64_t ldg, int n, double tol, int* flag, hipStream_t s) {
+    cholqr_check_kernel<T><<<1, 256, 0, s>>>(G, ldg, n, tol, flag);
+}
+
+#define SLATE_INST_CHOLQR(T)                                                            \
+    template void cholqr_shift<T>(T*, int64_t, int, double, hipStream_t);              \
+    template void cholqr_check<T>(const T*, int64_t, int, double, int*, hipStream_t);
+
+SLATE_INST_CHOLQR(float)
+SLATE_INST_CHOLQR(double)
+SLATE_INST_CHOLQR(cplx<float>)
+SLATE_INST_CHOLQR(cplx<double>)
+
+}  // namespace dev
+}  // namespace slate_amd

@@ -45,6 +45,14 @@ template <typename T>
 void panel_xfer(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb, int64_t maxr, T* G, T* P, int64_t ldp,
                 T* ap, int64_t lda, int mode, hipStream_t s);
 
+// ---- CholeskyQR panel helpers (cholqr.hip)
+/// G(i,i) += c * trace(G) (the shifted first pass); flag = 1 unless the
+/// upper triangle of G is within tol of the identity (and finite).
+template <typename T>
+void cholqr_shift(T* G, int64_t ldg, int n, double c, hipStream_t s);
+template <typename T>
+void cholqr_check(const T* G, int64_t ldg, int n, double tol, int* flag, hipStream_t s);
+
 // ---- in-process communicator (comm.hip)
 /// out[i] = op_b in[i + b stride], b < nbuf; type 'f' 'd' 'i' (int32) 'l'
 /// (int64) 'b' (int8); op 0 sum, 1 max, 2 min.

@@ -52,11 +52,29 @@ inline int64_t qr_kchunk() {
 /// update one 2-D larfb instead of the reference's tree application (ttmqr).
 /// Used by geqrf (process-column tree) and gelqf (process-row tree on the
 /// conjugate-transposed row panel).
+///
+/// CholeskyQR panel (default on the device; SLATE_QR_CHOLQR=0 turns it off):
+/// the tree (a)-(d) costs ~27 ms per 32768 x 512 panel on a 2 x 4 grid,
+/// several times the per-step trailing update (profiles/r4_critpath_*).  The
+/// explicit Q and R come instead from shifted CholeskyQR3 (Fukaya, Kannan,
+/// Nakatsukasa, Yamamoto, Yanagisawa 2020: stable for cond(panel) up to
+/// ~1/u): three passes of  G = Q^H Q (local herk + ONE kb x kb all-reduce),
+/// R_i = chol(G) (the first with a diagonal shift 11 (M kb + kb(kb+1)) u
+/// tr(G)), Q := Q R_i^{-1}; R = R3 R2 R1.  The Householder reconstruction
+/// (e)-(g) then turns Q into the same (V, T, R) the tree would give.  The
+/// last Gram matrix measures Q's orthogonality before the final pass; if it
+/// is not within 0.5 of I (a rank-deficient or NaN panel) the column's
+/// processes -- which all hold the same all-reduced G -- fall back to the
+/// TSQR tree on the untouched panel.  That decision is the one host wait per
+/// panel step (the panel queue drains; the trailing queues keep running).
 template <typename T>
 struct TsqrPanel {
     static constexpr int maxr = 8;   // tree levels (comm size <= 256)
     int64_t nb;
-    Work<T> Tloc, Rcur, Rrecv, Ecur, Etmp, Qloc, LUb, Ytmp, Dg, Tw, sgn, taul;
+    Work<T> Tloc, Rcur, Rrecv, Ecur, Etmp, Qloc, LUb, Ytmp, Dg, Tw, sgn, taul, Gq;
+    Work<int> cq_flag;
+    int* cq_host = nullptr;
+    bool cholqr_on = false;
     std::vector<Work<T>> Sst, Ttt;
     const int64_t tSel = Sched::tok(30, 0);
 
@@ -69,12 +87,91 @@ struct TsqrPanel {
         Qloc.resize(target, size_t(std::max<int64_t>(max_rows, 1)) * nb);
         Sst.resize(maxr); Ttt.resize(maxr);
         for (int r = 0; r < maxr; ++r) { Sst[r].resize(target, 2 * nn); Ttt[r].resize(target, nn); }
+        static const bool env_on = [] {
+            const char* e = std::getenv("SLATE_QR_CHOLQR");
+            return e ? std::atoi(e) != 0 : true;
+        }();
+        cholqr_on = env_on;
+        if (cholqr_on) {
+            Gq.resize(target, nn);
+            cq_flag.resize(target, 2);
+            cq_host = target == Target::Devices ? static_cast<int*>(device::malloc_host(sizeof(int) * 2)) : cq_flag.data();
+            dev_ = target == Target::Devices;
+        }
+    }
+    ~TsqrPanel() { if (cq_host && dev_) device::free_host(cq_host); }
+    bool dev_ = false;
+    TsqrPanel(TsqrPanel const&) = delete;
+    TsqrPanel& operator=(TsqrPanel const&) = delete;
+
+    /// Shifted CholeskyQR3 of the distributed panel into Qloc (mr x kb) and
+    /// Rcur (kb x kb, upper); every process of the column calls it.  Returns
+    /// whether Q passed the orthogonality test (same answer on every process).
+    bool cholqr(Sched& S, int qP, Comm& cm, T* ap, int64_t lda, int64_t mr, int64_t kb, int64_t M, int64_t tPan) {
+        using R = real_type<T>;
+        const double u = double(std::numeric_limits<R>::epsilon()) / 2;
+        const double shift = 11.0 * (double(M) * double(kb) + double(kb) * double(kb + 1)) * u;
+        S.task(qP, {tPan}, {tSel}, [&, ap, mr, kb, shift](lb::Ctx const& c) {
+            trace::Block t2("geqrf_cholqr");
+            using DT = slate_amd::dev::dev_t<T>;
+            const int64_t ldq = std::max<int64_t>(mr, 1);
+            int* dflag = cq_flag.data();
+            lb::copy2d(c, mr, kb, ap, lda, Qloc.data(), ldq);
+            for (int pass = 0; pass < 3; ++pass) {
+                lb::herk(c, Uplo::Upper, Op::ConjTrans, kb, mr, R(1), Qloc.data(), ldq, R(0), Gq.data(), kb);
+                cm.allreduce(Gq.data(), size_t(kb * kb), ReduceOp::Sum, c.loc(), c.stream);
+                T* G = Gq.data();
+                if (c.dev()) {
+                    if (pass == 0) slate_amd::dev::cholqr_shift<DT>(slate_amd::dev::dptr(G), kb, int(kb), shift, c.stream);
+                    if (pass == 2) slate_amd::dev::cholqr_check<DT>(slate_amd::dev::dptr(G), kb, int(kb), 0.5, dflag, c.stream);
+                } else if (pass == 0) {
+                    R tr = 0;
+                    for (int64_t i = 0; i < kb; ++i) tr += std::real(G[i + i * kb]);
+                    for (int64_t i = 0; i < kb; ++i) G[i + i * kb] += T(R(shift) * tr);
+                } else if (pass == 2) {
+                    R mx = 0;
+                    for (int64_t j = 0; j < kb; ++j)
+                        for (int64_t i = 0; i <= j; ++i) {
+                            R d = std::abs(G[i + j * kb] - (i == j ? T(1) : T(0)));
+                            mx = (d > mx || std::isnan(d)) ? d : mx;
+                        }
+                    dflag[0] = (mx <= R(0.5)) ? 0 : 1;
+                }
+                lb::potrf(c, Uplo::Upper, kb, Gq.data(), kb, dflag + 1, 0);
+                lb::trsm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, mr, kb, T(1), Gq.data(), kb,
+                         Qloc.data(), ldq);
+                if (pass == 0) {
+                    lb::set(c, Uplo::General, kb, kb, T(0), T(0), Rcur.data(), kb);
+                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, kb, kb, Gq.data(), kb, Rcur.data(), kb);
+                } else {
+                    lb::trmm(c, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, kb, kb, T(1), Gq.data(), kb,
+                             Rcur.data(), kb);
+                }
+            }
+            if (c.dev()) device::memcpy_async(cq_host, dflag, sizeof(int), c.stream);
+        });
+        if (dev_) slate_hip_call(hipStreamSynchronize(S.ctx(qP).stream));
+        return cq_host[0] == 0;
     }
 
     /// rows_r[r]: panel rows of comm rank r; me: my comm rank; tPan: the
     /// panel's data token; tP: output token of (V, T).
     void enqueue(Sched& S, int qP, Comm& cm, int root, int me, std::vector<int64_t> const& rows_r, T* ap,
                  int64_t lda, int64_t mr, int64_t kb, int64_t kd, T* Tk, int64_t tPan, int64_t tP) {
+        int64_t Mtot = 0;
+        for (auto r : rows_r) Mtot += r;
+        if (cholqr_on && kd == kb && Mtot >= 2 * kb && cholqr(S, qP, cm, ap, lda, mr, kb, Mtot, tPan)) {
+            reconstruct(S, qP, cm, root, me, ap, lda, mr, kb, kd, Tk, tPan, tP);
+            return;
+        }
+        tree(S, qP, cm, root, me, rows_r, ap, lda, mr, kb, kd, tPan);
+        reconstruct(S, qP, cm, root, me, ap, lda, mr, kb, kd, Tk, tPan, tP);
+    }
+
+    /// (a)-(d): TSQR tree; leaves Qloc (explicit Q, my rows) and, at the
+    /// root, Rcur.
+    void tree(Sched& S, int qP, Comm& cm, int root, int me, std::vector<int64_t> const& rows_r, T* ap,
+              int64_t lda, int64_t mr, int64_t kb, int64_t kd, int64_t tPan) {
         const int p = int(rows_r.size());
         const int pk = root;
         const bool diag = (me == root);
@@ -187,6 +284,14 @@ struct TsqrPanel {
                 lb::larfb(c, Side::Left, Op::NoTrans, mr, kd, rr, ap, lda, Tloc.data(), nb, Qloc.data(), mr);
             });
         }
+    }
+
+    /// (e)-(g): Householder reconstruction of (V, T, R) from Qloc / Rcur.
+    void reconstruct(Sched& S, int qP, Comm& cm, int root, int me, T* ap, int64_t lda, int64_t mr, int64_t kb,
+                     int64_t kd, T* Tk, int64_t tPan, int64_t tP) {
+        const int pk = root;
+        const bool diag = (me == root);
+        Comm& colF = cm;
         // (e) pk: sign-modified LU of [S - Q11]  ->  Y1, U', S
         if (diag) {
             S.task(qP, {tSel}, {tSel}, [&, mr, kd](lb::Ctx const& c) {

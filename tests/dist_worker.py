@@ -818,6 +818,43 @@ def case_geqrf_shapes(tg, dt, nb):
             assert relerr(s.to_numpy(C), c) < 100 * tol(dt), ("QQh", m, n, la)
 
 
+def case_geqrf_cholqr(tg, dt, nb):
+    """p > 1 QR panels by shifted CholeskyQR3 + Householder reconstruction,
+    with the TSQR tree as the fallback when the last Gram matrix shows a
+    non-orthogonal Q: a well-conditioned matrix never falls back; a matrix
+    with an all-zero block column (rank-deficient panel) does, for that panel,
+    and both give a correct QR."""
+    g = parallel.current_grid()
+    m, n = 7 * nb + 5, 4 * nb
+    for case in ("full", "zero"):
+        a = rnd(m, n, dt, 61)
+        if case == "zero":
+            a[:, nb:2 * nb] = 0
+        A = s.from_numpy(a, nb=nb, target=tg)
+        s._slate.lane_log_enable(True)
+        T = s.geqrf(A, target=tg)
+        log = s._slate.lane_log_take()
+        s._slate.lane_log_enable(False)
+        labels = [label for label, _ in log]
+        if g.p > 1:
+            import torch
+            import torch.distributed as dist
+            # over all ranks: some process column ran CholeskyQR panels, and
+            # the TSQR tree ran only for the rank-deficient matrix
+            f = torch.tensor([int("geqrf_cholqr" in labels), int("geqrf_tsqr_local" in labels)])
+            dist.all_reduce(f)
+            assert f[0] > 0, labels
+            assert (f[1] == 0) if case == "full" else (f[1] > 0), (case, f)
+        r = np.triu(s.to_numpy(A)[:n])
+        rref = np.linalg.qr(a, mode="r")[:n]
+        assert relerr(np.abs(r), np.abs(rref)) < 100 * tol(dt), case
+        C = s.from_numpy(a, nb=nb, target=tg)
+        s.unmqr(s.Side.Left, s.Op.ConjTrans, A, T, C, target=tg)
+        qa = s.to_numpy(C)
+        assert relerr(np.triu(qa[:n]), r) < 100 * tol(dt), case
+        assert np.abs(qa[n:]).max() <= 100 * tol(dt) * np.abs(a).max() * m, case
+
+
 def case_norm(tg, dt, nb):
     a = rnd(170, 110, dt, 13)
     A = s.from_numpy(a, nb=nb, target=tg)
