@@ -118,6 +118,10 @@ template <typename T>
 int64_t getrf_nopiv(Matrix<T>& A, Options const& opts = {});
 template <typename T>
 int64_t getrf_tntpiv(Matrix<T>& A, Pivots& pivots, Options const& opts = {});
+/// Exact LU row-exchange counters of this process (diagnostics / tests):
+/// elements sent and rows sent (summed over column ranges) since the reset.
+void lu_rowx_stats(int64_t& elems, int64_t& rows);
+void lu_rowx_reset();
 template <typename T>
 void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts = {});
 template <typename T>

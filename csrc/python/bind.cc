@@ -351,6 +351,8 @@ PYBIND11_MODULE(_slate, m) {
         .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>());
     py::class_<SelfComm, Comm, std::shared_ptr<SelfComm>>(m, "SelfComm").def(py::init<>());
     py::class_<HostComm, PyHostComm, Comm, std::shared_ptr<HostComm>>(m, "HostComm").def(py::init<>());
+    m.def("lu_rowx_stats", []() { int64_t e = 0, r = 0; lu_rowx_stats(e, r); return py::make_tuple(e, r); });
+    m.def("lu_rowx_reset", &lu_rowx_reset);
     m.def("inproc_run_count", &inproc_run_count);
     m.def("inproc_last_shape", []() { int p = 0, q = 0; inproc_last_shape(p, q); return py::make_tuple(p, q); });
     m.def("comm_abort_all", &comm_abort_all, py::call_guard<py::gil_scoped_release>());

@@ -165,6 +165,131 @@ void permute_rows_dist(BaseMatrix<T> const& A, RowPairs const& P, int64_t c0, in
     for (int r = 0; r < p; ++r) { hpk(rcv.data() + ro, recv_dst[r].size(), rb + ro * ncols, true); ro += recv_dst[r].size(); }
 }
 
+/// Per-process counters of the exact row exchange (tests / diagnostics):
+/// elements this process sent, and the rows behind them (summed over ranges).
+struct RowXStats { int64_t elems = 0, rows = 0; };
+RowXStats& rowx_stats() { static RowXStats s; return s; }
+
+/// Exact row exchange of one LU step on a p > 1 grid.  The slot lists of the
+/// step (slot s < kd: U row s <- winner ssrc[s]; s >= kd: displaced row
+/// ssrc[s] -> sdst[s]) are on the host, so every message carries exactly the
+/// rows that change process: the winner rows I own go to every other process
+/// of the column (each needs the whole U block row for its U12 and GEMM), the
+/// displaced rows only to the owner of their destination.  The reference
+/// moves the remote pivot rows the same way (internal_swap.cc:511-805).
+/// with_u = false (the left columns): every slot is a plain row move.
+struct RowXPlan {
+    int p = 1;
+    std::vector<std::vector<int64_t>> sU, sD, rU, rD;   // per peer
+    std::vector<int64_t> lUsrc, lUslot, lDsrc, lDdst;   // my own rows
+    std::vector<int64_t> flat;                          // all lists, host
+    std::vector<size_t> o_sU, o_sD, o_rU, o_rD;
+    size_t o_lUsrc = 0, o_lUslot = 0, o_lDsrc = 0, o_lDdst = 0;
+    int64_t sends = 0, recvs = 0;                       // rows per column
+    size_t slab(int r) const { return sU[r].size() + sD[r].size(); }
+    size_t rslab(int r) const { return rU[r].size() + rD[r].size(); }
+};
+
+RowXPlan rowx_plan(slate_amd::dev::RowDist const& rd, int64_t kd, int64_t const* ssrc, int64_t const* sdst,
+                   bool with_u) {
+    namespace kdv = slate_amd::dev;
+    RowXPlan P;
+    const int p = rd.p, me = rd.myrow;
+    P.p = p;
+    P.sU.assign(p, {}); P.sD.assign(p, {}); P.rU.assign(p, {}); P.rD.assign(p, {});
+    for (int64_t s = 0; s < 2 * kd; ++s) {
+        const int64_t src = ssrc[s], dst = sdst[s];
+        if (src < 0 || dst < 0) continue;
+        const int os = kdv::rd_owner(rd, src), od = kdv::rd_owner(rd, dst);
+        if (with_u && s < kd) {
+            if (os == me) {
+                P.lUsrc.push_back(kdv::rd_lrow(rd, src));
+                P.lUslot.push_back(s);
+                for (int r = 0; r < p; ++r) if (r != me) P.sU[r].push_back(kdv::rd_lrow(rd, src));
+            } else {
+                P.rU[os].push_back(s);
+            }
+            continue;
+        }
+        if (src == dst) continue;
+        if (os == me && od == me) { P.lDsrc.push_back(kdv::rd_lrow(rd, src)); P.lDdst.push_back(kdv::rd_lrow(rd, dst)); }
+        else if (os == me) P.sD[od].push_back(kdv::rd_lrow(rd, src));
+        else if (od == me) P.rD[os].push_back(kdv::rd_lrow(rd, dst));
+    }
+    auto put = [&](std::vector<int64_t> const& v) { size_t o = P.flat.size(); P.flat.insert(P.flat.end(), v.begin(), v.end()); return o; };
+    for (int r = 0; r < p; ++r) {
+        P.o_sU.push_back(put(P.sU[r])); P.o_sD.push_back(put(P.sD[r]));
+        P.o_rU.push_back(put(P.rU[r])); P.o_rD.push_back(put(P.rD[r]));
+        P.sends += int64_t(P.slab(r));
+        P.recvs += int64_t(P.rslab(r));
+    }
+    P.o_lUsrc = put(P.lUsrc); P.o_lUslot = put(P.lUslot); P.o_lDsrc = put(P.lDsrc); P.o_lDdst = put(P.lDdst);
+    if (P.flat.empty()) P.flat.push_back(0);
+    return P;
+}
+
+/// Execute a plan on local columns [0, nc) of A (ld lda): pack, exchange over
+/// `cm`, unpack.  U rows land in buf (ld ldu, slot s at row s); idx: the
+/// plan's flat lists where the context can read them (device copy on the
+/// device); SB (>= sends x nc), RB (>= recvs x nc), TB (>= 2 kd x nc) scratch.
+template <typename T>
+void rowx_run(lb::Ctx const& c, RowXPlan const& P, int64_t const* idx, int64_t nc, T* A, int64_t lda, T* buf,
+              int64_t ldu, T* SB, T* RB, T* TB, Comm& cm, int phase) {
+    if (nc <= 0) return;
+    auto mv = [&](int64_t const* ix, size_t cnt, T* M, int64_t ldm, T* slab, bool scatter) {
+        if (cnt == 0) return;
+        if (c.dev()) {
+            using DT = slate_amd::dev::dev_t<T>;
+            slate_amd::dev::rows_pack<DT>(nc, slate_amd::dev::dptr(M), ldm, ix, int(cnt), slate_amd::dev::dptr(slab),
+                                          scatter, c.stream);
+            return;
+        }
+        for (int64_t j = 0; j < nc; ++j)
+            for (size_t t = 0; t < cnt; ++t) {
+                T& a = M[ix[t] + j * ldm];
+                T& b = slab[t + j * cnt];
+                if (scatter) a = b; else b = a;
+            }
+    };
+    const int p = P.p;
+    // phase 1: reads (every source row before any destination is written)
+    if (phase & 1) {
+        size_t off = 0;
+        for (int r = 0; r < p; ++r) {
+            mv(idx + P.o_sU[r], P.sU[r].size(), A, lda, SB + off * nc, false);
+            mv(idx + P.o_sD[r], P.sD[r].size(), A, lda, SB + (off + P.sU[r].size()) * nc, false);
+            off += P.slab(r);
+        }
+        mv(idx + P.o_lUsrc, P.lUsrc.size(), A, lda, TB, false);
+        mv(idx + P.o_lDsrc, P.lDsrc.size(), A, lda, TB + P.lUsrc.size() * nc, false);
+    }
+    // phase 2: the messages (one send / one receive per peer that has rows)
+    if (phase & 2) {
+        std::vector<Comm::P2P> ops;
+        size_t so = 0, ro = 0;
+        for (int r = 0; r < p; ++r) {
+            if (P.slab(r)) ops.push_back({SB + so * nc, P.slab(r) * nc, r, true});
+            if (P.rslab(r)) ops.push_back({RB + ro * nc, P.rslab(r) * nc, r, false});
+            so += P.slab(r);
+            ro += P.rslab(r);
+        }
+        if (!ops.empty()) cm.exchange(ops, scalar_type<T>(), c.loc(), c.stream);
+        rowx_stats().elems += int64_t(so) * nc;
+        rowx_stats().rows += int64_t(so);
+    }
+    // phase 4: writes
+    if (phase & 4) {
+        size_t ro = 0;
+        for (int r = 0; r < p; ++r) {
+            mv(idx + P.o_rU[r], P.rU[r].size(), buf, ldu, RB + ro * nc, true);
+            mv(idx + P.o_rD[r], P.rD[r].size(), A, lda, RB + (ro + P.rU[r].size()) * nc, true);
+            ro += P.rslab(r);
+        }
+        mv(idx + P.o_lUslot, P.lUslot.size(), buf, ldu, TB, true);
+        mv(idx + P.o_lDdst, P.lDdst.size(), A, lda, TB + P.lUsrc.size() * nc, true);
+    }
+}
+
 enum class PanelMode { Partial, Tournament, NoPiv };
 
 //------------------------------------------------------------------------------
@@ -264,6 +389,28 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
         PP.resize(target, size_t(std::max<int64_t>(m, 1)) * nb);
     }
     Work<int64_t> ipiv_all(target, size_t(std::max<int64_t>(kt, 1)) * nb);
+    // exact row exchange (default; SLATE_LU_EXACT_SWAP=0: the slot all-reduce):
+    // the step's pivot slots come to the host once per step (after the pivot
+    // broadcast) and every trailing / left row move is a point-to-point
+    // message of exactly the rows that change process (see RowXPlan)
+    static const bool exact_env = [] {
+        const char* e = std::getenv("SLATE_LU_EXACT_SWAP");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    const bool exact = pivot && exact_env;
+    std::vector<RowXPlan> RPl(R), LPl(R);
+    std::vector<Work<int64_t>> PX(R), PXL(R);
+    Work<T> XS, XR, XT, XLS, XLR, XLT;
+    int64_t* hpv = nullptr;
+    const size_t pxn = size_t(p + 4) * 2 * nb + 16;
+    if (exact) {
+        for (int r = 0; r < R; ++r) { PX[r].resize(target, pxn); PXL[r].resize(target, pxn); }
+        const size_t nl = size_t(std::max<int64_t>(nloc, 1));
+        XS.resize(target, size_t(p) * nb * nl); XR.resize(target, 2 * size_t(nb) * nl); XT.resize(target, 2 * size_t(nb) * nl);
+        XLS.resize(target, size_t(p) * nb * nl); XLR.resize(target, 2 * size_t(nb) * nl); XLT.resize(target, 2 * size_t(nb) * nl);
+        if (target == Target::Devices) hpv = static_cast<int64_t*>(device::malloc_host(6 * nb * sizeof(int64_t)));
+    }
+    struct HostFree { int64_t* p; ~HostFree() { if (p) device::free_host(p); } } hpv_free{hpv};
     Work<int> dinfo(target, 2);               // [info, dummy]
     {
         lb::Ctx c0 = S.ctx(qP);
@@ -281,6 +428,24 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
         int64_t nc = lcol_of(A, k2);
         if (nc <= 0) return;
         const int s2 = int(k2 % R);
+        if (exact) {
+            const int qL = device::kTrailQueue;
+            RowXPlan const* P = &LPl[s2];
+            int64_t const* ix = target == Target::Devices ? PXL[s2].data() : LPl[s2].flat.data();
+            S.task(qL, {Sched::tok(31, s2), Sched::col(k2 - 1)}, {tLeft}, [&, nc, P, ix](lb::Ctx const& c) {
+                trace::Block t2("getrf_left_pack");
+                rowx_run<T>(c, *P, ix, nc, a, lda, (T*)nullptr, 0, XLS.data(), XLR.data(), XLT.data(), g.col(), 1);
+            });
+            S.task(qC, {}, {tLeft}, [&, nc, P, ix](lb::Ctx const& c) {
+                trace::Block t2("getrf_left_swap");
+                rowx_run<T>(c, *P, ix, nc, a, lda, (T*)nullptr, 0, XLS.data(), XLR.data(), XLT.data(), g.col(), 2);
+            });
+            S.task(qL, {Sched::tok(31, s2)}, {tLeft, Sched::col(k2 - 1)}, [&, nc, P, ix](lb::Ctx const& c) {
+                trace::Block t2("getrf_left_unpack");
+                rowx_run<T>(c, *P, ix, nc, a, lda, (T*)nullptr, 0, XLS.data(), XLR.data(), XLT.data(), g.col(), 4);
+            });
+            return;
+        }
         const int64_t kd2 = std::min(A.tileNb(k2), m - grow_of(A, k2));
         int64_t* pv2 = PV[s2].data();
         // pack / unpack on a compute queue, only the all-reduce on the comm
@@ -476,6 +641,27 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
             }
             bcast(rowF, LUk, size_t(kd * kb), qk, c);
         });
+        if (exact) {
+            // the step's pivot slots on the host (one wait per step: the panel
+            // queue drains, the trailing queues keep running), then the exact
+            // exchange plans of the trailing ranges and of the left columns
+            int64_t const* hp = pv;
+            if (target == Target::Devices) {
+                device::memcpy_async(hpv, pv, 6 * nb * sizeof(int64_t), S.ctx(qP).stream);
+                slate_hip_call(hipStreamSynchronize(S.ctx(qP).stream));
+                hp = hpv;
+            }
+            RPl[slot] = rowx_plan(rd, kd, hp + 2 * nb, hp + 4 * nb, true);
+            LPl[slot] = rowx_plan(rd, kd, hp + 2 * nb, hp + 4 * nb, false);
+            if (target == Target::Devices)
+                S.task(qP, {}, {tPV}, [&, slot](lb::Ctx const& c) {
+                    slate_error_if_msg(RPl[slot].flat.size() > pxn || LPl[slot].flat.size() > pxn, "getrf: row plan size");
+                    device::memcpy_async(PX[slot].data(), RPl[slot].flat.data(), RPl[slot].flat.size() * sizeof(int64_t),
+                                         c.stream);
+                    device::memcpy_async(PXL[slot].data(), LPl[slot].flat.data(),
+                                         LPl[slot].flat.size() * sizeof(int64_t), c.stream);
+                });
+        }
         S.task(qP, {}, {tW}, [&, kb, qk, mr, Wk](lb::Ctx const& c) {
             trace::Block t2("getrf_bcast_L");
             bcast(rowF, Wk, size_t(mr * kb), qk, c);
@@ -495,6 +681,32 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
             // the column); lookahead columns on the critical-path lane
             const bool crit = (queue == device::kLookaheadQueue);
             Comm& cc_ = crit ? colF : g.col();
+            if (pivot && exact) {
+                RowXPlan const* P = &RPl[slot];
+                int64_t const* ix = target == Target::Devices ? PX[slot].data() : RPl[slot].flat.data();
+                T* sb = XS.data() + c0 * (p * nb);
+                T* rb = XR.data() + c0 * (2 * nb);
+                T* tb = XT.data() + c0 * (2 * nb);
+                if (crit) {
+                    S.task(qP, {tPV}, cols, [&, c0, nc, buf, P, ix, sb, rb, tb](lb::Ctx const& c) {
+                        trace::Block t2("getrf_rows_exchange");
+                        rowx_run<T>(c, *P, ix, nc, a + c0 * lda, lda, buf, ldu, sb, rb, tb, colF, 7);
+                    });
+                } else {
+                    S.task(queue, {tPV}, cols, [&, c0, nc, buf, P, ix, sb, rb, tb](lb::Ctx const& c) {
+                        trace::Block t2("getrf_rows_pack");
+                        rowx_run<T>(c, *P, ix, nc, a + c0 * lda, lda, buf, ldu, sb, rb, tb, g.col(), 1);
+                    });
+                    S.task(qC, {}, cols, [&, c0, nc, buf, P, ix, sb, rb, tb](lb::Ctx const& c) {
+                        trace::Block t2("getrf_rows_exchange");
+                        rowx_run<T>(c, *P, ix, nc, a + c0 * lda, lda, buf, ldu, sb, rb, tb, g.col(), 2);
+                    });
+                    S.task(queue, {tPV}, cols, [&, c0, nc, buf, P, ix, sb, rb, tb](lb::Ctx const& c) {
+                        trace::Block t2("getrf_rows_unpack");
+                        rowx_run<T>(c, *P, ix, nc, a + c0 * lda, lda, buf, ldu, sb, rb, tb, g.col(), 4);
+                    });
+                }
+            } else
             if (!crit && pivot) {
                 // bulk lane: slot pack / unpack on the range's compute queue,
                 // only the all-reduce on the comm queue (the cols tokens
@@ -918,6 +1130,11 @@ template void apply_pivots<std::complex<float>>(Pivots const&, BaseMatrix<std::c
 template void apply_pivots<std::complex<double>>(Pivots const&, BaseMatrix<std::complex<double>> const&, Matrix<std::complex<double>>&, Target, bool);
 
 }  // namespace internal
+
+/// Counters of the exact LU row exchange on this process (elements sent,
+/// rows sent summed over column ranges); reset with lu_rowx_reset().
+void lu_rowx_stats(int64_t& elems, int64_t& rows) { elems = rowx_stats().elems; rows = rowx_stats().rows; }
+void lu_rowx_reset() { rowx_stats() = RowXStats{}; }
 
 #define SLATE_GETRF_INST(T)                                                                  \
     template int64_t getrf<T>(Matrix<T>&, Pivots&, Options const&);                         \

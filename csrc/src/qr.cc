@@ -78,8 +78,8 @@ struct TsqrPanel {
     std::vector<Work<T>> Sst, Ttt;
     const int64_t tSel = Sched::tok(30, 0);
 
-    TsqrPanel(Target target, int np, int64_t nb_, int64_t max_rows) : nb(nb_) {
-        if (np <= 1) return;
+    TsqrPanel(Target target, int np, int64_t nb_, int64_t max_rows, bool single_cholqr = false) : nb(nb_) {
+        if (np <= 1 && !single_cholqr) return;
         const size_t nn = size_t(nb) * nb;
         Tloc.resize(target, nn); Rcur.resize(target, nn); Rrecv.resize(target, nn);
         Ecur.resize(target, 2 * nn); Etmp.resize(target, 2 * nn); LUb.resize(target, nn); Ytmp.resize(target, nn);
@@ -368,7 +368,14 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         WW2[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         Wtau[r].resize(target, size_t(nb));
     }
-    TsqrPanel<T> tsqr(target, p > 1 ? p : 1, nb, mloc);
+    // p == 1: the local panel by CholeskyQR3 + reconstruction as well
+    // (SLATE_QR_CHOLQR1=1; else the on-chip TSQR panel, lb::geqrf_panel)
+    static const bool cq1_env = [] {
+        const char* e = std::getenv("SLATE_QR_CHOLQR1");
+        return e && std::atoi(e) != 0;
+    }();
+    const bool cq1 = p == 1 && cq1_env && target == Target::Devices;
+    TsqrPanel<T> tsqr(target, p > 1 ? p : 1, nb, mloc, cq1);
     const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
 
     for (int64_t k = 0; k < kt; ++k) {
@@ -388,7 +395,10 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         const int64_t tP = Sched::tok(6, slot), tB = Sched::bcast(slot);
 
         // ================================================================ panel
-        if (in_col && p == 1) {
+        if (in_col && p == 1 && cq1 && kd == kb && M >= 2 * kb) {
+            std::vector<int64_t> rows_r{M};
+            tsqr.enqueue(S, qP, g.col(), 0, 0, rows_r, ap, lda, mr, kb, kd, Tk, Sched::col(k), tP);
+        } else if (in_col && p == 1) {
             S.task(qP, {}, {Sched::col(k), tP}, [&, kb, M, Tk, tau, ap](lb::Ctx const& c) {
                 trace::Block t2("geqrf_panel");
                 lb::geqrf_panel(c, M, kb, ap, lda, tau, Tk, kb);

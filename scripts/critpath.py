@@ -157,6 +157,35 @@ if "lu" in todo:
     report("getrf_tntpiv", rows)
 
 if "qr" in todo:
+    # CholeskyQR3 + Householder reconstruction panel (qr.cc TsqrPanel::cholqr)
+    rows = []
+    for k in steps:
+        mr, nc = rows_local(k), cols_local_trailing(k)
+        parts = {}
+        Q = rnd(mr, nb)
+        G = rnd(nb, nb)
+        one_pass = timed(lambda: ops.herk("U", "C", 1.0, Q, 0.0, G))
+        D = rnd(nb, nb)
+        D = (D @ D.T + nb * torch.eye(nb, dtype=torch.float64, device=dev)).contiguous()
+        one_pass += timed(lambda X: ops.potrf("U", X), lambda: (D.clone(),))
+        U = tri(nb)
+        one_pass += timed(lambda: ops.trsm("R", "U", "N", "N", 1.0, U, Q))
+        parts["cholqr3"] = 3 * one_pass
+        # reconstruction: sign-LU of the kb x kb top block + V = -Q21 U'^{-1}
+        parts["hr"] = timed(lambda X: ops.getrf_panel(X, tournament=False), lambda: (rnd(nb, nb),)) + \
+            timed(lambda: ops.trsm("R", "U", "N", "N", 1.0, U, Q))
+        parts["la_vhc"] = gemm_ms(nb, nb, mr, ta="T")
+        parts["la_apply"] = gemm_ms(nb, nb, nb) + gemm_ms(mr, nb, nb)
+        c = 0.0
+        if p > 1:
+            c += 3 * comm(nb * nb * 8) + comm(nb * nb * 8) + comm(nb * nb * 8)   # Gram all-reduces, LU + T, W
+        if q > 1:
+            c += comm(nb * nb * 8) + comm(mr * nb * 8)
+        upd = (gemm_ms(nb, nc, mr, ta="T") + gemm_ms(mr, nc, nb)) if nc > 0 else 0.0
+        chain = sum(parts.values()) + c
+        rows.append(dict(k=k, mr=mr, nc=nc, parts=parts, comm=c, chain=chain, update=upd))
+        del Q
+    report("geqrf (CholeskyQR3 + reconstruction panel)", rows)
     rows = []
     for k in steps:
         mr, nc = rows_local(k), cols_local_trailing(k)
@@ -183,7 +212,7 @@ if "qr" in todo:
         chain = sum(parts.values()) + c
         rows.append(dict(k=k, mr=mr, nc=nc, parts=parts, comm=c, chain=chain, update=upd))
         del W
-    report("geqrf", rows)
+    report("geqrf (TSQR tree panel, the fallback)", rows)
 
 if "chol" in todo:
     rows = []

@@ -818,6 +818,56 @@ def case_geqrf_shapes(tg, dt, nb):
             assert relerr(s.to_numpy(C), c) < 100 * tol(dt), ("QQh", m, n, la)
 
 
+def case_rowx_bytes(tg, dt, nb):
+    """Exact row exchange of the p x q LU (getrf.cc RowXPlan): the elements
+    each process sends in the trailing / left row moves equal, step by step,
+    the rows that change process times its local columns -- winner rows it
+    owns go to the p-1 other processes of its column (every process needs the
+    U block row), displaced rows only to their destination's owner, nothing
+    padded -- recomputed here from the returned pivots."""
+    g = parallel.current_grid()
+    p, q, myrow, mycol = g.p, g.q, g.myrow, g.mycol
+    m, n = 6 * nb + 9, 5 * nb + 3
+    a = rnd(m, n, dt, 171)
+    for fn in (s.getrf_tntpiv, s.getrf):
+        A = s.from_numpy(a, nb=nb, target=tg)
+        s._slate.lu_rowx_reset()
+        info, piv = fn(A, target=tg)
+        elems, rows = s._slate.lu_rowx_stats()
+        assert info == 0
+        if p == 1:
+            assert elems == 0
+            continue
+        owner = lambda r: (r // nb) % p
+        nt = (n + nb - 1) // nb
+        tile_w = [min(nb, n - j * nb) for j in range(nt)]
+        local_cols = lambda j0, j1: sum(tile_w[j] for j in range(j0, j1) if j % q == mycol)
+        expect = 0
+        exp_rows = 0
+        for k, pk in enumerate(piv):
+            kk, kd = k * nb, len(pk)
+            content = {}
+            get = lambda r: content.get(r, r)
+            for t, (ti, off) in enumerate(pk):
+                dst, src = kk + t, (k + ti) * nb + off
+                content[dst], content[src] = get(src), get(dst)
+            # trailing columns: U rows I own to every other process, my displaced rows
+            u_me = sum(1 for t in range(kd) if owner(get(kk + t)) == myrow)
+            d_me = sum(1 for dst, src in content.items()
+                       if not (kk <= dst < kk + kd) and src != dst and owner(src) == myrow and owner(dst) != myrow)
+            ncr = local_cols(k + 1, nt)
+            expect += (u_me * (p - 1) + d_me) * ncr
+            exp_rows += (u_me * (p - 1) + d_me) * (1 if ncr else 0)
+            # left columns: every move whose source is mine and destination is not
+            l_me = sum(1 for dst, src in content.items() if src != dst and owner(src) == myrow and owner(dst) != myrow)
+            expect += l_me * local_cols(0, k)
+        assert elems == expect, (fn.__name__, elems, expect)
+        # and strictly less than the zero-padded slot all-reduce it replaces
+        # (2 kd rows per column range, every process, every step)
+        padded = sum(2 * len(pk) * local_cols(k + 1, nt) for k, pk in enumerate(piv))
+        assert elems < padded or padded == 0, (elems, padded)
+
+
 def case_geqrf_cholqr(tg, dt, nb):
     """p > 1 QR panels by shifted CholeskyQR3 + Householder reconstruction,
     with the TSQR tree as the fallback when the last Gram matrix shows a
