@@ -57,7 +57,7 @@ __global__ __launch_bounds__(256) void cholqr_shift_kernel(T* G, int64_t ldg, in
     }
 }
 
-/// flag = 1 if the upper triangle of G is not within tol of I (or not finite)
+/// flag = 1 if the lower triangle of G is not within tol of I (or not finite)
 template <typename T>
 __global__ __launch_bounds__(256) void cholqr_check_kernel(const T* G, int64_t ldg, int n, double tol, int* flag) {
     using R = real_t<T>;
@@ -65,7 +65,7 @@ __global__ __launch_bounds__(256) void cholqr_check_kernel(const T* G, int64_t l
     R m = 0;
     for (int64_t e = threadIdx.x; e < int64_t(n) * n; e += blockDim.x) {
         const int i = int(e % n), j = int(e / n);
-        if (i > j) continue;
+        if (i < j) continue;
         T g = G[i + j * ldg];
         R d;
         if constexpr (is_cplx<T>::value) d = fabs(g.re - (i == j ? R(1) : R(0))) + fabs(g.im);

@@ -47,7 +47,7 @@ void panel_xfer(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb, int
 
 // ---- CholeskyQR panel helpers (cholqr.hip)
 /// G(i,i) += c * trace(G) (the shifted first pass); flag = 1 unless the
-/// upper triangle of G is within tol of the identity (and finite).
+/// lower triangle of G is within tol of the identity (and finite).
 template <typename T>
 void cholqr_shift(T* G, int64_t ldg, int n, double c, hipStream_t s);
 template <typename T>

@@ -348,7 +348,11 @@ PYBIND11_MODULE(_slate, m) {
         .def("rank", &Comm::rank)
         .def("size", &Comm::size)
         .def("name", &Comm::name)
-        .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>());
+        .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>())
+        .def("allreduce_sum_i64", [](Comm& c, std::vector<int64_t> v) {
+            if (!v.empty()) c.allreduce(v.data(), v.data(), v.size(), ScalarType::Int64, ReduceOp::Sum, Loc::Host, nullptr);
+            return v;
+        }, py::call_guard<py::gil_scoped_release>());
     py::class_<SelfComm, Comm, std::shared_ptr<SelfComm>>(m, "SelfComm").def(py::init<>());
     py::class_<HostComm, PyHostComm, Comm, std::shared_ptr<HostComm>>(m, "HostComm").def(py::init<>());
     m.def("lu_rowx_stats", []() { int64_t e = 0, r = 0; lu_rowx_stats(e, r); return py::make_tuple(e, r); });

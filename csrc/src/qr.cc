@@ -58,14 +58,16 @@ inline int64_t qr_kchunk() {
 /// several times the per-step trailing update (profiles/r4_critpath_*).  The
 /// explicit Q and R come instead from shifted CholeskyQR3 (Fukaya, Kannan,
 /// Nakatsukasa, Yamamoto, Yanagisawa 2020: stable for cond(panel) up to
-/// ~1/u): three passes of  G = Q^H Q (local herk + ONE kb x kb all-reduce),
-/// R_i = chol(G) (the first with a diagonal shift 11 (M kb + kb(kb+1)) u
-/// tr(G)), Q := Q R_i^{-1}; R = R3 R2 R1.  The Householder reconstruction
-/// (e)-(g) then turns Q into the same (V, T, R) the tree would give.  The
-/// last Gram matrix measures Q's orthogonality before the final pass; if it
-/// is not within 0.5 of I (a rank-deficient or NaN panel) the column's
-/// processes -- which all hold the same all-reduced G -- fall back to the
-/// TSQR tree on the untouched panel.  That decision is the one host wait per
+/// ~1/u), tried after plain CholeskyQR2 (two passes, stable for cond <~
+/// u^{-1/2}): passes of  G = Q^H Q (local herk + ONE kb x kb all-reduce),
+/// G = L L^H (the shifted variant's first pass adds 11 (M kb + kb(kb+1)) u
+/// tr(G) to the diagonal), Q := Q L^{-H}; R = product of the L^H.  The
+/// Householder reconstruction (e)-(g) then turns Q into the same (V, T, R)
+/// the tree would give.  The Gram matrix before the last pass measures Q's
+/// orthogonality; if it is not within 0.5 of I the column's processes --
+/// which all hold the same all-reduced G -- retry with the shifted variant,
+/// then fall back to the TSQR tree on the untouched panel (a rank-deficient
+/// or NaN panel).  That decision is the one host wait per
 /// panel step (the panel queue drains; the trailing queues keep running).
 template <typename T>
 struct TsqrPanel {
@@ -104,48 +106,53 @@ struct TsqrPanel {
     TsqrPanel(TsqrPanel const&) = delete;
     TsqrPanel& operator=(TsqrPanel const&) = delete;
 
-    /// Shifted CholeskyQR3 of the distributed panel into Qloc (mr x kb) and
-    /// Rcur (kb x kb, upper); every process of the column calls it.  Returns
-    /// whether Q passed the orthogonality test (same answer on every process).
-    bool cholqr(Sched& S, int qP, Comm& cm, T* ap, int64_t lda, int64_t mr, int64_t kb, int64_t M, int64_t tPan) {
+    /// CholeskyQR of the distributed panel into Qloc (mr x kb) and Rcur (kb x
+    /// kb, upper); every process of the column calls it.  shifted = false:
+    /// CholeskyQR2 (two passes, stable for cond <~ u^{-1/2}); true: shifted
+    /// CholeskyQR3.  The Gram matrix before the last pass is tested against
+    /// I; returns whether it passed (the same answer on every process).
+    /// Passes use the lower Cholesky factor: G = L L^H, Q := Q L^{-H}, R_i = L^H.
+    bool cholqr(Sched& S, int qP, Comm& cm, T* ap, int64_t lda, int64_t mr, int64_t kb, int64_t M, int64_t tPan,
+                bool shifted) {
         using R = real_type<T>;
         const double u = double(std::numeric_limits<R>::epsilon()) / 2;
         const double shift = 11.0 * (double(M) * double(kb) + double(kb) * double(kb + 1)) * u;
-        S.task(qP, {tPan}, {tSel}, [&, ap, mr, kb, shift](lb::Ctx const& c) {
+        const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+        S.task(qP, {tPan}, {tSel}, [&, ap, mr, kb, shift, shifted, cT](lb::Ctx const& c) {
             trace::Block t2("geqrf_cholqr");
             using DT = slate_amd::dev::dev_t<T>;
             const int64_t ldq = std::max<int64_t>(mr, 1);
             int* dflag = cq_flag.data();
+            const int npass = shifted ? 3 : 2;
             lb::copy2d(c, mr, kb, ap, lda, Qloc.data(), ldq);
-            for (int pass = 0; pass < 3; ++pass) {
-                lb::herk(c, Uplo::Upper, Op::ConjTrans, kb, mr, R(1), Qloc.data(), ldq, R(0), Gq.data(), kb);
-                cm.allreduce(Gq.data(), size_t(kb * kb), ReduceOp::Sum, c.loc(), c.stream);
+            for (int pass = 0; pass < npass; ++pass) {
                 T* G = Gq.data();
+                lb::herk(c, Uplo::Lower, Op::ConjTrans, kb, mr, R(1), Qloc.data(), ldq, R(0), G, kb);
+                cm.allreduce(G, size_t(kb * kb), ReduceOp::Sum, c.loc(), c.stream);
+                const bool sh = shifted && pass == 0, chk = pass == npass - 1;
                 if (c.dev()) {
-                    if (pass == 0) slate_amd::dev::cholqr_shift<DT>(slate_amd::dev::dptr(G), kb, int(kb), shift, c.stream);
-                    if (pass == 2) slate_amd::dev::cholqr_check<DT>(slate_amd::dev::dptr(G), kb, int(kb), 0.5, dflag, c.stream);
-                } else if (pass == 0) {
+                    if (sh) slate_amd::dev::cholqr_shift<DT>(slate_amd::dev::dptr(G), kb, int(kb), shift, c.stream);
+                    if (chk) slate_amd::dev::cholqr_check<DT>(slate_amd::dev::dptr(G), kb, int(kb), 0.5, dflag, c.stream);
+                } else if (sh) {
                     R tr = 0;
                     for (int64_t i = 0; i < kb; ++i) tr += std::real(G[i + i * kb]);
                     for (int64_t i = 0; i < kb; ++i) G[i + i * kb] += T(R(shift) * tr);
-                } else if (pass == 2) {
+                } else if (chk) {
                     R mx = 0;
                     for (int64_t j = 0; j < kb; ++j)
-                        for (int64_t i = 0; i <= j; ++i) {
+                        for (int64_t i = j; i < kb; ++i) {
                             R d = std::abs(G[i + j * kb] - (i == j ? T(1) : T(0)));
                             mx = (d > mx || std::isnan(d)) ? d : mx;
                         }
                     dflag[0] = (mx <= R(0.5)) ? 0 : 1;
                 }
-                lb::potrf(c, Uplo::Upper, kb, Gq.data(), kb, dflag + 1, 0);
-                lb::trsm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, mr, kb, T(1), Gq.data(), kb,
-                         Qloc.data(), ldq);
+                lb::potrf(c, Uplo::Lower, kb, G, kb, dflag + 1, 0);
+                lb::trsm(c, Side::Right, Uplo::Lower, cT, Diag::NonUnit, mr, kb, T(1), G, kb, Qloc.data(), ldq);
                 if (pass == 0) {
                     lb::set(c, Uplo::General, kb, kb, T(0), T(0), Rcur.data(), kb);
-                    lb::copy<T, T>(c, Uplo::Upper, Op::NoTrans, kb, kb, Gq.data(), kb, Rcur.data(), kb);
+                    lb::copy<T, T>(c, Uplo::Upper, cT, kb, kb, G, kb, Rcur.data(), kb);     // L^H
                 } else {
-                    lb::trmm(c, Side::Left, Uplo::Upper, Op::NoTrans, Diag::NonUnit, kb, kb, T(1), Gq.data(), kb,
-                             Rcur.data(), kb);
+                    lb::trmm(c, Side::Left, Uplo::Lower, cT, Diag::NonUnit, kb, kb, T(1), G, kb, Rcur.data(), kb);
                 }
             }
             if (c.dev()) device::memcpy_async(cq_host, dflag, sizeof(int), c.stream);
@@ -160,7 +167,11 @@ struct TsqrPanel {
                  int64_t lda, int64_t mr, int64_t kb, int64_t kd, T* Tk, int64_t tPan, int64_t tP) {
         int64_t Mtot = 0;
         for (auto r : rows_r) Mtot += r;
-        if (cholqr_on && kd == kb && Mtot >= 2 * kb && cholqr(S, qP, cm, ap, lda, mr, kb, Mtot, tPan)) {
+        // CholeskyQR2, else shifted CholeskyQR3 (from the untouched panel),
+        // else the TSQR tree (see above)
+        if (cholqr_on && kd == kb && Mtot >= 2 * kb &&
+            (cholqr(S, qP, cm, ap, lda, mr, kb, Mtot, tPan, false) ||
+             cholqr(S, qP, cm, ap, lda, mr, kb, Mtot, tPan, true))) {
             reconstruct(S, qP, cm, root, me, ap, lda, mr, kb, kd, Tk, tPan, tP);
             return;
         }
