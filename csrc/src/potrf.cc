@@ -345,7 +345,7 @@ int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
         T* apan = a + lr_k + lc_k1 * lda;     // my columns right of the diagonal, row k
         const int64_t tDiag = Sched::tok(5, slot), tBc = Sched::bcast(slot);
         if (in_row && mycol == qk)
-            S.task(1, {}, {Sched::col(k)}, [&, akk, kb, kk](lb::Ctx const& c) {
+            S.task(1, {}, {Sched::row(k)}, [&, akk, kb, kk](lb::Ctx const& c) {
                 trace::Block tb("potrf_diag");
                 lb::potrf(c, Uplo::Upper, kb, akk, lda, dinfo.data(), kk);
             });
@@ -353,7 +353,7 @@ int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
         int64_t ldU = lda;
         if (in_row && q > 1) {
             T* D = Dk[slot].data();
-            S.task(1, {Sched::col(k)}, {tDiag}, [&, D, akk, kb, qk](lb::Ctx const& c) {
+            S.task(1, {Sched::row(k)}, {tDiag}, [&, D, akk, kb, qk](lb::Ctx const& c) {
                 trace::Block tb("bcast_diag");
                 if (mycol == qk) pack(c, kb, kb, akk, lda, D);
                 bcast(g.row_fast(), D, size_t(kb * kb), qk, c);
@@ -361,7 +361,7 @@ int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
             Ukk = D; ldU = kb;
         }
         if (in_row && ncols > 0)
-            S.task(1, {tDiag}, {Sched::col(k)}, [&, Ukk, ldU, apan, ncols, kb](lb::Ctx const& c) {
+            S.task(1, {tDiag}, {Sched::row(k)}, [&, Ukk, ldU, apan, ncols, kb](lb::Ctx const& c) {
                 trace::Block tb("potrf_trsm");
                 lb::trsm(c, Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, kb, ncols, T(1), Ukk, ldU, apan, lda);
             });
@@ -373,7 +373,7 @@ int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
         for (int64_t I = k + 1; I < nt; ++I)
             if (A.srow_owner(I) == myrow) lists[A.scol_owner(I)].push_back(I);
         T* Xk = (p * q > 1) ? X[slot].data() : nullptr;   // U(k, my rows > k) as kb x rows
-        S.task(1, {Sched::col(k)}, {tBc}, [&, Wk, ldW, apan, ncols, kb, pk, slot, lists, Xk, lr_k1](lb::Ctx const& c) {
+        S.task(1, {Sched::row(k)}, {tBc}, [&, Wk, ldW, apan, ncols, kb, pk, slot, lists, Xk, lr_k1](lb::Ctx const& c) {
             trace::Block tb("bcast_panel");
             if (p > 1) {
                 if (in_row) lb::copy2d(c, kb, ncols, apan, lda, Wk, ldW);
@@ -406,43 +406,45 @@ int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
                 }
             }
         });
-        // trailing update of local column tiles [j0, j1): rows k+1 .. J (upper part)
-        auto update = [&, Wk, ldW, Xk, kb, lr_k1, lc_k1](lb::Ctx const& c, int64_t j0, int64_t j1) {
+        // trailing update by ROW tiles [i0, i1) (the mirror of the lower
+        // factor's column lookahead: step k+1's panel needs block ROW k+1
+        // across every column, so the rows k+1 .. k+la go first on the
+        // lookahead queue, the rest on the trailing queue): for each row tile
+        // I, C(I, J > I) -= U(k, I)^H U(k, J) and the upper triangle of C(I, I)
+        auto update = [&, Wk, ldW, Xk, kb, lr_k1, lc_k1](lb::Ctx const& c, int64_t i0, int64_t i1) {
             trace::Block tb("potrf_update");
             if (p * q == 1) {
-                const int64_t c0 = lcol_of(A, j0), c1 = lcol_of(A, j1), r0 = lrow_of(A, j0);
-                const int64_t nc = c1 - c0, nabove = r0 - lr_k1;
-                T const* Wc = Wk + (c0 - lc_k1) * ldW;
-                lb::herk(c, Uplo::Upper, Op::ConjTrans, nc, kb, real_type<T>(-1), Wc, ldW, real_type<T>(1),
-                         a + r0 + c0 * lda, lda);
-                if (nabove > 0)
-                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, nabove, nc, kb, T(-1), Wk, ldW, Wc, ldW, T(1),
-                             a + lr_k1 + c0 * lda, lda);
+                const int64_t r0 = lrow_of(A, i0), r1 = lrow_of(A, i1), nr = r1 - r0, nright = nloc - r1;
+                T const* Wr = Wk + (r0 - lc_k1) * ldW;
+                lb::herk(c, Uplo::Upper, Op::ConjTrans, nr, kb, real_type<T>(-1), Wr, ldW, real_type<T>(1),
+                         a + r0 + r0 * lda, lda);
+                if (nright > 0)
+                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, nr, nright, kb, T(-1), Wr, ldW, Wk + (r1 - lc_k1) * ldW,
+                             ldW, T(1), a + r0 + r1 * lda, lda);
                 return;
             }
-            for (int64_t J = j0; J < j1; ++J) {
-                if (A.scol_owner(J) != mycol) continue;
-                const int64_t jb = A.tileNb(J), cJ = lcol_of(A, J);
-                T const* WJ = Wk + (cJ - lc_k1) * ldW;
-                // my rows in (k, J): above-diagonal; tile J itself if mine: upper triangle
-                const int64_t rJ = lrow_of(A, J), rJ1 = lrow_of(A, J + 1);
-                const bool diag_mine = A.srow_owner(J) == myrow;
-                const int64_t nabove = rJ - lr_k1;
-                if (nabove > 0)
-                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, nabove, jb, kb, T(-1), Xk, kb, WJ, ldW, T(1),
-                             a + lr_k1 + cJ * lda, lda);
-                if (diag_mine && rJ1 > rJ)
-                    lb::gemm_tri(c, Uplo::Upper, Op::ConjTrans, Op::NoTrans, jb, kb, T(-1), Xk + (rJ - lr_k1) * kb, kb,
-                                 WJ, ldW, T(1), a + rJ + cJ * lda, lda);
+            for (int64_t I = i0; I < i1; ++I) {
+                if (A.srow_owner(I) != myrow) continue;
+                const int64_t ib = A.tileMb(I), rI = lrow_of(A, I);
+                T const* XI = Xk + (rI - lr_k1) * kb;
+                const int64_t cR = lcol_of(A, I + 1), nright = nloc - cR;
+                if (nright > 0)
+                    lb::gemm(c, Op::ConjTrans, Op::NoTrans, ib, nright, kb, T(-1), XI, kb, Wk + (cR - lc_k1) * ldW, ldW,
+                             T(1), a + rI + cR * lda, lda);
+                if (A.scol_owner(I) == mycol) {
+                    const int64_t cI = lcol_of(A, I);
+                    lb::gemm_tri(c, Uplo::Upper, Op::ConjTrans, Op::NoTrans, ib, kb, T(-1), XI, kb,
+                                 Wk + (cI - lc_k1) * ldW, ldW, T(1), a + rI + cI * lda, lda);
+                }
             }
         };
-        const int64_t jla_end = std::min(nt, k + 1 + la);
-        for (int64_t j = k + 1; j < jla_end; ++j)
-            S.task(device::kLookaheadQueue, {tBc}, {Sched::col(j)}, [&, update, j](lb::Ctx const& c) { update(c, j, j + 1); });
-        if (jla_end < nt) {
+        const int64_t ila_end = std::min(nt, k + 1 + la);
+        for (int64_t i = k + 1; i < ila_end; ++i)
+            S.task(device::kLookaheadQueue, {tBc}, {Sched::row(i)}, [&, update, i](lb::Ctx const& c) { update(c, i, i + 1); });
+        if (ila_end < nt) {
             std::vector<int64_t> outs;
-            for (int64_t j = jla_end; j < nt; ++j) outs.push_back(Sched::col(j));
-            S.task(device::kTrailQueue, {tBc}, outs, [&, update, jla_end](lb::Ctx const& c) { update(c, jla_end, nt); });
+            for (int64_t i = ila_end; i < nt; ++i) outs.push_back(Sched::row(i));
+            S.task(device::kTrailQueue, {tBc}, outs, [&, update, ila_end](lb::Ctx const& c) { update(c, ila_end, nt); });
         }
     }
     S.wait_all();
