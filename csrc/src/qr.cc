@@ -597,6 +597,94 @@ void unmqr_left(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Targe
     C.storage()->update_origin();
 }
 
+/// C = C op(Q) (Side::Right) in place: C on A's grid with C's column tiles =
+/// A's row tiles (C's columns are Q's rows).  Per block k (ascending for Q,
+/// descending for Q^H): V_k -- A's block column k, unit upper on the
+/// diagonal block, zero above -- is gathered whole (along the process rows
+/// from its owner, then all-gathered over the process column), each process
+/// takes the rows matching its local columns of C, W = C V_k is summed over
+/// the process row, and C -= (W op(T_k)) V_k^H: no (conj-)transposed copy of
+/// C (the reference applies ttmqr / unmqr tile by tile on C's columns).
+template <typename T>
+void unmqr_right(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Target target) {
+    auto& g = *A.grid();
+    const int p = g.p(), myrow = g.myrow(), mycol = g.mycol();
+    const Loc loc = loc_of(target);
+    const int64_t kt = std::min(A.mt(), A.nt());
+    LocalBlock<T> L = A.local(loc, false);
+    LocalBlock<T> LC = C.local(loc, true);
+    LocalBlock<T> LT = Tf.local(loc, false);
+    const int64_t nb = A.nb(), mC = LC.m, ncC = LC.n, ldw = std::max<int64_t>(mC, 1), ldv = std::max<int64_t>(ncC, 1);
+    const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+    std::vector<int64_t> rowoff(size_t(A.mt()), 0), cnt(p, 0);
+    for (int64_t i = 0; i < A.mt(); ++i) {
+        rowoff[i] = cnt[A.srow_owner(i)];
+        cnt[A.srow_owner(i)] += A.tileMb(i);
+    }
+    const int64_t maxr = std::max<int64_t>(1, *std::max_element(cnt.begin(), cnt.end()));
+    Sched S(target);
+    const int R = 3;
+    std::vector<Work<T>> WG(R), WV(R), WW(R), WW2(R);
+    Work<T> Gs(target, size_t(maxr) * nb);
+    for (int r = 0; r < R; ++r) {
+        WG[r].resize(target, size_t(p) * maxr * nb);
+        WV[r].resize(target, size_t(ldv) * nb);
+        WW[r].resize(target, size_t(ldw) * nb);
+        WW2[r].resize(target, size_t(ldw) * nb);
+    }
+    const int64_t tC = Sched::tok(9, 0);
+    for (int64_t t = 0; t < kt; ++t) {
+        const int64_t k = (op == Op::NoTrans) ? t : kt - 1 - t;
+        const int64_t kb = A.tileNb(k), kk = grow_of(A, k);
+        const int pk = A.srow_owner(k), qk = A.scol_owner(k);
+        const int slot = int(t % R);
+        T* G = WG[slot].data();
+        T* Vc = WV[slot].data();
+        T* W = WW[slot].data();
+        T* W2 = WW2[slot].data();
+        const int64_t tV = Sched::bcast(slot);
+        S.task(1, {}, {tV}, [&, k, kb, kk, pk, qk, G, Vc](lb::Ctx const& c) {
+            trace::Block t2("unmqr_bcast_v");
+            if (mycol == qk) {
+                // my rows of A(:, k): zero above row kk, unit upper diagonal block
+                const int64_t lr_k = lrow_of(A, k);
+                lb::set(c, Uplo::General, maxr, kb, T(0), T(0), Gs.data(), maxr);
+                lb::copy2d(c, L.m - lr_k, kb, L.ptr + lr_k + lcol_of(A, k) * L.ld, L.ld, Gs.data() + lr_k, maxr);
+                if (myrow == pk)
+                    lb::set(c, Uplo::Upper, std::min<int64_t>(kb, L.m - lr_k), kb, T(0), T(1), Gs.data() + lr_k, maxr);
+            }
+            bcast(g.row_fast(), Gs.data(), size_t(maxr * kb), qk, c);
+            g.col_fast().allgather(Gs.data(), G, size_t(maxr * kb), scalar_type<T>(), c.loc(), c.stream);
+            // the rows of V matching my local columns of C (V is zero above kk)
+            lb::set(c, Uplo::General, ncC, kb, T(0), T(0), Vc, ldv);
+            for (int64_t J = k; J < C.nt(); ++J) {
+                if (C.scol_owner(J) != mycol) continue;
+                lb::copy2d(c, C.tileNb(J), kb, G + size_t(A.srow_owner(J)) * maxr * kb + rowoff[J], maxr,
+                           Vc + lcol_of(C, J), ldv);
+            }
+            (void)kk;
+        });
+        T const* Tk = LT.ptr + kk * LT.ld;
+        S.task(0, {tV}, {tC}, [&, kb, Vc, W](lb::Ctx const& c) {
+            trace::Block t2("unmqr_w");
+            if (mC > 0) lb::gemm(c, Op::NoTrans, Op::NoTrans, mC, kb, ncC, T(1), LC.ptr, LC.ld, Vc, ldv, T(0), W, ldw);
+        });
+        S.task(device::kCommQueue, {}, {tC}, [&, kb, W](lb::Ctx const& c) {
+            trace::Block t2("unmqr_allreduce");
+            if (mC > 0) g.row().allreduce(W, W, size_t(ldw * kb), scalar_type<T>(), ReduceOp::Sum, c.loc(), c.stream);
+        });
+        S.task(0, {tV}, {tC}, [&, kb, Vc, W, W2, Tk](lb::Ctx const& c) {
+            trace::Block t2("unmqr_c");
+            if (mC <= 0) return;
+            lb::gemm(c, Op::NoTrans, op == Op::NoTrans ? Op::NoTrans : cT, mC, kb, kb, T(1), W, ldw, Tk, LT.ld, T(0), W2,
+                     ldw);
+            lb::gemm(c, Op::NoTrans, cT, mC, ncC, kb, T(-1), W2, ldw, Vc, ldv, T(1), LC.ptr, LC.ld);
+        });
+    }
+    S.wait_all();
+    C.storage()->update_origin();
+}
+
 }  // namespace
 
 template <typename T>
@@ -656,6 +744,20 @@ void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
             slate::copy<T, T>(Cx, C, opts);
         }
         return;
+    }
+    {
+        // in place when C is on A's grid with C's column tiles = A's row tiles
+        bool conform = C.op() == Op::NoTrans && C.aligned() && A.aligned() && C.grid()->same_processes(*A.grid())
+                    && C.grid()->p() == A.grid()->p() && C.grid()->q() == A.grid()->q()
+                    && C.grid()->order() == A.grid()->order() && C.nt() == A.mt();
+        if (conform)
+            for (int64_t j = 0; j < A.mt(); ++j)
+                if (A.tileMb(j) != C.tileNb(j)) { conform = false; break; }
+        if (conform) {
+            unmqr_right<T>(op == Op::NoTrans ? Op::NoTrans : Op::ConjTrans, A, T_[0], C, target);
+            internal::finish_origin(C, opts);
+            return;
+        }
     }
     // C op(Q) = (op(Q)^H C^H)^H
     Matrix<T> Ch = C.emptyLike(0, 0, Op::ConjTrans);

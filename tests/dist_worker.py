@@ -676,6 +676,19 @@ def case_solve_notemp(tg, dt, nb):
         s.trsm(s.Side.Right, 1.0, Lop, Bn, target=tg)
         assert not chk or s._slate.storage_alloc_max() < full / 4, ("trsm right", opname, s._slate.storage_alloc_max(), full)
         assert relerr(s.to_numpy(Bn) @ ref, bb) < 100 * tol(dt), ("trsm right", opname)
+    # unmqr Right (C Q, C Q^H) in place on C (C's columns = Q's rows)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    T = s.geqrf(A, target=tg)
+    Qe = s.from_numpy(np.eye(n, dtype=dt), nb=nb, target=tg)
+    s.unmqr(s.Side.Left, s.Op.NoTrans, A, T, Qe, target=tg)
+    Qm = s.to_numpy(Qe)
+    for opq, ref in ((s.Op.NoTrans, Qm), (s.Op.ConjTrans, Qm.conj().T)):
+        cc = rnd(n, n, dt, 147)
+        Cn = s.from_numpy(cc, nb=nb, target=tg)
+        s._slate.storage_alloc_reset()
+        s.unmqr(s.Side.Right, opq, A, T, Cn, target=tg)
+        assert not chk or s._slate.storage_alloc_max() < full / 4, ("unmqr right", opq, s._slate.storage_alloc_max(), full)
+        assert relerr(s.to_numpy(Cn), cc @ ref) < 100 * tol(dt), ("unmqr right", opq)
     # potrf on Upper storage: in place (no conj-transposed n x n copies)
     Hu = s.HermitianMatrix(s.Uplo.Upper, s.from_numpy(h, nb=nb, target=tg))
     s._slate.storage_alloc_reset()
