@@ -648,6 +648,7 @@ int64_t getrf_dist(BaseMatrix<T>& A, Pivots& pivots, Options const& opts, PanelM
             int64_t const* hp = pv;
             if (target == Target::Devices) {
                 device::memcpy_async(hpv, pv, 6 * nb * sizeof(int64_t), S.ctx(qP).stream);
+                // allowed host wait: the step's pivot slots (exact row exchange)
                 slate_hip_call(hipStreamSynchronize(S.ctx(qP).stream));
                 hp = hpv;
             }
