@@ -379,11 +379,13 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         WW2[r].resize(target, size_t(nb) * std::max<int64_t>(nloc, 1));
         Wtau[r].resize(target, size_t(nb));
     }
-    // p == 1: the local panel by CholeskyQR3 + reconstruction as well
-    // (SLATE_QR_CHOLQR1=1; else the on-chip TSQR panel, lb::geqrf_panel)
+    // p == 1 on the device: the local panel by CholeskyQR2 (shifted CholQR3,
+    // then the TSQR tree, as fallbacks) + reconstruction as well; measured
+    // dgeqrf n = 65536: 6715 -> 6626 ms (profiles/r4_ab_tail.txt).
+    // SLATE_QR_CHOLQR1=0 keeps the on-chip TSQR panel (lb::geqrf_panel).
     static const bool cq1_env = [] {
         const char* e = std::getenv("SLATE_QR_CHOLQR1");
-        return e && std::atoi(e) != 0;
+        return !e || std::atoi(e) != 0;
     }();
     const bool cq1 = p == 1 && cq1_env && target == Target::Devices;
     TsqrPanel<T> tsqr(target, p > 1 ? p : 1, nb, mloc, cq1);
