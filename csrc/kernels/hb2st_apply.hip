@@ -1,0 +1,210 @@
+// Stage-2 back-transform of the two-stage eigensolver / SVD on gfx950:
+// Z := Q2 Z for the bulge-chasing reflectors (reference src/unmtr_hb2st.cc,
+// which applies them as a wavefront of small vendor GEMMs per block).
+//
+// The reflectors come in groups of up to 64: the reflectors of 64 consecutive
+// sweeps at one bulge step, reflector i of a group acting on rows
+// r0 + i .. r0 + i + kd - 1 (kd <= 64).  A group is one block reflector
+// I - V T V^H with V a 128 x 64 parallelogram (column i nonzero in rows
+// i .. i + 63) and T upper triangular.  Columns of Z are independent under Q2,
+// so:
+//   hb2st_tfac   one wave per group: G = V^H V on the parallelogram, then the
+//                forward larft recurrence T(0:j, j) = -tau_j T(0:j, 0:j) G(0:j, j)
+//                (tau = 0 leaves a zero column: H_j = I).
+//   hb2st_apply  one workgroup per NC-column slice of Z walks every group of a
+//                chunk in order -- no inter-workgroup synchronisation at all:
+//                Zr = Z(r0 : r0 + 127, slice) into LDS, W = V^H Zr, W2 = T W,
+//                Z(r0 : r0 + 127, slice) -= V W2, each on v_mfma_f64_16x16x4
+//                with the zero triangles of the parallelogram skipped at 16 x 4
+//                granularity (about 1.25x the useful flops instead of the
+//                2.5x of dense (GS + kd) x GS blocks).  V stays compact in LDS
+//                (V(rho, i) = Vc(i, rho - i)), so one group moves 32 KB of V,
+//                32 KB of T and a 128 x NC window of Z.
+// Group order is the caller's: groups that share rows of Z must be applied in
+// the order of Q2's factors (eig.cc unmtr_hb2st_blocked), which a sequential
+// walk per slice preserves.
+#include "device_common.hh"
+#include "kernels.hh"
+
+namespace slate_amd {
+namespace dev {
+
+namespace {
+
+constexpr int HB = 64;          // reflectors per group (columns of V)
+constexpr int HR = 128;         // rows of a group's window
+constexpr int LDV = HB + 2;     // compact V in LDS: Vs[i * LDV + l]
+constexpr int LDT = HB;         // T in LDS, column-major: Ts[k * LDT + i]
+
+__device__ inline void mfma16(double a, double b, double (&c)[4]) {
+    typedef double v4d __attribute__((ext_vector_type(4)));
+    v4d acc = {c[0], c[1], c[2], c[3]};
+    acc = __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, acc, 0, 0, 0);
+    c[0] = acc[0]; c[1] = acc[1]; c[2] = acc[2]; c[3] = acc[3];
+}
+
+// one wave per group
+__global__ __launch_bounds__(64) void hb2st_tfac_kernel(const double* __restrict__ Vc, const double* __restrict__ tau,
+                                                        double* __restrict__ Tf) {
+    __shared__ double Vs[HB * LDV];
+    __shared__ double Gs[HB * (HB + 1)];   // G(a, j) at Gs[j * (HB + 1) + a]
+    __shared__ double Ts[HB * (HB + 1)];   // T(i, j) at Ts[j * (HB + 1) + i]
+    const int t = threadIdx.x;
+    const size_t g = blockIdx.x;
+    const double* V = Vc + g * HB * HB;
+    for (int i = 0; i < HB; ++i) Vs[i * LDV + t] = V[i * HB + t];
+    __syncthreads();
+    // thread j: G(a, j) = sum_l v_a[l + (j - a)] v_j[l] for a < j
+    const int j = t;
+    for (int a = 0; a < j; ++a) {
+        const int d = j - a;
+        double s = 0.0;
+        for (int l = 0; l + d < HB; ++l) s += Vs[a * LDV + l + d] * Vs[j * LDV + l];
+        Gs[j * (HB + 1) + a] = s;
+    }
+    for (int i = 0; i < HB; ++i) Ts[j * (HB + 1) + i] = 0.0;
+    __syncthreads();
+    // column k of T needs columns 0 .. k-1: one step per column, thread i < k
+    for (int k = 0; k < HB; ++k) {
+        const double tk = tau[g * HB + k];
+        if (t < k) {
+            double s = 0.0;
+            for (int m = t; m < k; ++m) s += Ts[m * (HB + 1) + t] * Gs[k * (HB + 1) + m];
+            Ts[k * (HB + 1) + t] = -tk * s;
+        } else if (t == k) {
+            Ts[k * (HB + 1) + k] = tk;
+        }
+        __syncthreads();
+    }
+    double* Tg = Tf + g * HB * HB;
+    for (int c = 0; c < HB; ++c) Tg[c * HB + t] = Ts[c * (HB + 1) + t];
+}
+
+template <int NC>
+__global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int64_t* __restrict__ R0,
+                                                          const double* __restrict__ Vc,
+                                                          const double* __restrict__ Tf, double* Z, int64_t ldz,
+                                                          int64_t n, int64_t ncols) {
+    constexpr int LDZ = HR + 1;   // Zs[c * LDZ + rho]
+    constexpr int LDW = HB + 1;   // Ws[c * LDW + i]
+    constexpr int NCB = NC / 16;
+    __shared__ double Vs[HB * LDV];
+    __shared__ double Ts[HB * LDT];
+    __shared__ double Zs[NC * LDZ];
+    __shared__ double Ws[NC * LDW];
+    __shared__ double W2s[NC * LDW];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int lo = lane & 15, hi = lane >> 4;
+    const int64_t c0 = int64_t(blockIdx.x) * NC;
+    // rho blocks of the update, paired so every wave gets 20 k-steps
+    const int rbA = (w == 0) ? 0 : (w == 1) ? 1 : (w == 2) ? 4 : 5;
+    const int rbB = (w == 0) ? 3 : (w == 1) ? 2 : (w == 2) ? 7 : 6;
+    for (int64_t g = 0; g < ng; ++g) {
+        const int64_t r0 = R0[g];
+        const double* V = Vc + g * HB * HB;
+        const double* Tg = Tf + g * HB * HB;
+        for (int e = tid; e < HB * HB; e += 256) {
+            const int i = e / HB, l = e % HB;
+            Vs[i * LDV + l] = V[e];
+            Ts[e] = Tg[e];          // column-major, LDT = HB
+        }
+        for (int e = tid; e < HR * NC; e += 256) {
+            const int rho = e % HR, c = e / HR;
+            const int64_t row = r0 + rho, col = c0 + c;
+            Zs[c * LDZ + rho] = (row < n && col < ncols) ? Z[row + col * ldz] : 0.0;
+        }
+        __syncthreads();
+        // W = V^H Zr: wave w owns rows i in [16 w, 16 w + 16); V(rho, i) is
+        // nonzero for rho in [i, i + 63] -> rho in [16 w, 16 w + 79)
+        {
+            double acc[NCB][4];
+            #pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) acc[cb][0] = acc[cb][1] = acc[cb][2] = acc[cb][3] = 0.0;
+            const int i = 16 * w + lo;
+            #pragma unroll 4
+            for (int s = 0; s < 20; ++s) {
+                const int rho = 16 * w + 4 * s + hi;
+                const int l = rho - i;
+                const double a = (l >= 0 && l < HB) ? Vs[i * LDV + l] : 0.0;
+                #pragma unroll
+                for (int cb = 0; cb < NCB; ++cb) mfma16(a, Zs[(16 * cb + lo) * LDZ + rho], acc[cb]);
+            }
+            #pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) Ws[(16 * cb + lo) * LDW + 16 * w + hi + 4 * q] = acc[cb][q];
+        }
+        __syncthreads();
+        // W2 = T W (T upper triangular): rows i of block w need k >= 16 w
+        {
+            double acc[NCB][4];
+            #pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) acc[cb][0] = acc[cb][1] = acc[cb][2] = acc[cb][3] = 0.0;
+            const int i = 16 * w + lo;
+            for (int k0 = 16 * w; k0 < HB; k0 += 4) {
+                const int k = k0 + hi;
+                const double a = Ts[k * LDT + i];
+                #pragma unroll
+                for (int cb = 0; cb < NCB; ++cb) mfma16(a, Ws[(16 * cb + lo) * LDW + k], acc[cb]);
+            }
+            #pragma unroll
+            for (int cb = 0; cb < NCB; ++cb)
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) W2s[(16 * cb + lo) * LDW + 16 * w + hi + 4 * q] = acc[cb][q];
+        }
+        __syncthreads();
+        // Zr -= V W2: rho block rb needs i in [16 rb - 63, 16 rb + 15]
+        #pragma unroll
+        for (int pass = 0; pass < 2; ++pass) {
+            const int rb = pass ? rbB : rbA;
+            const int ilo = max(0, 16 * rb - 64), ihi = min(HB, 16 * rb + 16);
+            double acc[NCB][4];
+            #pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) acc[cb][0] = acc[cb][1] = acc[cb][2] = acc[cb][3] = 0.0;
+            const int rho = 16 * rb + lo;
+            for (int i0 = ilo; i0 < ihi; i0 += 4) {
+                const int i = i0 + hi, l = rho - i;
+                const double a = (l >= 0 && l < HB) ? Vs[i * LDV + l] : 0.0;
+                #pragma unroll
+                for (int cb = 0; cb < NCB; ++cb) mfma16(a, W2s[(16 * cb + lo) * LDW + i], acc[cb]);
+            }
+            #pragma unroll
+            for (int cb = 0; cb < NCB; ++cb) {
+                const int c = 16 * cb + lo;
+                const int64_t col = c0 + c;
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int rr = 16 * rb + hi + 4 * q;
+                    const int64_t row = r0 + rr;
+                    if (row < n && col < ncols) Z[row + col * ldz] = Zs[c * LDZ + rr] - acc[cb][q];
+                }
+            }
+        }
+        // the next group reloads rows this one stored (workgroup-scope
+        // visibility: same CU) and overwrites the LDS images
+        __syncthreads();
+    }
+}
+
+}  // namespace
+
+void hb2st_tfac(int64_t ng, const double* Vc, const double* tau, double* Tf, hipStream_t s) {
+    if (ng <= 0) return;
+    hipLaunchKernelGGL(hb2st_tfac_kernel, dim3(unsigned(ng)), dim3(64), 0, s, Vc, tau, Tf);
+}
+
+void hb2st_apply(int64_t ng, const int64_t* R0, const double* Vc, const double* Tf, double* Z, int64_t ldz,
+                 int64_t n, int64_t ncols, hipStream_t s) {
+    if (ng <= 0 || ncols <= 0) return;
+    // 32-column slices while that still gives a workgroup per CU, else 16
+    if ((ncols + 31) / 32 >= 256) {
+        const unsigned nb = unsigned((ncols + 31) / 32);
+        hipLaunchKernelGGL(hb2st_apply_kernel<32>, dim3(nb), dim3(256), 0, s, ng, R0, Vc, Tf, Z, ldz, n, ncols);
+    } else {
+        const unsigned nb = unsigned((ncols + 15) / 16);
+        hipLaunchKernelGGL(hb2st_apply_kernel<16>, dim3(nb), dim3(256), 0, s, ng, R0, Vc, Tf, Z, ldz, n, ncols);
+    }
+}
+
+}  // namespace dev
+}  // namespace slate_amd

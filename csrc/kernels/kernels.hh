@@ -125,6 +125,15 @@ void merge_matrix(StedcMerge const& m, int64_t c_first, int64_t ncols, T* M, int
 
 // ---- eigensolver back-transform (eig.hip)
 /// G (k x k Gram V^H V) -> T^{-1} = striu(G) + diag(1 / tau) in place.
+/// Stage-2 back-transform (hb2st_apply.hip), fp64.  ng groups of 64
+/// reflectors: Vc[g] = 64 x 64 compact reflectors (column i: the entries of
+/// reflector i, rows R0[g] + i + l), tau[g] = 64 scalars.  hb2st_tfac writes
+/// each group's 64 x 64 upper triangular T (forward larft); hb2st_apply
+/// applies Z := (I - V T V^H) Z for g = 0 .. ng-1 in order to the n x ncols Z.
+void hb2st_tfac(int64_t ng, const double* Vc, const double* tau, double* Tf, hipStream_t s);
+void hb2st_apply(int64_t ng, const int64_t* R0, const double* Vc, const double* Tf, double* Z, int64_t ldz,
+                 int64_t n, int64_t ncols, hipStream_t s);
+
 template <typename T>
 void tinv_from_gram(int64_t k, T* G, int64_t ldg, const T* tau, hipStream_t s);
 /// sweeps per rot_sweeps call

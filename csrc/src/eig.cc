@@ -114,6 +114,31 @@ std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, int64_t M, bool lower
     return ab;
 }
 
+/// Broadcast a host vector from `root` (size first: the other ranks may not
+/// know it).
+template <typename X>
+void bcast_vec(Comm& w, std::vector<X>& v, int root) {
+    int64_t sz = int64_t(v.size());
+    w.bcast(&sz, 1, root, Loc::Host, nullptr);
+    v.resize(size_t(sz));
+    if (sz > 0) w.bcast(v.data(), size_t(sz), root, Loc::Host, nullptr);
+}
+
+/// Stage-2 results of one rank to all (reference heev.cc:128-140 / svd.cc run
+/// hb2st / tb2bd on one rank and broadcast): the bulge chase is a host
+/// pipeline that uses every core of the node, so running it once instead of
+/// on every rank of the node at the same time (each with its own thread
+/// team) stops the ranks from competing for the cores.
+template <typename T>
+void bcast_reflectors(Comm& w, host::Reflectors<T>& Q, int root) {
+    bcast_vec(w, Q.off, root);
+    bcast_vec(w, Q.len, root);
+    bcast_vec(w, Q.voff, root);
+    bcast_vec(w, Q.tag, root);
+    bcast_vec(w, Q.tau, root);
+    bcast_vec(w, Q.v, root);
+}
+
 }  // namespace
 
 //------------------------------------------------------------------------------
@@ -191,12 +216,96 @@ void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& o
 /// the GEMMs large (about 2 n^2 / (GS kd) blocks).  Z holds all n rows of its
 /// columns (1-D column layout).  Host and device run the same blocked
 /// sequence (lb:: dispatch), so the CPU tests check the ordering.
+/// fp64 on the device: the same product through the fused kernels of
+/// hb2st_apply.hip -- groups of 64 reflectors (64 consecutive sweeps at one
+/// bulge step, so V is a 128 x 64 parallelogram kept compact), T per group by
+/// one wave, and one workgroup per column slice of Z walking the groups in
+/// order (no per-group launches, no dense zero blocks).  Groups are packed on
+/// the host into pinned chunks that upload while the previous chunk applies.
+/// SLATE_HB2ST_FUSED=0 keeps the blocked GEMM sequence.
+void unmtr_hb2st_fused(host::Reflectors<double> const& Q, int64_t n, int64_t kd, double* Z, int64_t ldz,
+                       int64_t ncols, lb::Ctx const& c) {
+    trace::Block tb("unmtr_hb2st_fused");
+    constexpr int64_t HB = 64;
+    std::map<std::pair<int64_t, int64_t>, std::vector<size_t>> groups;
+    for (size_t r = 0; r < Q.size(); ++r) {
+        const int64_t j = Q.tag[r];
+        slate_assert(j >= 0);
+        groups[{j / HB, (Q.off[r] - j - 1) / kd}].push_back(r);
+    }
+    std::vector<std::pair<int64_t, int64_t>> keys;
+    for (auto& kv : groups) keys.push_back(kv.first);
+    std::sort(keys.begin(), keys.end(), [](auto const& a, auto const& b) {
+        return a.first != b.first ? a.first > b.first : a.second < b.second;
+    });
+    const int64_t ng = int64_t(keys.size()), CG = 512;
+    const size_t vsz = size_t(CG) * HB * HB, tsz = size_t(CG) * HB;
+    // one pinned staging block per buffer: V | tau | R0
+    const size_t bytes = (vsz + tsz) * sizeof(double) + size_t(CG) * sizeof(int64_t);
+    void* hbuf[2] = {device::malloc_host(bytes), device::malloc_host(bytes)};
+    void* dbuf[2] = {device::malloc(bytes), device::malloc(bytes)};
+    double* dT[2] = {static_cast<double*>(device::malloc(vsz * sizeof(double))),
+                     static_cast<double*>(device::malloc(vsz * sizeof(double)))};
+    hipEvent_t ev[2] = {device::event_get(), device::event_get()};
+    for (int b = 0; b < 2; ++b) slate_hip_call(hipEventRecord(ev[b], c.stream));
+    int cur = 0;
+    for (int64_t g0 = 0; g0 < ng; g0 += CG) {
+        const int64_t nc = std::min(CG, ng - g0);
+        slate_hip_call(hipEventSynchronize(ev[cur]));   // buffers of two chunks ago are free
+        double* hV = static_cast<double*>(hbuf[cur]);
+        double* htau = hV + vsz;
+        int64_t* hR0 = reinterpret_cast<int64_t*>(htau + tsz);
+        #pragma omp parallel for schedule(dynamic, 8)
+        for (int64_t bi = 0; bi < nc; ++bi) {
+            const auto key = keys[size_t(g0 + bi)];
+            const int64_t J = key.first, t = key.second, r0 = J * HB + t * kd + 1;
+            double* Vg = hV + size_t(bi) * HB * HB;
+            std::fill(Vg, Vg + HB * HB, 0.0);
+            std::fill(htau + bi * HB, htau + (bi + 1) * HB, 0.0);
+            hR0[bi] = r0;
+            for (size_t r : groups.at(key)) {
+                const int64_t i = Q.tag[r] - J * HB;
+                slate_assert(Q.off[r] - r0 == i && Q.len[r] <= HB);
+                std::copy(Q.v.data() + Q.voff[r], Q.v.data() + Q.voff[r] + Q.len[r], Vg + i * HB);
+                htau[bi * HB + i] = Q.tau[r];
+            }
+        }
+        double* dV = static_cast<double*>(dbuf[cur]);
+        double* dtau = dV + vsz;
+        int64_t* dR0 = reinterpret_cast<int64_t*>(dtau + tsz);
+        device::memcpy_async(dV, hV, size_t(nc) * HB * HB * sizeof(double), c.stream);
+        device::memcpy_async(dtau, htau, size_t(nc) * HB * sizeof(double), c.stream);
+        device::memcpy_async(dR0, hR0, size_t(nc) * sizeof(int64_t), c.stream);
+        slate_amd::dev::hb2st_tfac(nc, dV, dtau, dT[cur], c.stream);
+        slate_amd::dev::hb2st_apply(nc, dR0, dV, dT[cur], Z, ldz, n, ncols, c.stream);
+        slate_hip_call(hipEventRecord(ev[cur], c.stream));
+        cur ^= 1;
+    }
+    slate_hip_call(hipStreamSynchronize(c.stream));
+    for (int b = 0; b < 2; ++b) {
+        device::event_put(ev[b]);
+        device::free_host(hbuf[b]);
+        device::free(dbuf[b]);
+        device::free(dT[b]);
+    }
+}
+
 template <typename T>
 void unmtr_hb2st_blocked(host::Reflectors<T> const& Q, int64_t n, int64_t kd, T* Z, int64_t ldz, int64_t ncols,
                         lb::Ctx const& c) {
-    trace::Block tb("unmtr_hb2st_blocked");
     namespace kd_ = slate_amd::dev;
     if (Q.size() == 0 || ncols <= 0) return;
+    if constexpr (std::is_same<T, double>::value) {
+        static const bool fused = [] {
+            const char* e = std::getenv("SLATE_HB2ST_FUSED");
+            return !e || std::atoi(e) != 0;
+        }();
+        if (c.dev() && fused && kd <= 64) {
+            unmtr_hb2st_fused(Q, n, kd, Z, ldz, ncols, c);
+            return;
+        }
+    }
+    trace::Block tb("unmtr_hb2st_blocked");
     const int64_t GS = 4 * kd;
     std::map<std::pair<int64_t, int64_t>, std::vector<size_t>> groups;
     for (size_t r = 0; r < Q.size(); ++r) {
@@ -394,7 +503,14 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     std::vector<T> phase;
     {
         trace::Block t2("hb2st");
-        host::hb2st<T>(n, kd, B.data() + 2 * kd, 4 * kd, d, e, Q2, phase);
+        Comm& w = gA->world();
+        if (w.rank() == 0) host::hb2st<T>(n, kd, B.data() + 2 * kd, 4 * kd, d, e, Q2, phase);
+        if (w.size() > 1) {
+            bcast_vec(w, d, 0);
+            bcast_vec(w, e, 0);
+            bcast_vec(w, phase, 0);
+            if (wanted(Z)) bcast_reflectors(w, Q2, 0);
+        }
     }
     B.clear(); B.shrink_to_fit();
     if (!wanted(Z)) {
@@ -657,7 +773,16 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
     {
         std::vector<T> Bb = gather_band(W, kd, Mg, false, false, opts);
         trace::Block t2("tb2bd");
-        host::tb2bd<T>(n, n, kd, Bb.data() + Mg, 2 * Mg, d, e, QU2, QV2, pu, pv);
+        Comm& w = gA->world();
+        if (w.rank() == 0) host::tb2bd<T>(n, n, kd, Bb.data() + Mg, 2 * Mg, d, e, QU2, QV2, pu, pv);
+        if (w.size() > 1) {
+            bcast_vec(w, d, 0);
+            bcast_vec(w, e, 0);
+            bcast_vec(w, pu, 0);
+            bcast_vec(w, pv, 0);
+            if (wanted(U)) bcast_reflectors(w, QU2, 0);
+            if (wanted(VT)) bcast_reflectors(w, QV2, 0);
+        }
     }
     const bool wu = wanted(U), wv = wanted(VT);
     if (!wu && !wv) {

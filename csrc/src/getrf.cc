@@ -854,6 +854,30 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         if (c0.dev()) device::memset_async(dinfo.data(), 0, sizeof(int), c0.stream);
         else dinfo.data()[0] = 0;
     }
+    // left columns [0, k): apply the step's interchanges.  Off the trailing
+    // queue (the comm queue is idle on a p == 1 grid): nothing on the
+    // critical path reads these columns again, so the memory-bound swaps
+    // overlap the trailing GEMM instead of serializing before it
+    static const int left_q = [] {
+        const char* e = std::getenv("SLATE_LU_LEFT_TRAIL");   // A/B: 1 = back on the trailing queue
+        return (e && std::atoi(e)) ? device::kTrailQueue : device::kCommQueue;
+    }();
+    // 1x1 device grid, square: once the remaining matrix is at most `tail_w`
+    // wide, factor it with ONE recursive device panel (32-column tournament /
+    // partial-pivoting narrow blocks, trsm + GEMM recursion) instead of
+    // nb-wide steps whose panels are exposed once the trailing GEMM has shrunk
+    // (at nb = 2048 the last panels cost ~20 ms each beside < 1 ms of GEMM).
+    // SLATE_GETRF_TAIL = width (0: off); the left-column permutation of the
+    // tail is one LDS-staged pass, so the width is capped at 64 KB of rows.
+    static const int64_t tail_env = [] {
+        const char* e = std::getenv("SLATE_GETRF_TAIL");
+        return e ? std::atoll(e) : int64_t(0);
+    }();
+    const int64_t tail_w = std::min<int64_t>(tail_env, int64_t(65536 / sizeof(T)));
+    const bool tail_ok = q == 1 && target == Target::Devices && pivot && tail_w > 0 && m == A.n();
+    int64_t tail_k = kt;                     // first tile of the tail (kt: none)
+    Work<int64_t> tpv;                       // [ipiv(w) | dst(2w) | src(2w)]
+    if (tail_ok) tpv.resize(target, size_t(5 * tail_w + 8));
 
     for (int64_t k = 0; k < kt; ++k) {
         const int64_t kb = A.tileNb(k);
@@ -861,6 +885,28 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         const int64_t M = m - kk;                         // panel rows (global)
         const int64_t kd = std::min(kb, M);                // pivots this step
         const int qk = A.scol_owner(k);
+        if (tail_ok && k > 0 && M <= tail_w) {
+            tail_k = k;
+            std::vector<int64_t> cols;
+            for (int64_t j = k; j < nt; ++j) cols.push_back(Sched::col(j));
+            std::vector<int64_t> outs = cols;
+            const int64_t tT = Sched::tok(15, 0);
+            outs.push_back(tT);
+            int64_t* tp = tpv.data();
+            S.task(1, cols, outs, [&, k, kk, M, tp](lb::Ctx const& c) {
+                trace::Block t2("getrf_tail");
+                lb::getrf_panel(c, M, M, a + kk + kk * lda, lda, tp, perm.data(), dinfo.data(), kk, pivot, tnt,
+                                thresh);
+                // square: the first M pairs (t <- perm[t]) already cover every row
+                slate_amd::dev::perm_pairs(M, perm.data(), tp, tp + tail_w, tp + 3 * tail_w, c.stream);
+                lb::copy2d(c, M, int64_t(1), tp, M, ipiv_all.data() + k * nb, M);
+            });
+            S.task(left_q, {tT}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, kk, M, tp](lb::Ctx const& c) {
+                slate_amd::dev::permute_rows(kk, slate_amd::dev::dptr(a + kk), lda, tp + tail_w, tp + 3 * tail_w,
+                                             nullptr, int(M), c.stream);
+            });
+            break;
+        }
         const bool in_col = (mycol == qk);
         const int64_t lr_k = lrow_of(A, k), lr_k1 = lrow_of(A, k + 1);
         const int64_t lc_k = in_col ? lcol_of(A, k) : 0;
@@ -1016,14 +1062,6 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             range_tasks(device::kLookaheadQueue, j, j + 1);
         if (jla_end < nt) range_tasks(device::kTrailQueue, jla_end, nt);
 
-        // left columns [0, k): apply the step's interchanges.  Off the
-        // trailing queue (the comm queue is idle on a p == 1 grid): nothing
-        // on the critical path reads these columns again, so the memory-bound
-        // swaps overlap the trailing GEMM instead of serializing before it
-        static const int left_q = [] {
-            const char* e = std::getenv("SLATE_LU_LEFT_TRAIL");   // A/B: 1 = back on the trailing queue
-            return (e && std::atoi(e)) ? device::kTrailQueue : device::kCommQueue;
-        }();
         if (k > 0 && pivot) {
             // reads PV[pvs] (tPV): the panel that next rewrites the slot, RP
             // steps later, waits for it (write-after-read across queues)
@@ -1048,9 +1086,11 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     pivots.assign(kt, {});
     for (int64_t k = 0; k < kt; ++k) {
         int64_t kk = grow_of(A, k), kd = std::min(A.tileNb(k), m - kk);
+        // the tail's pivots are relative to its first row
+        const int64_t base = k >= tail_k ? grow_of(A, tail_k) : kk;
         pivots[k].resize(kd);
         for (int64_t t = 0; t < kd; ++t) {
-            int64_t r = pivot ? ip[k * nb + t] + kk : kk + t;
+            int64_t r = pivot ? ip[k * nb + t] + base : kk + t;
             // tile index relative to k and offset within the tile
             int64_t ti = 0;
             while (ti + k + 1 < mt && grow_of(A, k + ti + 1) <= r) ++ti;

@@ -22,3 +22,11 @@ for gi, g in enumerate(groups[-3:]):
     print(f"== group {gi}: {len(g)} kernels, span {span:.1f} us, busy {busy:.1f} us, gaps {span - busy:.1f} us")
     for k, v in sorted(agg.items(), key=lambda kv: -kv[1][1])[:14]:
         print(f"  {v[0]:5d} x {v[1]/v[0]:8.1f} us = {v[1]:9.1f} us  {k}")
+if "--list" in sys.argv and groups:
+    # the last repetition kernel by kernel: start offset, duration, gap before it
+    g = groups[-1]
+    print(f"\n== last group, in order (t0 = first kernel start)")
+    prev = g[0][1]
+    for r in g:
+        print(f"  {(r[1] - g[0][1]) / 1e3:9.1f} {(r[2] - r[1]) / 1e3:8.1f} gap {(r[1] - prev) / 1e3:6.1f}  {short(r[0])}")
+        prev = r[2]

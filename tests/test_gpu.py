@@ -509,6 +509,24 @@ def test_heev_device(dtype):
     assert np.linalg.norm(a @ z - z * w) / (np.linalg.norm(a) * n) < 1e-12
 
 
+@pytest.mark.parametrize("n,nb", [(2200, 48), (8192, 256)])
+def test_heev_device_stage2_fused(n, nb):
+    """Fused stage-2 back-transform (hb2st_apply.hip): several 512-group
+    chunks, kd < 64 (nb = 48) and the 32-column slices (n = 8192); residual
+    and orthogonality checked on the GPU."""
+    import torch
+    g = torch.Generator(device="cuda").manual_seed(7)
+    a = torch.rand(n, n, dtype=torch.float64, device="cuda", generator=g) * 2 - 1
+    a = (a + a.T) / 2
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a.cpu().numpy(), nb=nb, target="d"))
+    Z = s.from_numpy(np.zeros((n, n)), nb=nb, target="d")
+    w = torch.tensor(np.asarray(s.heev(A, Z, target="d")), device="cuda")
+    z = torch.tensor(s.to_numpy(Z), device="cuda")
+    an = torch.linalg.norm(a)
+    assert float(torch.linalg.norm(a @ z - z * w) / (an * n)) < 1e-13
+    assert float(torch.linalg.norm(z.T @ z - torch.eye(n, dtype=torch.float64, device="cuda")) / n) < 1e-13
+
+
 def test_svd_device():
     m, n, nb = 320, 200, 64
     a = rnd(m, n, np.float64, 32)
