@@ -99,20 +99,40 @@ __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int6
     // rho blocks of the update, paired so every wave gets 20 k-steps
     const int rbA = (w == 0) ? 0 : (w == 1) ? 1 : (w == 2) ? 4 : 5;
     const int rbB = (w == 0) ? 3 : (w == 1) ? 2 : (w == 2) ? 7 : 6;
-    for (int64_t g = 0; g < ng; ++g) {
-        const int64_t r0 = R0[g];
+    // V and T of the next group are prefetched into registers while the
+    // current one computes (all loads of a group in flight together: a load /
+    // LDS-store loop would pay one memory latency per iteration)
+    constexpr int NV = HB * HB / 256, NZ = HR * NC / 256;
+    double rv[NV], rt[NV];
+    auto fetch_vt = [&](int64_t g) {
         const double* V = Vc + g * HB * HB;
         const double* Tg = Tf + g * HB * HB;
-        for (int e = tid; e < HB * HB; e += 256) {
-            const int i = e / HB, l = e % HB;
-            Vs[i * LDV + l] = V[e];
-            Ts[e] = Tg[e];          // column-major, LDT = HB
-        }
-        for (int e = tid; e < HR * NC; e += 256) {
-            const int rho = e % HR, c = e / HR;
+        #pragma unroll
+        for (int it = 0; it < NV; ++it) { rv[it] = V[tid + 256 * it]; rt[it] = Tg[tid + 256 * it]; }
+    };
+    if (ng > 0) fetch_vt(0);
+    int64_t r0n = ng > 0 ? R0[0] : 0;
+    for (int64_t g = 0; g < ng; ++g) {
+        const int64_t r0 = r0n;
+        double rz[NZ];
+        #pragma unroll
+        for (int it = 0; it < NZ; ++it) {
+            const int e = tid + 256 * it, rho = e % HR, c = e / HR;
             const int64_t row = r0 + rho, col = c0 + c;
-            Zs[c * LDZ + rho] = (row < n && col < ncols) ? Z[row + col * ldz] : 0.0;
+            rz[it] = (row < n && col < ncols) ? Z[row + col * ldz] : 0.0;
         }
+        #pragma unroll
+        for (int it = 0; it < NV; ++it) {
+            const int e = tid + 256 * it, i = e / HB, l = e % HB;
+            Vs[i * LDV + l] = rv[it];
+            Ts[e] = rt[it];         // column-major, LDT = HB
+        }
+        #pragma unroll
+        for (int it = 0; it < NZ; ++it) {
+            const int e = tid + 256 * it, rho = e % HR, c = e / HR;
+            Zs[c * LDZ + rho] = rz[it];
+        }
+        if (g + 1 < ng) { fetch_vt(g + 1); r0n = R0[g + 1]; }
         __syncthreads();
         // W = V^H Zr: wave w owns rows i in [16 w, 16 w + 16); V(rho, i) is
         // nonzero for rho in [i, i + 63] -> rho in [16 w, 16 w + 79)
@@ -168,17 +188,24 @@ __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int6
                 #pragma unroll
                 for (int cb = 0; cb < NCB; ++cb) mfma16(a, W2s[(16 * cb + lo) * LDW + i], acc[cb]);
             }
+            // (each wave owns its rho blocks of Zs: update in place)
             #pragma unroll
             for (int cb = 0; cb < NCB; ++cb) {
                 const int c = 16 * cb + lo;
-                const int64_t col = c0 + c;
                 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int rr = 16 * rb + hi + 4 * q;
-                    const int64_t row = r0 + rr;
-                    if (row < n && col < ncols) Z[row + col * ldz] = Zs[c * LDZ + rr] - acc[cb][q];
+                    Zs[c * LDZ + rr] -= acc[cb][q];
                 }
             }
+        }
+        __syncthreads();
+        // coalesced store of the window (down the columns)
+        #pragma unroll
+        for (int it = 0; it < NZ; ++it) {
+            const int e = tid + 256 * it, rho = e % HR, c = e / HR;
+            const int64_t row = r0 + rho, col = c0 + c;
+            if (row < n && col < ncols) Z[row + col * ldz] = Zs[c * LDZ + rho];
         }
         // the next group reloads rows this one stored (workgroup-scope
         // visibility: same CU) and overwrites the LDS images

@@ -10,6 +10,7 @@
 #include <numeric>
 #include <atomic>
 #include <memory>
+#include <immintrin.h>
 #include <thread>
 #include <omp.h>
 
@@ -17,6 +18,16 @@ namespace slate {
 namespace host {
 
 namespace {
+
+// Wait for a pipelined sweep's progress counter: a short pause spin first
+// (the lag between sweeps is a few microseconds of work), sched_yield only
+// when the producer is really behind.
+inline void wait_progress(std::atomic<int64_t> const& p, int64_t want) {
+    for (int spin = 0; p.load(std::memory_order_acquire) < want; ++spin) {
+        if (spin < 256) _mm_pause();
+        else std::this_thread::yield();
+    }
+}
 
 template <typename T> inline T cj(T x) { return x; }
 template <typename R> inline std::complex<R> cj(std::complex<R> x) { return std::conj(x); }
@@ -85,37 +96,63 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
     using R = real_type<T>;
     auto a = [&](int64_t i, int64_t j) -> T& { return A[i + j * lda]; };
     const int64_t b = std::max<int64_t>(kd, 1);
-    // per-thread scratch: v (reflector), w (window-length dot products)
-    auto two_sided = [&](int64_t k, int64_t s0, int64_t L, T tau, const T* v, T* w) {
-        // H^H A H on the window [w0, w1] (column/row k set explicitly by the
-        // caller).  Rows J = [s0, s0+L) hold nonzeros in columns [k, s0+L-1+b]:
-        // k is the bulge column (earlier columns are already tridiagonal) and
-        // the band reaches b past the diagonal; by symmetry the same rows are
-        // touched by the right update.
-        int64_t w0 = k, w1 = std::min<int64_t>(n - 1, s0 + L - 1 + b);
-        // left: rows J, columns in window (skip k)
-        for (int64_t c = w0; c <= w1; ++c) {
-            if (c == k) continue;
-            T s = T(0);
-            for (int64_t i = 0; i < L; ++i) s += cj(v[i]) * a(s0 + i, c);
-            s *= cj(tau);
-            if (s != T(0)) for (int64_t i = 0; i < L; ++i) a(s0 + i, c) -= v[i] * s;
+    // per-thread scratch: v (reflector), w (dot products / the rank-2 vector)
+    // H^H A H with H = I - tau v v^H on rows / columns J = [s0, s0 + L),
+    // maintaining the LOWER triangle only (every later read -- the bulge
+    // column, the next windows, d / e -- is a lower entry), which halves the
+    // flops and the bytes of a step against updating both triangles:
+    //   (d) rows J, columns (k, s0): left update only;
+    //   (b) the J x J block: x = tau A_JJ v (lower hemv), w = x - conj(tau)/2
+    //       (v^H x) v, A_JJ -= v w^H + w v^H (lower part);
+    //   (c) rows (s0 + L - 1, s0 + L - 1 + b], columns J: right update only.
+    // The upper triangle of the window is left stale (never read again).
+    auto two_sided = [&](int64_t k, int64_t s0, int64_t L, T tau, const T* __restrict__ v, T* __restrict__ w) {
+        const T ctau = cj(tau);
+        // (d)
+        for (int64_t c = k + 1; c < s0; ++c) {
+            T* __restrict__ col = &a(s0, c);
+            T sum = T(0);
+            for (int64_t i = 0; i < L; ++i) sum += cj(v[i]) * col[i];
+            sum *= ctau;
+            for (int64_t i = 0; i < L; ++i) col[i] -= v[i] * sum;
         }
-        // right: rows in window (skip k), columns J; column-oriented so every
-        // inner loop runs down a contiguous column
-        const int64_t nr = w1 - w0 + 1;
-        std::fill(w, w + nr, T(0));
-        for (int64_t i = 0; i < L; ++i) {
-            const T* col = &a(w0, s0 + i);
-            const T vi = v[i];
-            for (int64_t r = 0; r < nr; ++r) w[r] += col[r] * vi;
+        // (b)
+        std::fill(w, w + L, T(0));
+        for (int64_t l = 0; l < L; ++l) {
+            const T* __restrict__ col = &a(s0, s0 + l);
+            const T vl = v[l];
+            T acc = T(std::real(col[l])) * vl;
+            for (int64_t i = l + 1; i < L; ++i) {
+                w[i] += col[i] * vl;
+                acc += cj(col[i]) * v[i];
+            }
+            w[l] += acc;
         }
-        for (int64_t i = 0; i < L; ++i) {
-            T* col = &a(w0, s0 + i);
-            const T f = tau * cj(v[i]);
-            const T keep = col[k - w0];  // row k is excluded
-            for (int64_t r = 0; r < nr; ++r) col[r] -= w[r] * f;
-            col[k - w0] = keep;
+        T vx = T(0);
+        for (int64_t i = 0; i < L; ++i) { w[i] *= tau; vx += cj(v[i]) * w[i]; }
+        const T alpha = T(-0.5) * ctau * vx;
+        for (int64_t i = 0; i < L; ++i) w[i] += alpha * v[i];
+        for (int64_t l = 0; l < L; ++l) {
+            T* __restrict__ col = &a(s0, s0 + l);
+            const T cwl = cj(w[l]), cvl = cj(v[l]);
+            for (int64_t i = l; i < L; ++i) col[i] -= v[i] * cwl + w[i] * cvl;
+            if constexpr (is_complex_v<T>) col[l] = T(std::real(col[l]));
+        }
+        // (c)
+        const int64_t r0 = s0 + L, r1 = std::min<int64_t>(n - 1, s0 + L - 1 + b);
+        const int64_t nr = r1 - r0 + 1;
+        if (nr <= 0) return;
+        T* __restrict__ wr = w + L;
+        std::fill(wr, wr + nr, T(0));
+        for (int64_t l = 0; l < L; ++l) {
+            const T* __restrict__ col = &a(r0, s0 + l);
+            const T vl = v[l];
+            for (int64_t r = 0; r < nr; ++r) wr[r] += col[r] * vl;
+        }
+        for (int64_t l = 0; l < L; ++l) {
+            T* __restrict__ col = &a(r0, s0 + l);
+            const T f = tau * cj(v[l]);
+            for (int64_t r = 0; r < nr; ++r) col[r] -= wr[r] * f;
         }
     };
     // Sweeps are pipelined over threads (the reference's hb2st.cc runs its
@@ -136,7 +173,7 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
         int64_t k = j, s0 = j + 1, s1 = std::min(j + b, n - 1);
         for (int64_t t = 0;; ++t) {
             if (j > 0) {
-                while (prog[j - 1].load(std::memory_order_acquire) < t + kLag) std::this_thread::yield();
+                wait_progress(prog[j - 1], t + kLag);
             }
             int64_t L = s1 - s0 + 1;
             if (L < 2) break;
@@ -146,8 +183,7 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
             larfg(L, alpha, v + 1, 1, tau);
             v[0] = T(1);
             a(s0, k) = alpha;
-            a(k, s0) = cj(alpha);
-            for (int64_t i = 1; i < L; ++i) { a(s0 + i, k) = T(0); a(k, s0 + i) = T(0); }
+            for (int64_t i = 1; i < L; ++i) a(s0 + i, k) = T(0);
             if (tau != T(0)) {
                 two_sided(k, s0, L, tau, v, w);
                 Qs[j].push(s0, L, tau, v, j);
@@ -235,12 +271,15 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         }
     };
     // Sweeps pipelined over threads as in hb2st: step t of sweep j touches
-    // rows/columns [c0 - b, c0 + 2b) with c0 = j + 1 + t b, so it may run once
-    // sweep j-1 has finished its steps 0..t+5 (a conservative lag); reflectors
-    // are kept per sweep and concatenated in sweep order (out-of-order ones
-    // commute).
+    // rows/columns [c0 - b, c0 + 2b) with c0 = j + 1 + t b (right update rows
+    // [c0 - b, c0 + L), left update columns up to c0 + L - 1 + b); sweep j-1's
+    // step t' sits at c0 - 1 + (t' - t) b, disjoint once t' >= t + 4, so step
+    // t may run once sweep j-1 has finished its steps 0..t+3 (the chain of
+    // lags bounds the whole reduction: lag 4 instead of 6 shortens it by a
+    // third).  Reflectors are kept per sweep and concatenated in sweep order
+    // (out-of-order ones commute).
     const int64_t nsw = n > 1 ? n - 1 : 0;
-    constexpr int64_t kLag = 6;
+    constexpr int64_t kLag = 4;
     constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
     std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
     for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
@@ -249,7 +288,7 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         int64_t r = j, c0 = j + 1, c1 = std::min(j + b, n - 1);
         for (int64_t st = 0;; ++st) {
             if (j > 0) {
-                while (prog[j - 1].load(std::memory_order_acquire) < st + kLag) std::this_thread::yield();
+                wait_progress(prog[j - 1], st + kLag);
             }
             // right reflector: row r, columns [c0, c1]
             int64_t L = c1 - c0 + 1;

@@ -387,7 +387,10 @@ void geqrf_impl(BaseMatrix<T> A, Matrix<T>& Tf, Target target, int64_t la) {
         const char* e = std::getenv("SLATE_QR_CHOLQR1");
         return !e || std::atoi(e) != 0;
     }();
-    const bool cq1 = p == 1 && cq1_env && target == Target::Devices;
+    // (large factorizations only: for the narrow, short panels of he2hb /
+    // ge2tb -- 64-wide tiles, m <= n of the eigenproblem -- the on-chip TSQR
+    // panel is faster: he2hb at n = 8192 took 466 ms in geqrf with CholQR)
+    const bool cq1 = p == 1 && cq1_env && target == Target::Devices && nb >= 256 && A.m() >= 16384;
     TsqrPanel<T> tsqr(target, p > 1 ? p : 1, nb, mloc, cq1);
     const Op cT = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
 

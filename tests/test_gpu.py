@@ -111,16 +111,17 @@ def test_gemm_nn_rank_nb_packed(k):
 
 @pytest.mark.parametrize("dtype", [np.float64, np.float32])
 @pytest.mark.parametrize("uplo", ["L", "U"])
-def test_herk_kernel(dtype, uplo):
+@pytest.mark.parametrize("n,k,op", [(333, 97, "N"), (300, 5000, "N"), (300, 5000, "C")])   # k = 5000: split-K triangular path
+def test_herk_kernel(dtype, uplo, n, k, op):
     torch = _torch()
-    n, k = 333, 97
-    a = rnd(n, k, dtype, 4)
+    a = rnd(n, k, dtype, 4) if op == "N" else rnd(k, n, dtype, 4)
     c = rnd(n, n, dtype, 5)
     tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
     tC = torch.from_numpy(np.ascontiguousarray(c.T)).cuda()
-    s.ops.herk(uplo, "N", -1.0, tA, 1.0, tC)
+    s.ops.herk(uplo, op, -1.0, tA, 1.0, tC)
     got = tC.cpu().numpy().T
-    ref = c - a.astype(np.float64) @ a.T
+    a64 = a.astype(np.float64)
+    ref = c - (a64 @ a64.T if op == "N" else a64.T @ a64)
     mask = np.tril(np.ones((n, n), bool)) if uplo == "L" else np.triu(np.ones((n, n), bool))
     assert relerr(got[mask], ref[mask]) < tol(dtype)
     np.testing.assert_array_equal(got[~mask], c[~mask])  # other triangle untouched
