@@ -22,6 +22,8 @@
 #include "device.hh"
 
 #include <functional>
+#include <map>
+#include <set>
 #include <memory>
 #include <tuple>
 
@@ -36,12 +38,16 @@ struct Tile {
     Op op = Op::NoTrans;
     Uplo uplo = Uplo::General;
     int device = HostNum;
+    /// memory layout of the stored mb x nb block: ColMajor (element (r, c)
+    /// at data[r + c stride]) or RowMajor (at data[c + r stride]); see
+    /// BaseMatrix::tileLayoutConvert
+    Layout layout = Layout::ColMajor;
     int64_t mb_() const { return op == Op::NoTrans ? mb : nb; }
     int64_t nb_() const { return op == Op::NoTrans ? nb : mb; }
     /// element (i, j) of the (op-applied) tile, host tiles only
     T at(int64_t i, int64_t j) const {
-        if (op == Op::NoTrans) return data[i + j * stride];
-        T v = data[j + i * stride];
+        const int64_t r = op == Op::NoTrans ? i : j, c = op == Op::NoTrans ? j : i;
+        T v = layout == Layout::ColMajor ? data[r + c * stride] : data[c + r * stride];
         return op == Op::ConjTrans ? slate::conj(v) : v;
     }
 };
@@ -109,6 +115,17 @@ public:
         return base + (lr - boff[lj]) + lc * ld;
     }
     ~MatrixStorage();
+    /// Remote tiles received with tileRecv / tileBcast (reference workspace
+    /// tiles, MatrixStorage.hh tileInsertWorkspace): contiguous mb x nb
+    /// buffers at `loc`, keyed by absolute storage tile (row, col).  Local
+    /// tiles whose layout was converted to RowMajor are listed in
+    /// tile_layouts.
+    struct WsTile { T* ptr = nullptr; int64_t mb = 0, nb = 0; Loc loc = Loc::Host; };
+    std::map<std::pair<int64_t, int64_t>, WsTile> ws_tiles;
+    std::map<std::pair<int64_t, int64_t>, slate::Layout> tile_layouts;
+    /// workspace tile (si, sj) of mb x nb at loc, allocated if missing
+    T* ws_tile(int64_t si, int64_t sj, int64_t mb, int64_t nb, Loc loc);
+    void ws_erase(int64_t si, int64_t sj);
     MatrixStorage(MatrixStorage const&) = delete;
     MatrixStorage& operator=(MatrixStorage const&) = delete;
 
@@ -236,8 +253,36 @@ public:
     int64_t lrow_end() const;
     int64_t lcol_begin() const;
     int64_t lcol_end() const;
-    /// View of logical tile (i, j); must be local.
+    /// View of logical tile (i, j): a local tile, or a remote one received
+    /// into workspace by tileRecv / tileBcast.
     Tile<T> tile(int64_t i, int64_t j, Loc loc) const;
+
+    // ---- tile-level communication and layout (reference BaseMatrix.hh
+    // tileSend / tileRecv / tileBcast / tileBcastToSet / tileLayoutConvert,
+    // Tile.hh send / recv / bcast / layoutConvert).  Messages go over the
+    // grid's world communicator (RCCL on the device, the native TCP mesh or
+    // the in-process transport on the host); a strided tile is packed into one
+    // contiguous message.  Point-to-point order is per peer, so `tag` is
+    // accepted for source compatibility and not needed.
+    /// local tile, or a received workspace tile
+    bool tileExists(int64_t i, int64_t j) const;
+    Layout tileLayout(int64_t i, int64_t j) const;
+    /// send tile (i, j) (local) to dst_rank, which calls tileRecv
+    void tileSend(int64_t i, int64_t j, int dst_rank, int tag = 0) const;
+    /// receive tile (i, j) from src_rank: in place when local, else into a
+    /// workspace tile; `layout` is the layout the tile is left in
+    void tileRecv(int64_t i, int64_t j, int src_rank, Layout layout = Layout::ColMajor, int tag = 0);
+    /// broadcast tile (i, j) from its owner to every rank owning a tile of B
+    /// (called by every rank of the grid; others return at once)
+    void tileBcast(int64_t i, int64_t j, BaseMatrix<T> const& B, Layout layout = Layout::ColMajor, int tag = 0);
+    /// broadcast to an explicit rank set (binomial tree rooted at the owner);
+    /// every rank of the set (and the owner) calls it
+    void tileBcastToSet(int64_t i, int64_t j, std::set<int> const& ranks, Layout layout = Layout::ColMajor);
+    /// convert tile (i, j) in place between column- and row-major: square
+    /// tiles anywhere, rectangular ones only as contiguous workspace tiles
+    void tileLayoutConvert(int64_t i, int64_t j, Layout layout);
+    /// drop a received workspace tile (local tiles are kept)
+    void tileErase(int64_t i, int64_t j);
     Tile<T> operator()(int64_t i, int64_t j) const { return tile(i, j, Loc::Host); }
 
     /// Element access (global logical indices), host instance, local only.
@@ -274,9 +319,17 @@ public:
     int64_t ku() const { return ku_; }
     void set_band(int64_t kl, int64_t ku) { kl_ = kl; ku_ = ku; }
 
+    /// (drop every local tile back to column-major: drivers read local
+    /// arrays as column-major)
+    void tileLayoutReset();
+
 protected:
     void to_storage(int64_t i, int64_t j, int64_t& si, int64_t& sj) const {
         if (op_ == Op::NoTrans) { si = i; sj = j; } else { si = j; sj = i; }
+    }
+    /// absolute storage tile of view storage tile (si, sj): workspace key
+    std::pair<int64_t, int64_t> skey(int64_t si, int64_t sj) const {
+        return storage_->general() ? std::make_pair(si, sj) : std::make_pair(stile_r(si), stile_c(sj));
     }
     // storage-orientation tile counts and sizes of this view
     int64_t stile_r0() const { return r0_ / storage_->mb; }

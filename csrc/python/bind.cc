@@ -196,6 +196,44 @@ void bind_type(py::module_& m, const char* sfx) {
         .def("tileNb", &BaseMatrix<T>::tileNb)
         .def("tileRank", &BaseMatrix<T>::tileRank)
         .def("tileIsLocal", &BaseMatrix<T>::tileIsLocal)
+        // tile-level communication / layout (tile_comm.cc)
+        .def("tileExists", &BaseMatrix<T>::tileExists)
+        .def("tileLayout", &BaseMatrix<T>::tileLayout)
+        .def("tileSend", &BaseMatrix<T>::tileSend, py::arg("i"), py::arg("j"), py::arg("dst_rank"), py::arg("tag") = 0)
+        .def("tileRecv", &BaseMatrix<T>::tileRecv, py::arg("i"), py::arg("j"), py::arg("src_rank"),
+             py::arg("layout") = Layout::ColMajor, py::arg("tag") = 0)
+        .def("tileBcast", &BaseMatrix<T>::tileBcast, py::arg("i"), py::arg("j"), py::arg("B"),
+             py::arg("layout") = Layout::ColMajor, py::arg("tag") = 0)
+        .def("tileBcastToSet", &BaseMatrix<T>::tileBcastToSet, py::arg("i"), py::arg("j"), py::arg("ranks"),
+             py::arg("layout") = Layout::ColMajor)
+        .def("tileLayoutConvert", &BaseMatrix<T>::tileLayoutConvert)
+        .def("tileLayoutReset", &BaseMatrix<T>::tileLayoutReset)
+        .def("tileErase", &BaseMatrix<T>::tileErase)
+        .def("tileData", [](BaseMatrix<T> const& A, int64_t i, int64_t j) {
+            // logical tile (i, j) as a numpy array (host copy; layout and op applied)
+            Loc loc = Loc::Host;
+            if (!A.tileIsLocal(i, j)) {
+                try { (void)A.tile(i, j, Loc::Host); } catch (...) { loc = Loc::Device; }
+            } else {
+                A.tileGetAllForReading(Loc::Host);
+            }
+            Tile<T> t = A.tile(i, j, loc);
+            std::vector<T> h;
+            if (loc == Loc::Device) {
+                const int64_t rows = t.layout == Layout::ColMajor ? t.mb : t.nb;
+                const int64_t cols = t.layout == Layout::ColMajor ? t.nb : t.mb;
+                h.resize(size_t(std::max<int64_t>(rows * cols, 1)));
+                slate_hip_call(hipMemcpy2D(h.data(), rows * sizeof(T), t.data, t.stride * sizeof(T), rows * sizeof(T),
+                                           cols, hipMemcpyDeviceToHost));
+                t.data = h.data();
+                t.stride = std::max<int64_t>(rows, 1);
+            }
+            py::array_t<T, py::array::f_style> out({t.mb_(), t.nb_()});
+            auto r = out.template mutable_unchecked<2>();
+            for (int64_t jj = 0; jj < t.nb_(); ++jj)
+                for (int64_t ii = 0; ii < t.mb_(); ++ii) r(ii, jj) = t.at(ii, jj);
+            return out;
+        })
         .def("mpiRank", &BaseMatrix<T>::mpiRank)
         .def("local_shape", [](BaseMatrix<T> const& A) {
             return py::make_tuple(A.lrow_end() - A.lrow_begin(), A.lcol_end() - A.lcol_begin());
@@ -339,6 +377,7 @@ PYBIND11_MODULE(_slate, m) {
     py::enum_<Side>(m, "Side").value("Left", Side::Left).value("Right", Side::Right);
     py::enum_<Norm>(m, "Norm").value("One", Norm::One).value("Two", Norm::Two).value("Inf", Norm::Inf)
         .value("Fro", Norm::Fro).value("Max", Norm::Max);
+    py::enum_<Layout>(m, "Layout").value("ColMajor", Layout::ColMajor).value("RowMajor", Layout::RowMajor);
     py::enum_<GridOrder>(m, "GridOrder").value("Col", GridOrder::Col).value("Row", GridOrder::Row);
     py::enum_<Equed>(m, "Equed").value("None_", Equed::None).value("Row", Equed::Row).value("Col", Equed::Col)
         .value("Both", Equed::Both);

@@ -103,6 +103,10 @@ MatrixStorage<T>::MatrixStorage(int64_t m_, int64_t n_, int64_t nb_, GridPtr g, 
 
 template <typename T>
 MatrixStorage<T>::~MatrixStorage() {
+    for (auto& kv : ws_tiles) {
+        if (kv.second.loc == Loc::Host) std::free(kv.second.ptr);
+        else { try { device::free(kv.second.ptr); } catch (...) {} }
+    }
     if (host_owned_ && host_) std::free(host_);
     if (dev_owned_ && dev_) {
         try { device::free(dev_); } catch (...) {}
@@ -290,8 +294,22 @@ LocalBlock<T> BaseMatrix<T>::local(Loc loc, bool for_write) const {
 
 template <typename T>
 Tile<T> BaseMatrix<T>::tile(int64_t i, int64_t j, Loc loc) const {
-    slate_error_if_msg(!tileIsLocal(i, j), "tile: not local");
     int64_t si, sj; to_storage(i, j, si, sj);
+    if (!tileIsLocal(i, j)) {
+        // a remote tile received into workspace (tile_comm.cc)
+        auto it = storage_->ws_tiles.find(skey(si, sj));
+        slate_error_if_msg(it == storage_->ws_tiles.end(), "tile: not local (and not received)");
+        auto const& w = it->second;
+        slate_error_if_msg(w.loc != loc, "tile: the received tile lives at the other location");
+        Tile<T> t;
+        t.data = w.ptr; t.mb = w.mb; t.nb = w.nb;
+        auto lt = storage_->tile_layouts.find(skey(si, sj));
+        t.layout = lt == storage_->tile_layouts.end() ? Layout::ColMajor : lt->second;
+        t.stride = std::max<int64_t>(1, t.layout == Layout::ColMajor ? w.mb : w.nb);
+        t.op = op_; t.uplo = uplo_physical();
+        t.device = loc == Loc::Host ? HostNum : 0;
+        return t;
+    }
     if (storage_->general()) {
         auto const& L = *storage_->layout;
         T* base = storage_->raw(loc);
@@ -301,6 +319,8 @@ Tile<T> BaseMatrix<T>::tile(int64_t i, int64_t j, Loc loc) const {
         t.data = base + L.toff[si + sj * L.mt];
         t.op = op_; t.uplo = uplo_physical();
         t.device = loc == Loc::Host ? HostNum : 0;
+        auto lt = storage_->tile_layouts.find(skey(si, sj));
+        if (lt != storage_->tile_layouts.end()) t.layout = lt->second;
         return t;
     }
     auto& g = *storage_->grid;
@@ -315,6 +335,10 @@ Tile<T> BaseMatrix<T>::tile(int64_t i, int64_t j, Loc loc) const {
     t.mb = srow_size(si); t.nb = scol_size(sj); t.stride = ld;
     t.op = op_; t.uplo = uplo_physical();
     t.device = loc == Loc::Host ? HostNum : 0;
+    if (!storage_->tile_layouts.empty()) {
+        auto lt = storage_->tile_layouts.find(skey(si, sj));
+        if (lt != storage_->tile_layouts.end()) t.layout = lt->second;
+    }
     return t;
 }
 

@@ -17,7 +17,7 @@ try:
 except Exception:  # torch is optional for the native library
     _torch = None
 from . import _slate
-from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Equed, Grid, Job,  # noqa: F401
+from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Layout, Equed, Grid, Job,  # noqa: F401
                     Matrix, HermitianMatrix, SymmetricMatrix, TriangularMatrix, TrapezoidMatrix,
                     BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general, band_matrix,
                     hermitian_band_matrix,

@@ -18,6 +18,7 @@ Diag = _slate.Diag
 Side = _slate.Side
 Norm = _slate.Norm
 GridOrder = _slate.GridOrder
+Layout = _slate.Layout
 Equed = _slate.Equed
 Grid = _slate.Grid
 

@@ -959,6 +959,62 @@ def case_mixed(tg, dt, nb):
     assert relerr(a @ s.to_numpy(X), b) < 1e-12
 
 
+def case_tile_comm(tg, dt, nb):
+    """Tile-level messages (tile_comm.cc; reference Tile::send / recv / bcast,
+    BaseMatrix::tileBcast / tileLayoutConvert): a tile sent point to point, a
+    tile broadcast to the owners of a block row (binomial tree over the rank
+    set), received into workspace and read back; row-major conversion of a
+    square local tile and of a rectangular received one, and the reset."""
+    g = parallel.current_grid()
+    me = parallel.world_rank()
+    world = g.p * g.q
+    m, n = 4 * nb + 5, 3 * nb + 7
+    a = rnd(m, n, dt, 181)
+    A = s.from_numpy(a, nb=nb, target=tg)
+    tiles = lambda i, j: a[i * nb:min(m, (i + 1) * nb), j * nb:min(n, (j + 1) * nb)]
+    # point to point: the last tile (rectangular edge tile) to every other rank in turn
+    i0, j0 = A.mt - 1, A.nt - 1
+    own = A.tileRank(i0, j0)
+    for dst in range(world):
+        if dst == own:
+            continue
+        if me == own:
+            A.tileSend(i0, j0, dst)
+        elif me == dst:
+            A.tileRecv(i0, j0, own)
+            assert A.tileExists(i0, j0)
+            np.testing.assert_array_equal(A.tileData(i0, j0), tiles(i0, j0))
+            # rectangular received tile to row-major and back
+            A.tileLayoutConvert(i0, j0, s.Layout.RowMajor)
+            assert A.tileLayout(i0, j0) == s.Layout.RowMajor
+            np.testing.assert_array_equal(A.tileData(i0, j0), tiles(i0, j0))
+            A.tileErase(i0, j0)
+            assert not A.tileExists(i0, j0)
+    # broadcast tile (1, 0) to the owners of block row 2
+    B = A.sub(2, 2, 0, A.nt - 1)
+    A.tileBcast(1, 0, B)
+    owners = {A.tileRank(2, j) for j in range(A.nt)} | {A.tileRank(1, 0)}
+    if me in owners:
+        assert A.tileExists(1, 0)
+        np.testing.assert_array_equal(A.tileData(1, 0), tiles(1, 0))
+    elif not A.tileIsLocal(1, 0):
+        assert not A.tileExists(1, 0)
+    # explicit set (every rank), received row-major
+    A.tileBcastToSet(0, 1, set(range(world)), s.Layout.RowMajor)
+    np.testing.assert_array_equal(A.tileData(0, 1), tiles(0, 1))
+    if not A.tileIsLocal(0, 1):
+        assert A.tileLayout(0, 1) == s.Layout.RowMajor
+    # square local tile: row-major in place, data unchanged as a matrix; the
+    # reset puts the local array back into column-major (drivers read it)
+    if A.tileIsLocal(0, 0):
+        A.tileLayoutConvert(0, 0, s.Layout.RowMajor)
+        assert A.tileLayout(0, 0) == s.Layout.RowMajor
+        np.testing.assert_array_equal(A.tileData(0, 0), tiles(0, 0))
+    A.tileLayoutReset()
+    assert A.tileLayout(0, 0) == s.Layout.ColMajor
+    np.testing.assert_array_equal(s.to_numpy(A), a)
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 EXTRA = {}
 
