@@ -26,6 +26,8 @@
 #include "device_common.hh"
 #include "kernels.hh"
 
+#include <cstdlib>
+
 namespace slate_amd {
 namespace dev {
 
@@ -84,7 +86,7 @@ template <int NC>
 __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int64_t* __restrict__ R0,
                                                           const double* __restrict__ Vc,
                                                           const double* __restrict__ Tf, double* Z, int64_t ldz,
-                                                          int64_t n, int64_t ncols) {
+                                                          int64_t n, int64_t ncols, bool slide) {
     constexpr int LDZ = HR + 1;   // Zs[c * LDZ + rho]
     constexpr int LDW = HB + 1;   // Ws[c * LDW + i]
     constexpr int NCB = NC / 16;
@@ -111,15 +113,39 @@ __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int6
         for (int it = 0; it < NV; ++it) { rv[it] = V[tid + 256 * it]; rt[it] = Tg[tid + 256 * it]; }
     };
     if (ng > 0) fetch_vt(0);
-    int64_t r0n = ng > 0 ? R0[0] : 0;
+    // Sliding window: consecutive groups of one sweep block J sit 64 rows
+    // apart when kd = 64, so the lower half of the window stays in LDS (the
+    // halves swap roles: physical row = logical row ^ (flip << 6)), the upper
+    // half of the next window is prefetched into registers while this group
+    // computes, and only the departing 64 rows are stored.
+    constexpr int NZH = NZ / 2;
+    double rz2[NZH];
+    int flip = 0;
+    bool slid = false;
+    int64_t r0 = ng > 0 ? R0[0] : 0;
+    int64_t r0n = ng > 1 ? R0[1] : 0;
     for (int64_t g = 0; g < ng; ++g) {
-        const int64_t r0 = r0n;
-        double rz[NZ];
-        #pragma unroll
-        for (int it = 0; it < NZ; ++it) {
-            const int e = tid + 256 * it, rho = e % HR, c = e / HR;
-            const int64_t row = r0 + rho, col = c0 + c;
-            rz[it] = (row < n && col < ncols) ? Z[row + col * ldz] : 0.0;
+        const bool slide_next = slide && g + 1 < ng && r0n == r0 + 64;
+        const int64_t r0nn = g + 2 < ng ? R0[g + 2] : 0;
+        if (!slid) {
+            double rz[NZ];
+            #pragma unroll
+            for (int it = 0; it < NZ; ++it) {
+                const int e = tid + 256 * it, rho = e % HR, c = e / HR;
+                const int64_t row = r0 + rho, col = c0 + c;
+                rz[it] = (row < n && col < ncols) ? Z[row + col * ldz] : 0.0;
+            }
+            #pragma unroll
+            for (int it = 0; it < NZ; ++it) {
+                const int e = tid + 256 * it, rho = e % HR, c = e / HR;
+                Zs[c * LDZ + (rho ^ (flip << 6))] = rz[it];
+            }
+        } else {
+            #pragma unroll
+            for (int it = 0; it < NZH; ++it) {
+                const int e = tid + 256 * it, rho = 64 + e % 64, c = e / 64;
+                Zs[c * LDZ + (rho ^ (flip << 6))] = rz2[it];
+            }
         }
         #pragma unroll
         for (int it = 0; it < NV; ++it) {
@@ -127,12 +153,16 @@ __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int6
             Vs[i * LDV + l] = rv[it];
             Ts[e] = rt[it];         // column-major, LDT = HB
         }
-        #pragma unroll
-        for (int it = 0; it < NZ; ++it) {
-            const int e = tid + 256 * it, rho = e % HR, c = e / HR;
-            Zs[c * LDZ + rho] = rz[it];
+        if (g + 1 < ng) fetch_vt(g + 1);
+        if (slide_next) {
+            // rows r0 + 128 .. r0 + 191: untouched by this group
+            #pragma unroll
+            for (int it = 0; it < NZH; ++it) {
+                const int e = tid + 256 * it, rr = e % 64, c = e / 64;
+                const int64_t row = r0 + 128 + rr, col = c0 + c;
+                rz2[it] = (row < n && col < ncols) ? Z[row + col * ldz] : 0.0;
+            }
         }
-        if (g + 1 < ng) { fetch_vt(g + 1); r0n = R0[g + 1]; }
         __syncthreads();
         // W = V^H Zr: wave w owns rows i in [16 w, 16 w + 16); V(rho, i) is
         // nonzero for rho in [i, i + 63] -> rho in [16 w, 16 w + 79)
@@ -147,7 +177,7 @@ __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int6
                 const int l = rho - i;
                 const double a = (l >= 0 && l < HB) ? Vs[i * LDV + l] : 0.0;
                 #pragma unroll
-                for (int cb = 0; cb < NCB; ++cb) mfma16(a, Zs[(16 * cb + lo) * LDZ + rho], acc[cb]);
+                for (int cb = 0; cb < NCB; ++cb) mfma16(a, Zs[(16 * cb + lo) * LDZ + (rho ^ (flip << 6))], acc[cb]);
             }
             #pragma unroll
             for (int cb = 0; cb < NCB; ++cb)
@@ -195,21 +225,35 @@ __global__ __launch_bounds__(256) void hb2st_apply_kernel(int64_t ng, const int6
                 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     const int rr = 16 * rb + hi + 4 * q;
-                    Zs[c * LDZ + rr] -= acc[cb][q];
+                    Zs[c * LDZ + (rr ^ (flip << 6))] -= acc[cb][q];
                 }
             }
         }
         __syncthreads();
-        // coalesced store of the window (down the columns)
-        #pragma unroll
-        for (int it = 0; it < NZ; ++it) {
-            const int e = tid + 256 * it, rho = e % HR, c = e / HR;
-            const int64_t row = r0 + rho, col = c0 + c;
-            if (row < n && col < ncols) Z[row + col * ldz] = Zs[c * LDZ + rho];
+        // coalesced store (down the columns): the whole window, or only its
+        // departing lower half when the next group slides
+        if (slide_next) {
+            #pragma unroll
+            for (int it = 0; it < NZH; ++it) {
+                const int e = tid + 256 * it, rho = e % 64, c = e / 64;
+                const int64_t row = r0 + rho, col = c0 + c;
+                if (row < n && col < ncols) Z[row + col * ldz] = Zs[c * LDZ + (rho ^ (flip << 6))];
+            }
+        } else {
+            #pragma unroll
+            for (int it = 0; it < NZ; ++it) {
+                const int e = tid + 256 * it, rho = e % HR, c = e / HR;
+                const int64_t row = r0 + rho, col = c0 + c;
+                if (row < n && col < ncols) Z[row + col * ldz] = Zs[c * LDZ + (rho ^ (flip << 6))];
+            }
         }
-        // the next group reloads rows this one stored (workgroup-scope
+        // the next group may reload rows this one stored (workgroup-scope
         // visibility: same CU) and overwrites the LDS images
         __syncthreads();
+        if (slide_next) flip ^= 1;
+        slid = slide_next;
+        r0 = r0n;
+        r0n = r0nn;
     }
 }
 
@@ -223,13 +267,14 @@ void hb2st_tfac(int64_t ng, const double* Vc, const double* tau, double* Tf, hip
 void hb2st_apply(int64_t ng, const int64_t* R0, const double* Vc, const double* Tf, double* Z, int64_t ldz,
                  int64_t n, int64_t ncols, hipStream_t s) {
     if (ng <= 0 || ncols <= 0) return;
+    static const bool slide = [] { const char* e = std::getenv("SLATE_HB2ST_SLIDE"); return !e || std::atoi(e) != 0; }();
     // 32-column slices while that still gives a workgroup per CU, else 16
     if ((ncols + 31) / 32 >= 256) {
         const unsigned nb = unsigned((ncols + 31) / 32);
-        hipLaunchKernelGGL(hb2st_apply_kernel<32>, dim3(nb), dim3(256), 0, s, ng, R0, Vc, Tf, Z, ldz, n, ncols);
+        hipLaunchKernelGGL(hb2st_apply_kernel<32>, dim3(nb), dim3(256), 0, s, ng, R0, Vc, Tf, Z, ldz, n, ncols, slide);
     } else {
         const unsigned nb = unsigned((ncols + 15) / 16);
-        hipLaunchKernelGGL(hb2st_apply_kernel<16>, dim3(nb), dim3(256), 0, s, ng, R0, Vc, Tf, Z, ldz, n, ncols);
+        hipLaunchKernelGGL(hb2st_apply_kernel<16>, dim3(nb), dim3(256), 0, s, ng, R0, Vc, Tf, Z, ldz, n, ncols, slide);
     }
 }
 

@@ -123,7 +123,12 @@ struct RowRotSink : host::RotSink<real_type<T>> {
         namespace kd_ = slate_amd::dev;
         R* Du = hb[cur];
         R* Dv = hb[cur] + tsz;
-        auto ru = build(bu, Du), rv = build(bv, Dv);
+        std::pair<int64_t, int64_t> ru, rv;
+        {
+            trace::Block tb("bdsqr_rot_tables");
+            ru = build(bu, Du);
+            rv = build(bv, Dv);
+        }
         const size_t su = size_t(std::max<int64_t>(ru.second - ru.first + 2 * K - 3, 0)) * 2 * K;
         const size_t sv = size_t(std::max<int64_t>(rv.second - rv.first + 2 * K - 3, 0)) * 2 * K;
         if (su) device::memcpy_async(db[cur].data(), Du, su * sizeof(R), c.stream);
@@ -134,6 +139,7 @@ struct RowRotSink : host::RotSink<real_type<T>> {
         cur ^= 1;
         bu.clear();
         bv.clear();
+        trace::Block tw("bdsqr_rot_wait");
         slate_hip_call(hipEventSynchronize(ev[cur]));   // the other staging buffer is free again
     }
     void sweep(Rots const& ru, Rots const& rv) override {

@@ -9,3 +9,4 @@ from .cholesky import *   # noqa: F401,F403
 from .lu import *         # noqa: F401,F403
 from .qr import *         # noqa: F401,F403
 from .eig import *        # noqa: F401,F403
+from .factor import *     # noqa: F401,F403

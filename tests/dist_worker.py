@@ -1015,6 +1015,27 @@ def case_tile_comm(tg, dt, nb):
     np.testing.assert_array_equal(s.to_numpy(A), a)
 
 
+def case_factor_objects(tg, dt, nb):
+    """Factor-once objects (models/factor.py) on the grid: LU (tournament)
+    solve of two right-hand-side blocks and a mixed-precision solve that
+    refines to working precision against the untouched A."""
+    n = 3 * nb + 11
+    a = rnd(n, n, dt, 191) + 4 * np.eye(n, dtype=dt)
+    F = s.LUFactor(s.from_numpy(a.copy(), nb=nb, target=tg), target=tg)
+    for seed in (192, 193):
+        b = rnd(n, 2, dt, seed)
+        B = s.from_numpy(b, nb=nb, target=tg)
+        F.solve(B)
+        assert relerr(a @ s.to_numpy(B), b) < tol(dt)
+    if dt in (np.float64, np.complex128):
+        A = s.from_numpy(a, nb=nb, target=tg)
+        M = s.MixedLUFactor(A, target=tg)
+        b = rnd(n, 1, dt, 194)
+        X, it = M.solve(s.from_numpy(b, nb=nb, target=tg))
+        assert 0 <= it < 30
+        assert relerr(a @ s.to_numpy(X), b) < 1e-12
+
+
 CASES = {k[5:]: v for k, v in globals().items() if k.startswith("case_")}
 EXTRA = {}
 

@@ -12,7 +12,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 WORKER = os.path.join(HERE, "dist_worker.py")
-CASES = "tile_comm,lanes,pplu_exact,rowx_bytes,solve_notemp,geqrf_cholqr,gelqf,band_storage,gemm,herk,rank2k,trsm,trmm,hemm,stationary,rbt,heev,stages,band,band_blas,layout,aasen,potrf,getrf,getrf_shapes,getrf_thresh,geqrf,geqrf_shapes,norm,norm_masked,mixed"
+CASES = "tile_comm,factor_objects,lanes,pplu_exact,rowx_bytes,solve_notemp,geqrf_cholqr,gelqf,band_storage,gemm,herk,rank2k,trsm,trmm,hemm,stationary,rbt,heev,stages,band,band_blas,layout,aasen,potrf,getrf,getrf_shapes,getrf_thresh,geqrf,geqrf_shapes,norm,norm_masked,mixed"
 
 
 def _free_port():
