@@ -223,22 +223,32 @@ void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& o
 /// order (no per-group launches, no dense zero blocks).  Groups are packed on
 /// the host into pinned chunks that upload while the previous chunk applies.
 /// SLATE_HB2ST_FUSED=0 keeps the blocked GEMM sequence.
-void unmtr_hb2st_fused(host::Reflectors<double> const& Q, int64_t n, int64_t kd, double* Z, int64_t ldz,
-                       int64_t ncols, lb::Ctx const& c) {
+/// bc != nullptr: only rank 0 of bc holds Q (Qp); it packs each chunk and
+/// the chunk travels to the other ranks' device buffers by one broadcast, so
+/// no other rank keeps the O(n^2) reflectors on its host.  Every rank of bc
+/// calls this (ncols may be 0).
+void unmtr_hb2st_fused(host::Reflectors<double> const* Qp, int64_t n, int64_t kd, double* Z, int64_t ldz,
+                       int64_t ncols, lb::Ctx const& c, Comm* bc = nullptr) {
     trace::Block tb("unmtr_hb2st_fused");
     constexpr int64_t HB = 64;
+    const bool root = !bc || bc->rank() == 0;
     std::map<std::pair<int64_t, int64_t>, std::vector<size_t>> groups;
-    for (size_t r = 0; r < Q.size(); ++r) {
-        const int64_t j = Q.tag[r];
-        slate_assert(j >= 0);
-        groups[{j / HB, (Q.off[r] - j - 1) / kd}].push_back(r);
-    }
     std::vector<std::pair<int64_t, int64_t>> keys;
-    for (auto& kv : groups) keys.push_back(kv.first);
-    std::sort(keys.begin(), keys.end(), [](auto const& a, auto const& b) {
-        return a.first != b.first ? a.first > b.first : a.second < b.second;
-    });
-    const int64_t ng = int64_t(keys.size()), CG = 512;
+    if (root) {
+        host::Reflectors<double> const& Q = *Qp;
+        for (size_t r = 0; r < Q.size(); ++r) {
+            const int64_t j = Q.tag[r];
+            slate_assert(j >= 0);
+            groups[{j / HB, (Q.off[r] - j - 1) / kd}].push_back(r);
+        }
+        for (auto& kv : groups) keys.push_back(kv.first);
+        std::sort(keys.begin(), keys.end(), [](auto const& a, auto const& b) {
+            return a.first != b.first ? a.first > b.first : a.second < b.second;
+        });
+    }
+    int64_t ng = int64_t(keys.size());
+    const int64_t CG = 512;
+    if (bc && bc->size() > 1) bc->bcast(&ng, 1, 0, Loc::Host, nullptr);
     const size_t vsz = size_t(CG) * HB * HB, tsz = size_t(CG) * HB;
     // one pinned staging block per buffer: V | tau | R0
     const size_t bytes = (vsz + tsz) * sizeof(double) + size_t(CG) * sizeof(int64_t);
@@ -255,6 +265,11 @@ void unmtr_hb2st_fused(host::Reflectors<double> const& Q, int64_t n, int64_t kd,
         double* hV = static_cast<double*>(hbuf[cur]);
         double* htau = hV + vsz;
         int64_t* hR0 = reinterpret_cast<int64_t*>(htau + tsz);
+        double* dV = static_cast<double*>(dbuf[cur]);
+        double* dtau = dV + vsz;
+        int64_t* dR0 = reinterpret_cast<int64_t*>(dtau + tsz);
+        if (root) {
+        host::Reflectors<double> const& Q = *Qp;
         #pragma omp parallel for schedule(dynamic, 8)
         for (int64_t bi = 0; bi < nc; ++bi) {
             const auto key = keys[size_t(g0 + bi)];
@@ -270,13 +285,15 @@ void unmtr_hb2st_fused(host::Reflectors<double> const& Q, int64_t n, int64_t kd,
                 htau[bi * HB + i] = Q.tau[r];
             }
         }
-        double* dV = static_cast<double*>(dbuf[cur]);
-        double* dtau = dV + vsz;
-        int64_t* dR0 = reinterpret_cast<int64_t*>(dtau + tsz);
         device::memcpy_async(dV, hV, size_t(nc) * HB * HB * sizeof(double), c.stream);
         device::memcpy_async(dtau, htau, size_t(nc) * HB * sizeof(double), c.stream);
         device::memcpy_async(dR0, hR0, size_t(nc) * sizeof(int64_t), c.stream);
-        slate_amd::dev::hb2st_tfac(nc, dV, dtau, dT[cur], c.stream);
+        }
+        if (bc && bc->size() > 1) {
+            // the packed chunk (V | tau | R0, contiguous) to every rank
+            bc->bcast(dbuf[cur], bytes, ScalarType::Byte, 0, Loc::Device, c.stream);
+        }
+        if (ncols > 0) slate_amd::dev::hb2st_tfac(nc, dV, dtau, dT[cur], c.stream);
         slate_amd::dev::hb2st_apply(nc, dR0, dV, dT[cur], Z, ldz, n, ncols, c.stream);
         slate_hip_call(hipEventRecord(ev[cur], c.stream));
         cur ^= 1;
@@ -290,18 +307,48 @@ void unmtr_hb2st_fused(host::Reflectors<double> const& Q, int64_t n, int64_t kd,
     }
 }
 
+bool hb2st_fused_enabled() {
+    static const bool fused = [] {
+        const char* e = std::getenv("SLATE_HB2ST_FUSED");
+        return !e || std::atoi(e) != 0;
+    }();
+    return fused;
+}
+
+/// Do the stage-2 reflectors stay on rank 0 and stream to the others in
+/// packed device chunks (fp64, device, fused kernels, more than one rank)?
+template <typename T>
+bool stage2_streamed(Target target, int64_t kd, Comm& w) {
+    return std::is_same<T, double>::value && target == Target::Devices && hb2st_fused_enabled() && kd <= 64 &&
+           w.size() > 1;
+}
+
+template <typename T>
+void unmtr_hb2st_blocked(host::Reflectors<T> const& Q, int64_t n, int64_t kd, T* Z, int64_t ldz, int64_t ncols,
+                        lb::Ctx const& c);
+
+/// Stage-2 back-transform of this rank's columns; every rank calls it.
+/// streamed: Q is on rank 0 of w only (stage2_streamed).
+template <typename T>
+void stage2_apply(host::Reflectors<T> const& Q, bool streamed, int64_t n, int64_t kd, T* Z, int64_t ldz,
+                  int64_t ncols, lb::Ctx const& c, Comm& w) {
+    if constexpr (std::is_same<T, double>::value) {
+        if (streamed) {
+            unmtr_hb2st_fused(w.rank() == 0 ? &Q : nullptr, n, kd, Z, ldz, ncols, c, &w);
+            return;
+        }
+    }
+    if (ncols > 0) unmtr_hb2st_blocked(Q, n, kd, Z, ldz, ncols, c);
+}
+
 template <typename T>
 void unmtr_hb2st_blocked(host::Reflectors<T> const& Q, int64_t n, int64_t kd, T* Z, int64_t ldz, int64_t ncols,
                         lb::Ctx const& c) {
     namespace kd_ = slate_amd::dev;
     if (Q.size() == 0 || ncols <= 0) return;
     if constexpr (std::is_same<T, double>::value) {
-        static const bool fused = [] {
-            const char* e = std::getenv("SLATE_HB2ST_FUSED");
-            return !e || std::atoi(e) != 0;
-        }();
-        if (c.dev() && fused && kd <= 64) {
-            unmtr_hb2st_fused(Q, n, kd, Z, ldz, ncols, c);
+        if (c.dev() && hb2st_fused_enabled() && kd <= 64) {
+            unmtr_hb2st_fused(&Q, n, kd, Z, ldz, ncols, c);
             return;
         }
     }
@@ -509,7 +556,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
             bcast_vec(w, d, 0);
             bcast_vec(w, e, 0);
             bcast_vec(w, phase, 0);
-            if (wanted(Z)) bcast_reflectors(w, Q2, 0);
+            if (wanted(Z) && !stage2_streamed<T>(target, kd, w)) bcast_reflectors(w, Q2, 0);
         }
     }
     B.clear(); B.shrink_to_fit();
@@ -563,8 +610,9 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
                 for (int64_t j = 0; j < lz.n; ++j)
                     for (int64_t i = 0; i < n; ++i) lz.ptr[i + j * lz.ld] = phase[i] * T(lq.ptr[i + j * lq.ld]);
             }
-            unmtr_hb2st_blocked(Q2, n, kd, lz.ptr, lz.ld, lz.n, c);
         }
+        Comm& w = gA->world();
+        stage2_apply(Q2, stage2_streamed<T>(target, kd, w), n, kd, lz.ptr, lz.ld, lz.n, c, w);
     }
     // stage-1 back-transform (unmtr_he2hb) on F's layout, then into Z
     Matrix<T> Zw(n, n, kd, kd, gA);
@@ -780,8 +828,10 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
             bcast_vec(w, e, 0);
             bcast_vec(w, pu, 0);
             bcast_vec(w, pv, 0);
-            if (wanted(U)) bcast_reflectors(w, QU2, 0);
-            if (wanted(VT)) bcast_reflectors(w, QV2, 0);
+            if (!stage2_streamed<T>(target, kd, w)) {
+                if (wanted(U)) bcast_reflectors(w, QU2, 0);
+                if (wanted(VT)) bcast_reflectors(w, QV2, 0);
+            }
         }
     }
     const bool wu = wanted(U), wv = wanted(VT);
@@ -820,7 +870,8 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
         slate::copy<T, T>(U2, U1, opts);
         {
             LocalBlock<T> l1 = U1.local(loc_of(target), true);
-            if (l1.n > 0) unmtr_hb2st_blocked(QU2, n, kd, l1.ptr, l1.ld, l1.n, c);
+            Comm& w = gA->world();
+            stage2_apply(QU2, stage2_streamed<T>(target, kd, w), n, kd, l1.ptr, l1.ld, l1.n, c, w);
         }
         Matrix<T> Uw(m, n, kd, kd, gA);
         Uw.insertLocalTiles(target);
@@ -848,7 +899,8 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
         slate::copy<T, T>(V2, V1, opts);
         {
             LocalBlock<T> l1 = V1.local(loc_of(target), true);
-            if (l1.n > 0) unmtr_hb2st_blocked(QV2c, n, kd, l1.ptr, l1.ld, l1.n, c);
+            Comm& w = gA->world();
+            stage2_apply(QV2c, stage2_streamed<T>(target, kd, w), n, kd, l1.ptr, l1.ld, l1.n, c, w);
         }
         Matrix<T> VTw(n, n, kd, kd, gA);
         VTw.insertLocalTiles(target);
