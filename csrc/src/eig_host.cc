@@ -157,14 +157,16 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
     };
     // Sweeps are pipelined over threads (the reference's hb2st.cc runs its
     // bulge-chasing sweeps as OpenMP tasks the same way).  Step t of sweep j
-    // works on the window [s0 - b, s0 + 2b) with s0 = j + 1 + t b; it may run
-    // once sweep j-1 has finished its steps 0..t+3 (the last ones whose windows
-    // reach into it), and sweep j-1's later steps cannot reach back into it.
-    // Reflectors are collected per sweep and concatenated in sweep order:
-    // reflectors of different sweeps that ran out of order act on disjoint rows
-    // and commute.
+    // (lower triangle only) touches rows [s0, s0 + 2b) x columns [s0 - b,
+    // s0 + b) with s0 = j + 1 + t b; sweep j-1's step t' sits at s0 - 1 +
+    // (t' - t) b, so the two rectangles share elements only for t' <= t + 2
+    // (at t' = t + 2: its bulge column is row block (c) of this step).  Step t
+    // therefore runs once sweep j-1 has finished its steps 0..t+2, and sweep
+    // j-1's later steps cannot reach back into it.  Reflectors are collected
+    // per sweep and concatenated in sweep order: reflectors of different
+    // sweeps that ran out of order act on disjoint rows and commute.
     const int64_t nsw = (b > 1 && n > 2) ? n - 2 : 0;
-    constexpr int64_t kLag = 4;
+    constexpr int64_t kLag = 3;
     constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
     std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
     for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
@@ -271,15 +273,16 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         }
     };
     // Sweeps pipelined over threads as in hb2st: step t of sweep j touches
-    // rows/columns [c0 - b, c0 + 2b) with c0 = j + 1 + t b (right update rows
-    // [c0 - b, c0 + L), left update columns up to c0 + L - 1 + b); sweep j-1's
-    // step t' sits at c0 - 1 + (t' - t) b, disjoint once t' >= t + 4, so step
-    // t may run once sweep j-1 has finished its steps 0..t+3 (the chain of
-    // lags bounds the whole reduction: lag 4 instead of 6 shortens it by a
-    // third).  Reflectors are kept per sweep and concatenated in sweep order
-    // (out-of-order ones commute).
+    // rows [c0 - b, c0 + b) x columns [c0, c0 + 2b) with c0 = j + 1 + t b
+    // (right update rows [c0 - b, c0 + L) x columns [c0, c0 + L), left update
+    // rows [c0, c0 + L) x columns up to c0 + L - 1 + b); sweep j-1's step t'
+    // sits at c0 - 1 + (t' - t) b, whose rectangle shares elements with this
+    // one only for t' <= t + 2, so step t may run once sweep j-1 has finished
+    // its steps 0..t+2 (the chain of lags bounds the whole reduction: lag 3
+    // instead of 6 halves it).  Reflectors are kept per sweep and concatenated
+    // in sweep order (out-of-order ones commute).
     const int64_t nsw = n > 1 ? n - 1 : 0;
-    constexpr int64_t kLag = 4;
+    constexpr int64_t kLag = 3;
     constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
     std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
     for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
