@@ -115,8 +115,10 @@ struct PlaneRot { int64_t i; R c, s; };
 template <typename R>
 struct RotSink {
     virtual ~RotSink() = default;
-    /// one implicit-shift QR sweep: adjacent rotations, ascending, on U (ru) and Vt (rv)
-    virtual void sweep(std::vector<PlaneRot<R>> const& ru, std::vector<PlaneRot<R>> const& rv) = 0;
+    /// one implicit-shift QR sweep: adjacent rotations, ascending, on U (ru)
+    /// and Vt (rv).  The sink may take the vectors' contents (swap); the
+    /// caller clears them before the next sweep.
+    virtual void sweep(std::vector<PlaneRot<R>>& ru, std::vector<PlaneRot<R>>& rv) = 0;
     /// cancellation rotation on U columns (a, b): [x y] <- [x c + y s, y c - x s]
     virtual void rot_u(int64_t a, int64_t b, R c, R s) = 0;
     /// Vt column k *= -1

@@ -17,6 +17,7 @@
 #include <pybind11/numpy.h>
 
 #include <complex>
+#include <chrono>
 #include <cstring>
 
 namespace py = pybind11;
@@ -485,6 +486,29 @@ PYBIND11_MODULE(_slate, m) {
         for (int64_t i = 0; i < n; ++i) { U[i + i * n] = 1; VT[i + i * n] = 1; }
         slate::host::bdsqr<double, double>(n, d.data(), e.data(), U.data(), n, n, VT.data(), n, n);
         return py::make_tuple(d, mat(U, n, n), mat(VT, n, n)); });
+    // bdsqr's host loop alone (rotations generated and handed to a sink that
+    // only keeps them, as the device sink's batching does): its cost bounds
+    // the device SVD's bdsqr stage
+    m.def("bdsqr_core_bench", [](VD d, VD e) {
+        struct KeepSink : slate::host::RotSink<double> {
+            std::vector<std::vector<slate::host::PlaneRot<double>>> keep_u, keep_v;
+            size_t count = 0;
+            void sweep(std::vector<slate::host::PlaneRot<double>>& ru,
+                       std::vector<slate::host::PlaneRot<double>>& rv) override {
+                count += ru.size() + rv.size();
+                keep_u.emplace_back(); keep_u.back().swap(ru);
+                keep_v.emplace_back(); keep_v.back().swap(rv);
+                if (keep_u.size() == 16) { keep_u.clear(); keep_v.clear(); }
+            }
+            void rot_u(int64_t, int64_t, double, double) override {}
+            void negate_v(int64_t) override {}
+            void permute(std::vector<int64_t> const&) override {}
+        } sink;
+        const int64_t n = d.size();
+        auto t0 = std::chrono::steady_clock::now();
+        slate::host::bdsqr_core<double>(n, d.data(), e.data(), &sink);
+        double dt = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        return py::make_tuple(d, dt, sink.count); });
     m.def("timers", []() { return timers(); });
     m.def("clear_timers", []() { timers().clear(); });
 

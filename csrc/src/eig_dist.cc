@@ -352,7 +352,7 @@ struct QlRowSink : host::RotSink<real_type<T>> {
     int64_t n, rows, ld;
     T* Z;
     RowRotSink<T> rs;
-    const std::vector<host::PlaneRot<R>> none;
+    std::vector<host::PlaneRot<R>> none;
     QlRowSink(lb::Ctx const& c_, int64_t n_, T* Z_, int64_t ld_, int64_t rows_)
         : c(c_), n(n_), rows(rows_), ld(ld_), Z(Z_), rs(c_, n_) {
         rs.U = rows > 0 ? Z + (n - 1) * ld : nullptr;
@@ -360,10 +360,11 @@ struct QlRowSink : host::RotSink<real_type<T>> {
         rs.urows = rows;
     }
     void flush() { rs.finish(); }
-    void sweep(std::vector<host::PlaneRot<R>> const& ru, std::vector<host::PlaneRot<R>> const&) override {
+    void sweep(std::vector<host::PlaneRot<R>>& ru, std::vector<host::PlaneRot<R>>&) override {
         std::vector<host::PlaneRot<R>> asc(ru.size());
         for (size_t t = 0; t < ru.size(); ++t) asc[t] = {n - 2 - ru[t].i, ru[t].c, -ru[t].s};
         std::sort(asc.begin(), asc.end(), [](auto const& a, auto const& b) { return a.i < b.i; });
+        none.clear();
         rs.sweep(asc, none);
     }
     void rot_u(int64_t, int64_t, R, R) override { slate_error("steqr2: unexpected rotation"); }

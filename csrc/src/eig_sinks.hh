@@ -116,8 +116,7 @@ struct RowRotSink : host::RotSink<real_type<T>> {
             if (U) sweeps_host(urows, U, ldu, ru.first, ru.second, D.data());
             auto rv = build(bv, D.data());
             if (V) sweeps_host(vrows, V, ldv, rv.first, rv.second, D.data());
-            bu.clear();
-            bv.clear();
+            recycle();
             return;
         }
         namespace kd_ = slate_amd::dev;
@@ -137,15 +136,27 @@ struct RowRotSink : host::RotSink<real_type<T>> {
                          V && sv ? vrows : 0, kd_::dptr(V), ldv, rv.first, rv.second, db[cur].data() + tsz, c.stream);
         slate_hip_call(hipEventRecord(ev[cur], c.stream));
         cur ^= 1;
-        bu.clear();
-        bv.clear();
+        recycle();
         trace::Block tw("bdsqr_rot_wait");
         slate_hip_call(hipEventSynchronize(ev[cur]));   // the other staging buffer is free again
     }
-    void sweep(Rots const& ru, Rots const& rv) override {
-        bu.push_back(ru);
-        bv.push_back(rv);
+    void sweep(Rots& ru, Rots& rv) override {
+        // take the sweep's rotations without copying (the caller clears its
+        // vectors; spare ones keep their capacity for the next sweeps)
+        bu.emplace_back();
+        bv.emplace_back();
+        if (!spare.empty()) { bu.back().swap(spare.back()); spare.pop_back(); }
+        if (!spare.empty()) { bv.back().swap(spare.back()); spare.pop_back(); }
+        bu.back().swap(ru);
+        bv.back().swap(rv);
         if (int(bu.size()) == K) flush();
+    }
+    std::vector<Rots> spare;
+    void recycle() {
+        for (auto& r : bu) { r.clear(); spare.push_back(std::move(r)); }
+        for (auto& r : bv) { r.clear(); spare.push_back(std::move(r)); }
+        bu.clear();
+        bv.clear();
     }
     void rot_u(int64_t a, int64_t b, R cc, R sn) override {
         if (!U) return;
