@@ -307,6 +307,18 @@ void unmtr_hb2st_fused(host::Reflectors<double> const* Qp, int64_t n, int64_t kd
     }
 }
 
+/// Band width of the two-stage reductions: at most 64 (SLATE_EIG_KD lowers
+/// it: the host bulge chase costs O(n^2 kd) with a pipeline chain of
+/// O(n kd^2), the first stage prefers wide panels).
+int64_t eig_band_width() {
+    static const int64_t kd = [] {
+        const char* e = std::getenv("SLATE_EIG_KD");
+        const int64_t v = e ? std::atoll(e) : 64;
+        return std::max<int64_t>(8, std::min<int64_t>(v, 64));
+    }();
+    return kd;
+}
+
 bool hb2st_fused_enabled() {
     static const bool fused = [] {
         const char* e = std::getenv("SLATE_HB2ST_FUSED");
@@ -526,7 +538,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     // band width of the two-stage reduction: the bulge chase costs O(n^2 kd)
     // on the host, the first stage is memory-bound either way, so large tiles
     // are re-tiled to kd <= 64 (reference uses the tile size)
-    const int64_t kd = std::min<int64_t>(A.nb(), 64);
+    const int64_t kd = std::min<int64_t>(A.nb(), eig_band_width());
     auto gA = A.grid();
     Matrix<T> F(n, n, kd, kd, gA);
     F.insertLocalTiles(target);
@@ -806,7 +818,7 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
     const int64_t m = A.m(), n = A.n();
     slate_assert(m >= n);
     // stage 1 on kd-wide tiles (see heev)
-    const int64_t kd = std::min<int64_t>(A.nb(), 64);
+    const int64_t kd = std::min<int64_t>(A.nb(), eig_band_width());
     auto gA = A.grid();
     Matrix<T> W(m, n, kd, kd, gA);
     W.insertLocalTiles(target);

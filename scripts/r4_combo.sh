@@ -11,5 +11,6 @@ for S in 1 0; do
   echo "== slide=$S"; grep -v "^W20\|amdgpu.ids" $O/heev_slide$S.log | head -24
 done
 EIG_PROF_OUT=$O timeout -k 10 300 python3 -u scripts/eig_prof.py 8192 256 d svd > $O/svd.log 2>&1; grep -v "^W20\|amdgpu.ids" $O/svd.log | head -26
+SLATE_EIG_KD=32 EIG_PROF_OUT=$O timeout -k 10 400 python3 -u scripts/eig_prof.py 8192 256 d heev,svd > $O/eig_kd32.log 2>&1; echo "== kd=32"; grep -E "^(heev|svd)|hb2st|tb2bd|bdsqr |he2hb|ge2tb|unmtr_hb2st_fused" $O/eig_kd32.log | head -20
 timeout -k 10 300 python3 bench.py --routines dgeqrf --steps 2 --warmup 1 --extras none > $O/dgeqrf.log 2>&1 && grep -E "timed|backward" $O/dgeqrf.log || exit 1
 CP_ARGS="--routines qr" bash scripts/r4_critpath.sh
