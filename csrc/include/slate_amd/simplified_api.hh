@@ -310,6 +310,28 @@ void eig_vals(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::
     hegv(itype, A, B, Lambda, Z, opts);
 }
 template <typename T>
+void eig(int64_t itype, HermitianMatrix<T>& A, HermitianMatrix<T>& B, std::vector<real_type<T>>& Lambda,
+         Options const& opts = {}) {
+    eig_vals(itype, A, B, Lambda, opts);
+}
+/// real symmetric generalized problems (sygv)
+template <typename T>
+void eig(int64_t itype, SymmetricMatrix<T>& A, SymmetricMatrix<T>& B, std::vector<real_type<T>>& Lambda,
+         Matrix<T>& Z, Options const& opts = {}) {
+    sygv(itype, A, B, Lambda, Z, opts);
+}
+template <typename T>
+void eig_vals(int64_t itype, SymmetricMatrix<T>& A, SymmetricMatrix<T>& B, std::vector<real_type<T>>& Lambda,
+              Options const& opts = {}) {
+    Matrix<T> Z;
+    sygv(itype, A, B, Lambda, Z, opts);
+}
+template <typename T>
+void eig(int64_t itype, SymmetricMatrix<T>& A, SymmetricMatrix<T>& B, std::vector<real_type<T>>& Lambda,
+         Options const& opts = {}) {
+    eig_vals(itype, A, B, Lambda, opts);
+}
+template <typename T>
 void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Options const& opts = {}) {
     svd_vals(A, Sigma, opts);
 }

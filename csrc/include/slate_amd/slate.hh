@@ -61,6 +61,35 @@ void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Option
 template <typename T>
 void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
 
+/// Method-specific entry points (reference slate.hh hemmA / hemmC / trsmA /
+/// trsmB): the generic driver with the method option fixed.
+template <typename T>
+inline void hemmA(Side side, T alpha, HermitianMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
+                  Options const& opts = {}) {
+    Options o = opts;
+    o[Option::MethodHemm] = int64_t(MethodHemm::HemmA);
+    hemm(side, alpha, A, B, beta, C, o);
+}
+template <typename T>
+inline void hemmC(Side side, T alpha, HermitianMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
+                  Options const& opts = {}) {
+    Options o = opts;
+    o[Option::MethodHemm] = int64_t(MethodHemm::HemmC);
+    hemm(side, alpha, A, B, beta, C, o);
+}
+template <typename T>
+inline void trsmA(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts = {}) {
+    Options o = opts;
+    o[Option::MethodTrsm] = int64_t(MethodTrsm::TrsmA);
+    trsm(side, alpha, A, B, o);
+}
+template <typename T>
+inline void trsmB(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts = {}) {
+    Options o = opts;
+    o[Option::MethodTrsm] = int64_t(MethodTrsm::TrsmB);
+    trsm(side, alpha, A, B, o);
+}
+
 //------------------------------------------------------------------------------
 // Auxiliary
 template <typename T>
@@ -106,6 +135,11 @@ int64_t potri(HermitianMatrix<T>& A, Options const& opts = {});
 template <typename T>
 int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
 template <typename T>
+[[deprecated("Use posv_mixed")]] inline int64_t posvMixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter,
+                                                         Options const& opts = {}) {
+    return posv_mixed(A, B, X, iter, opts);
+}
+template <typename T>
 int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
 template <typename T>
 real_type<T> pocondest(Norm in_norm, HermitianMatrix<T>& A, real_type<T> Anorm, Options const& opts = {});
@@ -132,6 +166,12 @@ template <typename T>
 int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, Options const& opts = {});
 template <typename T>
 int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts = {});
+/// (reference's older camel-case name)
+template <typename T>
+[[deprecated("Use gesv_mixed")]] inline int64_t gesvMixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X,
+                                                         int& iter, Options const& opts = {}) {
+    return gesv_mixed(A, pivots, B, X, iter, opts);
+}
 template <typename T>
 int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter,
                          Options const& opts = {});
