@@ -50,28 +50,59 @@ struct RotJob {
 };
 
 template <typename T, typename R, int K, int PF>
-__device__ inline void rot_sweeps_row(RotJob<T, R> const& J, int64_t r) {
-    T* row = J.M + r;
+__device__ inline void rot_sweeps_row(RotJob<T, R> const& J, int64_t r, R* sD) {
+    // sD: this wave's LDS ring, 2 x PF steps x 2K reals.  The step tables are
+    // the same for every lane, so a block of PF steps is loaded once per wave
+    // with coalesced vector loads (8 reals per lane) one block ahead, and each
+    // step reads its 2K coefficients from LDS as broadcasts -- instead of 2K
+    // wave-uniform global loads per step, whose latency a lone wave per CU
+    // cannot hide.
+    constexpr int BLK = PF * 2 * K, PER = BLK / 64;
+    const int lane = threadIdx.x & 63;
+    const bool live = r < J.rows;
+    T* row = J.M + (live ? r : 0);
     const int64_t ld = J.ld, p0 = J.p0, p1 = J.p1;
     const R* D = J.D;
+    const int64_t tend = p1 - 2 + 2 * (K - 1);
+    const int64_t dtot = (tend - p0 + 1) * 2 * K;   // reals of the table in use
+    R nxt[PER];
+    auto fetch = [&](int64_t t0) {
+        const int64_t base = (t0 - p0) * 2 * K;
+        #pragma unroll
+        for (int i = 0; i < PER; ++i) {
+            const int64_t idx = base + lane + 64 * i;
+            nxt[i] = idx < dtot ? D[idx] : R(0);
+        }
+    };
+    auto stash = [&](int buf) {
+        #pragma unroll
+        for (int i = 0; i < PER; ++i) sD[buf * BLK + lane + 64 * i] = nxt[i];
+    };
+    fetch(p0);
+    stash(0);
+    __syncthreads();
     T w[2 * K];
     #pragma unroll
     for (int i = 0; i < 2 * K; ++i) w[i] = T();
-    w[2 * K - 2] = row[p0 * ld];
-    w[2 * K - 1] = (p0 + 1 < p1) ? row[(p0 + 1) * ld] : T();
+    if (live) {
+        w[2 * K - 2] = row[p0 * ld];
+        w[2 * K - 1] = (p0 + 1 < p1) ? row[(p0 + 1) * ld] : T();
+    }
     T pf[PF];
     #pragma unroll
     for (int i = 0; i < PF; ++i) {
         const int64_t cpf = p0 + 2 + i;
-        pf[i] = cpf < p1 ? row[cpf * ld] : T();
+        pf[i] = (live && cpf < p1) ? row[cpf * ld] : T();
     }
-    const int64_t tend = p1 - 2 + 2 * (K - 1);
+    int cur = 0;
     for (int64_t t0 = p0; t0 <= tend; t0 += PF) {
+        if (t0 + PF <= tend) fetch(t0 + PF);
+        const R* cb = sD + cur * BLK;
         #pragma unroll
         for (int u = 0; u < PF; ++u) {
             const int64_t tau = t0 + u;
             if (tau > tend) break;
-            const R* cs = D + 2 * K * (tau - p0);
+            const R* cs = cb + 2 * K * u;
             #pragma unroll
             for (int s = 0; s < K; ++s) {
                 const R c = cs[2 * s], sn = cs[2 * s + 1];
@@ -80,15 +111,18 @@ __device__ inline void rot_sweeps_row(RotJob<T, R> const& J, int64_t r) {
                 w[2 * K - 1 - 2 * s] = x * sn + y * c;
             }
             const int64_t cr = tau - 2 * K + 2;
-            if (cr >= p0) row[cr * ld] = w[0];
+            if (live && cr >= p0) row[cr * ld] = w[0];
             #pragma unroll
             for (int i = 0; i < 2 * K - 1; ++i) w[i] = w[i + 1];
             w[2 * K - 1] = pf[u];                         // column tau + 2
             const int64_t cn = tau + 2 + PF;
-            pf[u] = cn < p1 ? row[cn * ld] : T();
+            pf[u] = (live && cn < p1) ? row[cn * ld] : T();
         }
+        if (t0 + PF <= tend) stash(cur ^ 1);
+        __syncthreads();
+        cur ^= 1;
     }
-    if (p1 - 1 >= p0) row[(p1 - 1) * ld] = w[0];
+    if (live && p1 - 1 >= p0) row[(p1 - 1) * ld] = w[0];
 }
 
 constexpr int kRotPrefetch = 16;
@@ -97,13 +131,13 @@ constexpr int kRotPrefetch = 16;
 // take job a, the rest job b
 template <typename T, typename R, int K>
 __global__ __launch_bounds__(64) void rot_sweeps_kernel(RotJob<T, R> a, RotJob<T, R> b, int64_t nblk_a) {
+    __shared__ R sD[2 * kRotPrefetch * 2 * K];
     const bool first = int64_t(blockIdx.x) < nblk_a;
     const int64_t r = (first ? int64_t(blockIdx.x) : int64_t(blockIdx.x) - nblk_a) * 64 + threadIdx.x;
-    if (first) {
-        if (r < a.rows) rot_sweeps_row<T, R, K, kRotPrefetch>(a, r);
-    } else {
-        if (r < b.rows) rot_sweeps_row<T, R, K, kRotPrefetch>(b, r);
-    }
+    // (every lane of the wave takes part in the table loads; rows past the
+    // end only skip their matrix accesses)
+    if (first) rot_sweeps_row<T, R, K, kRotPrefetch>(a, r, sD);
+    else rot_sweeps_row<T, R, K, kRotPrefetch>(b, r, sD);
 }
 
 // one rotation on columns (a, b): [x y] <- [x c + y s, y c - x s]
