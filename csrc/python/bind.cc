@@ -11,6 +11,7 @@
 #include <pybind11/functional.h>
 
 #include "slate_amd/slate.hh"
+#include "../src/lu_dist.hh"
 #include "slate_amd/trace.hh"
 #include "slate_amd/runtime.hh"
 #include "bind_drivers.hh"

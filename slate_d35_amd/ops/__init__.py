@@ -10,7 +10,7 @@ from __future__ import annotations
 
 from .. import _slate
 
-__all__ = ["have_native_ops", "gemm", "herk", "trsm", "potrf", "getrf_panel", "geqrf_panel"]
+__all__ = ["have_native_ops", "gemm", "herk", "trsm", "potrf", "getrf_panel", "geqrf_panel", "lu_sign"]
 
 
 def have_native_ops() -> bool:
@@ -79,3 +79,12 @@ def geqrf_panel(A):
     fn = getattr(_slate, f"lb_geqrf_panel_{_suffix(A)}")
     pa, m, n, lda = _cm(A)
     return fn(m, n, pa, lda)
+
+
+def lu_sign(A):
+    """Sign-modified LU without pivoting of a column-major n x n block in
+    place (the Householder reconstruction step of the CholeskyQR / TSQR QR
+    panels, lu_dist.cc)."""
+    fn = getattr(_slate, f"lb_lu_sign_{_suffix(A)}")
+    pa, m, n, lda = _cm(A)
+    fn(n, pa, lda)
