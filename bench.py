@@ -154,7 +154,12 @@ def main():
     # Lookahead: 1 (the reference default), except on one GPU where dpotrf and
     # dgeqrf measured faster at 2 (profiles/r2_sweep2_la_nb_ppiv.txt: potrf
     # 59.4 -> 60.1, geqrf 55.7 -> 56.2 TFLOP/s at n=65536).
-    la_per = {"dpotrf": 2, "dgeqrf": 2} if world == 1 else {}
+    # p x q grids: lookahead 2 for every factorization, so one late panel
+    # (its chain of tournament / CholeskyQR kernels and messages is longer
+    # than a step's trailing update for most steps at 2 x 4,
+    # profiles/r4_critpath_2x4_*.txt) does not stall the trailing queue of
+    # the next step as well.
+    la_per = {"dpotrf": 2, "dgeqrf": 2} if world == 1 else {"dpotrf": 2, "dgeqrf": 2, "dgetrf": 2, "dgesv_mixed": 2}
 
     def la_of(rname):
         return a.lookahead or la_per.get(rname, 1)
