@@ -16,6 +16,7 @@
 #include <complex>
 #include <cstring>
 #include <vector>
+#include <type_traits>
 
 namespace slate {
 namespace host {
@@ -38,12 +39,141 @@ void pack(Op op, int64_t m, int64_t n, T const* A, int64_t lda, T* B) {
 }
 
 //------------------------------------------------------------------------------
+/// Packed, register-blocked GEMM for real types (the host target's compute
+/// path: BASELINE config 1 and every host-task driver).  Goto-style: B is
+/// packed into NR-column panels per (jc, pc) block, A into MR-row panels per
+/// thread, and an MR x NR micro-tile of C lives in 12 AVX2 registers (GCC
+/// vector extensions; -march=x86-64-v3 turns them into FMA ymm code).
+namespace gemm_detail {
+
+template <typename T> struct VecT;
+template <> struct VecT<double> { typedef double v __attribute__((vector_size(32))); static constexpr int W = 4; };
+template <> struct VecT<float> { typedef float v __attribute__((vector_size(32))); static constexpr int W = 8; };
+
+template <typename T>
+struct Blk {
+    static constexpr int W = VecT<T>::W, MR = 2 * W, NR = 6;
+    static constexpr int64_t KC = 256, MC = 16 * MR, NC = 6 * 512;
+};
+
+/// Ap[p][l][r] = op(A)(i0 + p MR + r, l0 + l), zero-padded rows
+template <typename T>
+inline void pack_a(Op op, T const* A, int64_t lda, int64_t i0, int64_t mc, int64_t l0, int64_t kc, T* Ap) {
+    constexpr int MR = Blk<T>::MR;
+    for (int64_t p = 0; p * MR < mc; ++p) {
+        T* dst = Ap + p * MR * kc;
+        const int64_t rv = std::min<int64_t>(MR, mc - p * MR);
+        for (int64_t l = 0; l < kc; ++l) {
+            for (int r = 0; r < rv; ++r) dst[l * MR + r] = opval(op, A, lda, i0 + p * MR + r, l0 + l);
+            for (int r = int(rv); r < MR; ++r) dst[l * MR + r] = T(0);
+        }
+    }
+}
+
+/// Bp[q][l][c] = op(B)(l0 + l, j0 + q NR + c), zero-padded columns
+template <typename T>
+inline void pack_b(Op op, T const* B, int64_t ldb, int64_t l0, int64_t kc, int64_t j0, int64_t nc, T* Bp) {
+    constexpr int NR = Blk<T>::NR;
+    const int64_t nq = (nc + NR - 1) / NR;
+    #pragma omp parallel for schedule(static) if (kc * nc > 32768)
+    for (int64_t q = 0; q < nq; ++q) {
+        T* dst = Bp + q * NR * kc;
+        const int64_t cv = std::min<int64_t>(NR, nc - q * NR);
+        for (int64_t l = 0; l < kc; ++l) {
+            for (int c = 0; c < cv; ++c) dst[l * NR + c] = opval(op, B, ldb, l0 + l, j0 + q * NR + c);
+            for (int c = int(cv); c < NR; ++c) dst[l * NR + c] = T(0);
+        }
+    }
+}
+
+/// C(mr x nr) += alpha Ap_panel Bp_panel over kc
+template <typename T>
+inline void micro(int64_t kc, T const* __restrict__ Ap, T const* __restrict__ Bp, T alpha, T* C, int64_t ldc,
+                  int mr, int nr) {
+    typedef typename VecT<T>::v V;
+    constexpr int W = VecT<T>::W, MR = Blk<T>::MR, NR = Blk<T>::NR;
+    V acc[2][NR];
+    for (int c = 0; c < NR; ++c) { acc[0][c] = V{} ; acc[1][c] = V{}; }
+    for (int64_t l = 0; l < kc; ++l) {
+        V a0, a1;
+        __builtin_memcpy(&a0, Ap + l * MR, sizeof(V));
+        __builtin_memcpy(&a1, Ap + l * MR + W, sizeof(V));
+        #pragma GCC unroll 6
+        for (int c = 0; c < NR; ++c) {
+            const T bv = Bp[l * NR + c];
+            V b;
+            for (int t = 0; t < W; ++t) b[t] = bv;
+            acc[0][c] += a0 * b;
+            acc[1][c] += a1 * b;
+        }
+    }
+    if (mr == MR && nr == NR) {
+        for (int c = 0; c < NR; ++c) {
+            T* cc = C + c * ldc;
+            for (int t = 0; t < W; ++t) { cc[t] += alpha * acc[0][c][t]; cc[W + t] += alpha * acc[1][c][t]; }
+        }
+        return;
+    }
+    for (int c = 0; c < nr; ++c) {
+        T* cc = C + c * ldc;
+        for (int r = 0; r < mr; ++r) cc[r] += alpha * (r < W ? acc[0][c][r] : acc[1][c][r - W]);
+    }
+}
+
+template <typename T>
+void gemm_packed(Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha, T const* A, int64_t lda, T const* B,
+                 int64_t ldb, T* C, int64_t ldc) {
+    using Bk = Blk<T>;
+    constexpr int MR = Bk::MR, NR = Bk::NR;
+    std::vector<T> Bp(size_t(Bk::KC) * size_t(((Bk::NC + NR - 1) / NR) * NR));
+    for (int64_t jc = 0; jc < n; jc += Bk::NC) {
+        const int64_t nc = std::min(Bk::NC, n - jc);
+        for (int64_t pc = 0; pc < k; pc += Bk::KC) {
+            const int64_t kc = std::min(Bk::KC, k - pc);
+            pack_b(opB, B, ldb, pc, kc, jc, nc, Bp.data());
+            const int64_t nic = (m + Bk::MC - 1) / Bk::MC;
+            #pragma omp parallel if (double(m) * nc * kc > 2e6)
+            {
+                std::vector<T> Ap(size_t(Bk::MC) * size_t(kc));
+                #pragma omp for schedule(dynamic)
+                for (int64_t ib = 0; ib < nic; ++ib) {
+                    const int64_t ic = ib * Bk::MC, mc = std::min(Bk::MC, m - ic);
+                    pack_a(opA, A, lda, ic, mc, pc, kc, Ap.data());
+                    for (int64_t jr = 0; jr < nc; jr += NR) {
+                        const int nr = int(std::min<int64_t>(NR, nc - jr));
+                        T const* bp = Bp.data() + (jr / NR) * NR * kc;
+                        for (int64_t ir = 0; ir < mc; ir += MR) {
+                            const int mr = int(std::min<int64_t>(MR, mc - ir));
+                            micro(kc, Ap.data() + (ir / MR) * MR * kc, bp, alpha, C + (ic + ir) + (jc + jr) * ldc,
+                                  ldc, mr, nr);
+                        }
+                    }
+                }
+            }
+        }
+    }
+}
+
+}  // namespace gemm_detail
+
 /// C = alpha op(A) op(B) + beta C
 template <typename T>
 void gemm(Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
           T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc)
 {
     if (m <= 0 || n <= 0) return;
+    if constexpr (std::is_same<T, double>::value || std::is_same<T, float>::value) {
+        if (double(m) * n * k >= 32768.0 && m >= 8 && n >= 6) {
+            #pragma omp parallel for schedule(static) if (m * n > 65536)
+            for (int64_t j = 0; j < n; ++j) {
+                T* c = C + j * ldc;
+                if (beta == T(0)) for (int64_t i = 0; i < m; ++i) c[i] = T(0);
+                else if (beta != T(1)) for (int64_t i = 0; i < m; ++i) c[i] *= beta;
+            }
+            if (alpha != T(0) && k > 0) gemm_detail::gemm_packed(opA, opB, m, n, k, alpha, A, lda, B, ldb, C, ldc);
+            return;
+        }
+    }
     std::vector<T> Ap, Bp;
     if (opA != Op::NoTrans && k > 0) { Ap.resize(size_t(m) * k); pack(opA, m, k, A, lda, Ap.data()); A = Ap.data(); lda = m; }
     if (opB != Op::NoTrans && k > 0) { Bp.resize(size_t(k) * n); pack(opB, k, n, B, ldb, Bp.data()); B = Bp.data(); ldb = k; }

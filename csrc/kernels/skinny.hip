@@ -184,11 +184,15 @@ void gemv_t_launch(int64_t m, int64_t k, int nr, T alpha, const T* A, int64_t ld
 }  // namespace
 
 // About 2048 workgroups in flight (8 per CU) unless the rows alone give that;
-// chunks of at least 256 columns.
+// chunks of at least 256 columns for the transposed form (a wave per row),
+// 32 for the row-per-lane form: the few-right-hand-side triangular solves of
+// mixed-precision refinement run it on tall m x 256 blocks (m = 32768: 128
+// workgroups walking 256 columns each, ~0.9 TB/s), where 8 column chunks
+// give 1024 workgroups.
 int gemv_chunks(char trans, int64_t m, int64_t k) {
     const int64_t row_blocks = trans == 'N' ? (m + GV_THREADS - 1) / GV_THREADS : (m + 3) / 4;
     int64_t want = (2048 + row_blocks - 1) / row_blocks;
-    want = std::min<int64_t>(want, std::max<int64_t>(1, k / 256));
+    want = std::min<int64_t>(want, std::max<int64_t>(1, k / (trans == 'N' ? 32 : 256)));
     return (int)std::max<int64_t>(1, std::min<int64_t>(want, 64));
 }
 
