@@ -49,10 +49,13 @@ class Block {
 public:
     explicit Block(const char* name);
     ~Block();
+    /// close the span before the end of the scope (once)
+    void end();
 private:
     const char* name_;
     double start_;
     bool active_;
+    bool ended_ = false;
 };
 
 /// RAII device span on a HIP queue (records timing events when tracing is on).

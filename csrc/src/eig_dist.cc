@@ -196,6 +196,7 @@ void stedc_dist(std::vector<R>& d, std::vector<R> const& e_in, Matrix<R>& Q, Opt
         // ---- z: row mid-1 of Q over [lo, mid) and row mid over [mid, hi)
         std::vector<double> z(n2, 0.0);
         {
+            trace::Block t3("stedc_m_z");
             LocalBlock<R> lq = Q.local(loc, false);
             auto grab = [&](int64_t grow, int64_t c0, int64_t c1, double scl) {
                 if (st.row_owner(grow / st.mb) != g.myrow()) return;
@@ -228,6 +229,7 @@ void stedc_dist(std::vector<R>& d, std::vector<R> const& e_in, Matrix<R>& Q, Opt
         std::vector<int64_t> rab;
         std::vector<double> rcs;
         {
+            trace::Block t3("stedc_m_deflate");
             const double eps = std::numeric_limits<R>::epsilon();
             double dmax = 0, zmax = 0;
             for (int64_t j = 0; j < n2; ++j) { dmax = std::max(dmax, std::abs(Ds[j])); zmax = std::max(zmax, std::abs(zs[j])); }
@@ -265,6 +267,7 @@ void stedc_dist(std::vector<R>& d, std::vector<R> const& e_in, Matrix<R>& Q, Opt
         const bool dev = c.dev();
         // device vector block: dd k | zz k | tau k | zh k | rcs 2 nrot ; ints: org k | act k | defl n2-k | ord n2 | inv n2 | rab 2 nrot
         const int64_t nrot = int64_t(rcs.size()) / 2;
+        trace::Block t3s("stedc_m_secular");
         if (dev) {
             dvec.resize(Target::Devices, size_t(4 * k + 2 * nrot + 1));
             divec.resize(Target::Devices, size_t(2 * k + 3 * n2 + 2 * nrot + 1));
@@ -284,6 +287,7 @@ void stedc_dist(std::vector<R>& d, std::vector<R> const& e_in, Matrix<R>& Q, Opt
         } else {
             secular_host(k, rho, dd, zz, org, tau, zh);
         }
+        t3s.end();
         std::vector<double> lam(n2);
         for (int64_t r = 0; r < k; ++r) lam[r] = dd[org[r]] + tau[r];
         for (int64_t cdx = 0; cdx < n2 - k; ++cdx) lam[k + cdx] = Ds[defl[cdx]];
@@ -292,6 +296,7 @@ void stedc_dist(std::vector<R>& d, std::vector<R> const& e_in, Matrix<R>& Q, Opt
         std::stable_sort(ord.begin(), ord.end(), [&](int64_t a, int64_t b) { return lam[a] < lam[b]; });
         for (int64_t s = 0; s < n2; ++s) inv_perm[perm[s]] = s;
         // ---- merge matrix: my local entries of the n2 x n2 block
+        trace::Block t3m("stedc_m_matrix");
         Matrix<R> Mb = M.sub(nd.t0, nd.t1 - 1, nd.t0, nd.t1 - 1);
         LocalBlock<R> lm = Mb.local(loc, true);
         slate_amd::dev::StedcMerge mg;
@@ -321,8 +326,10 @@ void stedc_dist(std::vector<R>& d, std::vector<R> const& e_in, Matrix<R>& Q, Opt
         } else {
             merge_matrix_host<R>(mg, dd, zh, tau, org, act, defl, ord, inv_perm, rab, rcs, lm.n, lm.ptr, lm.ld);
         }
+        t3m.end();
         // ---- Q_new = [Q1 0; 0 Q2] M  (two GEMMs on the halves), back into Q
         {
+            trace::Block t3("stedc_m_gemm");
             Matrix<R> Q1 = Q.sub(nd.t0, nd.tm - 1, nd.t0, nd.tm - 1), Q2 = Q.sub(nd.tm, nd.t1 - 1, nd.tm, nd.t1 - 1);
             Matrix<R> Mt = M.sub(nd.t0, nd.tm - 1, nd.t0, nd.t1 - 1), Mbot = M.sub(nd.tm, nd.t1 - 1, nd.t0, nd.t1 - 1);
             Matrix<R> Ct = Qb.sub(nd.t0, nd.tm - 1, nd.t0, nd.t1 - 1), Cb = Qb.sub(nd.tm, nd.t1 - 1, nd.t0, nd.t1 - 1);

@@ -222,7 +222,11 @@ Block::Block(const char* name) : name_(name), start_(0), active_(Trace::is_on())
     if (debug_calls()) std::fprintf(stderr, "[rank %d] > %s\n", debug_rank(), name);
 }
 
-Block::~Block() {
+Block::~Block() { end(); }
+
+void Block::end() {
+    if (ended_) return;
+    ended_ = true;
     if (debug_calls()) std::fprintf(stderr, "[rank %d] < %s\n", debug_rank(), name_);
     if (!active_) return;
     Event e{};
