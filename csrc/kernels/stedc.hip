@@ -4,9 +4,10 @@
 //
 // One merge of two halves (n2 = n1 + (n2 - n1) columns of Q) on the rank-one
 // modified system D + rho z z^T after sorting and deflation (host, O(n2)):
-//   * secular_roots: one thread per non-deflated root j, bisection to full
-//     relative precision of tau_j = lambda_j - dd[org_j] (distance to the
-//     nearest pole), which the Gu-Eisenstat vectors need;
+//   * secular_roots: one thread per non-deflated root j, the rational
+//     iteration of slate_amd/secular.hh to full relative precision of
+//     tau_j = lambda_j - dd[org_j] (distance to the nearest pole), which the
+//     Gu-Eisenstat vectors need;
 //   * gu_eisenstat_z: z recomputed from the computed roots, one thread per i;
 //   * merge_matrix: every rank builds ONLY its local entries of the n2 x n2
 //     merge matrix M (Q_new = Q_old M): per output column one workgroup forms
@@ -17,40 +18,21 @@
 //     MFMA GEMM; no n x n matrix exists on any host.
 #include "device_common.hh"
 #include "kernels.hh"
+#include "slate_amd/secular.hh"
 
 namespace slate_amd {
 namespace dev {
 
 namespace {
 
-__device__ inline double secular_f(int64_t k, double rho, const double* dd, const double* zz, int64_t o2, double t) {
-    double sum = 0;
-    const double d0 = dd[o2];
-    for (int64_t i = 0; i < k; ++i) sum += zz[i] * zz[i] / ((dd[i] - d0) - t);
-    return 1.0 + rho * sum;
-}
-
 __global__ __launch_bounds__(64) void secular_roots_kernel(int64_t k, double rho, const double* dd, const double* zz,
                                                            double znorm2, int64_t* org, double* tau) {
     const int64_t j = blockIdx.x * 64 + threadIdx.x;
     if (j >= k) return;
-    const double eps = 2.220446049250313e-16;
-    const double lo_abs = dd[j];
-    const double hi_abs = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2;
-    const double mid = (hi_abs - lo_abs) / 2;
     int64_t o2 = j;
-    double a = 0, b = mid;
-    if (j + 1 < k && secular_f(k, rho, dd, zz, j, mid) < 0) { o2 = j + 1; a = -mid; b = 0; }
-    else if (j + 1 >= k) { a = 0; b = hi_abs - lo_abs; }
-    for (int it = 0; it < 400; ++it) {
-        const double t = (a + b) / 2;
-        if (t == a || t == b) break;
-        const double fv = secular_f(k, rho, dd, zz, o2, t);
-        if (fv > 0) b = t; else a = t;
-        if (fabs(b - a) <= 2 * eps * fmin(fabs(a), fabs(b))) break;
-    }
+    const double t = slate::secular::root<double>(k, j, rho, dd, zz, znorm2, &o2);
     org[j] = o2;
-    tau[j] = (a + b) / 2;
+    tau[j] = t;
 }
 
 __global__ __launch_bounds__(64) void gu_eisenstat_kernel(int64_t k, double rho, const double* dd, const double* zz,

@@ -27,6 +27,7 @@
 #include "internal.hh"
 #include "eig_sinks.hh"
 #include "slate_amd/eig_host.hh"
+#include "slate_amd/secular.hh"
 #include "../kernels/kernels.hh"
 
 #include <algorithm>
@@ -92,30 +93,14 @@ void merge_matrix_host(slate_amd::dev::StedcMerge const& m, std::vector<double> 
 /// secular roots + Gu-Eisenstat z on the host (same algorithm as the kernels)
 void secular_host(int64_t k, double rho, std::vector<double> const& dd, std::vector<double> const& zz,
                   std::vector<int64_t>& org, std::vector<double>& tau, std::vector<double>& zh) {
-    const double eps = std::numeric_limits<double>::epsilon();
     double znorm2 = 0;
     for (int64_t i = 0; i < k; ++i) znorm2 += zz[i] * zz[i];
     org.assign(k, 0); tau.assign(k, 0.0); zh.assign(k, 0.0);
-    auto f = [&](int64_t o2, double t) {
-        double sum = 0;
-        for (int64_t i = 0; i < k; ++i) sum += zz[i] * zz[i] / ((dd[i] - dd[o2]) - t);
-        return 1.0 + rho * sum;
-    };
     #pragma omp parallel for schedule(dynamic, 8) if (k > 64)
     for (int64_t j = 0; j < k; ++j) {
-        const double lo = dd[j], hi = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2, mid = (hi - lo) / 2;
         int64_t o2 = j;
-        double a = 0, b = mid;
-        if (j + 1 < k && f(j, mid) < 0) { o2 = j + 1; a = -mid; b = 0; }
-        else if (j + 1 >= k) { a = 0; b = hi - lo; }
-        for (int it = 0; it < 400; ++it) {
-            const double t = (a + b) / 2;
-            if (t == a || t == b) break;
-            if (f(o2, t) > 0) b = t; else a = t;
-            if (std::abs(b - a) <= 2 * eps * std::min(std::abs(a), std::abs(b))) break;
-        }
+        tau[j] = secular::root<double>(k, j, rho, dd.data(), zz.data(), znorm2, &o2);
         org[j] = o2;
-        tau[j] = (a + b) / 2;
     }
     #pragma omp parallel for schedule(static) if (k > 256)
     for (int64_t i = 0; i < k; ++i) {

@@ -1,6 +1,7 @@
 // Host stages of the two-stage eigen/SVD reductions (see eig_host.hh).
 #include "slate_amd/eig_host.hh"
 #include "slate_amd/host_blas.hh"
+#include "slate_amd/secular.hh"
 #include "slate_amd/exception.hh"
 
 #include <algorithm>
@@ -44,6 +45,25 @@ inline void wait_progress(std::atomic<int64_t> const& p, int64_t want) {
 
 template <typename T> inline T cj(T x) { return x; }
 template <typename R> inline std::complex<R> cj(std::complex<R> x) { return std::conj(x); }
+
+/// sum_i conj(v[i]) x[i] with 16 independent partial sums: without
+/// -ffast-math the compiler keeps a plain `s += ...` loop as ONE dependent
+/// FMA chain (4 cycles a term), which made the bulge chase's dot products --
+/// tb2bd's left update, hb2st's hemv -- latency-bound at ~1 GFLOP/s (tb2bd
+/// 24 -> 9 us a step single-threaded with the split sums).
+template <typename T>
+inline T dotc(int64_t L, const T* __restrict__ v, const T* __restrict__ x) {
+    constexpr int U = 16;
+    T acc[U] = {};
+    int64_t i = 0;
+    for (; i + U <= L; i += U)
+        for (int u = 0; u < U; ++u) acc[u] += cj(v[i + u]) * x[i + u];
+    T s = T(0);
+    for (; i < L; ++i) s += cj(v[i]) * x[i];
+    for (int u = 0; u < U / 2; ++u) acc[u] += acc[u + U / 2];
+    for (int u = 0; u < U / 4; ++u) acc[u] += acc[u + U / 4];
+    return s + ((acc[0] + acc[2]) + (acc[1] + acc[3]));
+}
 
 /// One Givens rotation (c, s) on columns (i, i+1) of a row-major-agnostic
 /// column-major matrix: [x y] <- [c*x - s*y, s*x + c*y].
@@ -90,9 +110,7 @@ void Reflectors<T>::apply_left(bool trans, int64_t ncols, T* C, int64_t ldc) con
             int64_t o = off[k], L = len[k];
             for (int64_t j = c0; j < c1; ++j) {
                 T* cc = C + o + j * ldc;
-                T s = T(0);
-                for (int64_t i = 0; i < L; ++i) s += cj(vk[i]) * cc[i];
-                s *= tk;
+                T s = dotc(L, vk, cc) * tk;
                 for (int64_t i = 0; i < L; ++i) cc[i] -= vk[i] * s;
             }
         }
@@ -124,9 +142,7 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
         // (d)
         for (int64_t c = k + 1; c < s0; ++c) {
             T* __restrict__ col = &a(s0, c);
-            T sum = T(0);
-            for (int64_t i = 0; i < L; ++i) sum += cj(v[i]) * col[i];
-            sum *= ctau;
+            const T sum = dotc(L, v, col) * ctau;
             for (int64_t i = 0; i < L; ++i) col[i] -= v[i] * sum;
         }
         // (b)
@@ -134,15 +150,12 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
         for (int64_t l = 0; l < L; ++l) {
             const T* __restrict__ col = &a(s0, s0 + l);
             const T vl = v[l];
-            T acc = T(std::real(col[l])) * vl;
-            for (int64_t i = l + 1; i < L; ++i) {
-                w[i] += col[i] * vl;
-                acc += cj(col[i]) * v[i];
-            }
-            w[l] += acc;
+            for (int64_t i = l + 1; i < L; ++i) w[i] += col[i] * vl;
+            // sum_i conj(col[i]) v[i] = conj(sum_i conj(v[i]) col[i])
+            w[l] += T(std::real(col[l])) * vl + cj(dotc(L - l - 1, v + l + 1, col + l + 1));
         }
-        T vx = T(0);
-        for (int64_t i = 0; i < L; ++i) { w[i] *= tau; vx += cj(v[i]) * w[i]; }
+        for (int64_t i = 0; i < L; ++i) w[i] *= tau;
+        const T vx = dotc(L, v, w);
         const T alpha = T(-0.5) * ctau * vx;
         for (int64_t i = 0; i < L; ++i) w[i] += alpha * v[i];
         for (int64_t l = 0; l < L; ++l) {
@@ -257,19 +270,50 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         int64_t w0 = std::max<int64_t>(0, c0 - b), w1 = std::min<int64_t>(m - 1, c0 + L - 1);
         const int64_t nr = w1 - w0 + 1;
         if (nr <= 0) return;
+        // four columns per pass: w is loaded / stored once per four
+        // column FMAs instead of once per column (the passes were
+        // load/store-bound on w)
         std::fill(w, w + nr, T(0));
-        for (int64_t t = 0; t < L; ++t) {
-            const T* col = &a(w0, c0 + t);
+        int64_t t = 0;
+        for (; t + 4 <= L; t += 4) {
+            const T* __restrict__ x0 = &a(w0, c0 + t);
+            const T* __restrict__ x1 = x0 + lda;
+            const T* __restrict__ x2 = x1 + lda;
+            const T* __restrict__ x3 = x2 + lda;
+            const T v0 = v[t], v1 = v[t + 1], v2 = v[t + 2], v3 = v[t + 3];
+            for (int64_t i = 0; i < nr; ++i) w[i] += (x0[i] * v0 + x1[i] * v1) + (x2[i] * v2 + x3[i] * v3);
+        }
+        for (; t < L; ++t) {
+            const T* __restrict__ col = &a(w0, c0 + t);
             const T vt = v[t];
             for (int64_t i = 0; i < nr; ++i) w[i] += col[i] * vt;
         }
         const bool skip = (r >= w0 && r <= w1);
-        for (int64_t t = 0; t < L; ++t) {
-            T* col = &a(w0, c0 + t);
-            const T f = tau * cj(v[t]);
-            const T keep = skip ? col[r - w0] : T(0);  // row r is excluded
-            for (int64_t i = 0; i < nr; ++i) col[i] -= w[i] * f;
-            if (skip) col[r - w0] = keep;
+        T keep[4];
+        for (t = 0; t < L; t += 4) {
+            const int64_t nt = std::min<int64_t>(4, L - t);
+            if (skip) for (int64_t u = 0; u < nt; ++u) keep[u] = a(r, c0 + t + u);  // row r is excluded
+            if (nt == 4) {
+                T* __restrict__ x0 = &a(w0, c0 + t);
+                T* __restrict__ x1 = x0 + lda;
+                T* __restrict__ x2 = x1 + lda;
+                T* __restrict__ x3 = x2 + lda;
+                const T f0 = tau * cj(v[t]), f1 = tau * cj(v[t + 1]), f2 = tau * cj(v[t + 2]), f3 = tau * cj(v[t + 3]);
+                for (int64_t i = 0; i < nr; ++i) {
+                    const T wi = w[i];
+                    x0[i] -= wi * f0;
+                    x1[i] -= wi * f1;
+                    x2[i] -= wi * f2;
+                    x3[i] -= wi * f3;
+                }
+            } else {
+                for (int64_t u = 0; u < nt; ++u) {
+                    T* __restrict__ col = &a(w0, c0 + t + u);
+                    const T f = tau * cj(v[t + u]);
+                    for (int64_t i = 0; i < nr; ++i) col[i] -= w[i] * f;
+                }
+            }
+            if (skip) for (int64_t u = 0; u < nt; ++u) a(r, c0 + t + u) = keep[u];
         }
     };
     auto left = [&](int64_t c, int64_t r0, int64_t L, T tau, const T* v) {
@@ -279,10 +323,9 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
         int64_t w0 = r0, w1 = std::min<int64_t>(n - 1, r0 + L - 1 + b);
         for (int64_t jj = w0; jj <= w1; ++jj) {
             if (jj == c) continue;
-            T s = T(0);
-            for (int64_t t = 0; t < L; ++t) s += cj(v[t]) * a(r0 + t, jj);
-            s *= cj(tau);
-            if (s != T(0)) for (int64_t t = 0; t < L; ++t) a(r0 + t, jj) -= v[t] * s;
+            T* __restrict__ col = &a(r0, jj);
+            const T s = dotc(L, v, col) * cj(tau);
+            if (s != T(0)) for (int64_t t = 0; t < L; ++t) col[t] -= v[t] * s;
         }
     };
     // Sweeps pipelined over threads as in hb2st: step t of sweep j touches
@@ -581,7 +624,6 @@ int64_t stedc_deflate(int64_t n, R rho, R* D, R* z, R* Qp, int64_t ldqp, char* d
 template <typename R>
 void stedc_secular(int64_t k, R rho, R const* dd, R const* zz, R* lam, R* U, int64_t ldu) {
     if (k <= 0) return;
-    const R eps = std::numeric_limits<R>::epsilon();
     R znorm2 = 0;
     for (int64_t i = 0; i < k; ++i) znorm2 += zz[i] * zz[i];
     // roots: lambda_j = dd[org[j]] + tau[j], tau relative to the closer pole
@@ -589,29 +631,9 @@ void stedc_secular(int64_t k, R rho, R const* dd, R const* zz, R* lam, R* U, int
     std::vector<R> tau(k);
     #pragma omp parallel for schedule(dynamic, 8) if (k > 64)
     for (int64_t j = 0; j < k; ++j) {
-        R lo_abs = dd[j];
-        R hi_abs = (j + 1 < k) ? dd[j + 1] : dd[j] + rho * znorm2;
-        auto sec = [&](int64_t o2, R t) {   // f(dd[o2] + t)
-            R sum = 0;
-            for (int64_t i = 0; i < k; ++i) sum += zz[i] * zz[i] / ((dd[i] - dd[o2]) - t);
-            return R(1) + rho * sum;
-        };
-        R mid = (hi_abs - lo_abs) / R(2);
         int64_t o2 = j;
-        R a = 0, b = mid;
-        if (j + 1 < k && sec(j, mid) < R(0)) { o2 = j + 1; a = -mid; b = 0; }
-        else if (j + 1 >= k) { a = 0; b = hi_abs - lo_abs; }
-        // bisection to full relative precision of t (the distance to the
-        // nearest pole), which the Gu-Eisenstat vectors need
-        for (int it = 0; it < 400; ++it) {
-            R t = (a + b) / R(2);
-            if (t == a || t == b) break;
-            R fv = sec(o2, t);
-            if (fv > R(0)) b = t; else a = t;
-            if (std::abs(b - a) <= R(2) * eps * std::min(std::abs(a), std::abs(b))) break;
-        }
+        tau[j] = secular::root<R>(k, j, rho, dd, zz, znorm2, &o2);
         org[j] = o2;
-        tau[j] = (a + b) / R(2);
     }
     // Gu-Eisenstat: recompute z from the computed roots
     auto lam_minus_d = [&](int64_t j, int64_t i) { return (dd[org[j]] - dd[i]) + tau[j]; };

@@ -55,7 +55,7 @@ for r in routines:
             s.trace.clear()
             flops = (4.0 / 3.0 + 4.0) * n ** 3 if r == "heev" else 22.0 * n ** 3   # LAPACK-style op counts
             print(f"{r} n={n} nb={nb} {tg}: {dt:.3f} s  ({flops / dt / 1e9:.1f} GF/s nominal)", flush=True)
-            for k, v in list(st.items())[:22]:
+            for k, v in list(st.items())[:30]:
                 print(f"    {k:28s} {v:10.1f} ms", flush=True)
     if r == "heev":
         zz = s.to_numpy(Z)
