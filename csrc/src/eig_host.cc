@@ -5,6 +5,7 @@
 #include "slate_amd/exception.hh"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cmath>
 #include <complex>
 #include <limits>
@@ -40,6 +41,81 @@ inline void wait_progress(std::atomic<int64_t> const& p, int64_t want) {
     for (int spin = 0; p.load(std::memory_order_acquire) < want; ++spin) {
         if (spin < 256) _mm_pause();
         else std::this_thread::yield();
+    }
+}
+
+/// Sweeps per thread of the pipelined bulge chases (SLATE_SWEEP_GROUP;
+/// n = 8192, 16 threads: hb2st 585 / 517 / 584 ms and tb2bd 934 / 690 / 979
+/// ms at 1 / 2 / 4, profiles/r4_sweep_group.txt).
+int64_t sweep_group() {
+    static const int64_t g = [] {
+        const char* s = std::getenv("SLATE_SWEEP_GROUP");
+        const long v = s ? std::atol(s) : 0;
+        return int64_t(v > 0 ? std::min(v, 64L) : 2);
+    }();
+    return g;
+}
+
+/// The bulge chases' pipeline: nsw sweeps, sweep j's step t may run once
+/// sweep j-1 has finished kLag steps more (progress counters).  Each thread
+/// takes GROUPS of G consecutive sweeps and advances them as a wavefront
+/// (sweep g of the group kLag steps behind sweep g-1): step t of sweep j+1
+/// rewrites the window sweep j left kLag steps earlier, so with the two on
+/// one core the window is still in its L2, where handing every sweep to the
+/// next thread (the previous scheme) moved the whole window between cores
+/// each step -- 3x the single-thread cost of a step at 8 threads.  Only a
+/// group's first sweep waits on another thread.  init(j) -> state;
+/// step(state&, tid) -> false once the sweep has ended.
+template <typename Init, typename Step>
+void pipelined_sweeps(int64_t nsw, int64_t kLag, bool par, Init init, Step step) {
+    using State = decltype(init(int64_t(0)));
+    constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
+    std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
+    for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
+    const int64_t G = sweep_group();
+    const int64_t ngroups = (nsw + G - 1) / G;
+    #pragma omp parallel if (par)
+    {
+        const int nth = par ? omp_get_num_threads() : 1, tid = par ? omp_get_thread_num() : 0;
+        std::vector<State> st;
+        std::vector<int64_t> t;
+        std::vector<char> done;
+        // round-robin groups: the sweep before a group is always owned by
+        // another running thread (or finished earlier by this one)
+        for (int64_t gi = tid; gi < ngroups; gi += nth) {
+            const int64_t j0 = gi * G, ng = std::min(G, nsw - j0);
+            st.clear();
+            for (int64_t g = 0; g < ng; ++g) st.push_back(init(j0 + g));
+            t.assign(size_t(ng), 0);
+            done.assign(size_t(ng), 0);
+            int64_t left = ng;
+            while (left > 0) {
+                // latest sweep first: the next group waits on the last one,
+                // so it gets started after ~kLag steps per sweep of this
+                // group rather than kLag ROUNDS of all of them
+                bool moved = false;
+                for (int64_t g = ng - 1; g >= 0 && !moved; --g) {
+                    if (done[g]) continue;
+                    const int64_t j = j0 + g;
+                    if (j > 0 && prog[j - 1].load(std::memory_order_acquire) < t[g] + kLag) continue;
+                    const bool more = step(st[g], tid);
+                    ++t[g];
+                    moved = true;
+                    if (more) {
+                        prog[j].store(t[g], std::memory_order_release);
+                    } else {
+                        prog[j].store(kDone, std::memory_order_release);
+                        done[g] = 1;
+                        --left;
+                    }
+                }
+                if (!moved) {
+                    int64_t g = 0;
+                    while (done[g]) ++g;
+                    wait_progress(prog[j0 + g - 1], t[g] + kLag);
+                }
+            }
+        }
     }
 }
 
@@ -193,46 +269,36 @@ void hb2st(int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real_type<T>>& 
     // sweeps that ran out of order act on disjoint rows and commute.
     const int64_t nsw = (b > 1 && n > 2) ? n - 2 : 0;
     constexpr int64_t kLag = 3;
-    constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
-    std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
-    for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
     std::vector<Reflectors<T>> Qs(nsw);
-    auto sweep = [&](int64_t j, T* v, T* w) {
-        int64_t k = j, s0 = j + 1, s1 = std::min(j + b, n - 1);
-        for (int64_t t = 0;; ++t) {
-            if (j > 0) {
-                wait_progress(prog[j - 1], t + kLag);
-            }
-            int64_t L = s1 - s0 + 1;
-            if (L < 2) break;
-            T alpha = a(s0, k);
-            for (int64_t i = 1; i < L; ++i) v[i] = a(s0 + i, k);
+    struct St { int64_t j, k, s0, s1; };
+    const bool par = nsw >= 64 && n >= 8 * b;
+    std::vector<std::vector<T>> vs(size_t(par ? omp_get_max_threads() : 1)), ws(vs.size());
+    for (auto& x : vs) x.resize(size_t(b + 1));
+    for (auto& x : ws) x.resize(size_t(n));
+    pipelined_sweeps(nsw, kLag, par,
+        [&](int64_t j) { return St{j, j, j + 1, std::min(j + b, n - 1)}; },
+        [&](St& q, int tid) {
+            T* v = vs[tid].data();
+            T* w = ws[tid].data();
+            const int64_t L = q.s1 - q.s0 + 1;
+            if (L < 2) return false;
+            T alpha = a(q.s0, q.k);
+            for (int64_t i = 1; i < L; ++i) v[i] = a(q.s0 + i, q.k);
             T tau;
             larfg(L, alpha, v + 1, 1, tau);
             v[0] = T(1);
-            a(s0, k) = alpha;
-            for (int64_t i = 1; i < L; ++i) a(s0 + i, k) = T(0);
+            a(q.s0, q.k) = alpha;
+            for (int64_t i = 1; i < L; ++i) a(q.s0 + i, q.k) = T(0);
             if (tau != T(0)) {
-                two_sided(k, s0, L, tau, v, w);
-                Qs[j].push(s0, L, tau, v, j);
+                two_sided(q.k, q.s0, L, tau, v, w);
+                Qs[q.j].push(q.s0, L, tau, v, q.j);
             }
-            prog[j].store(t + 1, std::memory_order_release);
             // next bulge: column s0 below its band
-            int64_t ns0 = s0 + b, ns1 = std::min(s1 + b, n - 1);
-            if (ns0 >= n - 1 || ns1 <= ns0) break;
-            k = s0; s0 = ns0; s1 = ns1;
-        }
-        prog[j].store(kDone, std::memory_order_release);
-    };
-    const bool par = nsw >= 64 && n >= 8 * b;
-    #pragma omp parallel if (par)
-    {
-        std::vector<T> v(b + 1), w(n);
-        const int nth = par ? omp_get_num_threads() : 1, tid = par ? omp_get_thread_num() : 0;
-        // round-robin: sweep j-1 is always owned by another running thread (or
-        // finished earlier by this one), so every wait terminates
-        for (int64_t j = tid; j < nsw; j += nth) sweep(j, v.data(), w.data());
-    }
+            const int64_t ns0 = q.s0 + b, ns1 = std::min(q.s1 + b, n - 1);
+            if (ns0 >= n - 1 || ns1 <= ns0) return false;
+            q.k = q.s0; q.s0 = ns0; q.s1 = ns1;
+            return true;
+        });
     for (auto& q : Qs) {
         for (size_t r = 0; r < q.size(); ++r) Q.push(q.off[r], q.len[r], q.tau[r], q.v.data() + q.voff[r], q.tag[r]);
         q = Reflectors<T>();
@@ -339,18 +405,20 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
     // in sweep order (out-of-order ones commute).
     const int64_t nsw = n > 1 ? n - 1 : 0;
     constexpr int64_t kLag = 3;
-    constexpr int64_t kDone = std::numeric_limits<int64_t>::max();
-    std::unique_ptr<std::atomic<int64_t>[]> prog(new std::atomic<int64_t>[std::max<int64_t>(nsw, 1)]);
-    for (int64_t j = 0; j < nsw; ++j) prog[j].store(0, std::memory_order_relaxed);
     std::vector<Reflectors<T>> QUs(nsw), QVs(nsw);
-    auto sweep = [&](int64_t j, T* v, T* w) {
-        int64_t r = j, c0 = j + 1, c1 = std::min(j + b, n - 1);
-        for (int64_t st = 0;; ++st) {
-            if (j > 0) {
-                wait_progress(prog[j - 1], st + kLag);
-            }
+    struct St { int64_t j, r, c0, c1; };
+    const bool par = nsw >= 64 && n >= 8 * b;
+    std::vector<std::vector<T>> vs(size_t(par ? omp_get_max_threads() : 1)), ws(vs.size());
+    for (auto& x : vs) x.resize(size_t(b + 1));
+    for (auto& x : ws) x.resize(size_t(std::max<int64_t>(m, 1)));
+    pipelined_sweeps(nsw, kLag, par,
+        [&](int64_t j) { return St{j, j, j + 1, std::min(j + b, n - 1)}; },
+        [&](St& q, int tid) {
+            T* v = vs[tid].data();
+            T* w = ws[tid].data();
+            const int64_t j = q.j, r = q.r, c0 = q.c0, c1 = q.c1;
             // right reflector: row r, columns [c0, c1]
-            int64_t L = c1 - c0 + 1;
+            const int64_t L = c1 - c0 + 1;
             if (L >= 2) {
                 T alpha = cj(a(r, c0));
                 for (int64_t t = 1; t < L; ++t) v[t] = cj(a(r, c0 + t));
@@ -362,8 +430,8 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
                 if (tau != T(0)) { right(r, c0, L, tau, v, w); QVs[j].push(c0, L, tau, v, j); }
             }
             // left reflector: column c0, rows [c0, min(c1, m-1)]
-            int64_t r1 = std::min(c1, m - 1);
-            int64_t Ll = r1 - c0 + 1;
+            const int64_t r1 = std::min(c1, m - 1);
+            const int64_t Ll = r1 - c0 + 1;
             if (Ll >= 2) {
                 T alpha = a(c0, c0);
                 for (int64_t t = 1; t < Ll; ++t) v[t] = a(c0 + t, c0);
@@ -374,21 +442,12 @@ void tb2bd(int64_t m, int64_t n, int64_t kd, T* A, int64_t lda, std::vector<real
                 for (int64_t t = 1; t < Ll; ++t) a(c0 + t, c0) = T(0);
                 if (tau != T(0)) { left(c0, c0, Ll, tau, v); QUs[j].push(c0, Ll, tau, v, j); }
             }
-            prog[j].store(st + 1, std::memory_order_release);
             // next: row c0 beyond its band, columns [c0 + b, c1 + b]
-            int64_t nc0 = c0 + b, nc1 = std::min(c1 + b, n - 1);
-            if (nc0 >= n - 1 || nc1 <= nc0) break;
-            r = c0; c0 = nc0; c1 = nc1;
-        }
-        prog[j].store(kDone, std::memory_order_release);
-    };
-    const bool par = nsw >= 64 && n >= 8 * b;
-    #pragma omp parallel if (par)
-    {
-        std::vector<T> v(b + 1), w(size_t(std::max<int64_t>(m, 1)));
-        const int nth = par ? omp_get_num_threads() : 1, tid = par ? omp_get_thread_num() : 0;
-        for (int64_t j = tid; j < nsw; j += nth) sweep(j, v.data(), w.data());
-    }
+            const int64_t nc0 = c0 + b, nc1 = std::min(c1 + b, n - 1);
+            if (nc0 >= n - 1 || nc1 <= nc0) return false;
+            q.r = c0; q.c0 = nc0; q.c1 = nc1;
+            return true;
+        });
     for (int64_t j = 0; j < nsw; ++j) {
         for (size_t q = 0; q < QVs[j].size(); ++q)
             QV.push(QVs[j].off[q], QVs[j].len[q], QVs[j].tau[q], QVs[j].v.data() + QVs[j].voff[q], j);

@@ -1060,7 +1060,46 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         int64_t jla_end = std::min(nt, k + 1 + la);
         for (int64_t j = k + 1; j < jla_end; ++j)
             range_tasks(device::kLookaheadQueue, j, j + 1);
-        if (jla_end < nt) range_tasks(device::kTrailQueue, jla_end, nt);
+        // 1x1 device grid: the trailing range in two parts, A (the first
+        // 1/split_div of it) on the trailing queue and B on the idle comm
+        // queue, B starting once A's row interchanges and U rows are done.
+        // The interchanges are memory-bound scattered-row gathers (one 128-byte
+        // line per moved element: ~3 ms a step at n = 65536) that otherwise
+        // serialize before the one trailing GEMM; here only A's are exposed,
+        // B's run under A's GEMM.  SLATE_LU_TRAIL_SPLIT = split_div (0: off).
+        static const int64_t split_div = [] {
+            const char* e = std::getenv("SLATE_LU_TRAIL_SPLIT");
+            return e ? std::atoll(e) : int64_t(8);
+        }();
+        const int64_t nrest = nt - jla_end;
+        if (nrest >= 2 && split_div > 0 && q == 1 && target == Target::Devices && pivot) {
+            const int64_t ja = jla_end + std::max<int64_t>(1, nrest / split_div);
+            const int64_t tA = Sched::tok(16, slot);
+            std::vector<int64_t> colsA, colsB;
+            for (int64_t j = jla_end; j < ja; ++j) colsA.push_back(Sched::col(j));
+            for (int64_t j = ja; j < nt; ++j) colsB.push_back(Sched::col(j));
+            std::vector<int64_t> in = {tBc, tL, tPV};
+            if (use_linv) in.push_back(tLi);
+            if (use_tn && mloc > lr_k1) in.push_back(tLt);
+            std::vector<int64_t> outA = colsA;
+            outA.push_back(tA);
+            S.task(device::kTrailQueue, in, outA, [&, jla_end, ja](lb::Ctx const& c) {
+                auto cc = lcols(jla_end, ja);
+                permute(c, cc.first, cc.second);
+                urow(c, jla_end, ja);
+            });
+            S.task(device::kTrailQueue, in, colsA, [&, jla_end, ja](lb::Ctx const& c) { update(c, jla_end, ja); });
+            std::vector<int64_t> inB = in;
+            inB.push_back(tA);
+            S.task(device::kCommQueue, inB, colsB, [&, ja](lb::Ctx const& c) {
+                auto cc = lcols(ja, nt);
+                permute(c, cc.first, cc.second);
+                urow(c, ja, nt);
+                update(c, ja, nt);
+            });
+        } else if (jla_end < nt) {
+            range_tasks(device::kTrailQueue, jla_end, nt);
+        }
 
         if (k > 0 && pivot) {
             // reads PV[pvs] (tPV): the panel that next rewrites the slot, RP

@@ -609,7 +609,16 @@ void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int
         const char* e = std::getenv("SLATE_POTRF_BLOCKED");
         return e ? std::atoi(e) != 0 : true;
     }();
-    if (uplo == Uplo::Lower && blocked) {
+    // Above rec_max columns the recursive split below runs first (its trsm /
+    // herk at the top levels are large GEMMs), the blocked 64-column sweep
+    // only on the blocks of at most rec_max: the 1x1 potrf's tail (8192
+    // columns, potrf.cc) as one 128-leaf sweep ran its rank-64 updates at
+    // ~9 TFLOP/s.  SLATE_POTRF_REC_MAX (0: always blocked).
+    static const int64_t rec_max = [] {
+        const char* e = std::getenv("SLATE_POTRF_REC_MAX");
+        return e ? std::atoll(e) : int64_t(1024);
+    }();
+    if (uplo == Uplo::Lower && blocked && (rec_max <= 0 || n <= rec_max)) {
         // Right-looking over 64-column leaves, four launches per leaf: the
         // leaf's factor and its inverse in one kernel, the rows below as one
         // GEMM with the inverse (into Y), the trailing triangle as one

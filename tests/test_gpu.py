@@ -217,7 +217,7 @@ def test_trsm_small_kernel(dtype, uplo, diag, m, nr):
     assert relerr(te @ x, b) < (1e-13 if dtype == np.float64 else 1e-5)
 
 
-@pytest.mark.parametrize("n", [64, 200, 512, 1000])
+@pytest.mark.parametrize("n", [64, 200, 512, 1000, 2500])
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_potrf_kernel(n, uplo):
     torch = _torch()
@@ -233,13 +233,15 @@ def test_potrf_kernel(n, uplo):
         assert info == 0 and relerr(U.T @ U, a) < 1e-13
 
 
-def test_potrf_kernel_not_spd():
+@pytest.mark.parametrize("n,bad", [(200, 150), (2500, 2100)])
+def test_potrf_kernel_not_spd(n, bad):
+    # n = 2500: the failure sits in a recursive split's second half
     torch = _torch()
-    a = s.utils.spd_matrix(200)
-    a[150, 150] = -1e6
+    a = s.utils.spd_matrix(n)
+    a[bad, bad] = -1e6
     tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
     info = s.ops.potrf("L", tA)
-    assert info == 151
+    assert info == bad + 1
 
 
 @pytest.mark.parametrize("m,n", [(1000, 64), (4096, 256), (777, 100), (512, 512)])
@@ -395,7 +397,7 @@ def test_matgen_kinds_device_match_host(kind, dtype):
 
 
 @pytest.mark.parametrize("dtype", DTYPES)
-@pytest.mark.parametrize("mn", [(700, 700), (900, 500), (500, 900)])
+@pytest.mark.parametrize("mn", [(700, 700), (900, 500), (500, 900), (1500, 1300)])
 def test_getrf_driver_device(dtype, mn):
     m, n = mn
     nb = 128
