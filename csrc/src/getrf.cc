@@ -1066,10 +1066,14 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
         // The interchanges are memory-bound scattered-row gathers (one 128-byte
         // line per moved element: ~3 ms a step at n = 65536) that otherwise
         // serialize before the one trailing GEMM; here only A's are exposed,
-        // B's run under A's GEMM.  SLATE_LU_TRAIL_SPLIT = split_div (0: off).
+        // B's run under A's GEMM.  SLATE_LU_TRAIL_SPLIT = split_div (0: off,
+        // the default: same-box n = 65536 dgetrf 54.8 TFLOP/s unsplit against
+        // 53.4-53.8 at 4 / 8 / 16, dgesv_mixed neutral -- two concurrent
+        // trailing GEMMs lose more than the hidden interchanges gain;
+        // profiles/r4_lu_split_potrf_rec.txt).
         static const int64_t split_div = [] {
             const char* e = std::getenv("SLATE_LU_TRAIL_SPLIT");
-            return e ? std::atoll(e) : int64_t(8);
+            return e ? std::atoll(e) : int64_t(0);
         }();
         const int64_t nrest = nt - jla_end;
         if (nrest >= 2 && split_div > 0 && q == 1 && target == Target::Devices && pivot) {

@@ -613,10 +613,13 @@ void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int
     // herk at the top levels are large GEMMs), the blocked 64-column sweep
     // only on the blocks of at most rec_max: the 1x1 potrf's tail (8192
     // columns, potrf.cc) as one 128-leaf sweep ran its rank-64 updates at
-    // ~9 TFLOP/s.  SLATE_POTRF_REC_MAX (0: always blocked).
+    // ~9 TFLOP/s.  SLATE_POTRF_REC_MAX (0: always blocked, the default:
+    // config 2 measured 48.9 TFLOP/s all-blocked against 48.1 / 48.6 at 1024 /
+    // 2048 -- the recursion's own trsm / herk chain costs what the larger
+    // GEMMs save; profiles/r4_lu_split_potrf_rec.txt).
     static const int64_t rec_max = [] {
         const char* e = std::getenv("SLATE_POTRF_REC_MAX");
-        return e ? std::atoll(e) : int64_t(1024);
+        return e ? std::atoll(e) : int64_t(0);
     }();
     if (uplo == Uplo::Lower && blocked && (rec_max <= 0 || n <= rec_max)) {
         // Right-looking over 64-column leaves, four launches per leaf: the

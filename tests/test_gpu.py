@@ -542,6 +542,26 @@ def test_svd_device():
     assert np.linalg.norm(u @ np.diag(sv) @ vt - a) / (np.linalg.norm(a) * n) < 1e-12
 
 
+@pytest.mark.parametrize("n,nb", [(1000, 64), (2500, 256)])
+def test_bdsqr_device_vectors(n, nb):
+    """Device bdsqr with both vector sets: the step-table rotation kernel
+    (wave-pipelined rot_sweeps_pipe_kernel; row counts not multiples of 64,
+    several 16-sweep batches) against numpy's SVD of the bidiagonal."""
+    rng = np.random.default_rng(41)
+    d = rng.standard_normal(n)
+    e = rng.standard_normal(n - 1)
+    b = np.diag(d) + np.diag(e, 1)
+    Ub = s.from_numpy(np.eye(n), nb=nb, target="d")
+    VTb = s.from_numpy(np.eye(n), nb=nb, target="d")
+    sig = np.asarray(s.bdsqr_matrix(s.Job.Vec, s.Job.Vec, d, e, Ub, VTb, target="d"))
+    ref = np.linalg.svd(b, compute_uv=False)
+    assert np.abs(np.sort(sig)[::-1] - ref).max() < 1e-12 * ref.max()
+    u, vt = s.to_numpy(Ub), s.to_numpy(VTb)
+    assert relerr((u * sig[None, :]) @ vt, b) < 1e-12
+    assert np.linalg.norm(u.T @ u - np.eye(n)) / n < 1e-13
+    assert np.linalg.norm(vt @ vt.T - np.eye(n)) / n < 1e-13
+
+
 def test_condest_gmres_device():
     n, nb = 256, 64
     a = rnd(n, n, np.float64, 33) + n * np.eye(n)
