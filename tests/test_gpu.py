@@ -545,7 +545,7 @@ def test_svd_device():
 @pytest.mark.parametrize("n,nb", [(1000, 64), (2500, 256)])
 def test_bdsqr_device_vectors(n, nb):
     """Device bdsqr with both vector sets: the step-table rotation kernel
-    (wave-pipelined rot_sweeps_pipe_kernel; row counts not multiples of 64,
+    (row counts not multiples of 64,
     several 16-sweep batches) against numpy's SVD of the bidiagonal."""
     rng = np.random.default_rng(41)
     d = rng.standard_normal(n)
