@@ -114,6 +114,32 @@ std::vector<T> gather_band(Matrix<T> const& A, int64_t kd, int64_t M, bool lower
     return ab;
 }
 
+/// The T factors of the two-stage reductions' panels (he2hb / ge2tb: panel k
+/// factored on its own, T_k tile-column 0 of Ts[k][0]) side by side, as the T
+/// of the geqrf- / gelqf-shaped view the panels form together: the stage-1
+/// back-transforms are then ONE unmqr / unmlq call over all panels, one DAG
+/// with no host wait between panels, where the panel-by-panel loop built a
+/// scheduler and waited nt - 1 times.  Width: the view's
+/// columns plus one tile (gelqf's convention, room for a full last tile).
+template <typename T>
+TriangularFactors<T> stacked_T(std::vector<TriangularFactors<T>> const& Ts, int64_t nk, int64_t nb, int64_t ncols,
+                               Options const& opts) {
+    Target target = resolve_target(opts);
+    Matrix<T> Tf(nb, ncols + nb, nb, nb, Grid::self());
+    Tf.insertLocalTiles(target);
+    set(T(0), T(0), Tf, opts);
+    for (int64_t k = 0; k < nk && k < int64_t(Ts.size()); ++k) {
+        if (Ts[k].empty()) continue;
+        Matrix<T> const& Tk = Ts[k][0];
+        const int64_t w = std::min<int64_t>({Tk.n(), nb, ncols + nb - k * nb});
+        if (w <= 0) continue;
+        Matrix<T> src = Tk.slice(0, nb - 1, 0, w - 1);
+        Matrix<T> dst = Tf.slice(0, nb - 1, k * nb, k * nb + w - 1);
+        slate::copy<T, T>(src, dst, opts);
+    }
+    return TriangularFactors<T>{Tf};
+}
+
 /// Broadcast a host vector from `root` (size first: the other ranks may not
 /// know it).
 template <typename X>
@@ -632,11 +658,13 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     slate::copy<T, T>(Z1, Zw, opts);
     {
         trace::Block t3("unmtr_he2hb");
+        // panels F(k+1:, k), k = 0 .. nt-2, together: the QR-shaped view
+        // F(1:, 0:nt-2) applied to Z(1:, :) in one call
         const int64_t znt = Zw.nt();
-        for (int64_t k = nt - 2; k >= 0; --k) {
-            Matrix<T> panel = F.sub(k + 1, nt - 1, k, k);
-            Matrix<T> Zk = Zw.sub(k + 1, nt - 1, 0, znt - 1);
-            unmqr(Side::Left, Op::NoTrans, panel, Ts[k], Zk, opts);
+        if (nt >= 2) {
+            Matrix<T> P = F.sub(1, nt - 1, 0, nt - 2);
+            Matrix<T> Zs = Zw.sub(1, nt - 1, 0, znt - 1);
+            unmqr(Side::Left, Op::NoTrans, P, stacked_T(Ts, nt - 1, F.nb(), P.n(), opts), Zs, opts);
         }
     }
     slate::copy<T, T>(Zw, Z, opts);
@@ -893,12 +921,8 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
             slate::copy<T, T>(U1, Ut, opts);
         }
         trace::Block t3("unmbr_ge2tb_u");
-        const int64_t mt = W.mt(), unt = Uw.nt();
-        for (int64_t k = W.nt() - 1; k >= 0; --k) {
-            Matrix<T> cp = W.sub(k, mt - 1, k, k);
-            Matrix<T> Uk = Uw.sub(k, Uw.mt() - 1, 0, unt - 1);
-            unmqr(Side::Left, Op::NoTrans, cp, TU[k], Uk, opts);
-        }
+        // the QR panels W(k:, k) together: W itself is their geqrf-shaped view
+        unmqr(Side::Left, Op::NoTrans, W, stacked_T(TU, W.nt(), W.nb(), W.n(), opts), Uw, opts);
         slate::copy<T, T>(Uw, U, opts);
     }
     if (wv) {
@@ -918,11 +942,13 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
         VTw.insertLocalTiles(target);
         slate::copy<T, T>(transpose(V1), VTw, opts);
         trace::Block t3("unmbr_ge2tb_v");
+        // the LQ panels W(k, k+1:), k = 0 .. nt-2, together: the gelqf-shaped
+        // view W(0:nt-2, 1:) applied to VT(:, 1:)
         const int64_t nt = W.nt(), vmt = VTw.mt();
-        for (int64_t k = nt - 2; k >= 0; --k) {
-            Matrix<T> rp = W.sub(k, k, k + 1, nt - 1);
-            Matrix<T> Vk = VTw.sub(0, vmt - 1, k + 1, VTw.nt() - 1);
-            unmlq(Side::Right, Op::NoTrans, rp, TV[k], Vk, opts);
+        if (nt >= 2) {
+            Matrix<T> P = W.sub(0, nt - 2, 1, nt - 1);
+            Matrix<T> Vs = VTw.sub(0, vmt - 1, 1, VTw.nt() - 1);
+            unmlq(Side::Right, Op::NoTrans, P, stacked_T(TV, nt - 1, W.nb(), P.n(), opts), Vs, opts);
         }
         slate::copy<T, T>(VTw, VT, opts);
     }
