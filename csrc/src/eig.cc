@@ -165,6 +165,123 @@ void bcast_reflectors(Comm& w, host::Reflectors<T>& Q, int root) {
     bcast_vec(w, Q.v, root);
 }
 
+/// he2hb on one process: the same per-panel steps as the distributed loop
+/// below (panel QR, W = A22 V, the WY correction, her2k), but as local
+/// lb:: calls on one stream into preallocated buffers, with no driver, no
+/// scheduler and no host wait per panel.  The driver form paid a geqrf call
+/// (scheduler, T-matrix allocation, panel-error check) plus a V / W matrix
+/// allocation per panel: geqrf 168 of he2hb's 266 ms at n = 8192, nb = 256,
+/// for panel kernels worth 8 ms.  SLATE_HE2HB_LOCAL=0 keeps the driver form.
+template <typename T>
+bool he2hb_local(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& opts) {
+    static const bool env = [] {
+        const char* e = std::getenv("SLATE_HE2HB_LOCAL");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    auto gA = A.grid();
+    if (!env || gA->size() != 1 || A.mb() != A.nb() || A.arbitrary_layout() || A.op() != Op::NoTrans) return false;
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
+    const int64_t nt = A.nt(), n = A.n(), nb = A.nb();
+    Ts.assign(std::max<int64_t>(nt - 1, 0), {});
+    if (nt < 2) return true;
+    LocalBlock<T> la = A.local(loc, true);
+    T* a = la.ptr;
+    const int64_t lda = la.ld;
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    const int64_t mmax = std::max<int64_t>(n - A.tileNb(0), 1);
+    Work<T> V(target, size_t(mmax) * nb), W(target, size_t(mmax) * nb), X(target, size_t(nb) * nb), tau(target, size_t(nb));
+    int64_t r0 = 0;
+    for (int64_t k = 0; k + 1 < nt; ++k) {
+        const int64_t kb = A.tileNb(k);
+        const int64_t c0 = r0;
+        r0 += kb;
+        const int64_t m = n - r0;
+        Matrix<T> Tf(nb, std::max<int64_t>(kb, 1), nb, nb, Grid::self());
+        Tf.insertLocalTiles(target);
+        LocalBlock<T> lt = Tf.local(loc, true);
+        T* P = a + r0 + c0 * lda;
+        T* A22 = a + r0 + r0 * lda;
+        lb::geqrf_panel(c, m, kb, P, lda, tau.data(), lt.ptr, lt.ld);
+        // explicit unit-lower V
+        lb::copy2d(c, m, kb, P, lda, V.data(), m);
+        lb::set(c, Uplo::Upper, std::min(m, kb), kb, T(0), T(1), V.data(), m);
+        // W = A22 V T,  W -= V (T^H V^H W) / 2,  A22 -= V W^H + W V^H
+        lb::hemm(c, Side::Left, Uplo::Lower, m, kb, T(1), A22, lda, V.data(), m, T(0), W.data(), m);
+        lb::trmm(c, Side::Right, Uplo::Upper, Op::NoTrans, Diag::NonUnit, m, kb, T(1), lt.ptr, lt.ld, W.data(), m);
+        lb::gemm(c, Op::ConjTrans, Op::NoTrans, kb, kb, m, T(1), V.data(), m, W.data(), m, T(0), X.data(), kb);
+        lb::trmm(c, Side::Left, Uplo::Upper, Op::ConjTrans, Diag::NonUnit, kb, kb, T(1), lt.ptr, lt.ld, X.data(), kb);
+        lb::gemm(c, Op::NoTrans, Op::NoTrans, m, kb, kb, T(-0.5), V.data(), m, X.data(), kb, T(1), W.data(), m);
+        lb::her2k(c, Uplo::Lower, Op::NoTrans, m, kb, T(-1), V.data(), m, W.data(), m, real_type<T>(1), A22, lda);
+        Ts[k].push_back(Tf);
+    }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    return true;
+}
+
+/// ge2tb on one process, as he2hb_local: per block column the QR panel
+/// (geqrf_panel), Q^H on the columns to its right (larfb), the LQ panel of the
+/// block row as QR of its conjugate transpose (gelqf's own convention: row =
+/// Y^H, T_k at column 0 of an nb x (n1 + nb) T matrix), and H on the rows
+/// below (larfb from the right) -- local calls on one stream instead of a
+/// geqrf / unmqr / gelqf / unmlq driver call per panel (ge2tb ~470 of the
+/// n = 8192 svd's 3.4 s, for ~1.5 TFLOP).  SLATE_GE2TB_LOCAL=0: driver form.
+template <typename T>
+bool ge2tb_local(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<TriangularFactors<T>>& TV,
+                 Options const& opts) {
+    static const bool env = [] {
+        const char* e = std::getenv("SLATE_GE2TB_LOCAL");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    auto gA = A.grid();
+    if (!env || gA->size() != 1 || A.mb() != A.nb() || A.arbitrary_layout() || A.op() != Op::NoTrans) return false;
+    Target target = resolve_target(opts);
+    const Loc loc = loc_of(target);
+    const int64_t nt = A.nt(), M = A.m(), N = A.n(), nb = A.nb();
+    TU.assign(nt, {});
+    TV.assign(std::max<int64_t>(nt - 1, 0), {});
+    LocalBlock<T> la = A.local(loc, true);
+    T* a = la.ptr;
+    const int64_t lda = la.ld;
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    Work<T> Y(target, size_t(std::max<int64_t>(N, 1)) * nb), tau(target, size_t(nb));
+    int64_t r0 = 0;
+    for (int64_t k = 0; k < nt; ++k) {
+        const int64_t kb = A.tileNb(k), m = M - r0;
+        Matrix<T> Tq(nb, std::max<int64_t>(kb, 1), nb, nb, Grid::self());
+        Tq.insertLocalTiles(target);
+        LocalBlock<T> lq = Tq.local(loc, true);
+        T* P = a + r0 + r0 * lda;
+        if (m > 0) lb::geqrf_panel(c, m, kb, P, lda, tau.data(), lq.ptr, lq.ld);
+        else lb::set(c, Uplo::General, nb, kb, T(0), T(0), lq.ptr, lq.ld);
+        TU[k].push_back(Tq);
+        const int64_t c1 = r0 + kb, n1 = N - c1;
+        if (k + 1 < nt && n1 > 0) {
+            if (m > 0)
+                lb::larfb(c, Side::Left, Op::ConjTrans, m, n1, kb, P, lda, lq.ptr, lq.ld, a + r0 + c1 * lda, lda);
+            Matrix<T> Tl(nb, n1 + nb, nb, nb, Grid::self());
+            Tl.insertLocalTiles(target);
+            LocalBlock<T> ll = Tl.local(loc, true);
+            lb::set(c, Uplo::General, nb, n1 + nb, T(0), T(0), ll.ptr, ll.ld);
+            T* rp = a + r0 + c1 * lda;
+            const int64_t kr = std::min<int64_t>(kb, m);   // rows of the row panel
+            if (kr > 0) {
+                lb::copy<T, T>(c, Uplo::General, Op::ConjTrans, n1, kr, rp, lda, Y.data(), n1);
+                lb::geqrf_panel(c, n1, kr, Y.data(), n1, tau.data(), ll.ptr, ll.ld);
+                lb::copy<T, T>(c, Uplo::General, Op::ConjTrans, kr, n1, Y.data(), n1, rp, lda);
+                const int64_t mr = M - c1;   // rows below the row panel
+                if (mr > 0)
+                    lb::larfb(c, Side::Right, Op::NoTrans, mr, n1, kr, Y.data(), n1, ll.ptr, ll.ld, a + c1 + c1 * lda,
+                              lda);
+            }
+            TV[k].push_back(Tl);
+        }
+        r0 = c1;
+    }
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    return true;
+}
+
 }  // namespace
 
 //------------------------------------------------------------------------------
@@ -179,6 +296,7 @@ template <typename T>
 void he2hb(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options const& opts) {
     trace::Block tb("he2hb");
     internal::DriverScope ds_;
+    if (he2hb_local(A, Ts, opts)) return;
     Target target = resolve_target(opts);
     const Loc loc = loc_of(target);
     const int64_t nt = A.nt();
@@ -730,6 +848,7 @@ void ge2tb(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vector<Tria
            Options const& opts) {
     trace::Block tb("ge2tb");
     internal::DriverScope ds_;
+    if (ge2tb_local(A, TU, TV, opts)) return;
     const int64_t mt = A.mt(), nt = A.nt();
     TU.assign(nt, {});
     TV.assign(std::max<int64_t>(nt - 1, 0), {});
