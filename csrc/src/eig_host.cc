@@ -21,9 +21,6 @@ namespace host {
 
 namespace {
 
-// Wait for a pipelined sweep's progress counter: a short pause spin first
-// (the lag between sweeps is a few microseconds of work), sched_yield only
-// when the producer is really behind.
 /// sqrt(a^2 + b^2) without hypot's scaling when the squares are safely in
 /// range (bdsqr's host loop makes two per rotation and is the SVD's critical
 /// path: n = 4096 bidiagonal 1.17 -> 0.80-0.85 s); falls back to std::hypot
@@ -37,6 +34,9 @@ inline R fast_hypot(R a, R b) {
     return std::hypot(a, b);
 }
 
+// Wait for a pipelined sweep's progress counter: a short pause spin first
+// (the lag between sweeps is a few microseconds of work), sched_yield only
+// when the producer is really behind.
 inline void wait_progress(std::atomic<int64_t> const& p, int64_t want) {
     for (int spin = 0; p.load(std::memory_order_acquire) < want; ++spin) {
         if (spin < 256) _mm_pause();
