@@ -434,6 +434,20 @@ void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
     BaseMatrix<T> As = A.op() == Op::NoTrans ? BaseMatrix<T>(A) : A.transpose_view(cj_);
     if (cj_) { offdiag = slate::conj(offdiag); diag = slate::conj(diag); }
     Uplo u = trap ? As.uplo() : Uplo::General;
+    // whole local block in ONE launch when no diagonal bookkeeping is needed
+    // (a general matrix with diag == offdiag, on any grid) or the local block
+    // is the whole view with its diagonal on the storage diagonal (one
+    // process, row0 == col0): the tile loop below launched a kernel per tile
+    // -- 16384 launches for an 8192^2 matrix in 64-wide tiles (the svd's
+    // vector matrices), ~79 ms of the n = 8192 svd
+    if (!A.storage()->banded && A.op() == Op::NoTrans &&
+        ((u == Uplo::General && diag == offdiag) || (A.grid()->size() == 1 && A.row0() == A.col0()))) {
+        LocalBlock<T> la = A.local_raw(loc);
+        if (la.m > 0 && la.n > 0) lb::set(c, u, la.m, la.n, offdiag, diag, la.ptr, la.ld);
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+        internal::finish_origin(A, opts);
+        return;
+    }
     for_tz_tiles(As, u, [&](int64_t i, int64_t j, int64_t ri, int64_t cj) {
         Tile<T> t = As.tile(i, j, loc);
         if (u == Uplo::General) {

@@ -202,6 +202,9 @@ bool he2hb_local(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options co
         LocalBlock<T> lt = Tf.local(loc, true);
         T* P = a + r0 + c0 * lda;
         T* A22 = a + r0 + r0 * lda;
+        // all of T zero first: the host panel writes only its min(m, kb)
+        // square, and a ragged last panel (m < kb) multiplies the rest
+        lb::set(c, Uplo::General, nb, std::max<int64_t>(kb, 1), T(0), T(0), lt.ptr, lt.ld);
         lb::geqrf_panel(c, m, kb, P, lda, tau.data(), lt.ptr, lt.ld);
         // explicit unit-lower V
         lb::copy2d(c, m, kb, P, lda, V.data(), m);
@@ -252,8 +255,8 @@ bool ge2tb_local(Matrix<T>& A, std::vector<TriangularFactors<T>>& TU, std::vecto
         Tq.insertLocalTiles(target);
         LocalBlock<T> lq = Tq.local(loc, true);
         T* P = a + r0 + r0 * lda;
+        lb::set(c, Uplo::General, nb, std::max<int64_t>(kb, 1), T(0), T(0), lq.ptr, lq.ld);
         if (m > 0) lb::geqrf_panel(c, m, kb, P, lda, tau.data(), lq.ptr, lq.ld);
-        else lb::set(c, Uplo::General, nb, kb, T(0), T(0), lq.ptr, lq.ld);
         TU[k].push_back(Tq);
         const int64_t c1 = r0 + kb, n1 = N - c1;
         if (k + 1 < nt && n1 > 0) {
