@@ -21,6 +21,8 @@
 #include "../kernels/kernels.hh"
 
 #include <algorithm>
+#include <exception>
+#include <thread>
 #include <cmath>
 #include <map>
 
@@ -138,6 +140,37 @@ TriangularFactors<T> stacked_T(std::vector<TriangularFactors<T>> const& Ts, int6
         slate::copy<T, T>(src, dst, opts);
     }
     return TriangularFactors<T>{Tf};
+}
+
+/// Stage 2 and the stage-1 back-transform overlapped: the host bulge chase
+/// (hb2st / tb2bd, rank 0, OpenMP) runs in a side thread while this thread
+/// forms the explicit stage-1 orthogonal factor on the device (unmqr / unmlq
+/// of the panels on an identity); the back-transform at the end is then one
+/// GEMM instead of the reflector application, which used to run after the
+/// chase with the GPU idle meanwhile.  GPU work stays on the calling thread.
+/// SLATE_EIG_OVERLAP=0: sequential (the reflectors applied at the end);
+/// 2: on for the host target as well (the CPU tests cover the path with it).
+inline bool eig_overlap(Target target) {
+    const char* e = std::getenv("SLATE_EIG_OVERLAP");
+    const int v = e ? std::atoi(e) : 1;
+    return v == 2 || (v != 0 && target == Target::Devices);
+}
+
+template <typename Host, typename Dev>
+void overlapped(bool on, Host&& host_work, Dev&& dev_work) {
+    if (!on) { host_work(); return; }
+    std::exception_ptr err;
+    std::thread th([&] {
+        try { host_work(); } catch (...) { err = std::current_exception(); }
+    });
+    try {
+        dev_work();
+    } catch (...) {
+        th.join();
+        throw;
+    }
+    th.join();
+    if (err) std::rethrow_exception(err);
 }
 
 /// Broadcast a host vector from `root` (size first: the other ranks may not
@@ -707,10 +740,21 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     std::vector<R> d, e;
     host::Reflectors<T> Q2;
     std::vector<T> phase;
+    const bool ovl = wanted(Z) && eig_overlap(target) && nt >= 2;
+    Matrix<T> Q1x;   // explicit stage-1 Q (ovl)
     {
         trace::Block t2("hb2st");
         Comm& w = gA->world();
-        if (w.rank() == 0) host::hb2st<T>(n, kd, B.data() + 2 * kd, 4 * kd, d, e, Q2, phase);
+        overlapped(ovl, [&] { if (w.rank() == 0) host::hb2st<T>(n, kd, B.data() + 2 * kd, 4 * kd, d, e, Q2, phase); },
+                   [&] {
+                       trace::Block t3("unmtr_he2hb_form");
+                       Q1x = Matrix<T>(n, n, kd, kd, gA);
+                       Q1x.insertLocalTiles(target);
+                       set(T(0), T(1), Q1x, opts);
+                       Matrix<T> P = F.sub(1, nt - 1, 0, nt - 2);
+                       Matrix<T> Qs = Q1x.sub(1, nt - 1, 0, nt - 1);
+                       unmqr(Side::Left, Op::NoTrans, P, stacked_T(Ts, nt - 1, F.nb(), P.n(), opts), Qs, opts);
+                   });
         if (w.size() > 1) {
             bcast_vec(w, d, 0);
             bcast_vec(w, e, 0);
@@ -777,6 +821,14 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     Matrix<T> Zw(n, n, kd, kd, gA);
     Zw.insertLocalTiles(target);
     slate::copy<T, T>(Z1, Zw, opts);
+    if (ovl) {
+        trace::Block t3("unmtr_he2hb_gemm");
+        Matrix<T> Zo(n, n, kd, kd, gA);
+        Zo.insertLocalTiles(target);
+        gemm(T(1), Q1x, Zw, T(0), Zo, opts);
+        slate::copy<T, T>(Zo, Z, opts);
+        return;
+    }
     {
         trace::Block t3("unmtr_he2hb");
         // panels F(k+1:, k), k = 0 .. nt-2, together: the QR-shaped view
@@ -980,11 +1032,32 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
     std::vector<R> d, e;
     host::Reflectors<T> QU2, QV2;
     std::vector<T> pu, pv;
+    const bool ovl = (wanted(U) || wanted(VT)) && eig_overlap(target);
+    const int64_t wnt = W.nt();
+    Matrix<T> QUx, QVx;   // explicit stage-1 factors (ovl)
     {
         std::vector<T> Bb = gather_band(W, kd, Mg, false, false, opts);
         trace::Block t2("tb2bd");
         Comm& w = gA->world();
-        if (w.rank() == 0) host::tb2bd<T>(n, n, kd, Bb.data() + Mg, 2 * Mg, d, e, QU2, QV2, pu, pv);
+        overlapped(ovl, [&] { if (w.rank() == 0) host::tb2bd<T>(n, n, kd, Bb.data() + Mg, 2 * Mg, d, e, QU2, QV2, pu, pv); },
+                   [&] {
+                       trace::Block t3("unmbr_ge2tb_form");
+                       if (wanted(U)) {
+                           // Q_U [I_n; 0]
+                           QUx = Matrix<T>(m, n, kd, kd, gA);
+                           QUx.insertLocalTiles(target);
+                           set(T(0), T(1), QUx, opts);
+                           unmqr(Side::Left, Op::NoTrans, W, stacked_T(TU, wnt, W.nb(), W.n(), opts), QUx, opts);
+                       }
+                       if (wanted(VT) && wnt >= 2) {
+                           QVx = Matrix<T>(n, n, kd, kd, gA);
+                           QVx.insertLocalTiles(target);
+                           set(T(0), T(1), QVx, opts);
+                           Matrix<T> P = W.sub(0, wnt - 2, 1, wnt - 1);
+                           Matrix<T> Vs = QVx.sub(0, QVx.mt() - 1, 1, QVx.nt() - 1);
+                           unmlq(Side::Right, Op::NoTrans, P, stacked_T(TV, wnt - 1, W.nb(), P.n(), opts), Vs, opts);
+                       }
+                   });
         if (w.size() > 1) {
             bcast_vec(w, d, 0);
             bcast_vec(w, e, 0);
@@ -1035,6 +1108,15 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
             Comm& w = gA->world();
             stage2_apply(QU2, stage2_streamed<T>(target, kd, w), n, kd, l1.ptr, l1.ld, l1.n, c, w);
         }
+        if (ovl) {
+            trace::Block t3("unmbr_ge2tb_u_gemm");
+            Matrix<T> Un(n, n, kd, kd, gA), Uo(m, n, kd, kd, gA);
+            Un.insertLocalTiles(target);
+            Uo.insertLocalTiles(target);
+            slate::copy<T, T>(U1, Un, opts);
+            gemm(T(1), QUx, Un, T(0), Uo, opts);
+            slate::copy<T, T>(Uo, U, opts);
+        } else {
         Matrix<T> Uw(m, n, kd, kd, gA);
         Uw.insertLocalTiles(target);
         set(T(0), T(0), Uw, opts);
@@ -1046,6 +1128,7 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
         // the QR panels W(k:, k) together: W itself is their geqrf-shaped view
         unmqr(Side::Left, Op::NoTrans, W, stacked_T(TU, W.nt(), W.nb(), W.n(), opts), Uw, opts);
         slate::copy<T, T>(Uw, U, opts);
+        }
     }
     if (wv) {
         // VT2 := VT2 QV2^H  <=>  Vt := conj(QV2) Vt  (Vt = VT2^T), then the stage-1 reflectors
@@ -1063,6 +1146,14 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
         Matrix<T> VTw(n, n, kd, kd, gA);
         VTw.insertLocalTiles(target);
         slate::copy<T, T>(transpose(V1), VTw, opts);
+        if (ovl && wnt >= 2) {
+            trace::Block t3("unmbr_ge2tb_v_gemm");
+            Matrix<T> Vo(n, n, kd, kd, gA);
+            Vo.insertLocalTiles(target);
+            gemm(T(1), VTw, QVx, T(0), Vo, opts);
+            slate::copy<T, T>(Vo, VT, opts);
+            return;
+        }
         trace::Block t3("unmbr_ge2tb_v");
         // the LQ panels W(k, k+1:), k = 0 .. nt-2, together: the gelqf-shaped
         // view W(0:nt-2, 1:) applied to VT(:, 1:)

@@ -203,3 +203,30 @@ def test_heev_svd_nan_inf_guard():
         assert len(w) == n and (np.all(np.isnan(w)) if np.isnan(bad) else np.all(np.isinf(w)))
         sv = s.svd_vals(s.from_numpy(a[:, :30], nb=nb))
         assert len(sv) == 30 and (np.all(np.isnan(sv)) if np.isnan(bad) else np.all(np.isinf(sv)))
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.complex128])
+def test_eig_overlap_path(dt, monkeypatch):
+    """Stage 2 in a side thread with the explicit stage-1 factor formed
+    meanwhile, the back-transform as one GEMM (eig.cc `overlapped`; on by
+    default for the device target, forced here on the host with
+    SLATE_EIG_OVERLAP=2): heev and svd vectors against numpy, ragged tiles."""
+    monkeypatch.setenv("SLATE_EIG_OVERLAP", "2")
+    n, nb = 75, 16
+    a = herm(n, dt, 51)
+    A = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(a, nb=nb))
+    Z = s.from_numpy(np.zeros((n, n), dt), nb=nb)
+    w = np.asarray(s.heev(A, Z))
+    z = s.to_numpy(Z)
+    assert np.allclose(w, np.linalg.eigvalsh(a), atol=1e-12 * n)
+    assert np.linalg.norm(a @ z - z * w) / (np.linalg.norm(a) * n) < 1e-13
+    m = 90
+    g = rnd(m, n, dt, 52)
+    U = s.from_numpy(np.zeros((m, n), dt), nb=nb)
+    VT = s.from_numpy(np.zeros((n, n), dt), nb=nb)
+    sv = np.asarray(s.svd(s.from_numpy(g, nb=nb), U, VT))
+    ref = np.linalg.svd(g, compute_uv=False)
+    assert np.allclose(sv, ref, atol=1e-12 * ref.max())
+    u, vt = s.to_numpy(U), s.to_numpy(VT)
+    assert np.linalg.norm((u * sv[None, :]) @ vt - g) / (np.linalg.norm(g) * n) < 1e-13
+    assert np.linalg.norm(u.conj().T @ u - np.eye(n)) / n < 1e-13
