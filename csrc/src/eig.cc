@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <exception>
 #include <thread>
+#include <omp.h>
 #include <cmath>
 #include <map>
 
@@ -156,12 +157,38 @@ inline bool eig_overlap(Target target) {
     return v == 2 || (v != 0 && target == Target::Devices);
 }
 
+/// C = A B for the overlapped back-transforms: on one process one local
+/// GEMM over the whole arrays (the driver's SUMMA on the kd-wide tiles of
+/// these matrices ran at ~20 TFLOP/s), else the distributed gemm.
+template <typename T>
+void product(Matrix<T>& A, Matrix<T>& B, Matrix<T>& C, Options const& opts) {
+    Target target = resolve_target(opts);
+    if (A.grid()->size() == 1 && B.grid()->size() == 1 && C.grid()->size() == 1 && A.op() == Op::NoTrans &&
+        B.op() == Op::NoTrans && C.op() == Op::NoTrans) {
+        const Loc loc = loc_of(target);
+        LocalBlock<T> la = A.local(loc, false), lbk = B.local(loc, false), lc = C.local(loc, true);
+        lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+        lb::gemm(c, Op::NoTrans, Op::NoTrans, C.m(), C.n(), A.n(), T(1), la.ptr, la.ld, lbk.ptr, lbk.ld, T(0), lc.ptr,
+                 lc.ld);
+        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+        return;
+    }
+    gemm(T(1), A, B, T(0), C, opts);
+}
+
 template <typename Host, typename Dev>
 void overlapped(bool on, Host&& host_work, Dev&& dev_work) {
     if (!on) { host_work(); return; }
     std::exception_ptr err;
+    // one core less for the chase's OpenMP team: this thread keeps issuing
+    // and waiting on device work, and an oversubscribed team of spin-waiting
+    // pipeline threads slowed hb2st 473 -> 580 ms
+    const int nth = std::max(1, omp_get_max_threads() - 1);
     std::thread th([&] {
-        try { host_work(); } catch (...) { err = std::current_exception(); }
+        try {
+            omp_set_num_threads(nth);
+            host_work();
+        } catch (...) { err = std::current_exception(); }
     });
     try {
         dev_work();
@@ -825,7 +852,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         trace::Block t3("unmtr_he2hb_gemm");
         Matrix<T> Zo(n, n, kd, kd, gA);
         Zo.insertLocalTiles(target);
-        gemm(T(1), Q1x, Zw, T(0), Zo, opts);
+        product(Q1x, Zw, Zo, opts);
         slate::copy<T, T>(Zo, Z, opts);
         return;
     }
@@ -1114,7 +1141,7 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
             Un.insertLocalTiles(target);
             Uo.insertLocalTiles(target);
             slate::copy<T, T>(U1, Un, opts);
-            gemm(T(1), QUx, Un, T(0), Uo, opts);
+            product(QUx, Un, Uo, opts);
             slate::copy<T, T>(Uo, U, opts);
         } else {
         Matrix<T> Uw(m, n, kd, kd, gA);
@@ -1150,7 +1177,7 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
             trace::Block t3("unmbr_ge2tb_v_gemm");
             Matrix<T> Vo(n, n, kd, kd, gA);
             Vo.insertLocalTiles(target);
-            gemm(T(1), VTw, QVx, T(0), Vo, opts);
+            product(VTw, QVx, Vo, opts);
             slate::copy<T, T>(Vo, VT, opts);
             return;
         }
