@@ -166,6 +166,7 @@ void product(Matrix<T>& A, Matrix<T>& B, Matrix<T>& C, Options const& opts) {
     if (A.grid()->size() == 1 && B.grid()->size() == 1 && C.grid()->size() == 1 && A.op() == Op::NoTrans &&
         B.op() == Op::NoTrans && C.op() == Op::NoTrans) {
         const Loc loc = loc_of(target);
+        trace::Block tb("eig_product");
         LocalBlock<T> la = A.local(loc, false), lbk = B.local(loc, false), lc = C.local(loc, true);
         lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
         lb::gemm(c, Op::NoTrans, Op::NoTrans, C.m(), C.n(), A.n(), T(1), la.ptr, la.ld, lbk.ptr, lbk.ld, T(0), lc.ptr,
