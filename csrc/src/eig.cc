@@ -157,24 +157,25 @@ inline bool eig_overlap(Target target) {
     return v == 2 || (v != 0 && target == Target::Devices);
 }
 
-/// C = A B for the overlapped back-transforms: on one process one local
-/// GEMM over the whole arrays (the driver's SUMMA on the kd-wide tiles of
-/// these matrices ran at ~20 TFLOP/s), else the distributed gemm.
+/// C = op(A) B for the overlapped back-transforms on one process: one local
+/// GEMM straight from the operands' arrays into C's (no work copies of the
+/// n x n operands or the result).  Returns false (nothing done) otherwise.
 template <typename T>
-void product(Matrix<T>& A, Matrix<T>& B, Matrix<T>& C, Options const& opts) {
+bool local_product(Op opA, Matrix<T>& A, Matrix<T>& B, Matrix<T>& C, Options const& opts) {
+    if (A.grid()->size() != 1 || B.grid()->size() != 1 || C.grid()->size() != 1 || A.op() != Op::NoTrans ||
+        B.op() != Op::NoTrans || C.op() != Op::NoTrans || A.arbitrary_layout() || B.arbitrary_layout() ||
+        C.arbitrary_layout())
+        return false;
+    trace::Block tb("eig_product");
     Target target = resolve_target(opts);
-    if (A.grid()->size() == 1 && B.grid()->size() == 1 && C.grid()->size() == 1 && A.op() == Op::NoTrans &&
-        B.op() == Op::NoTrans && C.op() == Op::NoTrans) {
-        const Loc loc = loc_of(target);
-        trace::Block tb("eig_product");
-        LocalBlock<T> la = A.local(loc, false), lbk = B.local(loc, false), lc = C.local(loc, true);
-        lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
-        lb::gemm(c, Op::NoTrans, Op::NoTrans, C.m(), C.n(), A.n(), T(1), la.ptr, la.ld, lbk.ptr, lbk.ld, T(0), lc.ptr,
-                 lc.ld);
-        if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-        return;
-    }
-    gemm(T(1), A, B, T(0), C, opts);
+    const Loc loc = loc_of(target);
+    LocalBlock<T> la = A.local(loc, false), lbk = B.local(loc, false), lc = C.local(loc, true);
+    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
+    const int64_t k = opA == Op::NoTrans ? A.n() : A.m();
+    lb::gemm(c, opA, Op::NoTrans, C.m(), C.n(), k, T(1), la.ptr, la.ld, lbk.ptr, lbk.ld, T(0), lc.ptr, lc.ld);
+    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
+    internal::finish_origin(C, opts);
+    return true;
 }
 
 template <typename Host, typename Dev>
@@ -846,17 +847,20 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         stage2_apply(Q2, stage2_streamed<T>(target, kd, w), n, kd, lz.ptr, lz.ld, lz.n, c, w);
     }
     // stage-1 back-transform (unmtr_he2hb) on F's layout, then into Z
-    Matrix<T> Zw(n, n, kd, kd, gA);
-    Zw.insertLocalTiles(target);
-    slate::copy<T, T>(Z1, Zw, opts);
     if (ovl) {
         trace::Block t3("unmtr_he2hb_gemm");
-        Matrix<T> Zo(n, n, kd, kd, gA);
+        if (local_product(Op::NoTrans, Q1x, Z1, Z, opts)) return;
+        Matrix<T> Zw(n, n, kd, kd, gA), Zo(n, n, kd, kd, gA);
+        Zw.insertLocalTiles(target);
         Zo.insertLocalTiles(target);
-        product(Q1x, Zw, Zo, opts);
+        slate::copy<T, T>(Z1, Zw, opts);
+        gemm(T(1), Q1x, Zw, T(0), Zo, opts);
         slate::copy<T, T>(Zo, Z, opts);
         return;
     }
+    Matrix<T> Zw(n, n, kd, kd, gA);
+    Zw.insertLocalTiles(target);
+    slate::copy<T, T>(Z1, Zw, opts);
     {
         trace::Block t3("unmtr_he2hb");
         // panels F(k+1:, k), k = 0 .. nt-2, together: the QR-shaped view
@@ -1138,12 +1142,14 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
         }
         if (ovl) {
             trace::Block t3("unmbr_ge2tb_u_gemm");
-            Matrix<T> Un(n, n, kd, kd, gA), Uo(m, n, kd, kd, gA);
-            Un.insertLocalTiles(target);
-            Uo.insertLocalTiles(target);
-            slate::copy<T, T>(U1, Un, opts);
-            product(QUx, Un, Uo, opts);
-            slate::copy<T, T>(Uo, U, opts);
+            if (!local_product(Op::NoTrans, QUx, U1, U, opts)) {
+                Matrix<T> Un(n, n, kd, kd, gA), Uo(m, n, kd, kd, gA);
+                Un.insertLocalTiles(target);
+                Uo.insertLocalTiles(target);
+                slate::copy<T, T>(U1, Un, opts);
+                gemm(T(1), QUx, Un, T(0), Uo, opts);
+                slate::copy<T, T>(Uo, U, opts);
+            }
         } else {
         Matrix<T> Uw(m, n, kd, kd, gA);
         Uw.insertLocalTiles(target);
@@ -1171,14 +1177,18 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
             Comm& w = gA->world();
             stage2_apply(QV2c, stage2_streamed<T>(target, kd, w), n, kd, l1.ptr, l1.ld, l1.n, c, w);
         }
+        if (ovl && wnt >= 2) {
+            // VT = V1^T QVx
+            trace::Block t3("unmbr_ge2tb_v_gemm");
+            if (local_product(Op::Trans, V1, QVx, VT, opts)) return;
+        }
         Matrix<T> VTw(n, n, kd, kd, gA);
         VTw.insertLocalTiles(target);
         slate::copy<T, T>(transpose(V1), VTw, opts);
         if (ovl && wnt >= 2) {
-            trace::Block t3("unmbr_ge2tb_v_gemm");
             Matrix<T> Vo(n, n, kd, kd, gA);
             Vo.insertLocalTiles(target);
-            product(VTw, QVx, Vo, opts);
+            gemm(T(1), VTw, QVx, T(0), Vo, opts);
             slate::copy<T, T>(Vo, VT, opts);
             return;
         }
