@@ -150,10 +150,15 @@ TriangularFactors<T> stacked_T(std::vector<TriangularFactors<T>> const& Ts, int6
 /// GEMM instead of the reflector application, which used to run after the
 /// chase with the GPU idle meanwhile.  GPU work stays on the calling thread.
 /// SLATE_EIG_OVERLAP=0: sequential (the reflectors applied at the end);
-/// 2: on for the host target as well (the CPU tests cover the path with it).
-inline bool eig_overlap(Target target) {
+/// 1: on for the device target; 2: on for the host target as well (the CPU
+/// tests cover the path with it).  Unset: on for svd, off for heev -- the
+/// side thread slows hb2st's spin-waiting pipeline by 15-70 ms, about what
+/// hiding the 105 ms stage-1 application gains (same-box A/B 1.089 vs 1.135
+/// and 1.172 vs 1.157 s), while svd gains ~100 ms
+/// (profiles/r4_eig_overlap_ab.txt).
+inline bool eig_overlap(Target target, bool by_default) {
     const char* e = std::getenv("SLATE_EIG_OVERLAP");
-    const int v = e ? std::atoi(e) : 1;
+    const int v = e ? std::atoi(e) : (by_default ? 1 : 0);
     return v == 2 || (v != 0 && target == Target::Devices);
 }
 
@@ -769,7 +774,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
     std::vector<R> d, e;
     host::Reflectors<T> Q2;
     std::vector<T> phase;
-    const bool ovl = wanted(Z) && eig_overlap(target) && nt >= 2;
+    const bool ovl = wanted(Z) && eig_overlap(target, false) && nt >= 2;
     Matrix<T> Q1x;   // explicit stage-1 Q (ovl)
     {
         trace::Block t2("hb2st");
@@ -1064,7 +1069,7 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
     std::vector<R> d, e;
     host::Reflectors<T> QU2, QV2;
     std::vector<T> pu, pv;
-    const bool ovl = (wanted(U) || wanted(VT)) && eig_overlap(target);
+    const bool ovl = (wanted(U) || wanted(VT)) && eig_overlap(target, true);
     const int64_t wnt = W.nt();
     Matrix<T> QUx, QVx;   // explicit stage-1 factors (ovl)
     {
