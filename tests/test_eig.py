@@ -46,6 +46,45 @@ def test_stedc_clustered():
     assert np.linalg.norm(t @ z - z * np.asarray(w)) < 1e-10
 
 
+@pytest.mark.parametrize("kind", ["toeplitz", "wilkinson", "graded", "cluster", "tinyoff"])
+def test_stedc_secular_hard(kind):
+    """Secular roots by the rational two-pole iteration (secular.hh) on the
+    classic hard tridiagonals: roots next to poles (graded, tiny couplings),
+    dense clusters (1-2-1 Toeplitz, near-identical diagonals) -- residual,
+    orthogonality and eigenvalues at working precision, host stedc and the
+    distributed stedc_matrix path."""
+    n = 500
+    rng = np.random.default_rng(7)
+    if kind == "toeplitz":
+        d, e = np.full(n, 2.0), np.full(n - 1, -1.0)
+    elif kind == "wilkinson":
+        m = (n - 1) // 2
+        d, e = np.abs(np.arange(-m, n - m, dtype=float)), np.ones(n - 1)
+    elif kind == "graded":
+        d, e = np.logspace(0, -15, n), np.logspace(0, -15, n - 1) * 0.1
+    elif kind == "cluster":
+        d = np.ones(n)
+        d[::7] = 1 + 1e-12
+        e = np.full(n - 1, 1e-9)
+    else:
+        d, e = rng.standard_normal(n), rng.standard_normal(n - 1)
+        e[::5] = 1e-14
+    t = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    tn = np.linalg.norm(t, 2)
+    ref = np.linalg.eigvalsh(t)
+    w, z = s.stedc(d, e)
+    w = np.asarray(w)
+    assert np.abs(np.sort(w) - ref).max() <= 1e-13 * n * tn
+    assert np.linalg.norm(t @ z - z * w) <= 1e-14 * n * tn
+    assert np.linalg.norm(z.T @ z - np.eye(n)) <= 1e-14 * n
+    Q = s.from_numpy(np.zeros((n, n)), nb=64)
+    w2 = np.asarray(s.stedc_matrix(d, e, Q))
+    z2 = s.to_numpy(Q)
+    assert np.abs(np.sort(w2) - ref).max() <= 1e-13 * n * tn
+    assert np.linalg.norm(t @ z2 - z2 * w2) <= 1e-14 * n * tn
+    assert np.linalg.norm(z2.T @ z2 - np.eye(n)) <= 1e-14 * n
+
+
 def test_bdsqr():
     rng = np.random.default_rng(1)
     for n in (1, 3, 40, 120):

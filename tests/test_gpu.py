@@ -562,6 +562,29 @@ def test_bdsqr_device_vectors(n, nb):
     assert np.linalg.norm(vt @ vt.T - np.eye(n)) / n < 1e-13
 
 
+@pytest.mark.parametrize("kind", ["graded", "cluster", "toeplitz"])
+def test_stedc_secular_device(kind):
+    """Distributed stedc with the device secular-root kernel (rational
+    two-pole iteration, secular.hh) on hard tridiagonals, against numpy."""
+    n = 600
+    if kind == "graded":
+        d, e = np.logspace(0, -15, n), np.logspace(0, -15, n - 1) * 0.1
+    elif kind == "cluster":
+        d = np.ones(n)
+        d[::7] = 1 + 1e-12
+        e = np.full(n - 1, 1e-9)
+    else:
+        d, e = np.full(n, 2.0), np.full(n - 1, -1.0)
+    t = np.diag(d) + np.diag(e, 1) + np.diag(e, -1)
+    tn = np.linalg.norm(t, 2)
+    Q = s.from_numpy(np.zeros((n, n)), nb=64, target="d")
+    w = np.asarray(s.stedc_matrix(d, e, Q, target="d"))
+    z = s.to_numpy(Q)
+    assert np.abs(np.sort(w) - np.linalg.eigvalsh(t)).max() <= 1e-13 * n * tn
+    assert np.linalg.norm(t @ z - z * w) <= 1e-14 * n * tn
+    assert np.linalg.norm(z.T @ z - np.eye(n)) <= 1e-14 * n
+
+
 def test_condest_gmres_device():
     n, nb = 256, 64
     a = rnd(n, n, np.float64, 33) + n * np.eye(n)
