@@ -140,133 +140,6 @@ __global__ __launch_bounds__(64) void rot_sweeps_kernel(RotJob<T, R> a, RotJob<T
     else rot_sweeps_row<T, R, K, kRotPrefetch>(b, r, sD);
 }
 
-// Wave-pipelined form: the K sweeps of a batch split over G waves of one
-// workgroup (S = K / G sweeps each, one wave per SIMD), all on the same 64
-// rows.  In global step tau, wave g applies sweeps gS .. gS + S - 1, i.e. a
-// 2S-column window [tau - 2(g+1)S + 2, tau - 2gS + 1]; the column leaving
-// wave g's window at step tau (tau - 2(g+1)S + 2) is exactly the one entering
-// wave g+1's at that step, so columns stream wave 0 -> 1 -> ... -> G-1
-// through LDS.  Wave g runs one PF-step block behind wave g-1 (one barrier
-// per block; handoff double-buffered by block parity), wave 0 reads the
-// columns from memory (register ring, PF ahead), wave G-1 writes them back.
-// Against the single-wave kernel a step costs S instead of K rotations per
-// SIMD and the workgroup uses all four SIMDs of its CU (the single-wave
-// launch of n / 64 waves left three of them idle).  Same tables, same
-// arithmetic per element, so results are bitwise those of rot_sweeps_row.
-template <typename T, typename R, int K, int G, int PF>
-__global__ __launch_bounds__(64 * G) void rot_sweeps_pipe_kernel(RotJob<T, R> ja, RotJob<T, R> jb, int64_t nblk_a) {
-    constexpr int S = K / G;
-    constexpr int BLK = PF * 2 * K;                       // reals of one table block
-    constexpr int NT = 64 * G;
-    constexpr int PER = (BLK + NT - 1) / NT;
-    constexpr int RING = G + 1;                           // table blocks in flight
-    __shared__ R sD[RING * BLK];
-    __shared__ T H[(G > 1 ? G - 1 : 1) * 2 * PF * 64];    // handoff: [g][parity][step][lane]
-    const bool first = int64_t(blockIdx.x) < nblk_a;
-    RotJob<T, R> const& J = first ? ja : jb;
-    const int lane = threadIdx.x & 63, g = threadIdx.x >> 6, tid = threadIdx.x;
-    const int64_t r = (first ? int64_t(blockIdx.x) : int64_t(blockIdx.x) - nblk_a) * 64 + lane;
-    const bool live = r < J.rows;
-    T* row = J.M + (live ? r : 0);
-    const int64_t ld = J.ld, p0 = J.p0, p1 = J.p1;
-    const R* D = J.D;
-    const int64_t tend = p1 - 2 + 2 * (K - 1);
-    const int64_t dtot = (tend - p0 + 1) * 2 * K;
-    const int64_t nblocks = (tend - p0 + PF) / PF;
-    R nxt[PER];
-    auto fetch = [&](int64_t b) {
-        const int64_t base = b * BLK;
-        #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int64_t o = tid + int64_t(NT) * i, idx = base + o;
-            nxt[i] = (o < BLK && idx < dtot) ? D[idx] : R(0);
-        }
-    };
-    auto stash = [&](int64_t b) {
-        R* dst = sD + (b % RING) * BLK;
-        #pragma unroll
-        for (int i = 0; i < PER; ++i) {
-            const int o = tid + NT * i;
-            if (o < BLK) dst[o] = nxt[i];
-        }
-    };
-    fetch(0);
-    stash(0);
-    if (nblocks > 1) fetch(1);
-    // window: w[2S-2-2s'], w[2S-1-2s'] = the pair of local sweep s'
-    T w[2 * S];
-    #pragma unroll
-    for (int i = 0; i < 2 * S; ++i) w[i] = T();
-    T pf[PF];
-    if (g == 0) {
-        if (live) {
-            w[2 * S - 2] = row[p0 * ld];
-            w[2 * S - 1] = (p0 + 1 < p1) ? row[(p0 + 1) * ld] : T();
-        }
-        #pragma unroll
-        for (int i = 0; i < PF; ++i) {
-            const int64_t cpf = p0 + 2 + i;
-            pf[i] = (live && cpf < p1) ? row[cpf * ld] : T();
-        }
-    }
-    __syncthreads();
-    T* Hin = H + (g > 0 ? (g - 1) : 0) * 2 * PF * 64;     // from wave g-1
-    T* Hout = H + (g < G - 1 ? g : 0) * 2 * PF * 64;      // to wave g+1
-    for (int64_t it = 0; it < nblocks + G - 1; ++it) {
-        // table block it + 1 lands in the ring (wave 0 needs it next)
-        if (it + 1 < nblocks) stash(it + 1);
-        if (it + 2 < nblocks) fetch(it + 2);
-        const int64_t b = it - g;
-        if (b >= 0 && b < nblocks) {
-            const R* cb = sD + (b % RING) * BLK;
-            const int par = int(b & 1);
-            // the block's incoming columns into registers up front: Hin and
-            // Hout share one LDS array, so per-step reads could not be
-            // hoisted above the previous step's handoff store
-            T hin[PF];
-            if (g > 0) {
-                #pragma unroll
-                for (int u = 0; u < PF; ++u) hin[u] = Hin[(par * PF + u) * 64 + lane];
-            }
-            #pragma unroll
-            for (int u = 0; u < PF; ++u) {
-                const int64_t tau = p0 + b * PF + u;
-                if (tau > tend) break;
-                const R* cs = cb + 2 * K * u + 2 * S * g;
-                #pragma unroll
-                for (int s = 0; s < S; ++s) {
-                    const R c = cs[2 * s], sn = cs[2 * s + 1];
-                    const T x = w[2 * S - 2 - 2 * s], y = w[2 * S - 1 - 2 * s];
-                    w[2 * S - 2 - 2 * s] = x * c - y * sn;
-                    w[2 * S - 1 - 2 * s] = x * sn + y * c;
-                }
-                if (g == G - 1) {
-                    const int64_t cr = tau - 2 * K + 2;
-                    if (live && cr >= p0) row[cr * ld] = w[0];
-                } else {
-                    Hout[(par * PF + u) * 64 + lane] = w[0];
-                }
-                #pragma unroll
-                for (int i = 0; i < 2 * S - 1; ++i) w[i] = w[i + 1];
-                if (g == 0) {
-                    w[2 * S - 1] = pf[u];                  // column tau + 2
-                    const int64_t cn = tau + 2 + PF;
-                    pf[u] = (live && cn < p1) ? row[cn * ld] : T();
-                } else {
-                    w[2 * S - 1] = hin[u];
-                }
-            }
-        }
-        // LDS-only barrier: __syncthreads()'s workgroup fence waits vmcnt(0),
-        // which would drain wave 0's column prefetch ring and wave G-1's
-        // stores every block
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-        asm volatile("" ::: "memory");
-    }
-    if (g == G - 1 && live && p1 - 1 >= p0) row[(p1 - 1) * ld] = w[0];
-}
-
 // one rotation on columns (a, b): [x y] <- [x c + y s, y c - x s]
 template <typename T, typename R>
 __global__ __launch_bounds__(256) void rot_cols_kernel(int64_t rows, T* M, int64_t ld, int64_t a, int64_t b, R c,
@@ -293,16 +166,13 @@ void rot_sweeps2(int64_t rows_a, T* A, int64_t lda, int64_t pa0, int64_t pa1, co
     if (!ua && !ub) return;
     RotJob<T, rt<T>> ja{ua ? rows_a : 0, A, lda, pa0, pa1, Da}, jb{ub ? rows_b : 0, B, ldb, pb0, pb1, Db};
     const int64_t na = (ja.rows + 63) / 64, nbk = (jb.rows + 63) / 64;
-    // SLATE_ROT_PIPE=1: the four-wave pipelined kernel (A/B)
-    static const bool pipe = [] {
-        const char* e = std::getenv("SLATE_ROT_PIPE");
-        return e && std::atoi(e) != 0;
-    }();
-    if (pipe) {
-        hipLaunchKernelGGL((rot_sweeps_pipe_kernel<T, rt<T>, kRotBatch, 4, kRotPrefetch>), dim3((unsigned)(na + nbk)),
-                           dim3(256), 0, s, ja, jb, na);
-        return;
-    }
+    // (neither a four-wave variant of this kernel -- the 16 sweeps split over
+    // the SIMDs of a CU, columns handed between waves through LDS -- nor
+    // multishift rounds in the host loop made bdsqr faster: svd n = 8192
+    // bdsqr 1.44 s here against 2.17 s (four waves, even with an LDS-only
+    // barrier and the handoff read ahead) and 1.80-1.97 s (two / three
+    // shifts: cheaper host sweeps, but more of them for this kernel, which
+    // already takes about as long as the host loop); profiles/r4_rot_pipe_ab.txt)
     hipLaunchKernelGGL((rot_sweeps_kernel<T, rt<T>, kRotBatch>), dim3((unsigned)(na + nbk)), dim3(64), 0, s, ja, jb,
                        na);
 }

@@ -802,100 +802,6 @@ int64_t stedc(int64_t n, R* d, R* e, R* Q, int64_t ldq) {
     return 0;
 }
 
-namespace {
-
-/// Shifts per multishift round of bdsqr (SLATE_BDSQR_SHIFTS, 1..8; 1: the
-/// single-shift sweep only).
-int bdsqr_shifts() {
-    static const int m = [] {
-        const char* e = std::getenv("SLATE_BDSQR_SHIFTS");
-        const int v = e ? std::atoi(e) : 1;
-        return std::max(1, std::min(v, 8));
-    }();
-    return m;
-}
-
-/// One multishift round of bdsqr_core on the unreduced block [l, k]: M
-/// implicit-shift sweeps whose shifts are the singular values of the block's
-/// trailing M x M bidiagonal, run INTERLEAVED -- sweep i is two steps behind
-/// sweep i-1 (its step j reads w[j+1], rv1[j+1], which sweep i-1 finalizes at
-/// its step j+1, and writes only below what sweep i-1 still reads), so the
-/// result and every rotation equal M consecutive single sweeps with these
-/// shifts, while the M dependency chains (two sqrt + two divisions per step
-/// each) overlap in the core instead of running back to back: the chase is
-/// latency-bound, and bdsqr's host loop is the SVD's critical path (the
-/// device applies the rotations faster than this loop makes them).  The
-/// rotation lists go to the sink sweep by sweep, in order.  Returns false
-/// (nothing done) for short blocks.
-template <typename R>
-bool bdsqr_multi_sweep(int64_t l, int64_t k, R* w, R* rv1, RotSink<R>* sink) {
-    constexpr int MX = 8;
-    const int M = bdsqr_shifts();
-    if (M < 2 || k - l + 1 < 8 * int64_t(M) || w[l] == R(0)) return false;
-    R sh[MX], tb[MX];
-    for (int i = 0; i < M; ++i) sh[i] = w[k - M + 1 + i];
-    for (int i = 0; i + 1 < M; ++i) tb[i] = rv1[k - M + 2 + i];
-    if (bdsqr_core<R>(M, sh, tb, nullptr) != 0) return false;
-    thread_local std::vector<PlaneRot<R>> lu[MX], lv[MX];
-    for (int i = 0; i < M; ++i) {
-        lu[i].clear();
-        lv[i].clear();
-        if (sink) { lu[i].reserve(size_t(k - l)); lv[i].reserve(size_t(k - l)); }
-    }
-    R c[MX], s[MX], f[MX], x[MX];
-    const int64_t nsteps = k - l;   // j = l .. k-1
-    for (int64_t t = 0; t < nsteps + 2 * (M - 1); ++t) {
-        for (int i = 0; i < M; ++i) {
-            const int64_t j = l + t - 2 * int64_t(i);
-            if (j < l || j >= k) continue;
-            if (j == l) {
-                // (x - sigma)(x + sigma) / x: the first column of B^T B - sigma^2 I, scaled
-                const R xl = w[l];
-                x[i] = xl;
-                f[i] = xl != R(0) ? (xl - sh[i]) * (xl + sh[i]) / xl : R(0);
-                c[i] = R(1);
-                s[i] = R(1);
-            }
-            const int64_t ii = j + 1;
-            R g = rv1[ii], y = w[ii];
-            R h = s[i] * g;
-            g = c[i] * g;
-            R z = fast_hypot(f[i], h);
-            rv1[j] = z;
-            R rz = z != R(0) ? R(1) / z : R(0);
-            R cc = z != R(0) ? f[i] * rz : R(1);
-            R ss = h * rz;
-            R ff = x[i] * cc + g * ss;
-            g = g * cc - x[i] * ss;
-            h = y * ss;
-            y *= cc;
-            if (sink) lv[i].push_back(PlaneRot<R>{j, cc, -ss});
-            z = fast_hypot(ff, h);
-            w[j] = z;
-            if (z != R(0)) {
-                rz = R(1) / z;
-                cc = ff * rz;
-                ss = h * rz;
-            }
-            f[i] = cc * g + ss * y;
-            x[i] = cc * y - ss * g;
-            c[i] = cc;
-            s[i] = ss;
-            if (sink) lu[i].push_back(PlaneRot<R>{j, cc, -ss});
-            if (j == k - 1) {
-                rv1[l] = 0;
-                rv1[k] = f[i];
-                w[k] = x[i];
-            }
-        }
-    }
-    if (sink)
-        for (int i = 0; i < M; ++i) sink->sweep(lu[i], lv[i]);
-    return true;
-}
-
-}  // namespace
-
 //------------------------------------------------------------------------------
 // Golub-Reinsch implicit-shift QR on the upper bidiagonal (EISPACK svd).
 template <typename R>
@@ -942,7 +848,6 @@ int64_t bdsqr_core(int64_t n, R* w, R* e, RotSink<R>* sink) {
                 break;
             }
             if (its == 74) { ++fail; break; }
-            if (bdsqr_multi_sweep<R>(l, k, w, rv1.data(), sink)) continue;
             R x = w[l];
             nm = k - 1;
             R y = w[nm], g = rv1[nm], h = rv1[k];
