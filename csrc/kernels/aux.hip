@@ -275,146 +275,6 @@ void potrf_small_kernel(char uplo, int n, T* A, int64_t lda, int* info, int info
 }
 
 //------------------------------------------------------------------------------
-// Lower Cholesky of a whole diagonal block (n <= 512, real types) in ONE
-// workgroup: 32-column panels, each (1) factored by one wave (lane = row,
-// readlane broadcasts) with its inverse, (2) the rows below solved against
-// L11^{-H} into LDS and back to memory, (3) the trailing lower triangle
-// updated by all four waves in 4 x 4 register tiles from the LDS panel.  The
-// blocked form (potrf_inv_small + three more launches per 64 columns, 32
-// launches for nb = 512) sat ~1.9 ms per step on the factorization's
-// critical path behind the trailing GEMM's workgroups; this is one launch
-// that keeps its CU once resident.  The block stays L2-resident (2 MB).
-template <typename T>
-__global__ __launch_bounds__(256)
-void potrf_block_kernel(int n, T* A, int64_t lda, int* info, int info_offset) {
-    SLATE_PANEL_WAVE_PRIO();
-    constexpr int P = 32, MAXN = 512;
-    __shared__ T D[P][P + 1];
-    __shared__ T Li[P][P + 1];
-    __shared__ T X[MAXN - P][P + 1];
-    __shared__ int fail_s;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    if (tid == 0) fail_s = 0;
-    for (int j0 = 0; j0 < n; j0 += P) {
-        const int pb = min(P, n - j0), mr = n - j0 - pb;
-        T* A11 = A + j0 + (int64_t)j0 * lda;
-        for (int e = tid; e < P * P; e += 256) {
-            const int i = e % P, c = e / P;
-            D[i][c] = (i < pb && c < pb && i >= c) ? A11[i + (int64_t)c * lda] : zero<T>();
-        }
-        __syncthreads();
-        if (wv == 0) {
-            // unblocked Cholesky, lane i = row i (lanes >= pb idle)
-            T a[P];
-            #pragma unroll
-            for (int l = 0; l < P; ++l) a[l] = (lane < P) ? D[lane][l] : zero<T>();
-            int fail = 0;
-            #pragma unroll
-            for (int j = 0; j < P; ++j) {
-                if (j < pb) {
-                    T s = a[j];
-                    #pragma unroll
-                    for (int l = 0; l < j; ++l) s -= a[l] * bcast_lane(a[l], j);
-                    const T d = bcast_lane(s, j);
-                    if (!(d > T(0)) && fail == 0) fail = j + 1;
-                    const T sd = sqrt(d);
-                    if (lane == j) a[j] = sd;
-                    else if (lane > j) a[j] = s / sd;
-                }
-            }
-            if (fail && lane == 0 && fail_s == 0) fail_s = j0 + fail;
-            if (lane < P) {
-                #pragma unroll
-                for (int l = 0; l < P; ++l)
-                    D[lane][l] = (lane < pb && l < pb && l <= lane) ? a[l] : ((lane == l) ? T(1) : zero<T>());
-            }
-        }
-        __syncthreads();
-        if (wv == 0 && lane < P) {
-            // column j = lane of L11^{-1} by forward substitution
-            const int j = lane;
-            T x[P];
-            #pragma unroll
-            for (int i = 0; i < P; ++i) {
-                T s = zero<T>();
-                #pragma unroll
-                for (int l = 0; l < i; ++l) s += D[i][l] * x[l];
-                const T rd = T(1) / D[i][i];
-                x[i] = (i < j) ? zero<T>() : ((i == j) ? rd : -(s * rd));
-            }
-            #pragma unroll
-            for (int i = 0; i < P; ++i) Li[i][j] = x[i];
-        } else if (wv == 1) {
-            for (int e = lane; e < P * P; e += 64) {
-                const int i = e % P, c = e / P;
-                if (i < pb && c < pb && i >= c) A11[i + (int64_t)c * lda] = D[i][c];
-            }
-        }
-        __syncthreads();
-        // rows below: X = A21 L11^{-T}, X[r][c] = sum_{l <= c} A21[r][l] Li[c][l]
-        T* A21 = A11 + pb;
-        for (int r = tid; r < mr; r += 256) {
-            // x = sum_l a[l] Li[:, l] (Li is zero above its diagonal); the
-            // l loop stays rolled so the Li broadcasts are not all hoisted
-            // into registers
-            T x[P];
-            #pragma unroll
-            for (int c = 0; c < P; ++c) x[c] = zero<T>();
-            for (int l = 0; l < pb; ++l) {
-                const T al = A21[r + (int64_t)l * lda];
-                #pragma unroll
-                for (int c = 0; c < P; ++c) x[c] += al * Li[c][l];
-            }
-            #pragma unroll
-            for (int c = 0; c < P; ++c) {
-                X[r][c] = x[c];
-                if (c < pb) A21[r + (int64_t)c * lda] = x[c];
-            }
-        }
-        __syncthreads();
-        // trailing lower triangle: A22[i][k] -= sum_c X[i][c] X[k][c], i >= k,
-        // in 4 x 4 tiles (bi >= bk)
-        if (mr > 0) {
-            T* A22 = A11 + pb + (int64_t)pb * lda;
-            const int nt4 = (mr + 3) / 4, ntiles = nt4 * (nt4 + 1) / 2;
-            for (int t = tid; t < ntiles; t += 256) {
-                int bi = int((sqrtf(8.0f * float(t) + 1.0f) - 1.0f) * 0.5f);
-                while (bi * (bi + 1) / 2 > t) --bi;
-                while ((bi + 1) * (bi + 2) / 2 <= t) ++bi;
-                const int bk = t - bi * (bi + 1) / 2;
-                T acc[4][4];
-                #pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    #pragma unroll
-                    for (int q = 0; q < 4; ++q) acc[p][q] = zero<T>();
-                for (int c = 0; c < pb; ++c) {
-                    T xi[4], xk[4];
-                    #pragma unroll
-                    for (int p = 0; p < 4; ++p) {
-                        const int i = 4 * bi + p, k = 4 * bk + p;
-                        xi[p] = i < mr ? X[i][c] : zero<T>();
-                        xk[p] = k < mr ? X[k][c] : zero<T>();
-                    }
-                    #pragma unroll
-                    for (int p = 0; p < 4; ++p)
-                        #pragma unroll
-                        for (int q = 0; q < 4; ++q) acc[p][q] += xi[p] * xk[q];
-                }
-                #pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int i = 4 * bi + p, k = 4 * bk + q;
-                        if (i < mr && k < mr && i >= k) A22[i + (int64_t)k * lda] -= acc[p][q];
-                    }
-            }
-        }
-        __syncthreads();
-    }
-    if (tid == 0 && fail_s && info && *info == 0) *info = info_offset + fail_s;
-}
-
-//------------------------------------------------------------------------------
 // Lower Cholesky of a small (n <= 64) diagonal block AND the inverse of its
 // factor in one launch: the factorization as potrf_small (lane i owns row i),
 // then the factor goes through LDS and lane j computes column j of L^{-1} by
@@ -617,14 +477,6 @@ __global__ void laswp_kernel(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k
 
 //------------------------------------------------------------------------------
 // launchers
-template <typename T>
-void potrf_block(int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s) {
-    if (n <= 0) return;
-    hipLaunchKernelGGL(potrf_block_kernel<T>, dim3(1), dim3(256), 0, s, n, A, lda, info, info_offset);
-}
-template void potrf_block<float>(int, float*, int64_t, int*, int, hipStream_t);
-template void potrf_block<double>(int, double*, int64_t, int*, int, hipStream_t);
-
 template <typename T>
 void geset(char uplo, int64_t m, int64_t n, T offdiag, T diag, T* A, int64_t lda, hipStream_t s) {
     if (m <= 0 || n <= 0) return;

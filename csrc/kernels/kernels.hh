@@ -257,10 +257,6 @@ void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset
 /// Lower Cholesky of an n <= 64 block (in place) plus the 64 x 64 inverse of its factor in W
 template <typename T>
 void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int info_offset, hipStream_t s);
-/// Lower Cholesky of an n x n block, n <= 512, real types, in one workgroup
-/// (32-column panels; see aux.hip).
-template <typename T>
-void potrf_block(int n, T* A, int64_t lda, int* info, int info_offset, hipStream_t s);
 /// Left NoTrans triangular solve A X = B with m <= 64 (alpha = 1), one launch
 template <typename T>
 void trsm_small(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb, hipStream_t s);

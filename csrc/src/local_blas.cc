@@ -621,19 +621,6 @@ void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int
         const char* e = std::getenv("SLATE_POTRF_REC_MAX");
         return e ? std::atoll(e) : int64_t(0);
     }();
-    // one-workgroup Cholesky of the whole block (real types, n <= 512): one
-    // launch instead of four per 64 columns on the factorization's critical
-    // path.  SLATE_POTRF_BLOCK=0 keeps the blocked launches.
-    static const bool one_wg = [] {
-        const char* e = std::getenv("SLATE_POTRF_BLOCK");
-        return !e || std::atoi(e) != 0;
-    }();
-    if constexpr (!is_complex_v<T>) {
-        if (uplo == Uplo::Lower && one_wg && n <= 512) {
-            kd::potrf_block(int(n), dptr(A), lda, info, int(info_offset), c.stream);
-            return;
-        }
-    }
     if (uplo == Uplo::Lower && blocked && (rec_max <= 0 || n <= rec_max)) {
         // Right-looking over 64-column leaves, four launches per leaf: the
         // leaf's factor and its inverse in one kernel, the rows below as one
