@@ -303,7 +303,7 @@ bool unmtr_he2hb_local(Matrix<T>& F, std::vector<TriangularFactors<T>> const& Ts
                        Options const& opts) {
     static const int64_t GB = [] {
         const char* e = std::getenv("SLATE_UNMTR_GROUP");
-        return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(4);
+        return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1);
     }();
     const int64_t nt = F.nt(), n = F.n(), kd = F.nb();
     if (GB <= 1 || nt < 2 || F.grid()->size() != 1 || Zw.grid()->size() != 1 || F.arbitrary_layout() ||
