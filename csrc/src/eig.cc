@@ -18,7 +18,6 @@
 #include "internal.hh"
 #include "eig_sinks.hh"
 #include "slate_amd/eig_host.hh"
-#include "slate_amd/host_blas.hh"
 #include "../kernels/kernels.hh"
 
 #include <algorithm>
@@ -287,74 +286,6 @@ bool he2hb_local(Matrix<T>& A, std::vector<TriangularFactors<T>>& Ts, Options co
         Ts[k].push_back(Tf);
     }
     if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    return true;
-}
-
-/// unmtr_he2hb on one process: Z(kd:, :) := Q1 Z(kd:, :) with the he2hb
-/// panels taken GB at a time as ONE block reflector (V the union of their
-/// unit-lower trapezoids, T rebuilt from V^H V and the panels' taus, which
-/// are their T's diagonals), so each application is a rank-GB kd update
-/// (larfb) instead of GB rank-kd ones -- the kd = 64 panels ran their
-/// GEMMs at low efficiency (unmtr_he2hb 105 ms at n = 8192).  Blocks are
-/// applied last first (Q1 = H_0 H_1 ...).  SLATE_UNMTR_GROUP = GB (1: the
-/// per-panel unmqr).
-template <typename T>
-bool unmtr_he2hb_local(Matrix<T>& F, std::vector<TriangularFactors<T>> const& Ts, Matrix<T>& Zw,
-                       Options const& opts) {
-    static const int64_t GB = [] {
-        const char* e = std::getenv("SLATE_UNMTR_GROUP");
-        return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(1);
-    }();
-    const int64_t nt = F.nt(), n = F.n(), kd = F.nb();
-    if (GB <= 1 || nt < 2 || F.grid()->size() != 1 || Zw.grid()->size() != 1 || F.arbitrary_layout() ||
-        Zw.arbitrary_layout() || F.op() != Op::NoTrans || Zw.op() != Op::NoTrans || F.mb() != F.nb() ||
-        int64_t(Ts.size()) < nt - 1)
-        return false;
-    for (int64_t k = 0; k + 1 < nt; ++k)
-        if (Ts[k].empty()) return false;
-    trace::Block tb("unmtr_he2hb_blocked");
-    Target target = resolve_target(opts);
-    const Loc loc = loc_of(target);
-    lb::Ctx c = target == Target::Devices ? lb::Ctx::device(0) : lb::Ctx::host();
-    LocalBlock<T> lf = F.local(loc, false), lz = Zw.local(loc, true);
-    const int64_t np = nt - 1, W = GB * kd;
-    Work<T> V(target, size_t(std::max<int64_t>(n, 1)) * W), Tg(target, size_t(W) * W), Tb(target, size_t(W) * W);
-    std::vector<T> tau_h(static_cast<size_t>(W));
-    Work<T> tau_d(target, size_t(W));
-    for (int64_t b0 = ((np - 1) / GB) * GB; b0 >= 0; b0 -= GB) {
-        const int64_t b1 = std::min(np, b0 + GB);
-        const int64_t c0 = b0 * kd, r0 = (b0 + 1) * kd, m = n - r0;
-        if (m <= 0) continue;
-        int64_t w = 0;
-        for (int64_t k = b0; k < b1; ++k) w += F.tileNb(k);
-        const int64_t K = std::min(w, m);
-        // explicit V: F(r0:, c0:c0+K), unit diagonal, zeros above
-        lb::copy2d(c, m, K, lf.ptr + r0 + c0 * lf.ld, lf.ld, V.data(), m);
-        lb::set(c, Uplo::Upper, std::min(m, K), K, T(0), T(1), V.data(), m);
-        // taus: the diagonals of the panels' T factors
-        for (int64_t k = b0, off = 0; k < b1 && off < K; off += F.tileNb(k), ++k) {
-            LocalBlock<T> lt = Ts[k][0].local(loc, false);
-            const int64_t cnt = std::min(F.tileNb(k), K - off);
-            if (c.dev())
-                device::memcpy2d_async(tau_d.data() + off, sizeof(T), lt.ptr, (lt.ld + 1) * sizeof(T), sizeof(T), cnt,
-                                       c.stream);
-            else
-                for (int64_t i = 0; i < cnt; ++i) tau_h[size_t(off + i)] = lt.ptr[i * (lt.ld + 1)];
-        }
-        if (c.dev()) {
-            // T^{-1} = striu(V^H V) + diag(1 / tau), then T
-            lb::gemm(c, is_complex_v<T> ? Op::ConjTrans : Op::Trans, Op::NoTrans, K, K, m, T(1), V.data(), m, V.data(),
-                     m, T(0), Tg.data(), K);
-            slate_amd::dev::tinv_from_gram(K, slate_amd::dev::dptr(Tg.data()), K, slate_amd::dev::dptr(tau_d.data()),
-                                           c.stream);
-            lb::trtri_to(c, Uplo::Upper, Diag::NonUnit, K, Tg.data(), K, Tb.data(), K);
-        } else {
-            host::larft(m, K, V.data(), m, tau_h.data(), Tb.data(), K);
-        }
-        lb::larfb(c, Side::Left, Op::NoTrans, m, lz.n, K, V.data(), m, Tb.data(), K, lz.ptr + r0, lz.ld);
-    }
-    if (c.dev()) slate_hip_call(hipStreamSynchronize(c.stream));
-    internal::finish_origin(Zw, opts);
     return true;
 }
 
@@ -940,7 +871,7 @@ void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z
         // panels F(k+1:, k), k = 0 .. nt-2, together: the QR-shaped view
         // F(1:, 0:nt-2) applied to Z(1:, :) in one call
         const int64_t znt = Zw.nt();
-        if (nt >= 2 && !unmtr_he2hb_local(F, Ts, Zw, opts)) {
+        if (nt >= 2) {
             Matrix<T> P = F.sub(1, nt - 1, 0, nt - 2);
             Matrix<T> Zs = Zw.sub(1, nt - 1, 0, znt - 1);
             unmqr(Side::Left, Op::NoTrans, P, stacked_T(Ts, nt - 1, F.nb(), P.n(), opts), Zs, opts);
