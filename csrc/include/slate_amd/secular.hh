@@ -65,8 +65,11 @@ SLATE_SECULAR_FN Sums<R> sums(int64_t k, int64_t j, const R* d, const R* z, int6
 }
 
 /// Root j (0-based) of the secular equation; *org receives the origin pole.
-template <typename R>
-SLATE_SECULAR_FN R root(int64_t k, int64_t j, R rho, const R* d, const R* z, R znorm2, int64_t* org) {
+/// sum_fn(o, t) -> Sums<R> evaluates psi / phi and their derivatives (the
+/// serial `sums` here; the device kernel passes a wave-parallel one, every
+/// lane then runs the same iteration on the same reduced values).
+template <typename R, typename SumFn>
+SLATE_SECULAR_FN R root_with(int64_t k, int64_t j, R rho, const R* d, R znorm2, int64_t* org, SumFn&& sum_fn) {
     const R eps = std::numeric_limits<R>::epsilon();
     const R rhoinv = R(1) / rho;
     const bool last = j + 1 >= k;
@@ -76,13 +79,13 @@ SLATE_SECULAR_FN R root(int64_t k, int64_t j, R rho, const R* d, const R* z, R z
     if (!last) {
         // the sign of w at the midpoint picks the half, and with it the
         // nearer pole as origin
-        const Sums<R> s = sums(k, j, d, z, j, gap / 2);
+        const Sums<R> s = sum_fn(j, gap / 2);
         if (rhoinv + s.psi + s.phi < R(0)) { o = j + 1; a = -gap / 2; b = 0; t = -gap / 4; }
         else { b = gap / 2; t = gap / 4; }
     }
     const R dj0 = d[j] - d[o], dj1 = last ? R(0) : d[j + 1] - d[o];
     for (int it = 0; it < 200; ++it) {
-        const Sums<R> s = sums(k, j, d, z, o, t);
+        const Sums<R> s = sum_fn(o, t);
         const R w = rhoinv + s.psi + s.phi;
         if (w == R(0)) break;
         if (w > R(0)) b = t; else a = t;
@@ -114,6 +117,11 @@ SLATE_SECULAR_FN R root(int64_t k, int64_t j, R rho, const R* d, const R* z, R z
     }
     *org = o;
     return t;
+}
+
+template <typename R>
+SLATE_SECULAR_FN R root(int64_t k, int64_t j, R rho, const R* d, const R* z, R znorm2, int64_t* org) {
+    return root_with<R>(k, j, rho, d, znorm2, org, [&](int64_t o, R t) { return sums(k, j, d, z, o, t); });
 }
 
 }  // namespace secular

@@ -20,6 +20,8 @@
 #include "kernels.hh"
 #include "slate_amd/secular.hh"
 
+#include <cstdlib>
+
 namespace slate_amd {
 namespace dev {
 
@@ -33,6 +35,47 @@ __global__ __launch_bounds__(64) void secular_roots_kernel(int64_t k, double rho
     const double t = slate::secular::root<double>(k, j, rho, dd, zz, znorm2, &o2);
     org[j] = o2;
     tau[j] = t;
+}
+
+// One WAVE per root: the O(k) sums of every iteration are split over the
+// 64 lanes and reduced by an xor butterfly, then lane 0's totals are
+// broadcast so every lane runs the identical (uniform) iteration.  The
+// thread-per-root form left k / 64 waves for the whole chip with each lane
+// walking all k poles per iteration (~1.9 ms a launch, ~60 ms of heev at
+// n = 8192, profiles/r4_eig_kernel_stats_final.txt).
+__global__ __launch_bounds__(256) void secular_roots_wave_kernel(int64_t k, double rho, const double* dd,
+                                                                const double* zz, double znorm2, int64_t* org,
+                                                                double* tau) {
+    const int lane = threadIdx.x & 63;
+    const int64_t j = int64_t(blockIdx.x) * 4 + (threadIdx.x >> 6);
+    if (j >= k) return;   // wave-uniform
+    auto wsum = [&](int64_t o, double t) {
+        slate::secular::Sums<double> s;
+        const double d0 = dd[o];
+        for (int64_t i = lane; i < k; i += 64) {
+            const double r = zz[i] / ((dd[i] - d0) - t);
+            if (i <= j) { s.psi += zz[i] * r; s.dpsi += r * r; }
+            else { s.phi += zz[i] * r; s.dphi += r * r; }
+        }
+        #pragma unroll
+        for (int off = 32; off > 0; off >>= 1) {
+            s.psi += __shfl_xor(s.psi, off);
+            s.phi += __shfl_xor(s.phi, off);
+            s.dpsi += __shfl_xor(s.dpsi, off);
+            s.dphi += __shfl_xor(s.dphi, off);
+        }
+        s.psi = __shfl(s.psi, 0);
+        s.phi = __shfl(s.phi, 0);
+        s.dpsi = __shfl(s.dpsi, 0);
+        s.dphi = __shfl(s.dphi, 0);
+        return s;
+    };
+    int64_t o2 = j;
+    const double t = slate::secular::root_with<double>(k, j, rho, dd, znorm2, &o2, wsum);
+    if (lane == 0) {
+        org[j] = o2;
+        tau[j] = t;
+    }
 }
 
 __global__ __launch_bounds__(64) void gu_eisenstat_kernel(int64_t k, double rho, const double* dd, const double* zz,
@@ -121,6 +164,16 @@ __global__ __launch_bounds__(256) void merge_matrix_kernel(MergeArgs a, int64_t 
 void secular_roots(int64_t k, double rho, const double* dd, const double* zz, double znorm2, int64_t* org, double* tau,
                    hipStream_t s) {
     if (k <= 0) return;
+    // SLATE_SECULAR_WAVE=0: one thread per root (A/B)
+    static const bool wave = [] {
+        const char* e = std::getenv("SLATE_SECULAR_WAVE");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (wave) {
+        hipLaunchKernelGGL(secular_roots_wave_kernel, dim3((unsigned)((k + 3) / 4)), dim3(256), 0, s, k, rho, dd, zz,
+                           znorm2, org, tau);
+        return;
+    }
     hipLaunchKernelGGL(secular_roots_kernel, dim3((unsigned)((k + 63) / 64)), dim3(64), 0, s, k, rho, dd, zz, znorm2,
                        org, tau);
 }
