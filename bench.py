@@ -33,8 +33,17 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-import slate_d35_amd as s  # noqa: E402
-from slate_d35_amd.utils import flops as F  # noqa: E402
+# The package (and with it the HIP runtime) is imported by the ranks only:
+# a self-launching parent (launch_ranks) must not touch the GPU.
+s = None
+F = None
+
+
+def _import_slate():
+    global s, F
+    import slate_d35_amd as s_  # noqa: E402
+    from slate_d35_amd.utils import flops as F_  # noqa: E402
+    s, F = s_, F_
 
 METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
 ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
@@ -120,8 +129,100 @@ def parse():
     return ap.parse_args()
 
 
-def main():
-    a = parse()
+def launch_ranks(a) -> int:
+    """`python bench.py --gpus N` without a launcher: start N rank processes
+    (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR / MASTER_PORT, the
+    environment torchrun would give them; the reference's runner wraps itself
+    in `mpirun -np N` the same way, test/run_tests.py:127-173).  This parent
+    never imports the extension nor initialises the GPU, and never execs:
+    the ranks are fresh child processes.  They write straight to this
+    process's stdout / stderr (rank 0 prints the JSON line).  When a rank
+    fails the others get a grace period (their own watchdogs fire first),
+    then the whole set is killed; the exit code is the first failing rank's.
+    SLATE_BENCH_FAKE_HOSTS=1 gives every rank its own NCCL_HOSTID, so that N
+    ranks can rehearse the RCCL path on ONE GPU (RCCL's socket transport
+    over loopback instead of refusing a duplicate device)."""
+    import signal
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    n = a.gpus
+    fake = os.environ.get("SLATE_BENCH_FAKE_HOSTS", "0") == "1"
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   SLATE_MASTER_PORT=str(port), SLATE_BENCH_LAUNCHER="self")
+        if fake:
+            env.update(NCCL_HOSTID=f"slate-bench-host-{r}", NCCL_SOCKET_IFNAME="lo")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env,
+                                      start_new_session=True))
+
+    def kill_all(sig):
+        for p in procs:
+            if p.poll() is None:
+                try:
+                    os.killpg(p.pid, sig)
+                except ProcessLookupError:
+                    pass
+
+    def on_term(signum, _frame):
+        kill_all(signal.SIGTERM)
+        raise SystemExit(128 + signum)
+
+    signal.signal(signal.SIGTERM, on_term)
+    signal.signal(signal.SIGINT, on_term)
+    limit = float(os.environ.get("SLATE_BENCH_LAUNCH_TIMEOUT", "0")) or None
+    grace = float(os.environ.get("SLATE_BENCH_RANK_GRACE", "60"))
+    rc, failed_at = 0, None
+    t0 = time.time()
+    while True:
+        codes = [p.poll() for p in procs]
+        bad = [c for c in codes if c not in (None, 0)]
+        if bad and rc == 0:
+            rc, failed_at = bad[0], time.time()
+            print(f"# launcher: a rank exited with {rc}; stopping the others within {grace:.0f} s",
+                  file=sys.stderr, flush=True)
+        if all(c is not None for c in codes):
+            break
+        if failed_at is not None and time.time() - failed_at > grace:
+            kill_all(signal.SIGKILL)
+        if limit and time.time() - t0 > limit:
+            print(f"# launcher: time limit {limit:.0f} s reached; killing the ranks", file=sys.stderr, flush=True)
+            kill_all(signal.SIGKILL)
+            rc = rc or 124
+        time.sleep(0.2)
+    for p in procs:
+        p.wait()
+    return rc
+
+
+def comm_info(grid, world):
+    """What the communicators actually created report: transport name and
+    sizes (RCCL: ncclCommCount), plus every rank's HIP device
+    (ncclCommCuDevice for RCCL comms, else the process's current device)."""
+    info = {"backend": "self" if world == 1 else grid.world.name(), "world": grid.world.size() if world > 1 else 1,
+            "row": grid.row_comm.size() if world > 1 else 1, "col": grid.col_comm.size() if world > 1 else 1,
+            "grid": [grid.p, grid.q]}
+    dev = s._slate.get_device() if s.device_available() else -1
+    if world > 1:
+        d = grid.world.device()
+        dev = d if d >= 0 else dev
+        v = [0] * world
+        v[grid.world.rank()] = dev + 1
+        info["devices"] = [x - 1 for x in grid.world.allreduce_sum_i64(v)]
+        info["fast_lane"] = bool(grid.has_fast_lane)
+    else:
+        info["devices"] = [dev]
+    info["launcher"] = os.environ.get("SLATE_BENCH_LAUNCHER", "torchrun" if "TORCHELASTIC_RUN_ID" in os.environ
+                                      else ("env" if world > 1 else "none"))
+    return info
+
+
+def main(a):
+    _import_slate()
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     if world != a.gpus:
@@ -133,7 +234,10 @@ def main():
     wd = Watchdog(rank)
     wd.arm("init_grid")
     grid = s.init_grid(p, q)
+    comm = comm_info(grid, world)
     wd.disarm()
+    if rank == 0:
+        print(f"# comm: {json.dumps(comm)}", file=sys.stderr, flush=True)
     n = a.n
     # Default tiles: 512 everywhere, except on one GPU where dgetrf / dpotrf
     # run 2-4% faster at nb = 1024 (profiles/nb_sweep_r1_n65536_1gpu.txt:
@@ -397,7 +501,9 @@ def main():
             "model": "+".join(f"{k}(nb={v['nb']})" for k, v in results.items()) + f" n={n}",
             "global_batch": 1,
             "seq_len": n,
-            "parallelism": f"2d-block-cyclic {p}x{q} (one process per GPU, RCCL)" if world > 1 else "1x1",
+            "parallelism": (f"2d-block-cyclic {p}x{q} (one process per GPU, {comm['backend']})" if world > 1
+                            else "1x1"),
+            "comm": comm,
             "lookahead": {k: la_of(k) for k in results} if not a.lookahead else a.lookahead,
             "lu_method": a.method_lu,
         },
@@ -415,4 +521,7 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
+    main(args)

@@ -49,6 +49,8 @@ public:
 
     /// Can the transport read/write device memory directly (stream-ordered)?
     virtual bool device_native() const { return false; }
+    /// HIP device the communicator is bound to (RCCL: ncclCommCuDevice), -1 if none.
+    virtual int device() const { return -1; }
 
     // ---- raw transport operations (buffers in the transport's native space:
     // device memory if device_native(), else host memory).  `stream` orders

@@ -389,6 +389,7 @@ PYBIND11_MODULE(_slate, m) {
         .def("rank", &Comm::rank)
         .def("size", &Comm::size)
         .def("name", &Comm::name)
+        .def("device", &Comm::device)
         .def("barrier", &Comm::barrier, py::call_guard<py::gil_scoped_release>())
         .def("allreduce_sum_i64", [](Comm& c, std::vector<int64_t> v) {
             if (!v.empty()) c.allreduce(v.data(), v.data(), v.size(), ScalarType::Int64, ReduceOp::Sum, Loc::Host, nullptr);

@@ -77,6 +77,10 @@ public:
     int size() const override { return size_; }
     std::string name() const override { return "rccl"; }
     bool device_native() const override { return true; }
+    int device() const override {
+        int d = -1;
+        return ncclCommCuDevice(comm_, &d) == ncclSuccess ? d : -1;
+    }
     ncclComm_t raw() const { return comm_; }
 
     void bcast_raw(void* buf, size_t count, ScalarType t, int root, hipStream_t s) override {
