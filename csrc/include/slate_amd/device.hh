@@ -45,6 +45,9 @@ int  count();
 
 /// Select the device used by this process (default: $LOCAL_RANK % count).
 void set_device(int dev);
+/// Did the program choose its device (set_device)?  Then the single-process
+/// APIs stay on it instead of spreading over every visible GPU.
+bool device_explicit();
 int  get_device();
 
 /// Device contexts (intra-process multi-GPU).  A context is one rank's view
@@ -113,7 +116,9 @@ class Buffer {
 public:
     Buffer() = default;
     explicit Buffer(size_t n) { resize(n); }
-    ~Buffer() { reset(); }
+    // never throw out of a destructor (an exception already unwinding through
+    // the owner would become std::terminate and hide the original error)
+    ~Buffer() { try { reset(); } catch (...) {} }
     Buffer(Buffer const&) = delete;
     Buffer& operator=(Buffer const&) = delete;
     Buffer(Buffer&& o) noexcept : p_(o.p_), n_(o.n_) { o.p_ = nullptr; o.n_ = 0; }

@@ -31,9 +31,14 @@ void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const
 int64_t inproc_run_count();
 void inproc_last_shape(int& p, int& q);
 
-/// Ranks the single-process APIs (LAPACK-compatible shim) spread work over:
-/// $SLATE_INPROC_RANKS if set, else the number of visible GPUs (1 without).
+/// Ranks the single-process APIs (LAPACK-compatible shim, and the drivers
+/// called on a 1 x 1 grid) spread work over: $SLATE_INPROC_RANKS if set;
+/// else 1 in a multi-process job (WORLD_SIZE / LOCAL_RANK / MPI / Slurm
+/// environment), after set_device, or with a > 1-rank default grid; else
+/// the number of visible GPUs (1 without).
 int inproc_ranks();
+/// True when the environment shows a launcher started several processes.
+bool multi_process_job();
 /// Near-square p x q with p <= q for n ranks (1x1, 1x2, 2x2, 2x4, ...).
 void inproc_grid_shape(int n, int& p, int& q);
 

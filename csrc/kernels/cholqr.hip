@@ -63,19 +63,31 @@ __global__ __launch_bounds__(256) void cholqr_shift_kernel(T* G, int64_t ldg, in
 /// workgroup's loop (which took ~0.9 ms at nb = 512 beside the trailing GEMM).
 /// The flag is cleared by the launcher; only failing lanes store 1.
 template <typename T>
-__global__ __launch_bounds__(256) void cholqr_check_kernel(const T* G, int64_t ldg, int n, double tol, int* flag) {
+__global__ __launch_bounds__(256) void cholqr_check_kernel(const T* G, int64_t ldg, int n, double* ssq) {
+    // ||G - I||_F^2 from the lower triangle (off-diagonal terms twice); a
+    // wave per column, one f64 atomic add per wave.  NaN / Inf propagate.
     using R = real_t<T>;
     const int j = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
     if (j >= n) return;
-    bool bad = false;
+    double acc = 0;
     for (int i = j + lane; i < n; i += 64) {
         T g = G[i + int64_t(j) * ldg];
-        R d;
-        if constexpr (is_cplx<T>::value) d = fabs(g.re - (i == j ? R(1) : R(0))) + fabs(g.im);
-        else d = fabs(g - (i == j ? R(1) : R(0)));
-        bad |= !(d <= R(tol));   // NaN / Inf fail as well
+        double d2;
+        if constexpr (is_cplx<T>::value) {
+            const double re = double(g.re) - (i == j ? 1.0 : 0.0), im = double(g.im);
+            d2 = re * re + im * im;
+        } else {
+            const double d = double(g) - (i == j ? 1.0 : 0.0);
+            d2 = d * d;
+        }
+        acc += (i == j ? 1.0 : 2.0) * d2;
     }
-    if (bad) *flag = 1;
+    acc = wave_sum(acc);
+    if (lane == 0) atomicAdd(ssq, acc);
+}
+
+__global__ void cholqr_verdict_kernel(const double* ssq, double tol, int* flag) {
+    *flag = (*ssq <= tol * tol) ? 0 : 1;   // NaN fails
 }
 
 }  // namespace
@@ -87,15 +99,15 @@ void cholqr_shift(T* G, int64_t ldg, int n, double c, hipStream_t s) {
 }
 
 template <typename T>
-void cholqr_check(const T* G, int64_t ldg, int n, double tol, int* flag, hipStream_t s) {
-    (void)hipMemsetAsync(flag, 0, sizeof(int), s);
-    if (n <= 0) return;
-    cholqr_check_kernel<T><<<(n + 3) / 4, 256, 0, s>>>(G, ldg, n, tol, flag);
+void cholqr_check(const T* G, int64_t ldg, int n, double tol, int* flag, double* ssq, hipStream_t s) {
+    (void)hipMemsetAsync(ssq, 0, sizeof(double), s);
+    if (n > 0) cholqr_check_kernel<T><<<(n + 3) / 4, 256, 0, s>>>(G, ldg, n, ssq);
+    cholqr_verdict_kernel<<<1, 1, 0, s>>>(ssq, tol, flag);
 }
 
 #define SLATE_INST_CHOLQR(T)                                                            \
     template void cholqr_shift<T>(T*, int64_t, int, double, hipStream_t);              \
-    template void cholqr_check<T>(const T*, int64_t, int, double, int*, hipStream_t);
+    template void cholqr_check<T>(const T*, int64_t, int, double, int*, double*, hipStream_t);
 
 SLATE_INST_CHOLQR(float)
 SLATE_INST_CHOLQR(double)

@@ -47,11 +47,11 @@ void panel_xfer(int64_t M, int64_t kb, int64_t kk, RowDist d, PanelBases pb, int
 
 // ---- CholeskyQR panel helpers (cholqr.hip)
 /// G(i,i) += c * trace(G) (the shifted first pass); flag = 1 unless the
-/// lower triangle of G is within tol of the identity (and finite).
+/// ||G - I||_F <= tol (and finite); ssq: one double of scratch.
 template <typename T>
 void cholqr_shift(T* G, int64_t ldg, int n, double c, hipStream_t s);
 template <typename T>
-void cholqr_check(const T* G, int64_t ldg, int n, double tol, int* flag, hipStream_t s);
+void cholqr_check(const T* G, int64_t ldg, int n, double tol, int* flag, double* ssq, hipStream_t s);
 
 // ---- in-process communicator (comm.hip)
 /// out[i] = op_b in[i + b stride], b < nbuf; type 'f' 'd' 'i' (int32) 'l'
@@ -317,6 +317,8 @@ void iota(int64_t n, int64_t* p, hipStream_t s);
 /// device panel: rows [r, m), row interchanges applied over ncols columns of
 /// Apanel; work holds tslu_workspace(m - r) int64 entries.
 int64_t tslu_workspace(int64_t rows);
+/// Zero the tournament's arrival counters (once per panel workspace).
+void tslu_init(int64_t* work, hipStream_t s);
 template <typename T>
 void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
                  int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s);

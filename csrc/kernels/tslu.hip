@@ -27,8 +27,11 @@
 #include "device_common.hh"
 #include "kernels.hh"
 
+#include <algorithm>
 #include <climits>
 #include <cstdlib>
+#include <stdexcept>
+#include <string>
 #include <type_traits>
 
 namespace slate_amd {
@@ -414,15 +417,526 @@ __global__ __launch_bounds__(256) void tslu_rows_kernel(int64_t m, int64_t r, in
     }
 }
 
+
+//==============================================================================
+// Tournament v2: the whole reduction tree in ONE launch, and the permutation +
+// L21 in one more (two launches per narrow block instead of five).
+//
+//   tree    every workgroup (256 threads = one GEMM workgroup's slot, so it can
+//           start beside the trailing update; R rows per thread) plays one
+//           leaf: NT*R consecutive rows.  It writes its <= 32 winners' row
+//           indices and ORIGINAL rows (contiguous, column-major per level) with
+//           agent-scope `sc1` stores, waits for them and adds to its group's
+//           counter; the workgroup whose add comes last plays the group's node
+//           on the F = NT*R/32 children's candidates (coalesced sc1 loads of the
+//           level's slab instead of a strided gather from A), and so on up the
+//           tree -- no relaunch per level.  The root writes the LU of the
+//           winners into the top block, U11^{-1}, ipiv and the net row moves.
+//           Leaf 0 keeps the top block's original rows (the rows the moves
+//           displace below it) before anything overwrites them.
+//   step    (GEPP on the rows held in VGPRs) every thread picks the best of its
+//           R rows (32-bit fp32 key, as v1), ONE wave max, a ballot names the
+//           winning lane, which publishes its row (columns >= k only) and
+//           {key, thread-row, global row} to the wave's double-buffered LDS
+//           slot; ONE barrier; every thread takes the max of the wave keys and
+//           the lowest wave holding it (one ballot).  The next step's key comes
+//           from an approximate update (v_rcp without Newton steps) and the
+//           exact update is branch-free (l = 0 for inactive rows), so the
+//           scheduler can overlap it with the next wave max.  No global memory
+//           access inside the step loop (the v1 kernel stored its winner every
+//           step and waited for the store before the next key).
+//   finish  blocks [0, rgrid): L21 = A21 U11^{-1} on MFMA for rows below the
+//           top block (displaced rows read from leaf 0's copy); the other
+//           blocks apply the row moves to the panel columns outside the
+//           narrow block; the last block also updates perm.
+template <typename T> struct Tslu2Rows { static constexpr int R = 2; };
+template <> struct Tslu2Rows<float> { static constexpr int R = 4; };
+template <> struct Tslu2Rows<cplx<double>> { static constexpr int R = 1; };
+
+constexpr int T2_NT = 256;
+constexpr int T2_MOVES = 256;            // ints: [0] count, [2, 66) dst, [66, 130) src
+constexpr int T2_CTR_MAX = 4096;         // counters (ints), zeroed per panel (tslu_init)
+
+struct Tslu2Args {
+    int64_t m, r, lda;
+    int nn, nleaf;
+    int* cand;      // per tree item: TW candidate rows (global index)
+    int* ccnt;      // per tree item: candidate count
+    int* ctr;       // group arrival counters (reset to 0 by the last arriver)
+    void* slab;     // per level: the items' candidates' original rows, column-major, ld = items * TW
+    void* topc;     // TW x TW: original top-block rows (row-major: topc[i*TW + j])
+    int64_t* ipiv;
+    int* info;
+    int64_t info_offset;
+    int* moves;
+    void* uinv;     // TW x TW, Uinv[i*TW + j] = (U11^{-1})(i, j)
+};
+
+template <typename T> __device__ inline T rcp_approx(T d) { return fast_rcp(d); }
+template <> __device__ inline double rcp_approx<double>(double d) { return __builtin_amdgcn_rcp(d); }
+template <> __device__ inline float rcp_approx<float>(float d) { return __builtin_amdgcn_rcpf(d); }
+
+__device__ inline float opaque(float v) { asm volatile("" :: "v"(v)); return v; }
+__device__ inline double opaque(double v) { asm volatile("" :: "v"(v)); return v; }
+__device__ inline int opaque(int v) { asm volatile("" :: "v"(v)); return v; }
+template <typename R>
+__device__ inline cplx<R> opaque(cplx<R> v) { return cplx<R>(opaque(v.re), opaque(v.im)); }
+
+// agent-scope relaxed (sc1) loads / stores: the in-launch hand-off between workgroups
+template <typename T> __device__ inline T ld_sc1(const T* q) {
+    return __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename R> __device__ inline cplx<R> ld_sc1(const cplx<R>* q) {
+    const R* r = reinterpret_cast<const R*>(q);
+    return cplx<R>(ld_sc1(r), ld_sc1(r + 1));
+}
+template <typename T> __device__ inline void st_sc1(T* q, T v) {
+    __hip_atomic_store(q, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+template <typename R> __device__ inline void st_sc1(cplx<R>* q, cplx<R> v) {
+    R* r = reinterpret_cast<R*>(q);
+    st_sc1(r, v.re);
+    st_sc1(r + 1, v.im);
+}
+
+// wave max of a 32-bit key: DPP with bound_ctrl (0 is the identity), so each
+// stage folds into one v_max_u32_dpp
+__device__ inline uint32_t wave_max_key(uint32_t k) {
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x124, 0xF, 0xF, true));   // row_ror:4
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x128, 0xF, 0xF, true));   // row_ror:8
+    uint32_t a = __builtin_amdgcn_readlane(k, 0), b = __builtin_amdgcn_readlane(k, 16);
+    uint32_t c = __builtin_amdgcn_readlane(k, 32), d = __builtin_amdgcn_readlane(k, 48);
+    return max(max(a, b), max(c, d));
+}
+
+#ifdef TSLU_PROBE
+__device__ long long g_tslu_probe[128];
+#define TSLU_T(slot)                                                                      \
+    do {                                                                                  \
+        if (tid == 0 && (level > 0 || blockIdx.x == 0))                                   \
+            g_tslu_probe[level * 32 + (slot)] = (long long)__builtin_amdgcn_s_memtime();   \
+    } while (0)
+#define TSLU_S(k, sub)                                                                    \
+    do {                                                                                  \
+        if ((k) == 4 || (k) == 20) TSLU_T(((k) == 4 ? 16 : 24) + (sub));                  \
+    } while (0)
+#else
+#define TSLU_T(slot) do {} while (0)
+#define TSLU_S(k, sub) do {} while (0)
+#endif
+
+template <typename T, int R>
+__global__ __launch_bounds__(T2_NT) void tslu2_tree_kernel(Tslu2Args p, T* A) {
+    SLATE_PANEL_WAVE_PRIO();
+    constexpr int NT = T2_NT, NW = NT / 64, S = NT * R, F = S / TW;
+    constexpr bool kReal = !is_cplx<T>::value;
+    __shared__ int4 srec[2][NW];                 // {key, thread*R + row, global row, -}
+    __shared__ alignas(16) T srow[2][NW][TW];    // each wave's best row: columns k ..
+    __shared__ int swin[TW], swho[TW];
+    __shared__ int s_flag;
+    __shared__ T slu[TW][TW + 1];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int nn = p.nn;
+    const int64_t lda = p.lda;
+    T* slab = reinterpret_cast<T*>(p.slab);
+
+    int level = 0, item = blockIdx.x, nl = p.nleaf, off = 0, offprev = 0, nprev = 0;
+    while (true) {
+        int idx[R];
+        bool act[R];
+        int chosen[R];
+        T a[R][TW];
+        const T* pin = slab + (int64_t)offprev * TW * TW;   // the previous level's slab
+        const int64_t ldin = (int64_t)nprev * TW;
+        #pragma unroll
+        for (int i = 0; i < R; ++i) {
+            const int s = tid + i * NT;
+            idx[i] = 0;
+            act[i] = false;
+            chosen[i] = -1;
+            if (level == 0) {
+                const int64_t row = p.r + (int64_t)item * S + s;
+                if (row < p.m) { idx[i] = (int)row; act[i] = true; }
+                // branch-free loads (clamped addresses, then select)
+                const int64_t rs = act[i] ? idx[i] : p.r;
+                #pragma unroll
+                for (int j = 0; j < TW; ++j) {
+                    const T v = A[rs + (j < nn ? j : nn - 1) * lda];
+                    a[i][j] = (act[i] && j < nn) ? v : zero<T>();
+                }
+                if (item == 0 && s < TW) {
+                    // original top-block rows: the rows the interchanges displace
+                    T* tc = reinterpret_cast<T*>(p.topc) + s * TW;
+                    #pragma unroll
+                    for (int j = 0; j < TW; ++j) tc[j] = a[i][j];
+                }
+            } else {
+                const int child = item * F + s / TW, k = s % TW;
+                if (child < nprev && k < ld_sc1(&p.ccnt[offprev + child])) {
+                    idx[i] = ld_sc1(&p.cand[(int64_t)(offprev + child) * TW + k]);
+                    act[i] = true;
+                }
+                const int64_t rs = act[i] ? (int64_t)item * S + s : (int64_t)item * S;
+                #pragma unroll
+                for (int j = 0; j < TW; ++j) {
+                    const T v = ld_sc1(&pin[rs + j * ldin]);
+                    a[i][j] = act[i] ? v : zero<T>();
+                }
+            }
+        }
+
+        TSLU_T(0);
+        int cnt = 0;
+        bool done = false;
+        T tn[R];
+        #pragma unroll
+        for (int i = 0; i < R; ++i) tn[i] = a[i][0];
+        const bool root = nl == 1;
+        static_for<0, TW>([&](auto kc) {
+            constexpr int k = decltype(kc)::value;
+            constexpr int bf = k & 1;
+            if (k < nn && !done) {
+                // best of this thread's rows (full fp32 key; ties -> lowest row)
+                uint32_t kt = 0u;
+                int bi = 0;
+                #pragma unroll
+                for (int i = 0; i < R; ++i) {
+                    const uint32_t key = act[i] ? pivot_key(kReal ? tn[i] : a[i][k]) : 0u;
+                    if (key > kt) { kt = key; bi = i; }
+                }
+                TSLU_S(k, 0);
+                const uint32_t kw = wave_max_key(kt);
+                TSLU_S(k, 1);
+                if (kw != 0u) {
+                    const unsigned long long win = __ballot(kt == kw);
+                    if (lane == __ffsll((long long)win) - 1) {
+                        static_for<0, R>([&](auto ic) {
+                            constexpr int i = decltype(ic)::value;
+                            if (i == bi) {
+                                // opaque() pins each branch's reads of row i: merged
+                                // branches would read a dynamically indexed a[bi][j],
+                                // which demotes a[][] to scratch memory
+                                srec[bf][w] = make_int4((int)kw, tid * R + i, opaque(idx[i]), 0);
+                                #pragma unroll
+                                for (int j = k; j < TW; ++j) srow[bf][w][j] = opaque(a[i][j]);
+                            }
+                        });
+                    }
+                } else if (lane == 0) {
+                    srec[bf][w].x = 0;
+                }
+                TSLU_S(k, 2);
+                __syncthreads();
+                TSLU_S(k, 3);
+                uint32_t kb = (uint32_t)srec[bf][0].x;
+                #pragma unroll
+                for (int q = 1; q < NW; ++q) kb = max(kb, (uint32_t)srec[bf][q].x);
+                if (kb == 0u) {
+                    done = true;                       // uniform: no candidates left
+                } else {
+                    const uint32_t myk = lane < NW ? (uint32_t)srec[bf][lane].x : 0u;
+                    const int wb = __ffsll((long long)__ballot(myk == kb)) - 1;   // lowest wave
+                    // the pivot row in registers at once (one batch of LDS reads and
+                    // one wait, not a read / wait / FMA chain per column and row)
+                    T u[TW];
+                    #pragma unroll
+                    for (int j = k; j < TW; ++j) u[j] = srow[bf][wb][j];
+                    const int4 rec = srec[bf][wb];
+                    const T d = u[k];
+                    TSLU_S(k, 4);
+                    if constexpr (kReal && k + 1 < TW) {
+                        // approximate next-column values: only the next key uses them
+                        const T u1 = u[k + 1];
+                        const T r0 = is_zero(d) ? zero<T>() : rcp_approx<T>(d);
+                        #pragma unroll
+                        for (int i = 0; i < R; ++i) tn[i] = a[i][k + 1] - (a[i][k] * r0) * u1;
+                    }
+                    TSLU_S(k, 5);
+                    #pragma unroll
+                    for (int i = 0; i < R; ++i) {
+                        const bool hit = tid * R + i == rec.y;
+                        act[i] = act[i] && !hit;
+                        chosen[i] = hit ? k : chosen[i];
+                    }
+                    // Branch-free update: inactive rows get l = 0.  A chosen row's
+                    // columns >= its step are saved (root) before they change; its
+                    // multipliers (columns < its step) are never written again.
+                    const T rd = is_zero(d) ? zero<T>() : fast_rcp(d);
+                    #pragma unroll
+                    for (int i = 0; i < R; ++i) {
+                        const T l = act[i] ? a[i][k] * rd : zero<T>();
+                        #pragma unroll
+                        for (int j = k + 1; j < TW; ++j) a[i][j] -= l * u[j];
+                        a[i][k] = act[i] ? l : a[i][k];
+                    }
+                    TSLU_S(k, 6);
+                    if (tid == 0) { swin[k] = rec.z; swho[k] = rec.y; }
+                    if (root && tid >= k && tid < TW) slu[k][tid] = srow[bf][wb][tid];
+                    cnt = k + 1;
+                    if (k < 8 || k == 16 || k == 31) TSLU_T(1 + (k < 8 ? k : (k == 16 ? 8 : 9)));
+                }
+            }
+        });
+
+        TSLU_T(11);
+        if (root) {
+            // ---- root: outputs for the finish launch -------------------------
+            // multipliers of the winners (their U parts were saved at selection)
+            #pragma unroll
+            for (int i = 0; i < R; ++i)
+                if (chosen[i] >= 0) {
+                    #pragma unroll
+                    for (int j = 0; j < TW; ++j)
+                        if (j < chosen[i]) slu[chosen[i]][j] = a[i][j];
+                }
+            __syncthreads();
+            if (w == 0) {
+                // LAPACK ipiv and the net row moves (pos <- orig)
+                int pos, orig;
+                const bool mv = tslu_interchanges((int)p.r, swin, cnt, p.ipiv, pos, orig);
+                const unsigned long long bal = __ballot(mv);
+                const int slot = __popcll(bal & ((1ull << lane) - 1));
+                if (mv) { p.moves[2 + slot] = pos; p.moves[66 + slot] = orig; }
+                if (lane == 0) p.moves[0] = __popcll(bal);
+            } else if (w == 1) {
+                // U11^{-1}, lane j = column j (axpy-form back substitution)
+                T x[TW];
+                #pragma unroll
+                for (int i = 0; i < TW; ++i) x[i] = (i == lane && lane < nn) ? one<T>() : zero<T>();
+                #pragma unroll
+                for (int k = TW - 1; k >= 0; --k) {
+                    if (k < nn) {
+                        const T dk = slu[k][k];
+                        const T xk = x[k] * (is_zero(dk) ? zero<T>() : fast_rcp(dk));
+                        x[k] = xk;
+                        #pragma unroll
+                        for (int i = 0; i < k; ++i) x[i] -= slu[i][k] * xk;
+                    }
+                }
+                T* U = reinterpret_cast<T*>(p.uinv);
+                if (lane < TW) {
+                    #pragma unroll
+                    for (int i = 0; i < TW; ++i) U[i * TW + lane] = x[i];
+                }
+            } else {
+                // the LU of the winners into the top block; the info flag
+                for (int e = tid - 128; e < TW * TW; e += NT - 128) {
+                    const int i = e % TW, j = e / TW;
+                    if (i < cnt && j < nn) A[p.r + i + j * lda] = slu[i][j];
+                }
+                if (tid == 128 && p.info) {
+                    int bad = -1;
+                    for (int k = 0; k < nn; ++k)
+                        if (is_zero(slu[k][k])) { bad = k; break; }
+                    if (bad >= 0 && *p.info == 0) *p.info = (int)(p.info_offset + p.r + bad + 1);
+                }
+            }
+            TSLU_T(12);
+            return;
+        }
+
+        // ---- not the root: hand the winners to the group's node --------------
+        __syncthreads();
+        {
+            T* pout = slab + (int64_t)off * TW * TW;
+            const int64_t ldout = (int64_t)nl * TW;
+            for (int e = tid; e < TW * TW; e += NT) {
+                const int k = e % TW, j = e / TW;
+                if (k >= cnt) continue;            // (cnt < TW: a narrow last block)
+                const int who = swho[k];
+                T v;
+                if (level == 0) v = j < nn ? A[swin[k] + j * lda] : zero<T>();
+                else v = ld_sc1(&pin[(int64_t)item * S + (who / R) + (who % R) * NT + j * ldin]);
+                st_sc1(&pout[(int64_t)item * TW + k + j * ldout], v);
+            }
+        }
+        if (tid < cnt) st_sc1(&p.cand[(int64_t)(off + item) * TW + tid], swin[tid]);
+        if (tid == 0) st_sc1(&p.ccnt[off + item], cnt);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        if (tid == 0) {
+            const int g = item / F, ng = min(F, nl - g * F);
+            int* c = &p.ctr[off + nl + g];
+            const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int last = old == ng - 1;
+            if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            s_flag = last;
+        }
+        __syncthreads();
+        TSLU_T(13);
+        if (!s_flag) return;
+        offprev = off;
+        nprev = nl;
+        off += nl;
+        nl = (nl + F - 1) / F;
+        item /= F;
+        ++level;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) void tslu2_finish_kernel(int64_t m, int64_t r, int nn, int64_t c0, T* Ap,
+                                                           int64_t lda, int64_t ncols, int rgrid, const int* moves,
+                                                           const T* uinv, const T* topc, int64_t* perm) {
+    SLATE_PANEL_WAVE_PRIO();
+    __shared__ int s_dst[64], s_src[64];
+    __shared__ T Uinv[TW * TW];
+    __shared__ short smap[256];
+    const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+    const int np = moves[0];
+    if (tid < np) { s_dst[tid] = moves[2 + tid]; s_src[tid] = moves[66 + tid]; }
+    if (perm && blockIdx.x == gridDim.x - 1 && tid < 64) {
+        // net permutation of the panel rows (all loads before any store)
+        const int64_t pv = tid < np ? perm[moves[66 + tid]] : 0;
+        if (tid < np) perm[moves[2 + tid]] = pv;
+    }
+    if ((int)blockIdx.x >= rgrid) {
+        // row moves on the panel columns outside the narrow block, a column per wave
+        __syncthreads();
+        const int pb = blockIdx.x - rgrid, pg = gridDim.x - rgrid;
+        for (int64_t jj = pb * 4 + w; jj < ncols - nn; jj += (int64_t)pg * 4) {
+            const int64_t j = jj < c0 ? jj : jj + nn;
+            T* col = Ap + j * lda;
+            T v = zero<T>();
+            if (lane < np) v = col[s_src[lane]];
+            __builtin_amdgcn_wave_barrier();
+            if (lane < np) col[s_dst[lane]] = v;
+        }
+        return;
+    }
+    T* A = Ap + c0 * lda;
+    const int64_t base = r + nn + blockIdx.x * (int64_t)256;
+    for (int t = tid; t < TW * TW; t += 256) Uinv[t] = uinv[t];
+    smap[tid] = -1;
+    __syncthreads();
+    if (tid < np) {
+        const int64_t d = s_dst[tid] - base;
+        if (s_dst[tid] >= r + nn && d >= 0 && d < 256) smap[d] = (short)tid;
+    }
+    __syncthreads();
+    if constexpr (std::is_same<T, double>::value) {
+        double ub[TW / 4][2];
+        #pragma unroll
+        for (int ks = 0; ks < TW / 4; ++ks)
+            #pragma unroll
+            for (int nt = 0; nt < 2; ++nt) ub[ks][nt] = Uinv[(ks * 4 + (lane >> 4)) * TW + nt * 16 + (lane & 15)];
+        #pragma unroll
+        for (int sl = 0; sl < 4; ++sl) {
+            const int loc = (w * 4 + sl) * 16 + (lane & 15);
+            const int64_t row = base + loc;
+            const bool ok = row < m;
+            const int e = smap[loc];
+            const double* src = e >= 0 ? topc + (s_src[e] - r) * TW : A + row;
+            const int64_t sld = e >= 0 ? 1 : lda;
+            double av[TW / 4];
+            #pragma unroll
+            for (int ks = 0; ks < TW / 4; ++ks) {
+                const int col = ks * 4 + (lane >> 4);
+                av[ks] = (ok && col < nn) ? src[col * sld] : 0.0;
+            }
+            double c0v[4] = {0, 0, 0, 0}, c1v[4] = {0, 0, 0, 0};
+            #pragma unroll
+            for (int ks = 0; ks < TW / 4; ++ks) {
+                mfma16(ub[ks][0], av[ks], c0v);
+                mfma16(ub[ks][1], av[ks], c1v);
+            }
+            if (ok) {
+                #pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int col0 = (lane >> 4) + 4 * q, col1 = 16 + col0;
+                    if (col0 < nn) A[row + col0 * lda] = c0v[q];
+                    if (col1 < nn) A[row + col1 * lda] = c1v[q];
+                }
+            }
+        }
+    } else {
+        const int64_t row = base + tid;
+        if (row < m) {
+            const int e = smap[tid];
+            const T* src = e >= 0 ? topc + (s_src[e] - r) * TW : A + row;
+            const int64_t sld = e >= 0 ? 1 : lda;
+            T av[TW];
+            #pragma unroll
+            for (int k = 0; k < TW; ++k) av[k] = k < nn ? src[k * sld] : zero<T>();
+            #pragma unroll 1
+            for (int j = 0; j < nn; ++j) {
+                T s = zero<T>();
+                #pragma unroll
+                for (int k = 0; k < TW; ++k) s += av[k] * Uinv[k * TW + j];
+                A[row + j * lda] = s;
+            }
+        }
+    }
+}
+
 }  // namespace
 
 // Utop scratch (TW x TW, up to 16-byte scalars) first, then the candidate
 // ping-pong buffers and counts (int); sizes in int64 units.
 constexpr int64_t kUtopI64 = 2 * TW * TW;
 
+// v2 layout (int64 units): [uinv | top-block copy | moves | counters | item
+// counts | candidate rows | per-level slabs of candidate rows (16-byte scalars max)]
+constexpr int64_t kT2Uinv = 0, kT2Top = 2 * TW * TW, kT2Moves = kT2Top + 2 * TW * TW;
+constexpr int64_t kT2Ctr = kT2Moves + T2_MOVES / 2, kT2Cnt = kT2Ctr + T2_CTR_MAX / 2;
+
+static int64_t tslu2_items_max(int64_t rows) {
+    const int64_t nleaf = rows / T2_NT + 1;   // leaves hold >= T2_NT rows
+    return 2 * nleaf + 16;                    // every tree level
+}
+
 int64_t tslu_workspace(int64_t rows) {
     int64_t nleaf = (rows + TR - 1) / TR;
-    return 2 * kUtopI64 + nleaf * TW + nleaf + 64;
+    int64_t v1 = 2 * kUtopI64 + nleaf * TW + nleaf + 64;
+    const int64_t items = tslu2_items_max(rows);
+    int64_t v2 = kT2Cnt + (items + items * TW + 2) / 2 + 2 + items * TW * TW * 2 + 64;
+    return std::max(v1, v2);
+}
+
+void tslu_init(int64_t* work, hipStream_t s) {
+    (void)hipMemsetAsync(work + kT2Ctr, 0, T2_CTR_MAX * sizeof(int), s);
+}
+
+static bool tslu_v1() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_TSLU_V1");
+        return e && std::atoi(e) != 0;
+    }();
+    return v;
+}
+
+template <typename T>
+static void tslu2_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
+                         int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
+    constexpr int R = Tslu2Rows<T>::R, S = T2_NT * R;
+    const int64_t rows = m - r;
+    Tslu2Args p;
+    p.m = m; p.r = r; p.lda = lda; p.nn = nn;
+    p.nleaf = (int)((rows + S - 1) / S);
+    int64_t items = 0;
+    for (int64_t n = p.nleaf; ; n = (n + S / TW - 1) / (S / TW)) { items += n; if (n == 1) break; }
+    if (items + 1 > T2_CTR_MAX || items > tslu2_items_max(m))
+        throw std::runtime_error("tslu: panel too tall for the tournament workspace");
+    p.uinv = work + kT2Uinv;
+    p.topc = work + kT2Top;
+    p.moves = reinterpret_cast<int*>(work + kT2Moves);
+    p.ctr = reinterpret_cast<int*>(work + kT2Ctr);
+    p.ccnt = reinterpret_cast<int*>(work + kT2Cnt);
+    p.cand = p.ccnt + items + 1;
+    p.slab = work + kT2Cnt + (items + items * TW + 2) / 2 + 2;
+    p.ipiv = ipiv; p.info = info; p.info_offset = info_offset;
+    hipLaunchKernelGGL((tslu2_tree_kernel<T, R>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess)
+        throw std::runtime_error(std::string("tslu tree kernel launch: ") + hipGetErrorString(e));
+    const int64_t c0 = (Ablk - Apanel) / lda;
+    const int rgrid = (int)std::max<int64_t>(0, (rows - nn + 255) / 256);
+    const int pgrid = ncols > nn ? (int)std::min<int64_t>((ncols - nn + 3) / 4, 128) : 0;
+    hipLaunchKernelGGL(tslu2_finish_kernel<T>, dim3(std::max(1, rgrid + pgrid)), dim3(256), 0, s, m, r, nn, c0,
+                       Apanel, lda, ncols, rgrid, (const int*)p.moves, (const T*)p.uinv, (const T*)p.topc, perm);
+    if (hipError_t e = hipGetLastError(); e != hipSuccess)
+        throw std::runtime_error(std::string("tslu finish kernel launch: ") + hipGetErrorString(e));
 }
 
 template <typename T>
@@ -430,6 +944,10 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
                  int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
+    if (!tslu_v1()) {
+        tslu2_narrow<T>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
+        return;
+    }
     const int64_t nleaf_max = (rows + TR - 1) / TR;
     T* Utop = reinterpret_cast<T*>(work);
     T* LU11 = reinterpret_cast<T*>(work + kUtopI64);      // final round's LU of the winners
@@ -462,10 +980,12 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
 #define SLATE_INST_TSLU(T) \
     template void tslu_narrow<T>(int64_t, int64_t, int, T*, T*, int64_t, int64_t, int64_t*, int64_t*, int*, int64_t, int64_t*, hipStream_t);
 
-SLATE_INST_TSLU(float)
 SLATE_INST_TSLU(double)
+#ifndef TSLU_PROBE
+SLATE_INST_TSLU(float)
 SLATE_INST_TSLU(cplx<float>)
 SLATE_INST_TSLU(cplx<double>)
+#endif
 
 }  // namespace dev
 }  // namespace slate_amd

@@ -3,6 +3,7 @@
 
 #include <cstdlib>
 #include <algorithm>
+#include <atomic>
 #include <deque>
 #include <string>
 
@@ -15,6 +16,7 @@ struct State {
     std::mutex mtx;
     int device = -1;
     bool streams_ready = false;
+    bool destroyed = false;   // context_destroy ran while blocks were still live
     int reserved_cus = 0;
     hipStream_t streams[kNumQueues] = {};
     std::vector<hipEvent_t> events;
@@ -67,7 +69,13 @@ State& owner_of(void* p) {
     if (!g_multi_ctx) return st();
     std::lock_guard<std::mutex> l(g_owner_mtx);
     auto it = owners().find(p);
-    if (it == owners().end()) return st();
+    if (it == owners().end()) {
+        // allocated by the process context before any other context existed
+        // (so never recorded): return it there, not to the freeing thread's
+        State& ps = process_state();
+        std::lock_guard<std::mutex> g(ps.mtx);
+        return ps.live.count(p) ? ps : st();
+    }
     State* s = it->second;
     owners().erase(it);
     return *s;
@@ -215,8 +223,15 @@ void context_destroy(Context* ctx) {
     }
     t_ctx = prev;
     context_bind(static_cast<Context*>(prev));
-    // blocks still live (handed out, not yet freed) keep the context alive
-    if (ctx->live.empty()) delete ctx;
+    // blocks still live (handed out, not yet freed) keep the context alive;
+    // free() deletes it with its last block
+    bool empty;
+    {
+        std::lock_guard<std::mutex> g(ctx->mtx);
+        empty = ctx->live.empty();
+        ctx->destroyed = !empty;
+    }
+    if (empty) delete ctx;
 }
 
 int reserved_cus() { return st().reserved_cus; }
@@ -232,9 +247,13 @@ int count() {
     return n;
 }
 
+namespace { std::atomic<bool> g_explicit_device{false}; }
+bool device_explicit() { return g_explicit_device.load(); }
+
 void set_device(int dev) {
     auto& s = st();
     std::lock_guard<std::mutex> g(s.mtx);
+    g_explicit_device = true;
     if (s.device == dev) return;
     slate_error_if_msg(s.streams_ready, "set_device after streams were created");
     slate_hip_call(hipSetDevice(dev));
@@ -370,13 +389,23 @@ size_t bytes_stream_cached() { return st().stream_cached; }
 void free(void* ptr) {
     if (!ptr) return;
     auto& s = owner_of(ptr);
-    std::lock_guard<std::mutex> g(s.mtx);
+    std::unique_lock<std::mutex> g(s.mtx);
     auto it = s.live.find(ptr);
     slate_assert(it != s.live.end());
     size_t b = it->second;
     s.live.erase(it);
     s.live_stream.erase(ptr);
     s.in_use -= b;
+    if (s.destroyed) {
+        // its context is gone (streams destroyed): release the block to HIP,
+        // and the context itself with its last block
+        (void)hipDeviceSynchronize();
+        (void)hipFree(ptr);
+        const bool last = s.live.empty();
+        g.unlock();
+        if (last) delete static_cast<Context*>(&s);
+        return;
+    }
     if (!s.streams_ready) {
         // no queue ever ran: only synchronous (null-stream) use is possible
         slate_hip_call(hipStreamSynchronize(nullptr));

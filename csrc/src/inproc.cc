@@ -24,9 +24,21 @@ int g_last_p = 0, g_last_q = 0;
 int64_t inproc_run_count() { return g_runs.load(); }
 void inproc_last_shape(int& p, int& q) { p = g_last_p; q = g_last_q; }
 
+bool multi_process_job() {
+    auto num = [](const char* k) { const char* e = std::getenv(k); return e ? std::atoi(e) : 0; };
+    return num("WORLD_SIZE") > 1 || std::getenv("LOCAL_RANK") || num("OMPI_COMM_WORLD_SIZE") > 1 ||
+           num("PMI_SIZE") > 1 || num("PMIX_SIZE") > 1 || (std::getenv("SLURM_PROCID") && num("SLURM_NTASKS") > 1);
+}
+
 int inproc_ranks() {
     if (const char* e = std::getenv("SLATE_INPROC_RANKS")) return std::max(1, std::atoi(e));
-    return device::available() ? std::max(1, device::count()) : 1;
+    if (!device::available()) return 1;
+    // One process per GPU (torchrun / MPI environment, a p x q grid already
+    // set up, or a program that picked its device): stay on this process's
+    // GPU -- spreading every process over all GPUs would oversubscribe them.
+    if (multi_process_job() || device::device_explicit()) return 1;
+    if (auto g = default_grid(); g && g->size() > 1) return 1;
+    return std::max(1, device::count());
 }
 
 void inproc_grid_shape(int n, int& p, int& q) {

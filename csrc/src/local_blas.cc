@@ -750,6 +750,7 @@ void getrf_panel(Ctx const& c, int64_t m, int64_t n, T* A, int64_t lda, int64_t*
     P.info = info; P.info_offset = info_offset; P.pivot = pivot; P.tournament = tournament; P.ctx = c;
     P.thresh = pivot_threshold;
     P.tws = tournament ? sc.alloc<int64_t>(size_t(kd::tslu_workspace(m))) : nullptr;
+    if (P.tws) kd::tslu_init(P.tws, c.stream);
     int64_t np = ceildiv(m, 256) + 1;
     P.pval = sc.alloc<real_type<T>>(np);
     P.pidx = sc.alloc<int64_t>(np);

@@ -64,9 +64,12 @@ inline int64_t qr_kchunk() {
 /// tr(G) to the diagonal), Q := Q L^{-H}; R = product of the L^H.  The
 /// Householder reconstruction (e)-(g) then turns Q into the same (V, T, R)
 /// the tree would give.  The Gram matrix before the last pass measures Q's
-/// orthogonality; if it is not within 0.5 of I the column's processes --
-/// which all hold the same all-reduced G -- retry with the shifted variant,
-/// then fall back to the TSQR tree on the untouched panel (a rank-deficient
+/// orthogonality: it must satisfy ||G - I||_F <= 0.5 (then every singular
+/// value of Q lies in [0.7, 1.23] and the last pass leaves Q orthogonal to
+/// working precision), and no pass's Cholesky factorization may report a
+/// non-positive pivot.  Otherwise the column's processes -- which all hold the
+/// same all-reduced G -- retry with the shifted variant, then fall back to
+/// the TSQR tree on the untouched panel (an ill-conditioned, rank-deficient
 /// or NaN panel).  That decision is the one host wait per
 /// panel step (the panel queue drains; the trailing queues keep running).
 template <typename T>
@@ -75,6 +78,7 @@ struct TsqrPanel {
     int64_t nb;
     Work<T> Tloc, Rcur, Rrecv, Ecur, Etmp, Qloc, LUb, Ytmp, Dg, Tw, sgn, taul, Gq;
     Work<int> cq_flag;
+    Work<double> cq_ssq;
     int* cq_host = nullptr;
     bool cholqr_on = false;
     std::vector<Work<T>> Sst, Ttt;
@@ -97,6 +101,7 @@ struct TsqrPanel {
         if (cholqr_on) {
             Gq.resize(target, nn);
             cq_flag.resize(target, 2);
+            cq_ssq.resize(target, 1);
             cq_host = target == Target::Devices ? static_cast<int*>(device::malloc_host(sizeof(int) * 2)) : cq_flag.data();
             dev_ = target == Target::Devices;
         }
@@ -125,6 +130,9 @@ struct TsqrPanel {
             int* dflag = cq_flag.data();
             const int npass = shifted ? 3 : 2;
             lb::copy2d(c, mr, kb, ap, lda, Qloc.data(), ldq);
+            // dflag[1]: first non-positive Cholesky pivot of any pass
+            if (c.dev()) device::memset_async(dflag + 1, 0, sizeof(int), c.stream);
+            else dflag[1] = 0;
             for (int pass = 0; pass < npass; ++pass) {
                 T* G = Gq.data();
                 lb::herk(c, Uplo::Lower, Op::ConjTrans, kb, mr, R(1), Qloc.data(), ldq, R(0), G, kb);
@@ -132,19 +140,21 @@ struct TsqrPanel {
                 const bool sh = shifted && pass == 0, chk = pass == npass - 1;
                 if (c.dev()) {
                     if (sh) slate_amd::dev::cholqr_shift<DT>(slate_amd::dev::dptr(G), kb, int(kb), shift, c.stream);
-                    if (chk) slate_amd::dev::cholqr_check<DT>(slate_amd::dev::dptr(G), kb, int(kb), 0.5, dflag, c.stream);
+                    if (chk)
+                        slate_amd::dev::cholqr_check<DT>(slate_amd::dev::dptr(G), kb, int(kb), 0.5, dflag,
+                                                         cq_ssq.data(), c.stream);
                 } else if (sh) {
                     R tr = 0;
                     for (int64_t i = 0; i < kb; ++i) tr += std::real(G[i + i * kb]);
                     for (int64_t i = 0; i < kb; ++i) G[i + i * kb] += T(R(shift) * tr);
                 } else if (chk) {
-                    R mx = 0;
+                    double ssq = 0;   // ||G - I||_F^2 from the lower triangle
                     for (int64_t j = 0; j < kb; ++j)
                         for (int64_t i = j; i < kb; ++i) {
-                            R d = std::abs(G[i + j * kb] - (i == j ? T(1) : T(0)));
-                            mx = (d > mx || std::isnan(d)) ? d : mx;
+                            const double d = double(std::abs(G[i + j * kb] - (i == j ? T(1) : T(0))));
+                            ssq += (i == j ? 1.0 : 2.0) * d * d;
                         }
-                    dflag[0] = (mx <= R(0.5)) ? 0 : 1;
+                    dflag[0] = (ssq <= 0.25) ? 0 : 1;
                 }
                 lb::potrf(c, Uplo::Lower, kb, G, kb, dflag + 1, 0);
                 lb::trsm(c, Side::Right, Uplo::Lower, cT, Diag::NonUnit, mr, kb, T(1), G, kb, Qloc.data(), ldq);
@@ -155,10 +165,10 @@ struct TsqrPanel {
                     lb::trmm(c, Side::Left, Uplo::Lower, cT, Diag::NonUnit, kb, kb, T(1), G, kb, Rcur.data(), kb);
                 }
             }
-            if (c.dev()) device::memcpy_async(cq_host, dflag, sizeof(int), c.stream);
+            if (c.dev()) device::memcpy_async(cq_host, dflag, 2 * sizeof(int), c.stream);
         });
         if (dev_) slate_hip_call(hipStreamSynchronize(S.ctx(qP).stream));
-        return cq_host[0] == 0;
+        return cq_host[0] == 0 && cq_host[1] == 0;
     }
 
     /// rows_r[r]: panel rows of comm rank r; me: my comm rank; tPan: the

@@ -154,6 +154,7 @@ class MixedLUFactor:
         eps = np.finfo(self.dt).eps
         cte = self.anorm * eps * np.sqrt(n)
         R = empty_like(B, target=tg)
+        C = empty_like(B, target=tg)
         Rlo = _like(B, _LOW[self.dt], tg)
         # x0 = A_lo^{-1} b
         aux.copy(B, Rlo, target=tg)
@@ -162,13 +163,14 @@ class MixedLUFactor:
         for it in range(1, self.itermax + 1):
             aux.copy(B, R, target=tg)
             blas3.gemm(-1.0, self.A, X, 1.0, R, target=tg)          # r = b - A x
-            rn = aux.norm(Norm.Max, R, target=tg)
-            xn = aux.norm(Norm.Max, X, target=tg)
-            if rn <= xn * cte:
+            # per right-hand side, as the reference (gesv_mixed.cc:209-212):
+            # every column must meet ||r_j|| <= ||x_j|| ||A|| eps sqrt(n)
+            rn = np.asarray(aux.colNorms(Norm.Max, R, target=tg))
+            xn = np.asarray(aux.colNorms(Norm.Max, X, target=tg))
+            if np.all(rn <= xn * cte):
                 return X, it - 1
             aux.copy(R, Rlo, target=tg)
             self.F.solve(Rlo)
-            C = empty_like(B, target=tg)
             aux.copy(Rlo, C, target=tg)
             aux.add(1.0, C, 1.0, X, target=tg)                      # x += c
         # fallback: working-precision LU of a copy of A
