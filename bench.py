@@ -54,6 +54,9 @@ EXTRAS = {
     "cfg2_dpotrf_n32768_nb512": ("dpotrf", -2, 512, None),       # -2: half of --dim (32768 at the default)
     "cfg4_dgeqrf_nb256": ("dgeqrf", None, 256, None),
     "cfg5_dgesv_mixed": ("dgesv_mixed", None, None, None),
+    # the reference's semantics (src/gesv_mixed.cc:219-279): classical
+    # refinement, then the fp64 fallback -- no GMRES-IR escalation
+    "cfg5_dgesv_mixed_refsem": ("dgesv_mixed", None, None, None),
 }
 
 
@@ -402,15 +405,17 @@ def main(a):
                 # refinement stalls (Option::EscalateGmres; the fp64 fallback
                 # stays behind it): a random n = 65536 matrix is sometimes too
                 # ill-conditioned for classical fp32 refinement within 30 steps
+                esc = a.mixed_escalate == "yes" and not label.endswith("_refsem")
                 info, piv, iters = s.gesv_mixed(mats["A"], mats["B"], mats["X"], method_lu=lu,
-                                                escalate_gmres=a.mixed_escalate == "yes", **o)
+                                                escalate_gmres=esc, **o)
                 mats["piv"] = piv
                 assert info == 0, f"dgesv_mixed info={info} iters={iters}"
                 if step >= warmup:
                     extra.setdefault("iterations_per_step", []).append(int(iters))
                     extra["iterations"] = int(iters)
                     extra["fallback"] = bool(extra.get("fallback", False) or iters < 0)
-                    extra["escalate_gmres"] = a.mixed_escalate == "yes"
+                    extra["escalate_gmres"] = esc
+                    extra.setdefault("fallback_per_step", []).append(bool(iters < 0))
                 if rank == 0:
                     tm = {k: round(v * 1e3, 1) for k, v in s._slate.timers().items()
                           if "gesv_mixed" in k or "gmres" in k}

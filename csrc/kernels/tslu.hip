@@ -899,12 +899,22 @@ void tslu_init(int64_t* work, hipStream_t s) {
     (void)hipMemsetAsync(work + kT2Ctr, 0, T2_CTR_MAX * sizeof(int), s);
 }
 
-static bool tslu_v1() {
-    static const bool v = [] {
-        const char* e = std::getenv("SLATE_TSLU_V1");
-        return e && std::atoi(e) != 0;
+// Which tournament: v2 (one tree launch + one finish launch) for fp64, where
+// it measured dgetrf n = 65536 56.4 -> 58.0 TFLOP/s and the isolated
+// 32768 x 512 panel 3.71 -> 2.96 ms; v1 (per-level launches) elsewhere: its
+// 60-VGPR fp32 waves fit beside the trailing GEMM's, and the fp32 factor of
+// dgesv_mixed measured 1.92 s (v1) against 2.11 s (v2, 256-VGPR waves that
+// wait for a whole GEMM slot); complex v2 spills.  SLATE_TSLU=1|2 forces one
+// (profiles/r5_tslu_v2.txt).
+template <typename T>
+static bool tslu_use_v2() {
+    static const int forced = [] {
+        const char* e = std::getenv("SLATE_TSLU");
+        if (!e) e = std::getenv("SLATE_TSLU_V1") ? "1" : nullptr;
+        return e ? std::atoi(e) : 0;
     }();
-    return v;
+    if (forced) return forced == 2;
+    return std::is_same<T, double>::value;
 }
 
 template <typename T>
@@ -944,7 +954,7 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
                  int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
-    if (!tslu_v1()) {
+    if (tslu_use_v2<T>()) {
         tslu2_narrow<T>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
         return;
     }

@@ -315,10 +315,14 @@ enum class PanelMode { Partial, Tournament, NoPiv };
 ///     pivoting, the same pivots as on one GPU) and keeps its own rows.
 ///     1 collective per panel instead of nb.
 ///   NoPiv: pk factors the diagonal block, the column solves L21 locally.
-/// Row permutation of every other column range: lu_dist.hip slots (pack ->
-/// all-reduce over the column communicator -> unpack), which also delivers
-/// the (unsolved) U block row to every process of the column, so U12 =
-/// L11^{-1} (...) is computed redundantly instead of broadcast.
+/// Row permutation of every other column range: an exact point-to-point
+/// exchange (the default, SLATE_LU_EXACT_SWAP=1): only the rows that change
+/// process move, each once, with grouped send / recv over the column
+/// communicator; the pivot-row owners then broadcast the U block row to the
+/// column, where U12 = L11^{-1} (...) is computed redundantly instead of
+/// broadcast solved.  SLATE_LU_EXACT_SWAP=0 keeps the older slot scheme
+/// (lu_dist.hip: pack -> all-reduce over the column communicator -> unpack,
+/// which delivers the unsolved U block row to every process at once).
 /// Two communication lanes (Grid::row_fast / col_fast): every message on the
 /// critical path -- tournament / panel gather, LU11 + pivots + L panel
 /// broadcasts, and the row exchange of the lookahead columns -- is issued on
