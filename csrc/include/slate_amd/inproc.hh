@@ -39,6 +39,8 @@ void inproc_last_shape(int& p, int& q);
 int inproc_ranks();
 /// True when the environment shows a launcher started several processes.
 bool multi_process_job();
+/// Is the calling thread one of run_in_process's rank threads?
+bool in_inproc_rank();
 /// Near-square p x q with p <= q for n ranks (1x1, 1x2, 2x2, 2x4, ...).
 void inproc_grid_shape(int n, int& p, int& q);
 

@@ -18,6 +18,7 @@
 // gemmA / trsmA / hemmA replicate the narrow operand on the device instead of
 //   moving A (reference method.hh select_algo: B.nt() < 2).
 #include "internal.hh"
+#include "spread.hh"
 
 #include <numeric>
 
@@ -271,6 +272,10 @@ void gemmA(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
 
 template <typename T>
 void gemm(T alpha, Matrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C, Options const& opts) {
+    if (internal::spread<T>(opts, {{&C, true}, {&A, false}, {&B, false}}, [&](std::vector<Matrix<T>>& M, int) {
+            gemm(alpha, M[1], M[2], beta, M[0], opts);
+        }))
+        return;
     if (A.arbitrary_layout() || B.arbitrary_layout() || C.arbitrary_layout()) {
         Matrix<T> Ab = bc_operand(A, opts), Bb = bc_operand(B, opts), Cb = block_cyclic(C, opts);
         gemm(alpha, Ab, Bb, beta, Cb, opts);

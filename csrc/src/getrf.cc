@@ -22,6 +22,7 @@
 // every 32-column narrow block by a tournament over 256-row leaves on the
 // device (kernels/tslu.hip), then factors that block without further pivoting.
 #include "internal.hh"
+#include "spread.hh"
 #include "lu_dist.hh"
 #include "../kernels/kernels.hh"
 
@@ -1154,6 +1155,15 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
 
 template <typename T>
 int64_t getrf(Matrix<T>& A, Pivots& pivots, Options const& opts) {
+    {   // one process, several GPUs: in-process ranks (spread.hh)
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+                Pivots P;
+                const int64_t i = getrf(M[0], P, opts);
+                if (rank == 0) { info = i; pivots = P; }
+            }))
+            return info;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> Ab = internal::block_cyclic(A, opts);
         int64_t info = getrf(Ab, pivots, opts);
@@ -1167,6 +1177,15 @@ int64_t getrf(Matrix<T>& A, Pivots& pivots, Options const& opts) {
 
 template <typename T>
 int64_t getrf_tntpiv(Matrix<T>& A, Pivots& pivots, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+                Pivots P;
+                const int64_t i = getrf_tntpiv(M[0], P, opts);
+                if (rank == 0) { info = i; pivots = P; }
+            }))
+            return info;
+    }
     return getrf_impl(A, pivots, opts, PanelMode::Tournament);
 }
 

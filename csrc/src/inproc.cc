@@ -22,6 +22,9 @@ int g_last_p = 0, g_last_q = 0;
 }  // namespace
 
 int64_t inproc_run_count() { return g_runs.load(); }
+
+namespace { thread_local bool t_in_rank = false; }
+bool in_inproc_rank() { return t_in_rank; }
 void inproc_last_shape(int& p, int& q) { p = g_last_p; q = g_last_q; }
 
 bool multi_process_job() {
@@ -73,6 +76,7 @@ void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const
     std::vector<std::thread> th;
     for (int r = 0; r < n; ++r) {
         th.emplace_back([&, r] {
+            t_in_rank = true;
             try {
                 if (dev) device::context_bind(g_ctx[r]);
                 set_thread_default_grid(grids[r]);

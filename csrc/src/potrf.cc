@@ -23,6 +23,7 @@
 // The reference instead issues one batched herk/gemm per tile group per
 // step and syncs its queues after each op (internal_herk.cc:491-530).
 #include "internal.hh"
+#include "spread.hh"
 #include "../kernels/kernels.hh"
 
 #include <algorithm>
@@ -457,6 +458,16 @@ int64_t potrf_upper(BaseMatrix<T> A, Target target, int64_t la) {
 
 template <typename T>
 int64_t potrf(HermitianMatrix<T>& A_in, Options const& opts) {
+    {   // one process, several GPUs: in-process ranks (spread.hh)
+        int64_t info = 0;
+        const Uplo u = A_in.uplo();
+        if (internal::spread<T>(opts, {{&A_in, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+                HermitianMatrix<T> H(u, M[0]);
+                const int64_t i = potrf(H, opts);
+                if (rank == 0) info = i;
+            }))
+            return info;
+    }
     if (A_in.arbitrary_layout()) {
         HermitianMatrix<T> Ab(A_in.uplo(), internal::block_cyclic(A_in, opts));
         int64_t info = potrf(Ab, opts);

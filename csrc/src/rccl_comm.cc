@@ -6,6 +6,7 @@
 #include <rccl/rccl.h>
 #include <algorithm>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
 #include <vector>
 
@@ -83,10 +84,60 @@ public:
     }
     ncclComm_t raw() const { return comm_; }
 
+    /// Broadcast transport (SLATE_BCAST, read once; reference: listBcast's
+    /// radix-2 / radix-4 hypercube trees over point-to-point messages,
+    /// include/slate/BaseMatrix.hh:2129-2212, 2326-2386):
+    ///   rccl     ncclBroadcast (RCCL's pipelined ring / tree; default)
+    ///   sendrecv flat fan-out: the root sends to every peer in ONE group --
+    ///            on the fully connected xGMI mesh each message has its own link
+    ///   tree     binomial tree of grouped send / recv, log2(n) rounds
+    /// All three are stream-ordered RCCL operations (kernels on the CUs).  The
+    /// copy-engine path is the in-process transport (thread_comm.cc:
+    /// hipMemcpyAsync peer copies).
+    enum class BcastMode { Rccl, SendRecv, Tree };
+    static BcastMode bcast_mode() {
+        static const BcastMode m = [] {
+            const char* e = std::getenv("SLATE_BCAST");
+            std::string v = e ? e : "rccl";
+            if (v == "sendrecv") return BcastMode::SendRecv;
+            if (v == "tree") return BcastMode::Tree;
+            slate_error_if_msg(v != "rccl", "SLATE_BCAST must be rccl, sendrecv or tree");
+            return BcastMode::Rccl;
+        }();
+        return m;
+    }
+
     void bcast_raw(void* buf, size_t count, ScalarType t, int root, hipStream_t s) override {
         size_t mult;
         auto dt = nccl_type(t, mult);
-        slate_nccl_call(ncclBroadcast(buf, buf, count * mult, dt, root, comm_, s));
+        const size_t n = count * mult;
+        if (size_ == 1 || n == 0) return;
+        switch (bcast_mode()) {
+            case BcastMode::Rccl:
+                slate_nccl_call(ncclBroadcast(buf, buf, n, dt, root, comm_, s));
+                return;
+            case BcastMode::SendRecv:
+                slate_nccl_call(ncclGroupStart());
+                if (rank_ == root) {
+                    for (int d = 1; d < size_; ++d)
+                        slate_nccl_call(ncclSend(buf, n, dt, (root + d) % size_, comm_, s));
+                } else {
+                    slate_nccl_call(ncclRecv(buf, n, dt, root, comm_, s));
+                }
+                slate_nccl_call(ncclGroupEnd());
+                return;
+            case BcastMode::Tree: {
+                const int vr = (rank_ - root + size_) % size_;   // rank relative to the root
+                for (int mask = 1; mask < size_; mask <<= 1) {
+                    if (vr < mask && vr + mask < size_) {
+                        slate_nccl_call(ncclSend(buf, n, dt, (vr + mask + root) % size_, comm_, s));
+                    } else if (vr >= mask && vr < 2 * mask) {
+                        slate_nccl_call(ncclRecv(buf, n, dt, (vr - mask + root) % size_, comm_, s));
+                    }
+                }
+                return;
+            }
+        }
     }
     void allreduce_raw(const void* send, void* recv, size_t count, ScalarType t,
                        ReduceOp op, hipStream_t s) override {

@@ -10,6 +10,7 @@
 // ||R||_max < ||X||_max * ||A||_inf * eps * sqrt(n) (iterRefConverged);
 // fall back to a full-precision factorization if it does not converge.
 #include "internal.hh"
+#include "spread.hh"
 
 #include <cmath>
 
@@ -29,6 +30,10 @@ TriangularMatrix<T> tri(Uplo u, Diag d, BaseMatrix<T> const& A) {
 //------------------------------------------------------------------------------
 template <typename T>
 void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            getrs(M[0], pivots, M[1], opts);
+        }))
+        return;
     if (needs_bc(A, B)) {
         // factors of an arbitrary-layout A live in its block-cyclic tiling
         Matrix<T> Ab = bc_operand(A, opts);
@@ -50,6 +55,10 @@ void getrs(Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const
 template <typename T>
 void getrs(Op trans, Matrix<T> const& A, Pivots const& pivots, Matrix<T>& B, Options const& opts) {
     if (trans == Op::NoTrans) { getrs(A, pivots, B, opts); return; }
+    if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            getrs(trans, M[0], pivots, M[1], opts);
+        }))
+        return;
     if (needs_bc(A, B)) {
         Matrix<T> Ab = bc_operand(A, opts);
         Matrix<T> Bb = block_cyclic_rows_of(Ab, B, opts);
@@ -82,6 +91,15 @@ void getrs_nopiv(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 int64_t gesv(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Options const& opts) {
+    {   // one process, several GPUs: factor and solve on the same in-process ranks
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+                Pivots P;
+                const int64_t i = gesv(M[0], P, M[1], opts);
+                if (rank == 0) { info = i; pivots = P; }
+            }))
+            return info;
+    }
     if (A.arbitrary_layout() || B.arbitrary_layout()) {
         Matrix<T> Ab = internal::block_cyclic(A, opts), Bb = internal::block_cyclic(B, opts);
         int64_t info = gesv(Ab, pivots, Bb, opts);
@@ -107,6 +125,14 @@ int64_t gesv_nopiv(Matrix<T>& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    {
+        const Uplo u = A.uplo();
+        if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+                HermitianMatrix<T> H(u, M[0]);
+                potrs(H, M[1], opts);
+            }))
+            return;
+    }
     trace::Block tb("potrs");
     internal::DriverScope ds_;
     // A = L L^H (lower) or U^H U (upper) in the physical triangle
@@ -124,6 +150,16 @@ void potrs(HermitianMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 int64_t posv(HermitianMatrix<T>& A, Matrix<T>& B, Options const& opts) {
+    {
+        int64_t info = 0;
+        const Uplo u = A.uplo();
+        if (internal::spread<T>(opts, {{&A, true}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int rank) {
+                HermitianMatrix<T> H(u, M[0]);
+                const int64_t i = posv(H, M[1], opts);
+                if (rank == 0) info = i;
+            }))
+            return info;
+    }
     if (A.arbitrary_layout() || B.arbitrary_layout()) {
         HermitianMatrix<T> Ab(A.uplo(), internal::block_cyclic(A, opts));
         Matrix<T> Bb = internal::block_cyclic(B, opts);

@@ -6,6 +6,7 @@
 #pragma once
 
 #include "slate_amd/slate.hh"
+#include "slate_amd/inproc.hh"
 
 #include <cmath>
 #include <cstdio>
@@ -71,6 +72,13 @@ slate::Matrix<T> copy_of(slate::Matrix<T> const& A) {
 
 inline int finish(int fails) {
     int total = int(slate::default_grid()->world().allreduce_scalar<int32_t>(fails, slate::ReduceOp::Sum));
+    // drivers that ran on in-process ranks (one process, several GPUs: spread.hh)
+    if (rank() == 0 && slate::inproc_run_count() > 0) {
+        int p = 0, q = 0;
+        slate::inproc_last_shape(p, q);
+        std::printf("  in-process multi-GPU driver runs: %lld (last grid %d x %d)\n",
+                    (long long)slate::inproc_run_count(), p, q);
+    }
     if (rank() == 0) std::printf("  %s\n", total ? "FAILED" : "all passed");
     slate::finalize();
     return total ? 1 : 0;

@@ -139,3 +139,18 @@ def test_rccl_2x2_no_fast_lane():
                         "--grid", "2x2", "--target", "d", "--lookahead", "2"],
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode,nprocs,grid", [("sendrecv", 8, "2x4"), ("tree", 8, "2x4"), ("tree", 4, "2x2"),
+                                             ("sendrecv", 2, "2x1")])
+def test_rccl_bcast_modes(mode, nprocs, grid):
+    """SLATE_BCAST runtime broadcast transports over real RCCL (rccl_comm.cc):
+    flat send / recv fan-out and the binomial send / recv tree must give the
+    same LU / QR / Cholesky results as ncclBroadcast (tester residuals)."""
+    env = dict(os.environ, SLATE_BCAST=mode)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), str(nprocs),
+                        "getrf,getrf_tntpiv,geqrf,potrf,gemm", "--type", "d", "--dim", "1536", "--nb", "128",
+                        "--grid", grid, "--target", "d", "--lookahead", "2"],
+                       capture_output=True, text=True, timeout=900, env=env)
+    assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]

@@ -69,3 +69,20 @@ def test_example_multi_process(exe, nprocs):
 def test_example_device(exe):
     codes, outs = launch(exe, 1, target="d")
     assert codes == [0] and "all passed" in outs[0], outs[0][-3000:]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("exe", ["ex05_blas", "ex06_linear_system_lu", "ex07_linear_system_cholesky"])
+def test_example_inproc_transparent(exe):
+    """One process, several GPUs, no explicit run_in_process: the unchanged
+    examples (1 x 1 grid, Target::Devices) with SLATE_INPROC_RANKS=4 run
+    gemm / getrf / getrs / gesv / potrf / potrs / posv on a 2 x 2 grid of
+    in-process ranks (csrc/src/spread.hh; 4 ranks on the box's one GPU here)
+    and pass their residual checks.  The example reports the number of
+    driver calls that took the in-process path."""
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE")}
+    env.update(SLATE_TARGET="d", SLATE_INPROC_RANKS="4", SLATE_SPREAD_MIN_N="256", OMP_NUM_THREADS="2")
+    r = subprocess.run([os.path.join(BIN, exe)], env=env, capture_output=True, text=True, timeout=300)
+    out = r.stdout + r.stderr
+    assert r.returncode == 0 and "all passed" in out, out[-3000:]
+    assert "in-process multi-GPU driver runs:" in out and "last grid 2 x 2" in out, out[-3000:]

@@ -1,6 +1,8 @@
 """GPU tests: gfx950 kernels vs fp64 torch/numpy references and device-target
 drivers (reference unit_test/test_Tile_kernels.cc, test_internal_blas.cc and
 the tester's residual checks)."""
+import os
+
 import numpy as np
 import pytest
 
@@ -8,6 +10,7 @@ import slate_d35_amd as s
 from helpers import DTYPES, rnd, tol, relerr
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def _torch():
@@ -702,3 +705,80 @@ def test_inproc_multirank_lapack_device(ranks):
     r = subprocess.run([sys.executable, os.path.join(root, "scripts", "inproc_check.py"), "1536"], env=env,
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "INPROC_OK" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("variant", ["1", "2"])
+def test_tournament_variants_all_types(variant):
+    """Both tournament implementations (SLATE_TSLU=1: per-level launches, v1;
+    2: one-launch tree + fused finish, v2) on every type, including the
+    narrow last block (n = 100) and a three-level tree (complex: 256-row
+    leaves, a node with fewer children than the fan-in).  The variant is read
+    once per process, so each runs in its own interpreter."""
+    import subprocess
+    import sys
+    code = r'''
+import numpy as np, torch, sys
+sys.path.insert(0, "ROOTDIR")
+import slate_d35_amd as s
+for dt in (np.float64, np.float32, np.complex128, np.complex64):
+    for m, n in ((3000, 100), (9000, 64), (700, 96)):
+        rng = np.random.default_rng(5)
+        a = rng.uniform(-1, 1, (m, n))
+        if np.iscomplexobj(np.zeros(1, dt)):
+            a = a + 1j * rng.uniform(-1, 1, (m, n))
+        a = a.astype(dt)
+        tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+        info, ipiv = s.ops.getrf_panel(tA, tournament=True)
+        f = tA.cpu().numpy().T
+        k = min(m, n)
+        L = np.tril(f[:, :k], -1) + np.eye(m, k)
+        U = np.triu(f[:k, :])
+        pa = a.copy()
+        for j, p in enumerate(ipiv):
+            pa[[j, p]] = pa[[p, j]]
+        err = np.linalg.norm(L @ U - pa) / np.linalg.norm(pa)
+        tol = 1e-4 if dt in (np.float32, np.complex64) else 1e-12
+        assert info == 0 and err < tol and np.abs(L).max() < 8, (dt, m, n, info, err)
+print("VARIANT_OK")
+'''.replace("ROOTDIR", ROOT)
+    env = dict(os.environ, SLATE_TSLU=variant)
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "VARIANT_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+def test_python_inproc_transparent():
+    """A Python script on one process, no run_in_process: with
+    SLATE_INPROC_RANKS=4 the device-target gesv / posv / gemm calls on a 1 x 1
+    grid run on 2 x 2 in-process ranks (spread.hh); inproc_run_count() shows
+    the path was taken and the residuals pass."""
+    import subprocess
+    import sys
+    code = r'''
+import sys, numpy as np
+sys.path.insert(0, "ROOTDIR")
+import slate_d35_amd as s
+n, nb = 1024, 128
+rng = np.random.default_rng(3)
+a = rng.uniform(-1, 1, (n, n)); b = rng.uniform(-1, 1, (n, 4))
+A = s.from_numpy(a, nb=nb, target="d"); B = s.from_numpy(b, nb=nb, target="d")
+c0 = s._slate.inproc_run_count()
+info, piv = s.gesv(A, B, target="d")
+x = s.to_numpy(B)
+r1 = np.linalg.norm(a @ x - b) / (np.linalg.norm(a) * np.linalg.norm(x) * n * 1e-16)
+spd = a @ a.T + n * np.eye(n)
+H = s.HermitianMatrix(s.Uplo.Lower, s.from_numpy(spd, nb=nb, target="d")); B2 = s.from_numpy(b, nb=nb, target="d")
+info2 = s.posv(H, B2, target="d")
+x2 = s.to_numpy(B2)
+r2 = np.linalg.norm(spd @ x2 - b) / (np.linalg.norm(spd) * np.linalg.norm(x2) * n * 1e-16)
+C = s.from_numpy(np.zeros((n, n)), nb=nb, target="d")
+s.gemm(1.0, s.from_numpy(a, nb=nb, target="d"), s.from_numpy(a.T.copy(), nb=nb, target="d"), 0.0, C, target="d")
+r3 = np.abs(s.to_numpy(C) - a @ a.T).max()
+runs = s._slate.inproc_run_count() - c0
+print("RES", info, info2, r1, r2, r3, runs, s._slate.inproc_last_shape())
+assert info == 0 and info2 == 0 and r1 < 50 and r2 < 50 and r3 < 1e-10 and runs >= 3, (r1, r2, r3, runs)
+print("INPROC_OK")
+'''.replace("ROOTDIR", ROOT)
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "LOCAL_RANK", "WORLD_SIZE")}
+    env.update(SLATE_INPROC_RANKS="4", SLATE_SPREAD_MIN_N="256", OMP_NUM_THREADS="2")
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "INPROC_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
