@@ -79,7 +79,23 @@ examples/bin/%: examples/cpp/%.cc examples/cpp/util.hh $(PUB_HDR)
 	@mkdir -p examples/bin
 	$(CXX) $(CXXFLAGS) $< -o $@ -L$(PKG) -lslate_amd -Wl,-rpath,'$$ORIGIN/../../$(PKG)' $(LDLIBS)
 
+# ThreadSanitizer CPU build of the threaded runtime (in-process ranks,
+# ThreadComm, scheduler lanes): every host source instrumented, the device
+# objects linked unchanged; bin/tsan_check runs on the host target.
+#   make tsan && TSAN_OPTIONS=halt_on_error=1 OMP_NUM_THREADS=1 bin/tsan_check
+TSAN_BUILD := build/tsan
+TSAN_FLAGS := -std=c++17 -O1 -g -fPIC -fsanitize=thread -fno-omit-frame-pointer -fopenmp -march=x86-64-v3 \
+              -fcx-fortran-rules -Wno-unused-function -Wno-sign-compare $(INC) $(DEFS)
+TSAN_OBJ  := $(patsubst csrc/src/%.cc,$(TSAN_BUILD)/s_%.o,$(CC_SRC))
+$(TSAN_BUILD)/s_%.o: csrc/src/%.cc $(HDRS)
+	@mkdir -p $(TSAN_BUILD)
+	$(CXX) $(TSAN_FLAGS) -c $< -o $@
+bin/tsan_check: csrc/tools/tsan_check.cc $(TSAN_OBJ) $(HIP_OBJ)
+	@mkdir -p bin
+	$(CXX) $(TSAN_FLAGS) $< $(TSAN_OBJ) $(HIP_OBJ) -o $@ $(LDLIBS)
+tsan: bin/tsan_check
+
 clean:
 	rm -rf build $(LIB) $(PYMOD) $(LAPACK_API) $(SCALAPACK_API)
 
-.PHONY: all clean tester examples
+.PHONY: all clean tester examples tsan

@@ -26,6 +26,7 @@
 #include "lu_dist.hh"
 #include "../kernels/kernels.hh"
 
+#include <atomic>
 #include <algorithm>
 #include <numeric>
 #include <unordered_map>
@@ -168,7 +169,8 @@ void permute_rows_dist(BaseMatrix<T> const& A, RowPairs const& P, int64_t c0, in
 
 /// Per-process counters of the exact row exchange (tests / diagnostics):
 /// elements this process sent, and the rows behind them (summed over ranges).
-struct RowXStats { int64_t elems = 0, rows = 0; };
+// updated by every rank thread of an in-process grid: atomics (TSan, make tsan)
+struct RowXStats { std::atomic<int64_t> elems{0}, rows{0}; };
 RowXStats& rowx_stats() { static RowXStats s; return s; }
 
 /// Exact row exchange of one LU step on a p > 1 grid.  The slot lists of the
@@ -1241,7 +1243,7 @@ template void apply_pivots<std::complex<double>>(Pivots const&, BaseMatrix<std::
 /// Counters of the exact LU row exchange on this process (elements sent,
 /// rows sent summed over column ranges); reset with lu_rowx_reset().
 void lu_rowx_stats(int64_t& elems, int64_t& rows) { elems = rowx_stats().elems; rows = rowx_stats().rows; }
-void lu_rowx_reset() { rowx_stats() = RowXStats{}; }
+void lu_rowx_reset() { rowx_stats().elems = 0; rowx_stats().rows = 0; }
 
 #define SLATE_GETRF_INST(T)                                                                  \
     template int64_t getrf<T>(Matrix<T>&, Pivots&, Options const&);                         \
