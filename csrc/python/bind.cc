@@ -450,6 +450,9 @@ PYBIND11_MODULE(_slate, m) {
     m.def("set_device", &device::set_device);
     m.def("get_device", &device::get_device);
     m.def("sync", &slate::sync, py::call_guard<py::gil_scoped_release>());
+    m.def("set_ops_queue", [](int q) { ops_queue() = q; });
+    m.def("queue_sync", [](int q) { slate_hip_call(hipStreamSynchronize(device::queue(q))); },
+          py::call_guard<py::gil_scoped_release>());
     m.def("release_cache", &device::release_cache);
     m.def("lane_log_enable", &Sched::lane_log_enable);
     m.def("storage_alloc_max", &storage_alloc_max);

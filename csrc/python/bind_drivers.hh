@@ -12,6 +12,12 @@ namespace py = pybind11;
 
 slate::Options to_options(py::dict d);
 
+/// HIP queue of the direct local-kernel entry points (lb_*): 0 by default;
+/// measurement scripts put them on the panel queue (1) with a background
+/// GEMM on the trailing queue to time a factorization's critical path under
+/// the contention the real run has (scripts/critpath.py --contended).
+inline int& ops_queue() { static int q = 0; return q; }
+
 template <typename T>
 void bind_drivers(py::module_& m, std::string const& s) {
     using namespace slate;
@@ -364,10 +370,17 @@ void bind_drivers(py::module_& m, std::string const& s) {
         return py::make_tuple(d, e); });
 
     // ---- direct local-kernel access on raw device pointers (single process)
-    auto dctx = []() { return lb::Ctx::device(0); };
+    auto dctx = []() { return lb::Ctx::device(ops_queue()); };
     auto dsync = [](lb::Ctx const& c) { slate_hip_call(hipStreamSynchronize(c.stream)); };
     auto cop = [](std::string const& x) { return x == "N" ? Op::NoTrans : x == "T" ? Op::Trans : Op::ConjTrans; };
     auto cup = [](std::string const& x) { return x == "L" ? Uplo::Lower : x == "U" ? Uplo::Upper : Uplo::General; };
+    // background GEMM: launched on `queue`, not waited for (queue_sync(queue))
+    DEF("lb_gemm_async", [=](int queue, std::string ta, std::string tb, int64_t mm, int64_t n, int64_t k, T a,
+                             uintptr_t A, int64_t lda, uintptr_t B, int64_t ldb, T b, uintptr_t C, int64_t ldc) {
+        py::gil_scoped_release r;
+        lb::gemm<T>(lb::Ctx::device(queue), cop(ta), cop(tb), mm, n, k, a, (T const*)A, lda, (T const*)B, ldb, b,
+                    (T*)C, ldc);
+    });
     DEF("lb_gemm", [=](std::string ta, std::string tb, int64_t mm, int64_t n, int64_t k, T a, uintptr_t A, int64_t lda,
                        uintptr_t B, int64_t ldb, T b, uintptr_t C, int64_t ldc) {
         py::gil_scoped_release r;

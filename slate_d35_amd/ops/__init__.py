@@ -10,7 +10,17 @@ from __future__ import annotations
 
 from .. import _slate
 
-__all__ = ["have_native_ops", "gemm", "herk", "trsm", "potrf", "getrf_panel", "geqrf_panel", "lu_sign"]
+__all__ = ["have_native_ops", "gemm", "gemm_async", "herk", "trsm", "potrf", "getrf_panel", "geqrf_panel", "lu_sign",
+           "set_queue", "queue_sync"]
+
+
+def set_queue(q: int):
+    """HIP queue of the calls below (0 default; 1 = the high-priority panel queue)."""
+    _slate.set_ops_queue(q)
+
+
+def queue_sync(q: int):
+    _slate.queue_sync(q)
 
 
 def have_native_ops() -> bool:
@@ -30,7 +40,9 @@ def _cm(t):
     import torch
     assert t.dim() == 2 and t.stride(1) == 1, "row-major contiguous rows expected"
     if t.is_cuda:
-        torch.cuda.synchronize(t.device)
+        # torch's own stream only: a device-wide synchronize would also wait
+        # for work queued on the framework's queues (e.g. gemm_async)
+        torch.cuda.current_stream(t.device).synchronize()
     return t.data_ptr(), t.shape[1], t.shape[0], t.stride(0)
 
 
@@ -43,6 +55,16 @@ def gemm(opA: str, opB: str, alpha, A, B, beta, C):
     pc, mc, nc, ldc = _cm(C)
     k = na if opA == "N" else ma
     fn(opA, opB, mc, nc, k, alpha, pa, lda, pb, ldb, beta, pc, ldc)
+
+
+def gemm_async(queue: int, opA: str, opB: str, alpha, A, B, beta, C):
+    """gemm launched on `queue` without waiting for it (queue_sync(queue))."""
+    fn = getattr(_slate, f"lb_gemm_async_{_suffix(C)}")
+    pa, ma, na, lda = _cm(A)
+    pb, mb, nb, ldb = _cm(B)
+    pc, mc, nc, ldc = _cm(C)
+    k = na if opA == "N" else ma
+    fn(queue, opA, opB, mc, nc, k, alpha, pa, lda, pb, ldb, beta, pc, ldc)
 
 
 def herk(uplo: str, op: str, alpha, A, beta, C):
