@@ -14,9 +14,12 @@
 #include "../src/lu_dist.hh"
 #include "slate_amd/trace.hh"
 #include "slate_amd/runtime.hh"
+#include "slate_amd/inproc.hh"
 #include "bind_drivers.hh"
 #include <pybind11/numpy.h>
 
+#include <algorithm>
+#include <cmath>
 #include <complex>
 #include <chrono>
 #include <cstring>
@@ -400,6 +403,32 @@ PYBIND11_MODULE(_slate, m) {
     m.def("lu_rowx_stats", []() { int64_t e = 0, r = 0; lu_rowx_stats(e, r); return py::make_tuple(e, r); });
     m.def("lu_rowx_reset", &lu_rowx_reset);
     m.def("inproc_run_count", &inproc_run_count);
+    // self-check of the in-process all-reduce (small: all-to-all copies;
+    // >= 1 MiB with > 2 ranks: reduce-scatter + all-gather): every rank
+    // contributes x_r[i] = r + i * 1e-3; returns the max error over ranks
+    m.def("inproc_allreduce_check", [](int nranks, int64_t count) {
+        std::vector<double> err(nranks, 0.0);
+        {
+            py::gil_scoped_release r;
+            run_in_process(1, nranks, [&](int rank, GridPtr const& g) {
+                const bool dev = device::available();
+                std::vector<double> h(count);
+                for (int64_t i = 0; i < count; ++i) h[i] = rank + double(i % 1000) * 1e-3;
+                device::Buffer<double> d(dev ? count : 0);
+                hipStream_t st = dev ? device::queue(0) : nullptr;
+                double* p = h.data();
+                if (dev) { device::memcpy_async(d.data(), h.data(), count * 8, st); p = d.data(); }
+                g->world().allreduce(p, p, size_t(count), ScalarType::Float64, ReduceOp::Sum,
+                                     dev ? Loc::Device : Loc::Host, st);
+                if (dev) { device::memcpy_async(h.data(), d.data(), count * 8, st); slate_hip_call(hipStreamSynchronize(st)); }
+                const double base = nranks * (nranks - 1) / 2.0;
+                double e = 0;
+                for (int64_t i = 0; i < count; ++i) e = std::max(e, std::abs(h[i] - (base + nranks * double(i % 1000) * 1e-3)));
+                err[rank] = e;
+            });
+        }
+        return *std::max_element(err.begin(), err.end());
+    });
     m.def("inproc_last_shape", []() { int p = 0, q = 0; inproc_last_shape(p, q); return py::make_tuple(p, q); });
     m.def("comm_abort_all", &comm_abort_all, py::call_guard<py::gil_scoped_release>());
     m.def("comm_async_errors", &comm_async_errors);

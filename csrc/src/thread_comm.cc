@@ -25,7 +25,9 @@
 #include <algorithm>
 #include <complex>
 #include <condition_variable>
+#include <cstdio>
 #include <cstring>
+#include <string>
 #include <deque>
 #include <map>
 #include <mutex>
@@ -178,6 +180,10 @@ public:
             std::memcpy(recv, acc.data(), bytes);
             return;
         }
+        if (h.n > 2 && bytes >= (size_t(1) << 20)) {
+            allreduce_sliced(send, recv, elems, bytes / elems, tc, op, s);
+            return;
+        }
         h.a[me_] = {send, record(s)};
         h.barrier();
         destroy(pend_b_);
@@ -196,6 +202,49 @@ public:
                                      int64_t(elems), int64_t(elems), s);
         device::free_async(tmp, s);
         destroy(my_a);
+        pend_b_ = mine;
+    }
+
+    /// Large all-reduce as reduce-scatter + all-gather: rank r pulls slice r
+    /// of every rank's buffer, reduces it, and every rank then pulls the n
+    /// reduced slices -- about 2 x bytes of peer traffic per rank instead of
+    /// n x bytes for the all-to-all copy of the small-message path.
+    void allreduce_sliced(const void* send, void* recv, size_t elems, size_t esize, char tc, ReduceOp op,
+                          hipStream_t s) {
+        Hub& h = *hub_;
+        const int n = h.n;
+        auto lo = [&](int r) { return elems * size_t(r) / size_t(n); };
+        const size_t smax = (elems + n - 1) / n;                 // longest slice (elements)
+        const size_t mine_lo = lo(me_), mine_len = lo(me_ + 1) - mine_lo;
+        h.a[me_] = {send, record(s)};
+        h.barrier();                                             // (1) every send buffer ready
+        destroy(pend_b_);
+        char* tmp = static_cast<char*>(device::malloc_async(std::max<size_t>((n + 1) * smax * esize, 1), s));
+        char* red = tmp + size_t(n) * smax * esize;
+        for (int r = 0; r < n; ++r) {
+            if (r != me_) wait_on(s, h.a[r].ev);
+            device::memcpy_async(tmp + size_t(r) * smax * esize,
+                                 static_cast<const char*>(h.a[r].ptr) + mine_lo * esize, mine_len * esize, s);
+        }
+        if (mine_len > 0)
+            slate_amd::dev::reduce_slabs(tc, op == ReduceOp::Sum ? 0 : op == ReduceOp::Max ? 1 : 2, red, tmp, n,
+                                         int64_t(mine_len), int64_t(smax), s);
+        hipEvent_t my_a = h.a[me_].ev;
+        h.b[me_] = {red, record(s)};
+        h.barrier();                                             // (2) every reduced slice published
+        destroy(my_a);
+        // recv may alias send: every rank's reads of my send finished before its slice event
+        for (int r = 0; r < n; ++r) if (r != me_) wait_on(s, h.b[r].ev);
+        for (int r = 0; r < n; ++r)
+            device::memcpy_async(static_cast<char*>(recv) + lo(r) * esize, h.b[r].ptr, (lo(r + 1) - lo(r)) * esize,
+                                 s);
+        hipEvent_t my_b = h.b[me_].ev;
+        hipEvent_t mine = record(s);
+        h.a[me_] = {nullptr, mine};
+        h.barrier();                                             // (3) every copy of the slices issued
+        destroy(my_b);
+        for (int r = 0; r < n; ++r) if (r != me_) wait_on(s, h.a[r].ev);
+        device::free_async(tmp, s);                              // after the others read my slice
         pend_b_ = mine;
     }
 
@@ -325,10 +374,24 @@ void enable_peer_access(std::vector<int> const& devs) {
         for (int b : devs) {
             if (a == b) continue;
             int can = 0;
-            if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) continue;
+            if (hipDeviceCanAccessPeer(&can, a, b) != hipSuccess || !can) {
+                // copies between a and b still work, staged by the runtime through
+                // host memory -- far slower than xGMI: say so once
+                static std::once_flag warned;
+                std::call_once(warned, [&] {
+                    std::fprintf(stderr, "slate: GPU %d cannot access GPU %d as a peer; in-process ranks "
+                                 "exchange data through host staging (slow)\n", a, b);
+                });
+                continue;
+            }
             (void)hipSetDevice(a);
             hipError_t e = hipDeviceEnablePeerAccess(b, 0);
-            if (e != hipSuccess) (void)hipGetLastError();   // already enabled
+            if (e == hipErrorPeerAccessAlreadyEnabled || e == hipSuccess) { (void)hipGetLastError(); continue; }
+            (void)hipGetLastError();
+            (void)hipSetDevice(cur);
+            throw DeviceException(std::string("hipDeviceEnablePeerAccess(") + std::to_string(a) + " -> " +
+                                      std::to_string(b) + "): " + hipGetErrorString(e),
+                                  __func__, __FILE__, __LINE__);
         }
     (void)hipSetDevice(cur);
 }

@@ -782,3 +782,11 @@ print("INPROC_OK")
     env.update(SLATE_INPROC_RANKS="4", SLATE_SPREAD_MIN_N="256", OMP_NUM_THREADS="2")
     r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "INPROC_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize("nranks,count", [(3, 1000), (4, 300000), (5, 1 << 20), (2, 300000)])
+def test_inproc_allreduce_device(nranks, count):
+    """In-process all-reduce on device buffers: the all-to-all copy path for
+    small messages and the reduce-scatter + all-gather path (>= 1 MiB, more
+    than two ranks; uneven slices for 5 ranks)."""
+    assert s._slate.inproc_allreduce_check(nranks, count) < 1e-12

@@ -80,3 +80,11 @@ def test_set_lambda():
 def test_func_and_version():
     assert s.version()
     assert s.choose_grid(8) == (2, 4) and s.choose_grid(4) == (2, 2) and s.choose_grid(2) == (1, 2)
+
+
+def test_inproc_allreduce_host():
+    """The in-process transport's host mode (no GPU): all-reduce across rank threads."""
+    import slate_d35_amd as s
+    if s.device_available():
+        pytest.skip("host-mode check")
+    assert s._slate.inproc_allreduce_check(3, 5000) < 1e-12
