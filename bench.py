@@ -57,6 +57,9 @@ EXTRAS = {
     # the reference's semantics (src/gesv_mixed.cc:219-279): classical
     # refinement, then the fp64 fallback -- no GMRES-IR escalation
     "cfg5_dgesv_mixed_refsem": ("dgesv_mixed", None, None, None),
+    # the default LU (MethodLU::PartialPiv: what gesv / LAPACK / ScaLAPACK
+    # callers get), tracked next to the tournament LU of the suite
+    "dgetrf_ppiv": ("dgetrf", None, 1024, None),
 }
 
 
@@ -390,10 +393,11 @@ def main(a):
                 info = s.potrf(s.HermitianMatrix(s.Uplo.Lower, mats["A"]), **o)
                 assert info == 0, f"dpotrf info={info}"
             elif rname == "dgetrf":
-                if a.method_lu == "tntpiv":
+                if a.method_lu == "tntpiv" and not label.endswith("_ppiv"):
                     info, piv = s.getrf_tntpiv(mats["A"], **o)
                 else:
                     info, piv = s.getrf(mats["A"], **o)
+                extra["method"] = "tntpiv" if (a.method_lu == "tntpiv" and not label.endswith("_ppiv")) else "ppiv"
                 mats["piv"] = piv
                 assert info == 0, f"dgetrf info={info}"
             elif rname == "dgeqrf":
