@@ -12,6 +12,7 @@
 
 #include <cstdlib>
 #include <stdexcept>
+#include <type_traits>
 
 namespace slate_amd {
 namespace dev {
@@ -331,6 +332,252 @@ void potrf_inv_small_kernel(int n, T* A, int64_t lda, T* W, int64_t ldw, int* in
 }
 
 //------------------------------------------------------------------------------
+// Leaf of the blocked device potrf (lower): the Cholesky factor of the b x b
+// (b <= 64) diagonal block at A AND the rows below it, A21 := A21 L11^{-H}, in
+// ONE launch of single-wave workgroups.  Replaces the factor + inverse kernel,
+// the A21 * inv GEMM and the copy back per 64 columns (50 + 22 + 5 us per leaf
+// on an idle MI355X).
+//  * Every workgroup factors the diagonal block, right-looking, lane i owning
+//    row i in registers: step j takes the pivot by v_readlane, writes column j
+//    of L to LDS (diagonal as its reciprocal), updates element j+1 at once
+//    from lane j+1 (the next step's pivot: the only update on the step-to-step
+//    chain) and applies the rest of column j-1's rank-1 update from LDS
+//    broadcast reads one step late, so those reads are in flight behind the
+//    pivot chain.  Workgroup 0 writes L11; workgroup w >= 1 solves rows
+//    (w-1)*64 .. +63 of A21 (right-looking substitution: the updates of a
+//    step are independent FMAs).
+//  * LDS columns stream in 16-row groups with the next group's reads issued
+//    before the current group's FMAs, each group ending in an empty volatile
+//    asm on its registers plus a scheduling barrier (left alone, the
+//    scheduler sank the FMAs below every read and spilled 15 KB per lane).
+//  * A partial leaf (b < 64) is factored as diag(A11, I), so every step is
+//    unconditional; loads use wave-uniform column pointers and clamped rows
+//    (no per-load branches or 64-bit address math per lane).
+//  * rsqrt by v_rsq plus one Newton step instead of sqrt and a division.
+constexpr int kLeafG = 16;    // rows per LDS group
+#ifdef LEAF_PROBE
+__device__ long long g_leaf_probe[64 * 8];
+#define LEAF_STAMP(k)                                                                      \
+    do {                                                                                   \
+        __builtin_amdgcn_s_waitcnt(0);                                                     \
+        const long long t_ = clock64();                                                    \
+        if (threadIdx.x == 0 && blockIdx.x < 64) g_leaf_probe[blockIdx.x * 8 + (k)] = t_;  \
+    } while (0)
+#else
+#define LEAF_STAMP(k) do {} while (0)
+#endif
+template <typename T>
+__device__ __forceinline__ void leaf_pin1(T& v) {
+    if constexpr (is_cplx<T>::value) asm volatile("" : "+v"(v.re), "+v"(v.im));
+    else asm volatile("" : "+v"(v));
+}
+template <typename R>
+__device__ __forceinline__ R leaf_rsqrt(R d) {
+    R r;
+    if constexpr (sizeof(R) == 8) r = __builtin_amdgcn_rsq(d);
+    else r = __builtin_amdgcn_rsqf(d);
+    const R e = fma(-d * r, r, R(1));       // 1 - d r^2
+    return fma(R(0.5) * r, e, r);
+}
+// first group of a stream column: the factor's delayed update of column k
+// covers rows >= k + 2, the solve's column c rows >= c (diagonal first)
+__device__ constexpr int leaf_g0(int first_row) { return first_row / kLeafG; }
+// groups before the factor stream's column k (rows >= k + 2 of each column)
+__device__ constexpr int leaf_fq0(int k) {
+    int q = 0;
+    for (int t = 0; t < k; ++t) q += 64 / kLeafG - leaf_g0(t + 2);
+    return q;
+}
+// groups before the solve stream's column c (rows >= c)
+__device__ constexpr int leaf_sq0(int c) {
+    int q = 0;
+    for (int t = 0; t < c; ++t) q += 64 / kLeafG - leaf_g0(t);
+    return q;
+}
+// solve stream: next group after (col, grp)
+struct LeafPos { int col, grp; };
+__device__ constexpr LeafPos leaf_snext(LeafPos p) {
+    return p.grp + 1 < 64 / kLeafG ? LeafPos{p.col, p.grp + 1} : LeafPos{p.col + 1, leaf_g0(p.col + 1)};
+}
+// The 64 steps are expanded by the preprocessor, each a call of a generic
+// lambda with its step number as a type: a `#pragma unroll` loop of this size
+// exceeds LLVM's full-unroll threshold and falls back to a rolled loop whose
+// register arrays are indexed dynamically (scratch).
+#define LEAF_REP4(M, x) M((x)) M((x) + 1) M((x) + 2) M((x) + 3)
+#define LEAF_REP16(M, x) LEAF_REP4(M, (x)) LEAF_REP4(M, (x) + 4) LEAF_REP4(M, (x) + 8) LEAF_REP4(M, (x) + 12)
+#define LEAF_REP64(M) LEAF_REP16(M, 0) LEAF_REP16(M, 16) LEAF_REP16(M, 32) LEAF_REP16(M, 48)
+
+template <typename T>
+__global__ __launch_bounds__(64)
+void potrf_leaf_kernel(int b, int r, T* A, int64_t lda, int* info, int info_offset, T* W, const T* Wprev, T* Aprev,
+                       int bprev) {
+    SLATE_PANEL_WAVE_PRIO();
+    using R = real_t<T>;
+    constexpr int LS = 64 + 2;              // column stride (16-B aligned groups)
+    __shared__ __attribute__((aligned(16))) T LT[64 * LS];   // LT[j*LS + l] = L(l, j)
+    const int i = threadIdx.x;
+    LEAF_STAMP(0);
+    {
+        T a[64];
+        {
+            // columns past b re-read column b-1 (their values are not used:
+            // i >= l >= b fails i < b); the column offset runs in SGPRs
+            const T* Ai = A + min(i, b - 1);
+            int64_t off = 0;
+            #pragma unroll
+            for (int l = 0; l < 64; ++l) {
+                const T v = Ai[off];
+                a[l] = (i >= l && i < b) ? v : ((i == l) ? one<T>() : zero<T>());
+                if (l + 1 < b) off += lda;
+            }
+        }
+        LEAF_STAMP(1);
+        int fail = 0;
+        T buf[2][kLeafG];
+        auto step = [&](auto jc) __attribute__((always_inline)) {
+            constexpr int j = decltype(jc)::value;
+            // pivot: all earlier columns' updates of element j are in
+            const R d = real(bcast_lane(a[j], j));
+            if (!(d > R(0)) && fail == 0) fail = j + 1;
+            const R rs = leaf_rsqrt(d);
+            const R sd = d * rs;
+            const T Lij = (i == j) ? make_val<T>((double)sd) : ((i > j) ? a[j] * rs : zero<T>());
+            a[j] = Lij;
+            LT[j * LS + i] = (i == j) ? make_val<T>((double)rs) : Lij;
+            if constexpr (j + 1 < 64) {
+                a[j + 1] -= Lij * conj(bcast_lane(Lij, j + 1));
+                leaf_pin1(a[j + 1]);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            if constexpr (j == 0) {
+                // prime the stream: column 0's first group (rows >= 2)
+                #pragma unroll
+                for (int e = 0; e < kLeafG; ++e) buf[0][e] = LT[leaf_g0(2) * kLeafG + e];
+            }
+            // column k = j - 1's update of rows >= j + 1, prefetching one group ahead
+            constexpr int k = j - 1;
+            if constexpr (k >= 0 && k + 2 < 64) {
+                constexpr int q0 = leaf_fq0(k), g0 = leaf_g0(k + 2);
+                const T Lk = a[k];           // L(i, k)
+                #pragma unroll
+                for (int g = g0; g < 64 / kLeafG; ++g) {
+                    const int q = q0 + g - g0;
+                    const int nk = (g + 1 < 64 / kLeafG) ? k : k + 1;
+                    const int ng = (g + 1 < 64 / kLeafG) ? g + 1 : leaf_g0(k + 3);
+                    if (nk + 2 < 64) {
+                        #pragma unroll
+                        for (int e = 0; e < kLeafG; ++e) buf[(q + 1) & 1][e] = LT[nk * LS + ng * kLeafG + e];
+                    }
+                    #pragma unroll
+                    for (int e = 0; e < kLeafG; ++e)
+                        if (g * kLeafG + e >= k + 2) a[g * kLeafG + e] -= Lk * conj(buf[q & 1][e]);
+                    #pragma unroll
+                    for (int e = 0; e < kLeafG; ++e)
+                        if (g * kLeafG + e >= k + 2) leaf_pin1(a[g * kLeafG + e]);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            }
+        };
+#define LEAF_FSTEP(x) step(std::integral_constant<int, (x)>{});
+        LEAF_REP64(LEAF_FSTEP)
+#undef LEAF_FSTEP
+        LEAF_STAMP(2);
+        if (blockIdx.x == 0) {
+            if (fail && fail <= b && info && i == 0 && *info == 0) *info = info_offset + fail;
+            // With r > 0 the other workgroups may not have read A11 yet (they
+            // can start late behind a concurrent GEMM): L11 goes to W and the
+            // next leaf's workgroup 0 copies it into place (Wprev -> Aprev),
+            // when every reader of that block has finished.
+            const bool direct = (r == 0);
+            T* Ai = direct ? A + i : W + i;
+            const int64_t ld = direct ? lda : 64;
+            int64_t off = 0;
+            #pragma unroll
+            for (int l = 0; l < 64; ++l) {
+                if (l <= i && i < b) Ai[off] = a[l];
+                if (l + 1 < b) off += ld;
+                else break;
+            }
+        }
+    }
+    if (blockIdx.x == 0 && Aprev) {
+        T* Ap = Aprev + i;
+        const T* Wp = Wprev + i;
+        int64_t off = 0;
+        #pragma unroll
+        for (int l = 0; l < 64; ++l) {
+            if (l >= bprev) break;
+            if (l <= i && i < bprev) Ap[off] = Wp[l * 64];
+            off += lda;
+        }
+    }
+    if (blockIdx.x == 0) return;
+    __syncthreads();
+    const int64_t row = b + (int64_t)(blockIdx.x - 1) * 64 + i;
+    const bool live = row < b + (int64_t)r;
+    const int64_t rr = live ? row : b;      // r > 0 here: row b exists
+    T y[64];
+    {
+        const T* Ar = A + rr;
+        int64_t off = 0;
+        #pragma unroll
+        for (int c = 0; c < 64; ++c) {
+            const T v = Ar[off];
+            y[c] = (live && c < b) ? v : zero<T>();
+            if (c + 1 < b) off += lda;
+        }
+    }
+    LEAF_STAMP(3);
+    {
+        // two groups in flight: prefetch group q + 2 while consuming group q
+        T buf[3][kLeafG];
+        #pragma unroll
+        for (int e = 0; e < kLeafG; ++e) {
+            buf[0][e] = LT[e];
+            buf[1][e] = LT[kLeafG + e];
+        }
+        auto step = [&](auto cc) __attribute__((always_inline)) {
+            constexpr int c = decltype(cc)::value;
+            constexpr int q0 = leaf_sq0(c), g0 = leaf_g0(c);
+            #pragma unroll
+            for (int g = g0; g < 64 / kLeafG; ++g) {
+                const int q = q0 + g - g0;
+                const LeafPos n2 = leaf_snext(leaf_snext(LeafPos{c, g}));
+                if (n2.col < 64) {
+                    #pragma unroll
+                    for (int e = 0; e < kLeafG; ++e) buf[(q + 2) % 3][e] = LT[n2.col * LS + n2.grp * kLeafG + e];
+                }
+                #pragma unroll
+                for (int e = 0; e < kLeafG; ++e) {
+                    const int l = g * kLeafG + e;
+                    if (l == c) y[c] = y[c] * buf[q % 3][e];          // reciprocal diagonal
+                    else if (l > c) y[l] -= y[c] * conj(buf[q % 3][e]);
+                }
+                #pragma unroll
+                for (int e = 0; e < kLeafG; ++e)
+                    if (g * kLeafG + e >= c) leaf_pin1(y[g * kLeafG + e]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+        };
+#define LEAF_SSTEP(x) step(std::integral_constant<int, (x)>{});
+        LEAF_REP64(LEAF_SSTEP)
+#undef LEAF_SSTEP
+    }
+    LEAF_STAMP(4);
+    if (live) {
+        T* Ar = A + row;
+        int64_t off = 0;
+        #pragma unroll
+        for (int c = 0; c < 64; ++c) {
+            Ar[off] = y[c];
+            if (c + 1 < b) off += lda;
+            else break;
+        }
+    }
+    LEAF_STAMP(5);
+}
+
+//------------------------------------------------------------------------------
 // Left triangular solve A X = B (NoTrans) with a small triangle (m <= 64):
 // the triangle (identity-padded) and its diagonal reciprocals in LDS, one lane
 // per right-hand-side column holding that column in registers (forward or
@@ -548,6 +795,24 @@ void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int
 }
 
 template <typename T>
+void potrf_leaf(int b, int64_t r, T* A, int64_t lda, int* info, int info_offset, T* W, const T* Wprev, T* Aprev,
+                int bprev, hipStream_t s) {
+    if (b <= 0) return;
+    if (b > 64 || r < 0 || bprev > 64) throw std::invalid_argument("potrf_leaf: b, bprev must be <= 64 and r >= 0");
+    if (r > 0 && !W) throw std::invalid_argument("potrf_leaf: r > 0 needs the 64 x 64 staging block W");
+    if (Aprev && !Wprev) throw std::invalid_argument("potrf_leaf: Aprev needs Wprev");
+    if constexpr (sizeof(T) > 8) {
+        // complex<double>: the per-lane rows need 256 VGPRs each; the
+        // blocked potrf keeps the inverse-based leaf for it
+        throw std::invalid_argument("potrf_leaf: complex<double> is not supported");
+    } else {
+        const unsigned nblk = 1 + (unsigned)((r + 63) / 64);
+        hipLaunchKernelGGL(potrf_leaf_kernel<T>, dim3(nblk), dim3(64), 0, s, b, (int)r, A, lda, info, info_offset, W,
+                           Wprev, Aprev, bprev);
+    }
+}
+
+template <typename T>
 void trsm_small(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
     if (m <= 32)
@@ -614,6 +879,7 @@ void laswp(int64_t n, T* A, int64_t lda, int64_t k1, int64_t k2, const int64_t* 
     template void trtri_diag_stack<T>(char, char, int64_t, int, const T*, int64_t, T*, int64_t, hipStream_t); \
     template void potrf_small<T>(char, int, T*, int64_t, int*, int, hipStream_t);                          \
     template void potrf_inv_small<T>(int, T*, int64_t, T*, int64_t, int*, int, hipStream_t);                 \
+    template void potrf_leaf<T>(int, int64_t, T*, int64_t, int*, int, T*, const T*, T*, int, hipStream_t);   \
     template void trsm_small<T>(char, char, int, int64_t, const T*, int64_t, T*, int64_t, hipStream_t);     \
     template void permute_rows<T>(int64_t, T*, int64_t, const int64_t*, const int64_t*, const int*, int, hipStream_t); \
     template void form_v<T>(int64_t, int64_t, int64_t, const T*, int64_t, T*, int64_t, hipStream_t);                     \

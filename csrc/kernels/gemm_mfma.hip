@@ -479,6 +479,19 @@ static bool big_tiles(int64_t m, int64_t n, int64_t batch) {
     return m >= 512 && ((m + 255) / 256) * ((n + 127) / 128) * batch >= 512;
 }
 
+// Latency-bound products (the panels' and the Cholesky leaves' GEMMs: a few
+// hundred rows, K <= 512): fewer 128 x 128 tiles than half the CUs leave
+// most of the chip idle while each workgroup walks K alone at one CU's fp64
+// MFMA rate (~0.3 TFLOP/s: a 128 x 128 x 64 tile is >= 7 us).  64 x 64 tiles
+// (4 waves of 32 x 32) give 4x the workgroups.  SLATE_GEMM_SMALL=0 disables.
+static bool small_tiles(int64_t m, int64_t n, int64_t batch, bool tri) {
+    static int env = [] { const char* e = std::getenv("SLATE_GEMM_SMALL"); return e ? std::atoi(e) : 1; }();
+    if (!env) return false;
+    const int64_t mt = (m + 127) / 128, nt = (n + 127) / 128;
+    const int64_t tiles = (tri ? mt * (mt + 1) / 2 : mt * nt) * batch;
+    return tiles < 128;
+}
+
 template <typename T, bool A_KC, bool B_KC, char TRI = 0>
 static void launch_gemm(int64_t m, int64_t n, int64_t k, T alpha,
                         const T* A, int64_t lda, int64_t sA,
@@ -490,6 +503,13 @@ static void launch_gemm(int64_t m, int64_t n, int64_t k, T alpha,
     auto al = [](const void* p) { return (reinterpret_cast<uintptr_t>(p) % 16) == 0; };
     bool aligned = al(A) && al(B) && (lda % VEC == 0) && (ldb % VEC == 0)
                 && (batch == 1 || (sA % VEC == 0 && sB % VEC == 0));
+    if constexpr (TRI != 'S') {
+        if (small_tiles(m, n, batch, TRI != 0)) {
+            launch_tile<T, A_KC, B_KC, TRI, 64, 64, 16, 32, 32>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc,
+                                                                 sC, batch, aligned, stream);
+            return;
+        }
+    }
     if constexpr (TRI == 0 && sizeof(T) == 4) {
         if (big_tiles(m, n, batch)) {
             launch_tile<T, A_KC, B_KC, TRI, 256, 128>(m, n, k, alpha, A, lda, sA, B, ldb, sB, beta, C, ldc, sC,

@@ -257,6 +257,13 @@ void potrf_small(char uplo, int n, T* A, int64_t lda, int* info, int info_offset
 /// Lower Cholesky of an n <= 64 block (in place) plus the 64 x 64 inverse of its factor in W
 template <typename T>
 void potrf_inv_small(int n, T* A, int64_t lda, T* W, int64_t ldw, int* info, int info_offset, hipStream_t s);
+/// Lower Cholesky of a b <= 64 diagonal block and A21 := A21 L11^{-H} for the
+/// r rows below it, one launch.  With r > 0, L11 goes to the 64 x 64 block W
+/// (ld 64), to be copied into A by the next call (Wprev -> Aprev, bprev
+/// columns), when no workgroup of this call can still be reading A11.
+template <typename T>
+void potrf_leaf(int b, int64_t r, T* A, int64_t lda, int* info, int info_offset, T* W, const T* Wprev, T* Aprev,
+                int bprev, hipStream_t s);
 /// Left NoTrans triangular solve A X = B with m <= 64 (alpha = 1), one launch
 template <typename T>
 void trsm_small(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb, hipStream_t s);

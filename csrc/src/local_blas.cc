@@ -604,7 +604,21 @@ void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int
         return;
     }
     constexpr int64_t NB0 = 64;
-    if (n <= NB0) { kd::potrf_small(upc(uplo), int(n), dptr(A), lda, info, int(info_offset), c.stream); return; }
+    // Two launches per leaf (sizeof(T) <= 8: the leaf kernel's per-lane row
+    // fits in 128 VGPRs): factor + A21 solve in one kernel, then the trailing
+    // triangle.  SLATE_POTRF_LEAF=0 keeps the inverse-based leaf.
+    static const bool leaf = [] {
+        const char* e = std::getenv("SLATE_POTRF_LEAF");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    const bool use_leaf = sizeof(T) <= 8 && leaf && uplo == Uplo::Lower;
+    if (n <= NB0) {
+        if (use_leaf)
+            kd::potrf_leaf<kd::dev_t<T>>(int(n), 0, dptr(A), lda, info, int(info_offset), nullptr, nullptr, nullptr, 0,
+                                     c.stream);
+        else kd::potrf_small(upc(uplo), int(n), dptr(A), lda, info, int(info_offset), c.stream);
+        return;
+    }
     static const bool blocked = [] {
         const char* e = std::getenv("SLATE_POTRF_BLOCKED");
         return e ? std::atoi(e) != 0 : true;
@@ -630,6 +644,25 @@ void potrf(Ctx const& c, Uplo uplo, int64_t n, T* A, int64_t lda, int* info, int
         // n = 512 against ~29 here); on the factorization's critical path
         // each launch waits for a CU slot behind the trailing update.
         hipStream_t s = c.stream;
+        if (use_leaf) {
+            // L11 of leaf k is staged in Wk[k & 1] and copied into A by leaf k+1
+            Scratch sc(c);
+            T* Wk[2] = {sc.alloc<T>(size_t(NB0) * NB0), sc.alloc<T>(size_t(NB0) * NB0)};
+            T* Aprev = nullptr;
+            int bprev = 0;
+            for (int64_t j0 = 0, k = 0; j0 < n; j0 += NB0, ++k) {
+                const int64_t b = std::min(NB0, n - j0), r = n - j0 - b;
+                T* Ajj = A + j0 + j0 * lda;
+                kd::potrf_leaf<kd::dev_t<T>>(int(b), r, dptr(Ajj), lda, info, int(info_offset + j0), dptr(Wk[k & 1]),
+                                         Aprev ? dptr(Wk[(k + 1) & 1]) : nullptr, dptr(Aprev), bprev, s);
+                Aprev = Ajj;
+                bprev = int(b);
+                if (r == 0) break;
+                T* Ab = Ajj + b;
+                dgemm(s, 'L', Op::NoTrans, Op::ConjTrans, r, r, b, T(-1), Ab, lda, Ab, lda, T(1), Ab + b * lda, lda);
+            }
+            return;
+        }
         Scratch sc(c);
         T* Winv = sc.alloc<T>(size_t(NB0) * NB0);
         T* Y = sc.alloc<T>(size_t(n) * NB0);

@@ -247,6 +247,27 @@ def test_potrf_kernel_not_spd(n, bad):
     assert info == bad + 1
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32, np.complex64, np.complex128])
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 130, 700, 1024])
+def test_potrf_leaf_all_types(n, dt):
+    """Blocked lower potrf: 64-column leaves (factor + A21 solve in one launch
+    for sizeof(T) <= 8, the inverse-based leaf for complex128), partial last
+    leaves, and the small-tile triangular updates between them."""
+    torch = _torch()
+    a = s.utils.spd_matrix(n, dtype=dt)
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    info = s.ops.potrf("L", tA)
+    L = np.tril(tA.cpu().numpy().T).astype(np.complex128)
+    tol = 1e-5 if dt in (np.float32, np.complex64) else 1e-13
+    assert info == 0 and relerr(L @ L.conj().T, a) < tol
+    if n >= 130:
+        for bad in (0, 63, 64, 100, n - 1):
+            b = a.copy()
+            b[bad, bad] = -1e6
+            tB = torch.from_numpy(np.ascontiguousarray(b.T)).cuda()
+            assert s.ops.potrf("L", tB) == bad + 1, bad
+
+
 @pytest.mark.parametrize("m,n", [(1000, 64), (4096, 256), (777, 100), (512, 512)])
 def test_getrf_panel_kernel(m, n):
     torch = _torch()
