@@ -9,6 +9,7 @@
 // each thread handles several columns.
 #include "device_common.hh"
 #include "kernels.hh"
+#include "leaf_common.hh"
 
 #include <cstdlib>
 #include <stdexcept>
@@ -354,66 +355,13 @@ void potrf_inv_small_kernel(int n, T* A, int64_t lda, T* W, int64_t ldw, int* in
 //    unconditional; loads use wave-uniform column pointers and clamped rows
 //    (no per-load branches or 64-bit address math per lane).
 //  * rsqrt by v_rsq plus one Newton step instead of sqrt and a division.
-constexpr int kLeafG = 16;    // rows per LDS group
-#ifdef LEAF_PROBE
-__device__ long long g_leaf_probe[64 * 8];
-#define LEAF_STAMP(k)                                                                      \
-    do {                                                                                   \
-        __builtin_amdgcn_s_waitcnt(0);                                                     \
-        const long long t_ = clock64();                                                    \
-        if (threadIdx.x == 0 && blockIdx.x < 64) g_leaf_probe[blockIdx.x * 8 + (k)] = t_;  \
-    } while (0)
-#else
-#define LEAF_STAMP(k) do {} while (0)
-#endif
-template <typename T>
-__device__ __forceinline__ void leaf_pin1(T& v) {
-    if constexpr (is_cplx<T>::value) asm volatile("" : "+v"(v.re), "+v"(v.im));
-    else asm volatile("" : "+v"(v));
-}
-template <typename R>
-__device__ __forceinline__ R leaf_rsqrt(R d) {
-    R r;
-    if constexpr (sizeof(R) == 8) r = __builtin_amdgcn_rsq(d);
-    else r = __builtin_amdgcn_rsqf(d);
-    const R e = fma(-d * r, r, R(1));       // 1 - d r^2
-    return fma(R(0.5) * r, e, r);
-}
-// first group of a stream column: the factor's delayed update of column k
-// covers rows >= k + 2, the solve's column c rows >= c (diagonal first)
-__device__ constexpr int leaf_g0(int first_row) { return first_row / kLeafG; }
-// groups before the factor stream's column k (rows >= k + 2 of each column)
-__device__ constexpr int leaf_fq0(int k) {
-    int q = 0;
-    for (int t = 0; t < k; ++t) q += 64 / kLeafG - leaf_g0(t + 2);
-    return q;
-}
-// groups before the solve stream's column c (rows >= c)
-__device__ constexpr int leaf_sq0(int c) {
-    int q = 0;
-    for (int t = 0; t < c; ++t) q += 64 / kLeafG - leaf_g0(t);
-    return q;
-}
-// solve stream: next group after (col, grp)
-struct LeafPos { int col, grp; };
-__device__ constexpr LeafPos leaf_snext(LeafPos p) {
-    return p.grp + 1 < 64 / kLeafG ? LeafPos{p.col, p.grp + 1} : LeafPos{p.col + 1, leaf_g0(p.col + 1)};
-}
-// The 64 steps are expanded by the preprocessor, each a call of a generic
-// lambda with its step number as a type: a `#pragma unroll` loop of this size
-// exceeds LLVM's full-unroll threshold and falls back to a rolled loop whose
-// register arrays are indexed dynamically (scratch).
-#define LEAF_REP4(M, x) M((x)) M((x) + 1) M((x) + 2) M((x) + 3)
-#define LEAF_REP16(M, x) LEAF_REP4(M, (x)) LEAF_REP4(M, (x) + 4) LEAF_REP4(M, (x) + 8) LEAF_REP4(M, (x) + 12)
-#define LEAF_REP64(M) LEAF_REP16(M, 0) LEAF_REP16(M, 16) LEAF_REP16(M, 32) LEAF_REP16(M, 48)
-
 template <typename T>
 __global__ __launch_bounds__(64)
 void potrf_leaf_kernel(int b, int r, T* A, int64_t lda, int* info, int info_offset, T* W, const T* Wprev, T* Aprev,
                        int bprev) {
     SLATE_PANEL_WAVE_PRIO();
     using R = real_t<T>;
-    constexpr int LS = 64 + 2;              // column stride (16-B aligned groups)
+    constexpr int LS = kLeafLS;
     __shared__ __attribute__((aligned(16))) T LT[64 * LS];   // LT[j*LS + l] = L(l, j)
     const int i = threadIdx.x;
     LEAF_STAMP(0);
@@ -493,10 +441,9 @@ void potrf_leaf_kernel(int b, int r, T* A, int64_t lda, int* info, int info_offs
             const int64_t ld = direct ? lda : 64;
             int64_t off = 0;
             #pragma unroll
-            for (int l = 0; l < 64; ++l) {
-                if (l <= i && i < b) Ai[off] = a[l];
-                if (l + 1 < b) off += ld;
-                else break;
+            for (int l = 0; l < 64; ++l) {      // predicated, not `break`: an early
+                if (l <= i && i < b) Ai[off] = a[l];   // exit can leave the loop
+                off += ld;                      // rolled and a[] in scratch
             }
         }
     }
@@ -506,8 +453,7 @@ void potrf_leaf_kernel(int b, int r, T* A, int64_t lda, int* info, int info_offs
         int64_t off = 0;
         #pragma unroll
         for (int l = 0; l < 64; ++l) {
-            if (l >= bprev) break;
-            if (l <= i && i < bprev) Ap[off] = Wp[l * 64];
+            if (l < bprev && l <= i && i < bprev) Ap[off] = Wp[l * 64];
             off += lda;
         }
     }
@@ -528,50 +474,15 @@ void potrf_leaf_kernel(int b, int r, T* A, int64_t lda, int* info, int info_offs
         }
     }
     LEAF_STAMP(3);
-    {
-        // two groups in flight: prefetch group q + 2 while consuming group q
-        T buf[3][kLeafG];
-        #pragma unroll
-        for (int e = 0; e < kLeafG; ++e) {
-            buf[0][e] = LT[e];
-            buf[1][e] = LT[kLeafG + e];
-        }
-        auto step = [&](auto cc) __attribute__((always_inline)) {
-            constexpr int c = decltype(cc)::value;
-            constexpr int q0 = leaf_sq0(c), g0 = leaf_g0(c);
-            #pragma unroll
-            for (int g = g0; g < 64 / kLeafG; ++g) {
-                const int q = q0 + g - g0;
-                const LeafPos n2 = leaf_snext(leaf_snext(LeafPos{c, g}));
-                if (n2.col < 64) {
-                    #pragma unroll
-                    for (int e = 0; e < kLeafG; ++e) buf[(q + 2) % 3][e] = LT[n2.col * LS + n2.grp * kLeafG + e];
-                }
-                #pragma unroll
-                for (int e = 0; e < kLeafG; ++e) {
-                    const int l = g * kLeafG + e;
-                    if (l == c) y[c] = y[c] * buf[q % 3][e];          // reciprocal diagonal
-                    else if (l > c) y[l] -= y[c] * conj(buf[q % 3][e]);
-                }
-                #pragma unroll
-                for (int e = 0; e < kLeafG; ++e)
-                    if (g * kLeafG + e >= c) leaf_pin1(y[g * kLeafG + e]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-        };
-#define LEAF_SSTEP(x) step(std::integral_constant<int, (x)>{});
-        LEAF_REP64(LEAF_SSTEP)
-#undef LEAF_SSTEP
-    }
+    leaf_solve<T, true, false>(y, LT);
     LEAF_STAMP(4);
     if (live) {
         T* Ar = A + row;
         int64_t off = 0;
         #pragma unroll
         for (int c = 0; c < 64; ++c) {
-            Ar[off] = y[c];
-            if (c + 1 < b) off += lda;
-            else break;
+            if (c < b) Ar[off] = y[c];
+            off += lda;
         }
     }
     LEAF_STAMP(5);

@@ -178,6 +178,13 @@ void rbt_combine(bool by_rows, int64_t m, int64_t n, T* A, int64_t lda, const T*
 // Utop = copy of the nn x nn top block (ld 32); sgn[r+j] receives s_j.
 template <typename T>
 void lu_sign_narrow(int64_t m, int64_t r, int nn, T* A, int64_t lda, const T* Utop, T* sgn, hipStream_t s);
+/// Sign-modified LU of the 64-column leaf at column c0 (width b) of the n x n
+/// matrix A: LU11 (staged in W when r = n - c0 - b > 0, copied into place by
+/// the next call via Wprev -> Aprev), L21 = A21 U11^{-1}, U12 = L11^{-1} A12,
+/// signs into sgn[c0 ..]; the caller applies A22 -= L21 U12.  sizeof(T) <= 8.
+template <typename T>
+void lu_sign_leaf(int64_t n, int64_t c0, int b, T* A, int64_t lda, T* sgn, T* W, const T* Wprev, T* Aprev, int bprev,
+                  hipStream_t s);
 /// On-chip TSQR + Householder reconstruction of a narrow panel block: rows x nn
 /// (nn <= 32) at A -> V below the diagonal, R on/above, the nn x nn T at Tm,
 /// tau[0..nn).  work: qr_tsqr_workspace(rows) scalars.

@@ -20,6 +20,9 @@
 // are FMAs against U11^{-1} in LDS.
 #include "device_common.hh"
 #include "kernels.hh"
+#include "leaf_common.hh"
+
+#include <stdexcept>
 
 // the many-workgroup tree kernels (qr_node / qr_node_q) may opt out of the
 // panel wave priority (A/B builds: SLATE_QR_NODE_PRIO=0)
@@ -448,7 +451,178 @@ __global__ __launch_bounds__(64) void qr_hr_finish_kernel(int nn, const T* LU, i
     }
 }
 
+//------------------------------------------------------------------------------
+// Sign-modified LU leaf: the 64-column block at column c0 of the n x n matrix
+// A in ONE launch of single-wave workgroups (lu_dist.cc lu_sign; replaces the
+// 32-column narrow kernels and the recursion's trsm / gemm levels between
+// them).  Every workgroup factors the b x b diagonal block in registers
+// (lane = row, right-looking, row k of U broadcast from lane k by v_readlane;
+// identity padding past b); then by role:
+//   0            LU11 -> W (or A when no other workgroup reads A11) and the
+//                signs; copies the previous leaf's staged block into place
+//   1 .. nr      a 64-row block of L21 = A21 U11^{-1} (rows of U in LDS)
+//   nr+1 ..      a 64-column block of U12 = L11^{-1} A12 (columns of L in
+//                LDS; the block is transposed through LDS so that global
+//                loads and stores stay coalesced)
+// The trailing A22 -= L21 U12 is one GEMM launch after it.
+template <typename T>
+__global__ __launch_bounds__(64)
+void lu_sign_leaf_kernel(int64_t n, int64_t c0, int b, T* A, int64_t lda, T* sgn, T* W, const T* Wprev, T* Aprev,
+                         int bprev, int nr) {
+    SLATE_PANEL_WAVE_PRIO();
+    constexpr int LS = kLeafLS, XS = 65;
+    __shared__ __attribute__((aligned(16))) T S[64 * LS];
+    __shared__ T X[64 * XS];
+    const int i = threadIdx.x;
+    const int wg = blockIdx.x;
+    const int64_t r = n - c0 - b;          // rows below = columns to the right
+    T* A11 = A + c0 + c0 * lda;
+    T a[64];
+    {
+        const T* Ai = A11 + min(i, b - 1);
+        int64_t off = 0;
+        #pragma unroll
+        for (int l = 0; l < 64; ++l) {
+            const T v = Ai[off];
+            a[l] = (i < b && l < b) ? v : ((i == l) ? one<T>() : zero<T>());
+            if (l + 1 < b) off += lda;
+        }
+    }
+    T s_mine = one<T>();
+    auto fstep = [&](auto jc) __attribute__((always_inline)) {
+        constexpr int j = decltype(jc)::value;
+        const T p = bcast_lane(a[j], j);
+        const T sg = unit_phase(p);
+        const T d = p + sg;                 // |d| >= 1
+        const T rd = rcp_nr(d);
+        const T lij = (i > j) ? a[j] * rd : zero<T>();
+        if (i == j) {
+            a[j] = d;
+            s_mine = sg;
+        } else if (i > j) {
+            a[j] = lij;
+        }
+        // row j of U from lane j, 8 columns per scheduling group (the
+        // readlanes land in SGPRs: hoisting a whole row spilled)
+        #pragma unroll
+        for (int l = j + 1; l < 64; ++l) {
+            a[l] -= lij * bcast_lane(a[l], j);
+            if ((l & 7) == 7) __builtin_amdgcn_sched_barrier(0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+    };
+#define LU_FSTEP(x) fstep(std::integral_constant<int, (x)>{});
+    LEAF_REP64(LU_FSTEP)
+#undef LU_FSTEP
+    if (wg == 0) {
+        const bool direct = (r == 0);
+        T* Fi = direct ? A11 + i : W + i;
+        const int64_t ld = direct ? lda : 64;
+        if (i < b) {
+            sgn[c0 + i] = s_mine;
+            int64_t off = 0;
+            #pragma unroll
+            for (int l = 0; l < 64; ++l) {      // predicated, not `break`: an early
+                if (l < b) Fi[off] = a[l];      // exit left the loop rolled and a[]
+                off += ld;                      // in scratch
+            }
+        }
+        if (Aprev && i < bprev) {
+            T* Ap = Aprev + i;
+            const T* Wp = Wprev + i;
+            int64_t off = 0;
+            #pragma unroll
+            for (int l = 0; l < 64; ++l) {
+                if (l < bprev) Ap[off] = Wp[l * 64];
+                off += lda;
+            }
+        }
+        return;
+    }
+    if (wg <= nr) {
+        // rows of U, reciprocal pivots on the diagonal
+        #pragma unroll
+        for (int l = 0; l < 64; ++l) S[i * LS + l] = (l == i) ? rcp_nr(a[l]) : a[l];
+        __syncthreads();
+        const int64_t row = c0 + b + (int64_t)(wg - 1) * 64 + i;
+        const bool live = row < n;
+        T* Ar = A + (live ? row : c0 + b) + c0 * lda;
+        T y[64];
+        {
+            int64_t off = 0;
+            #pragma unroll
+            for (int c = 0; c < 64; ++c) {
+                const T v = Ar[off];
+                y[c] = (live && c < b) ? v : zero<T>();
+                if (c + 1 < b) off += lda;
+            }
+        }
+        leaf_solve<T, false, false>(y, S);
+        if (live) {
+            int64_t off = 0;
+            #pragma unroll
+            for (int c = 0; c < 64; ++c) {
+                if (c < b) Ar[off] = y[c];
+                off += lda;
+            }
+        }
+        return;
+    }
+    // columns of L (unit diagonal): S(c, l) = L(l, c)
+    #pragma unroll
+    for (int l = 0; l < 64; ++l) S[l * LS + i] = a[l];
+    // the 64-column block of A12, transposed through X (lane = row on the
+    // global side, lane = column in the solve)
+    const int64_t col0 = c0 + b + (int64_t)(wg - nr - 1) * 64;
+    const int ncol = (int)min<int64_t>(64, n - col0);
+    T* A12 = A + c0 + col0 * lda;
+    {
+        const T* Ai = A12 + min(i, b - 1);
+        int64_t off = 0;
+        #pragma unroll
+        for (int e = 0; e < 64; ++e) {
+            const T v = Ai[off];
+            X[e * XS + i] = (i < b && e < ncol) ? v : zero<T>();
+            if (e + 1 < ncol) off += lda;
+        }
+    }
+    __syncthreads();
+    T x[64];
+    #pragma unroll
+    for (int c = 0; c < 64; ++c) x[c] = X[i * XS + c];
+    leaf_solve<T, false, true>(x, S);
+    #pragma unroll
+    for (int c = 0; c < 64; ++c) X[i * XS + c] = x[c];
+    __syncthreads();
+    if (i < b) {
+        T* Ai = A12 + i;
+        int64_t off = 0;
+        #pragma unroll
+        for (int e = 0; e < 64; ++e) {
+            if (e < ncol) Ai[off] = X[e * XS + i];
+            off += lda;
+        }
+    }
+}
+
 }  // namespace
+
+template <typename T>
+void lu_sign_leaf(int64_t n, int64_t c0, int b, T* A, int64_t lda, T* sgn, T* W, const T* Wprev, T* Aprev, int bprev,
+                  hipStream_t s) {
+    if (b <= 0) return;
+    const int64_t r = n - c0 - b;
+    if (b > 64 || r < 0 || bprev > 64) throw std::invalid_argument("lu_sign_leaf: b, bprev <= 64, c0 + b <= n");
+    if (r > 0 && !W) throw std::invalid_argument("lu_sign_leaf: r > 0 needs the 64 x 64 staging block W");
+    if (Aprev && !Wprev) throw std::invalid_argument("lu_sign_leaf: Aprev needs Wprev");
+    if constexpr (sizeof(T) > 8) {
+        throw std::invalid_argument("lu_sign_leaf: complex<double> is not supported");
+    } else {
+        const int nr = (int)((r + 63) / 64);
+        hipLaunchKernelGGL(lu_sign_leaf_kernel<T>, dim3(1 + 2 * nr), dim3(64), 0, s, n, c0, b, A, lda, sgn, W, Wprev,
+                           Aprev, bprev, nr);
+    }
+}
 
 template <typename T>
 void lu_sign_narrow(int64_t m, int64_t r, int nn, T* A, int64_t lda, const T* Utop, T* sgn, hipStream_t s) {
@@ -520,6 +694,7 @@ void qr_tsqr_narrow(int64_t rows, int nn, T* A, int64_t lda, T* Tm, int64_t ldt,
 
 #define SLATE_INST_TSQR(T) \
     template void lu_sign_narrow<T>(int64_t, int64_t, int, T*, int64_t, const T*, T*, hipStream_t); \
+    template void lu_sign_leaf<T>(int64_t, int64_t, int, T*, int64_t, T*, T*, const T*, T*, int, hipStream_t); \
     template void qr_tsqr_narrow<T>(int64_t, int, T*, int64_t, T*, int64_t, T*, T*, hipStream_t);
 
 SLATE_INST_TSQR(float)

@@ -415,12 +415,18 @@ void bind_drivers(py::module_& m, std::string const& s) {
         return h;
     });
     DEF("lb_lu_sign", [=](int64_t n, uintptr_t A, int64_t lda) {
-        // sign-modified LU of the Householder reconstruction (lu_dist.cc)
-        py::gil_scoped_release r;
-        auto c = dctx();
-        device::Buffer<T> sgn(n + 1);
-        internal::ludist::lu_sign<T>(c, n, (T*)A, lda, sgn.data());
-        dsync(c);
+        // sign-modified LU of the Householder reconstruction (lu_dist.cc):
+        // L U = A + diag(s); returns s
+        std::vector<T> h(std::max<int64_t>(n, 0));
+        {
+            py::gil_scoped_release r;
+            auto c = dctx();
+            device::Buffer<T> sgn(n + 1);
+            internal::ludist::lu_sign<T>(c, n, (T*)A, lda, sgn.data());
+            if (n > 0) device::memcpy_async(h.data(), sgn.data(), sizeof(T) * size_t(n), c.stream);
+            dsync(c);
+        }
+        return h;
     });
     DEF("lb_getrf_panel", [=](int64_t mm, int64_t n, uintptr_t A, int64_t lda, bool tournament) {
         std::vector<int64_t> ipiv(std::min(mm, n));

@@ -3,6 +3,7 @@
 #include "lu_dist.hh"
 
 #include <cstring>
+#include <cstdlib>
 #include <functional>
 #include <vector>
 
@@ -111,6 +112,30 @@ void lu_sign(lb::Ctx const& c, int64_t n, T* A, int64_t lda, T* sgn) {
                 T u = A[k + j * lda];
                 for (int64_t i = k + 1; i < n; ++i) A[i + j * lda] -= A[i + k * lda] * u;
             }
+        }
+        return;
+    }
+    // 64-column leaves (tsqr.hip lu_sign_leaf: diagonal block, L21 and U12
+    // in one launch) and one GEMM per leaf; SLATE_LU_SIGN_LEAF=0 keeps the
+    // recursion over 32-column narrow blocks
+    static const bool leaf = [] {
+        const char* e = std::getenv("SLATE_LU_SIGN_LEAF");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    if (sizeof(T) <= 8 && leaf) {
+        lb::Scratch sc(c);
+        T* Wk[2] = {sc.alloc<T>(64 * 64), sc.alloc<T>(64 * 64)};
+        T* Aprev = nullptr;
+        int bprev = 0;
+        for (int64_t c0 = 0, k = 0; c0 < n; c0 += 64, ++k) {
+            const int64_t b = std::min<int64_t>(64, n - c0), r = n - c0 - b;
+            kd::lu_sign_leaf<kd::dev_t<T>>(n, c0, int(b), dptr(A), lda, dptr(sgn), dptr(Wk[k & 1]),
+                                           Aprev ? dptr(Wk[(k + 1) & 1]) : nullptr, dptr(Aprev), bprev, c.stream);
+            Aprev = A + c0 + c0 * lda;
+            bprev = int(b);
+            if (r == 0) break;
+            lb::gemm(c, Op::NoTrans, Op::NoTrans, r, r, b, T(-1), A + (c0 + b) + c0 * lda, lda,
+                     A + c0 + (c0 + b) * lda, lda, T(1), A + (c0 + b) + (c0 + b) * lda, lda);
         }
         return;
     }

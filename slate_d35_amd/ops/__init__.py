@@ -106,7 +106,8 @@ def geqrf_panel(A):
 def lu_sign(A):
     """Sign-modified LU without pivoting of a column-major n x n block in
     place (the Householder reconstruction step of the CholeskyQR / TSQR QR
-    panels, lu_dist.cc)."""
+    panels, lu_dist.cc): L U = A + diag(s), s_k = the unit phase of the k-th
+    pivot; returns s."""
     fn = getattr(_slate, f"lb_lu_sign_{_suffix(A)}")
     pa, m, n, lda = _cm(A)
-    fn(n, pa, lda)
+    return fn(n, pa, lda)

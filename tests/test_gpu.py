@@ -268,6 +268,26 @@ def test_potrf_leaf_all_types(n, dt):
             assert s.ops.potrf("L", tB) == bad + 1, bad
 
 
+@pytest.mark.parametrize("dt", [np.float64, np.float32, np.complex128])
+@pytest.mark.parametrize("n", [1, 31, 64, 100, 512, 700])
+def test_lu_sign_device(n, dt):
+    """Sign-modified LU without pivoting (Householder reconstruction step):
+    L U = A + diag(s) with |s_k| = 1 and |U_kk| >= 1 for A = -Q11 of an
+    orthonormal Q."""
+    torch = _torch()
+    q, _ = np.linalg.qr(rnd(2 * n, n, dt, 21))
+    a = -q[:n, :n]
+    tA = torch.from_numpy(np.ascontiguousarray(a.T)).cuda()
+    sg = np.array(s.ops.lu_sign(tA))
+    f = tA.cpu().numpy().T.astype(np.complex128)
+    L = np.tril(f, -1) + np.eye(n)
+    U = np.triu(f)
+    tol = 1e-5 if dt == np.float32 else 1e-13
+    assert np.allclose(np.abs(sg), 1.0)
+    assert np.abs(np.diag(U)).min() >= 1.0 - tol
+    assert np.abs(L @ U - (a + np.diag(sg))).max() < tol * max(1, n) ** 0.5
+
+
 @pytest.mark.parametrize("m,n", [(1000, 64), (4096, 256), (777, 100), (512, 512)])
 def test_getrf_panel_kernel(m, n):
     torch = _torch()
