@@ -60,16 +60,18 @@ __device__ constexpr int leaf_fq0(int k) {
     for (int t = 0; t < k; ++t) q += 64 / kLeafG - leaf_g0(t + 2);
     return q;
 }
-// groups before the solve stream's column c (rows >= c)
+// groups before the solve stream's column c (rows >= c) of an N-row solve
+template <int N = 64>
 __device__ constexpr int leaf_sq0(int c) {
     int q = 0;
-    for (int t = 0; t < c; ++t) q += 64 / kLeafG - leaf_g0(t);
+    for (int t = 0; t < c; ++t) q += N / kLeafG - leaf_g0(t);
     return q;
 }
 // solve stream: next group after (col, grp)
 struct LeafPos { int col, grp; };
+template <int N = 64>
 __device__ constexpr LeafPos leaf_snext(LeafPos p) {
-    return p.grp + 1 < 64 / kLeafG ? LeafPos{p.col, p.grp + 1} : LeafPos{p.col + 1, leaf_g0(p.col + 1)};
+    return p.grp + 1 < N / kLeafG ? LeafPos{p.col, p.grp + 1} : LeafPos{p.col + 1, leaf_g0(p.col + 1)};
 }
 // The 64 steps are expanded by the preprocessor, each a call of a generic
 // lambda with its step number as a type: a `#pragma unroll` loop of this size
@@ -77,18 +79,20 @@ __device__ constexpr LeafPos leaf_snext(LeafPos p) {
 // register arrays are indexed dynamically (scratch).
 #define LEAF_REP4(M, x) M((x)) M((x) + 1) M((x) + 2) M((x) + 3)
 #define LEAF_REP16(M, x) LEAF_REP4(M, (x)) LEAF_REP4(M, (x) + 4) LEAF_REP4(M, (x) + 8) LEAF_REP4(M, (x) + 12)
+#define LEAF_REP32(M) LEAF_REP16(M, 0) LEAF_REP16(M, 16)
 #define LEAF_REP64(M) LEAF_REP16(M, 0) LEAF_REP16(M, 16) LEAF_REP16(M, 32) LEAF_REP16(M, 48)
 
 
-// Row-streamed substitution of one 64-element row per lane against the
-// 64 x 64 matrix S in LDS (row stride kLeafLS): for c = 0..63,
+// Row-streamed substitution of one N-element row per lane (N = 32 or 64)
+// against the N x N matrix S in LDS (row stride kLeafLS): for c = 0..N-1,
 //   y[c] *= S(c, c)                          (skipped when UNIT)
 //   y[l] -= y[c] * op(S(c, l))  for l > c    (op = conj when CONJ)
 // i.e. y := y op(U)^{-1} for the upper triangle U whose rows are S's rows
 // (S's diagonal holds the reciprocal pivots).  The updates of a step are
 // independent FMAs; S streams in groups with two groups in flight.
-template <typename T, bool CONJ, bool UNIT>
-__device__ __forceinline__ void leaf_solve(T (&y)[64], const T* S) {
+template <typename T, bool CONJ, bool UNIT, int N = 64>
+__device__ __forceinline__ void leaf_solve(T (&y)[N], const T* S) {
+    static_assert(N == 32 || N == 64, "leaf_solve: N = 32 or 64");
     constexpr int LS = kLeafLS;
     T buf[3][kLeafG];
     #pragma unroll
@@ -98,12 +102,12 @@ __device__ __forceinline__ void leaf_solve(T (&y)[64], const T* S) {
     }
     auto step = [&](auto cc) __attribute__((always_inline)) {
         constexpr int c = decltype(cc)::value;
-        constexpr int q0 = leaf_sq0(c), g0 = leaf_g0(c);
+        constexpr int q0 = leaf_sq0<N>(c), g0 = leaf_g0(c);
         #pragma unroll
-        for (int g = g0; g < 64 / kLeafG; ++g) {
+        for (int g = g0; g < N / kLeafG; ++g) {
             const int q = q0 + g - g0;
-            const LeafPos n2 = leaf_snext(leaf_snext(LeafPos{c, g}));
-            if (n2.col < 64) {
+            const LeafPos n2 = leaf_snext<N>(leaf_snext<N>(LeafPos{c, g}));
+            if (n2.col < N) {
                 #pragma unroll
                 for (int e = 0; e < kLeafG; ++e) buf[(q + 2) % 3][e] = S[n2.col * LS + n2.grp * kLeafG + e];
             }
@@ -124,7 +128,11 @@ __device__ __forceinline__ void leaf_solve(T (&y)[64], const T* S) {
         }
     };
 #define LEAF_SSTEP(x) step(std::integral_constant<int, (x)>{});
-    LEAF_REP64(LEAF_SSTEP)
+    if constexpr (N == 64) {
+        LEAF_REP64(LEAF_SSTEP)
+    } else {
+        LEAF_REP32(LEAF_SSTEP)
+    }
 #undef LEAF_SSTEP
 }
 

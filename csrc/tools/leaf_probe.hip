@@ -62,5 +62,26 @@ int main(int argc, char** argv) {
         }
         printf("\n");
     }
+    // small triangular solve (LU panel U12 solves): m = 64 unit lower, 448 columns
+    {
+        const int64_t nc = 448;
+        float bt = 1e30f;
+        for (int k = 0; k < reps; ++k) {
+            (void)hipMemcpy(A, h.data(), h.size() * 8, hipMemcpyHostToDevice);
+            (void)hipStreamSynchronize(s);
+            (void)hipEventRecord(e0, s);
+            trsm_small<double>('L', 'U', 64, nc, A, lda, A + 64 * lda, lda, s);
+            (void)hipEventRecord(e1, s);
+            (void)hipEventSynchronize(e1);
+            float ms;
+            (void)hipEventElapsedTime(&ms, e0, e1);
+            bt = std::min(bt, ms);
+        }
+        (void)hipMemcpyFromSymbol(st, HIP_SYMBOL(g_leaf_probe), sizeof(st));
+        const char* tn[] = {"load triangle", "load B", "y from LDS", "solve", "store"};
+        printf("trsm_small m=64 n=%ld: best %.1f us\n  wg 0:", (long)nc, bt * 1e3);
+        for (int k = 0; k < 5; ++k) printf("  %s %lld", tn[k], st[k + 1] - st[k]);
+        printf("\n");
+    }
     return 0;
 }
