@@ -179,7 +179,8 @@ __global__ void transpose_kernel(bool conjugate, int64_t m, int64_t n, const T* 
 //------------------------------------------------------------------------------
 // Small triangular solve on one wave: X := A^{-1} B for the m x m (m <= MM,
 // MM = 32 or 64) lower or upper triangle A and ncol <= 64 right-hand-side
-// columns (B == nullptr: the identity, i.e. the inverse), result into Out.
+// columns (B == nullptr: the identity, i.e. the inverse; then X may be null
+// and S, (MM + 1) x 64 at least, carries the result), result into Out.
 // One lane per column; the triangle in LDS as the row stream of leaf_solve
 // (column c of the triangle as row c, reciprocal pivots on the diagonal; an
 // upper triangle is solved as the lower one of the index-reversed system);
@@ -197,51 +198,67 @@ __device__ __forceinline__ void tri_solve_cols(bool lower, bool unit, int m, con
     const int lp = lower ? lane : MM - 1 - lane;     // lane = row l of the triangle
     const int lr = min(lane, m - 1);
     LEAF_STAMP(0);
+    // (loads into registers first, LDS stores after: a load feeding the
+    // LDS store of the same iteration waited alone, ~750 cycles per column)
     {
         const T* Al = A + lr;
         int64_t off = 0;
         const T dg = A[lr + (int64_t)lr * lda];
+        T t[MM];
+        #pragma unroll
+        for (int c = 0; c < MM; ++c) {
+            t[c] = Al[off];
+            if (c + 1 < m) off += lda;
+        }
         const T rdg = (unit || lane >= m) ? one<T>() : one<T>() / dg;
         #pragma unroll
         for (int c = 0; c < MM; ++c) {
-            const T v = Al[off];
-            if (c + 1 < m) off += lda;
-            const T w = (lane == c) ? rdg : ((lane < m && c < m) ? v : zero<T>());
+            const T w = (lane == c) ? rdg : ((lane < m && c < m) ? t[c] : zero<T>());
             if (lane < MM) S[(lower ? c : MM - 1 - c) * LS + lp] = w;
         }
     }
     LEAF_STAMP(1);
+    T y[MM];
     if (B) {
         const T* Bl = B + lr;
         int64_t off = 0;
+        T t[64];
         #pragma unroll
         for (int e = 0; e < 64; ++e) {
-            const T v = Bl[off];
+            t[e] = Bl[off];
             if (e + 1 < ncol) off += ldb;
-            if (lane < MM) X[e * XS + lp] = (lane < m && e < ncol) ? v : zero<T>();
         }
-    } else {
         #pragma unroll
         for (int e = 0; e < 64; ++e)
-            if (lane < MM) X[e * XS + lp] = (lane == e && lane < m) ? one<T>() : zero<T>();
+            if (lane < MM) X[e * XS + lp] = (lane < m && e < ncol) ? t[e] : zero<T>();
+        __syncthreads();
+        LEAF_STAMP(2);
+        #pragma unroll
+        for (int c = 0; c < MM; ++c) y[c] = X[lane * XS + c];
+    } else {
+        // the identity: lane j's column has its one at solve index lp(j)
+        __syncthreads();
+        LEAF_STAMP(2);
+        #pragma unroll
+        for (int c = 0; c < MM; ++c) y[c] = (c == lp && lane < m) ? one<T>() : zero<T>();
     }
-    __syncthreads();
-    LEAF_STAMP(2);
-    T y[MM];
-    #pragma unroll
-    for (int c = 0; c < MM; ++c) y[c] = X[lane * XS + c];
     LEAF_STAMP(3);
     leaf_solve<T, false, false, MM>(y, S);
     LEAF_STAMP(4);
+    // the result goes back through LDS (X, or S once the solve has read it
+    // when there is no X: the inverse needs no right-hand side)
+    T* R = X ? X : S;
+    constexpr int RS = XS;
+    __syncthreads();
     #pragma unroll
-    for (int c = 0; c < MM; ++c) X[lane * XS + c] = y[c];
+    for (int c = 0; c < MM; ++c) R[lane * RS + c] = y[c];
     __syncthreads();
     if (lane < m) {
         T* Ol = Out + lane;
         int64_t off = 0;
         #pragma unroll
         for (int e = 0; e < 64; ++e) {
-            if (e < ncol) Ol[off] = X[e * XS + lp];
+            if (e < ncol) Ol[off] = R[e * RS + lp];
             off += ldo;
         }
     }
@@ -259,7 +276,6 @@ void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
                        const T* A, int64_t lda, T* W, int64_t ldw, int64_t wrap) {
     SLATE_PANEL_WAVE_PRIO();
     __shared__ __attribute__((aligned(16))) T S[64 * kLeafLS];
-    __shared__ T X[64 * 65];
     const int b = blockIdx.x;
     const int64_t off = (int64_t)b * nbs;
     const int nb = (int)min<int64_t>(nbs, n - off);
@@ -269,7 +285,7 @@ void trtri_diag_kernel(char uplo, char diag, int64_t n, int nbs,
     T* Wb = wrap > 0 ? W + (off / wrap) * wrap * wrap + (off % wrap) * (1 + ldw) : W + off + off * ldw;
     // the inverse = the solve against the identity (exact zeros outside the
     // triangle: the full square block is written)
-    tri_solve_cols<T, 64>(uplo == 'L', diag == 'U', nb, Ab, lda, nullptr, 0, Wb, ldw, nb, S, X);
+    tri_solve_cols<T, 64>(uplo == 'L', diag == 'U', nb, Ab, lda, nullptr, 0, Wb, ldw, nb, S, nullptr);
 }
 
 //------------------------------------------------------------------------------
@@ -489,12 +505,17 @@ void potrf_leaf_kernel(int b, int r, T* A, int64_t lda, int* info, int info_offs
         }
     }
     if (blockIdx.x == 0 && Aprev) {
+        // all loads, then all stores (a load feeding the same iteration's
+        // store waited alone: ~24 us on the leaf's workgroup 0)
         T* Ap = Aprev + i;
         const T* Wp = Wprev + i;
+        T t[64];
+        #pragma unroll
+        for (int l = 0; l < 64; ++l) t[l] = Wp[l * 64];
         int64_t off = 0;
         #pragma unroll
         for (int l = 0; l < 64; ++l) {
-            if (l < bprev && l <= i && i < bprev) Ap[off] = Wp[l * 64];
+            if (l < bprev && l <= i && i < bprev) Ap[off] = t[l];
             off += lda;
         }
     }
@@ -542,6 +563,108 @@ void trsm_small_kernel(char uplo, char diag, int m, int64_t n, const T* A, int64
     const int64_t col0 = (int64_t)blockIdx.x * 64;
     tri_solve_cols<T, MM>(uplo == 'L', diag == 'U', m, A, lda, B + col0 * ldb, ldb, B + col0 * ldb, ldb,
                           (int)min<int64_t>(64, n - col0), S, X);
+}
+
+// Round-4 forms (dot-product substitution, triangle in LDS): the default
+// (see small_solve_v1: slower alone, faster beside the concurrent trailing GEMM).
+template <typename T, int MM>
+__global__ __launch_bounds__(64)
+void trsm_small_v1_kernel(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb) {
+    SLATE_PANEL_WAVE_PRIO();
+    // MM = 32 or 64 (m <= MM): the padded triangle, and the workgroup's 64
+    // right-hand-side columns staged through LDS so that global loads and
+    // stores run along the columns (a lane-per-column access would touch a
+    // different cache line in every lane)
+    __shared__ T L[MM][MM + 1];
+    __shared__ T X[64][MM + 1];
+    __shared__ T rd[MM];
+    const int lane = threadIdx.x;
+    const int64_t col0 = (int64_t)blockIdx.x * 64;
+    const int ncol = (int)min<int64_t>(64, n - col0);
+    for (int j = 0; j < MM; ++j)
+        if (lane < MM)
+            L[lane][j] = (lane < m && j < m) ? A[lane + (int64_t)j * lda] : (lane == j ? one<T>() : zero<T>());
+    for (int c = 0; c < ncol; ++c)
+        if (lane < m) X[c][lane] = B[lane + (col0 + c) * ldb];
+    __syncthreads();
+    if (lane < MM) rd[lane] = (diag == 'U') ? one<T>() : one<T>() / L[lane][lane];
+    __syncthreads();
+    const bool live = lane < ncol;
+    T x[MM];
+    #pragma unroll
+    for (int i = 0; i < MM; ++i) x[i] = (live && i < m) ? X[lane][i] : zero<T>();
+    if (uplo == 'L') {
+        #pragma unroll
+        for (int i = 0; i < MM; ++i) {
+            T s = x[i];
+            #pragma unroll
+            for (int l = 0; l < i; ++l) s -= L[i][l] * x[l];
+            x[i] = s * rd[i];
+        }
+    } else {
+        #pragma unroll
+        for (int i = MM - 1; i >= 0; --i) {
+            T s = x[i];
+            #pragma unroll
+            for (int l = i + 1; l < MM; ++l) s -= L[i][l] * x[l];
+            x[i] = s * rd[i];
+        }
+    }
+    if (live) {
+        #pragma unroll
+        for (int i = 0; i < MM; ++i) X[lane][i] = x[i];
+    }
+    __syncthreads();
+    for (int c = 0; c < ncol; ++c)
+        if (lane < m) B[lane + (col0 + c) * ldb] = X[c][lane];
+}
+
+template <typename T>
+__global__ __launch_bounds__(64)
+void trtri_diag_v1_kernel(char uplo, char diag, int64_t n, int nbs,
+                       const T* A, int64_t lda, T* W, int64_t ldw, int64_t wrap) {
+    SLATE_PANEL_WAVE_PRIO();
+    __shared__ T L[64][64];
+    __shared__ T rd[64];
+    const int b = blockIdx.x;
+    const int64_t off = (int64_t)b * nbs;
+    const int nb = (int)min<int64_t>(nbs, n - off);
+    const int lane = threadIdx.x;
+    const T* Ab = A + off + off * lda;
+    // wrap > 0: W is a stack of wrap x wrap blocks (block t at W + t wrap^2,
+    // ld = wrap), each holding the inverse of A's t-th diagonal wrap-block
+    T* Wb = wrap > 0 ? W + (off / wrap) * wrap * wrap + (off % wrap) * (1 + ldw) : W + off + off * ldw;
+    const bool unit = (diag == 'U');
+    const bool lower = (uplo == 'L');
+    for (int j = 0; j < 64; ++j)
+        L[lane][j] = (lane < nb && j < nb) ? Ab[lane + j * lda] : (lane == j ? one<T>() : zero<T>());
+    __syncthreads();
+    rd[lane] = unit ? one<T>() : one<T>() / L[lane][lane];
+    __syncthreads();
+    const int j = lane;
+    T x[64];
+    if (lower) {
+        #pragma unroll
+        for (int i = 0; i < 64; ++i) {
+            T s = zero<T>();
+            #pragma unroll
+            for (int l = 0; l < i; ++l) s += L[i][l] * x[l];
+            x[i] = (i < j) ? zero<T>() : ((i == j) ? rd[i] : -(s * rd[i]));
+        }
+    } else {
+        #pragma unroll
+        for (int i = 63; i >= 0; --i) {
+            T s = zero<T>();
+            #pragma unroll
+            for (int l = i + 1; l < 64; ++l) s += L[i][l] * x[l];
+            x[i] = (i > j) ? zero<T>() : ((i == j) ? rd[i] : -(s * rd[i]));
+        }
+    }
+    if (lane < nb) {
+        #pragma unroll
+        for (int i = 0; i < 64; ++i)
+            if (i < nb) Wb[i + (int64_t)j * ldw] = x[i];
+    }
 }
 
 //------------------------------------------------------------------------------
@@ -676,18 +799,40 @@ void gescale_row_col(int64_t m, int64_t n, const real_t<T>* R, const real_t<T>* 
     hipLaunchKernelGGL(scale_row_col_kernel<T>, grid2d(m, n), dim3(TX, TY), 0, s, m, n, R, C, A, lda);
 }
 
+// Small triangular solves: the dot-product kernels (default) or the
+// solve-stream ones (SLATE_SMALL_SOLVE=2).  The stream kernels are 2x faster
+// alone (trsm_small 64 x 448: 41 -> 22 us, trtri_diag 33 -> 20 us; the
+// 32768 x 512 tournament panel 2.88 -> 2.66 ms) but the 1-GPU dgetrf, whose
+// panel runs beside the trailing GEMM, measured 55.9 against 59.0-59.1
+// TFLOP/s with them (same box, interleaved runs, profiles/r5_small_solve_ab.txt).
+inline bool small_solve_v1() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_SMALL_SOLVE");
+        return !(e && std::atoi(e) == 2);
+    }();
+    return v;
+}
+
 template <typename T>
 void trtri_diag(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t ldw, hipStream_t s) {
     if (n <= 0) return;
     int nblk = (int)((n + nbs - 1) / nbs);
-    hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, ldw, int64_t(0));
+    if (small_solve_v1())
+        hipLaunchKernelGGL(trtri_diag_v1_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, ldw,
+                           int64_t(0));
+    else
+        hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, ldw,
+                           int64_t(0));
 }
 
 template <typename T>
 void trtri_diag_stack(char uplo, char diag, int64_t n, int nbs, const T* A, int64_t lda, T* W, int64_t bs, hipStream_t s) {
     if (n <= 0) return;
     int nblk = (int)((n + nbs - 1) / nbs);
-    hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, bs, bs);
+    if (small_solve_v1())
+        hipLaunchKernelGGL(trtri_diag_v1_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, bs, bs);
+    else
+        hipLaunchKernelGGL(trtri_diag_kernel<T>, dim3(nblk), dim3(64), 0, s, uplo, diag, n, nbs, A, lda, W, bs, bs);
 }
 
 template <typename T>
@@ -723,12 +868,18 @@ void potrf_leaf(int b, int64_t r, T* A, int64_t lda, int* info, int info_offset,
 template <typename T>
 void trsm_small(char uplo, char diag, int m, int64_t n, const T* A, int64_t lda, T* B, int64_t ldb, hipStream_t s) {
     if (m <= 0 || n <= 0) return;
-    if (m <= 32)
-        hipLaunchKernelGGL((trsm_small_kernel<T, 32>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, uplo, diag, m,
-                           n, A, lda, B, ldb);
-    else
-        hipLaunchKernelGGL((trsm_small_kernel<T, 64>), dim3((unsigned)((n + 63) / 64)), dim3(64), 0, s, uplo, diag, m,
-                           n, A, lda, B, ldb);
+    const dim3 grid((unsigned)((n + 63) / 64));
+    if (small_solve_v1()) {
+        if (m <= 32)
+            hipLaunchKernelGGL((trsm_small_v1_kernel<T, 32>), grid, dim3(64), 0, s, uplo, diag, m, n, A, lda, B, ldb);
+        else
+            hipLaunchKernelGGL((trsm_small_v1_kernel<T, 64>), grid, dim3(64), 0, s, uplo, diag, m, n, A, lda, B, ldb);
+    } else {
+        if (m <= 32)
+            hipLaunchKernelGGL((trsm_small_kernel<T, 32>), grid, dim3(64), 0, s, uplo, diag, m, n, A, lda, B, ldb);
+        else
+            hipLaunchKernelGGL((trsm_small_kernel<T, 64>), grid, dim3(64), 0, s, uplo, diag, m, n, A, lda, B, ldb);
+    }
 }
 
 template <typename T>

@@ -808,7 +808,16 @@ __global__ __launch_bounds__(256) void tslu2_finish_kernel(int64_t m, int64_t r,
     }
     T* A = Ap + c0 * lda;
     const int64_t base = r + nn + blockIdx.x * (int64_t)256;
-    for (int t = tid; t < TW * TW; t += 256) Uinv[t] = uinv[t];
+    {
+        // all loads, then the LDS stores (a load feeding the same iteration's
+        // store waits alone)
+        static_assert(TW * TW % 256 == 0, "finish: Uinv staging");
+        T u[TW * TW / 256];
+        #pragma unroll
+        for (int k = 0; k < TW * TW / 256; ++k) u[k] = uinv[tid + 256 * k];
+        #pragma unroll
+        for (int k = 0; k < TW * TW / 256; ++k) Uinv[tid + 256 * k] = u[k];
+    }
     smap[tid] = -1;
     __syncthreads();
     if (tid < np) {

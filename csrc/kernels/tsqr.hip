@@ -528,12 +528,16 @@ void lu_sign_leaf_kernel(int64_t n, int64_t c0, int b, T* A, int64_t lda, T* sgn
             }
         }
         if (Aprev && i < bprev) {
+            // all loads, then all stores (see aux.hip tri_solve_cols)
             T* Ap = Aprev + i;
             const T* Wp = Wprev + i;
+            T t[64];
+            #pragma unroll
+            for (int l = 0; l < 64; ++l) t[l] = Wp[l * 64];
             int64_t off = 0;
             #pragma unroll
             for (int l = 0; l < 64; ++l) {
-                if (l < bprev) Ap[off] = Wp[l * 64];
+                if (l < bprev) Ap[off] = t[l];
                 off += lda;
             }
         }
@@ -579,12 +583,14 @@ void lu_sign_leaf_kernel(int64_t n, int64_t c0, int b, T* A, int64_t lda, T* sgn
     {
         const T* Ai = A12 + min(i, b - 1);
         int64_t off = 0;
+        T t[64];
         #pragma unroll
         for (int e = 0; e < 64; ++e) {
-            const T v = Ai[off];
-            X[e * XS + i] = (i < b && e < ncol) ? v : zero<T>();
+            t[e] = Ai[off];
             if (e + 1 < ncol) off += lda;
         }
+        #pragma unroll
+        for (int e = 0; e < 64; ++e) X[e * XS + i] = (i < b && e < ncol) ? t[e] : zero<T>();
     }
     __syncthreads();
     T x[64];
