@@ -268,7 +268,7 @@ def test_potrf_leaf_all_types(n, dt):
             assert s.ops.potrf("L", tB) == bad + 1, bad
 
 
-@pytest.mark.parametrize("dt", [np.float64, np.float32, np.complex128])
+@pytest.mark.parametrize("dt", [np.float64, np.float32, np.complex64, np.complex128])
 @pytest.mark.parametrize("n", [1, 31, 64, 100, 512, 700])
 def test_lu_sign_device(n, dt):
     """Sign-modified LU without pivoting (Householder reconstruction step):
@@ -282,7 +282,7 @@ def test_lu_sign_device(n, dt):
     f = tA.cpu().numpy().T.astype(np.complex128)
     L = np.tril(f, -1) + np.eye(n)
     U = np.triu(f)
-    tol = 1e-5 if dt == np.float32 else 1e-13
+    tol = 1e-5 if dt in (np.float32, np.complex64) else 1e-13
     assert np.allclose(np.abs(sg), 1.0)
     assert np.abs(np.diag(U)).min() >= 1.0 - tol
     assert np.abs(L @ U - (a + np.diag(sg))).max() < tol * max(1, n) ** 0.5
