@@ -255,7 +255,10 @@ def main(a):
     # (LDS-staged row permutation): 3370 -> 3283-3299 ms at n = 65536
     # (profiles/r3_nb_sweep.txt); dgeqrf 512 vs 1024 and dpotrf 1024 vs 2048
     # measured equal on one box.
-    default_nb = {"dgetrf": 2048, "dpotrf": 1024, "dgesv_mixed": 1024} if world == 1 else {}
+    # Round 5 (single-wave leaf kernels make wide diagonal blocks cheap):
+    # dpotrf 1536 vs 1024 62.7-63.0 -> 63.3-63.4, dgeqrf 1024 vs 512 59.2 ->
+    # 59.8-59.9 TFLOP/s, interleaved on one box (profiles/r5_nb_ab.txt).
+    default_nb = {"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024} if world == 1 else {}
     if a.nb:
         default_nb = {}
     a.nb = a.nb or 512
