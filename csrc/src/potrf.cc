@@ -127,13 +127,15 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
 
     // 1x1 device grid: once the remaining matrix is at most `tail` wide, factor
     // it with ONE recursive device potrf (local_blas.cc: 64-column leaves,
-    // four launches each) instead of nb-wide steps, whose per-step panel,
+    // two launches each) instead of nb-wide steps, whose per-step panel,
     // trsm and lookahead hops dominate when the trailing update has shrunk to
     // a few hundred microseconds.  SLATE_POTRF_TAIL = width (0: off); config 2
-    // (n = 32768, nb = 512): 237.4 ms at 0, 234.2 at 4096, 233.0 at 8192.
+    // (n = 32768, nb = 512): round 4 237.4 ms at 0, 234.2 at 4096, 233.0 at
+    // 8192; round 5 (leaf kernels) 4096 214.0-214.7 ms against 215.2-216.2 at
+    // 8192 and 248-250 at 16384 (profiles/r5_potrf_tail_ab.txt).
     static const int64_t tail_env = [] {
         const char* e = std::getenv("SLATE_POTRF_TAIL");
-        return e ? std::atoll(e) : int64_t(8192);
+        return e ? std::atoll(e) : int64_t(4096);
     }();
     const bool tail_ok = p * q == 1 && target == Target::Devices && tail_env > 0;
     for (int64_t k = 0; k < nt; ++k) {
