@@ -272,7 +272,10 @@ def main(a):
     # than a step's trailing update for most steps at 2 x 4,
     # profiles/r4_critpath_2x4_*.txt) does not stall the trailing queue of
     # the next step as well.
-    la_per = {"dpotrf": 2, "dgeqrf": 2} if world == 1 else {"dpotrf": 2, "dgeqrf": 2, "dgetrf": 2, "dgesv_mixed": 2}
+    # Round 5: dgetrf at 2 on one GPU too (58.65-58.85 -> 58.89-59.00 TFLOP/s,
+    # interleaved, profiles/r5_lookahead_ab.txt).
+    la_per = ({"dpotrf": 2, "dgeqrf": 2, "dgetrf": 2} if world == 1
+              else {"dpotrf": 2, "dgeqrf": 2, "dgetrf": 2, "dgesv_mixed": 2})
 
     def la_of(rname):
         return a.lookahead or la_per.get(rname, 1)
