@@ -86,5 +86,8 @@ void set_thread_default_grid(GridPtr g);   // nullptr: back to the process defau
 std::vector<GridPtr> make_thread_grids(int p, int q, GridOrder order, std::vector<int> const& devices);
 /// Abort every in-process communicator of g (see thread_comm_abort).
 void thread_grid_abort(Grid const& g);
+/// Clear the aborted state of g's in-process communicators (all of the
+/// group's rank threads have stopped), so a persistent group runs again.
+void thread_grid_reset(Grid const& g);
 
 }  // namespace slate

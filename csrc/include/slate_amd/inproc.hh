@@ -18,6 +18,43 @@
 
 namespace slate {
 
+/// A persistent p x q group of in-process ranks: the rank threads' grids and
+/// communicators (thread_comm.cc) are made once and reused by every run, so
+/// matrices whose storage lives on the group's devices (multi-device
+/// matrices, MatrixStorage::parts) keep valid grids from one driver call to
+/// the next.  Groups are cached per (p, q, order, devices).
+class InprocGroup {
+public:
+    /// the cached group of p x q ranks (devices: one per rank, default r % device count)
+    static std::shared_ptr<InprocGroup> get(int p, int q, std::vector<int> devices = {},
+                                            GridOrder order = GridOrder::Col);
+    /// the group of n ranks on the first n devices with the near-square
+    /// shape of inproc_grid_shape (n = 0: inproc_ranks())
+    static std::shared_ptr<InprocGroup> of_size(int n = 0);
+    int p() const { return p_; }
+    int q() const { return q_; }
+    int size() const { return p_ * q_; }
+    GridOrder order() const { return order_; }
+    GridPtr const& grid(int rank) const { return grids_[rank]; }
+    /// device of rank r (-1 in host mode)
+    int device(int rank) const { return devices_.empty() ? -1 : devices_[rank]; }
+    /// fn(rank, grid) on every rank thread (serialized with run_in_process)
+    void run(std::function<void(int, GridPtr const&)> const& fn);
+
+    InprocGroup(int p, int q, GridOrder order, std::vector<int> devices);
+private:
+    int p_, q_;
+    GridOrder order_;
+    std::vector<int> devices_;
+    std::vector<GridPtr> grids_;
+};
+using InprocGroupPtr = std::shared_ptr<InprocGroup>;
+
+/// Bytes the single-process paths copied between a caller's operand and the
+/// in-process ranks (scatter_from_host + gather_to_host): zero for drivers
+/// called on multi-device matrices (tests pin that no re-scatter happens).
+int64_t inproc_copy_bytes();
+
 /// Run fn(rank, grid) on p*q in-process ranks (threads; rank r on device
 /// devices[r], default r % device count; host mode when no GPU is visible).
 /// Each thread sees `grid` as its default grid.  The first exception of any

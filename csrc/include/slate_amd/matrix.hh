@@ -29,6 +29,8 @@
 
 namespace slate {
 
+class InprocGroup;   // inproc.hh
+
 //------------------------------------------------------------------------------
 /// Non-owning view of one tile (reference Tile.hh:395-419).
 template <typename T>
@@ -128,6 +130,18 @@ public:
     void ws_erase(int64_t si, int64_t sj);
     MatrixStorage(MatrixStorage const&) = delete;
     MatrixStorage& operator=(MatrixStorage const&) = delete;
+
+    /// Multi-device storage (reference: one MPI rank spreads its tiles over
+    /// all of its GPUs, tileDevice = func::device_1d_grid, MatrixStorage.hh:
+    /// 503-506; Matrix::fromDevices(Aarray, num_devices), Matrix.hh:396-404).
+    /// The matrix lives on the ranks of an in-process group (inproc.hh):
+    /// parts[r] is rank r's block-cyclic local storage on group->grid(r), on
+    /// rank r's device.  This caller-side storage holds no data; drivers
+    /// called with it run on the group's ranks directly on the parts
+    /// (spread.hh) -- no scatter or gather per call.
+    std::shared_ptr<InprocGroup> group;
+    std::vector<std::shared_ptr<MatrixStorage<T>>> parts;
+    bool multi() const { return !parts.empty(); }
 
     int64_t m, n, mb, nb;
     GridPtr grid;
@@ -289,6 +303,22 @@ public:
     T& elem(int64_t i, int64_t j);
 
     std::shared_ptr<MatrixStorage<T>> storage() const { return storage_; }
+    /// multi-device matrix: spread over the devices of an in-process group
+    bool is_multi_device() const { return storage_ && storage_->multi(); }
+    /// the view v (of another storage with the same geometry) on this storage
+    BaseMatrix rebase(BaseMatrix const& v) const {
+        BaseMatrix r = v;
+        r.storage_ = storage_;
+        return r;
+    }
+    /// the same view (offsets, op, uplo, diag, kind, bands) on in-process
+    /// rank r's part of a multi-device matrix
+    BaseMatrix on_part(int r) const {
+        slate_error_if_msg(!is_multi_device(), "on_part: not a multi-device matrix");
+        BaseMatrix v = *this;
+        v.storage_ = storage_->parts.at(size_t(r));
+        return v;
+    }
     bool aligned() const { return r0_ % storage_->mb == 0 && c0_ % storage_->nb == 0; }
 
     /// Make the host or device instance valid; mark modified.
@@ -411,13 +441,38 @@ public:
     /// Wrap a ScaLAPACK local array (2D block-cyclic on `grid`).
     static Matrix fromScaLAPACK(int64_t m, int64_t n, T* A, int64_t lld, int64_t mb, int64_t nb,
                                 GridPtr grid, Loc loc = Loc::Host, int rsrc = 0, int csrc = 0);
-    /// Wrap a device-resident local array (reference fromDevices).
+    /// Wrap a device-resident local array (one GPU per process).
     static Matrix fromDevices(int64_t m, int64_t n, T* dA, int64_t lld, int64_t mb, int64_t nb, GridPtr grid) {
         return fromScaLAPACK(m, n, dA, lld, mb, nb, grid, Loc::Device);
     }
+    /// Reference fromDevices (Matrix.hh:396-404, 529-563): one process, its
+    /// tiles 1-D block-cyclic over num_devices GPUs by tile column (tile
+    /// column j on device j % num_devices); Aarray[d] is device d's local
+    /// array (its tile columns side by side, leading dimension lda).  The
+    /// matrix is a multi-device matrix over a 1 x num_devices in-process
+    /// group on devices 0 .. num_devices-1.  p x q must be 1 x 1 (a
+    /// multi-process job runs one GPU per process: use the overload above).
+    /// Without a GPU (CPU builds and tests) the arrays are host memory.
+    static Matrix fromDevices(int64_t m, int64_t n, T** Aarray, int num_devices, int64_t lda, int64_t mb,
+                              int64_t nb, int p = 1, int q = 1);
+    /// New multi-device matrix, 2-D block-cyclic over the near-square grid
+    /// of num_devices in-process ranks (0: every GPU the process may use;
+    /// 8 GPUs -> 2 x 4), allocated on the devices.  Every driver that accepts
+    /// it (gemm, trsm, herk, getrf / getrs / gesv, potrf / potrs / posv,
+    /// geqrf / gels, the mixed-precision solvers, heev, svd, norm, copy,
+    /// add, scale, set) runs on those ranks in place.
+    static Matrix multiDevice(int64_t m, int64_t n, int64_t mb, int64_t nb, int num_devices = 0);
+    /// Caller-side multi-device matrix over `group` whose parts are the
+    /// per-rank matrices parts[r] (made on the group's rank threads, same
+    /// geometry, whole views): drivers' distributed outputs (QR T factors).
+    static Matrix fromParts(std::shared_ptr<InprocGroup> const& group, std::vector<Matrix<T>> const& parts);
+    /// Gather the whole matrix into a column-major host array (every rank
+    /// of a multi-process grid, or the caller of a multi-device matrix).
+    void gather(T* A, int64_t lda) const;
 
     /// Allocate local storage at the target's location (Matrix.hh:832).
     void insertLocalTiles(Target target = Target::Host) const {
+        if (this->storage_->multi()) { insert_parts(target); return; }
         auto loc = target == Target::Devices ? Loc::Device : Loc::Host;
         auto other = loc == Loc::Device ? Loc::Host : Loc::Device;
         bool fresh = !(this->storage_->has(other) && this->storage_->state(other) != Invalid);
@@ -431,6 +486,9 @@ public:
     Matrix emptyLike(int64_t mb = 0, int64_t nb = 0, Op deepOp = Op::NoTrans) const;
 
     Matrix sub(int64_t i1, int64_t i2, int64_t j1, int64_t j2) const { return Matrix(BaseMatrix<T>::sub(i1, i2, j1, j2)); }
+private:
+    void insert_parts(Target target) const;
+public:
     Matrix slice(int64_t r1, int64_t r2, int64_t c1, int64_t c2) const { return Matrix(BaseMatrix<T>::slice(r1, r2, c1, c2)); }
 };
 

@@ -244,6 +244,14 @@ void hbmm(Side side, T alpha, HermitianBandMatrix<T> const& A, Matrix<T> const& 
           Options const& opts = {});
 template <typename T>
 void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Matrix<T>& B, Options const& opts = {});
+/// tbsm with gbtrf's row interchanges (reference slate.hh:305-310,
+/// src/tbsmPivots.cc): the interchanges of tile k are applied to
+/// B(k:mt-1, :) before tile k's solve on a forward sweep (op(A) lower, the L
+/// of gbtrf) or after it on a backward sweep (op(A) upper); empty pivots =
+/// plain tbsm.
+template <typename T>
+void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B,
+          Options const& opts = {});
 
 //------------------------------------------------------------------------------
 // Hermitian indefinite (reference hetrf.cc, hetrs.cc, hesv.cc); LAPACK ipiv.

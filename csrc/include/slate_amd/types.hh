@@ -68,9 +68,14 @@ inline T get_option(Options const& opts, Option key, T defval) {
         return T(it->second.i_);
 }
 
+/// Target used when the options name none: the caller's default, unless the
+/// thread runs a driver on the parts of multi-device matrices (spread.hh),
+/// whose data lives on the devices -- then Target::Devices.
+inline Target& thread_default_target() { thread_local Target t = Target(0); return t; }
 inline Target get_target(Options const& opts, Target def = Target::HostTask) {
     auto it = opts.find(Option::Target);
-    return it == opts.end() ? def : Target(char(it->second.i_));
+    if (it != opts.end()) return Target(char(it->second.i_));
+    return thread_default_target() != Target(0) ? thread_default_target() : def;
 }
 
 //------------------------------------------------------------------------------

@@ -6,6 +6,8 @@
 // implemented in Python (torch.distributed / gloo) re-acquire it through the
 // trampoline below.
 #include <pybind11/pybind11.h>
+#include <chrono>
+#include <thread>
 #include <pybind11/numpy.h>
 #include <pybind11/stl.h>
 #include <pybind11/functional.h>
@@ -296,7 +298,11 @@ void bind_type(py::module_& m, const char* sfx) {
         }, py::arg("target") = Target::Host)
         .def("tileUpdateAllOrigin", &BaseMatrix<T>::tileUpdateAllOrigin)
         .def("releaseWorkspace", &BaseMatrix<T>::releaseWorkspace)
-        .def("origin_is_device", [](BaseMatrix<T> const& A) { return A.storage()->origin() == Loc::Device; });
+        .def("origin_is_device", [](BaseMatrix<T> const& A) { return A.storage()->origin() == Loc::Device; })
+        .def_property_readonly("is_multi_device", &BaseMatrix<T>::is_multi_device)
+        .def_property_readonly("num_parts", [](BaseMatrix<T> const& A) {
+            return A.is_multi_device() ? int(A.storage()->parts.size()) : 1;
+        });
 
     py::class_<Matrix<T>, BaseMatrix<T>>(m, ("Matrix_" + s).c_str())
         .def(py::init([](int64_t mm, int64_t n, int64_t mb, int64_t nb, GridPtr g) {
@@ -317,6 +323,27 @@ void bind_type(py::module_& m, const char* sfx) {
         }, py::arg("m"), py::arg("n"), py::arg("row_sizes"), py::arg("col_sizes"), py::arg("owner"),
            py::arg("grid") = nullptr)
         .def("arbitrary_layout", &BaseMatrix<T>::arbitrary_layout)
+        // multi-device matrices (reference fromDevices(Aarray, num_devices)):
+        // 2-D block-cyclic over num_devices in-process ranks, or the
+        // reference's 1-D tile-column layout over given per-device arrays
+        .def_static("multiDevice", [](int64_t mm, int64_t n, int64_t mb, int64_t nb, int num_devices) {
+            py::gil_scoped_release r;
+            return Matrix<T>::multiDevice(mm, n, mb, nb, num_devices);
+        }, py::arg("m"), py::arg("n"), py::arg("mb"), py::arg("nb"), py::arg("num_devices") = 0)
+        .def_static("fromDevicesArray", [](int64_t mm, int64_t n, std::vector<uintptr_t> ptrs, int64_t lda,
+                                           int64_t mb, int64_t nb) {
+            std::vector<T*> a;
+            for (auto p : ptrs) a.push_back(reinterpret_cast<T*>(p));
+            return Matrix<T>::fromDevices(mm, n, a.data(), int(a.size()), lda, mb, nb);
+        })
+        .def("gather_into", [](Matrix<T> const& A, py::array_t<T, py::array::f_style> out) {
+            py::buffer_info bi = out.request();
+            slate_error_if_msg(bi.ndim != 2 || bi.shape[0] < A.m() || bi.shape[1] < A.n(), "gather_into: shape");
+            T* ptr = static_cast<T*>(bi.ptr);
+            const int64_t ld = bi.shape[0];
+            py::gil_scoped_release r;
+            A.gather(ptr, ld);
+        })
         .def_static("fromDevicePointer", [](int64_t mm, int64_t n, uintptr_t ptr, int64_t lld, int64_t mb,
                                               int64_t nb, GridPtr g) {
             return Matrix<T>::fromScaLAPACK(mm, n, reinterpret_cast<T*>(ptr), lld, mb, nb, g, Loc::Device);
@@ -406,29 +433,51 @@ PYBIND11_MODULE(_slate, m) {
     // self-check of the in-process all-reduce (small: all-to-all copies;
     // >= 1 MiB with > 2 ranks: reduce-scatter + all-gather): every rank
     // contributes x_r[i] = r + i * 1e-3; returns the max error over ranks
-    m.def("inproc_allreduce_check", [](int nranks, int64_t count) {
+    // rounds > 1: every round is a (large) all-reduce immediately followed by
+    // a bcast and a small all-reduce, with rank-dependent host delays, so a
+    // fast rank enters the next collective while a slow one is still in the
+    // last hand-off of the previous one (sliced all-reduce phase 3)
+    m.def("inproc_allreduce_check", [](int nranks, int64_t count, int rounds) {
         std::vector<double> err(nranks, 0.0);
         {
             py::gil_scoped_release r;
             run_in_process(1, nranks, [&](int rank, GridPtr const& g) {
                 const bool dev = device::available();
-                std::vector<double> h(count);
-                for (int64_t i = 0; i < count; ++i) h[i] = rank + double(i % 1000) * 1e-3;
-                device::Buffer<double> d(dev ? count : 0);
+                const Loc loc = dev ? Loc::Device : Loc::Host;
+                std::vector<double> h(count), hs(64);
+                device::Buffer<double> d(dev ? count : 0), ds(dev ? 64 : 0);
                 hipStream_t st = dev ? device::queue(0) : nullptr;
-                double* p = h.data();
-                if (dev) { device::memcpy_async(d.data(), h.data(), count * 8, st); p = d.data(); }
-                g->world().allreduce(p, p, size_t(count), ScalarType::Float64, ReduceOp::Sum,
-                                     dev ? Loc::Device : Loc::Host, st);
-                if (dev) { device::memcpy_async(h.data(), d.data(), count * 8, st); slate_hip_call(hipStreamSynchronize(st)); }
-                const double base = nranks * (nranks - 1) / 2.0;
+                double* p = dev ? d.data() : h.data();
+                double* ps = dev ? ds.data() : hs.data();
                 double e = 0;
-                for (int64_t i = 0; i < count; ++i) e = std::max(e, std::abs(h[i] - (base + nranks * double(i % 1000) * 1e-3)));
+                for (int it = 0; it < rounds; ++it) {
+                    for (int64_t i = 0; i < count; ++i) h[i] = rank + it + double(i % 1000) * 1e-3;
+                    for (int i = 0; i < 64; ++i) hs[i] = rank == it % nranks ? double(it * 100 + i) : -1.0;
+                    if (dev) {
+                        device::memcpy_async(d.data(), h.data(), count * 8, st);
+                        device::memcpy_async(ds.data(), hs.data(), 64 * 8, st);
+                    }
+                    if ((rank + it) % nranks == 0) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+                    g->world().allreduce(p, p, size_t(count), ScalarType::Float64, ReduceOp::Sum, loc, st);
+                    if ((rank + it) % nranks == 1) std::this_thread::sleep_for(std::chrono::milliseconds(2));
+                    g->world().bcast(ps, 64, ScalarType::Float64, it % nranks, loc, st);
+                    g->world().allreduce(ps, ps, 64, ScalarType::Float64, ReduceOp::Max, loc, st);
+                    if (dev) {
+                        device::memcpy_async(h.data(), d.data(), count * 8, st);
+                        device::memcpy_async(hs.data(), ds.data(), 64 * 8, st);
+                        slate_hip_call(hipStreamSynchronize(st));
+                    }
+                    const double base = nranks * (nranks - 1) / 2.0 + double(nranks) * it;
+                    for (int64_t i = 0; i < count; ++i)
+                        e = std::max(e, std::abs(h[i] - (base + nranks * double(i % 1000) * 1e-3)));
+                    for (int i = 0; i < 64; ++i) e = std::max(e, std::abs(hs[i] - double(it * 100 + i)));
+                }
                 err[rank] = e;
             });
         }
         return *std::max_element(err.begin(), err.end());
-    });
+    }, py::arg("nranks"), py::arg("count"), py::arg("rounds") = 1);
+    m.def("inproc_copy_bytes", &inproc_copy_bytes);
     m.def("inproc_last_shape", []() { int p = 0, q = 0; inproc_last_shape(p, q); return py::make_tuple(p, q); });
     m.def("comm_abort_all", &comm_abort_all, py::call_guard<py::gil_scoped_release>());
     m.def("comm_async_errors", &comm_async_errors);

@@ -234,6 +234,9 @@ void bind_drivers(py::module_& m, std::string const& s) {
         Options op = to_options(o); py::gil_scoped_release r; hbmm(sd, a, A, B, b, C, op); });
     DEF("tbsm", [](Side sd, T a, TriangularBandMatrix<T> const& A, Matrix<T>& B, py::dict o) {
         Options op = to_options(o); py::gil_scoped_release r; tbsm(sd, a, A, B, op); });
+    DEF("tbsm_pivots", [piv_in](Side sd, T a, TriangularBandMatrix<T> const& A, py::list piv, Matrix<T>& B,
+                                py::dict o) {
+        Options op = to_options(o); Pivots P = piv_in(piv); py::gil_scoped_release r; tbsm(sd, a, A, P, B, op); });
     // ---- Hermitian indefinite (LAPACK-style ipiv list)
     DEF("hetrf", [](HermitianMatrix<T>& A, py::dict o) {
         Options op = to_options(o); std::vector<int64_t> ip; int64_t info;

@@ -4,6 +4,7 @@
 // scale_row_col.cc, set.cc, set_lambdas.cc, redistribute.cc, norm.cc,
 // colNorms.cc, internal_reduce_info.cc.
 #include "internal.hh"
+#include "spread.hh"
 
 #include <algorithm>
 
@@ -220,6 +221,10 @@ bool co_located(BaseMatrix<Ts> const& A, BaseMatrix<Td> const& B) {
 
 template <typename Ts, typename Td>
 void copy(BaseMatrix<Ts> const& A, BaseMatrix<Td>& B, Options const& opts) {
+    if (A.is_multi_device() || B.is_multi_device()) {
+        internal::copy_multi<Ts, Td>(A, B, opts);
+        return;
+    }
     trace::Block tb("copy");
     internal::DriverScope ds_;
     if (A.storage()->banded || B.storage()->banded) {
@@ -292,6 +297,10 @@ void redistribute(Matrix<T> const& A, Matrix<T>& B, Options const& opts) {
 
 template <typename T>
 void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            add(alpha, M[0], beta, M[1], opts);
+        }, false))
+        return;
     if (A.arbitrary_layout() || B.arbitrary_layout()) {
         Matrix<T> Ab = bc_operand(A, opts), Bb = block_cyclic(B, opts);
         add(alpha, Ab, beta, Bb, opts);
@@ -313,6 +322,12 @@ void add(T alpha, Matrix<T> const& A, T beta, Matrix<T>& B, Options const& opts)
 
 template <typename T>
 void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T>& B, Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            auto Ar = internal::rewrap(A, M[0]);
+            auto Br = internal::rewrap(B, M[1]);
+            add(alpha, Ar, beta, Br, opts);
+        }, false))
+        return;
     trace::Block tb("tzadd");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -338,6 +353,13 @@ void add(T alpha, BaseTrapezoidMatrix<T> const& A, T beta, BaseTrapezoidMatrix<T
 
 template <typename T>
 void scale(real_type<T> numer, real_type<T> denom, BaseMatrix<T>& A, Options const& opts) {
+    if (A.is_multi_device()) {
+        A.storage()->group->run([&](int r, GridPtr const&) {
+            BaseMatrix<T> Ar = A.on_part(r);
+            scale(numer, denom, Ar, opts);
+        });
+        return;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> B = block_cyclic(A, opts);
         BaseMatrix<T>& Bb = B;
@@ -405,6 +427,14 @@ void scale_row_col(Equed equed, std::vector<real_type<T>> const& R, std::vector<
 
 template <typename T>
 void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
+    if (A.is_multi_device()) {
+        A.storage()->group->run([&](int r, GridPtr const&) {
+            internal::TargetScope ts(Target::Devices);
+            BaseMatrix<T> Ar = A.on_part(r);
+            set(offdiag, diag, Ar, opts);
+        });
+        return;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> B = block_cyclic(A, opts);
         B.set_uplo(A.uplo());
@@ -471,6 +501,13 @@ void set(T offdiag, T diag, BaseMatrix<T>& A, Options const& opts) {
 
 template <typename T>
 void set(std::function<T(int64_t, int64_t)> const& value, BaseMatrix<T>& A, Options const&) {
+    if (A.is_multi_device()) {
+        A.storage()->group->run([&](int r, GridPtr const&) {
+            BaseMatrix<T> Ar = A.on_part(r);
+            set(value, Ar, Options{});
+        });
+        return;
+    }
     trace::Block tb("set_lambda");
     internal::DriverScope ds_;
     // evaluated on the host instance, then marked modified
@@ -493,6 +530,14 @@ void set(std::function<T(int64_t, int64_t)> const& value, BaseMatrix<T>& A, Opti
 
 template <typename T>
 void gather(BaseMatrix<T> const& A, std::vector<T>& full, Options const& opts) {
+    if (A.is_multi_device()) {
+        A.storage()->group->run([&](int r, GridPtr const&) {
+            std::vector<T> f;
+            gather(A.on_part(r), f, opts);
+            if (r == 0) full.swap(f);
+        });
+        return;
+    }
     trace::Block tb("gather");
     internal::DriverScope ds_;
     (void)opts;
@@ -737,6 +782,15 @@ real_type<T> norm_band_stored(Norm in_norm, BaseMatrix<T> const& A) {
 
 template <typename T>
 real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
+    if (A.is_multi_device()) {
+        real_type<T> v = 0;
+        A.storage()->group->run([&](int r, GridPtr const&) {
+            internal::TargetScope ts(Target::Devices);
+            const real_type<T> x = norm(in_norm, A.on_part(r), opts);
+            if (r == 0) v = x;
+        });
+        return v;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> B = block_cyclic(A, opts);
         B.set_kind(A.matrix_kind());
@@ -887,6 +941,15 @@ real_type<T> norm(Norm in_norm, BaseMatrix<T> const& A, Options const& opts) {
 
 template <typename T>
 void colNorms(Norm in_norm, Matrix<T> const& A, real_type<T>* values, Options const& opts) {
+    if (A.is_multi_device()) {
+        A.storage()->group->run([&](int r, GridPtr const&) {
+            internal::TargetScope ts(Target::Devices);
+            std::vector<real_type<T>> v(size_t(A.n()));
+            colNorms(in_norm, Matrix<T>(A.on_part(r)), v.data(), opts);
+            if (r == 0) std::copy(v.begin(), v.end(), values);
+        });
+        return;
+    }
     trace::Block tb("colNorms");
     internal::DriverScope ds_;
     using R = real_type<T>;

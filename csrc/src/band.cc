@@ -696,6 +696,77 @@ void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Matrix<T>& B, Op
     slate::copy<T, T>(op_view(t, Bt), B, opts);
 }
 
+/// tbsm with the pivots of gbtrf (reference src/tbsmPivots.cc): op(A) X =
+/// alpha B (Left) or X op(A) = alpha B (Right) where the row interchanges of
+/// tile k are applied to B(k:mt-1, :) just before tile k's solve on a
+/// forward sweep (op(A) lower: the L factor of gbtrf) or right after it on a
+/// backward sweep (op(A) upper: L^T).  Tile by tile: the diagonal tile's band
+/// part by one trsm, the band below / above it by one gemm; empty pivots:
+/// plain tbsm.
+template <typename T>
+void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B,
+          Options const& opts) {
+    if (pivots.empty()) { tbsm(side, alpha, A, B, opts); return; }
+    trace::Block tb("tbsm_pivots");
+    internal::DriverScope ds_;
+    if (side == Side::Right) {
+        // X op(A) = alpha B  <=>  t(op(A)) t(X) = alpha' t(B), on a transposed copy of B
+        const Op t = is_complex_v<T> ? Op::ConjTrans : Op::Trans;
+        const T alpha2 = t == Op::ConjTrans ? slate::conj(alpha) : alpha;
+        Matrix<T> Bt = B.emptyLike(0, 0, Op::Trans);
+        Bt.insertLocalTiles(resolve_target(opts));
+        slate::copy<T, T>(op_view(t, B), Bt, opts);
+        TriangularBandMatrix<T> At = t == Op::ConjTrans ? conj_transpose(A) : transpose(A);
+        tbsm(Side::Left, alpha2, At, pivots, Bt, opts);
+        slate::copy<T, T>(op_view(t, Bt), B, opts);
+        return;
+    }
+    const Target target = resolve_target(opts);
+    BaseMatrix<T> Ap = physical<T>(A);
+    const Uplo u = A.uplo_physical();
+    const Op op = A.op();
+    const int64_t kd = A.bandwidth(), nt = Ap.nt(), n = Ap.n();
+    const int64_t dmin = u == Uplo::Lower ? 0 : -kd, dmax = u == Uplo::Lower ? kd : 0;
+    const bool forward = (u == Uplo::Lower) == (op == Op::NoTrans);
+    slate_error_if_msg(B.mt() != nt, "tbsm: B's tile rows must match A's tiles");
+    scale_by(alpha, B, opts);
+    auto block = [&](int64_t r0, int64_t r1, int64_t c0, int64_t c1) {
+        return op == Op::NoTrans ? band_chunk(Ap, r0, r1, c0, c1, dmin, dmax, false, target)
+                                 : op_view(op, band_chunk(Ap, c0, c1, r0, r1, dmin, dmax, false, target));
+    };
+    auto swaps = [&](int64_t k, bool fwd) {
+        if (k >= int64_t(pivots.size()) || pivots[k].empty()) return;
+        Matrix<T> Bk = B.sub(k, B.mt() - 1, 0, B.nt() - 1);
+        internal::apply_pivots(Pivots{pivots[k]}, BaseMatrix<T>(Bk), Bk, target, fwd);
+    };
+    for (int64_t s = 0; s < nt; ++s) {
+        const int64_t k = forward ? s : nt - 1 - s;
+        if (forward) swaps(k, true);
+        Matrix<T> Bk = B.sub(k, k, 0, B.nt() - 1);
+        const int64_t e0 = col_off(Ap, k), e1 = e0 + Ap.tileNb(k) - 1;
+        if (!forward && k + 1 < nt && kd > 0) {
+            // B(k) -= op(A)(k, k+1 : k_end) B(k+1 : k_end)
+            const int64_t c1 = tile_col_of(Ap, std::min(n - 1, e1 + kd));
+            Matrix<T> Bs = B.sub(k + 1, c1, 0, B.nt() - 1);
+            gemm(T(-1), block(k, k, k + 1, c1), Bs, T(1), Bk, opts);
+        }
+        {
+            Matrix<T> D = band_chunk(Ap, k, k, k, k, dmin, dmax, false, target);
+            TriangularMatrix<T> Tk(u, A.diag(), D);
+            if (op == Op::NoTrans) trsm(Side::Left, T(1), Tk, Bk, opts);
+            else if (op == Op::Trans) trsm(Side::Left, T(1), transpose(Tk), Bk, opts);
+            else trsm(Side::Left, T(1), conj_transpose(Tk), Bk, opts);
+        }
+        if (forward && k + 1 < nt && kd > 0) {
+            // B(k+1 : i_end) -= op(A)(k+1 : i_end, k) B(k)
+            const int64_t r1 = tile_col_of(Ap, std::min(n - 1, e1 + kd));
+            Matrix<T> Bs = B.sub(k + 1, r1, 0, B.nt() - 1);
+            gemm(T(-1), block(k + 1, r1, k, k), Bk, T(1), Bs, opts);
+        }
+        if (!forward) swaps(k, false);
+    }
+}
+
 #define SLATE_BAND_INST(T)                                                                                 \
     template int64_t gbtrf<T>(BandMatrix<T>&, Pivots&, Options const&);                                   \
     template void gbtrs<T>(BandMatrix<T> const&, Pivots const&, Matrix<T>&, Options const&);              \
@@ -704,6 +775,7 @@ void tbsm(Side side, T alpha, TriangularBandMatrix<T> const& A, Matrix<T>& B, Op
     template void pbtrs<T>(HermitianBandMatrix<T> const&, Matrix<T>&, Options const&);                    \
     template int64_t pbsv<T>(HermitianBandMatrix<T>&, Matrix<T>&, Options const&);                        \
     template void gbmm<T>(T, BandMatrix<T> const&, Matrix<T> const&, T, Matrix<T>&, Options const&);      \
+    template void tbsm<T>(Side, T, TriangularBandMatrix<T> const&, Pivots const&, Matrix<T>&, Options const&); \
     template void hbmm<T>(Side, T, HermitianBandMatrix<T> const&, Matrix<T> const&, T, Matrix<T>&,        \
                           Options const&);                                                                 \
     template void tbsm<T>(Side, T, TriangularBandMatrix<T> const&, Matrix<T>&, Options const&);

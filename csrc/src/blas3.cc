@@ -703,6 +703,11 @@ bool b_conforms(BaseMatrix<T> const& Ap, Op op, BaseMatrix<T> const& B) {
 
 template <typename T>
 void trsm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            auto Ar = internal::rewrap(A, M[0]);
+            trsm(side, alpha, Ar, M[1], opts);
+        }, false))
+        return;
     if (A.arbitrary_layout() || B.arbitrary_layout()) {
         TriangularMatrix<T> Ab(A.uplo(), A.diag(), bc_operand(A, opts));
         Matrix<T> Bb = block_cyclic(B, opts);
@@ -920,6 +925,11 @@ void tri_summa(Uplo uplo, T alpha, BaseMatrix<T> const& A_in, BaseMatrix<T> cons
 
 template <typename T>
 void herk(real_type<T> alpha, Matrix<T> const& A, real_type<T> beta, HermitianMatrix<T>& C, Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&C, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            auto Cr = internal::rewrap(C, M[1]);
+            herk(alpha, M[0], beta, Cr, opts);
+        }, false))
+        return;
     trace::Block tb("herk");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -1392,6 +1402,11 @@ void hemm_dist(Side side, bool herm, T alpha, BaseTrapezoidMatrix<T> const& A, M
 template <typename T>
 void hemm(Side side, T alpha, HermitianMatrix<T> const& A, Matrix<T> const& B, T beta, Matrix<T>& C,
           Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&B, false}, {&C, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            auto Ar = internal::rewrap(A, M[0]);
+            hemm(side, alpha, Ar, M[1], beta, M[2], opts);
+        }, false))
+        return;
     trace::Block tb("hemm");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);
@@ -1431,6 +1446,11 @@ void symm(Side side, T alpha, SymmetricMatrix<T> const& A, Matrix<T> const& B, T
 
 template <typename T>
 void trmm(Side side, T alpha, TriangularMatrix<T> const& A, Matrix<T>& B, Options const& opts) {
+    if (internal::spread<T>(opts, {{&A, false}, {&B, true}}, [&](std::vector<Matrix<T>>& M, int) {
+            auto Ar = internal::rewrap(A, M[0]);
+            trmm(side, alpha, Ar, M[1], opts);
+        }, false))
+        return;
     trace::Block tb("trmm");
     internal::DriverScope ds_;
     Target target = resolve_target(opts);

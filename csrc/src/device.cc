@@ -106,41 +106,57 @@ void ensure_streams_locked(State& s) {
     if (s.streams_ready) return;
     int lo = 0, hi = 0;
     slate_hip_call(hipDeviceGetStreamPriorityRange(&lo, &hi));
-    // CU partitioning: the panel (1) and comm queues run on a reserved set of
-    // CUs so their many short kernels never queue behind the trailing update's
-    // long-running GEMM workgroups; the trailing update (kTrailQueue) runs on
-    // the rest; queue 0 and the lookahead queues (2..6) may use every CU.  SLATE_PANEL_CUS=0 disables it.
-    int ncu = 0;
+    // CU partitioning (SLATE_PANEL_CUS=R, 0 = off): the trailing-update queue
+    // (and by default the lookahead queue) run on a CU mask that leaves R CUs
+    // free, so the panel chain's short kernels always find idle CUs instead of
+    // waiting for a SIMD of the trailing GEMM to drain.
+    //
+    // Mask bit i selects a CU of XCC (i mod #XCC) -- the KFD deals user-mask
+    // bits round-robin over the XCCs -- so reserving bits 0 .. R-1 takes R/8
+    // CUs from every XCD and the XCD-balanced trailing GEMM loses R/256 of its
+    // rate (round 5 reserved bits c % (256/R) == 0, i.e. all of them on XCD 0,
+    // which then ran the balanced GEMM at the speed of a crippled XCD; the
+    // placement and the complement-mask GEMM rate are measured by
+    // csrc/tools/cu_mask_probe.hip, profiles/r6_cu_mask_probe.txt).
+    //
+    // SLATE_PANEL_CUS_MODE: "shared" (default) keeps the panel and comm queues
+    // unmasked at high priority -- they may use every CU, and the R reserved
+    // ones are never held by the update; "exclusive" confines them to the R
+    // reserved CUs (a masked stream cannot carry a priority).
+    // SLATE_PANEL_CUS_LA=0 leaves the lookahead queue unmasked as well.
+    int ncu = 0, nxcc = 1;
     {
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, s.device) == hipSuccess) ncu = prop.multiProcessorCount;
+        int x = 0;
+        if (hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, s.device) == hipSuccess && x > 0) nxcc = x;
     }
     int reserve = 0;
     if (const char* e = std::getenv("SLATE_PANEL_CUS")) reserve = std::atoi(e);
     if (ncu < 64) reserve = 0;
     reserve = std::max(0, std::min(reserve, ncu / 2));
+    reserve = (reserve + nxcc - 1) / nxcc * nxcc;   // whole CUs per XCC
+    bool exclusive = false, mask_la = true;
+    if (const char* e = std::getenv("SLATE_PANEL_CUS_MODE")) exclusive = std::string(e) == "exclusive";
+    if (const char* e = std::getenv("SLATE_PANEL_CUS_LA")) mask_la = std::atoi(e) != 0;
     std::vector<uint32_t> mask_panel, mask_update;
     if (reserve > 0) {
-        int words = (ncu + 31) / 32;
+        const int words = (ncu + 31) / 32;
         mask_panel.assign(words, 0);
         mask_update.assign(words, 0);
-        // spread the reserved CUs evenly over the CU index space
-        int stride = ncu / reserve;
-        for (int c = 0; c < ncu; ++c) {
-            bool res = (c % stride == 0) && (c / stride < reserve);
-            (res ? mask_panel : mask_update)[c / 32] |= (1u << (c % 32));
-        }
+        for (int c = 0; c < ncu; ++c)
+            (c < reserve ? mask_panel : mask_update)[c / 32] |= (1u << (c % 32));
     }
     s.reserved_cus = reserve;
-    int prio_unused = 0;
     for (int i = 0; i < kNumQueues; ++i) {
-        bool panel = (i == 1 || i == kCommQueue);
-        if (reserve > 0 && (panel || i == kTrailQueue || i == kLookaheadQueue)) {
+        const bool panel = (i == 1 || i == kCommQueue);
+        const bool masked = reserve > 0 &&
+            (panel ? exclusive : (i == kTrailQueue || (i == kLookaheadQueue && mask_la)));
+        if (masked) {
             auto& m = panel ? mask_panel : mask_update;
-            (void)prio_unused;
             slate_hip_call(hipExtStreamCreateWithCUMask(&s.streams[i], uint32_t(m.size() * 32), m.data()));
         } else {
-            int prio = panel ? hi : lo;
+            const int prio = panel ? hi : lo;
             slate_hip_call(hipStreamCreateWithPriority(&s.streams[i], hipStreamNonBlocking, prio));
         }
     }
@@ -370,16 +386,34 @@ void* malloc_async(size_t bytes, hipStream_t stream) {
     return p;
 }
 
+namespace {
+/// a block whose context was destroyed (its streams are gone): wait for the
+/// context's device, hand the block back to HIP, and delete the context with
+/// its last block.  Called with s.mtx held through `g`, which it releases.
+void release_destroyed(State& s, void* ptr, std::unique_lock<std::mutex>& g) {
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(s.device);
+    (void)hipDeviceSynchronize();
+    (void)hipFree(ptr);
+    if (cur >= 0) (void)hipSetDevice(cur);
+    const bool last = s.live.empty();
+    g.unlock();
+    if (last) delete static_cast<Context*>(&s);
+}
+}  // namespace
+
 void free_async(void* ptr, hipStream_t stream) {
     if (!ptr) return;
     auto& s = owner_of(ptr);
-    std::lock_guard<std::mutex> g(s.mtx);
+    std::unique_lock<std::mutex> g(s.mtx);
     auto it = s.live.find(ptr);
     slate_assert(it != s.live.end());
     const size_t b = it->second;
     s.live.erase(it);
     s.live_stream.erase(ptr);
     s.in_use -= b;
+    if (s.destroyed) { release_destroyed(s, ptr, g); return; }
     s.stream_free[stream].emplace(b, ptr);
     s.stream_cached += b;
 }
@@ -399,11 +433,7 @@ void free(void* ptr) {
     if (s.destroyed) {
         // its context is gone (streams destroyed): release the block to HIP,
         // and the context itself with its last block
-        (void)hipDeviceSynchronize();
-        (void)hipFree(ptr);
-        const bool last = s.live.empty();
-        g.unlock();
-        if (last) delete static_cast<Context*>(&s);
+        release_destroyed(s, ptr, g);
         return;
     }
     if (!s.streams_ready) {
@@ -413,10 +443,16 @@ void free(void* ptr) {
         s.cached += b;
         return;
     }
-    // free on events: work already queued on any queue may still read the block
+    // free on events: work already queued on any queue may still read the
+    // block.  The null stream too -- except with CU-masked queues: those are
+    // created blocking (hipExtStreamCreateWithCUMask takes no flags), so an
+    // event on the legacy null stream would be a device-wide barrier between
+    // the panel chain and the trailing update (profiles/r6_queue_overlap_probe.txt);
+    // the library itself never works on the null stream.
     State::Pending pd{ptr, b, {}};
-    pd.ev.reserve(kNumQueues + 1);
-    for (int i = 0; i <= kNumQueues; ++i) {
+    const int nq = s.reserved_cus > 0 ? kNumQueues : kNumQueues + 1;
+    pd.ev.reserve(nq);
+    for (int i = 0; i < nq; ++i) {
         hipEvent_t e = event_get_locked(s);
         slate_hip_call(hipEventRecord(e, i < kNumQueues ? s.streams[i] : nullptr));
         pd.ev.push_back(e);

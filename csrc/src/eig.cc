@@ -16,6 +16,7 @@
 // stage-1 back-transform runs distributed (unmqr / unmlq on Z, U, VT).  No
 // rank holds an n x n array on the host.
 #include "internal.hh"
+#include "spread.hh"
 #include "eig_sinks.hh"
 #include "slate_amd/eig_host.hh"
 #include "../kernels/kernels.hh"
@@ -728,6 +729,15 @@ void rescale_values(std::vector<R>& v, R anorm, R alpha) {
 
 template <typename T>
 void heev(HermitianMatrix<T>& A, std::vector<real_type<T>>& Lambda, Matrix<T>& Z, Options const& opts) {
+    {   // multi-device A (and Z): on its devices
+        bool ran = internal::spread<T>(opts, {{&A, true}, {&Z, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+            auto H = internal::rewrap(A, M[0]);
+            std::vector<real_type<T>> L;
+            heev(H, L, M[1], opts);
+            if (r == 0) Lambda.swap(L);
+        }, false);
+        if (ran) return;
+    }
     if (A.arbitrary_layout() || Z.arbitrary_layout()) {
         HermitianMatrix<T> Ab(A.uplo(), bc_operand(A, opts));
         Matrix<T> Zb = wanted(Z) ? block_cyclic(Z, opts) : Z;
@@ -973,6 +983,15 @@ void svd_square(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Ma
 /// and never form a transposed copy of A.
 template <typename T>
 void svd(Matrix<T>& A, std::vector<real_type<T>>& Sigma, Matrix<T>& U, Matrix<T>& VT, Options const& opts) {
+    {
+        bool ran = internal::spread<T>(opts, {{&A, true}, {&U, true}, {&VT, true}}, [&](std::vector<Matrix<T>>& M,
+                                                                                          int r) {
+            std::vector<real_type<T>> S;
+            svd(M[0], S, M[1], M[2], opts);
+            if (r == 0) Sigma.swap(S);
+        }, false);
+        if (ran) return;
+    }
     if (A.arbitrary_layout() || U.arbitrary_layout() || VT.arbitrary_layout()) {
         Matrix<T> Ab = bc_operand(A, opts);
         Matrix<T> Ub = wanted(U) ? block_cyclic(U, opts) : U, Vb = wanted(VT) ? block_cyclic(VT, opts) : VT;

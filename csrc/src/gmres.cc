@@ -9,6 +9,7 @@
 // least-squares problem are replicated on every rank (O(n * restart) memory,
 // negligible next to A).  One right-hand side, as in the reference.
 #include "internal.hh"
+#include "spread.hh"
 
 #include <cmath>
 
@@ -201,6 +202,16 @@ template bool gmres_refine<std::complex<double>>(
 
 template <typename T>
 int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}, {&B, false}, {&X, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                Pivots P;
+                int it = 0;
+                const int64_t i = gesv_mixed_gmres(M[0], P, M[1], M[2], it, opts);
+                if (r == 0) { info = i; pivots = P; iter = it; }
+            }))
+            return info;
+    }
     trace::Block tb("gesv_mixed_gmres");
     internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;
@@ -249,6 +260,16 @@ int64_t gesv_mixed_gmres(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& 
 
 template <typename T>
 int64_t posv_mixed_gmres(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}, {&B, false}, {&X, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                auto H = internal::rewrap(A, M[0]);
+                int it = 0;
+                const int64_t i = posv_mixed_gmres(H, M[1], M[2], it, opts);
+                if (r == 0) { info = i; iter = it; }
+            }))
+            return info;
+    }
     trace::Block tb("posv_mixed_gmres");
     internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;

@@ -7,7 +7,9 @@
 #include <cstring>
 #include <exception>
 #include <mutex>
+#include <map>
 #include <thread>
+#include <tuple>
 
 namespace slate {
 
@@ -50,26 +52,58 @@ void inproc_grid_shape(int n, int& p, int& q) {
     q = n / p;
 }
 
-void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const& fn, std::vector<int> devices,
-                    GridOrder order) {
-    std::lock_guard<std::mutex> run_lock(g_run_mtx);
+namespace {
+std::atomic<int64_t> g_copy_bytes{0};
+std::mutex g_groups_mtx;
+std::map<std::tuple<int, int, int, std::vector<int>>, std::shared_ptr<InprocGroup>>& groups() {
+    static auto* m = new std::map<std::tuple<int, int, int, std::vector<int>>, std::shared_ptr<InprocGroup>>();
+    return *m;
+}
+}  // namespace
+
+int64_t inproc_copy_bytes() { return g_copy_bytes.load(); }
+
+InprocGroup::InprocGroup(int p, int q, GridOrder order, std::vector<int> devices)
+    : p_(p), q_(q), order_(order), devices_(std::move(devices)) {
+    grids_ = make_thread_grids(p, q, order, devices_);
+}
+
+std::shared_ptr<InprocGroup> InprocGroup::get(int p, int q, std::vector<int> devices, GridOrder order) {
+    slate_error_if_msg(p < 1 || q < 1, "InprocGroup: p, q >= 1");
     const int n = p * q;
-    ++g_runs;
-    g_last_p = p;
-    g_last_q = q;
     const bool dev = device::available();
     if (dev && devices.empty())
         for (int r = 0; r < n; ++r) devices.push_back(r % device::count());
     if (!dev) devices.clear();
-    slate_error_if_msg(dev && int(devices.size()) != n, "run_in_process: one device per rank");
-    auto grids = make_thread_grids(p, q, order, devices);
+    slate_error_if_msg(dev && int(devices.size()) != n, "InprocGroup: one device per rank");
+    std::lock_guard<std::mutex> l(g_groups_mtx);
+    auto key = std::make_tuple(p, q, int(order), devices);
+    auto& slot = groups()[key];
+    if (!slot) slot = std::make_shared<InprocGroup>(p, q, order, devices);
+    return slot;
+}
+
+std::shared_ptr<InprocGroup> InprocGroup::of_size(int n) {
+    if (n <= 0) n = inproc_ranks();
+    int p, q;
+    inproc_grid_shape(n, p, q);
+    return get(p, q);
+}
+
+void InprocGroup::run(std::function<void(int, GridPtr const&)> const& fn) {
+    std::lock_guard<std::mutex> run_lock(g_run_mtx);
+    const int n = size();
+    ++g_runs;
+    g_last_p = p_;
+    g_last_q = q_;
+    const bool dev = !devices_.empty();
     if (dev) {
         if (int(g_ctx.size()) < n) { g_ctx.resize(n, nullptr); g_ctx_dev.resize(n, -1); }
         for (int r = 0; r < n; ++r)
-            if (!g_ctx[r] || g_ctx_dev[r] != devices[r]) {
+            if (!g_ctx[r] || g_ctx_dev[r] != devices_[r]) {
                 if (g_ctx[r]) device::context_destroy(g_ctx[r]);
-                g_ctx[r] = device::context_create(devices[r]);
-                g_ctx_dev[r] = devices[r];
+                g_ctx[r] = device::context_create(devices_[r]);
+                g_ctx_dev[r] = devices_[r];
             }
     }
     std::vector<std::exception_ptr> err(n);
@@ -79,12 +113,12 @@ void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const
             t_in_rank = true;
             try {
                 if (dev) device::context_bind(g_ctx[r]);
-                set_thread_default_grid(grids[r]);
-                fn(r, grids[r]);
+                set_thread_default_grid(grids_[r]);
+                fn(r, grids_[r]);
                 if (dev) device::sync_all();
             } catch (...) {
                 err[r] = std::current_exception();
-                thread_grid_abort(*grids[r]);   // wake the ranks waiting on me
+                thread_grid_abort(*grids_[r]);   // wake the ranks waiting on me
             }
             set_thread_default_grid(nullptr);
             if (dev) {
@@ -102,7 +136,15 @@ void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const
         catch (CommException const&) { if (!first) first = e; continue; }
         catch (...) { first = e; break; }
     }
-    if (first) std::rethrow_exception(first);
+    if (first) {
+        for (auto& g : grids_) thread_grid_reset(*g);   // the group stays usable
+        std::rethrow_exception(first);
+    }
+}
+
+void run_in_process(int p, int q, std::function<void(int, GridPtr const&)> const& fn, std::vector<int> devices,
+                    GridOrder order) {
+    InprocGroup::get(p, q, std::move(devices), order)->run(fn);
 }
 
 template <typename T>
@@ -121,6 +163,7 @@ void scatter_from_host(T const* A, int64_t lda, Matrix<T>& M, Target target) {
             const int64_t lr = lrow_of(M, i), gr = grow_of(M, i), mbi = M.tileMb(i);
             T const* src = A + gr + gc * lda;
             T* dst = L.ptr + lr + lc * L.ld;
+            g_copy_bytes += mbi * nbj * int64_t(sizeof(T));
             if (s) device::memcpy2d_async(dst, L.ld * sizeof(T), src, lda * sizeof(T), mbi * sizeof(T), nbj, s);
             else for (int64_t c = 0; c < nbj; ++c) std::memcpy(dst + c * L.ld, src + c * lda, mbi * sizeof(T));
         }
@@ -147,6 +190,7 @@ void gather_to_host(Matrix<T>& M, T* A, int64_t lda) {
             const int64_t lr = lrow_of(M, i), gr = grow_of(M, i), mbi = M.tileMb(i);
             T const* src = L.ptr + lr + lc * L.ld;
             T* dst = A + gr + gc * lda;
+            g_copy_bytes += mbi * nbj * int64_t(sizeof(T));
             if (s) device::memcpy2d_async(dst, lda * sizeof(T), src, L.ld * sizeof(T), mbi * sizeof(T), nbj, s);
             else for (int64_t c = 0; c < nbj; ++c) std::memcpy(dst + c * lda, src + c * L.ld, mbi * sizeof(T));
         }

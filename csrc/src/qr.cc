@@ -24,6 +24,7 @@
 // T factors: T[0] is an nb x n matrix replicated on every rank (tile k holds
 // the panel's nb x nb upper-triangular T).
 #include "internal.hh"
+#include "spread.hh"
 #include "lu_dist.hh"
 
 #include <cstdlib>
@@ -704,6 +705,14 @@ void unmqr_right(Op op, BaseMatrix<T> A, Matrix<T> const& Tf, Matrix<T>& C, Targ
 
 template <typename T>
 void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
+    if (auto grp = internal::multi_group<T>({&A})) {   // multi-device A: factor on its devices
+        std::vector<TriangularFactors<T>> Tr(grp->size());
+        internal::spread<T>(opts, {{&A, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+            geqrf(M[0], Tr[r], opts);
+        }, false);
+        T_ = internal::factors_from_parts(grp, Tr);
+        return;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> Ab = internal::block_cyclic(A, opts);
         geqrf(Ab, T_, opts);
@@ -728,6 +737,14 @@ void geqrf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
 
 template <typename T>
 void unmqr(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C, Options const& opts) {
+    if (internal::multi_group<T>({&A, &C})) {
+        auto args = internal::with_factors<T>({{&A, false}, {&C, true}}, T_);
+        internal::spread<T>(opts, args, [&](std::vector<Matrix<T>>& M, int) {
+            TriangularFactors<T> Tr(M.begin() + 2, M.end());
+            unmqr(side, op, M[0], Tr, M[1], opts);
+        }, false);
+        return;
+    }
     if (A.arbitrary_layout()) {
         // T is expressed in the tiling of A's block-cyclic working copy
         Matrix<T> Ab = internal::block_cyclic(A, opts);
@@ -1051,6 +1068,14 @@ bool rows_follow_cols(BaseMatrix<T> const& A, BaseMatrix<T> const& C) {
 
 template <typename T>
 void gelqf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
+    if (auto grp = internal::multi_group<T>({&A})) {
+        std::vector<TriangularFactors<T>> Tr(grp->size());
+        internal::spread<T>(opts, {{&A, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+            gelqf(M[0], Tr[r], opts);
+        }, false);
+        T_ = internal::factors_from_parts(grp, Tr);
+        return;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> Ab = internal::block_cyclic(A, opts);
         gelqf(Ab, T_, opts);
@@ -1075,6 +1100,14 @@ void gelqf(Matrix<T>& A, TriangularFactors<T>& T_, Options const& opts) {
 
 template <typename T>
 void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_, Matrix<T>& C, Options const& opts) {
+    if (internal::multi_group<T>({&A, &C})) {
+        auto args = internal::with_factors<T>({{&A, false}, {&C, true}}, T_);
+        internal::spread<T>(opts, args, [&](std::vector<Matrix<T>>& M, int) {
+            TriangularFactors<T> Tr(M.begin() + 2, M.end());
+            unmlq(side, op, M[0], Tr, M[1], opts);
+        }, false);
+        return;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> Ab = internal::block_cyclic(A, opts);
         unmlq(side, op, Ab, T_, C, opts);
@@ -1117,6 +1150,14 @@ void unmlq(Side side, Op op, Matrix<T> const& A, TriangularFactors<T> const& T_,
 
 template <typename T>
 void gels(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options const& opts) {
+    if (auto grp = internal::multi_group<T>({&A, &BX})) {
+        std::vector<TriangularFactors<T>> Tr(grp->size());
+        internal::spread<T>(opts, {{&A, true}, {&BX, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+            gels(M[0], Tr[r], M[1], opts);
+        }, false);
+        T_ = internal::factors_from_parts(grp, Tr);
+        return;
+    }
     trace::Block tb("gels");
     internal::DriverScope ds_;
     const int64_t m = A.m(), n = A.n(), nrhs = BX.n();
@@ -1160,6 +1201,14 @@ void gels(Matrix<T>& A, TriangularFactors<T>& T_, Matrix<T>& BX, Options const& 
 
 template <typename T>
 int64_t cholqr(Matrix<T>& A, Matrix<T>& R, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}, {&R, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                const int64_t i = cholqr(M[0], M[1], opts);
+                if (r == 0) info = i;
+            }, false))
+            return info;
+    }
     trace::Block tb("cholqr");
     internal::DriverScope ds_;
     // R^H R = A^H A ; Q = A R^{-1} (reference src/cholqr.cc:24-130).

@@ -231,6 +231,15 @@ void trtrm(TriangularMatrix<T>& A, Options const& opts) {
 
 template <typename T>
 int64_t potri(HermitianMatrix<T>& A, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                auto H = internal::rewrap(A, M[0]);
+                const int64_t i = potri(H, opts);
+                if (r == 0) info = i;
+            }, false))
+            return info;
+    }
     trace::Block tb("potri");
     internal::DriverScope ds_;
     int64_t info = 0;
@@ -243,6 +252,14 @@ int64_t potri(HermitianMatrix<T>& A, Options const& opts) {
 
 template <typename T>
 int64_t getri(Matrix<T>& A, Pivots const& pivots, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                const int64_t i = getri(M[0], pivots, opts);
+                if (r == 0) info = i;
+            }, false))
+            return info;
+    }
     if (A.arbitrary_layout()) {
         Matrix<T> Ab = internal::block_cyclic(A, opts);
         int64_t info = getri(Ab, pivots, opts);
@@ -395,6 +412,16 @@ int64_t mixed_refine(Matrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Option
 
 template <typename T>
 int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
+    {   // one process, several GPUs: the whole refinement on the in-process ranks
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}, {&B, false}, {&X, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                Pivots P;
+                int it = 0;
+                const int64_t i = gesv_mixed(M[0], P, M[1], M[2], it, opts);
+                if (r == 0) { info = i; pivots = P; iter = it; }
+            }))
+            return info;
+    }
     trace::Block tb("gesv_mixed");
     internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;
@@ -415,6 +442,16 @@ int64_t gesv_mixed(Matrix<T>& A, Pivots& pivots, Matrix<T>& B, Matrix<T>& X, int
 
 template <typename T>
 int64_t posv_mixed(HermitianMatrix<T>& A, Matrix<T>& B, Matrix<T>& X, int& iter, Options const& opts) {
+    {
+        int64_t info = 0;
+        if (internal::spread<T>(opts, {{&A, true}, {&B, false}, {&X, true}}, [&](std::vector<Matrix<T>>& M, int r) {
+                auto H = internal::rewrap(A, M[0]);
+                int it = 0;
+                const int64_t i = posv_mixed(H, M[1], M[2], it, opts);
+                if (r == 0) { info = i; iter = it; }
+            }))
+            return info;
+    }
     trace::Block tb("posv_mixed");
     internal::DriverScope ds_;
     using Lo = typename lower_prec<T>::type;

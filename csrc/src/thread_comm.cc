@@ -54,7 +54,12 @@ struct Hub {
     int arrived = 0;
     bool aborted = false;
     struct Slot { const void* ptr = nullptr; hipEvent_t ev = nullptr; };
-    std::vector<Slot> a, b;          // phase A: data ready; phase B: reads done
+    // phase A: data ready; phase B: reads done; phase C: the sliced
+    // all-reduce's last hand-off.  C is written by no collective before its
+    // first barrier, so a fast rank that has already entered the next
+    // collective (and rewritten its A slot) cannot clobber the event a slow
+    // rank still has to read after barrier (3) of allreduce_sliced.
+    std::vector<Slot> a, b, c;
     struct Msg {
         const void* ptr;
         size_t bytes;
@@ -64,7 +69,7 @@ struct Hub {
     };
     std::map<std::pair<int, int>, std::deque<std::shared_ptr<Msg>>> box;   // (src, dst) FIFO
 
-    Hub(int n_, bool d) : n(n_), dev(d), a(n_), b(n_) {}
+    Hub(int n_, bool d) : n(n_), dev(d), a(n_), b(n_), c(n_) {}
 
     void check() {
         if (aborted) throw CommException("in-process communicator aborted (another rank failed)", __func__,
@@ -87,6 +92,14 @@ struct Hub {
         std::lock_guard<std::mutex> l(m);
         aborted = true;
         cv.notify_all();
+    }
+    /// back to a clean state after an aborted run (every rank thread joined):
+    /// persistent in-process groups reuse their communicators
+    void reset() {
+        std::lock_guard<std::mutex> l(m);
+        aborted = false;
+        arrived = 0;
+        box.clear();
     }
 };
 
@@ -127,6 +140,7 @@ public:
     std::string name() const override { return "inproc"; }
     bool device_native() const override { return hub_->dev; }
     void abort() { hub_->abort(); }
+    void reset() { hub_->reset(); }
 
     void bcast_raw(void* buf, size_t count, ScalarType t, int root, hipStream_t s) override {
         const size_t bytes = count * scalar_size(t);
@@ -240,10 +254,10 @@ public:
                                  s);
         hipEvent_t my_b = h.b[me_].ev;
         hipEvent_t mine = record(s);
-        h.a[me_] = {nullptr, mine};
+        h.c[me_] = {nullptr, mine};
         h.barrier();                                             // (3) every copy of the slices issued
         destroy(my_b);
-        for (int r = 0; r < n; ++r) if (r != me_) wait_on(s, h.a[r].ev);
+        for (int r = 0; r < n; ++r) if (r != me_) wait_on(s, h.c[r].ev);
         device::free_async(tmp, s);                              // after the others read my slice
         pend_b_ = mine;
     }
@@ -440,6 +454,11 @@ std::vector<GridPtr> make_thread_grids(int p, int q, GridOrder order, std::vecto
 void thread_grid_abort(Grid const& g) {
     for (CommPtr c : {g.world_ptr(), g.row_ptr(), g.col_ptr(), g.row_fast_ptr(), g.col_fast_ptr()})
         if (c) thread_comm_abort(*c);
+}
+
+void thread_grid_reset(Grid const& g) {
+    for (CommPtr c : {g.world_ptr(), g.row_ptr(), g.col_ptr(), g.row_fast_ptr(), g.col_fast_ptr()})
+        if (auto* t = c ? dynamic_cast<ThreadComm*>(c.get()) : nullptr) t->reset();
 }
 
 }  // namespace slate

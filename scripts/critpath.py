@@ -67,6 +67,10 @@ n, nb, p, q = a.n, a.nb, a.p, a.q
 nt = n // nb
 g = torch.Generator(device=dev).manual_seed(0)
 ops.set_queue(1)   # chain tasks on the panel queue, as in the drivers
+# torch's own work (operand copies) on a non-blocking stream: with CU-masked
+# queues (SLATE_PANEL_CUS, created blocking) any legacy-null-stream op would
+# be a device-wide barrier between the chain and the update
+torch.cuda.set_stream(torch.cuda.Stream())
 
 
 def rnd(rows, cols):
@@ -116,7 +120,15 @@ class Gemm:
 
 
 def measure(tasks, updates, cm):
-    """(per-task alone, chain alone, update alone, contended step), ms, best of reps."""
+    """(per-task alone, chain alone, update alone, contended step, contended
+    step with CU-free comm), ms, best of reps.
+
+    step    = the chain's kernels on the panel queue while the update runs,
+              plus the modelled messages added on top (messages on the CUs,
+              serialized with the chain: RCCL kernels);
+    step_ov = the same with the messages as host waits INSIDE the chain,
+              right before its lookahead task (a copy-engine transport,
+              SLATE_BCAST=peer: the bytes move while the update runs)."""
     alone = {}
     for t in tasks:
         best = math.inf
@@ -146,7 +158,28 @@ def measure(tasks, updates, cm):
             t.fn(*ar)
         ops.queue_sync(0)
         step = min(step, time.perf_counter() - t0)
-    return alone, sum(alone.values()) + cm, upd * 1e3, step * 1e3 + cm
+    step_ov = math.inf
+    # the messages land before the lookahead task (the last GEMM-like task)
+    la_at = min([i for i, t in enumerate(tasks) if t.name.startswith("la_")] or [len(tasks)])
+    for _ in range(a.reps):
+        args = [t.setup() for t in tasks]
+        sync_all()
+        t0 = time.perf_counter()
+        for u in updates:
+            u.launch(0)
+        for i, (t, ar) in enumerate(zip(tasks, args)):
+            if i == la_at and cm > 0:
+                t1 = time.perf_counter()
+                while time.perf_counter() - t1 < cm * 1e-3:
+                    pass
+            t.fn(*ar)
+        if la_at >= len(tasks) and cm > 0:
+            t1 = time.perf_counter()
+            while time.perf_counter() - t1 < cm * 1e-3:
+                pass
+        ops.queue_sync(0)
+        step_ov = min(step_ov, time.perf_counter() - t0)
+    return alone, sum(alone.values()) + cm, upd * 1e3, step * 1e3 + cm, step_ov * 1e3
 
 
 def host_wait_task():
@@ -177,18 +210,24 @@ def report(name, rows):
     print(f"\n== {name}: n={n} nb={nb} grid {p}x{q} la={a.la}; comm model {a.lat_us:.0f} us + bytes/{a.bw_gbs:.0f} GB/s")
     hdr = "   k     mr  nc_trail | " + " ".join(f"{c:>9s}" for c in rows[0]["parts"]) + \
         " |  comm_ms  chain_ms update_ms   step_ms  fits"
-    print(hdr)
+    print(hdr + "   step_ov")
     for r in rows:
         parts = " ".join(f"{v:9.3f}" for v in r["parts"].values())
         print(f"{r['k']:4d} {r['mr']:6d} {r['nc']:8d} | {parts} | {r['comm']:8.3f} {r['chain']:9.3f} "
-              f"{r['update']:9.3f} {r['step']:9.3f}  {'yes' if r['chain'] <= r['update'] else 'NO'}")
+              f"{r['update']:9.3f} {r['step']:9.3f}  {'yes' if r['chain'] <= r['update'] else 'NO '} "
+              f"{r['step_ov']:9.3f}")
     fits = sum(1 for r in rows if r["chain"] <= r["update"])
-    tc, tu, ts = (sum(r[x] for r in rows) for x in ("chain", "update", "step"))
-    pred = ts * a.every
+    tc, tu, ts, to = (sum(r[x] for r in rows) for x in ("chain", "update", "step", "step_ov"))
+    tmax = sum(max(r["chain"], r["update"]) for r in rows)
     print(f"   steps whose chain <= update: {fits}/{len(rows)} ({100.0 * fits / len(rows):.0f}%); "
-          f"sampled sums: chain {tc:.1f} ms, update {tu:.1f} ms, contended step {ts:.1f} ms")
-    print(f"   predicted: sum_k step x {a.every} = {pred:.0f} ms -> {lawn41(name) / (pred * 1e-3) / 1e12:.1f} "
-          f"TFLOP/s whole node ({p}x{q})")
+          f"sampled sums: chain {tc:.1f} ms, update {tu:.1f} ms, contended step {ts:.1f} ms, "
+          f"with CU-free comm {to:.1f} ms; sum max(chain, update) {tmax:.1f} ms -> "
+          f"contended / max = {ts / tmax:.2f} (CU-free comm {to / tmax:.2f})")
+    for lab, t in (("messages on the CUs", ts), ("CU-free messages (peer copies)", to)):
+        pred = t * a.every
+        print(f"   predicted ({lab}): sum_k step x {a.every} = {pred:.0f} ms -> "
+              f"{lawn41(name) / (pred * 1e-3) / 1e12:.1f} TFLOP/s whole node ({p}x{q}, panel CUs "
+              f"{os.environ.get('SLATE_PANEL_CUS', '0')})")
     sys.stdout.flush()
 
 
@@ -219,8 +258,8 @@ if "lu" in todo:
             c += lv * comm(nb * nb * 8 + nb * 8, 2) + comm(nb * nb * 8, 2) + comm(2 * nb * nb * 8)
         if q > 1:
             c += comm(nb * nb * 8 + 6 * nb * 8, 2) + comm(mr * nb * 8)
-        alone, chain, upd, step = measure(tasks, [Gemm(mr - nb, nc, nb)] if nc > 0 else [], c)
-        rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step))
+        alone, chain, upd, step, step_ov = measure(tasks, [Gemm(mr - nb, nc, nb)] if nc > 0 else [], c)
+        rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step, step_ov=step_ov))
         del W, L21
     report("getrf_tntpiv", rows)
 
@@ -248,8 +287,8 @@ if "qr" in todo:
         if q > 1:
             c += comm(nb * nb * 8) + comm(mr * nb * 8)
         upds = [Gemm(nb, nc, mr, ta="T"), Gemm(mr, nc, nb)] if nc > 0 else []
-        alone, chain, upd, step = measure(tasks, upds, c)
-        rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step))
+        alone, chain, upd, step, step_ov = measure(tasks, upds, c)
+        rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step, step_ov=step_ov))
         del Q
     report("geqrf (CholeskyQR2 + reconstruction panel)", rows)
 
@@ -285,8 +324,8 @@ if "chol" in todo:
         if p > 1:
             c += comm(math.ceil(nc / nb) * nb * nb * 8 / max(q, 1))  # transposed tiles
         ncs = int(nc * stair_fraction(k)) // nb * nb if nc > 0 else 0
-        alone, chain, upd, step = measure(tasks, [Gemm(mr - nb, ncs, nb)] if ncs > 0 else [], c)
-        rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step))
+        alone, chain, upd, step, step_ov = measure(tasks, [Gemm(mr - nb, ncs, nb)] if ncs > 0 else [], c)
+        rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step, step_ov=step_ov))
     report("potrf", rows)
 
 if "gemm" in todo:

@@ -21,7 +21,7 @@ from ._core import (Target, Op, Uplo, Diag, Side, Norm, GridOrder, Layout, Equed
                     Matrix, HermitianMatrix, SymmetricMatrix, TriangularMatrix, TrapezoidMatrix,
                     BandMatrix, TriangularBandMatrix, HermitianBandMatrix, general, band_matrix,
                     hermitian_band_matrix,
-                    from_numpy, to_numpy, matrix_layout, empty_like, local_tensor, transpose, conj_transpose,
+                    from_numpy, to_numpy, multi_device, to_multi_device, from_devices, matrix_layout, empty_like, local_tensor, transpose, conj_transpose,
                     version, suffix_of, dtype_of, opts, target_of)
 from .parallel import init_grid, choose_grid, TorchHostComm, current_grid, finalize  # noqa: F401
 from .models import *  # noqa: F401,F403

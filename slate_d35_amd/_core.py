@@ -169,6 +169,40 @@ def matrix_layout(m, n, tile_mb, tile_nb, tile_rank, dtype=np.float64, grid=None
     return A
 
 
+def multi_device(m, n, nb=256, dtype=np.float64, num_devices=0, mb=None):
+    """New multi-device matrix: 2-D block-cyclic over num_devices in-process
+    ranks of this process (0: every GPU it may use; 8 GPUs -> 2 x 4), storage
+    on the devices.  Drivers called with it run on those GPUs in place
+    (reference: one MPI rank spreads its tiles over all of its GPUs,
+    MatrixStorage.hh:503-506)."""
+    cls = getattr(_slate, "Matrix_" + _SUFFIX[np.dtype(dtype)])
+    return cls.multiDevice(m, n, mb or nb, nb, num_devices)
+
+
+def to_multi_device(full: np.ndarray, nb=256, num_devices=0, dtype=None):
+    """Copy a numpy array into a new multi-device matrix (one scatter)."""
+    full = np.asarray(full)
+    if dtype is None:
+        dtype = full.dtype if full.dtype in _SUFFIX else np.float64
+    full = np.asfortranarray(full.astype(dtype, copy=False))
+    if full.ndim == 1:
+        full = full.reshape(-1, 1)
+    m, n = full.shape
+    src = Matrix(m, n, nb, dtype, _slate.Grid.self())
+    src.insertLocalTiles(Target.Host)
+    src.set_local(full)
+    A = multi_device(m, n, nb, dtype, num_devices)
+    native("copy", A)(src, A, opts())
+    return A
+
+
+def from_devices(m, n, ptrs, lda, nb, dtype=np.float64, mb=None):
+    """Reference fromDevices(m, n, Aarray, num_devices, lda, mb, nb): one
+    device pointer per GPU, tile column j on device j % len(ptrs)."""
+    cls = getattr(_slate, "Matrix_" + _SUFFIX[np.dtype(dtype)])
+    return cls.fromDevicesArray(m, n, [int(p) for p in ptrs], lda, mb or nb, nb)
+
+
 def to_numpy(A) -> np.ndarray:
     """Gather a distributed matrix (logical view) to a full numpy array on every rank."""
     return A.gather()

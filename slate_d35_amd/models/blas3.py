@@ -103,6 +103,12 @@ def hbmm(side, alpha, A, B, beta, C, target=None, **kw):
     call("hbmm", A, side, alpha, A, B, beta, C, target=target, **kw)
 
 
-def tbsm(side, alpha, A, B, target=None, **kw):
-    """Solve op(A) X = alpha B with A a TriangularBandMatrix (src/tbsm.cc)."""
+def tbsm(side, alpha, A, B, target=None, pivots=None, **kw):
+    """Solve op(A) X = alpha B with A a TriangularBandMatrix (src/tbsm.cc).
+    pivots (per tile: [(tile offset, row offset), ...], as gbtrf / getrf
+    return them): the row interchanges of tile k are applied to B(k:, :)
+    before tile k's solve on a forward sweep, after it on a backward sweep
+    (reference src/tbsmPivots.cc)."""
+    if pivots is not None:
+        return call("tbsm_pivots", A, side, alpha, A, [list(map(tuple, p)) for p in pivots], B, target=target, **kw)
     call("tbsm", A, side, alpha, A, B, target=target, **kw)

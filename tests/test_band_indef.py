@@ -72,6 +72,72 @@ def test_gbmm_hbmm_tbsm(dt):
     assert relerr(t @ s.to_numpy(X), b) < tol(dt)
 
 
+def _tbsm_pivots_ref(t, b, piv, nb, lower, alpha):
+    """numpy rendering of the reference's pivoted band solve
+    (src/tbsmPivots.cc): forward sweep (lower) swapping tile k's rows before
+    its solve, backward sweep (upper) swapping after it."""
+    n = t.shape[0]
+    x = alpha * b.copy()
+    nt = -(-n // nb)
+
+    def swap(k, forward):
+        seq = [(k * nb + i, (k + ti) * nb + off) for i, (ti, off) in enumerate(piv[k])]
+        for r, p in (seq if forward else reversed(seq)):
+            x[[r, p]] = x[[p, r]]
+
+    ks = range(nt) if lower else range(nt - 1, -1, -1)
+    for k in ks:
+        r0, r1 = k * nb, min(n, (k + 1) * nb)
+        if lower:
+            swap(k, True)
+            x[r0:r1] = np.linalg.solve(t[r0:r1, r0:r1], x[r0:r1])
+            x[r1:] -= t[r1:, r0:r1] @ x[r0:r1]
+        else:
+            x[r0:r1] -= t[r0:r1, r1:] @ x[r1:]
+            x[r0:r1] = np.linalg.solve(t[r0:r1, r0:r1], x[r0:r1])
+            swap(k, False)
+    return x
+
+
+@pytest.mark.parametrize("dt", [np.float64, np.complex128])
+@pytest.mark.parametrize("lower,side", [(True, "L"), (False, "L"), (True, "R")])
+def test_tbsm_pivots(dt, lower, side):
+    """tbsm(side, alpha, A, pivots, B) against a numpy rendering of the
+    reference's sweep (interchanges of tile k inside the band reach)."""
+    n, nb, kd = 100, 16, 9
+    r = np.random.default_rng(31)
+    a = rnd(n, n, dt, 11)
+    t = (np.tril(band(a, kd, 0)) if lower else np.triu(band(a, 0, kd))) + 4 * np.eye(n)
+    nt = -(-n // nb)
+    piv = []
+    for k in range(nt):
+        pk = []
+        for i in range(min(nb, n - k * nb)):
+            row = k * nb + i
+            p = int(r.integers(row, min(n, row + kd + 1)))
+            pk.append((p // nb - k, p % nb))
+        piv.append(pk)
+    b = rnd(n, 5, dt, 12) if side == "L" else rnd(5, n, dt, 12)
+    T = s.TriangularBandMatrix(s.Uplo.Lower if lower else s.Uplo.Upper, s.Diag.NonUnit, kd,
+                               s.from_numpy(t, nb=nb))
+    X = s.from_numpy(b, nb=nb)
+    alpha = 0.5
+    s.tbsm(s.Side.Left if side == "L" else s.Side.Right, alpha, T, X, pivots=piv)
+    if side == "L":
+        ref = _tbsm_pivots_ref(t, b, piv, nb, lower, alpha)
+    else:
+        # X A = alpha B  <=>  A^H X^H = alpha' B^H: the same pivoted sweep on the
+        # transposed system (A^H upper for lower A: backward sweep)
+        tt = t.conj().T
+        ref = _tbsm_pivots_ref(tt, b.conj().T, piv, nb, not lower, np.conj(alpha)).conj().T
+    assert relerr(s.to_numpy(X), ref) < tol(dt)
+    # empty pivots: plain tbsm
+    X2 = s.from_numpy(b, nb=nb)
+    if side == "L":
+        s.tbsm(s.Side.Left, alpha, T, X2, pivots=[])
+        assert relerr(t @ s.to_numpy(X2), alpha * b) < tol(dt)
+
+
 @pytest.mark.parametrize("dt", DTYPES)
 @pytest.mark.parametrize("uplo", ["L", "U"])
 def test_hesv(dt, uplo):

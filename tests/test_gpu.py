@@ -825,9 +825,64 @@ print("INPROC_OK")
     assert r.returncode == 0 and "INPROC_OK" in r.stdout, r.stdout[-2000:] + r.stderr[-3000:]
 
 
-@pytest.mark.parametrize("nranks,count", [(3, 1000), (4, 300000), (5, 1 << 20), (2, 300000)])
-def test_inproc_allreduce_device(nranks, count):
+@pytest.mark.parametrize("nranks,count,rounds", [(3, 1000, 1), (4, 300000, 1), (5, 1 << 20, 1), (2, 300000, 1),
+                                                  (4, 1 << 18, 12), (3, 3000, 8)])
+def test_inproc_allreduce_device(nranks, count, rounds):
     """In-process all-reduce on device buffers: the all-to-all copy path for
     small messages and the reduce-scatter + all-gather path (>= 1 MiB, more
-    than two ranks; uneven slices for 5 ranks)."""
-    assert s._slate.inproc_allreduce_check(nranks, count) < 1e-12
+    than two ranks; uneven slices for 5 ranks).  rounds > 1: back-to-back
+    all-reduce / bcast / all-reduce with skewed ranks (a fast rank enters the
+    next collective while a slow one finishes the sliced hand-off)."""
+    assert s._slate.inproc_allreduce_check(nranks, count, rounds) < 1e-12
+
+
+# ---- multi-device matrices on the device (test_multi_device.py runs them in
+# host mode on the CPU): the parts live in each in-process rank's device
+# context -- four ranks on this box's one GPU -- and the drivers run on them
+# in place (no scatter / gather per call, pinned by inproc_copy_bytes).
+def test_multi_device_lu_on_device():
+    import test_multi_device as md
+    md.test_lu_factor_then_solve_twice_no_copies(np.float64)
+
+
+def test_multi_device_cholesky_blas_on_device():
+    import test_multi_device as md
+    md.test_cholesky_and_trsm_herk_gemm()
+
+
+def test_multi_device_qr_on_device():
+    import test_multi_device as md
+    md.test_qr_least_squares_and_unmqr()
+
+
+def test_multi_device_mixed_eig_on_device():
+    import test_multi_device as md
+    md.test_mixed_precision_and_eig_svd()
+
+
+def test_multi_device_layout_on_device():
+    import test_multi_device as md
+    md.test_multi_device_layout_and_gather()
+    A = s.multi_device(300, 300, 64, np.float64, 4)
+    assert A.is_multi_device and A.num_parts == 4
+
+
+def test_from_devices_device_arrays():
+    """fromDevices(Aarray, num_devices) over device arrays (torch tensors on
+    this GPU standing in for per-GPU arrays: 1 x 3 in-process ranks)."""
+    torch = _torch()
+    m, n, nb, nd = 200, 170, 32, 3
+    a = np.random.default_rng(3).standard_normal((m, n))
+    nt = -(-n // nb)
+    cols = [[j for j in range(nt) if j % nd == d] for d in range(nd)]
+    idx = [np.concatenate([np.arange(j * nb, min(n, (j + 1) * nb)) for j in c]) for c in cols]
+    if torch.cuda.device_count() >= nd:
+        pytest.skip("one-GPU layout check (several GPUs: device d must hold array d)")
+    ts = [torch.tensor(np.ascontiguousarray(a[:, ix].T), device="cuda") for ix in idx]   # column-major m x k
+    torch.cuda.synchronize()
+    A = s.from_devices(m, n, [t.data_ptr() for t in ts], m, nb)
+    assert A.is_multi_device and A.num_parts == nd
+    assert np.array_equal(s.to_numpy(A), a)
+    s.scale(2.0, 1.0, A)                         # in place, in the caller's arrays
+    torch.cuda.synchronize()
+    assert np.array_equal(ts[1].cpu().numpy().T, 2 * a[:, idx[1]])

@@ -88,3 +88,4 @@ def test_inproc_allreduce_host():
     if s.device_available():
         pytest.skip("host-mode check")
     assert s._slate.inproc_allreduce_check(3, 5000) < 1e-12
+    assert s._slate.inproc_allreduce_check(4, 1 << 18, 6) < 1e-12
