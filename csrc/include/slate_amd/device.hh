@@ -95,6 +95,9 @@ void  free_async(void* ptr, hipStream_t s);
 size_t bytes_stream_cached();
 void* malloc_host(size_t bytes);   // pinned host memory
 void  free_host(void* ptr);
+/// Number of times blocks went back to HIP (hipFree) so far: caches keyed by
+/// device address (IPC handles) are stale once it changes.
+uint64_t alloc_epoch();
 /// Release all cached (unused) blocks back to HIP.
 void  release_cache();
 /// Bytes held in use / cached.

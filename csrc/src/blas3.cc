@@ -177,43 +177,72 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
         internal::finish_origin(C, opts);
         return;
     }
-    const int R = int(std::max<int64_t>(2, la + 2));
+    // Wide SUMMA steps: w consecutive k tiles are broadcast into one
+    // buffer per operand (one message per tile, each from its owner) and
+    // multiplied by ONE local GEMM with K = w nb.  A K = 512 GEMM runs ~11 %
+    // below the long-K rate (profiles/r5_critpath_2x4.txt: 63.2 vs 70.9
+    // TFLOP/s); with 288 GB per GPU the wider panels cost nothing that
+    // matters.  $SLATE_SUMMA_K = target K per step (default 2048; <= nb: one
+    // tile per step, the classic SUMMA).
+    const int64_t summa_k = [] {
+        const char* e = std::getenv("SLATE_SUMMA_K");
+        return e ? std::max<int64_t>(1, std::atoll(e)) : int64_t(2048);
+    }();
     int64_t kbmax = 0;
     for (int64_t k = 0; k < kt; ++k) kbmax = std::max(kbmax, A.tileNb(k));
-    std::vector<Work<T>> WA(R), WB(R);
+    const int64_t w = std::max<int64_t>(1, std::min<int64_t>(kt, summa_k / std::max<int64_t>(kbmax, 1)));
+    const int R = int(std::max<int64_t>(2, la + 2));
+    const int64_t kw = w * kbmax;                       // widest K of a step
+    std::vector<Work<T>> WA(R), WB(R), WS(R);
     for (int r = 0; r < R; ++r) {
-        if (q > 1) WA[r].resize(target, size_t(std::max<int64_t>(lc.m, 1)) * kbmax);
-        if (p > 1) WB[r].resize(target, size_t(kbmax) * std::max<int64_t>(lc.n, 1));
+        if (q > 1) WA[r].resize(target, size_t(std::max<int64_t>(lc.m, 1)) * kw);
+        if (p > 1) WB[r].resize(target, size_t(kw) * std::max<int64_t>(lc.n, 1));
+        if (p > 1 && w > 1) WS[r].resize(target, size_t(kbmax) * std::max<int64_t>(lc.n, 1));
     }
-    for (int64_t k = 0; k < kt; ++k) {
-        const int slot = int(k % R);
-        const int64_t kb = A.tileNb(k);
-        const int qa = A.scol_owner(k), pb = B.srow_owner(k);
+    const int64_t nsteps = (kt + w - 1) / w;
+    for (int64_t st = 0; st < nsteps; ++st) {
+        const int slot = int(st % R);
+        const int64_t k0 = st * w, k1 = std::min(kt, k0 + w);   // tiles [k0, k1)
+        int64_t K = 0;
+        for (int64_t k = k0; k < k1; ++k) K += A.tileNb(k);
         T* pa = (q > 1) ? WA[slot].data() : nullptr;
         T* pbuf = (p > 1) ? WB[slot].data() : nullptr;
-        int64_t ldwa = std::max<int64_t>(lc.m, 1), ldwb = kb;
+        const int64_t ldwa = std::max<int64_t>(lc.m, 1), ldwb = std::max<int64_t>(K, 1);
         T const* Ak = nullptr; int64_t ldak = 0;
         T const* Bk = nullptr; int64_t ldbk = 0;
-        if (q == 1) { Ak = la_.ptr + lcol_of(A, k) * la_.ld; ldak = la_.ld; }
+        // one process column (row): the step's tiles are adjacent local columns (rows)
+        if (q == 1) { Ak = la_.ptr + lcol_of(A, k0) * la_.ld; ldak = la_.ld; }
         else { Ak = pa; ldak = ldwa; }
-        if (p == 1) { Bk = lb_.ptr + lrow_of(B, k); ldbk = lb_.ld; }
+        if (p == 1) { Bk = lb_.ptr + lrow_of(B, k0); ldbk = lb_.ld; }
         else { Bk = pbuf; ldbk = ldwb; }
         const int64_t tBc = Sched::bcast(slot);
-        S.task(device::kCommQueue, {}, {tBc}, [&, k, kb, qa, pb, pa, pbuf, ldwa, ldwb](lb::Ctx const& c) {
+        S.task(device::kCommQueue, {}, {tBc}, [&, k0, k1, slot, pa, pbuf, ldwa, ldwb](lb::Ctx const& c) {
             trace::Block t2("gemm_bcast");
-            if (q > 1) {
-                if (mycol == qa) pack(c, lc.m, kb, la_.ptr + lcol_of(A, k) * la_.ld, la_.ld, pa);
-                bcast(g.row(), pa, size_t(lc.m * kb), qa, c);
-            }
-            if (p > 1) {
-                if (myrow == pb) lb::copy2d(c, kb, lc.n, lb_.ptr + lrow_of(B, k), lb_.ld, pbuf, ldwb);
-                bcast(g.col(), pbuf, size_t(kb * lc.n), pb, c);
+            int64_t off = 0;
+            for (int64_t k = k0; k < k1; ++k) {
+                const int64_t kb = A.tileNb(k);
+                if (q > 1) {
+                    const int qa = A.scol_owner(k);
+                    T* dst = pa + off * ldwa;
+                    if (mycol == qa) pack(c, lc.m, kb, la_.ptr + lcol_of(A, k) * la_.ld, la_.ld, dst);
+                    bcast(g.row(), dst, size_t(lc.m * kb), qa, c);
+                }
+                if (p > 1) {
+                    // B(k, :) travels packed (kb x n contiguous) and lands in
+                    // rows [off, off + kb) of the step's K x n operand
+                    const int pb = B.srow_owner(k);
+                    T* msg = (w == 1) ? pbuf : WS[slot].data();
+                    if (myrow == pb) lb::copy2d(c, kb, lc.n, lb_.ptr + lrow_of(B, k), lb_.ld, msg, kb);
+                    bcast(g.col(), msg, size_t(kb * lc.n), pb, c);
+                    if (w > 1) lb::copy2d(c, kb, lc.n, msg, kb, pbuf + off, ldwb);
+                }
+                off += kb;
             }
         });
-        T bk = (k == 0) ? beta : T(1);
-        S.task(0, {tBc}, {Sched::tok(9, 0)}, [&, Ak, ldak, Bk, ldbk, kb, bk](lb::Ctx const& c) {
+        T bk = (st == 0) ? beta : T(1);
+        S.task(0, {tBc}, {Sched::tok(9, 0)}, [&, Ak, ldak, Bk, ldbk, K, bk](lb::Ctx const& c) {
             trace::Block t2("gemm_update");
-            lb::gemm(c, Op::NoTrans, Op::NoTrans, lc.m, lc.n, kb, alpha, Ak, ldak, Bk, ldbk, bk, lc.ptr, lc.ld);
+            lb::gemm(c, Op::NoTrans, Op::NoTrans, lc.m, lc.n, K, alpha, Ak, ldak, Bk, ldbk, bk, lc.ptr, lc.ld);
         });
     }
     S.wait_all();

@@ -8,9 +8,17 @@
 #include <string>
 
 namespace slate {
+
+bool multi_process_job();   // inproc.cc: a launcher started one process per GPU
+
 namespace device {
 
 namespace {
+
+// bumped whenever a block goes back to HIP (hipFree): address-keyed caches
+// of other subsystems (IPC handles of the peer broadcast) use it to notice
+// that an address may now name a different allocation
+std::atomic<uint64_t> g_free_epoch{0};
 
 struct State {
     std::mutex mtx;
@@ -131,7 +139,13 @@ void ensure_streams_locked(State& s) {
         int x = 0;
         if (hipDeviceGetAttribute(&x, hipDeviceAttributeNumberOfXccs, s.device) == hipSuccess && x > 0) nxcc = x;
     }
-    int reserve = 0;
+    // default: 32 CUs (one per shader engine, so the SE-balanced dispatcher
+    // loses exactly 1/8) for one-process-per-GPU jobs, whose p x q panel
+    // chains are longer than their trailing updates; 0 on one GPU, where the
+    // update dominates (profiles/r6_cu_mask_bench_ab.txt: -9 %), and for
+    // in-process ranks.  The 2 x 4 critical-path model:
+    // profiles/r6_critpath_2x4_cus_nonblocking.txt.
+    int reserve = multi_process_job() ? 32 : 0;
     if (const char* e = std::getenv("SLATE_PANEL_CUS")) reserve = std::atoi(e);
     if (ncu < 64) reserve = 0;
     reserve = std::max(0, std::min(reserve, ncu / 2));
@@ -229,6 +243,7 @@ void context_destroy(Context* ctx) {
         reclaim_locked(*ctx, true);
         flush_stream_free_locked(*ctx);
         for (auto& kv : ctx->free_blocks) (void)hipFree(kv.second);
+        ++g_free_epoch;
         ctx->free_blocks.clear();
         ctx->cached = 0;
         for (auto e : ctx->events) (void)hipEventDestroy(e);
@@ -264,6 +279,7 @@ int count() {
 }
 
 namespace { std::atomic<bool> g_explicit_device{false}; }
+uint64_t alloc_epoch() { return g_free_epoch.load(); }
 bool device_explicit() { return g_explicit_device.load(); }
 
 void set_device(int dev) {
@@ -340,6 +356,7 @@ void* malloc_locked(State& s, size_t b) {
             reclaim_locked(s, true);
             flush_stream_free_locked(s);
             for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
+            ++g_free_epoch;
             s.free_blocks.clear();
             s.cached = 0;
             slate_hip_call(hipMalloc(&p, b));
@@ -396,6 +413,7 @@ void release_destroyed(State& s, void* ptr, std::unique_lock<std::mutex>& g) {
     (void)hipSetDevice(s.device);
     (void)hipDeviceSynchronize();
     (void)hipFree(ptr);
+    ++g_free_epoch;
     if (cur >= 0) (void)hipSetDevice(cur);
     const bool last = s.live.empty();
     g.unlock();
@@ -466,6 +484,7 @@ void release_cache() {
     reclaim_locked(s, true);
     flush_stream_free_locked(s);
     for (auto& kv : s.free_blocks) (void)hipFree(kv.second);
+            ++g_free_epoch;
     s.free_blocks.clear();
     s.cached = 0;
 }

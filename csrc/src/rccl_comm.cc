@@ -5,10 +5,21 @@
 
 #include <rccl/rccl.h>
 #include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <cstdio>
 #include <cstring>
 #include <cstdlib>
+#include <map>
+#include <memory>
 #include <mutex>
+#include <string>
+#include <thread>
 #include <vector>
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <unistd.h>
 
 #define slate_nccl_call(call) do {                                            \
     ncclResult_t _r = (call);                                                 \
@@ -54,6 +65,207 @@ std::vector<ncclComm_t>& registry() {
 }
 bool g_aborted = false;
 
+//------------------------------------------------------------------------------
+/// Copy-engine broadcast between the processes of one node (SLATE_BCAST=peer;
+/// SURVEY §5.8, reference listBcast, include/slate/BaseMatrix.hh:2129-2212):
+/// the root's buffer is exported once per allocation (hipIpcGetMemHandle),
+/// every receiver PULLS the bytes with one hipMemcpyAsync from the mapped
+/// root buffer on its own stream -- an SDMA copy over xGMI, no kernel on the
+/// CUs the trailing GEMM is using -- ordered by interprocess events:
+///   root:     record ready[seq % K] on its stream, publish (handle, offset,
+///             bytes) and seq in the shared control block, wait (host) until
+///             every receiver has issued its copy, then make its stream wait
+///             on the receivers' done events (the buffer may be rewritten
+///             after that, as after an ncclBroadcast);
+///   receiver: wait (host) for the root's seq, stream-wait on ready[seq % K],
+///             copy, record done[seq % K], publish seq.
+/// The host hand-off is a rendezvous of the communicator's ranks per
+/// broadcast (collective order is the same on every rank, as for RCCL); the
+/// control block is a POSIX shared-memory segment named once by rank 0 (one
+/// ncclBroadcast of the name at setup).  Event slots are reused after K
+/// broadcasts: by then every rank has issued its waits on the slot (the root
+/// returns from broadcast #seq only after every receiver arrived).
+class PeerBcast {
+public:
+    static constexpr int kMaxRanks = 64, kRing = 16;
+    struct alignas(64) Slot {
+        std::atomic<uint64_t> ready_seq;   // root: broadcast #seq published
+        std::atomic<uint64_t> done_seq;    // receiver: copy of #seq issued
+        std::atomic<int> inited;
+        hipIpcMemHandle_t mem;
+        uint64_t off, bytes;
+        hipIpcEventHandle_t ready_ev[kRing], done_ev[kRing];
+    };
+    struct Block { Slot r[kMaxRanks]; };
+
+    /// Collective set-up over `comm`; ok() is false on every rank when any
+    /// rank could not map the control block, export / import interprocess
+    /// events or open a peer's memory handle (the communicator then keeps
+    /// ncclBroadcast) -- the ranks agree through one all-reduce.
+    PeerBcast(ncclComm_t comm, int rank, int size) : rank_(rank), size_(size) {
+        hipStream_t st = device::queue(device::kCommQueue);
+        auto allmin = [&](int v) {
+            device::Buffer<int> d(1);
+            device::memcpy_async(d.data(), &v, sizeof v, st);
+            slate_nccl_call(ncclAllReduce(d.data(), d.data(), 1, ncclInt32, ncclMin, comm, st));
+            device::memcpy_async(&v, d.data(), sizeof v, st);
+            slate_hip_call(hipStreamSynchronize(st));
+            return v;
+        };
+        // rank 0 names and creates the segment, the others learn the name
+        char name[64] = {};
+        if (rank == 0) {
+            static std::atomic<int> counter{0};
+            std::snprintf(name, sizeof name, "/slate_pb_%d_%d", int(getpid()), counter++);
+            int fd = shm_open(name, O_CREAT | O_EXCL | O_RDWR, 0600);
+            if (fd < 0 || ftruncate(fd, sizeof(Block)) != 0) name[0] = 0;
+            if (fd >= 0) close(fd);
+        }
+        {
+            device::Buffer<char> d(sizeof name);
+            device::memcpy_async(d.data(), name, sizeof name, st);
+            slate_nccl_call(ncclBroadcast(d.data(), d.data(), sizeof name, ncclInt8, 0, comm, st));
+            device::memcpy_async(name, d.data(), sizeof name, st);
+            slate_hip_call(hipStreamSynchronize(st));
+        }
+        int ok = size <= kMaxRanks && name[0] != 0;
+        if (ok) {
+            int fd = shm_open(name, O_RDWR, 0600);
+            void* p = fd >= 0 ? mmap(nullptr, sizeof(Block), PROT_READ | PROT_WRITE, MAP_SHARED, fd, 0) : MAP_FAILED;
+            if (fd >= 0) close(fd);
+            if (p == MAP_FAILED) ok = 0;
+            else blk_ = static_cast<Block*>(p);
+        }
+        // probe buffer: every rank exports one, every rank opens the others'
+        device::Buffer<char> probe(256);
+        if (ok) {
+            try {
+                Slot& me = blk_->r[rank_];
+                for (int i = 0; i < kRing; ++i) {
+                    slate_hip_call(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming | hipEventInterprocess));
+                    slate_hip_call(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming | hipEventInterprocess));
+                    slate_hip_call(hipIpcGetEventHandle(&me.ready_ev[i], ready_[i]));
+                    slate_hip_call(hipIpcGetEventHandle(&me.done_ev[i], done_[i]));
+                }
+                me.mem = export_handle(probe.data());
+                me.inited.store(1, std::memory_order_release);
+            } catch (std::exception const&) { ok = 0; }
+        }
+        ok = allmin(ok);
+        if (ok) {
+            try {
+                for (int r = 0; r < size_; ++r) {
+                    spin([&] { return blk_->r[r].inited.load(std::memory_order_acquire) != 0; });
+                    if (r == rank_) continue;
+                    (void)imported(r, 0, true);
+                    (void)imported(r, 0, false);
+                    (void)open_handle(blk_->r[r].mem);
+                }
+            } catch (std::exception const&) { ok = 0; }
+            ok = allmin(ok);   // also: every rank mapped the segment, the name can go
+        }
+        if (rank == 0 && name[0]) shm_unlink(name);
+        ok_ = ok != 0;
+        if (ok_ && rank == 0 && std::getenv("SLATE_BCAST_VERBOSE"))
+            std::fprintf(stderr, "slate: SLATE_BCAST=peer active on a communicator of %d ranks\n", size);
+        if (!ok_ && rank == 0) {
+            static std::once_flag warned;
+            std::call_once(warned, [] {
+                std::fprintf(stderr, "slate: SLATE_BCAST=peer unavailable (interprocess memory / events); "
+                                     "using ncclBroadcast\n");
+            });
+        }
+    }
+    bool ok() const { return ok_; }
+    ~PeerBcast() {
+        // at interpreter exit the HIP runtime may be gone: release what is safe
+        if (blk_) munmap(blk_, sizeof(Block));
+    }
+
+    void bcast(void* buf, size_t bytes, int root, hipStream_t s) {
+        const uint64_t seq = ++seq_;
+        const int slot = int(seq % kRing);
+        Block& B = *blk_;
+        if (rank_ == root) {
+            Slot& me = B.r[rank_];
+            char* base = nullptr;
+            size_t size = 0;
+            slate_hip_call(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t*>(&base), &size, buf));
+            me.mem = export_handle(base);
+            me.off = uint64_t(static_cast<char*>(buf) - base);
+            me.bytes = bytes;
+            slate_hip_call(hipEventRecord(ready_[slot], s));
+            me.ready_seq.store(seq, std::memory_order_release);
+            for (int r = 0; r < size_; ++r) {
+                if (r == root) continue;
+                spin([&] { return B.r[r].done_seq.load(std::memory_order_acquire) >= seq; });
+                slate_hip_call(hipStreamWaitEvent(s, imported(r, slot, false), 0));
+            }
+            return;
+        }
+        Slot& rs = B.r[root];
+        spin([&] { return rs.ready_seq.load(std::memory_order_acquire) >= seq; });
+        slate_error_if_msg(rs.bytes != bytes, "SLATE_BCAST=peer: message size mismatch");
+        char* src = static_cast<char*>(open_handle(rs.mem)) + rs.off;
+        slate_hip_call(hipStreamWaitEvent(s, imported(root, slot, true), 0));
+        slate_hip_call(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToDevice, s));
+        slate_hip_call(hipEventRecord(done_[slot], s));
+        B.r[rank_].done_seq.store(seq, std::memory_order_release);
+    }
+
+private:
+    template <typename F>
+    void spin(F&& ready) {
+        // a peer that never arrives is a hung job: fail loudly instead of spinning forever
+        const auto t0 = std::chrono::steady_clock::now();
+        for (int i = 0; !ready(); ++i) {
+            if (i > 64) std::this_thread::yield();
+            if ((i & 1023) == 1023 &&
+                std::chrono::steady_clock::now() - t0 > std::chrono::seconds(600))
+                throw CommException("SLATE_BCAST=peer: a peer did not arrive within 600 s", __func__, __FILE__,
+                                    __LINE__);
+        }
+    }
+    hipIpcMemHandle_t export_handle(char* base) {
+        const uint64_t ep = device::alloc_epoch();
+        if (ep != epoch_) { exported_.clear(); epoch_ = ep; }   // an address may name a new allocation
+        auto it = exported_.find(base);
+        if (it != exported_.end()) return it->second;
+        hipIpcMemHandle_t h;
+        slate_hip_call(hipIpcGetMemHandle(&h, base));
+        exported_[base] = h;
+        return h;
+    }
+    void* open_handle(hipIpcMemHandle_t const& h) {
+        std::string key(reinterpret_cast<char const*>(&h), sizeof h);
+        auto it = opened_.find(key);
+        if (it != opened_.end()) return it->second;
+        void* p = nullptr;
+        slate_hip_call(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
+        opened_[key] = p;
+        return p;
+    }
+    hipEvent_t imported(int r, int slot, bool ready) {
+        auto& m = ready ? imp_ready_ : imp_done_;
+        const int key = r * kRing + slot;
+        auto it = m.find(key);
+        if (it != m.end()) return it->second;
+        hipEvent_t e;
+        slate_hip_call(hipIpcOpenEventHandle(&e, ready ? blk_->r[r].ready_ev[slot] : blk_->r[r].done_ev[slot]));
+        m[key] = e;
+        return e;
+    }
+
+    int rank_, size_;
+    bool ok_ = false;
+    Block* blk_ = nullptr;
+    uint64_t seq_ = 0, epoch_ = 0;
+    hipEvent_t ready_[kRing] = {}, done_[kRing] = {};
+    std::map<char*, hipIpcMemHandle_t> exported_;
+    std::map<std::string, void*> opened_;
+    std::map<int, hipEvent_t> imp_ready_, imp_done_;
+};
+
 class RcclComm : public Comm {
 public:
     RcclComm(ncclComm_t c) : comm_(c) {
@@ -91,17 +303,22 @@ public:
     ///   sendrecv flat fan-out: the root sends to every peer in ONE group --
     ///            on the fully connected xGMI mesh each message has its own link
     ///   tree     binomial tree of grouped send / recv, log2(n) rounds
-    /// All three are stream-ordered RCCL operations (kernels on the CUs).  The
-    /// copy-engine path is the in-process transport (thread_comm.cc:
-    /// hipMemcpyAsync peer copies).
-    enum class BcastMode { Rccl, SendRecv, Tree };
+    ///   peer     copy-engine pull of the root's buffer (PeerBcast above):
+    ///            no kernel on the CUs; processes of one node
+    /// The first three are stream-ordered RCCL operations (kernels on the CUs).
+    enum class BcastMode { Rccl, SendRecv, Tree, Peer };
+    /// Default: peer (the panel broadcasts then take no CUs from the trailing
+    /// GEMM: profiles/r6_critpath_2x4_cus_nonblocking.txt, CU-free messages);
+    /// a communicator whose ranks cannot map each other's memory keeps
+    /// ncclBroadcast by itself (PeerBcast::ok).
     static BcastMode bcast_mode() {
         static const BcastMode m = [] {
             const char* e = std::getenv("SLATE_BCAST");
-            std::string v = e ? e : "rccl";
+            std::string v = e ? e : "peer";
             if (v == "sendrecv") return BcastMode::SendRecv;
             if (v == "tree") return BcastMode::Tree;
-            slate_error_if_msg(v != "rccl", "SLATE_BCAST must be rccl, sendrecv or tree");
+            if (v == "peer") return BcastMode::Peer;
+            slate_error_if_msg(v != "rccl", "SLATE_BCAST must be rccl, sendrecv, tree or peer");
             return BcastMode::Rccl;
         }();
         return m;
@@ -113,6 +330,14 @@ public:
         const size_t n = count * mult;
         if (size_ == 1 || n == 0) return;
         switch (bcast_mode()) {
+            case BcastMode::Peer:
+                if (!peer_) peer_ = std::make_unique<PeerBcast>(comm_, rank_, size_);
+                if (peer_->ok()) {
+                    peer_->bcast(buf, count * scalar_size(t), root, s);
+                    return;
+                }
+                slate_nccl_call(ncclBroadcast(buf, buf, n, dt, root, comm_, s));
+                return;
             case BcastMode::Rccl:
                 slate_nccl_call(ncclBroadcast(buf, buf, n, dt, root, comm_, s));
                 return;
@@ -175,6 +400,7 @@ public:
 private:
     ncclComm_t comm_ = nullptr;
     int rank_ = 0, size_ = 1;
+    std::unique_ptr<PeerBcast> peer_;
 };
 
 }  // namespace

@@ -24,7 +24,11 @@ for r in range(n):
     env = dict(env0, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1",
                MASTER_PORT=str(port), SLATE_MASTER_PORT=str(port), NCCL_HOSTID=f"slate-fake-host-{r}",
                NCCL_SOCKET_IFNAME="lo", NCCL_DEBUG=os.environ.get("NCCL_DEBUG", "WARN"), OMP_NUM_THREADS="2")
-    procs.append(subprocess.Popen(cmd, stdout=files[r], stderr=subprocess.STDOUT, text=True, env=env))
+    # RANK0_WRAP: a prefix for rank 0's command only, e.g. a profiler
+    # ("rocprofv3 --kernel-trace --memory-copy-trace -d DIR -o r0 --"): the
+    # profiled program is the tester itself, started from this launcher
+    wrap = os.environ.get("RANK0_WRAP", "").split() if r == 0 else []
+    procs.append(subprocess.Popen(wrap + cmd, stdout=files[r], stderr=subprocess.STDOUT, text=True, env=env))
 outs, codes = [], []
 try:
     for r, p in enumerate(procs):

@@ -32,6 +32,25 @@ def case_gemm(tg, dt, nb):
     assert relerr(s.to_numpy(C), 1.5 * a @ b - 0.5 * c) < tol(dt)
 
 
+def case_gemm_wide(tg, dt, nb):
+    """SUMMA steps of w tiles (SLATE_SUMMA_K): one tile per step, 2 tiles
+    (a short last step), all tiles in one step; tiles of the step come from
+    different process columns / rows."""
+    a, b, c = rnd(150, 7 * nb + 5, dt, 51), rnd(7 * nb + 5, 110, dt, 52), rnd(150, 110, dt, 53)
+    old = os.environ.get("SLATE_SUMMA_K")
+    try:
+        for kk in (1, 2 * nb, 3 * nb, 100 * nb):
+            os.environ["SLATE_SUMMA_K"] = str(kk)
+            A, B, C = (s.from_numpy(x, nb=nb, target=tg) for x in (a, b, c))
+            s.gemm(1.5, A, B, -0.5, C, target=tg, method_gemm="C")
+            assert relerr(s.to_numpy(C), 1.5 * a @ b - 0.5 * c) < tol(dt), kk
+    finally:
+        if old is None:
+            os.environ.pop("SLATE_SUMMA_K", None)
+        else:
+            os.environ["SLATE_SUMMA_K"] = old
+
+
 def case_herk(tg, dt, nb):
     a = rnd(130, 70, dt, 4)
     A = s.from_numpy(a, nb=nb, target=tg)

@@ -12,7 +12,7 @@ import pytest
 HERE = os.path.dirname(os.path.abspath(__file__))
 ROOT = os.path.dirname(HERE)
 WORKER = os.path.join(HERE, "dist_worker.py")
-CASES = "tile_comm,factor_objects,lanes,pplu_exact,rowx_bytes,solve_notemp,geqrf_cholqr,gelqf,band_storage,gemm,herk,rank2k,trsm,trmm,hemm,stationary,rbt,heev,stages,band,band_blas,layout,aasen,potrf,getrf,getrf_shapes,getrf_thresh,geqrf,geqrf_shapes,norm,norm_masked,mixed"
+CASES = "tile_comm,factor_objects,lanes,pplu_exact,rowx_bytes,solve_notemp,geqrf_cholqr,gelqf,band_storage,gemm,gemm_wide,herk,rank2k,trsm,trmm,hemm,stationary,rbt,heev,stages,band,band_blas,layout,aasen,potrf,getrf,getrf_shapes,getrf_thresh,geqrf,geqrf_shapes,norm,norm_masked,mixed"
 
 
 def _free_port():
@@ -143,14 +143,22 @@ def test_rccl_2x2_no_fast_lane():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode,nprocs,grid", [("sendrecv", 8, "2x4"), ("tree", 8, "2x4"), ("tree", 4, "2x2"),
-                                             ("sendrecv", 2, "2x1")])
+                                             ("sendrecv", 2, "2x1"), ("peer", 8, "2x4"), ("peer", 4, "2x2"),
+                                             ("peer", 2, "2x1")])
 def test_rccl_bcast_modes(mode, nprocs, grid):
     """SLATE_BCAST runtime broadcast transports over real RCCL (rccl_comm.cc):
-    flat send / recv fan-out and the binomial send / recv tree must give the
-    same LU / QR / Cholesky results as ncclBroadcast (tester residuals)."""
-    env = dict(os.environ, SLATE_BCAST=mode)
+    flat send / recv fan-out, the binomial send / recv tree and the
+    copy-engine peer pull (interprocess memory + events, no RCCL kernel) must
+    give the same LU / QR / Cholesky results as ncclBroadcast (tester
+    residuals)."""
+    import tempfile
+    logdir = tempfile.mkdtemp(prefix="bcast_")
+    env = dict(os.environ, SLATE_BCAST=mode, SLATE_BCAST_VERBOSE="1", RANK_LOGDIR=logdir)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "scripts", "rccl_multi.py"), str(nprocs),
                         "getrf,getrf_tntpiv,geqrf,potrf,gemm", "--type", "d", "--dim", "1536", "--nb", "128",
                         "--grid", grid, "--target", "d", "--lookahead", "2"],
                        capture_output=True, text=True, timeout=900, env=env)
     assert r.returncode == 0 and "all tests passed" in r.stdout, r.stdout[-5000:] + r.stderr[-2000:]
+    if mode == "peer":   # the copy-engine path really ran (no silent ncclBroadcast fallback)
+        logs = "".join(open(os.path.join(logdir, f)).read() for f in os.listdir(logdir))
+        assert "SLATE_BCAST=peer active" in logs and "peer unavailable" not in logs, logs[-3000:]
