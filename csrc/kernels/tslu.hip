@@ -527,8 +527,11 @@ __device__ long long g_tslu_probe[128];
 #define TSLU_S(k, sub) do {} while (0)
 #endif
 
-template <typename T, int R>
-__global__ __launch_bounds__(T2_NT) void tslu2_tree_kernel(Tslu2Args p, T* A) {
+// WPE: waves per SIMD the kernel is compiled for (register budget 512 / WPE
+// per lane); the fp32 R = 2 variant asks for 4 (<= 128 VGPRs), so its waves
+// can start beside the trailing fp32 GEMM's
+template <typename T, int R, int WPE = 1>
+__global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* A) {
     SLATE_PANEL_WAVE_PRIO();
     constexpr int NT = T2_NT, NW = NT / 64, S = NT * R, F = S / TW;
     constexpr bool kReal = !is_cplx<T>::value;
@@ -759,7 +762,11 @@ __global__ __launch_bounds__(T2_NT) void tslu2_tree_kernel(Tslu2Args p, T* A) {
         if (tid == 0) {
             const int g = item / F, ng = min(F, nl - g * F);
             int* c = &p.ctr[off + nl + g];
-            const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            // acq_rel at agent scope: the release publishes this workgroup's
+            // winners (stored above) before the count, the acquire makes the
+            // other workgroups' winners visible to the last arriver -- the
+            // HIP memory model's guarantee, not a gfx9 store-ordering detail
+            const int old = __hip_atomic_fetch_add(c, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
             const int last = old == ng - 1;
             if (last) __hip_atomic_store(c, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             s_flag = last;
@@ -926,10 +933,10 @@ static bool tslu_use_v2() {
     return std::is_same<T, double>::value;
 }
 
-template <typename T>
+template <typename T, int R = Tslu2Rows<T>::R, int WPE = 1>
 static void tslu2_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
                          int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
-    constexpr int R = Tslu2Rows<T>::R, S = T2_NT * R;
+    constexpr int S = T2_NT * R;
     const int64_t rows = m - r;
     Tslu2Args p;
     p.m = m; p.r = r; p.lda = lda; p.nn = nn;
@@ -946,7 +953,7 @@ static void tslu2_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64
     p.cand = p.ccnt + items + 1;
     p.slab = work + kT2Cnt + (items + items * TW + 2) / 2 + 2;
     p.ipiv = ipiv; p.info = info; p.info_offset = info_offset;
-    hipLaunchKernelGGL((tslu2_tree_kernel<T, R>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
+    hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
     if (hipError_t e = hipGetLastError(); e != hipSuccess)
         throw std::runtime_error(std::string("tslu tree kernel launch: ") + hipGetErrorString(e));
     const int64_t c0 = (Ablk - Apanel) / lda;
@@ -964,6 +971,17 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
     if (tslu_use_v2<T>()) {
+        // fp32: SLATE_TSLU_F32_R=2 selects two rows per thread at <= 128 VGPRs
+        static const bool f32_small = [] {
+            const char* e = std::getenv("SLATE_TSLU_F32_R");
+            return e && std::atoi(e) == 2;
+        }();
+        if constexpr (std::is_same<T, float>::value) {
+            if (f32_small) {
+                tslu2_narrow<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
+                return;
+            }
+        }
         tslu2_narrow<T>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
         return;
     }

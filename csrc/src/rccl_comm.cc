@@ -67,42 +67,52 @@ bool g_aborted = false;
 
 //------------------------------------------------------------------------------
 /// Copy-engine broadcast between the processes of one node (SLATE_BCAST=peer;
-/// SURVEY §5.8, reference listBcast, include/slate/BaseMatrix.hh:2129-2212):
-/// the root's buffer is exported once per allocation (hipIpcGetMemHandle),
-/// every receiver PULLS the bytes with one hipMemcpyAsync from the mapped
-/// root buffer on its own stream -- an SDMA copy over xGMI, no kernel on the
-/// CUs the trailing GEMM is using -- ordered by interprocess events:
-///   root:     record ready[seq % K] on its stream, publish (handle, offset,
-///             bytes) and seq in the shared control block, wait (host) until
-///             every receiver has issued its copy, then make its stream wait
-///             on the receivers' done events (the buffer may be rewritten
-///             after that, as after an ncclBroadcast);
-///   receiver: wait (host) for the root's seq, stream-wait on ready[seq % K],
-///             copy, record done[seq % K], publish seq.
-/// The host hand-off is a rendezvous of the communicator's ranks per
-/// broadcast (collective order is the same on every rank, as for RCCL); the
-/// control block is a POSIX shared-memory segment named once by rank 0 (one
-/// ncclBroadcast of the name at setup).  Event slots are reused after K
-/// broadcasts: by then every rank has issued its waits on the slot (the root
-/// returns from broadcast #seq only after every receiver arrived).
+/// SURVEY §5.8, reference listBcast, include/slate/BaseMatrix.hh:2129-2212).
+///
+/// Every rank owns a ring of kStage staging buffers (hipMalloc'd and exported
+/// once, re-exported only when a larger message outgrows one) and maps every
+/// other rank's buffers once.  Every rank sees every broadcast of the
+/// communicator in the same order (collective semantics), so each one knows,
+/// without asking, the root's message number rm and with it the staging slot
+/// rm % kStage and event slot rm % kRing.  One broadcast:
+///   root:     (slot reuse) waits until every receiver has issued its copy out
+///             of the slot's previous message and makes its stream wait on
+///             each receiver's latest copy; copies the message into the
+///             staging slot on its stream, records ready[rm % kRing],
+///             publishes (seq, bytes) -- and returns: its buffer is free;
+///   receiver: waits (host) for the root's seq, then on its single copy
+///             stream: after the caller's stream (buffer reuse) and the
+///             root's ready event, PULLS the bytes with one hipMemcpyAsync
+///             from the mapped staging buffer -- an SDMA copy over xGMI, no
+///             kernel on the CUs the trailing GEMM is using -- records its
+///             done event; the caller's stream waits on it.
+/// One copy stream per receiver makes "latest done event complete" imply
+/// every earlier copy complete, which is what the root's slot reuse needs.
+/// The host of the root waits only when the receivers lag kStage of its
+/// messages behind.  No handle depends on the lifetime of the caller's
+/// buffers.  The control block is a POSIX shared-memory segment named by
+/// rank 0 (one ncclBroadcast at set-up); a communicator whose ranks cannot
+/// map each other's memory / events keeps ncclBroadcast (the ranks agree
+/// through an all-reduce).
 class PeerBcast {
 public:
-    static constexpr int kMaxRanks = 64, kRing = 16;
+    static constexpr int kMaxRanks = 64, kRing = 16, kStage = 4;
+    struct Stage { hipIpcMemHandle_t mem; uint64_t id, cap; };
+    struct Msg { std::atomic<uint64_t> seq; uint64_t bytes; };
     struct alignas(64) Slot {
-        std::atomic<uint64_t> ready_seq;   // root: broadcast #seq published
-        std::atomic<uint64_t> done_seq;    // receiver: copy of #seq issued
+        std::atomic<uint64_t> done_seq;    // every broadcast up to this one processed
+        std::atomic<int> last_done;        // event slot of my latest receive copy (-1: none)
         std::atomic<int> inited;
-        hipIpcMemHandle_t mem;
-        uint64_t off, bytes;
+        Msg msg[kStage];                   // my messages as root, by staging slot
+        Stage st[kStage];                  // my staging buffers
         hipIpcEventHandle_t ready_ev[kRing], done_ev[kRing];
     };
     struct Block { Slot r[kMaxRanks]; };
 
     /// Collective set-up over `comm`; ok() is false on every rank when any
     /// rank could not map the control block, export / import interprocess
-    /// events or open a peer's memory handle (the communicator then keeps
-    /// ncclBroadcast) -- the ranks agree through one all-reduce.
-    PeerBcast(ncclComm_t comm, int rank, int size) : rank_(rank), size_(size) {
+    /// events or open a peer's staging memory.
+    PeerBcast(ncclComm_t comm, int rank, int size) : rank_(rank), size_(size), count_(size, 0) {
         hipStream_t st = device::queue(device::kCommQueue);
         auto allmin = [&](int v) {
             device::Buffer<int> d(1);
@@ -136,30 +146,31 @@ public:
             if (p == MAP_FAILED) ok = 0;
             else blk_ = static_cast<Block*>(p);
         }
-        // probe buffer: every rank exports one, every rank opens the others'
-        device::Buffer<char> probe(256);
         if (ok) {
             try {
                 Slot& me = blk_->r[rank_];
+                me.last_done.store(-1, std::memory_order_relaxed);
                 for (int i = 0; i < kRing; ++i) {
                     slate_hip_call(hipEventCreateWithFlags(&ready_[i], hipEventDisableTiming | hipEventInterprocess));
                     slate_hip_call(hipEventCreateWithFlags(&done_[i], hipEventDisableTiming | hipEventInterprocess));
                     slate_hip_call(hipIpcGetEventHandle(&me.ready_ev[i], ready_[i]));
                     slate_hip_call(hipIpcGetEventHandle(&me.done_ev[i], done_[i]));
+                    slate_hip_call(hipEventCreateWithFlags(&fork_[i], hipEventDisableTiming));
                 }
-                me.mem = export_handle(probe.data());
+                slate_hip_call(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
+                for (int j = 0; j < kStage; ++j) grow(j, size_t(1) << 20);   // 1 MiB to start
                 me.inited.store(1, std::memory_order_release);
             } catch (std::exception const&) { ok = 0; }
         }
         ok = allmin(ok);
         if (ok) {
-            try {
+            try {   // every rank maps every other rank's events and staging buffers once
                 for (int r = 0; r < size_; ++r) {
                     spin([&] { return blk_->r[r].inited.load(std::memory_order_acquire) != 0; });
                     if (r == rank_) continue;
                     (void)imported(r, 0, true);
                     (void)imported(r, 0, false);
-                    (void)open_handle(blk_->r[r].mem);
+                    for (int j = 0; j < kStage; ++j) (void)staged(r, j);
                 }
             } catch (std::exception const&) { ok = 0; }
             ok = allmin(ok);   // also: every rank mapped the segment, the name can go
@@ -178,39 +189,53 @@ public:
     }
     bool ok() const { return ok_; }
     ~PeerBcast() {
-        // at interpreter exit the HIP runtime may be gone: release what is safe
+        // at interpreter exit the HIP runtime may be gone: unmap the control
+        // block only (staging memory goes with the process)
         if (blk_) munmap(blk_, sizeof(Block));
     }
 
     void bcast(void* buf, size_t bytes, int root, hipStream_t s) {
         const uint64_t seq = ++seq_;
-        const int slot = int(seq % kRing);
+        const uint64_t rm = count_[root]++;                   // the root's message number
+        const int j = int(rm % kStage), e = int(rm % kRing);
         Block& B = *blk_;
+        Slot& me = B.r[rank_];
         if (rank_ == root) {
-            Slot& me = B.r[rank_];
-            char* base = nullptr;
-            size_t size = 0;
-            slate_hip_call(hipMemGetAddressRange(reinterpret_cast<hipDeviceptr_t*>(&base), &size, buf));
-            me.mem = export_handle(base);
-            me.off = uint64_t(static_cast<char*>(buf) - base);
-            me.bytes = bytes;
-            slate_hip_call(hipEventRecord(ready_[slot], s));
-            me.ready_seq.store(seq, std::memory_order_release);
-            for (int r = 0; r < size_; ++r) {
-                if (r == root) continue;
-                spin([&] { return B.r[r].done_seq.load(std::memory_order_acquire) >= seq; });
-                slate_hip_call(hipStreamWaitEvent(s, imported(r, slot, false), 0));
+            if (rm >= uint64_t(kStage)) {
+                // staging slot j carried message stage_seq_[j]: every receiver
+                // has issued its copy out of it (host), and its copy stream
+                // finished it (GPU: its latest done event)
+                const uint64_t prev = stage_seq_[j];
+                for (int r = 0; r < size_; ++r) {
+                    if (r == rank_) continue;
+                    spin([&] { return B.r[r].done_seq.load(std::memory_order_acquire) >= prev; });
+                    const int ld = B.r[r].last_done.load(std::memory_order_acquire);
+                    if (ld >= 0) slate_hip_call(hipStreamWaitEvent(s, imported(r, ld, false), 0));
+                }
             }
+            if (bytes > stage_cap_[j]) grow(j, bytes);
+            slate_hip_call(hipMemcpyAsync(stage_[j], buf, bytes, hipMemcpyDeviceToDevice, s));
+            slate_hip_call(hipEventRecord(ready_[e], s));
+            me.msg[j].bytes = bytes;
+            me.msg[j].seq.store(seq, std::memory_order_release);
+            stage_seq_[j] = seq;
+            me.done_seq.store(seq, std::memory_order_release);
             return;
         }
-        Slot& rs = B.r[root];
-        spin([&] { return rs.ready_seq.load(std::memory_order_acquire) >= seq; });
-        slate_error_if_msg(rs.bytes != bytes, "SLATE_BCAST=peer: message size mismatch");
-        char* src = static_cast<char*>(open_handle(rs.mem)) + rs.off;
-        slate_hip_call(hipStreamWaitEvent(s, imported(root, slot, true), 0));
-        slate_hip_call(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToDevice, s));
-        slate_hip_call(hipEventRecord(done_[slot], s));
-        B.r[rank_].done_seq.store(seq, std::memory_order_release);
+        Msg& msg = B.r[root].msg[j];
+        spin([&] { return msg.seq.load(std::memory_order_acquire) == seq; });
+        slate_error_if_msg(msg.bytes != bytes, "SLATE_BCAST=peer: broadcast sizes differ between ranks");
+        char* src = static_cast<char*>(staged(root, j));
+        const int f = int(recv_ % kRing);
+        ++recv_;
+        slate_hip_call(hipEventRecord(fork_[f], s));              // buf's earlier users on the caller's stream
+        slate_hip_call(hipStreamWaitEvent(cs_, fork_[f], 0));
+        slate_hip_call(hipStreamWaitEvent(cs_, imported(root, e, true), 0));
+        slate_hip_call(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToDevice, cs_));
+        slate_hip_call(hipEventRecord(done_[f], cs_));
+        slate_hip_call(hipStreamWaitEvent(s, done_[f], 0));
+        me.last_done.store(f, std::memory_order_release);
+        me.done_seq.store(seq, std::memory_order_release);
     }
 
 private:
@@ -226,24 +251,31 @@ private:
                                     __LINE__);
         }
     }
-    hipIpcMemHandle_t export_handle(char* base) {
-        const uint64_t ep = device::alloc_epoch();
-        if (ep != epoch_) { exported_.clear(); epoch_ = ep; }   // an address may name a new allocation
-        auto it = exported_.find(base);
-        if (it != exported_.end()) return it->second;
-        hipIpcMemHandle_t h;
-        slate_hip_call(hipIpcGetMemHandle(&h, base));
-        exported_[base] = h;
-        return h;
-    }
-    void* open_handle(hipIpcMemHandle_t const& h) {
-        std::string key(reinterpret_cast<char const*>(&h), sizeof h);
-        auto it = opened_.find(key);
-        if (it != opened_.end()) return it->second;
+    /// (re)allocate and export my staging buffer j; an outgrown buffer stays
+    /// allocated (receivers may still read it; sizes only grow, so this
+    /// happens a few times per communicator)
+    void grow(int j, size_t bytes) {
+        const size_t cap = std::max<size_t>(bytes, stage_cap_[j] * 2);
         void* p = nullptr;
-        slate_hip_call(hipIpcOpenMemHandle(&p, h, hipIpcMemLazyEnablePeerAccess));
-        opened_[key] = p;
-        return p;
+        slate_hip_call(hipMalloc(&p, cap));
+        stage_[j] = static_cast<char*>(p);
+        stage_cap_[j] = cap;
+        Stage& st = blk_->r[rank_].st[j];
+        slate_hip_call(hipIpcGetMemHandle(&st.mem, p));
+        st.cap = cap;
+        st.id = ++stage_ids_;
+    }
+    /// rank r's staging buffer j mapped here (re-mapped when r grew it; the
+    /// old mapping stays: copies from it may still be queued)
+    void* staged(int r, int j) {
+        Stage const& st = blk_->r[r].st[j];
+        auto& m = mapped_[r * kStage + j];
+        if (!m.first || m.second != st.id) {
+            void* p = nullptr;
+            slate_hip_call(hipIpcOpenMemHandle(&p, st.mem, hipIpcMemLazyEnablePeerAccess));
+            m = {p, st.id};
+        }
+        return m.first;
     }
     hipEvent_t imported(int r, int slot, bool ready) {
         auto& m = ready ? imp_ready_ : imp_done_;
@@ -259,10 +291,14 @@ private:
     int rank_, size_;
     bool ok_ = false;
     Block* blk_ = nullptr;
-    uint64_t seq_ = 0, epoch_ = 0;
-    hipEvent_t ready_[kRing] = {}, done_[kRing] = {};
-    std::map<char*, hipIpcMemHandle_t> exported_;
-    std::map<std::string, void*> opened_;
+    uint64_t seq_ = 0, recv_ = 0, stage_ids_ = 0;
+    std::vector<uint64_t> count_;                 // messages rooted at each rank so far
+    uint64_t stage_seq_[kStage] = {};
+    hipEvent_t ready_[kRing] = {}, done_[kRing] = {}, fork_[kRing] = {};
+    hipStream_t cs_ = nullptr;                    // my single copy stream (receiver)
+    char* stage_[kStage] = {};
+    size_t stage_cap_[kStage] = {};
+    std::map<int, std::pair<void*, uint64_t>> mapped_;
     std::map<int, hipEvent_t> imp_ready_, imp_done_;
 };
 

@@ -60,6 +60,7 @@ ap.add_argument("--bw-gbs", type=float, default=64.0, help="modelled per-message
 ap.add_argument("--lat-us", type=float, default=25.0, help="modelled per-message latency (us)")
 ap.add_argument("--routines", default="lu,qr,chol,gemm")
 ap.add_argument("--reps", type=int, default=3)
+ap.add_argument("--summa-k", type=int, default=2048, help="SUMMA K per step (gemmC: w = K / nb tiles per step)")
 a = ap.parse_args()
 
 dev = "cuda"
@@ -332,7 +333,8 @@ if "gemm" in todo:
     # SUMMA: every process multiplies its (n/p x n/q) block, K = nb per step;
     # the panel broadcasts overlap the previous step's GEMM
     mloc, nloc = n // p, n // q
-    G1 = Gemm(mloc, nloc, nb)
+    w = max(1, a.summa_k // nb)
+    G1 = Gemm(mloc, nloc, w * nb)
     best = math.inf
     for _ in range(a.reps):
         sync_all()
@@ -342,7 +344,8 @@ if "gemm" in todo:
         ops.queue_sync(0)
         best = min(best, (time.perf_counter() - t0) / 8)
     per_k = best * 1e3
-    c = comm(mloc * nb * 8) + comm(nb * nloc * 8) if p * q > 1 else 0.0
-    pred = nt * max(per_k, c)
-    print(f"\n== dgemm: n={n} nb={nb} grid {p}x{q}: per-step local GEMM {per_k:.3f} ms, comm {c:.3f} ms; "
-          f"predicted {pred:.0f} ms -> {2.0 * n ** 3 / (pred * 1e-3) / 1e12:.1f} TFLOP/s whole node")
+    c = w * (comm(mloc * nb * 8) + comm(nb * nloc * 8)) if p * q > 1 else 0.0
+    steps_ = math.ceil(nt / w)
+    pred = steps_ * max(per_k, c)
+    print(f"\n== dgemm: n={n} nb={nb} grid {p}x{q} SUMMA K={w * nb} per step: local GEMM {per_k:.3f} ms, "
+          f"comm {c:.3f} ms; predicted {pred:.0f} ms -> {2.0 * n ** 3 / (pred * 1e-3) / 1e12:.1f} TFLOP/s whole node")
