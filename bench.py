@@ -47,6 +47,8 @@ def _import_slate():
 
 METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
 ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
+# per-routine grid shapes by world size (none: the job's p x q for all)
+GRID_PER = {}
 # BASELINE.json configs beyond the 4-routine headline suite (run after it,
 # reported under "configs"): name -> (routine, n or None = --dim, nb, target)
 EXTRAS = {
@@ -120,6 +122,7 @@ def parse():
     ap.add_argument("--p", type=int, default=0)
     ap.add_argument("--q", type=int, default=0)
     ap.add_argument("--lookahead", type=int, default=0, help="0: per-routine default (see la_per)")
+    ap.add_argument("--grid-per", default="", help="per-routine grid shapes, e.g. dgetrf=4x2,dgeqrf=2x4")
     ap.add_argument("--method-lu", default="tntpiv", choices=["ppiv", "tntpiv"])
     ap.add_argument("--trace", default="")
     ap.add_argument("--mixed-escalate", default="yes", choices=["yes", "no"],
@@ -280,6 +283,24 @@ def main(a):
     def la_of(rname):
         return a.lookahead or la_per.get(rname, 1)
 
+    # Grid shape per routine on p x q > 1 (--grid-per dgetrf=4x2,...; the
+    # defaults come from the 8-GPU critical-path sweep,
+    # profiles/r6_critpath_8gpu_sweep.txt): extra grids are split from the
+    # same world communicator, created on first use in the same order on
+    # every rank.
+    grid_per = dict(GRID_PER.get(world, {}))
+    grid_per.update({k: tuple(int(x) for x in v.split("x")) for k, v in
+                     (kv.split("=") for kv in a.grid_per.split(",") if kv)})
+    grids = {(grid.p, grid.q): grid}
+
+    def grid_for(label, rname):
+        shape = grid_per.get(label) or grid_per.get(rname)
+        if world == 1 or shape is None or a.p:
+            return grid
+        if shape not in grids:
+            grids[shape] = s.parallel.reshape_grid(*shape)
+        return grids[shape]
+
     def barrier_sync():
         s.sync()
         if world > 1:
@@ -294,7 +315,7 @@ def main(a):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         return float(t.item())
 
-    def residual(rname, mats, kind, seed, nb, n_, tg):
+    def residual(rname, mats, kind, seed, nb, n_, tg, grid):
         """Backward error of the result just computed (reference tester
         formulas, test/test_gesv.cc:330-377, test_posv.cc:302-343):
         ||b - A x|| / (||A|| ||x|| n eps) for the solves, and
@@ -355,25 +376,26 @@ def main(a):
         mats = {}
         tgt = s.target_of(tg)
         o = dict(target=tg, lookahead=la_of(rname))
+        grid_r = grid_for(label, rname)
         if rname == "dgemm":
             for key, seed in (("A", 1), ("B", 2), ("C", 3)):
-                M = s.Matrix(n_, n_, nb, np.float64, grid)
+                M = s.Matrix(n_, n_, nb, np.float64, grid_r)
                 M.insertLocalTiles(tgt)
                 s._slate.generate_matrix_d("rands", M, seed, -1.0, s.opts(tg))
                 mats[key] = M
             flops = F.gemm_flops(n_, n_, n_)
         elif rname == "dgesv_mixed":
             for key, seed in (("B", 7), ("X", 0)):
-                M = s.Matrix(n_, 1, nb, np.float64, grid)
+                M = s.Matrix(n_, 1, nb, np.float64, grid_r)
                 M.insertLocalTiles(tgt)
                 s._slate.generate_matrix_d("rands", M, seed + 1, -1.0, s.opts(tg))
                 mats[key] = M
-            M = s.Matrix(n_, n_, nb, np.float64, grid)
+            M = s.Matrix(n_, n_, nb, np.float64, grid_r)
             M.insertLocalTiles(tgt)
             mats["A"] = M
             flops = F.getrf_flops(n_)   # tester convention: counted as the fp64 LU
         else:
-            M = s.Matrix(n_, n_, nb, np.float64, grid)
+            M = s.Matrix(n_, n_, nb, np.float64, grid_r)
             M.insertLocalTiles(tgt)
             mats["A"] = M
             flops = {"dpotrf": F.potrf_flops, "dgetrf": F.getrf_flops, "dgeqrf": F.geqrf_flops}[rname](n_)
@@ -436,7 +458,7 @@ def main(a):
             if first_dt is None:
                 first_dt = dt
             if a.trace and step == warmup:
-                s.trace.finish(grid.world, f"{a.trace}_{label}")
+                s.trace.finish(grid_r.world, f"{a.trace}_{label}")
                 s.trace.off()
                 s.trace.clear()
             if step >= warmup:
@@ -455,7 +477,7 @@ def main(a):
                "steps": len(times), "warmup": warmup}
         if a.check == "yes":
             wd.arm(f"{label} residual check")
-            err = residual(rname, mats, kind, seed, nb, n_, tg)
+            err = residual(rname, mats, kind, seed, nb, n_, tg, grid_r)
             wd.disarm()
             res["backward_error"] = float(f"{err:.3e}")
             res["check"] = "pass" if err < 50 else "FAIL"
@@ -468,7 +490,7 @@ def main(a):
         return res
 
     results = {}
-    routines = [r.strip() for r in a.routines.split(",") if r.strip()]
+    routines = [r.strip() for r in a.routines.split(",") if r.strip() and r.strip() != "none"]
     for rname in routines:
         results[rname] = run(rname, n, nb_per.get(rname, a.nb), target, rname)
     configs = {}
@@ -480,7 +502,7 @@ def main(a):
         tg_ = tg_ or target
         if tg_ == "h" and world > 1:
             continue   # config 1 is a one-process host-target plumbing check
-        nb_ = nb_ or nb_per.get(rname, a.nb)
+        nb_ = nb_per.get(name) or nb_ or nb_per.get(rname, a.nb)   # --nb-per <extra name>=nb overrides
         n_ = n if n_ is None else (n // 2 if n_ == -2 else n_)
         fl = {"dgemm": F.gemm_flops(n_, n_, n_), "dpotrf": F.potrf_flops(n_), "dgeqrf": F.geqrf_flops(n_)}.get(
             rname, F.getrf_flops(n_))
@@ -498,7 +520,7 @@ def main(a):
 
     tot_flops = sum(r["flops"] for r in results.values())
     tot_t = sum(r["ms"] for r in results.values()) / 1e3
-    value = tot_flops / tot_t / 1e12
+    value = tot_flops / tot_t / 1e12 if tot_t > 0 else 0.0   # (--routines none: extras only)
     line = {
         "metric": METRIC,
         "value": round(value, 3),

@@ -917,11 +917,11 @@ void tslu_init(int64_t* work, hipStream_t s) {
 
 // Which tournament: v2 (one tree launch + one finish launch) for fp64, where
 // it measured dgetrf n = 65536 56.4 -> 58.0 TFLOP/s and the isolated
-// 32768 x 512 panel 3.71 -> 2.96 ms; v1 (per-level launches) elsewhere: its
-// 60-VGPR fp32 waves fit beside the trailing GEMM's, and the fp32 factor of
-// dgesv_mixed measured 1.92 s (v1) against 2.11 s (v2, 256-VGPR waves that
-// wait for a whole GEMM slot); complex v2 spills.  SLATE_TSLU=1|2 forces one
-// (profiles/r5_tslu_v2.txt).
+// 32768 x 512 panel 3.71 -> 2.96 ms, and for fp32 with two rows per thread
+// at <= 128 VGPRs (round 6: the dgesv_mixed fp32 factor 1876 ms (v1) ->
+// 1849 ms; the round-5 four-row v2, whose 256-VGPR waves wait for a whole
+// GEMM slot, 2039 ms, profiles/r6_cfg5_tslu_ab.txt); v1 (per-level
+// launches) for complex, where v2 spills.  SLATE_TSLU=1|2 forces one.
 template <typename T>
 static bool tslu_use_v2() {
     static const int forced = [] {
@@ -930,7 +930,7 @@ static bool tslu_use_v2() {
         return e ? std::atoi(e) : 0;
     }();
     if (forced) return forced == 2;
-    return std::is_same<T, double>::value;
+    return std::is_same<T, double>::value || std::is_same<T, float>::value;
 }
 
 template <typename T, int R = Tslu2Rows<T>::R, int WPE = 1>
@@ -971,10 +971,11 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
     int64_t rows = m - r;
     if (rows <= 0 || nn <= 0) return;
     if (tslu_use_v2<T>()) {
-        // fp32: SLATE_TSLU_F32_R=2 selects two rows per thread at <= 128 VGPRs
+        // fp32: two rows per thread at <= 128 VGPRs (default; SLATE_TSLU_F32_R=4:
+        // four rows per thread, 256-VGPR waves that wait for a whole GEMM slot)
         static const bool f32_small = [] {
             const char* e = std::getenv("SLATE_TSLU_F32_R");
-            return e && std::atoi(e) == 2;
+            return !e || std::atoi(e) == 2;
         }();
         if constexpr (std::is_same<T, float>::value) {
             if (f32_small) {

@@ -885,6 +885,24 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
     int64_t tail_k = kt;                     // first tile of the tail (kt: none)
     Work<int64_t> tpv;                       // [ipiv(w) | dst(2w) | src(2w)]
     if (tail_ok) tpv.resize(target, size_t(5 * tail_w + 8));
+    // Deferred left interchanges: once the remaining matrix is at most m / D
+    // tall (SLATE_LU_DEFER_LEFT = D, default 2, 0 = off), the steps' row
+    // interchanges are no longer applied to the left columns [0, k_def) step
+    // by step -- in the tail those swaps of up to 2 kb rows across almost the
+    // whole width ran beside trailing GEMMs too small to hide them
+    // (profiles/r6_final_trace_dgetrf.txt: 136 ms of permute_rows in the last
+    // decile's GEMM-idle windows) -- but composed on the host at the end and
+    // applied once: each moved row of those columns is gathered and scattered
+    // a single time.  n = 65536: dgetrf 3203-3207 ms (off) -> 3174 ms (D = 2),
+    // 3191 ms (D = 4), interleaved (profiles/r6_lu_defer_left_ab.txt).
+    static const double defer_div = [] {
+        const char* e = std::getenv("SLATE_LU_DEFER_LEFT");
+        return e ? std::atof(e) : 2.0;
+    }();
+    int64_t k_def = kt;
+    if (pivot && target == Target::Devices && defer_div >= 1.0 && !tail_ok)
+        for (int64_t k = 1; k < kt; ++k)
+            if (double(m - grow_of(A, k)) * defer_div <= double(m)) { k_def = k; break; }
 
     for (int64_t k = 0; k < kt; ++k) {
         const int64_t kb = A.tileNb(k);
@@ -1112,11 +1130,11 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             range_tasks(device::kTrailQueue, jla_end, nt);
         }
 
-        if (k > 0 && pivot) {
+        if (k > 0 && pivot && k != k_def) {
             // reads PV[pvs] (tPV): the panel that next rewrites the slot, RP
             // steps later, waits for it (write-after-read across queues)
             S.task(left_q, {tPV}, {Sched::tok(11, 0), Sched::col(k - 1)}, [&, k](lb::Ctx const& c) {
-                auto cc = lcols(0, k);
+                auto cc = lcols(k > k_def ? k_def : 0, k);   // [0, k_def) deferred
                 permute(c, cc.first, cc.second);
             });
         }
@@ -1131,6 +1149,39 @@ int64_t getrf_impl(Matrix<T>& A_in, Pivots& pivots, Options const& opts, PanelMo
             slate_hip_call(hipStreamSynchronize(s1));
         } else {
             std::copy(ipiv_all.data(), ipiv_all.data() + ip.size(), ip.begin());
+        }
+    }
+    if (k_def < kt) {
+        // the deferred interchanges of steps k_def.. on local columns [0, k_def):
+        // compose them (row i of the result holds original row where[i]),
+        // then gather the moved rows and scatter them to their places
+        const int64_t r0 = grow_of(A, k_def), R = m - r0;
+        std::vector<int64_t> where(static_cast<size_t>(R), int64_t(0));
+        std::iota(where.begin(), where.end(), int64_t(0));
+        for (int64_t k = k_def; k < kt; ++k) {
+            const int64_t kk = grow_of(A, k) - r0, kd = std::min(A.tileNb(k), m - r0 - kk);
+            for (int64_t t = 0; t < kd; ++t) std::swap(where[kk + t], where[kk + ip[k * nb + t]]);
+        }
+        std::vector<int64_t> idx;   // [src rows | dst rows], relative to r0
+        for (int64_t i = 0; i < R; ++i) if (where[i] != i) idx.push_back(where[i]);
+        const int64_t cnt = int64_t(idx.size());
+        for (int64_t i = 0; i < R; ++i) if (where[i] != i) idx.push_back(i);
+        const int64_t ncl = lcol_of(A, k_def);
+        if (cnt > 0 && ncl > 0) {
+            lb::Ctx c = S.ctx(left_q);
+            Work<int64_t> didx(target, idx.size());
+            device::memcpy_async(didx.data(), idx.data(), idx.size() * sizeof(int64_t), c.stream);
+            const int64_t chunk = std::max<int64_t>(1, std::min<int64_t>(ncl, 32768));
+            Work<T> buf(target, size_t(cnt) * chunk);
+            for (int64_t j0 = 0; j0 < ncl; j0 += chunk) {
+                const int64_t nc = std::min(chunk, ncl - j0);
+                T* a0 = a + r0 + j0 * lda;
+                slate_amd::dev::rows_pack(nc, slate_amd::dev::dptr(a0), lda, didx.data(), int(cnt),
+                                          slate_amd::dev::dptr(buf.data()), false, c.stream);
+                slate_amd::dev::rows_pack(nc, slate_amd::dev::dptr(a0), lda, didx.data() + cnt, int(cnt),
+                                          slate_amd::dev::dptr(buf.data()), true, c.stream);
+            }
+            slate_hip_call(hipStreamSynchronize(c.stream));
         }
     }
     pivots.assign(kt, {});

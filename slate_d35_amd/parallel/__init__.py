@@ -212,6 +212,52 @@ def init_grid(p: int | None = None, q: int | None = None, order=GridOrder.Col, t
     return _GRID
 
 
+def reshape_grid(p: int, q: int, order=GridOrder.Col):
+    """Another p x q grid over the SAME processes as the current grid (its
+    world communicator; new row / column -- and fast-lane -- communicators
+    split from it).  Every rank must call it, in the same order.  Used to
+    run each routine on its best grid shape in one job (bench.py)."""
+    g = current_grid()
+    n = world_size()
+    if p * q != n:
+        raise ValueError(f"grid {p}x{q} does not match world size {n}")
+    if n == 1 or (g.p == p and g.q == q and g.order == order):
+        return g
+    world = g.world
+    rank = world.rank()
+    myrow, mycol = (rank % p, rank // p) if order == GridOrder.Col else (rank // q, rank % q)
+    if world.name() == "rccl":
+        rowc = _slate.rccl_split(world, myrow, mycol)
+        colc = _slate.rccl_split(world, p + mycol, myrow)
+        grid = _slate.Grid(p, q, order, world, rowc, colc)
+        _KEEP.extend([rowc, colc])
+        if os.environ.get("SLATE_FAST_LANE", "1") != "0":
+            fast = (_slate.rccl_split(world, myrow, mycol), _slate.rccl_split(world, p + mycol, myrow))
+            _KEEP.extend(fast)
+            grid.set_fast(*fast)
+        return grid
+    if world.name() == "tcp":
+        rowc = _slate.tcp_split(world, myrow, mycol)
+        colc = _slate.tcp_split(world, p + mycol, myrow)
+        _KEEP.extend([rowc, colc])
+        return _slate.Grid(p, q, order, world, rowc, colc)
+    import torch.distributed as dist
+    rank_of = (lambda i, j: i + j * p) if order == GridOrder.Col else (lambda i, j: i * q + j)
+    rowc = colc = None
+    for i in range(p):
+        ranks = [rank_of(i, j) for j in range(q)]
+        gg = dist.new_group(ranks)
+        if i == myrow:
+            rowc = TorchHostComm(ranks, gg)
+    for j in range(q):
+        ranks = [rank_of(i, j) for i in range(p)]
+        gg = dist.new_group(ranks)
+        if j == mycol:
+            colc = TorchHostComm(ranks, gg)
+    _KEEP.extend([rowc, colc])
+    return _slate.Grid(p, q, order, world, rowc, colc)
+
+
 def finalize():
     """Tear down the grid and the torch.distributed process group (the
     reference's MPI_Finalize point).  Call before exit in multi-process runs:
