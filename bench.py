@@ -47,8 +47,11 @@ def _import_slate():
 
 METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
 ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
-# per-routine grid shapes by world size (none: the job's p x q for all)
-GRID_PER = {}
+# per-routine grid shapes by world size (none: the job's p x q for all):
+# the 8-GPU critical-path sweep (profiles/r6_critpath_8gpu_sweep.txt, 32
+# reserved CUs, copy-engine broadcasts) predicts QR 308 / Cholesky 279
+# TFLOP/s on 4 x 2 against 275 / 250 on 2 x 4, LU best on 2 x 4 with nb 256
+GRID_PER = {8: {"dgeqrf": (4, 2), "dpotrf": (4, 2)}}
 # BASELINE.json configs beyond the 4-routine headline suite (run after it,
 # reported under "configs"): name -> (routine, n or None = --dim, nb, target)
 EXTRAS = {
@@ -261,7 +264,8 @@ def main(a):
     # Round 5 (single-wave leaf kernels make wide diagonal blocks cheap):
     # dpotrf 1536 vs 1024 62.7-63.0 -> 63.3-63.4, dgeqrf 1024 vs 512 59.2 ->
     # 59.8-59.9 TFLOP/s, interleaved on one box (profiles/r5_nb_ab.txt).
-    default_nb = {"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024} if world == 1 else {}
+    default_nb = ({"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024} if world == 1
+                  else {"dgetrf": 256})   # p x q: the LU panel chain shrinks with nb (r6 sweep)
     if a.nb:
         default_nb = {}
     a.nb = a.nb or 512

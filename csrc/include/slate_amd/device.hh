@@ -73,6 +73,10 @@ hipStream_t queue(int index);
 void sync_all();
 /// CUs reserved for the panel/comm queues (0 = no partitioning).
 int reserved_cus();
+/// A queue whose kernels may run on every CU: 0 without reservation, the
+/// (unmasked) panel queue in shared mode.  Drivers without a panel chain
+/// (SUMMA gemm) put their GEMMs there.
+int full_queue();
 
 /// Pooled event (disable-timing events for dependency edges).
 hipEvent_t event_get();

@@ -200,6 +200,7 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
         if (p > 1 && w > 1) WS[r].resize(target, size_t(kbmax) * std::max<int64_t>(lc.n, 1));
     }
     const int64_t nsteps = (kt + w - 1) / w;
+    const int gq = target == Target::Devices ? device::full_queue() : 0;
     for (int64_t st = 0; st < nsteps; ++st) {
         const int slot = int(st % R);
         const int64_t k0 = st * w, k1 = std::min(kt, k0 + w);   // tiles [k0, k1)
@@ -240,7 +241,8 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
             }
         });
         T bk = (st == 0) ? beta : T(1);
-        S.task(0, {tBc}, {Sched::tok(9, 0)}, [&, Ak, ldak, Bk, ldbk, K, bk](lb::Ctx const& c) {
+        // no panel chain to protect: the GEMMs take every CU (device::full_queue)
+        S.task(gq, {tBc}, {Sched::tok(9, 0)}, [&, Ak, ldak, Bk, ldbk, K, bk](lb::Ctx const& c) {
             trace::Block t2("gemm_update");
             lb::gemm(c, Op::NoTrans, Op::NoTrans, lc.m, lc.n, K, alpha, Ak, ldak, Bk, ldbk, bk, lc.ptr, lc.ld);
         });

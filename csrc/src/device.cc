@@ -26,6 +26,7 @@ struct State {
     bool streams_ready = false;
     bool destroyed = false;   // context_destroy ran while blocks were still live
     int reserved_cus = 0;
+    int full_queue = 0;        // a queue whose kernels may use every CU
     hipStream_t streams[kNumQueues] = {};
     std::vector<hipEvent_t> events;
     // caching allocator: bucket size -> free list; ptr -> bucket size
@@ -162,6 +163,7 @@ void ensure_streams_locked(State& s) {
             (c < reserve ? mask_panel : mask_update)[c / 32] |= (1u << (c % 32));
     }
     s.reserved_cus = reserve;
+    s.full_queue = (reserve > 0 && !exclusive) ? 1 : (reserve > 0 ? kCommQueue : 0);
     for (int i = 0; i < kNumQueues; ++i) {
         const bool panel = (i == 1 || i == kCommQueue);
         const bool masked = reserve > 0 &&
@@ -266,6 +268,13 @@ void context_destroy(Context* ctx) {
 }
 
 int reserved_cus() { return st().reserved_cus; }
+
+int full_queue() {
+    auto& s = st();
+    std::lock_guard<std::mutex> g(s.mtx);
+    ensure_streams_locked(s);
+    return s.full_queue;
+}
 
 bool available() {
     int n = 0;
