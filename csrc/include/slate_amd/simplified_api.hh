@@ -75,6 +75,12 @@ template <typename T>
 void triangular_solve(T alpha, Matrix<T>& B, TriangularBandMatrix<T> const& A, Options const& opts = {}) {
     tbsm(Side::Right, alpha, A, B, opts);
 }
+/// with band LU row interchanges (tbsm with pivots, reference src/tbsmPivots.cc)
+template <typename T>
+void triangular_solve(T alpha, TriangularBandMatrix<T> const& A, Pivots const& pivots, Matrix<T>& B,
+                      Options const& opts = {}) {
+    tbsm(Side::Left, alpha, A, pivots, B, opts);
+}
 
 /// C = alpha A A^H + beta C (herk) / alpha A A^T + beta C (syrk)
 template <typename T>

@@ -892,7 +892,7 @@ Result r_cholqr(Case<T>& c) {
 }
 
 template <typename T>
-Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbtrs, 3 gbmm, 4 hbmm, 5 tbsm
+Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbtrs, 3 gbmm, 4 hbmm, 5 tbsm, 6 gbtrs, 7 pbtrs, 8 tbsm with pivots
     const int64_t kd = std::max<int64_t>(1, c.nb / 2);
     Result r;
     if (variant == 1 || variant == 2 || variant == 4 || variant == 7) {
@@ -972,6 +972,51 @@ Result r_band(Case<T>& c, int variant) {   // 0 gbtrf+gbtrs, 1 pbsv, 2 pbtrf+pbt
             gbmm(T(1), Db, X, T(0), LX, c.opts);
             add(T(-1), B0, T(1), LX, c.opts);
             r.error = c.nrm(LX) / (c.nrm(B0) * double(c.n));
+        }
+        return r;
+    }
+    if (variant == 8) {   // tbsm with row interchanges (reference src/tbsmPivots.cc)
+        scale(R_<T>(1), R_<T>(2 * kd), Ag, c.opts);   // |L(i, j)| <= 1 / (4 kd): no growth in the sweep
+        TriangularBandMatrix<T> L(Uplo::Lower, Diag::Unit, kd, Ag);
+        const int64_t mt = Ag.mt();
+        std::vector<int64_t> r0(mt + 1, 0);
+        for (int64_t k = 0; k < mt; ++k) r0[k + 1] = r0[k] + Ag.tileMb(k);
+        // pivots of tile k: rows within the band reach, as gbtrf produces them
+        Pivots piv(mt);
+        uint64_t s = 7;
+        for (int64_t k = 0; k < mt; ++k)
+            for (int64_t row = r0[k]; row < r0[k + 1]; ++row) {
+                s = s * 6364136223846793005ull + 1442695040888963407ull;
+                const int64_t p = row + int64_t((s >> 33) % uint64_t(std::min(c.n, row + kd + 1) - row));
+                const int64_t tp = std::upper_bound(r0.begin(), r0.end(), p) - r0.begin() - 1;
+                piv[k].emplace_back(tp - k, p - r0[tp]);
+            }
+        auto X = c.copy_of(B);
+        r.time = c.timed([&] { tbsm(Side::Left, T(1), L, piv, X, c.opts); });
+        r.flops = cfac<T>() * double(c.n) * kd * c.P.nrhs;
+        if (c.P.check) {   // the reference's sweep on the host: tile k's swaps, then its eliminations
+            std::vector<T> l, xs, x1;
+            gather(Ag, l, c.opts);
+            gather(B, xs, c.opts);
+            gather(X, x1, c.opts);
+            const int64_t n = c.n, nr = c.P.nrhs;
+            for (int64_t k = 0; k < mt; ++k) {
+                for (int64_t t = 0; t < r0[k + 1] - r0[k]; ++t) {
+                    const int64_t row = r0[k] + t, p = r0[k + piv[k][t].tileIndex()] + piv[k][t].elementOffset();
+                    if (p != row)
+                        for (int64_t j = 0; j < nr; ++j) std::swap(xs[size_t(row + j * n)], xs[size_t(p + j * n)]);
+                }
+                for (int64_t col = r0[k]; col < r0[k + 1]; ++col)
+                    for (int64_t i = col + 1; i <= std::min(n - 1, col + kd); ++i)
+                        for (int64_t j = 0; j < nr; ++j)
+                            xs[size_t(i + j * n)] -= l[size_t(i + col * n)] * xs[size_t(col + j * n)];
+            }
+            double err = 0, mx = 1e-300;
+            for (size_t i = 0; i < xs.size(); ++i) {
+                err = std::max(err, double(std::abs(x1[i] - xs[i])));
+                mx = std::max(mx, double(std::abs(xs[i])));
+            }
+            r.error = err / (mx * double(kd));
         }
         return r;
     }
@@ -1838,6 +1883,7 @@ std::map<std::string, Fn<T>> routines() {
         {"gbmm", [](Case<T>& c) { return r_band<T>(c, 3); }},
         {"hbmm", [](Case<T>& c) { return r_band<T>(c, 4); }},
         {"tbsm", [](Case<T>& c) { return r_band<T>(c, 5); }},
+        {"tbsm_pivots", [](Case<T>& c) { return r_band<T>(c, 8); }},
         {"hetrf", r_hetrf<T>},
         {"hesv_aasen", r_hesv_aasen<T>},
         {"heev_vals", [](Case<T>& c) { return r_vals<T>(c, 0); }},

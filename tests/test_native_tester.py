@@ -60,7 +60,7 @@ def test_breadth_distributed_2x2():
     """The breadth additions (rank-2k, stationary-A, condest, unm*, cholqr,
     band, indefinite, generalized eig, tridiagonal, aux) on a 2x2 grid."""
     codes, outs = launch(["syrk,her2k,syr2k,symm,gemmA,gemmC,getrs,potrs,potri,gesv_nopiv,gesv_tntpiv,gesv_rbt,"
-                          "gecondest,pocondest,unmqr,unmlq,cholqr,gbtrf,pbsv,gbmm,hbmm,tbsm,hetrf,heev_vals,svd_vals,"
+                          "gecondest,pocondest,unmqr,unmlq,cholqr,gbtrf,pbsv,gbmm,hbmm,tbsm,tbsm_pivots,hetrf,heev_vals,svd_vals,"
                           "hegv,steqr2,add,copy,scale,set,trtrm,colnorms,henorm,redistribute",
                           "--type", "d,z", "--dim", "150", "--nb", "32", "--grid", "2x2"], 4)
     assert codes == [0] * 4 and "all tests passed" in outs[0], "\n".join(o[-2500:] for o in outs)
@@ -111,7 +111,7 @@ def test_nonuniform_and_grid_order():
 @pytest.mark.gpu
 def test_device_routines():
     codes, outs = launch(["gemm,herk,trsm,potrf,getrf,getrf_tntpiv,geqrf,gesv_mixed,posv_mixed,heev,svd,"
-                          "syr2k,symm,gemmA,getrs,potri,gesv_rbt,unmqr,unmlq,cholqr,gbtrf,pbsv,hbmm,tbsm,heev_vals,"
+                          "syr2k,symm,gemmA,getrs,potri,gesv_rbt,unmqr,unmlq,cholqr,gbtrf,pbsv,hbmm,tbsm,tbsm_pivots,heev_vals,"
                           "svd_vals,hegv,steqr2,redistribute",
                           "--type", "d,z", "--dim", "1000", "--nb", "128"], target="d")
     assert codes == [0] and "all tests passed" in outs[0], outs[0][-4000:]
