@@ -477,7 +477,8 @@ def main(a):
                 fit = int(left // (max_over_ranks(dt) * 1.15))
                 total = min(total, max(warmup + 1, step + fit))
         t = max_over_ranks(float(np.mean(times)))
-        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_, "lookahead": la_of(rname),
+        res = {"ms": t * 1e3, "tflops": flops / t / 1e12, "flops": flops, "nb": nb, "n": n_,
+               "grid": f"{grid_r.p}x{grid_r.q}", "lookahead": la_of(rname),
                "steps": len(times), "warmup": warmup}
         if a.check == "yes":
             wd.arm(f"{label} residual check")
@@ -539,7 +540,8 @@ def main(a):
         "dtype": "fp64",
         "data": "synthetic random (rands: counter-hash uniform[-1,1); SPD = symmetric + n*I for dpotrf)",
         "config": {
-            "model": "+".join(f"{k}(nb={v['nb']})" for k, v in results.items()) + f" n={n}",
+            "model": "+".join(f"{k}(nb={v['nb']}" + (f", {v['grid']}" if v["grid"] != f"{p}x{q}" else "") + ")"
+                              for k, v in results.items()) + f" n={n}",
             "global_batch": 1,
             "seq_len": n,
             "parallelism": (f"2d-block-cyclic {p}x{q} (one process per GPU, {comm['backend']})" if world > 1

@@ -76,16 +76,18 @@ bool g_aborted = false;
 /// without asking, the root's message number rm and with it the staging slot
 /// rm % kStage and event slot rm % kRing.  One broadcast:
 ///   root:     (slot reuse) waits until every receiver has issued its copy out
-///             of the slot's previous message and makes its stream wait on
-///             each receiver's latest copy; copies the message into the
+///             of the slot's previous message and (host) until each
+///             receiver's latest copy has finished; copies the message into the
 ///             staging slot on its stream, records ready[rm % kRing],
 ///             publishes (seq, bytes) -- and returns: its buffer is free;
 ///   receiver: waits (host) for the root's seq, then on its single copy
-///             stream: after the caller's stream (buffer reuse) and the
-///             root's ready event, PULLS the bytes with one hipMemcpyAsync
+///             stream: once the root's ready event has completed (host
+///             query) and after the caller's stream (buffer reuse), PULLS the bytes with one hipMemcpyAsync
 ///             from the mapped staging buffer -- an SDMA copy over xGMI, no
 ///             kernel on the CUs the trailing GEMM is using -- records its
-///             done event; the caller's stream waits on it.
+///             interprocess done event (for the root) and a plain event the
+///             caller's stream waits on.  Interprocess events are only
+///             queried (host_wait), never waited on by a stream.
 /// One copy stream per receiver makes "latest done event complete" imply
 /// every earlier copy complete, which is what the root's slot reuse needs.
 /// The host of the root waits only when the receivers lag kStage of its
@@ -156,6 +158,7 @@ public:
                     slate_hip_call(hipIpcGetEventHandle(&me.ready_ev[i], ready_[i]));
                     slate_hip_call(hipIpcGetEventHandle(&me.done_ev[i], done_[i]));
                     slate_hip_call(hipEventCreateWithFlags(&fork_[i], hipEventDisableTiming));
+                    slate_hip_call(hipEventCreateWithFlags(&local_[i], hipEventDisableTiming));
                 }
                 slate_hip_call(hipStreamCreateWithFlags(&cs_, hipStreamNonBlocking));
                 for (int j = 0; j < kStage; ++j) grow(j, size_t(1) << 20);   // 1 MiB to start
@@ -210,7 +213,9 @@ public:
                     if (r == rank_) continue;
                     spin([&] { return B.r[r].done_seq.load(std::memory_order_acquire) >= prev; });
                     const int ld = B.r[r].last_done.load(std::memory_order_acquire);
-                    if (ld >= 0) slate_hip_call(hipStreamWaitEvent(s, imported(r, ld, false), 0));
+                    if (ld < 0) continue;
+                    // kStage messages later that copy has almost always finished
+                    host_wait(imported(r, ld, false));
                 }
             }
             if (bytes > stage_cap_[j]) grow(j, bytes);
@@ -230,10 +235,11 @@ public:
         ++recv_;
         slate_hip_call(hipEventRecord(fork_[f], s));              // buf's earlier users on the caller's stream
         slate_hip_call(hipStreamWaitEvent(cs_, fork_[f], 0));
-        slate_hip_call(hipStreamWaitEvent(cs_, imported(root, e, true), 0));
+        host_wait(imported(root, e, true));                        // the root's staging copy
         slate_hip_call(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToDevice, cs_));
-        slate_hip_call(hipEventRecord(done_[f], cs_));
-        slate_hip_call(hipStreamWaitEvent(s, done_[f], 0));
+        slate_hip_call(hipEventRecord(done_[f], cs_));         // for the root (interprocess)
+        slate_hip_call(hipEventRecord(local_[f], cs_));        // for this process's stream
+        slate_hip_call(hipStreamWaitEvent(s, local_[f], 0));
         me.last_done.store(f, std::memory_order_release);
         me.done_seq.store(seq, std::memory_order_release);
     }
@@ -250,6 +256,18 @@ private:
                 throw CommException("SLATE_BCAST=peer: a peer did not arrive within 600 s", __func__, __FILE__,
                                     __LINE__);
         }
+    }
+    /// Host-side wait for an interprocess event.  A stream wait on an
+    /// imported event that is still pending fails on this runtime with
+    /// "invalid argument" (seen on the 2-rank bench rig, rccl_comm r6 notes),
+    /// while queries are reliable: poll, on this rank's comm lane only.
+    void host_wait(hipEvent_t ev) {
+        spin([&] {
+            const hipError_t q = hipEventQuery(ev);
+            if (q == hipSuccess) return true;
+            if (q != hipErrorNotReady) slate_hip_call(q);
+            return false;
+        });
     }
     /// (re)allocate and export my staging buffer j; an outgrown buffer stays
     /// allocated (receivers may still read it; sizes only grow, so this
@@ -294,7 +312,7 @@ private:
     uint64_t seq_ = 0, recv_ = 0, stage_ids_ = 0;
     std::vector<uint64_t> count_;                 // messages rooted at each rank so far
     uint64_t stage_seq_[kStage] = {};
-    hipEvent_t ready_[kRing] = {}, done_[kRing] = {}, fork_[kRing] = {};
+    hipEvent_t ready_[kRing] = {}, done_[kRing] = {}, fork_[kRing] = {}, local_[kRing] = {};
     hipStream_t cs_ = nullptr;                    // my single copy stream (receiver)
     char* stage_[kStage] = {};
     size_t stage_cap_[kStage] = {};
