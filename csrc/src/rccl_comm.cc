@@ -76,18 +76,19 @@ bool g_aborted = false;
 /// without asking, the root's message number rm and with it the staging slot
 /// rm % kStage and event slot rm % kRing.  One broadcast:
 ///   root:     (slot reuse) waits until every receiver has issued its copy out
-///             of the slot's previous message and (host) until each
-///             receiver's latest copy has finished; copies the message into the
+///             of the slot's previous message and (wait_ipc) on each
+///             receiver's latest copy; copies the message into the
 ///             staging slot on its stream, records ready[rm % kRing],
 ///             publishes (seq, bytes) -- and returns: its buffer is free;
 ///   receiver: waits (host) for the root's seq, then on its single copy
-///             stream: once the root's ready event has completed (host
-///             query) and after the caller's stream (buffer reuse), PULLS the bytes with one hipMemcpyAsync
+///             stream: after the root's ready event (wait_ipc) and the
+///             caller's stream (buffer reuse), PULLS the bytes with one hipMemcpyAsync
 ///             from the mapped staging buffer -- an SDMA copy over xGMI, no
 ///             kernel on the CUs the trailing GEMM is using -- records its
 ///             interprocess done event (for the root) and a plain event the
-///             caller's stream waits on.  Interprocess events are only
-///             queried (host_wait), never waited on by a stream.
+///             caller's stream waits on.  Waits on interprocess events go
+///             through wait_ipc (query, stream wait, host poll as the last
+///             resort).
 /// One copy stream per receiver makes "latest done event complete" imply
 /// every earlier copy complete, which is what the root's slot reuse needs.
 /// The host of the root waits only when the receivers lag kStage of its
@@ -215,7 +216,7 @@ public:
                     const int ld = B.r[r].last_done.load(std::memory_order_acquire);
                     if (ld < 0) continue;
                     // kStage messages later that copy has almost always finished
-                    host_wait(imported(r, ld, false));
+                    wait_ipc(s, imported(r, ld, false));
                 }
             }
             if (bytes > stage_cap_[j]) grow(j, bytes);
@@ -235,7 +236,7 @@ public:
         ++recv_;
         slate_hip_call(hipEventRecord(fork_[f], s));              // buf's earlier users on the caller's stream
         slate_hip_call(hipStreamWaitEvent(cs_, fork_[f], 0));
-        host_wait(imported(root, e, true));                        // the root's staging copy
+        wait_ipc(cs_, imported(root, e, true));                    // the root's staging copy
         slate_hip_call(hipMemcpyAsync(buf, src, bytes, hipMemcpyDeviceToDevice, cs_));
         slate_hip_call(hipEventRecord(done_[f], cs_));         // for the root (interprocess)
         slate_hip_call(hipEventRecord(local_[f], cs_));        // for this process's stream
@@ -257,13 +258,21 @@ private:
                                     __LINE__);
         }
     }
-    /// Host-side wait for an interprocess event.  A stream wait on an
-    /// imported event that is still pending fails on this runtime with
-    /// "invalid argument" (seen on the 2-rank bench rig, rccl_comm r6 notes),
-    /// while queries are reliable: poll, on this rank's comm lane only.
-    void host_wait(hipEvent_t ev) {
+    /// Make stream `s` wait for an interprocess event.  A completed event
+    /// needs nothing.  A stream wait on an imported event that is still
+    /// pending failed on the shared-GPU rig with "invalid argument"
+    /// (profiles/r6_bench_verify.txt); then the host polls it instead -- on
+    /// this rank's comm lane only, and only in that case, since a host that
+    /// blocks on GPU progress can deadlock against collectives that other
+    /// ranks have not issued yet.
+    void wait_ipc(hipStream_t s, hipEvent_t ev) {
+        hipError_t q = hipEventQuery(ev);
+        if (q == hipSuccess) return;
+        if (q != hipErrorNotReady) slate_hip_call(q);
+        if (hipStreamWaitEvent(s, ev, 0) == hipSuccess) return;
+        (void)hipGetLastError();
         spin([&] {
-            const hipError_t q = hipEventQuery(ev);
+            q = hipEventQuery(ev);
             if (q == hipSuccess) return true;
             if (q != hipErrorNotReady) slate_hip_call(q);
             return false;
