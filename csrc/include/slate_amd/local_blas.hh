@@ -47,6 +47,16 @@ private:
 };
 
 // ---------------- BLAS-3
+/// While alive on this thread, device NN gemms with K in (1000, 2048] and
+/// m, n >= 8192 run as TN on a packed copy of A (SUMMA steps: the copy is
+/// amortized over a large output; profiles/r6_gemm_pack_a_k.txt).
+struct PackAHint {
+    PackAHint();
+    ~PackAHint();
+    PackAHint(PackAHint const&) = delete;
+    PackAHint& operator=(PackAHint const&) = delete;
+};
+
 template <typename T>
 void gemm(Ctx const& c, Op opA, Op opB, int64_t m, int64_t n, int64_t k, T alpha,
           T const* A, int64_t lda, T const* B, int64_t ldb, T beta, T* C, int64_t ldc);

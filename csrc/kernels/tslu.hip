@@ -511,6 +511,44 @@ __device__ inline uint32_t wave_max_key(uint32_t k) {
     return max(max(a, b), max(c, d));
 }
 
+// the same with the cross-row stages as DPP row broadcasts (gfx9 row_bcast:15
+// into rows 1 and 3, row_bcast:31 into rows 2 and 3): lane 63 ends with the
+// wave max, ONE readlane instead of four plus three scalar maxes
+__device__ inline uint32_t wave_max_key_bcast(uint32_t k) {
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x124, 0xF, 0xF, true));   // row_ror:4
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x128, 0xF, 0xF, true));   // row_ror:8
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x142, 0xA, 0xF, false));   // row_bcast:15
+    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp((int)k, (int)k, 0x143, 0xC, 0xF, false));   // row_bcast:31
+    return __builtin_amdgcn_readlane(k, 63);
+}
+
+// one wave-row publish of columns [K, TW) with 16-byte LDS stores (the
+// single-lane ds_write_b64 per element was the step's longest part,
+// profiles/r5_tslu_v2.txt): all values first (opaque() pins them, and a
+// store between two asm statements cannot be paired), then the stores
+template <int K, typename T>
+__device__ inline void publish_row(T* dst, const T (&v)[TW]) {
+    if constexpr (!is_cplx<T>::value && (sizeof(T) == 8 || sizeof(T) == 4)) {
+        constexpr int VEC = 16 / sizeof(T);
+        using V = T __attribute__((ext_vector_type(VEC)));
+        constexpr int J0 = (K + VEC - 1) / VEC * VEC;
+        #pragma unroll
+        for (int j = K; j < J0 && j < TW; ++j) dst[j] = v[j];
+        #pragma unroll
+        for (int j = J0; j + VEC <= TW; j += VEC) {
+            V x;
+            #pragma unroll
+            for (int e = 0; e < VEC; ++e) x[e] = v[j + e];
+            *reinterpret_cast<V*>(dst + j) = x;
+        }
+    } else {
+        #pragma unroll
+        for (int j = K; j < TW; ++j) dst[j] = v[j];
+    }
+}
+
 #ifdef TSLU_PROBE
 __device__ long long g_tslu_probe[128];
 #define TSLU_T(slot)                                                                      \
@@ -530,7 +568,7 @@ __device__ long long g_tslu_probe[128];
 // WPE: waves per SIMD the kernel is compiled for (register budget 512 / WPE
 // per lane); the fp32 R = 2 variant asks for 4 (<= 128 VGPRs), so its waves
 // can start beside the trailing fp32 GEMM's
-template <typename T, int R, int WPE = 1>
+template <typename T, int R, int WPE = 1, bool FAST = true>
 __global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* A) {
     SLATE_PANEL_WAVE_PRIO();
     constexpr int NT = T2_NT, NW = NT / 64, S = NT * R, F = S / TW;
@@ -610,7 +648,7 @@ __global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* 
                     if (key > kt) { kt = key; bi = i; }
                 }
                 TSLU_S(k, 0);
-                const uint32_t kw = wave_max_key(kt);
+                const uint32_t kw = FAST ? wave_max_key_bcast(kt) : wave_max_key(kt);
                 TSLU_S(k, 1);
                 if (kw != 0u) {
                     const unsigned long long win = __ballot(kt == kw);
@@ -622,8 +660,15 @@ __global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* 
                                 // branches would read a dynamically indexed a[bi][j],
                                 // which demotes a[][] to scratch memory
                                 srec[bf][w] = make_int4((int)kw, tid * R + i, opaque(idx[i]), 0);
-                                #pragma unroll
-                                for (int j = k; j < TW; ++j) srow[bf][w][j] = opaque(a[i][j]);
+                                if constexpr (FAST) {
+                                    T v[TW];
+                                    #pragma unroll
+                                    for (int j = k; j < TW; ++j) v[j] = opaque(a[i][j]);
+                                    publish_row<k>(&srow[bf][w][0], v);
+                                } else {
+                                    #pragma unroll
+                                    for (int j = k; j < TW; ++j) srow[bf][w][j] = opaque(a[i][j]);
+                                }
                             }
                         });
                     }
@@ -934,7 +979,7 @@ static bool tslu_use_v2() {
 }
 
 template <typename T, int R = Tslu2Rows<T>::R, int WPE = 1>
-static void tslu2_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
+static void tslu2_narrow_launch(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
                          int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
     constexpr int S = T2_NT * R;
     const int64_t rows = m - r;
@@ -953,7 +998,13 @@ static void tslu2_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64
     p.cand = p.ccnt + items + 1;
     p.slab = work + kT2Cnt + (items + items * TW + 2) / 2 + 2;
     p.ipiv = ipiv; p.info = info; p.info_offset = info_offset;
-    hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
+    // SLATE_TSLU_FAST=0: the round-5 step (four-readlane wave max, 8-byte publish)
+    static const bool fast = [] {
+        const char* e = std::getenv("SLATE_TSLU_FAST");
+        return !e || std::atoi(e) != 0;
+    }();
+    if (fast) hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE, true>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
+    else hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE, false>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
     if (hipError_t e = hipGetLastError(); e != hipSuccess)
         throw std::runtime_error(std::string("tslu tree kernel launch: ") + hipGetErrorString(e));
     const int64_t c0 = (Ablk - Apanel) / lda;
@@ -979,11 +1030,11 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
         }();
         if constexpr (std::is_same<T, float>::value) {
             if (f32_small) {
-                tslu2_narrow<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
+                tslu2_narrow_launch<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
                 return;
             }
         }
-        tslu2_narrow<T>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
+        tslu2_narrow_launch<T>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
         return;
     }
     const int64_t nleaf_max = (rows + TR - 1) / TR;

@@ -244,6 +244,7 @@ void gemmC(T alpha, Matrix<T> const& A_in, Matrix<T> const& B_in, T beta, Matrix
         // no panel chain to protect: the GEMMs take every CU (device::full_queue)
         S.task(gq, {tBc}, {Sched::tok(9, 0)}, [&, Ak, ldak, Bk, ldbk, K, bk](lb::Ctx const& c) {
             trace::Block t2("gemm_update");
+            lb::PackAHint tn;   // K = summa_k steps: TN on a packed A beats NT on a copied B
             lb::gemm(c, Op::NoTrans, Op::NoTrans, lc.m, lc.n, K, alpha, Ak, ldak, Bk, ldbk, bk, lc.ptr, lc.ld);
         });
     }

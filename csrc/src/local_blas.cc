@@ -117,6 +117,36 @@ void dgemm_splitk(hipStream_t s, char ta, char tb, int64_t m, int64_t n, int64_t
     kd::splitk_reduce<T>(m, n, int(splits), P, alpha, beta, C, ldc, s);
 }
 
+/// Does an NN product run as TN on a packed copy of A?  Always above K =
+/// 2048; under a PackAHint (gemmC's SUMMA steps) also for K in
+/// (SLATE_GEMM_PACK_A_MINK = 1000, 2048] when m, n >= 8192: the step GEMM
+/// 32768 x 16384 x 2048 68.2 -> 69.2-69.7 TFLOP/s, 65536^2 x 1024 66.6 ->
+/// 68.6, copies included; not for the factorizations' chunked updates
+/// (dgeqrf 60.1 -> 59.8) (profiles/r6_gemm_pack_a_k.txt).  Otherwise NT on a
+/// copy of B.
+thread_local int t_pack_a_hint = 0;
+inline int64_t pack_a_mink() {
+    static const int64_t v = [] {
+        const char* e = std::getenv("SLATE_GEMM_PACK_A_MINK");
+        return e ? std::atoll(e) : int64_t(1000);
+    }();
+    return v;
+}
+inline bool pack_a_on() {
+    static const bool v = [] {
+        const char* e = std::getenv("SLATE_GEMM_PACK_A");
+        return e ? std::atoi(e) != 0 : true;
+    }();
+    return v;
+}
+inline bool pack_a_form(int64_t m, int64_t n, int64_t k) {
+    if (k > 2048) return m >= 4096 && n >= 4096;
+    return t_pack_a_hint > 0 && k > pack_a_mink() && m >= 8192 && n >= 8192;
+}
+}  // namespace
+slate::lb::PackAHint::PackAHint() { ++t_pack_a_hint; }
+slate::lb::PackAHint::~PackAHint() { --t_pack_a_hint; }
+namespace {
 // SLATE_UPDATE_NT=0 keeps NN products in NN form (as internal::update_nt)
 inline bool nt_pack() {
     static const bool v = [] {
@@ -166,7 +196,7 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
         // (the copy is n x k <= n x 2048: bounded scratch, stream-ordered
         // reuse, so steady-state calls never reach hipMalloc)
         if (uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && nt_pack() && m >= 4096 &&
-            n >= 1024 && k >= 256 && k <= 2048) {
+            n >= 1024 && k >= 256 && k <= 2048 && !(pack_a_on() && pack_a_form(m, n, k))) {
             const size_t bytes = size_t(n) * size_t(k) * sizeof(T);
             T* Bt = static_cast<T*>(device::malloc_async(bytes, s));
             kd::gecopy<T, T>('G', 'T', n, k, B, ldb, Bt, n, s);
@@ -182,11 +212,7 @@ void dgemm(hipStream_t s, char uplo, Op opA, Op opB, int64_t m, int64_t n, int64
         // The copy is made in K slices of at most pack_bytes() (default
         // 8 GiB; later slices accumulate with beta = 1), so the scratch is
         // bounded independently of k and of the free HBM.
-        static const bool pack_a = [] {
-            const char* e = std::getenv("SLATE_GEMM_PACK_A");
-            return e ? std::atoi(e) != 0 : true;
-        }();
-        if (pack_a && uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && k > 2048 && m >= 4096 && n >= 4096) {
+        if (pack_a_on() && uplo == 'G' && ta == 'N' && tb == 'N' && sizeof(T) == 8 && pack_a_form(m, n, k)) {
             const char* be = std::getenv("SLATE_GEMM_PACK_BYTES");
             const size_t budget = be ? size_t(std::atoll(be)) : (size_t(8) << 30);
             const int64_t kc = std::min<int64_t>(k, std::max<int64_t>(2048, int64_t(budget / (size_t(m) * sizeof(T))) / 256 * 256));
