@@ -51,12 +51,15 @@ ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
 # the 8-GPU critical-path sweep (profiles/r6_critpath_8gpu_sweep.txt, 32
 # reserved CUs, copy-engine broadcasts) predicts QR 308 / Cholesky 279
 # TFLOP/s on 4 x 2 against 275 / 250 on 2 x 4, LU best on 2 x 4 with nb 256
-GRID_PER = {8: {"dgeqrf": (4, 2), "dpotrf": (4, 2)}}
+# (the BASELINE configs 3-5 keep the reference's 2 x 4)
+GRID_PER = {8: {"dgeqrf": (4, 2), "dpotrf": (4, 2), "cfg4_dgeqrf_nb256": (2, 4)}}
 # BASELINE.json configs beyond the 4-routine headline suite (run after it,
 # reported under "configs"): name -> (routine, n or None = --dim, nb, target)
 EXTRAS = {
     "cfg1_dgemm_host_n2048_nb256": ("dgemm", 2048, 256, "h"),
     "cfg2_dpotrf_n32768_nb512": ("dpotrf", -2, 512, None),       # -2: half of --dim (32768 at the default)
+    # config 3: the reference's 8-GPU tournament LU, 2 x 4, nb 512 (multi-GPU jobs only)
+    "cfg3_dgetrf_tntpiv_nb512": ("dgetrf", None, 512, None),
     "cfg4_dgeqrf_nb256": ("dgeqrf", None, 256, None),
     "cfg5_dgesv_mixed": ("dgesv_mixed", None, None, None),
     # the reference's semantics (src/gesv_mixed.cc:219-279): classical
@@ -507,6 +510,8 @@ def main(a):
         tg_ = tg_ or target
         if tg_ == "h" and world > 1:
             continue   # config 1 is a one-process host-target plumbing check
+        if name.startswith("cfg3") and world == 1:
+            continue   # config 3 is the 2 x 4 LU (the 1-GPU suite's dgetrf covers one GPU)
         nb_ = nb_per.get(name) or nb_ or nb_per.get(rname, a.nb)   # --nb-per <extra name>=nb overrides
         n_ = n if n_ is None else (n // 2 if n_ == -2 else n_)
         fl = {"dgemm": F.gemm_flops(n_, n_, n_), "dpotrf": F.potrf_flops(n_), "dgeqrf": F.geqrf_flops(n_)}.get(
