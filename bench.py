@@ -47,12 +47,28 @@ def _import_slate():
 
 METRIC = "fp64 TFLOP/s (whole node) for dgemm / dpotrf / dgetrf / dgeqrf, n=64k, at 1/2/4/8 MI355X"
 ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
-# per-routine grid shapes by world size (none: the job's p x q for all):
-# the 8-GPU critical-path sweep (profiles/r6_critpath_8gpu_sweep.txt, 32
-# reserved CUs, copy-engine broadcasts) predicts QR 308 / Cholesky 279
-# TFLOP/s on 4 x 2 against 275 / 250 on 2 x 4, LU best on 2 x 4 with nb 256
-# (the BASELINE configs 3-5 keep the reference's 2 x 4)
-GRID_PER = {8: {"dgeqrf": (4, 2), "dpotrf": (4, 2), "cfg4_dgeqrf_nb256": (2, 4)}}
+# Per-routine grid shapes and tile sizes by world size (absent: the job's
+# p x q / --nb), chosen with the critical-path model (32 reserved CUs,
+# copy-engine broadcasts; profiles/r6_critpath_8gpu_sweep.txt,
+# profiles/r6_critpath_2_4gpu_sweep.txt), predicted whole-job TFLOP/s:
+#   8: LU 2 x 4 nb 256 (170), QR 8 x 1 nb 512 (337; 4 x 2: 308), Cholesky
+#      4 x 2 nb 512 (279; 8 x 1: 220)
+#   4: LU 2 x 2 nb 512 (133), QR 4 x 1 nb 1024 (187; 2 x 2: 170), Cholesky
+#      4 x 1 nb 1024 (167; 2 x 2: 160)
+#   2: everything 2 x 1 (1 x 2 is 5-10 % lower): LU nb 1024 (90; the p > 1
+#      LU takes tiles <= 1024), QR nb 1024 (97), Cholesky nb 1536 (97)
+# The BASELINE configs 3-5 keep the reference's 2 x 4.
+GRID_PER = {
+    2: {"dgetrf": (2, 1), "dpotrf": (2, 1), "dgeqrf": (2, 1)},
+    4: {"dgeqrf": (4, 1), "dpotrf": (4, 1)},
+    8: {"dgeqrf": (8, 1), "dpotrf": (4, 2), "cfg4_dgeqrf_nb256": (2, 4)},
+}
+NB_PER_WORLD = {
+    1: {"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024},
+    2: {"dgetrf": 1024, "dpotrf": 1536, "dgeqrf": 1024},
+    4: {"dgetrf": 512, "dpotrf": 1024, "dgeqrf": 1024},
+    8: {"dgetrf": 256},
+}
 # BASELINE.json configs beyond the 4-routine headline suite (run after it,
 # reported under "configs"): name -> (routine, n or None = --dim, nb, target)
 EXTRAS = {
@@ -267,8 +283,8 @@ def main(a):
     # Round 5 (single-wave leaf kernels make wide diagonal blocks cheap):
     # dpotrf 1536 vs 1024 62.7-63.0 -> 63.3-63.4, dgeqrf 1024 vs 512 59.2 ->
     # 59.8-59.9 TFLOP/s, interleaved on one box (profiles/r5_nb_ab.txt).
-    default_nb = ({"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024} if world == 1
-                  else {"dgetrf": 256})   # p x q: the LU panel chain shrinks with nb (r6 sweep)
+    # p x q: NB_PER_WORLD (the critical-path sweeps; at 8 the LU chain shrinks with nb)
+    default_nb = dict(NB_PER_WORLD.get(world, {"dgetrf": 256}))
     if a.nb:
         default_nb = {}
     a.nb = a.nb or 512
