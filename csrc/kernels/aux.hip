@@ -9,6 +9,7 @@
 // each thread handles several columns.
 #include "device_common.hh"
 #include "kernels.hh"
+#include "slate_amd/device.hh"
 #include "leaf_common.hh"
 
 #include <cstdlib>
@@ -805,10 +806,15 @@ void gescale_row_col(int64_t m, int64_t n, const real_t<T>* R, const real_t<T>* 
 // 32768 x 512 tournament panel 2.88 -> 2.66 ms) but the 1-GPU dgetrf, whose
 // panel runs beside the trailing GEMM, measured 55.9 against 59.0-59.1
 // TFLOP/s with them (same box, interleaved runs, profiles/r5_small_solve_ab.txt).
+// With CUs reserved for the panel queues (the one-process-per-GPU default)
+// the panel no longer waits for GEMM slots and the stream kernels win: 2 x 4
+// LU model 170.8 / 173.4 -> 174.1 / 177.6 TFLOP/s (profiles/r6_redecide.txt),
+// so they are the default there.
 inline bool small_solve_v1() {
     static const bool v = [] {
         const char* e = std::getenv("SLATE_SMALL_SOLVE");
-        return !(e && std::atoi(e) == 2);
+        if (e) return std::atoi(e) != 2;
+        return slate::device::reserved_cus() == 0;
     }();
     return v;
 }
