@@ -55,6 +55,10 @@ def test_bench_self_launch_4_ranks():
     assert comm["world"] == 4 and comm["row"] * comm["col"] == 4 and comm["grid"] == [2, 2]
     assert comm["launcher"] == "self" and len(comm["devices"]) == 4
     assert all(v["check"] == "pass" for v in line["routines"].values())
+    # per-routine grids of the 4-GPU defaults (bench.GRID_PER, from the
+    # critical-path sweep): QR and Cholesky on 4 x 1, the rest on the job's 2 x 2
+    grids = {k: v["grid"] for k, v in line["routines"].items()}
+    assert grids == {"dgemm": "2x2", "dpotrf": "4x1", "dgetrf": "2x2", "dgeqrf": "4x1"}, grids
 
 
 def test_bench_self_launch_propagates_failure():
