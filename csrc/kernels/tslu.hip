@@ -500,21 +500,11 @@ template <typename R> __device__ inline void st_sc1(cplx<R>* q, cplx<R> v) {
 }
 
 // wave max of a 32-bit key: DPP with bound_ctrl (0 is the identity), so each
-// stage folds into one v_max_u32_dpp
+// stage folds into one v_max_u32_dpp; the cross-row stages are DPP row
+// broadcasts (gfx9 row_bcast:15 into rows 1 and 3, row_bcast:31 into rows 2
+// and 3): lane 63 ends with the wave max, ONE readlane instead of four plus
+// three scalar maxes
 __device__ inline uint32_t wave_max_key(uint32_t k) {
-    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
-    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
-    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x124, 0xF, 0xF, true));   // row_ror:4
-    k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x128, 0xF, 0xF, true));   // row_ror:8
-    uint32_t a = __builtin_amdgcn_readlane(k, 0), b = __builtin_amdgcn_readlane(k, 16);
-    uint32_t c = __builtin_amdgcn_readlane(k, 32), d = __builtin_amdgcn_readlane(k, 48);
-    return max(max(a, b), max(c, d));
-}
-
-// the same with the cross-row stages as DPP row broadcasts (gfx9 row_bcast:15
-// into rows 1 and 3, row_bcast:31 into rows 2 and 3): lane 63 ends with the
-// wave max, ONE readlane instead of four plus three scalar maxes
-__device__ inline uint32_t wave_max_key_bcast(uint32_t k) {
     k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0xB1, 0xF, 0xF, true));    // quad_perm [1,0,3,2]
     k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x4E, 0xF, 0xF, true));    // quad_perm [2,3,0,1]
     k = max(k, (uint32_t)__builtin_amdgcn_update_dpp(0, (int)k, 0x124, 0xF, 0xF, true));   // row_ror:4
@@ -568,10 +558,14 @@ __device__ long long g_tslu_probe[128];
 // WPE: waves per SIMD the kernel is compiled for (register budget 512 / WPE
 // per lane); the fp32 R = 2 variant asks for 4 (<= 128 VGPRs), so its waves
 // can start beside the trailing fp32 GEMM's
-template <typename T, int R, int WPE = 1, bool FAST = true>
-__global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* A) {
+// NT: threads per workgroup (256: a GEMM workgroup's slot, so a leaf starts
+// beside the trailing update; 512: twice the rows per leaf, fan-in 32, one
+// tree level fewer for panels up to 32 K rows -- for CUs kept free of the
+// update, SLATE_TSLU_NT)
+template <typename T, int R, int WPE = 1, int NT = T2_NT>
+__global__ __launch_bounds__(NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* A) {
     SLATE_PANEL_WAVE_PRIO();
-    constexpr int NT = T2_NT, NW = NT / 64, S = NT * R, F = S / TW;
+    constexpr int NW = NT / 64, S = NT * R, F = S / TW;
     constexpr bool kReal = !is_cplx<T>::value;
     __shared__ int4 srec[2][NW];                 // {key, thread*R + row, global row, -}
     __shared__ alignas(16) T srow[2][NW][TW];    // each wave's best row: columns k ..
@@ -648,7 +642,7 @@ __global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* 
                     if (key > kt) { kt = key; bi = i; }
                 }
                 TSLU_S(k, 0);
-                const uint32_t kw = FAST ? wave_max_key_bcast(kt) : wave_max_key(kt);
+                const uint32_t kw = wave_max_key(kt);
                 TSLU_S(k, 1);
                 if (kw != 0u) {
                     const unsigned long long win = __ballot(kt == kw);
@@ -660,15 +654,10 @@ __global__ __launch_bounds__(T2_NT, WPE) void tslu2_tree_kernel(Tslu2Args p, T* 
                                 // branches would read a dynamically indexed a[bi][j],
                                 // which demotes a[][] to scratch memory
                                 srec[bf][w] = make_int4((int)kw, tid * R + i, opaque(idx[i]), 0);
-                                if constexpr (FAST) {
-                                    T v[TW];
-                                    #pragma unroll
-                                    for (int j = k; j < TW; ++j) v[j] = opaque(a[i][j]);
-                                    publish_row<k>(&srow[bf][w][0], v);
-                                } else {
-                                    #pragma unroll
-                                    for (int j = k; j < TW; ++j) srow[bf][w][j] = opaque(a[i][j]);
-                                }
+                                T v[TW];
+                                #pragma unroll
+                                for (int j = k; j < TW; ++j) v[j] = opaque(a[i][j]);
+                                publish_row<k>(&srow[bf][w][0], v);
                             }
                         });
                     }
@@ -978,10 +967,10 @@ static bool tslu_use_v2() {
     return std::is_same<T, double>::value || std::is_same<T, float>::value;
 }
 
-template <typename T, int R = Tslu2Rows<T>::R, int WPE = 1>
+template <typename T, int R = Tslu2Rows<T>::R, int WPE = 1, int NT = T2_NT>
 static void tslu2_narrow_launch(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, int64_t ncols,
                          int64_t* ipiv, int64_t* perm, int* info, int64_t info_offset, int64_t* work, hipStream_t s) {
-    constexpr int S = T2_NT * R;
+    constexpr int S = NT * R;
     const int64_t rows = m - r;
     Tslu2Args p;
     p.m = m; p.r = r; p.lda = lda; p.nn = nn;
@@ -998,13 +987,7 @@ static void tslu2_narrow_launch(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel
     p.cand = p.ccnt + items + 1;
     p.slab = work + kT2Cnt + (items + items * TW + 2) / 2 + 2;
     p.ipiv = ipiv; p.info = info; p.info_offset = info_offset;
-    // SLATE_TSLU_FAST=0: the round-5 step (four-readlane wave max, 8-byte publish)
-    static const bool fast = [] {
-        const char* e = std::getenv("SLATE_TSLU_FAST");
-        return !e || std::atoi(e) != 0;
-    }();
-    if (fast) hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE, true>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
-    else hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE, false>), dim3(p.nleaf), dim3(T2_NT), 0, s, p, Ablk);
+    hipLaunchKernelGGL((tslu2_tree_kernel<T, R, WPE, NT>), dim3(p.nleaf), dim3(NT), 0, s, p, Ablk);
     if (hipError_t e = hipGetLastError(); e != hipSuccess)
         throw std::runtime_error(std::string("tslu tree kernel launch: ") + hipGetErrorString(e));
     const int64_t c0 = (Ablk - Apanel) / lda;
@@ -1031,6 +1014,18 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
         if constexpr (std::is_same<T, float>::value) {
             if (f32_small) {
                 tslu2_narrow_launch<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
+                return;
+            }
+        }
+        // SLATE_TSLU_NT=512: 512-thread tree workgroups (fp64)
+        static const int nt = [] {
+            const char* e = std::getenv("SLATE_TSLU_NT");
+            return e ? std::atoi(e) : T2_NT;
+        }();
+        if constexpr (std::is_same<T, double>::value) {
+            if (nt == 512) {
+                tslu2_narrow_launch<T, Tslu2Rows<T>::R, 1, 512>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info,
+                                                                info_offset, work, s);
                 return;
             }
         }
