@@ -26,6 +26,7 @@
 //           v_mfma_f64_16x16x4 for fp64, 16-row slabs per wave.
 #include "device_common.hh"
 #include "kernels.hh"
+#include "slate_amd/device.hh"
 
 #include <algorithm>
 #include <climits>
@@ -1017,10 +1018,16 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
                 return;
             }
         }
-        // SLATE_TSLU_NT=512: 512-thread tree workgroups (fp64)
+        // SLATE_TSLU_NT: tree workgroup size (fp64).  512 by default when CUs
+        // are reserved for the panel queues (the one-process-per-GPU default):
+        // whole-CU leaves then find free CUs, and the tree is one level
+        // shallower -- 2 x 4 / nb 256 LU model 175.8 -> 188.0 TFLOP/s; 256
+        // otherwise, where a whole-CU leaf waits for the trailing GEMM to
+        // drain a CU (1-GPU dgetrf 59.0 -> 55.0) (profiles/r6_tslu_nt.txt)
         static const int nt = [] {
             const char* e = std::getenv("SLATE_TSLU_NT");
-            return e ? std::atoi(e) : T2_NT;
+            if (e) return std::atoi(e);
+            return slate::device::reserved_cus() > 0 ? 512 : T2_NT;
         }();
         if constexpr (std::is_same<T, double>::value) {
             if (nt == 512) {
