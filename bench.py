@@ -51,11 +51,12 @@ ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
 # p x q / --nb), chosen with the critical-path model (32 reserved CUs,
 # copy-engine broadcasts; profiles/r6_critpath_8gpu_sweep.txt,
 # profiles/r6_critpath_2_4gpu_sweep.txt), predicted whole-job TFLOP/s:
-#   8: LU 2 x 4 nb 256 (170), QR 8 x 1 nb 512 (337; 4 x 2: 308), Cholesky
-#      4 x 2 nb 512 (279; 8 x 1: 220)
-#   4: LU 2 x 2 nb 512 (133), QR 4 x 1 nb 1024 (187; 2 x 2: 170), Cholesky
+#   8: LU 2 x 4 nb 512 (193-194 with the 512-thread tournament tree; nb 256:
+#      185-187, profiles/r6_tslu_nt.txt), QR 8 x 1 nb 512 (337; 4 x 2: 308),
+#      Cholesky 4 x 2 nb 512 (279; 8 x 1: 220)
+#   4: LU 2 x 2 nb 512 (143), QR 4 x 1 nb 1024 (187; 2 x 2: 170), Cholesky
 #      4 x 1 nb 1024 (167; 2 x 2: 160)
-#   2: everything 2 x 1 (1 x 2 is 5-10 % lower): LU nb 1024 (90; the p > 1
+#   2: everything 2 x 1 (1 x 2 is 5-10 % lower): LU nb 1024 (92; the p > 1
 #      LU takes tiles <= 1024), QR nb 1024 (97), Cholesky nb 1536 (97)
 # The BASELINE configs 3-5 keep the reference's 2 x 4.
 GRID_PER = {
@@ -67,7 +68,7 @@ NB_PER_WORLD = {
     1: {"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024},
     2: {"dgetrf": 1024, "dpotrf": 1536, "dgeqrf": 1024},
     4: {"dgetrf": 512, "dpotrf": 1024, "dgeqrf": 1024},
-    8: {"dgetrf": 256},
+    8: {},
 }
 # BASELINE.json configs beyond the 4-routine headline suite (run after it,
 # reported under "configs"): name -> (routine, n or None = --dim, nb, target)
@@ -283,8 +284,8 @@ def main(a):
     # Round 5 (single-wave leaf kernels make wide diagonal blocks cheap):
     # dpotrf 1536 vs 1024 62.7-63.0 -> 63.3-63.4, dgeqrf 1024 vs 512 59.2 ->
     # 59.8-59.9 TFLOP/s, interleaved on one box (profiles/r5_nb_ab.txt).
-    # p x q: NB_PER_WORLD (the critical-path sweeps; at 8 the LU chain shrinks with nb)
-    default_nb = dict(NB_PER_WORLD.get(world, {"dgetrf": 256}))
+    # p x q: NB_PER_WORLD (the critical-path sweeps)
+    default_nb = dict(NB_PER_WORLD.get(world, {}))
     if a.nb:
         default_nb = {}
     a.nb = a.nb or 512
