@@ -1029,8 +1029,14 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
             if (e) return std::atoi(e);
             return slate::device::reserved_cus() > 0 ? 512 : T2_NT;
         }();
+        // SLATE_TSLU_NT512_ROWS: also 512 for panels of at most this many rows
+        // (a short panel's trailing update no longer fills the GPU)
+        static const int64_t nt512_rows = [] {
+            const char* e = std::getenv("SLATE_TSLU_NT512_ROWS");
+            return e ? std::atoll(e) : int64_t(0);
+        }();
         if constexpr (std::is_same<T, double>::value) {
-            if (nt == 512) {
+            if (nt == 512 || rows <= nt512_rows) {
                 tslu2_narrow_launch<T, Tslu2Rows<T>::R, 1, 512>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info,
                                                                 info_offset, work, s);
                 return;
