@@ -274,9 +274,11 @@ if "qr" in todo:
         U = tri(nb)
         Dm = rnd(nb, nb) + 4 * torch.eye(nb, dtype=torch.float64, device=dev)
         vhc, ap1, ap2 = Gemm(nb, nb, mr, ta="T"), Gemm(nb, nb, nb), Gemm(mr, nb, nb)
-        one = [Task("gram", lambda: ops.herk("U", "C", 1.0, Q, 0.0, G)),
-               Task("potrf", lambda X: ops.potrf("U", X), lambda: (D.clone(),)),
-               Task("trsm", lambda: ops.trsm("R", "U", "N", "N", 1.0, U, Q))]
+        # as the driver (qr.cc cholqr): Lower Gram, Lower Cholesky (the leaf
+        # kernel's path), Q L^-H
+        one = [Task("gram", lambda: ops.herk("L", "C", 1.0, Q, 0.0, G)),
+               Task("potrf", lambda X: ops.potrf("L", X), lambda: (D.clone(),)),
+               Task("trsm", lambda: ops.trsm("R", "L", "C", "N", 1.0, U, Q))]
         tasks = [Task(t.name + str(i), t.fn, t.setup) for i in range(2) for t in one]   # CholeskyQR2
         tasks += [host_wait_task(),
                   Task("hr_lu", lambda X: ops.lu_sign(X), lambda: (Dm.clone(),)),
