@@ -55,10 +55,27 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
     std::vector<Work<T>> W(R), Wt(R), Dk(R), Ws(R);
     const int64_t lcm = std::lcm(int64_t(p), int64_t(q));
     const int64_t maxcnt = ceildiv(nt, lcm) + 1;
+    // Transposed tiles arrive in two all-gathers: first the lookahead columns'
+    // (a prefix of every process row's list: c1(k) tiles, region 1 of Wt),
+    // so the next panel's update does not wait for the whole set; then the
+    // rest (region 2).  Same layout on every rank of the process column.
+    const int64_t la_tiles = std::max<int64_t>(la, 1);
+    const int64_t R1 = int64_t(p) * la_tiles * nb * nb;
+    auto c1_of = [&](int64_t k) {
+        int64_t c1 = 0;
+        std::vector<int64_t> cnt(p, 0);
+        for (int64_t J = k + 1; J < std::min(nt, k + 1 + la); ++J)
+            if (A.scol_owner(J) == mycol) c1 = std::max(c1, ++cnt[A.srow_owner(J)]);
+        return c1;
+    };
+    // element offset in Wt of tile idx of process row r's list at step k
+    auto toff = [&, R1](int64_t c1, int r, int64_t idx) -> int64_t {
+        return idx < c1 ? (int64_t(r) * c1 + idx) * nb * nb : R1 + (int64_t(r) * (maxcnt - c1) + idx - c1) * nb * nb;
+    };
     for (int r = 0; r < R; ++r) {
         if (q > 1) W[r].resize(target, size_t(std::max<int64_t>(mloc, 1)) * nb);
         if (p > 1) {
-            Wt[r].resize(target, size_t(p) * maxcnt * nb * nb);
+            Wt[r].resize(target, size_t(R1) + size_t(p) * maxcnt * nb * nb);
             Ws[r].resize(target, size_t(maxcnt) * nb * nb);
             Dk[r].resize(target, size_t(nb) * nb);
         }
@@ -88,13 +105,13 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
     if (stair && nlt > 0) {
         std::vector<int64_t> tab(size_t(nt) * nlt, 0);
         for (int64_t k = 0; k + 1 < nt; ++k) {
-            const int64_t lr_k1 = lrow_of(A, k + 1);
+            const int64_t lr_k1 = lrow_of(A, k + 1), c1 = c1_of(k);
             std::vector<int64_t> seen(p, 0);
             for (int64_t J = k + 1; J < nt; ++J) {
                 if (A.scol_owner(J) != mycol) continue;
                 const int64_t t = (lcol_of(A, J)) / nb;
                 const int r = A.srow_owner(J);
-                tab[size_t(k) * nlt + t] = (p == 1) ? lrow_of(A, J) - lr_k1 : (int64_t(r) * maxcnt + seen[r]) * nb * nb;
+                tab[size_t(k) * nlt + t] = (p == 1) ? lrow_of(A, J) - lr_k1 : toff(c1, r, seen[r]);
                 ++seen[r];
             }
         }
@@ -161,7 +178,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         T* akk = a + lr_k + lc_k * lda;          // diag tile (if mine)
         T* apan = a + lr_k1 + lc_k * lda;        // my rows below the diagonal
 
-        const int64_t tDiag = Sched::tok(5, slot), tBc = Sched::bcast(slot);
+        const int64_t tDiag = Sched::tok(5, slot), tBc = Sched::bcast(slot), tLa = Sched::tok(6, slot);
 
         // ---- panel: potrf(A(k,k))
         if (in_col && myrow == pk) {
@@ -199,24 +216,30 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         std::vector<std::vector<int64_t>> lists(p);
         for (int64_t J = k + 1; J < nt; ++J)
             if (A.scol_owner(J) == mycol) lists[A.srow_owner(J)].push_back(J);
-        S.task(qM, {Sched::col(k)}, {tBc}, [&, Wk, apan, mrows, kb, qk, slot, lists, lr_k1, ldW](lb::Ctx const& c) {
+        const int64_t c1 = p > 1 ? c1_of(k) : 0;
+        // pack my tiles [i0, i1) of my list (rows of Wk) and all-gather them
+        auto gather_t = [&, Wk, ldW, kb, slot, lists, lr_k1](lb::Ctx const& c, int64_t i0, int64_t i1, T* dst) {
+            if (i1 <= i0) return;
+            T* Sb = Ws[slot].data();
+            auto const& mine = lists[myrow];
+            for (int64_t i = i0; i < std::min<int64_t>(i1, int64_t(mine.size())); ++i) {
+                const int64_t J = mine[size_t(i)];
+                lb::copy2d(c, A.tileMb(J), kb, Wk + (lrow_of(A, J) - lr_k1), ldW, Sb + (i - i0) * nb * nb, nb);
+            }
+            colM.allgather(Sb, dst, size_t((i1 - i0) * nb * nb), scalar_type<T>(), c.loc(), c.stream);
+        };
+        // (tBc as an output too: the slot's W / Wt reuse waits for step k - R's trailing readers)
+        S.task(qM, {Sched::col(k)}, {tLa, tBc}, [&, Wk, apan, mrows, kb, qk, slot, c1, gather_t](lb::Ctx const& c) {
             trace::Block tb("bcast_panel");
             if (q > 1) {
                 if (mycol == qk) pack(c, mrows, kb, apan, lda, Wk);
                 bcast(rowM, Wk, size_t(mrows * kb), qk, c);
             }
-            if (p > 1) {
-                // pack my tiles (rows of Wk) for the column all-gather
-                T* Sb = Ws[slot].data();
-                int64_t cnt = 0;
-                for (int64_t J : lists[myrow]) {
-                    int64_t off = lrow_of(A, J) - lr_k1;
-                    int64_t jb = A.tileMb(J);
-                    lb::copy2d(c, jb, kb, Wk + off, ldW, Sb + cnt * nb * nb, nb);
-                    ++cnt;
-                }
-                colM.allgather(Sb, Wt[slot].data(), size_t(maxcnt * nb * nb), scalar_type<T>(), c.loc(), c.stream);
-            }
+            if (p > 1) gather_t(c, 0, c1, Wt[slot].data());             // the lookahead columns' tiles
+        });
+        S.task(qM, {tLa}, {tBc}, [&, slot, c1, gather_t, R1](lb::Ctx const& c) {
+            trace::Block tb("bcast_transposed");
+            if (p > 1) gather_t(c, c1, maxcnt, Wt[slot].data() + R1);   // the rest
         });
 
         // ---- trailing updates
@@ -262,7 +285,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
                     int r = A.srow_owner(J);
                     auto const& lst = lists[r];
                     int64_t idx = std::find(lst.begin(), lst.end(), J) - lst.begin();
-                    Bt = Wt[slot].data() + (int64_t(r) * maxcnt + idx) * nb * nb; ldB = nb;
+                    Bt = Wt[slot].data() + toff(c1_of(k), r, idx); ldB = nb;
                 }
                 T const* Ar = Wk + (rJ - lr_k1);
                 T* Cc = a + rJ + cJ * lda;
@@ -280,7 +303,7 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
         int64_t jla_end = std::min(nt, k + 1 + la);
         for (int64_t j = k + 1; j < jla_end; ++j) {
             int qi = device::kLookaheadQueue;
-            S.task(qi, {tBc}, {Sched::col(j)}, [&, update, j](lb::Ctx const& c) { update(c, j, j + 1); });
+            S.task(qi, {tLa}, {Sched::col(j)}, [&, update, j](lb::Ctx const& c) { update(c, j, j + 1); });
         }
         if (jla_end < nt) {
             std::vector<int64_t> outs;

@@ -325,7 +325,7 @@ if "chol" in todo:
         if q > 1:
             c += comm(mr * nb * 8)                                  # L panel along the row
         if p > 1:
-            c += comm(math.ceil(nc / nb) * nb * nb * 8 / max(q, 1))  # transposed tiles
+            c += comm(p * nb * nb * 8)                              # lookahead column's transposed tiles (first all-gather)
         ncs = int(nc * stair_fraction(k)) // nb * nb if nc > 0 else 0
         alone, chain, upd, step, step_ov = measure(tasks, [Gemm(mr - nb, ncs, nb)] if ncs > 0 else [], c)
         rows.append(dict(k=k, mr=mr, nc=nc, parts=alone, comm=c, chain=chain, update=upd, step=step, step_ov=step_ov))
