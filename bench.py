@@ -53,16 +53,17 @@ ALL = ["dgemm", "dpotrf", "dgetrf", "dgeqrf"]
 # profiles/r6_critpath_2_4gpu_sweep.txt), predicted whole-job TFLOP/s:
 #   8: LU 2 x 4 nb 512 (193-194 with the 512-thread tournament tree; nb 256:
 #      185-187, profiles/r6_tslu_nt.txt), QR 8 x 1 nb 512 (337; 4 x 2: 308),
-#      Cholesky 4 x 2 nb 512 (279; 8 x 1: 220)
+#      Cholesky 8 x 1 nb 512 (321 once the lookahead column's transposed
+#      tiles travel first, profiles/r6_potrf_split.txt; 4 x 2: 296)
 #   4: LU 2 x 2 nb 512 (143), QR 4 x 1 nb 1024 (187; 2 x 2: 170), Cholesky
-#      4 x 1 nb 1024 (167; 2 x 2: 160)
+#      4 x 1 nb 1024 (187; 2 x 2: 161)
 #   2: everything 2 x 1 (1 x 2 is 5-10 % lower): LU nb 1024 (92; the p > 1
 #      LU takes tiles <= 1024), QR nb 1024 (97), Cholesky nb 1536 (97)
 # The BASELINE configs 3-5 keep the reference's 2 x 4.
 GRID_PER = {
     2: {"dgetrf": (2, 1), "dpotrf": (2, 1), "dgeqrf": (2, 1)},
     4: {"dgeqrf": (4, 1), "dpotrf": (4, 1)},
-    8: {"dgeqrf": (8, 1), "dpotrf": (4, 2), "cfg4_dgeqrf_nb256": (2, 4)},
+    8: {"dgeqrf": (8, 1), "dpotrf": (8, 1), "cfg4_dgeqrf_nb256": (2, 4)},
 }
 NB_PER_WORLD = {
     1: {"dgetrf": 2048, "dpotrf": 1536, "dgeqrf": 1024, "dgesv_mixed": 1024},
