@@ -237,10 +237,12 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
             }
             if (p > 1) gather_t(c, 0, c1, Wt[slot].data());             // the lookahead columns' tiles
         });
-        S.task(qM, {tLa}, {tBc}, [&, slot, c1, gather_t, R1](lb::Ctx const& c) {
-            trace::Block tb("bcast_transposed");
-            if (p > 1) gather_t(c, c1, maxcnt, Wt[slot].data() + R1);   // the rest
-        });
+        if (p > 1) {
+            S.task(qM, {tLa}, {tBc}, [&, slot, c1, gather_t, R1](lb::Ctx const& c) {
+                trace::Block tb("bcast_transposed");
+                gather_t(c, c1, maxcnt, Wt[slot].data() + R1);   // the rest
+            });
+        }
 
         // ---- trailing updates
         auto update = [&, Wk, ldW, kb, slot, lists, lr_k1, k](lb::Ctx const& c, int64_t j0, int64_t j1) {
