@@ -59,10 +59,16 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
     // (a prefix of every process row's list: c1(k) tiles, region 1 of Wt),
     // so the next panel's update does not wait for the whole set; then the
     // rest (region 2).  Same layout on every rank of the process column.
+    // SLATE_POTRF_SPLIT=0: one all-gather of every tile (round 5)
+    static const bool split_env = [] {
+        const char* e = std::getenv("SLATE_POTRF_SPLIT");
+        return !e || std::atoi(e) != 0;
+    }();
     const int64_t la_tiles = std::max<int64_t>(la, 1);
     const int64_t R1 = int64_t(p) * la_tiles * nb * nb;
     auto c1_of = [&](int64_t k) {
         int64_t c1 = 0;
+        if (!split_env) return c1;
         std::vector<int64_t> cnt(p, 0);
         for (int64_t J = k + 1; J < std::min(nt, k + 1 + la); ++J)
             if (A.scol_owner(J) == mycol) c1 = std::max(c1, ++cnt[A.srow_owner(J)]);
@@ -235,9 +241,10 @@ int64_t potrf_lower(BaseMatrix<T> A, Target target, int64_t la) {
                 if (mycol == qk) pack(c, mrows, kb, apan, lda, Wk);
                 bcast(rowM, Wk, size_t(mrows * kb), qk, c);
             }
-            if (p > 1) gather_t(c, 0, c1, Wt[slot].data());             // the lookahead columns' tiles
+            if (p > 1 && split_env) gather_t(c, 0, c1, Wt[slot].data());    // the lookahead columns' tiles
+            if (p > 1 && !split_env) gather_t(c, 0, maxcnt, Wt[slot].data() + R1);
         });
-        if (p > 1) {
+        if (p > 1 && split_env) {
             S.task(qM, {tLa}, {tBc}, [&, slot, c1, gather_t, R1](lb::Ctx const& c) {
                 trace::Block tb("bcast_transposed");
                 gather_t(c, c1, maxcnt, Wt[slot].data() + R1);   // the rest
