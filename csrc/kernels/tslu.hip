@@ -1012,14 +1012,9 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
             const char* e = std::getenv("SLATE_TSLU_F32_R");
             return !e || std::atoi(e) == 2;
         }();
-        if constexpr (std::is_same<T, float>::value) {
-            if (f32_small) {
-                tslu2_narrow_launch<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work, s);
-                return;
-            }
-        }
-        // SLATE_TSLU_NT: tree workgroup size (fp64).  512 by default when CUs
-        // are reserved for the panel queues (the one-process-per-GPU default):
+        // SLATE_TSLU_NT: tree workgroup size (fp64; fp32 at two rows per
+        // thread).  512 by default when CUs are reserved for the panel
+        // queues (the one-process-per-GPU default):
         // whole-CU leaves then find free CUs, and the tree is one level
         // shallower -- 2 x 4 / nb 256 LU model 175.8 -> 188.0 TFLOP/s; 256
         // otherwise, where a whole-CU leaf waits for the trailing GEMM to
@@ -1029,6 +1024,17 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
             if (e) return std::atoi(e);
             return slate::device::reserved_cus() > 0 ? 512 : T2_NT;
         }();
+        if constexpr (std::is_same<T, float>::value) {
+            if (f32_small) {
+                if (nt == 512)
+                    tslu2_narrow_launch<T, 2, 2, 512>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset,
+                                                      work, s);
+                else
+                    tslu2_narrow_launch<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work,
+                                                 s);
+                return;
+            }
+        }
         // SLATE_TSLU_NT512_ROWS: also 512 for panels of at most this many rows
         // (a short panel's trailing update no longer fills the GPU)
         static const int64_t nt512_rows = [] {

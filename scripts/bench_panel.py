@@ -11,7 +11,7 @@ m = int(sys.argv[1]) if len(sys.argv) > 1 else 32768
 nb = int(sys.argv[2]) if len(sys.argv) > 2 else 512
 reps = 5
 torch.manual_seed(0)
-A0 = torch.rand(nb, m, dtype=torch.float64, device="cuda") * 2 - 1   # column-major m x nb
+A0 = torch.rand(nb, m, dtype=getattr(torch, os.environ.get("DTYPE", "float64")), device="cuda") * 2 - 1   # column-major m x nb
 ONLY = os.environ.get("PANELS", "")
 for name, fn in [("getrf_partial", lambda A: s.ops.getrf_panel(A, tournament=False)),
                  ("getrf_tournament", lambda A: s.ops.getrf_panel(A, tournament=True)),
