@@ -1026,9 +1026,20 @@ void tslu_narrow(int64_t m, int64_t r, int nn, T* Ablk, T* Apanel, int64_t lda, 
         }();
         if constexpr (std::is_same<T, float>::value) {
             if (f32_small) {
+                // SLATE_TSLU_F32_WPE: register budget of the 256-thread tree --
+                // 2 (default): <= 256 VGPRs, 169 used, no spill; 4: <= 128
+                // VGPRs, 180 bytes of scratch.  Config-5 fp32 factor 1852 ->
+                // 1800 ms on one GPU (profiles/r6_f32_nt.txt)
+                static const int f32_wpe = [] {
+                    const char* e = std::getenv("SLATE_TSLU_F32_WPE");
+                    return e ? std::atoi(e) : 2;
+                }();
                 if (nt == 512)
                     tslu2_narrow_launch<T, 2, 2, 512>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset,
                                                       work, s);
+                else if (f32_wpe == 2)
+                    tslu2_narrow_launch<T, 2, 2>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work,
+                                                 s);
                 else
                     tslu2_narrow_launch<T, 2, 4>(m, r, nn, Ablk, Apanel, lda, ncols, ipiv, perm, info, info_offset, work,
                                                  s);
